@@ -1,0 +1,279 @@
+"""Benchmark: DeepWalk/node2vec SGNS training on the synthetic 1M-node R-MAT graph (BASELINE C3/C4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-walks B] ...
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+One step = one pass of the hot path over one batch of synthetic input, all on the device:
+  1. B walks of length 80 from the Philox fast walker (start node = global walk id // 10, i.e.
+     node-id order x 10 walks per node, over successive steps);
+  2. the fused SGNS kernel (R=5 windows, K=5 uniform device negatives, d=128) accumulating the
+     dense gradient of the batch-mean loss into both tables;
+  3. dense Adam over both full 1,048,577 x 128 tables (torch.optim.Adam semantics), with the
+     node-id-range sharded reduce-scatter / all-gather exchange over RCCL when N > 1.
+Weak scaling: every rank processes B walks per step; `value` = positive pairs of ALL ranks / s.
+
+Also reported: walks/s of the walker alone (DeepWalk and node2vec p=.25 q=4), the SGNS kernel
+against the HBM roofline (algorithmic bytes / live HIP-event kernel time), and the CPU
+baseline (the oracle = reference-algorithm restatement, rank 0 at N=1, bounded sample).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'deepwalk-and-node2vec_amd'))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
+    """Algorithmic HBM bytes per positive pair: every gathered fp32 row read
+    once and its gradient written once; int64 ids. 6,295 B at d=128, K=5, R=5."""
+    return 8 * d * (1 + K) + 8 * d / (2 * R) + 8 * (1 + K) + 8 / (2 * R)
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(csr, args, budget_s: float):
+    """The oracle (reference algorithm restated on the CPU) on a bounded sample."""
+    from oracle import sgns_ref, walk_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    V, d, R, K = csr.vocab_size, args.dim, args.radius, args.neg
+    rng = np.random.default_rng(0)
+    w_in, w_out = sgns_ref.xavier_tables(V, d, seed=0)
+    ref = sgns_ref.TorchAdamRef(w_in, w_out, lr=args.lr)
+    # the reference's own batch: 64 walks per step (configs: batch_size 64)
+    walks = rng.integers(1, V, size=(64, args.walk_length)).astype(np.int32)
+    ins, tgt = sgns_ref.sg_windows(walks, R)
+    ref.train_step(ins, tgt, rng.integers(0, V, size=(len(ins), 2 * R, K)))  # state alloc
+    t0, steps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s * 0.7 or steps < 2:
+        ref.train_step(ins, tgt, rng.integers(0, V, size=(len(ins), 2 * R, K)))
+        steps += 1
+    sgns_dt = time.perf_counter() - t0
+    pairs_per_s = steps * tgt.size / sgns_dt
+    # walker: the reference's per-step algorithm (Python, one process)
+    g = walk_ref.CSR(csr.row_ptr, csr.col)
+    n_w, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s * 0.3 or n_w < 1:
+        s = int(rng.integers(1, V))
+        walk_ref.deepwalk_walk(g, s, args.walk_length, rng.random(args.walk_length - 1))
+        n_w += 1
+    walk_dt = time.perf_counter() - t0
+    return {
+        'value': pairs_per_s, 'unit': 'positive-pairs/s', 'cores': threads, 'kind': 'port',
+        'sample': (f'oracle SGNS step (torch-CPU restatement of model.py/loss.py + autograd + '
+                   f'torch.optim.Adam, V={V}, d={d}, K={K}, R={R}, 64 walks x L={args.walk_length}'
+                   f' = {tgt.size} pairs/step) x {steps} steps in {sgns_dt:.1f}s, '
+                   f'{threads} torch threads; walker: {n_w} oracle DeepWalk walks (Python, 1 core)'
+                   f' in {walk_dt:.1f}s'),
+        'walks_per_s': n_w / walk_dt,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch-walks', type=int, default=8192)
+    ap.add_argument('--method', default='deepwalk', choices=['deepwalk', 'node2vec'])
+    ap.add_argument('--p', type=float, default=1.0)
+    ap.add_argument('--q', type=float, default=1.0)
+    ap.add_argument('--scale', type=int, default=20)
+    ap.add_argument('--edges', type=int, default=10_000_000)
+    ap.add_argument('--dim', type=int, default=128)
+    ap.add_argument('--neg', type=int, default=5)
+    ap.add_argument('--radius', type=int, default=5)
+    ap.add_argument('--walk-length', type=int, default=80)
+    ap.add_argument('--walks-per-node', type=int, default=10)
+    ap.add_argument('--lr', type=float, default=0.01)
+    ap.add_argument('--cpu-budget', type=float, default=20.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-walk-bench', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    dev = torch.device('cuda', local_rank)
+    torch.cuda.set_device(dev)
+
+    from shallow_encoders import _native
+    from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
+    from shallow_encoders.graph.rmat import rmat_graph
+    from shallow_encoders.word2vec.sgns import loss_terms, sgns_accumulate
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    _native.require_device(dev)
+
+    t0 = time.time()
+    csr = rmat_graph(args.scale, args.edges, 0)
+    V = csr.vocab_size
+    N = V - 1
+    log(rank, f'[bench] R-MAT scale {args.scale}: {N} nodes, {csr.nnz // 2} edges '
+              f'({time.time() - t0:.1f}s)')
+    csr.device_tensors(dev, need_sorted=True)
+    R, K, d, L, B = args.radius, args.neg, args.dim, args.walk_length, args.batch_walks
+    if args.method == 'node2vec':
+        walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
+    else:
+        walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
+    tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0)
+    centres = B * (L - 2 * R)
+    pairs_per_step = centres * 2 * R
+    grad_scale = 1.0 / (pairs_per_step * world)   # mean over the GLOBAL batch
+    walks_total = N * args.walks_per_node
+    walks_buf = torch.empty((B, L), dtype=torch.int32, device=dev)
+    starts_buf = torch.empty(B, dtype=torch.int32, device=dev)
+    loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    step_idx = [0]
+    ev = {k: [] for k in ('walk', 'sgns', 'adam')}
+
+    def one_step(record: bool):
+        s = step_idx[0]
+        step_idx[0] += 1
+        g0 = (s * world + rank) * B                   # global walk id of this rank's batch
+        ids = (torch.arange(g0, g0 + B, device=dev, dtype=torch.int64) % walks_total)
+        torch.floor_divide(ids, args.walks_per_node, out=ids)
+        starts_buf.copy_(ids + 1)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
+        if record:
+            e[1].record()
+        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K,
+                        walks=walks_buf, context_radius=R, noise=None, seed=99,
+                        noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale,
+                        loss_acc=loss_acc, status=status)
+        if record:
+            e[2].record()
+        tables.step()
+        if record:
+            e[3].record()
+            ev['walk'].append((e[0], e[1]))
+            ev['sgns'].append((e[1], e[2]))
+            ev['adam'].append((e[2], e[3]))
+
+    for _ in range(args.warmup):
+        one_step(False)
+    torch.cuda.synchronize(dev)
+    _native.check_status(status, 'bench warmup')
+    loss_acc.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    _native.check_status(status, 'bench')
+    kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    terms = loss_terms(loss_acc, pairs_per_step * args.steps, K)
+    mean_loss = float(terms['loss'])
+
+    total_pairs = pairs_per_step * args.steps * world
+    value = total_pairs / elapsed
+    bpp = sgns_bytes_per_pair(d, K, R)
+    sgns_gbs = pairs_per_step * bpp / (kern_ms['sgns'] * 1e-3) / 1e9
+
+    # ---- walker alone: walks/s (DeepWalk over one walk per node; node2vec sample) ------------
+    walk_stats = {}
+    if not args.no_walk_bench:
+        for meth, n_walks, p, q in (('deepwalk', N, 1.0, 1.0), ('node2vec', 65_536, 0.25, 4.0)):
+            w = (Node2Vec(csr, L, p=p, q=q, rng='philox', seed=7, device=dev)
+                 if meth == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=7, device=dev))
+            st = torch.arange(1, n_walks + 1, dtype=torch.int32, device=dev)
+            out = torch.empty((n_walks, L), dtype=torch.int32, device=dev)
+            w.walk_batch(st[:1024], walk_id0=0, out=out[:1024], check=False)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            a = time.perf_counter()
+            w.walk_batch(st, walk_id0=rank * n_walks, out=out, check=False)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - a
+            if world > 1:
+                t = torch.tensor([dt], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt = float(t)
+            walk_stats[meth] = n_walks * world / dt
+            del out
+
+    result = {
+        'metric': 'positive-pairs/s + random-walks/s, 1M-node d=128 k=5, 1/2/4/8 MI355X',
+        'value': value,
+        'unit': 'positive-pairs/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'fp32',
+        'data': 'synthetic (R-MAT scale 20 graph, Philox walks, uniform device negatives, '
+                'random Xavier init)',
+        'config': {
+            'workload': (f'C3: R-MAT {N} nodes / {csr.nnz // 2} edges, {args.method} L={L}, '
+                         f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU'),
+            'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
+            'parallelism': f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather)',
+        },
+        'walks_per_s': walk_stats.get('deepwalk'),
+        'walks_per_s_node2vec_p0.25_q4': walk_stats.get('node2vec'),
+        'kernel_ms': kern_ms,
+        'mean_loss': mean_loss,
+        'roofline': {
+            'kernel': 'dw_sgns_walks (k_sgns)',
+            'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
+            'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,
+        },
+        'cpu_baseline': None,
+    }
+    prof = os.path.join(REPO, 'profiles', 'sgns_pmc.json')
+    if os.path.exists(prof):
+        try:
+            with open(prof) as f:
+                pmc = json.load(f)
+            if pmc.get('pairs_per_launch') == pairs_per_step:
+                result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
+        except (OSError, ValueError):
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(csr, args, args.cpu_budget)
+        result['cpu_baseline'] = cb
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,35 @@
+// Library-level C ABI: error string, version, stream sync, elementwise scale.
+#include <stdarg.h>
+#include <string.h>
+
+#include "dw_common.h"
+
+namespace dw {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+}  // namespace dw
+
+extern "C" {
+
+const char *dw_last_error_string(void) { return dw::g_err; }
+
+int dw_abi_version(void) { return 1; }
+
+int dw_device_sync(void *stream) {
+    hipError_t e = hipStreamSynchronize(dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    return DW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+// Dense Adam over the embedding tables (the dominant HBM stream of one reference step).
+//
+// Reference: the configs instantiate torch.optim.Adam (configs/sge_sg_*.yaml `_target_`,
+// config_parser/core.py:43-53); PL calls optimizer.step() + zero_grad() every batch. The
+// single-tensor update (torch/optim/adam.py, amsgrad=False) is restated with the per-step
+// scalars precomputed on the host in float64 and cast to float32 exactly as torch's scalar
+// arguments are:
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2);
+//   denom = (v.sqrt() / bias_correction2_sqrt).add_(eps); p.addcdiv_(m, denom, value=-step_size)
+// Streaming: 16 B per lane per tensor; p, g, m, v read once, p, m, v (and g=0) written once.
+#include "dw_common.h"
+
+namespace {
+
+struct AdamScalars {
+    float w1, b2, omb2, bc2s, nstep, eps, wd;
+};
+
+__device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
+                                          const AdamScalars &s) {
+    float gg = g;
+    if (s.wd != 0.f) gg = gg + s.wd * p;
+    m = fmaf(s.w1, gg - m, m);  // lerp with weight < 0.5: self + weight * (end - self)
+    v = v * s.b2;
+    v = v + s.omb2 * gg * gg;
+    const float denom = sqrtf(v) / s.bc2s + s.eps;
+    p = p + s.nstep * (m / denom);
+}
+
+template <bool ZERO>
+__global__ void __launch_bounds__(256)
+    k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
+           float *__restrict__ v, int64_t n, AdamScalars s) {
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float4 *p4 = reinterpret_cast<float4 *>(p);
+    float4 *g4 = reinterpret_cast<float4 *>(g);
+    float4 *m4 = reinterpret_cast<float4 *>(m);
+    float4 *v4 = reinterpret_cast<float4 *>(v);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
+        adam_elem(pp.x, gg.x, mm.x, vv.x, s);
+        adam_elem(pp.y, gg.y, mm.y, vv.y, s);
+        adam_elem(pp.z, gg.z, mm.z, vv.z, s);
+        adam_elem(pp.w, gg.w, mm.w, vv.w, s);
+        p4[i] = pp;
+        m4[i] = mm;
+        v4[i] = vv;
+        if (ZERO) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // tail (n % 4 elements)
+    for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += stride) {
+        adam_elem(p[i], g[i], m[i], v[i], s);
+        if (ZERO) g[i] = 0.f;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+    k_scale(float *__restrict__ x, int64_t n, float alpha, const float *__restrict__ alpha_dev) {
+    if (alpha_dev) alpha *= *alpha_dev;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+        x[i] *= alpha;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n_elem,
+                  float one_minus_beta1, float beta2, float one_minus_beta2,
+                  float bias_correction2_sqrt, float neg_step_size, float eps,
+                  float weight_decay, int32_t zero_grad, void *stream) {
+    DW_REQUIRE(n_elem >= 0, "dw_adam_dense: negative size");
+    if (n_elem == 0) return DW_OK;
+    DW_REQUIRE(param && grad && exp_avg && exp_avg_sq, "dw_adam_dense: null pointer");
+    DW_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) %
+                       16 == 0,
+               "dw_adam_dense: buffers must be 16-byte aligned");
+    DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_adam_dense: bias_correction2_sqrt must be > 0");
+    AdamScalars s{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size,
+                  eps, weight_decay};
+    int64_t blocks = ((n_elem >> 2) + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond
+    if (zero_grad)
+        hipLaunchKernelGGL(k_adam<true>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
+    else
+        hipLaunchKernelGGL(k_adam<false>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
+    DW_LAUNCH_CHECK("dw_adam_dense");
+    return DW_OK;
+}
+
+int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream) {
+    DW_REQUIRE(n_elem >= 0, "dw_scale: negative size");
+    if (n_elem == 0) return DW_OK;
+    DW_REQUIRE(x, "dw_scale: null pointer");
+    int64_t blocks = (n_elem + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream), x,
+                       n_elem, alpha, alpha_dev);
+    DW_LAUNCH_CHECK("dw_scale");
+    return DW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// Internal helpers shared by the gfx950 kernels of libdw_hip.so (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/dw_hip.h"
+
+namespace dw {
+
+// ---- error reporting across the C ABI ---------------------------------------------------------
+void set_error(const char *fmt, ...);
+
+#define DW_REQUIRE(cond, ...)                 \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::dw::set_error(__VA_ARGS__);     \
+            return DW_E_INVALID_ARG;          \
+        }                                     \
+    } while (0)
+
+#define DW_LAUNCH_CHECK(what)                                                         \
+    do {                                                                              \
+        hipError_t e_ = hipGetLastError();                                            \
+        if (e_ != hipSuccess) {                                                       \
+            ::dw::set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e_)); \
+            return DW_E_HIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- Philox4x32-10 (Salmon et al., SC'11), the device RNG of every fast-mode kernel ----------
+// Restated bit-for-bit on the host in oracle/philox.py (test infrastructure).
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+// Stream tags keep the counter spaces of different consumers disjoint.
+constexpr uint32_t TAG_DEEPWALK = 0x44570000u;   // 'DW'
+constexpr uint32_t TAG_NODE2VEC = 0x4E320000u;   // 'N2'
+
+// Uniform index in [0, n) from 32 random bits (multiply-high; bias <= n / 2^32).
+__device__ __forceinline__ uint32_t bounded32(uint32_t r, uint32_t n) { return __umulhi(r, n); }
+
+// Uniform index in [0, n) from 64 random bits (bias <= n / 2^64) — torch.randint(0, V) analogue.
+__device__ __forceinline__ uint64_t bounded64(uint32_t lo, uint32_t hi, uint64_t n) {
+    const uint64_t r = (static_cast<uint64_t>(hi) << 32) | lo;
+    return __umul64hi(r, n);
+}
+
+__device__ __forceinline__ void status_or(int32_t *status, int32_t bits) {
+    if (status) atomicOr(status, bits);
+}
+
+// Wave-level LDS visibility for a wave that owns a private LDS slice (no s_barrier needed).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+}  // namespace dw

@@ -1,0 +1,182 @@
+// CSR utilities on gfx950: validation, sorted neighbour copy, per-row alias tables.
+//
+// The reference keeps its graph as a networkx dict-of-dicts and walks it from Python
+// (shallow_encoders/graph/random_walk_generator.py:41-53). On the device the graph is a CSR in
+// HBM (row_ptr int64, col int32, optional float64 weights) in vocabulary-id space.
+#include <hipcub/hipcub.hpp>
+
+#include "dw_common.h"
+
+namespace {
+
+__global__ void k_csr_validate(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                               int64_t n_rows, int64_t nnz, int32_t *status) {
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (tid == 0) {
+        if (row_ptr[0] != 0 || row_ptr[n_rows] != nnz) dw::status_or(status, DW_S_BAD_CSR);
+    }
+    for (int64_t r = tid; r < n_rows; r += stride)
+        if (row_ptr[r] > row_ptr[r + 1]) dw::status_or(status, DW_S_BAD_CSR);
+    for (int64_t e = tid; e < nnz; e += stride) {
+        const int32_t c = col[e];
+        if (c < 0 || (int64_t)c >= n_rows) dw::status_or(status, DW_S_BAD_CSR);
+    }
+}
+
+// key = row << 32 | col: one global radix sort orders every row's neighbours ascending.
+__global__ void k_make_keys(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                            int64_t n_rows, uint64_t *__restrict__ keys) {
+    const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + threadIdx.x / 64; r < n_rows;
+         r += stride) {
+        const int64_t a = row_ptr[r], b = row_ptr[r + 1];
+        for (int64_t e = a + lane; e < b; e += 64)
+            keys[e] = (static_cast<uint64_t>(r) << 32) | static_cast<uint32_t>(col[e]);
+    }
+}
+
+__global__ void k_keys_to_col(const uint64_t *__restrict__ keys, int64_t nnz,
+                              int32_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz; e += stride)
+        out[e] = static_cast<int32_t>(keys[e] & 0xFFFFFFFFull);
+}
+
+// Vose alias construction, one thread per row (rows are independent; hubs are serial but rare).
+// Small-list grows from the row's front of work_idx, large-list from its back: they never meet.
+__global__ void k_alias_build(const int64_t *__restrict__ row_ptr, const double *__restrict__ w,
+                              int64_t n_rows, uint32_t *__restrict__ prob_thr,
+                              int32_t *__restrict__ alias, double *__restrict__ scaled,
+                              int32_t *__restrict__ stack, int32_t *status) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_rows; r += stride) {
+        const int64_t a = row_ptr[r], b = row_ptr[r + 1];
+        const int64_t n = b - a;
+        if (n == 0) continue;
+        double sum = 0.0;
+        for (int64_t e = a; e < b; ++e) sum += w ? w[e] : 1.0;
+        if (!(sum > 0.0)) {
+            dw::status_or(status, DW_S_ZERO_WEIGHT);
+            for (int64_t e = a; e < b; ++e) {
+                prob_thr[e] = 0xFFFFFFFFu;
+                alias[e] = static_cast<int32_t>(e - a);
+            }
+            continue;
+        }
+        int64_t ns = 0, nl = 0;
+        for (int64_t e = a; e < b; ++e) {
+            const double s = (w ? w[e] : 1.0) * static_cast<double>(n) / sum;
+            scaled[e] = s;
+            alias[e] = static_cast<int32_t>(e - a);
+            if (s < 1.0)
+                stack[a + ns++] = static_cast<int32_t>(e - a);
+            else
+                stack[b - 1 - nl++] = static_cast<int32_t>(e - a);
+        }
+        while (ns > 0 && nl > 0) {
+            const int32_t l = stack[a + --ns];
+            const int32_t g = stack[b - 1 - --nl];
+            const double pl = scaled[a + l];
+            prob_thr[a + l] = static_cast<uint32_t>(fmin(floor(pl * 4294967296.0), 4294967295.0));
+            alias[a + l] = g;
+            const double pg = (scaled[a + g] + pl) - 1.0;
+            scaled[a + g] = pg;
+            if (pg < 1.0)
+                stack[a + ns++] = g;
+            else
+                stack[b - 1 - nl++] = g;
+        }
+        while (nl > 0) {
+            const int32_t g = stack[b - 1 - --nl];
+            prob_thr[a + g] = 0xFFFFFFFFu;
+        }
+        while (ns > 0) {
+            const int32_t l = stack[a + --ns];
+            prob_thr[a + l] = 0xFFFFFFFFu;
+        }
+    }
+}
+
+inline int grid_for(int64_t work, int block, int cap = 8192) {
+    int64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<int>(g);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dw_csr_validate(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                    int32_t *status, void *stream) {
+    DW_REQUIRE(row_ptr && status, "dw_csr_validate: null pointer");
+    DW_REQUIRE(n_rows >= 0 && nnz >= 0, "dw_csr_validate: negative size");
+    DW_REQUIRE(nnz == 0 || col, "dw_csr_validate: col is null");
+    hipLaunchKernelGGL(k_csr_validate, dim3(grid_for(n_rows > nnz ? n_rows : nnz, 256)), dim3(256),
+                       0, dw::as_stream(stream), row_ptr, col, n_rows, nnz, status);
+    DW_LAUNCH_CHECK("dw_csr_validate");
+    return DW_OK;
+}
+
+int dw_csr_sort_copy(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                     int32_t *col_sorted, void *temp, size_t *temp_bytes, void *stream) {
+    DW_REQUIRE(temp_bytes, "dw_csr_sort_copy: temp_bytes is null");
+    DW_REQUIRE(n_rows >= 0 && nnz >= 0, "dw_csr_sort_copy: negative size");
+    DW_REQUIRE(n_rows < (int64_t(1) << 31), "dw_csr_sort_copy: n_rows must fit int32");
+    int end_bit = 32;
+    while (end_bit < 64 && (uint64_t(n_rows) >> (end_bit - 32)) != 0) ++end_bit;
+    const size_t keys_bytes = ((size_t)nnz * sizeof(uint64_t) + 255) & ~size_t(255);
+    size_t cub_bytes = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortKeys(nullptr, cub_bytes, (uint64_t *)nullptr,
+                                                     (uint64_t *)nullptr, (int)nnz, 0, end_bit,
+                                                     dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_csr_sort_copy: hipcub size query: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    const size_t need = 2 * keys_bytes + cub_bytes;
+    if (temp == nullptr) {
+        *temp_bytes = need;
+        return DW_OK;
+    }
+    DW_REQUIRE(*temp_bytes >= need, "dw_csr_sort_copy: temp too small (%zu < %zu)", *temp_bytes,
+               need);
+    DW_REQUIRE(nnz < (int64_t(1) << 31), "dw_csr_sort_copy: nnz must fit int32 for hipcub");
+    if (nnz == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && col_sorted, "dw_csr_sort_copy: null pointer");
+    char *base = static_cast<char *>(temp);
+    uint64_t *k_in = reinterpret_cast<uint64_t *>(base);
+    uint64_t *k_out = reinterpret_cast<uint64_t *>(base + keys_bytes);
+    void *cub_tmp = base + 2 * keys_bytes;
+    hipLaunchKernelGGL(k_make_keys, dim3(grid_for(n_rows * 64, 256)), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, col, n_rows, k_in);
+    DW_LAUNCH_CHECK("dw_csr_sort_copy/keys");
+    e = hipcub::DeviceRadixSort::SortKeys(cub_tmp, cub_bytes, k_in, k_out, (int)nnz, 0, end_bit,
+                                          dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_csr_sort_copy: hipcub sort: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(nnz, 256)), dim3(256), 0,
+                       dw::as_stream(stream), k_out, nnz, col_sorted);
+    DW_LAUNCH_CHECK("dw_csr_sort_copy/extract");
+    return DW_OK;
+}
+
+int dw_alias_build(const int64_t *row_ptr, const double *weights, int64_t n_rows, int64_t nnz,
+                   uint32_t *prob_thr, int32_t *alias, double *work_prob, int32_t *work_idx,
+                   int32_t *status, void *stream) {
+    DW_REQUIRE(row_ptr && prob_thr && alias && work_prob && work_idx,
+               "dw_alias_build: null pointer");
+    DW_REQUIRE(n_rows >= 0 && nnz >= 0, "dw_alias_build: negative size");
+    hipLaunchKernelGGL(k_alias_build, dim3(grid_for(n_rows, 64)), dim3(64), 0,
+                       dw::as_stream(stream), row_ptr, weights, n_rows, prob_thr, alias, work_prob,
+                       work_idx, status);
+    DW_LAUNCH_CHECK("dw_alias_build");
+    return DW_OK;
+}
+
+}  // extern "C"

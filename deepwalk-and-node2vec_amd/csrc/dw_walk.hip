@@ -1,0 +1,441 @@
+// Random-walk generation on gfx950 (hot path A).
+//
+// Reference: shallow_encoders/graph/random_walk_generator.py
+//   DeepWalk.walk   61-72   first-order step: random.choices(neighbors, normalized weights)
+//   Node2Vec.walk   94-119  second-order step with the reference's (p, q) rule:
+//                           x == prev -> w *= 1/p ; prev in N(x) -> w *= 1/q ; else w
+//
+// Two families of kernels:
+//   * replay: bit-exact with the reference given the uniforms random.random() returns. The
+//     weights of one step are computed lane-parallel (one wave per walker, adjacency tests
+//     against N(prev) staged sorted in LDS), then ONE lane reproduces CPython's left-to-right
+//     fp64 sum / accumulate / bisect_right serially — a parallel scan would round differently.
+//     This file is compiled with -ffp-contract=off so no mul+add pair fuses into an FMA.
+//   * fast: Philox4x32-10 keyed by (seed, global walk id, step, lane/round).
+//     DeepWalk: one lane per walker. node2vec: one wave per walker, 64 proposals per round,
+//     exact rejection against alpha/alpha_max, lowest accepting lane wins (ballot).
+#include "dw_common.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr uint32_t ALWAYS = 0xFFFFFFFFu;
+
+// ---- adjacency tests ------------------------------------------------------------------------
+__device__ __forceinline__ bool contains_global(const int32_t *__restrict__ s, int64_t n,
+                                                int32_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t v = s[mid];
+        if (v < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo < n && s[lo] == key;
+}
+
+__device__ __forceinline__ bool contains_lds(const int32_t *s, int n, int32_t key) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo < n && s[lo] == key;
+}
+
+// =============================================================================================
+// Replay walker
+// =============================================================================================
+constexpr int REPLAY_WAVES = 2;      // waves per block
+constexpr int REPLAY_CH = 2048;      // cached step weights per wave (float64): 16 KiB
+constexpr int REPLAY_NCAP = 2048;    // staged N(prev) entries per wave (int32): 8 KiB
+
+struct ReplayCtx {
+    const int64_t *row_ptr;
+    const int32_t *col;
+    const int32_t *col_sorted;
+    const double *w;
+    bool node2vec;
+    double inv_p, inv_q;
+};
+
+// Weight of candidate e (global CSR index) after the node2vec modification
+// (random_walk_generator.py:100-108). `nprev` is N(prev) sorted, in LDS or global memory.
+__device__ __forceinline__ double step_weight(const ReplayCtx &c, int64_t e, int32_t prev,
+                                              const int32_t *nprev_lds, int nprev_lds_n,
+                                              const int32_t *nprev_g, int64_t nprev_g_n) {
+    double w = c.w ? c.w[e] : 1.0;
+    if (c.node2vec && prev >= 0) {
+        const int32_t x = c.col[e];
+        if (x == prev) {
+            w = w * c.inv_p;
+        } else {
+            // prev in N(x)  <=>  x in N(prev) on an undirected graph
+            const bool adj = nprev_lds ? contains_lds(nprev_lds, nprev_lds_n, x)
+                                       : contains_global(nprev_g, nprev_g_n, x);
+            if (adj) w = w * c.inv_q;
+        }
+    }
+    return w;
+}
+
+// bisect_right(cum, x, 0, hi) over a non-decreasing array (CPython Lib/bisect.py).
+__device__ __forceinline__ int64_t bisect_right_lds(const double *cum, double x, int64_t hi) {
+    int64_t lo = 0;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (x < cum[mid])
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
+    k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
+                  int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
+                  int32_t *__restrict__ out, int32_t *status) {
+    __shared__ double s_buf[REPLAY_WAVES][REPLAY_CH];
+    __shared__ int32_t s_nprev[REPLAY_WAVES][REPLAY_NCAP];
+    __shared__ int64_t s_pick[REPLAY_WAVES];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    double *buf = s_buf[wv];
+    int32_t *nprev_lds = s_nprev[wv];
+    const int64_t n_waves = (int64_t)gridDim.x * REPLAY_WAVES;
+
+    for (int64_t wk = (int64_t)blockIdx.x * REPLAY_WAVES + wv; wk < n_walks; wk += n_waves) {
+        int32_t v = starts[wk];
+        int32_t prev = -1;
+        int32_t *o = out + wk * (int64_t)L;
+        if (lane == 0) o[0] = v;
+        const double *u = uniforms + wk * (int64_t)(L - 1);
+        int32_t s = 1;
+        for (; s < L; ++s) {
+            if (v < 0 || (int64_t)v >= n_rows) {
+                if (lane == 0) dw::status_or(status, DW_S_BAD_CSR);
+                break;
+            }
+            const int64_t a = c.row_ptr[v];
+            const int64_t n = c.row_ptr[v + 1] - a;
+            if (n <= 0) {  // random.choices on an empty population -> IndexError
+                if (lane == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
+                break;
+            }
+            // N(prev), sorted, for the adjacency test
+            const int32_t *np_lds = nullptr;
+            int np_lds_n = 0;
+            const int32_t *np_g = nullptr;
+            int64_t np_g_n = 0;
+            if (c.node2vec && prev >= 0) {
+                const int64_t pa = c.row_ptr[prev];
+                const int64_t pn = c.row_ptr[prev + 1] - pa;
+                if (pn <= REPLAY_NCAP) {
+                    for (int64_t e = lane; e < pn; e += WAVE) nprev_lds[e] = c.col_sorted[pa + e];
+                    dw::wave_lds_sync();
+                    np_lds = nprev_lds;
+                    np_lds_n = static_cast<int>(pn);
+                } else {
+                    np_g = c.col_sorted + pa;
+                    np_g_n = pn;
+                }
+            }
+            const double uu = u[s - 1];
+            if (n <= REPLAY_CH) {
+                for (int64_t i = lane; i < n; i += WAVE)
+                    buf[i] = step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n);
+                dw::wave_lds_sync();
+                if (lane == 0) {
+                    double sum = 0.0;  // sum(neighbor_weights), left to right
+                    for (int64_t i = 0; i < n; ++i) sum = sum + buf[i];
+                    if (sum == 0.0) {
+                        dw::status_or(status, DW_S_ZERO_WEIGHT);
+                        s_pick[wv] = -1;
+                    } else {
+                        double cum = 0.0;  // itertools.accumulate(nw / sum)
+                        for (int64_t i = 0; i < n; ++i) {
+                            const double nw = buf[i] / sum;
+                            cum = (i == 0) ? nw : cum + nw;
+                            buf[i] = cum;
+                        }
+                        const double total = buf[n - 1] + 0.0;
+                        s_pick[wv] = bisect_right_lds(buf, uu * total, n - 1);
+                    }
+                }
+            } else {  // hub row: lane 0 recomputes the weights on the fly (same arithmetic)
+                if (lane == 0) {
+                    double sum = 0.0;
+                    for (int64_t i = 0; i < n; ++i)
+                        sum = sum + step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n);
+                    if (sum == 0.0) {
+                        dw::status_or(status, DW_S_ZERO_WEIGHT);
+                        s_pick[wv] = -1;
+                    } else {
+                        double total = 0.0;
+                        for (int64_t i = 0; i < n; ++i) {
+                            const double nw =
+                                step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n) / sum;
+                            total = (i == 0) ? nw : total + nw;
+                        }
+                        total = total + 0.0;
+                        const double x = uu * total;
+                        int64_t pick = n - 1;  // bisect_right(cum, x, 0, n-1)
+                        double cum = 0.0;
+                        for (int64_t i = 0; i < n - 1; ++i) {
+                            const double nw =
+                                step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n) / sum;
+                            cum = (i == 0) ? nw : cum + nw;
+                            if (x < cum) {
+                                pick = i;
+                                break;
+                            }
+                        }
+                        s_pick[wv] = pick;
+                    }
+                }
+            }
+            dw::wave_lds_sync();
+            const int64_t pick = s_pick[wv];
+            dw::wave_lds_sync();
+            if (pick < 0) break;
+            const int32_t child = c.col[a + pick];
+            if (lane == 0) o[s] = child;
+            prev = v;
+            v = child;
+        }
+        if (lane == 0)
+            for (; s < L; ++s) o[s] = -1;  // marks an aborted walk
+    }
+}
+
+// =============================================================================================
+// Fast walkers
+// =============================================================================================
+
+// One first-order draw from row [a, a+n): uniform neighbour, or Vose alias when weighted.
+__device__ __forceinline__ int64_t first_order_pick(uint32_t r0, uint32_t r1, int64_t a,
+                                                    int64_t n, const uint32_t *prob_thr,
+                                                    const int32_t *alias) {
+    int64_t i = dw::bounded32(r0, static_cast<uint32_t>(n));
+    if (prob_thr) {
+        const uint32_t t = prob_thr[a + i];
+        if (t != ALWAYS && r1 >= t) i = alias[a + i];
+    }
+    return i;
+}
+
+__global__ void __launch_bounds__(256)
+    k_walk_deepwalk_fast(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                         const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
+                         int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
+                         int32_t L, uint32_t k0, uint32_t k1, uint64_t walk_id0,
+                         int32_t *__restrict__ out, int32_t *status) {
+    const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (w >= n_walks) return;
+    const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
+    int32_t *o = out + w * (int64_t)L;
+    int32_t v = starts[w];
+    o[0] = v;
+    int32_t s = 1;
+    for (; s < L; ++s) {
+        if (v < 0 || (int64_t)v >= n_rows) {
+            dw::status_or(status, DW_S_BAD_CSR);
+            break;
+        }
+        const int64_t a = row_ptr[v];
+        const int64_t n = row_ptr[v + 1] - a;
+        if (n <= 0) {
+            dw::status_or(status, DW_S_ISOLATED_NODE);
+            break;
+        }
+        const dw::U4 r = dw::philox(dw::U4{static_cast<uint32_t>(wid),
+                                           static_cast<uint32_t>(wid >> 32),
+                                           static_cast<uint32_t>(s) << 8, dw::TAG_DEEPWALK},
+                                    k0, k1);
+        v = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+        o[s] = v;
+    }
+    for (; s < L; ++s) o[s] = -1;
+}
+
+constexpr int N2V_WAVES = 4;     // waves per block, each owns one walker at a time
+constexpr int N2V_NCAP = 1024;   // staged N(prev) entries per wave (int32): 4 KiB
+
+struct N2VThr {
+    uint32_t p, q, one;  // accept iff r < thr (ALWAYS = unconditional)
+};
+
+__global__ void __launch_bounds__(N2V_WAVES *WAVE)
+    k_walk_node2vec_fast(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                         const int32_t *__restrict__ col_sorted,
+                         const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
+                         int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
+                         int32_t L, N2VThr thr, uint32_t k0, uint32_t k1, uint64_t walk_id0,
+                         int32_t *__restrict__ out, int32_t *status) {
+    __shared__ int32_t s_nprev[N2V_WAVES][N2V_NCAP];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    int32_t *nprev = s_nprev[wv];
+    const int64_t n_waves = (int64_t)gridDim.x * N2V_WAVES;
+
+    for (int64_t w = (int64_t)blockIdx.x * N2V_WAVES + wv; w < n_walks; w += n_waves) {
+        const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
+        const uint32_t c0 = static_cast<uint32_t>(wid), c1 = static_cast<uint32_t>(wid >> 32);
+        int32_t *o = out + w * (int64_t)L;
+        int32_t v = starts[w];
+        int32_t prev = -1;
+        if (lane == 0) o[0] = v;
+        int32_t s = 1;
+        for (; s < L; ++s) {
+            if (v < 0 || (int64_t)v >= n_rows) {
+                if (lane == 0) dw::status_or(status, DW_S_BAD_CSR);
+                break;
+            }
+            const int64_t a = row_ptr[v];
+            const int64_t n = row_ptr[v + 1] - a;
+            if (n <= 0) {
+                if (lane == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
+                break;
+            }
+            int32_t nxt;
+            if (prev < 0) {  // first step: prev_node is None -> unbiased (random_walk_generator.py:97)
+                const dw::U4 r = dw::philox(
+                    dw::U4{c0, c1, static_cast<uint32_t>(s) << 8, dw::TAG_NODE2VEC}, k0, k1);
+                nxt = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+            } else {
+                const int64_t pa = row_ptr[prev];
+                const int64_t pn = row_ptr[prev + 1] - pa;
+                const bool staged = pn <= N2V_NCAP;
+                if (staged) {
+                    for (int64_t e = lane; e < pn; e += WAVE) nprev[e] = col_sorted[pa + e];
+                    dw::wave_lds_sync();
+                }
+                nxt = -1;
+                for (uint32_t round = 0; round < DW_MAX_REJECTION_ROUNDS; ++round) {
+                    const dw::U4 r = dw::philox(
+                        dw::U4{c0, c1, (static_cast<uint32_t>(s) << 8) | static_cast<uint32_t>(lane),
+                               dw::TAG_NODE2VEC ^ round},
+                        k0, k1);
+                    const int32_t x = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+                    uint32_t t;
+                    if (x == prev)
+                        t = thr.p;
+                    else if (staged ? contains_lds(nprev, static_cast<int>(pn), x)
+                                    : contains_global(col_sorted + pa, pn, x))
+                        t = thr.q;
+                    else
+                        t = thr.one;
+                    const bool acc = (t == ALWAYS) || (r.z < t);
+                    const unsigned long long m = __ballot(acc);
+                    if (m) {
+                        nxt = __shfl(x, __ffsll(static_cast<long long>(m)) - 1, WAVE);
+                        break;
+                    }
+                }
+                if (staged) dw::wave_lds_sync();  // WAR on nprev before the next staging
+                if (nxt < 0) {
+                    if (lane == 0) dw::status_or(status, DW_S_REJECTION_CAP);
+                    break;
+                }
+            }
+            if (lane == 0) o[s] = nxt;
+            prev = v;
+            v = nxt;
+        }
+        if (lane == 0)
+            for (; s < L; ++s) o[s] = -1;
+    }
+}
+
+inline uint32_t accept_threshold(double alpha, double alpha_max) {
+    const double r = alpha / alpha_max;
+    if (r >= 1.0) return ALWAYS;
+    double t = floor(r * 4294967296.0);
+    if (t < 0.0) t = 0.0;
+    if (t > 4294967294.0) t = 4294967294.0;
+    return static_cast<uint32_t>(t);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
+                   const double *weights, int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                   int32_t walk_length, int32_t method, double p, double q,
+                   const double *uniforms, int32_t *out, int32_t *status, void *stream) {
+    DW_REQUIRE(walk_length >= 1, "dw_walk_replay: Minimum walk length is 1!");
+    DW_REQUIRE(method == DW_METHOD_DEEPWALK || method == DW_METHOD_NODE2VEC,
+               "dw_walk_replay: unknown method %d", method);
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_replay: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && starts && out && status, "dw_walk_replay: null pointer");
+    DW_REQUIRE(walk_length == 1 || uniforms, "dw_walk_replay: uniforms is null");
+    DW_REQUIRE(method == DW_METHOD_DEEPWALK || col_sorted,
+               "dw_walk_replay: node2vec needs col_sorted");
+    DW_REQUIRE(method == DW_METHOD_DEEPWALK || (p != 0.0 && q != 0.0),
+               "dw_walk_replay: p and q must be non-zero");
+    ReplayCtx c;
+    c.row_ptr = row_ptr;
+    c.col = col;
+    c.col_sorted = col_sorted;
+    c.w = weights;
+    c.node2vec = method == DW_METHOD_NODE2VEC;
+    c.inv_p = c.node2vec ? 1.0 / p : 1.0;  // `1 / self._p` (host IEEE division)
+    c.inv_q = c.node2vec ? 1.0 / q : 1.0;
+    int64_t blocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_walk_replay, dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
+                       dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length, uniforms,
+                       out, status);
+    DW_LAUNCH_CHECK("dw_walk_replay");
+    return DW_OK;
+}
+
+int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
+                 const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
+                 const int32_t *starts, int64_t n_walks, int32_t walk_length, int32_t method,
+                 double p, double q, uint64_t seed, uint64_t walk_id0, int32_t *out,
+                 int32_t *status, void *stream) {
+    DW_REQUIRE(walk_length >= 1, "dw_walk_fast: Minimum walk length is 1!");
+    DW_REQUIRE(walk_length < (1 << 24), "dw_walk_fast: walk_length too large");
+    DW_REQUIRE(method == DW_METHOD_DEEPWALK || method == DW_METHOD_NODE2VEC,
+               "dw_walk_fast: unknown method %d", method);
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_fast: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && starts && out && status, "dw_walk_fast: null pointer");
+    DW_REQUIRE((prob_thr == nullptr) == (alias == nullptr),
+               "dw_walk_fast: prob_thr and alias must be both set or both null");
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    if (method == DW_METHOD_DEEPWALK) {
+        const int64_t blocks = (n_walks + 255) / 256;
+        DW_REQUIRE(blocks < (int64_t(1) << 31), "dw_walk_fast: too many walks");
+        hipLaunchKernelGGL(k_walk_deepwalk_fast, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), row_ptr, col, prob_thr, alias, n_rows, starts,
+                           n_walks, walk_length, k0, k1, walk_id0, out, status);
+        DW_LAUNCH_CHECK("dw_walk_fast/deepwalk");
+        return DW_OK;
+    }
+    DW_REQUIRE(col_sorted, "dw_walk_fast: node2vec needs col_sorted");
+    DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_fast: p and q must be positive");
+    const double ip = 1.0 / p, iq = 1.0 / q;
+    double amax = 1.0;
+    if (ip > amax) amax = ip;
+    if (iq > amax) amax = iq;
+    N2VThr thr{accept_threshold(ip, amax), accept_threshold(iq, amax), accept_threshold(1.0, amax)};
+    int64_t blocks = (n_walks + N2V_WAVES - 1) / N2V_WAVES;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_walk_node2vec_fast, dim3((unsigned)blocks), dim3(N2V_WAVES * WAVE), 0,
+                       dw::as_stream(stream), row_ptr, col, col_sorted, prob_thr, alias, n_rows,
+                       starts, n_walks, walk_length, thr, k0, k1, walk_id0, out, status);
+    DW_LAUNCH_CHECK("dw_walk_fast/node2vec");
+    return DW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+"""CSR adjacency in vocabulary-id space — the device layout of the reference's networkx graph.
+
+The reference walks a ``networkx.Graph`` from Python (random_walk_generator.py:41-48) and maps
+node names to ids through a torchtext vocabulary built from one extra epoch of walks
+(torch_dataset.py:91-110: ``<unk>`` first, then tokens sorted lexicographically since every
+node occurs once). Here the vocabulary is built directly from the node names with the same
+rule, and the adjacency becomes
+
+    row_ptr int64[V+1]   row 0 = ``<unk>`` (no neighbours), row i = node with vocab id i
+    col     int32[nnz]   neighbour ids in ``graph.neighbors(node)`` order (insertion order)
+    weights float64[nnz] the ``'weight'`` attribute when ``nx.is_weighted(graph)``, else None
+    col_sorted int32[nnz] each row ascending (device-built by dw_csr_sort_copy), for the
+                          node2vec adjacency test ``prev_node in candidate_neighbors``.
+"""
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from shallow_encoders import _native
+
+UNK = '<unk>'
+_TOKEN_RE = re.compile(r"[A-Za-z]+[\w^']*|[\w^']*[A-Za-z]+[\w^']*|<unk>")
+
+
+def node_token(name) -> str:
+    """The vocabulary token of a node name (reference tokenizer, torch_dataset.py:23-39).
+
+    A node name must tokenize to exactly one token (the reference joins walk names with
+    spaces and re-tokenizes them); names such as ``'a b'`` or ``'1'`` cannot round-trip.
+    """
+    s = str(name)
+    toks = _TOKEN_RE.findall(s.lower())
+    if len(toks) != 1 or toks[0] != s.lower():
+        raise ValueError(f'node name {s!r} does not tokenize to a single vocabulary token '
+                         f'(got {toks}); node names must start with a letter')
+    return toks[0]
+
+
+@dataclass
+class CSRGraph:
+    """Host (numpy) CSR plus lazily built device copies."""
+    row_ptr: np.ndarray                 # int64 [V+1]
+    col: np.ndarray                     # int32 [nnz]
+    weights: Optional[np.ndarray]       # float64 [nnz] or None
+    itos: List[str]                     # vocabulary (id -> token), itos[0] == '<unk>'
+    names: List[object]                 # id -> original node object (None for <unk>)
+    _dev: Dict[str, torch.Tensor] = field(default_factory=dict, repr=False)
+    _dev_device: Optional[torch.device] = field(default=None, repr=False)
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def from_networkx(graph) -> 'CSRGraph':
+        import networkx as nx
+        nodes = list(graph)
+        tokens = [node_token(n) for n in nodes]
+        if len(set(tokens)) != len(tokens):
+            raise ValueError('two node names map to the same vocabulary token')
+        itos = [UNK] + sorted(tokens)
+        stoi = {t: i for i, t in enumerate(itos)}
+        names: List[object] = [None] * len(itos)
+        for n, t in zip(nodes, tokens):
+            names[stoi[t]] = n
+        weighted = nx.is_weighted(graph) if graph.number_of_edges() > 0 else False
+        V = len(itos)
+        deg = np.zeros(V, dtype=np.int64)
+        rows = [None] * V
+        wrows = [None] * V
+        adj = graph.adj
+        for n, t in zip(nodes, tokens):
+            i = stoi[t]
+            nbrs = adj[n]
+            rows[i] = [stoi[node_token(x)] for x in nbrs]
+            if weighted:
+                wrows[i] = [float(nbrs[x]['weight']) for x in nbrs]
+            deg[i] = len(rows[i])
+        row_ptr = np.zeros(V + 1, dtype=np.int64)
+        np.cumsum(deg, out=row_ptr[1:])
+        col = np.empty(int(row_ptr[-1]), dtype=np.int32)
+        w = np.empty(int(row_ptr[-1]), dtype=np.float64) if weighted else None
+        for i in range(1, V):
+            a, b = row_ptr[i], row_ptr[i + 1]
+            col[a:b] = rows[i]
+            if weighted:
+                w[a:b] = wrows[i]
+        return CSRGraph(row_ptr, col, w, itos, names)
+
+    @staticmethod
+    def from_arrays(row_ptr, col, weights=None, itos: Optional[Sequence[str]] = None,
+                    names: Optional[Sequence[object]] = None) -> 'CSRGraph':
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        weights = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        V = len(row_ptr) - 1
+        if itos is None:
+            width = max(7, len(str(V - 1)))
+            itos = [UNK] + [f'n{i:0{width}d}' for i in range(V - 1)]
+        itos = list(itos)
+        if names is None:
+            names = [None] + itos[1:]
+        if len(itos) != V:
+            raise ValueError('itos length must equal the number of CSR rows')
+        return CSRGraph(row_ptr, col, weights, itos, list(names))
+
+    # ------------------------------------------------------------------ host helpers
+    @property
+    def vocab_size(self) -> int:
+        return len(self.row_ptr) - 1
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row_ptr[-1])
+
+    @property
+    def weighted(self) -> bool:
+        return self.weights is not None
+
+    def degree(self) -> np.ndarray:
+        return np.diff(self.row_ptr)
+
+    def neighbors(self, i: int) -> np.ndarray:
+        return self.col[self.row_ptr[i]:self.row_ptr[i + 1]]
+
+    def stoi(self) -> Dict[str, int]:
+        return {t: i for i, t in enumerate(self.itos)}
+
+    def node_id(self, node) -> int:
+        tok = node_token(node)
+        sto = self.__dict__.setdefault('_stoi_cache', None)
+        if sto is None:
+            sto = self.stoi()
+            self.__dict__['_stoi_cache'] = sto
+        return sto[tok]
+
+    # ------------------------------------------------------------------ device side
+    def device_tensors(self, device=None, need_sorted: bool = False,
+                       need_alias: bool = False) -> Dict[str, torch.Tensor]:
+        """Copy the CSR to HBM once (and derive col_sorted / alias tables on the device)."""
+        dev = _native.require_device(device)
+        if self._dev_device != dev:
+            self._dev = {}
+            self._dev_device = dev
+        d = self._dev
+        if 'row_ptr' not in d:
+            d['row_ptr'] = torch.from_numpy(self.row_ptr).to(dev)
+            d['col'] = torch.from_numpy(self.col).to(dev)
+            d['weights'] = None if self.weights is None else torch.from_numpy(self.weights).to(dev)
+            d['status'] = torch.zeros(1, dtype=torch.int32, device=dev)
+            st = d['status']
+            with torch.cuda.device(dev):
+                _native.call('dw_csr_validate', _native.ptr(d['row_ptr']),
+                             _native.ptr(d['col']) if self.nnz else None, self.vocab_size,
+                             self.nnz, _native.ptr(st), _native.stream(dev))
+            _native.check_status(st, 'CSR validation')
+        if need_sorted and 'col_sorted' not in d:
+            d['col_sorted'] = self._sorted_copy(dev)
+        if need_alias and self.weights is not None and 'prob_thr' not in d:
+            self._build_alias(dev)
+        return d
+
+    def _sorted_copy(self, dev) -> torch.Tensor:
+        d = self._dev
+        out = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
+        import ctypes
+        nbytes = ctypes.c_size_t(0)
+        with torch.cuda.device(dev):
+            s = _native.stream(dev)
+            _native.call('dw_csr_sort_copy', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                         self.vocab_size, self.nnz, _native.ptr(out), None, ctypes.byref(nbytes),
+                         s)
+            tmp = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+            _native.call('dw_csr_sort_copy', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                         self.vocab_size, self.nnz, _native.ptr(out), _native.ptr(tmp),
+                         ctypes.byref(nbytes), s)
+            del tmp
+        return out[:self.nnz] if self.nnz else out
+
+    def _build_alias(self, dev) -> None:
+        d = self._dev
+        n = max(self.nnz, 1)
+        d['prob_thr'] = torch.empty(n, dtype=torch.int32, device=dev)  # uint32 bit pattern
+        d['alias'] = torch.empty(n, dtype=torch.int32, device=dev)
+        work_p = torch.empty(n, dtype=torch.float64, device=dev)
+        work_i = torch.empty(n, dtype=torch.int32, device=dev)
+        st = d['status']
+        with torch.cuda.device(dev):
+            _native.call('dw_alias_build', _native.ptr(d['row_ptr']), _native.ptr(d['weights']),
+                         self.vocab_size, self.nnz, _native.ptr(d['prob_thr']),
+                         _native.ptr(d['alias']), _native.ptr(work_p), _native.ptr(work_i),
+                         _native.ptr(st), _native.stream(dev))
+        _native.check_status(st, 'alias build')

@@ -1,0 +1,193 @@
+"""Random walk generators — the reference API (random_walk_generator.py:11-151) on gfx950 kernels.
+
+Two sampling modes, one kernel family each (include/dw_hip.h):
+
+* ``rng='python'`` (default, reference-exact): every step consumes ONE double of CPython's
+  global ``random`` stream, exactly as ``random.choices(..., k=1)`` does in the reference
+  (random_walk_generator.py:68,113). The doubles are drawn on the host (rng.draw_uniforms) and
+  the replay kernel ``dw_walk_replay`` reproduces CPython's fp64 arithmetic, so
+  ``random.seed(s)`` yields the reference's walks bit for bit.
+* ``rng='philox'``: ``dw_walk_fast``, Philox4x32-10 keyed by (seed, global walk id); the walk
+  law is the reference's (including its inverted node2vec q rule), the stream is not.
+
+``walk(node) -> str`` keeps the reference signature; ``walk_batch`` is the batched device API
+(int32 vocabulary ids, shape [n_walks, length]) that feeds the fused SGNS kernel.
+"""
+from abc import ABC
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from shallow_encoders import _native
+from shallow_encoders.graph.csr import CSRGraph
+from shallow_encoders.graph.rng import draw_uniforms
+
+_CSR_CACHE_ATTR = '_dw_csr_cache'
+
+
+def _csr_of(graph) -> CSRGraph:
+    """CSR of a networkx graph, cached on the graph object (the walker borrows the graph)."""
+    if isinstance(graph, CSRGraph):
+        return graph
+    cached = graph.graph.get(_CSR_CACHE_ATTR) if hasattr(graph, 'graph') else None
+    if cached is not None and cached[0] == (graph.number_of_nodes(), graph.number_of_edges()):
+        return cached[1]
+    csr = CSRGraph.from_networkx(graph)
+    graph.graph[_CSR_CACHE_ATTR] = ((graph.number_of_nodes(), graph.number_of_edges()), csr)
+    return csr
+
+
+class RandomWalk(ABC):
+    """RandomWalk method interface (random_walk_generator.py:11-53)."""
+    METHOD = _native.DW_METHOD_DEEPWALK
+
+    def __init__(self, graph, length: int, rng: str = 'python', seed: int = 0, device=None):
+        """
+        Args:
+            graph: ``networkx.Graph`` (or a prebuilt ``CSRGraph`` for large synthetic graphs)
+            length: random walk length
+            rng: 'python' (bit-exact replay of the global ``random`` stream) or 'philox'
+            seed: Philox key (rng='philox')
+            device: HIP device (default: current)
+        """
+        assert length >= 1, 'Minimum walk length is 1!'
+        if rng not in ('python', 'philox'):
+            raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
+        self._graph = graph
+        self._length = length
+        self._rng = rng
+        self._seed = int(seed)
+        self._device = device
+        self._csr = _csr_of(graph)
+        self._next_walk_id = 0
+
+    # ---- reference host helpers (random_walk_generator.py:41-53) -----------------------
+    @property
+    def csr(self) -> CSRGraph:
+        return self._csr
+
+    @property
+    def length(self) -> int:
+        return self._length
+
+    def get_node_neighbors(self, node) -> List:
+        if isinstance(self._graph, CSRGraph):
+            return [self._csr.names[i] for i in self._csr.neighbors(self._csr.node_id(node))]
+        return list(self._graph.neighbors(node))
+
+    def get_node_unnormalized_edge_weights(self, node) -> List[float]:
+        i = self._csr.node_id(node)
+        a, b = self._csr.row_ptr[i], self._csr.row_ptr[i + 1]
+        if self._csr.weights is None:
+            return [1 for _ in range(a, b)]
+        return [float(w) for w in self._csr.weights[a:b]]
+
+    def get_node_normalized_edge_weights(self, node) -> List[float]:
+        w = self.get_node_unnormalized_edge_weights(node)
+        s = sum(w)
+        return [x / s for x in w]
+
+    # ---- walks ------------------------------------------------------------------------
+    def _params(self):
+        return 1.0, 1.0
+
+    def walk(self, node) -> str:
+        """Performs a random walk starting from ``node``; returns ``'n1 n2 n3'``."""
+        ids = self.walk_batch(torch.tensor([self._csr.node_id(node)], dtype=torch.int32))
+        return ' '.join(str(self._csr.names[i]) for i in ids[0].tolist())
+
+    def walk_batch(self, start_ids: Union[torch.Tensor, Sequence[int]],
+                   uniforms: Optional[np.ndarray] = None, walk_id0: Optional[int] = None,
+                   out: Optional[torch.Tensor] = None, check: bool = True) -> torch.Tensor:
+        """Walks from every start id (vocabulary ids) — int32 [n, length] on the device.
+
+        rng='python': the next n*(length-1) doubles of the global ``random`` stream are used
+        (or ``uniforms`` when given, shape [n, length-1]). rng='philox': walk ``k`` of this
+        call has global walk id ``walk_id0 + k`` (default: continues the previous call).
+        ``check=False`` skips the synchronising status check (stream stays asynchronous).
+        """
+        dev = _native.require_device(self._device)
+        starts = torch.as_tensor(start_ids, dtype=torch.int32)
+        starts = starts.to(dev, non_blocking=True).contiguous()
+        n = int(starts.numel())
+        L = self._length
+        d = self._csr.device_tensors(dev, need_sorted=self.METHOD == _native.DW_METHOD_NODE2VEC,
+                                     need_alias=self._rng == 'philox')
+        if out is None:
+            out = torch.empty((n, L), dtype=torch.int32, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        p, q = self._params()
+        with torch.cuda.device(dev):
+            s = _native.stream(dev)
+            if self._rng == 'python':
+                if uniforms is None:
+                    uniforms = draw_uniforms(n * (L - 1))
+                u = torch.from_numpy(np.ascontiguousarray(uniforms, dtype=np.float64).reshape(-1))
+                if u.numel() != n * (L - 1):
+                    raise ValueError('uniforms must have n_walks * (length - 1) values')
+                u = u.to(dev)
+                _native.call('dw_walk_replay', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                             _native.ptr(d.get('col_sorted')), _native.ptr(d['weights']),
+                             self._csr.vocab_size, _native.ptr(starts), n, L, self.METHOD,
+                             float(p), float(q), _native.ptr(u) if u.numel() else None,
+                             _native.ptr(out), _native.ptr(status), s)
+            else:
+                wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
+                _native.call('dw_walk_fast', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                             _native.ptr(d.get('col_sorted')), _native.ptr(d.get('prob_thr')),
+                             _native.ptr(d.get('alias')), self._csr.vocab_size,
+                             _native.ptr(starts), n, L, self.METHOD, float(p), float(q),
+                             self._seed & 0xFFFFFFFFFFFFFFFF, wid0, _native.ptr(out),
+                             _native.ptr(status), s)
+                self._next_walk_id = wid0 + n
+        if check:
+            _native.check_status(status, f'{type(self).__name__}.walk')
+        return out
+
+
+class DeepWalk(RandomWalk):
+    """First-order walk (random_walk_generator.py:56-72). https://arxiv.org/pdf/1403.6652.pdf"""
+    METHOD = _native.DW_METHOD_DEEPWALK
+
+
+class Node2Vec(RandomWalk):
+    """Second-order (p, q) walk (random_walk_generator.py:75-119).
+
+    Reproduces the reference's rule exactly, including its inversion of the paper's q:
+    a candidate equal to the previous node gets ``w * (1/p)``; a candidate ADJACENT to the
+    previous node gets ``w * (1/q)``; distance-2 candidates keep ``w``
+    (random_walk_generator.py:101-108). https://arxiv.org/pdf/1607.00653.pdf
+    """
+    METHOD = _native.DW_METHOD_NODE2VEC
+
+    def __init__(self, graph, length: int, p: float = 1.0, q: float = 1.0, **kwargs):
+        super().__init__(graph=graph, length=length, **kwargs)
+        self._p = p
+        self._q = q
+
+    def _params(self):
+        return self._p, self._q
+
+
+def random_walk_factory(name: str, graph, length: int,
+                        additional_params: Optional[dict] = None, **walker_kwargs) -> RandomWalk:
+    """Creates a random walk generator by name (random_walk_generator.py:122-151).
+
+    ``walker_kwargs`` (rng, seed, device) select the sampling mode; method parameters (p, q)
+    come through ``additional_params`` exactly as in the reference.
+    """
+    name = name.lower()
+    if additional_params is None:
+        additional_params = {}
+
+    SUPPORTED_METHODS = {
+        'deepwalk': DeepWalk,
+        'dfs': DeepWalk,
+        'node2vec': Node2Vec,
+    }
+    assert name in SUPPORTED_METHODS, \
+        f'Unknown method "{name}". Supported: {list(SUPPORTED_METHODS.keys())}'
+    return SUPPORTED_METHODS[name](graph=graph, length=length, **additional_params,
+                                   **walker_kwargs)
+

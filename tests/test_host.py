@@ -1,0 +1,270 @@
+"""Host-side logic of the product (CPU only): CSR/vocabulary, the replay stream, start-node
+order, collate, R-MAT spec, config loading, the C ABI surface, and the fast-mode oracle."""
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden
+from oracle import philox as ph
+from oracle import sgns_ref, walk_ref
+
+from shallow_encoders import _native
+from shallow_encoders.graph.csr import CSRGraph, node_token
+from shallow_encoders.graph.datasets import GraphTriplets, KarateClubDataset, RandomWalkDataset
+from shallow_encoders.graph.random_walk_generator import (DeepWalk, Node2Vec,
+                                                          random_walk_factory)
+from shallow_encoders.graph.rmat import csr_from_edges, rmat_edges
+from shallow_encoders.graph.rng import draw_uniforms, skip_uniforms
+from shallow_encoders.word2vec.dataloader.torch_dataset import W2VCollateFunctional, tokenize
+
+
+# ------------------------------------------------------------------------------ CSR / vocab
+@pytest.mark.parametrize('name,cls', [('walks_karate_node2vec_p1_q0.5.npz', KarateClubDataset),
+                                      ('walks_karate_deepwalk.npz', KarateClubDataset),
+                                      ('walks_triplets_deepwalk.npz', GraphTriplets)])
+def test_csr_from_networkx_matches_reference_layout(name, cls):
+    f = golden(name)
+    random.seed(0)
+    ds = cls(walks_per_node=1, walk_length=5)
+    csr = ds.csr
+    assert csr.itos == list(f['itos'])
+    np.testing.assert_array_equal(csr.row_ptr, f['row_ptr'])
+    np.testing.assert_array_equal(csr.col, f['col'])
+    if bool(f['weighted']):
+        np.testing.assert_array_equal(csr.weights, f['weights'])
+    else:
+        assert csr.weights is None
+
+
+@pytest.mark.parametrize('name', ['walks_rmat12_deepwalk.npz', 'walks_rmat12_node2vec_p0.25_q4.npz'])
+def test_rmat_csr_matches_networkx_order(name):
+    f = golden(name)
+    edges, _ = rmat_edges(int(f['scale']), int(f['n_edges']), int(f['graph_seed']))
+    np.testing.assert_array_equal(edges, f['edges'])
+    csr = csr_from_edges(1 << int(f['scale']), edges)
+    np.testing.assert_array_equal(csr.row_ptr, f['row_ptr'])
+    np.testing.assert_array_equal(csr.col, f['col'])
+
+
+def test_rmat_spec_properties():
+    edges, n_patched = rmat_edges(12, 40_000, 0)
+    n = 1 << 12
+    assert (edges[:, 0] != edges[:, 1]).all()
+    key = np.minimum(edges[:, 0], edges[:, 1]) * n + np.maximum(edges[:, 0], edges[:, 1])
+    assert len(np.unique(key)) == len(key)
+    deg = np.bincount(edges.ravel(), minlength=n)
+    assert (deg > 0).all() and n_patched > 0
+    g = csr_from_edges(n, edges)
+    assert g.vocab_size == n + 1 and g.degree()[0] == 0
+    assert g.itos[1] == 'n0000000' and g.itos[-1] == f'n{n - 1:07d}'
+
+
+def test_node_tokens_and_tokenizer():
+    assert node_token('N01') == 'n01'
+    assert tokenize('n01 a2 <unk> B7') == ['n01', 'a2', '<unk>', 'b7']
+    with pytest.raises(ValueError):
+        node_token('12')
+    with pytest.raises(ValueError):
+        node_token('a b')
+
+
+# ------------------------------------------------------------------------------ random stream
+def test_draw_uniforms_is_the_python_stream():
+    random.seed(123)
+    a = draw_uniforms(5000)
+    after = random.random()
+    random.seed(123)
+    b = np.array([random.random() for _ in range(5000)])
+    np.testing.assert_array_equal(a, b)
+    assert random.random() == after
+    random.seed(9)
+    skip_uniforms(777)
+    x = random.random()
+    random.seed(9)
+    for _ in range(777):
+        random.random()
+    assert random.random() == x
+
+
+@pytest.mark.parametrize('name,cls,kw', [
+    ('walks_karate_node2vec_p1_q0.5.npz', KarateClubDataset,
+     dict(method='node2vec', method_params={'p': 1, 'q': 0.5})),
+    ('walks_karate_node2vec_p0.3_q3.npz', KarateClubDataset,
+     dict(method='node2vec', method_params={'p': 0.3, 'q': 3})),
+    ('walks_karate_deepwalk.npz', KarateClubDataset, dict(method='deepwalk')),
+    ('walks_triplets_deepwalk.npz', GraphTriplets, dict(method='deepwalk'))])
+def test_dataset_order_and_stream_match_reference(name, cls, kw):
+    """Constructor shuffle, the uniforms one epoch consumes, and the end-of-epoch reshuffle."""
+    f = golden(name)
+    random.seed(int(f['seed']))
+    ds = cls(walks_per_node=int(f['walks_per_node']), walk_length=int(f['walk_length']), **kw)
+    np.testing.assert_array_equal(ds.start_ids(0, len(ds)), f['starts'])
+    np.testing.assert_array_equal(ds._node_ids, f['order'])
+    u = draw_uniforms(len(ds) * (int(f['walk_length']) - 1))
+    np.testing.assert_array_equal(u.reshape(f['uniforms'].shape), f['uniforms'])
+    ds._reshuffle()
+    np.testing.assert_array_equal(ds._node_ids, f['order_after'])
+
+
+def test_factory_contract():
+    import networkx as nx
+    g = nx.path_graph(['a', 'b', 'c'])
+    assert isinstance(random_walk_factory('DeepWalk', g, 3), DeepWalk)
+    assert isinstance(random_walk_factory('dfs', g, 3), DeepWalk)
+    w = random_walk_factory('node2vec', g, 3, {'p': 2, 'q': 3})
+    assert isinstance(w, Node2Vec) and w._params() == (2, 3)
+    with pytest.raises(AssertionError):
+        random_walk_factory('bfs', g, 3)
+    with pytest.raises(TypeError):
+        random_walk_factory('deepwalk', g, 3, {'p': 2})
+    with pytest.raises(AssertionError):
+        DeepWalk(g, 0)
+    assert w.get_node_neighbors('b') == ['a', 'c']
+    assert w.get_node_normalized_edge_weights('b') == [0.5, 0.5]
+
+
+# ------------------------------------------------------------------------------ collate
+@pytest.mark.parametrize('R', [1, 2, 5])
+def test_collate_matches_reference_rule(R):
+    rng = np.random.default_rng(R)
+    texts = [torch.as_tensor(rng.integers(0, 100, size=rng.integers(2 * R + 1, 40)))
+             for _ in range(7)]
+    inp, tgt = W2VCollateFunctional('sg', R, 256)(texts)
+    ins, tgts = [], []
+    for t in texts:
+        i, g = sgns_ref.sg_windows(t.numpy()[None, :], R)
+        ins.append(i)
+        tgts.append(g)
+    np.testing.assert_array_equal(inp.numpy(), np.concatenate(ins))
+    np.testing.assert_array_equal(tgt.numpy(), np.concatenate(tgts))
+    ci, ct = W2VCollateFunctional('cbow', R, 256)(texts)
+    np.testing.assert_array_equal(ci.numpy(), tgt.numpy())
+    np.testing.assert_array_equal(ct.numpy(), inp.numpy())
+    with pytest.raises(AssertionError):
+        W2VCollateFunctional('sg', R, 256)([torch.arange(2 * R)])
+    clipped, _ = W2VCollateFunctional('sg', R, 2 * R + 3)([torch.arange(50)])
+    assert clipped.shape[0] == 3
+
+
+# ------------------------------------------------------------------------------ configs
+@pytest.mark.parametrize('cfg', ['sge_sg_karate_club', 'sge_sg_cora', 'sge_sg_graph_triplets',
+                                 'sge_sg_rmat20'])
+def test_reference_configs_load(cfg):
+    from shallow_encoders.config_parser import load_config
+    c = load_config(cfg)
+    assert c.datamodule.is_graph and c.datamodule.mode == 'sg'
+    assert c.model['_target_'] == 'shallow_encoders.word2vec.model.SkipGram'
+    assert c.train.optimizer['_target_'] == 'torch.optim.Adam'
+    assert c.analysis.checkpoint == 'last.ckpt'
+
+
+def test_config_overrides_and_instantiation():
+    from shallow_encoders.config_parser import instantiate, load_config
+    from shallow_encoders.word2vec.optim import Adam
+    c = load_config('sge_sg_cora', overrides=['model.embedding_size=128',
+                                              'datamodule.additional_parameters.method_params.q=1'])
+    assert c.model['embedding_size'] == 128
+    assert c.datamodule.additional_parameters['method_params']['q'] == 1
+    m = instantiate(c.model, vocab_size=11)
+    assert tuple(m.input_embedding.shape) == (11, 128)
+    assert set(m.state_dict()) == {'_input_embedding.weight', '_output_embedding.weight'}
+    opt = c.train.instantiate_optimizer(m.parameters())
+    assert isinstance(opt, Adam) and opt.param_groups[0]['lr'] == 0.1
+    sched = c.train.instantiate_scheduler(opt)
+    assert isinstance(sched, torch.optim.lr_scheduler.StepLR)
+
+
+# ------------------------------------------------------------------------------ C ABI surface
+def _header_functions():
+    text = open(os.path.join(REPO, 'include', 'dw_hip.h')).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(dw_[a-z0-9_]+)\s*\(', text)))
+
+
+def test_abi_library_exports_every_declared_symbol():
+    lib = _native.load()  # loads without a GPU; no compute call is made
+    declared = _header_functions()
+    assert declared == sorted(_native.SIGNATURES)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.dw_abi_version() == _native.ABI_VERSION
+
+
+def test_abi_rejects_bad_arguments_without_a_device():
+    lib = _native.load()
+    # argument validation returns an error code and sets the message (no launch happens)
+    rc = lib.dw_walk_replay(None, None, None, None, 0, None, 1, 0, 0, 1.0, 1.0, None, None, None,
+                            None)
+    assert rc == _native.DW_E_INVALID_ARG
+    assert b'Minimum walk length' in lib.dw_last_error_string()
+    rc = lib.dw_sgns_walks(None, 1, 4, 2, 1, 10, 8, None, None, None, None, None, 0, 0, 1.0,
+                           None, None, None)
+    assert rc == _native.DW_E_INVALID_ARG
+    assert b'2R+1' in lib.dw_last_error_string()
+
+
+def test_product_paths_refuse_host_tensors():
+    with pytest.raises(ValueError):
+        _native.ptr(torch.zeros(3))
+
+
+# ------------------------------------------------------------------------------ fast-mode oracle
+def test_philox_known_answers():
+    # Random123 known-answer vectors for philox4x32-10
+    r = ph.philox(0, 0, 0, 0, 0, 0)
+    assert [int(x) for x in r] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    m = 0xFFFFFFFF
+    r = ph.philox(m, m, m, m, m, m)
+    assert [int(x) for x in r] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    r = ph.philox(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0)
+    assert [int(x) for x in r] == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_alias_oracle_represents_the_weights():
+    f = golden('walks_karate_deepwalk.npz')
+    prob, alias = ph.alias_tables(f['row_ptr'], f['weights'])
+    rp = f['row_ptr']
+    for r in range(1, len(rp) - 1):
+        a, b = rp[r], rp[r + 1]
+        n = b - a
+        mass = np.zeros(n)
+        for i in range(n):
+            t = int(prob[a + i])
+            pa = 1.0 if t == ph.ALWAYS else t / 4294967296.0
+            mass[i] += pa / n
+            mass[alias[a + i]] += (1 - pa) / n
+        w = f['weights'][a:b]
+        np.testing.assert_allclose(mass, w / w.sum(), atol=1e-8)
+
+
+def test_fast_node2vec_oracle_law_matches_reference_rule():
+    """The ballot-rejection restatement samples the reference's transition law."""
+    f = golden('walks_karate_node2vec_p0.3_q3.npz')
+    g = walk_ref.CSR(f['row_ptr'], f['col'], f['weights'])
+    prob, alias = ph.alias_tables(f['row_ptr'], f['weights'])
+    # many one-step transitions out of (prev=1, v=34's first neighbour pair) via length-3 walks
+    v, prev = 34, int(g.neighbors(34)[0])
+    starts = [prev] * 4000
+    walks = ph.fast_walks(f['row_ptr'], f['col'], starts, 3, 'node2vec', 0.3, 3.0, seed=5,
+                          walk_id0=0, prob_thr=prob, alias=alias)
+    sel = walks[walks[:, 1] == v][:, 2]
+    law = walk_ref.node2vec_transition(g, prev, v, 0.3, 3.0)
+    xs = sorted(law)
+    counts = np.array([(sel == x).sum() for x in xs], dtype=float)
+    expected = np.array([law[x] for x in xs]) * len(sel)
+    chi2 = ((counts - expected) ** 2 / np.maximum(expected, 1e-12)).sum()
+    from scipy.stats import chi2 as chi2_dist
+    assert len(sel) > 50
+    assert chi2_dist.sf(chi2, len(xs) - 1) > 1e-3
+
+
+def test_device_noise_oracle_is_uniform():
+    nz = ph.device_noise(seed=3, noise_offset=0, n_centres=400, n_ctx=4, k=5, vocab_size=7)
+    assert nz.shape == (400, 4, 5) and nz.min() >= 0 and nz.max() < 7
+    counts = np.bincount(nz.ravel(), minlength=7)
+    from scipy.stats import chisquare
+    assert chisquare(counts).pvalue > 1e-3

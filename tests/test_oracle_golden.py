@@ -1,0 +1,123 @@
+"""The oracle against the reference's own outputs (golden fixtures). CPU only.
+
+Pins oracle/walk_ref.py and oracle/sgns_ref.py before any device result is judged by them.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from oracle import sgns_ref, walk_ref
+
+WALK_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'walks_*.npz')))
+SGNS_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'sgns_*.npz')))
+
+
+def _graph(f):
+    w = f['weights'] if ('weights' in f.files and f['weights'].size) else None
+    return walk_ref.CSR(f['row_ptr'], f['col'], w)
+
+
+@pytest.mark.parametrize('name', WALK_FIXTURES)
+def test_oracle_replays_reference_walks_bit_exact(name):
+    f = golden(name)
+    g = _graph(f)
+    out = walk_ref.walks_replay(g, f['starts'], int(f['walk_length']), str(f['method']),
+                                float(f['p']), float(f['q']), f['uniforms'])
+    np.testing.assert_array_equal(out, f['walks'])
+
+
+@pytest.mark.parametrize('name', [n for n in WALK_FIXTURES if 'karate' in n or 'triplets' in n])
+def test_oracle_transition_law_matches_reference(name):
+    """Every random.choices weight vector the reference used equals the oracle's law."""
+    f = golden(name)
+    g = _graph(f)
+    walks, L = f['walks'], int(f['walk_length'])
+    offs, pop, w = f['step_off'], f['step_pop'], f['step_w']
+    method, p, q = str(f['method']), float(f['p']), float(f['q'])
+    k = 0
+    for wk in walks:
+        prev = None
+        for s in range(1, L):
+            v = int(wk[s - 1])
+            a, b = offs[k], offs[k + 1]
+            law = walk_ref.node2vec_transition(g, prev if method == 'node2vec' else None, v,
+                                               p if method == 'node2vec' else 1.0,
+                                               q if method == 'node2vec' else 1.0)
+            np.testing.assert_array_equal(pop[a:b], g.neighbors(v))
+            got = np.array([law[x] for x in pop[a:b]])
+            np.testing.assert_array_equal(got, w[a:b])  # bit-exact normalised weights
+            prev = v
+            k += 1
+    assert k == len(offs) - 1
+
+
+@pytest.mark.parametrize('name', SGNS_FIXTURES)
+def test_oracle_sgns_matches_reference(name):
+    f = golden(name)
+    loss, g_in, g_out, rec, prec = sgns_ref.sgns_forward_backward(
+        f['w_in0'], f['w_out0'], f['inputs'], f['targets'], f['noise'][0])
+    np.testing.assert_allclose([loss['loss'], loss['positive-loss'], loss['negative-loss']],
+                               f['losses'][0], rtol=1e-6)
+    np.testing.assert_allclose(g_in, f['g_in'], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(g_out, f['g_out'], rtol=1e-5, atol=1e-9)
+    assert rec == pytest.approx(float(f['recall'][0]))
+    assert prec == pytest.approx(float(f['precision'][0]))
+    # independent float64 closed form of the same gradient (clamp mask + batch mean)
+    l64, gi64, go64 = sgns_ref.sgns_grads_closed_form(f['w_in0'], f['w_out0'], f['inputs'],
+                                                      f['targets'], f['noise'][0])
+    assert l64 == pytest.approx(float(f['losses'][0][0]), rel=1e-5)
+    np.testing.assert_allclose(gi64, f['g_in'], rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(go64, f['g_out'], rtol=1e-4, atol=1e-8)
+
+
+@pytest.mark.parametrize('name', SGNS_FIXTURES)
+def test_oracle_adam_trajectory_matches_reference(name):
+    f = golden(name)
+    ref = sgns_ref.TorchAdamRef(f['w_in0'], f['w_out0'], lr=float(f['lr']))
+    for step in range(f['noise'].shape[0]):
+        loss = ref.train_step(f['inputs'], f['targets'], f['noise'][step])
+        assert loss['loss'] == pytest.approx(float(f['losses'][step][0]), rel=1e-6)
+        if step == 0:
+            w_in, w_out = ref.tables()
+            np.testing.assert_allclose(w_in, f['w_in1'], rtol=1e-6, atol=1e-7)
+            np.testing.assert_allclose(w_out, f['w_out1'], rtol=1e-6, atol=1e-7)
+    w_in, w_out = ref.tables()
+    np.testing.assert_allclose(w_in, f['w_in_n'], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(w_out, f['w_out_n'], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('name', SGNS_FIXTURES)
+def test_oracle_windows_match_reference_collate(name):
+    f = golden(name)
+    ins, tgt = sgns_ref.sg_windows(f['walks'], int(f['R']))
+    np.testing.assert_array_equal(ins, f['inputs'])
+    np.testing.assert_array_equal(tgt, f['targets'])
+
+
+def test_oracle_trajectory_with_steplr():
+    import torch
+    f = golden('traj_karate_node2vec.npz')
+    ref = sgns_ref.TorchAdamRef(f['w_in0'], f['w_out0'], lr=float(f['lr']))
+    sched = torch.optim.lr_scheduler.StepLR(ref.opt, step_size=int(f['step_size']),
+                                            gamma=float(f['gamma']))
+    R, K = int(f['R']), int(f['K'])
+    offs = np.concatenate([[0], np.cumsum(f['batch_sizes'])])
+    noff = 0
+    epoch = 0
+    for step, nb in enumerate(f['batch_sizes']):
+        if f['epoch_of_step'][step] != epoch:
+            sched.step()
+            epoch = int(f['epoch_of_step'][step])
+        walks = f['walks'][offs[step]:offs[step + 1]]
+        ins, tgt = sgns_ref.sg_windows(walks, R)
+        nz = f['noise'][noff:noff + len(ins)]
+        noff += len(ins)
+        assert ref.opt.param_groups[0]['lr'] == pytest.approx(float(f['lrs'][step]))
+        loss = ref.train_step(ins, tgt, nz)
+        assert loss['loss'] == pytest.approx(float(f['losses'][step]), rel=1e-6)
+    w_in, w_out = ref.tables()
+    np.testing.assert_allclose(w_in, f['w_in'], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(w_out, f['w_out'], rtol=1e-5, atol=1e-6)
