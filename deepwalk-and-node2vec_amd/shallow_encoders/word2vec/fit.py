@@ -1,0 +1,98 @@
+"""Training loop used by tools/train.py (the reference delegates to PL ``Trainer.fit``,
+tools/train.py:60-83, which is not installed in this image).
+
+Semantics kept from PL's automatic optimisation (SURVEY.md §8c "PL loop semantics"):
+one ``optimizer.step()`` per batch, gradients zeroed every step, the scheduler stepped once
+per epoch (or per step for ``{'scheduler': ..., 'interval': 'step'}`` configs,
+config_parser/core.py:55-94), ``on_train_epoch_end`` metric flush, and a
+``ModelCheckpoint(save_top_k=-1, save_last=True)`` equivalent (tools/train.py:74-80): one
+``checkpoint_epoch=EEEEEE_step=SSSSSSSSS.ckpt`` per epoch plus ``last.ckpt``, each a
+torch-loadable dict whose ``state_dict`` keys are ``_model._input_embedding.weight`` /
+``_model._output_embedding.weight`` like a Lightning checkpoint of Word2VecTrainer.
+Metrics go to ``metrics.csv`` (one row per logged step / epoch) under the TensorBoard
+directory layout of tools/conventions.py.
+"""
+import csv
+import os
+import time
+from typing import Dict, Iterable, Optional
+
+import torch
+
+from shallow_encoders.word2vec.trainer import Word2VecTrainer
+
+
+def save_checkpoint(path: str, trainer: Word2VecTrainer, epoch: int, global_step: int) -> None:
+    state = {f'_model.{k}': v.detach().cpu() for k, v in trainer.model.state_dict().items()}
+    torch.save({'epoch': epoch, 'global_step': global_step, 'state_dict': state,
+                'pytorch-lightning_version': None}, path)
+
+
+class CSVMetricLogger:
+    """metrics.csv with columns step, epoch, name, value."""
+
+    def __init__(self, dirpath: Optional[str]):
+        self.dirpath = dirpath
+        self._rows = []
+        if dirpath:
+            os.makedirs(dirpath, exist_ok=True)
+
+    def log(self, step: int, epoch: int, values: Dict[str, float]) -> None:
+        for k, v in values.items():
+            self._rows.append((step, epoch, k, float(v)))
+
+    def flush(self) -> None:
+        if not self.dirpath or not self._rows:
+            return
+        path = os.path.join(self.dirpath, 'metrics.csv')
+        new = not os.path.exists(path)
+        with open(path, 'a', newline='') as f:
+            w = csv.writer(f)
+            if new:
+                w.writerow(['step', 'epoch', 'name', 'value'])
+            w.writerows(self._rows)
+        self._rows = []
+
+
+def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
+        checkpoint_dir: Optional[str] = None, log_dir: Optional[str] = None,
+        log_every_n_steps: int = 50, verbose: bool = True) -> Dict[str, float]:
+    """Train for ``max_epochs``; returns the last epoch's metric means."""
+    trainer.manual_grads = True
+    opt = trainer.optimizer
+    sched = trainer.scheduler
+    step_sched = isinstance(sched, dict) and sched.get('interval', 'epoch') == 'step'
+    sched_obj = sched['scheduler'] if isinstance(sched, dict) else sched
+    logger = CSVMetricLogger(log_dir)
+    if checkpoint_dir:
+        os.makedirs(checkpoint_dir, exist_ok=True)
+    global_step = 0
+    last = {}
+    for epoch in range(max_epochs):
+        t0 = time.perf_counter()
+        n_batches = 0
+        for batch in dataloader:
+            loss = trainer.training_step(batch)
+            opt.step()
+            opt.zero_grad()
+            if step_sched and sched_obj is not None:
+                sched_obj.step()
+            if log_dir and global_step % log_every_n_steps == 0:
+                logger.log(global_step, epoch, {f'train/{k}': v for k, v in loss.items()})
+            global_step += 1
+            n_batches += 1
+        if not step_sched and sched_obj is not None:
+            sched_obj.step()
+        last = trainer.on_train_epoch_end()
+        last['epoch/lr'] = float(opt.param_groups[0]['lr'])
+        logger.log(global_step, epoch, last)
+        logger.flush()
+        if checkpoint_dir:
+            name = f'checkpoint_epoch={epoch:06d}_step={global_step:09d}.ckpt'
+            save_checkpoint(os.path.join(checkpoint_dir, name), trainer, epoch, global_step)
+            save_checkpoint(os.path.join(checkpoint_dir, 'last.ckpt'), trainer, epoch, global_step)
+        if verbose:
+            dt = time.perf_counter() - t0
+            msg = ' '.join(f'{k}={v:.4f}' for k, v in last.items() if k.endswith('loss'))
+            print(f'epoch {epoch}: {n_batches} batches in {dt:.2f}s {msg}', flush=True)
+    return last
