@@ -137,9 +137,10 @@ class RandomWalkDataset:
 
     def next_walk_batch(self, max_walks: int, check: bool = True) -> Optional[torch.Tensor]:
         """The next <= max_walks walks of the epoch as device int32 [n, L]; None at epoch end
-        (which reshuffles, as ``StopIteration`` does)."""
+        (which reshuffles, as ``StopIteration`` does, and rewinds like ``__iter__``)."""
         if self._index >= len(self):
             self._reshuffle()
+            self._index = 0
             return None
         n = min(int(max_walks), len(self) - self._index)
         starts = torch.from_numpy(self.start_ids(self._index, n))

@@ -55,12 +55,20 @@ def test_trajectory_matches_reference(manual_grads, hip_device):
     f = golden('traj_karate_node2vec.npz')
     model, losses = _reference_run(f, manual_grads)
     np.testing.assert_allclose(losses, f['losses'], rtol=1e-4)
-    from test_gpu_sgns import assert_params_close
+    from oracle import sgns_ref
+    from test_gpu_sgns import assert_within_envelope, reference_envelope
+    offs = np.concatenate([[0], np.cumsum(f['batch_sizes'])])
+    batches, noff = [], 0
+    for step in range(len(f['batch_sizes'])):
+        ins, tgt = sgns_ref.sg_windows(f['walks'][offs[step]:offs[step + 1]], int(f['R']))
+        batches.append((ins, tgt, f['noise'][noff:noff + len(ins)], float(f['lrs'][step])))
+        noff += len(ins)
+    ex_in, ex_out = reference_envelope(f['w_in0'], f['w_out0'], float(f['lr']), batches)
     lr = float(f['lr'])
-    assert_params_close(model.input_embedding.numpy(), f['w_in'], lr, rtol=1e-4, atol=1e-5,
-                        max_frac=2e-2)
-    assert_params_close(model.output_embedding.numpy(), f['w_out'], lr, rtol=1e-4, atol=1e-5,
-                        max_frac=2e-2)
+    assert_within_envelope(model.input_embedding.numpy(), f['w_in'], ex_in, lr, rtol=1e-4,
+                           atol=1e-5)
+    assert_within_envelope(model.output_embedding.numpy(), f['w_out'], ex_out, lr, rtol=1e-4,
+                           atol=1e-5)
 
 
 def test_train_cli_karate_end_to_end(tmp_path, hip_device):
