@@ -100,6 +100,8 @@ def main():
     ap.add_argument('--walk-length', type=int, default=80)
     ap.add_argument('--walks-per-node', type=int, default=10)
     ap.add_argument('--lr', type=float, default=0.01)
+    ap.add_argument('--scatter', default='sorted', choices=['sorted', 'atomic'],
+                    help='output-table gradient: records+sort+gather (sorted) or float atomics')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-walk-bench', action='store_true')
@@ -162,7 +164,7 @@ def main():
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K,
                         walks=walks_buf, context_radius=R, noise=None, seed=99,
                         noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale,
-                        loss_acc=loss_acc, status=status)
+                        loss_acc=loss_acc, status=status, scatter=args.scatter)
         if record:
             e[2].record()
         tables.step()
@@ -240,7 +242,8 @@ def main():
                 'random Xavier init)',
         'config': {
             'workload': (f'C3: R-MAT {N} nodes / {csr.nnz // 2} edges, {args.method} L={L}, '
-                         f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU'),
+                         f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU; '
+                         f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
             'parallelism': f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather)',
         },
@@ -249,7 +252,8 @@ def main():
         'kernel_ms': kern_ms,
         'mean_loss': mean_loss,
         'roofline': {
-            'kernel': 'dw_sgns_walks (k_sgns)',
+            'kernel': ('dw_sgns_walks: k_sgns + hipcub radix sort + k_rec_gather, timed together'
+                       if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
             'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,

@@ -32,7 +32,7 @@ DW_S_BAD_INDEX = 16
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -55,9 +55,10 @@ SIGNATURES = {
     'dw_walk_fast': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _i32, _f64, _f64,
                                     _u64, _u64, _p, _p, _p]),
     'dw_sgns_walks': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
-                                     _p, _u64, _u64, _f32, _p, _p, _p]),
+                                     _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_pairs': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
-                                     _p, _u64, _u64, _f32, _p, _p, _p]),
+                                     _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
+    'dw_sgns_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),
     'dw_skipgram_logits': (ctypes.c_int, [_p, _p, _i64, _i32, _i64, _i32, _p, _p, _i32, _p, _p,
                                           _p]),
     'dw_skipgram_logits_backward': (ctypes.c_int, [_p, _p, _i64, _i32, _i64, _i32, _p, _p, _p,

@@ -17,6 +17,9 @@ from typing import Dict, Optional
 
 import torch
 
+# (T = 2R(1+K) <= 256 and V < 2^31 for the records path; larger falls back to 'atomic')
+RECORDS_MAX_ROWS = 256
+
 from shallow_encoders import _native
 
 
@@ -35,18 +38,44 @@ def loss_terms(acc: torch.Tensor, n_terms: int, neg_samples: int) -> Dict[str, t
     return out
 
 
+_WORKSPACES: Dict[torch.device, torch.Tensor] = {}
+
+
+def _use_records(scatter: str, n_ctx: int, neg_samples: int, vocab_size: int) -> bool:
+    return (scatter == 'sorted' and n_ctx * (1 + neg_samples) <= RECORDS_MAX_ROWS
+            and vocab_size < 2 ** 31)
+
+
+def workspace_for(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int,
+                  device: torch.device) -> torch.Tensor:
+    """Device workspace of the atomic-free (records) output-table path, cached per device and
+    grown on demand (allocated outside any timed region after the first call)."""
+    import ctypes
+    nbytes = ctypes.c_size_t(0)
+    _native.call('dw_sgns_workspace_bytes', int(n_centres), int(n_ctx), int(neg_samples),
+                 int(vocab_size), ctypes.byref(nbytes))
+    ws = _WORKSPACES.get(device)
+    if ws is None or ws.numel() < nbytes.value:
+        _WORKSPACES.pop(device, None)
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=device)
+        _WORKSPACES[device] = ws
+    return ws
+
+
 def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                     g_out: torch.Tensor, neg_samples: int, *, walks: Optional[torch.Tensor] = None,
                     context_radius: int = 0, inputs: Optional[torch.Tensor] = None,
                     targets: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                     seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                     loss_acc: Optional[torch.Tensor] = None,
-                    status: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Launch the fused SGNS kernel; returns the float64[4] loss accumulator.
+                    status: Optional[torch.Tensor] = None, scatter: str = 'sorted') -> torch.Tensor:
+    """Launch the fused SGNS kernel(s); returns the float64[4] loss accumulator.
 
     Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B,1]) +
     ``targets`` (int64 [B, C]). ``noise``: int64 [B', C, K] replayed negatives or None (device
     Philox keyed by (seed, noise_offset + centre)). ``grad_scale`` defaults to 1/(B'*C).
+    ``scatter``: 'sorted' (records + radix sort + per-row gather, no output-table atomics) or
+    'atomic' (float atomics straight into g_out).
     """
     dev = w_in.device
     V, d = w_in.shape
@@ -55,6 +84,8 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
     for t in (w_in, w_out, g_in, g_out):
         if t.dtype != torch.float32:
             raise TypeError('embedding tables and gradients must be float32')
+    if scatter not in ('sorted', 'atomic'):
+        raise ValueError('scatter must be "sorted" or "atomic"')
     if loss_acc is None:
         loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     if status is None:
@@ -72,11 +103,13 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
             if noise is not None and noise.numel() != n_centres * C * K:
                 raise ValueError('noise must have B\' * 2R * K entries')
             scale = 1.0 / max(n_centres * C, 1) if grad_scale is None else grad_scale
+            ws = workspace_for(n_centres, C, K, V, dev) \
+                if _use_records(scatter, C, K, V) else None
             _native.call('dw_sgns_walks', _native.ptr(walks), n, L, R, K, V, d,
                          _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_in),
                          _native.ptr(g_out), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), float(scale), _native.ptr(loss_acc),
-                         _native.ptr(status), s)
+                         _native.ptr(status), _native.ptr(ws), 0 if ws is None else ws.numel(), s)
         else:
             if inputs is None or targets is None:
                 raise ValueError('give walks, or inputs and targets')
@@ -87,11 +120,13 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
             if noise is not None and noise.numel() != B * C * K:
                 raise ValueError('noise must have B * C * K entries')
             scale = 1.0 / max(B * C, 1) if grad_scale is None else grad_scale
+            ws = workspace_for(B, C, K, V, dev) if _use_records(scatter, C, K, V) else None
             _native.call('dw_sgns_pairs', _native.ptr(inputs.contiguous()),
                          _native.ptr(targets.contiguous()), B, C, K, V, d, _native.ptr(w_in),
                          _native.ptr(w_out), _native.ptr(g_in), _native.ptr(g_out),
                          _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
-                         float(scale), _native.ptr(loss_acc), _native.ptr(status), s)
+                         float(scale), _native.ptr(loss_acc), _native.ptr(status),
+                         _native.ptr(ws), 0 if ws is None else ws.numel(), s)
     return loss_acc
 
 

@@ -118,15 +118,22 @@ int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_
  *   noise: int64[B', 2R, K] replayed negatives, or NULL = draw uniform [0,V) on device with
  *          Philox keyed by (seed, noise_offset + b, j*K + k).
  *   w_in/w_out: float32[V, d] (in/out embedding tables, row-major);
- *   g_in/g_out: float32[V, d] gradients, ACCUMULATED (+=) with atomics;
+ *   g_in/g_out: float32[V, d] gradients, ACCUMULATED (+=);
  *   grad_scale: d(loss)/d(term) = 1/M, M = total centres*2R of the (global) batch.
  *   loss_acc: float64[4] accumulated (+=): sum positive-loss, sum negative-loss (summed over K),
- *             count(sigmoid(s)>=0.5), count(sigmoid(t)>=0.5)  (trainer.py:145-150). */
+ *             count(sigmoid(s)>=0.5), count(sigmoid(t)>=0.5)  (trainer.py:145-150).
+ *   workspace: NULL -> output-table gradients scattered with float atomics;
+ *              non-NULL (>= dw_sgns_workspace_bytes) -> atomic-free output-table path: one
+ *              {row, centre, coef} record per output row, radix-sorted by row, then summed per
+ *              row from gathered centre rows (stable order: g_out is reproducible run to run
+ *              except at rows straddling two 512-record chunks). The centre-table gradient is
+ *              one float-atomic row per centre in both modes. */
 int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                   int32_t context_radius, int32_t neg_samples, int64_t vocab_size, int32_t dim,
                   const float *w_in, const float *w_out, float *g_in, float *g_out,
                   const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
-                  double *loss_acc, int32_t *status, void *stream);
+                  double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
+                  void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
@@ -134,7 +141,13 @@ int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, 
                   int32_t neg_samples, int64_t vocab_size, int32_t dim,
                   const float *w_in, const float *w_out, float *g_in, float *g_out,
                   const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
-                  double *loss_acc, int32_t *status, void *stream);
+                  double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
+                  void *stream);
+
+/* Bytes of device workspace the records path needs for n_centres centres with n_ctx contexts
+ * and neg_samples negatives each over a vocabulary of vocab_size rows. */
+int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
+                            int64_t vocab_size, size_t *bytes);
 
 /* SkipGram.forward(inputs, outputs, proba) (model.py:79-91): logits[b, n] =
  * <w_in[inputs[b]], w_out[outputs[b, n]]>, sigmoid applied when proba != 0. */

@@ -73,7 +73,8 @@ def _tables(f):
 
 @pytest.mark.parametrize('name', SGNS_FIXTURES)
 @pytest.mark.parametrize('mode', ['pairs', 'walks'])
-def test_fused_sgns_step_vs_reference(name, mode, hip_device):
+@pytest.mark.parametrize('scatter', ['sorted', 'atomic'])
+def test_fused_sgns_step_vs_reference(name, mode, scatter, hip_device):
     f = golden(name)
     w_in, w_out = _tables(f)
     g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
@@ -81,10 +82,11 @@ def test_fused_sgns_step_vs_reference(name, mode, hip_device):
     noise = _dev(f['noise'][0], torch.int64)
     if mode == 'pairs':
         acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, inputs=_dev(f['inputs'], torch.int64),
-                              targets=_dev(f['targets'], torch.int64), noise=noise)
+                              targets=_dev(f['targets'], torch.int64), noise=noise,
+                              scatter=scatter)
     else:
         acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=_dev(f['walks'], torch.int32),
-                              context_radius=R, noise=noise)
+                              context_radius=R, noise=noise, scatter=scatter)
     t = loss_terms(acc, f['targets'].size, K)
     np.testing.assert_allclose([float(t['loss']), float(t['positive-loss']),
                                 float(t['negative-loss'])], f['losses'][0], rtol=1e-5)
@@ -149,13 +151,18 @@ def test_adam_kernel_vs_torch_adam_random_grads(hip_device):
                                ropt.state[ref]['exp_avg_sq'].numpy(), rtol=1e-5, atol=1e-10)
 
 
-@pytest.mark.parametrize('d', [100, 128, 256, 300])
-def test_fused_sgns_random_case_vs_oracle(d, hip_device):
-    """Larger vocabularies / masked widths against the torch-CPU oracle (autograd)."""
+@pytest.mark.parametrize('d,hub', [(100, False), (128, False), (256, False), (300, False),
+                                   (128, True), (64, True)])
+def test_fused_sgns_random_case_vs_oracle(d, hub, hip_device):
+    """Larger vocabularies / masked widths against the torch-CPU oracle (autograd). `hub`:
+    every 3rd walk position is node 7, so row 7 collects thousands of records and straddles
+    many 512-record chunks of the sorted path (boundary atomics)."""
     rng = np.random.default_rng(d)
     V, R, K, L, n = 20_000, 5, 5, 40, 48
     w_in0, w_out0 = sgns_ref.xavier_tables(V, d, seed=d)
     walks = rng.integers(0, V, size=(n, L)).astype(np.int32)
+    if hub:
+        walks[:, ::3] = 7
     ins, tgt = sgns_ref.sg_windows(walks, R)
     noise = rng.integers(0, V, size=(len(ins), 2 * R, K))
     loss, gi, go, rec, prec = sgns_ref.sgns_forward_backward(w_in0, w_out0, ins, tgt, noise)
@@ -168,6 +175,18 @@ def test_fused_sgns_random_case_vs_oracle(d, hip_device):
     scale = float(np.abs(gi).max())
     np.testing.assert_allclose(g_in.cpu().numpy(), gi, rtol=1e-4, atol=1e-6 * scale)
     np.testing.assert_allclose(g_out.cpu().numpy(), go, rtol=1e-4, atol=1e-6 * scale)
+    # the atomic path agrees with the sorted one
+    g_in2, g_out2 = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    sgns_accumulate(w_in, w_out, g_in2, g_out2, K, walks=_dev(walks), context_radius=R,
+                    noise=_dev(noise), scatter='atomic')
+    torch.testing.assert_close(g_out2, g_out, rtol=1e-4, atol=1e-6 * scale)
+    torch.testing.assert_close(g_in2, g_in, rtol=1e-4, atol=1e-6 * scale)
+    # the sorted path is reproducible run to run (stable sort, fixed per-row summation order)
+    if not hub:
+        g_in3, g_out3 = torch.zeros_like(w_in), torch.zeros_like(w_out)
+        sgns_accumulate(w_in, w_out, g_in3, g_out3, K, walks=_dev(walks), context_radius=R,
+                        noise=_dev(noise))
+        assert torch.equal(g_out3, g_out)
 
 
 def test_device_noise_matches_philox_oracle(hip_device):

@@ -202,9 +202,18 @@ def test_abi_rejects_bad_arguments_without_a_device():
     assert rc == _native.DW_E_INVALID_ARG
     assert b'Minimum walk length' in lib.dw_last_error_string()
     rc = lib.dw_sgns_walks(None, 1, 4, 2, 1, 10, 8, None, None, None, None, None, 0, 0, 1.0,
-                           None, None, None)
+                           None, None, None, 0, None)
     assert rc == _native.DW_E_INVALID_ARG
     assert b'2R+1' in lib.dw_last_error_string()
+    import ctypes
+    nbytes = ctypes.c_size_t(0)
+    rc = lib.dw_sgns_workspace_bytes(573440, 10, 5, 1048577, ctypes.byref(nbytes))
+    if torch.cuda.is_available():
+        assert rc == 0
+        # records (12 B) double-buffered for the sort + hipcub temp storage
+        assert nbytes.value >= 573440 * 60 * 24
+    else:  # hipcub's temp-size query needs a device; the error is reported, not raised
+        assert rc in (0, _native.DW_E_HIP)
 
 
 def test_product_paths_refuse_host_tensors():
