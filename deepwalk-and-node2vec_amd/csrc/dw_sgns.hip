@@ -20,6 +20,8 @@
 //     pass 2 (k_rec_gather) gathers the centre rows and sums every output row's records in
 //     registers. No float atomics except where a row straddles two fixed-size chunks; the
 //     gathered bytes move at read speed, not atomic speed.
+#include <stdlib.h>
+
 #include <hipcub/hipcub.hpp>
 
 #include "dw_common.h"
@@ -28,7 +30,7 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int WAVES_PER_BLOCK = 4;
-constexpr int CHUNK = 6;
+constexpr int CHUNK = 12;            // output rows in flight per wave
 constexpr int TMAX = 256;            // max output rows per centre in records mode
 constexpr int GCH = 512;             // records per pass-2 wave chunk
 constexpr int GU = 8;                // records in flight per pass-2 iteration
@@ -95,11 +97,29 @@ __device__ __forceinline__ uint64_t pack_record(float coef, int64_t centre) {
            static_cast<uint32_t>(centre);
 }
 
+// Output row t of centre b (t < T = C(1+K)): t = j(1+K) is context j, t = j(1+K)+1+k is the
+// k-th negative of context j (the reference's (B', 2R) / (B', 2R, K) orders).
+template <bool FROM_WALKS>
+__device__ __forceinline__ int64_t row_id(const SgnsArgs &a, int64_t b, const int32_t *walk,
+                                          int64_t i, int t) {
+    const int rows_per_ctx = 1 + a.K;
+    const int j = t / rows_per_ctx, k = t - j * rows_per_ctx - 1;
+    if (k < 0) {
+        if (FROM_WALKS) return walk[(j < a.R) ? (i - a.R + j) : (i + 1 + (j - a.R))];
+        return a.targets[b * a.C + j];
+    }
+    return noise_id(a, b, j, k);
+}
+
 // VPL = values per lane (d <= 64*VPL); MASKED when d is not exactly 64*VPL.
-template <int VPL, bool MASKED, bool FROM_WALKS, bool RECORDS>
+// Work split inside a wave: every lane loads / draws the id of ONE output row (lane t <-> row
+// g0 + t of the current group of 64 rows), so the Philox negatives cost one draw per lane, not
+// one per row per lane; the row loop reads the ids back with v_readlane. After each chunk's
+// butterfly every lane holds every logit; lane t evaluates sigmoid / log / the clamp mask for
+// its own row only and the coefficients are read back per row. Records are written by the
+// owning lane (coalesced), so no LDS staging is needed.
+template <int VPL, bool MASKED, bool FROM_WALKS, bool RECORDS, int CH>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
-    __shared__ uint32_t s_key[RECORDS ? WAVES_PER_BLOCK : 1][RECORDS ? TMAX : 1];
-    __shared__ uint64_t s_val[RECORDS ? WAVES_PER_BLOCK : 1][RECORDS ? TMAX : 1];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
@@ -110,10 +130,21 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
 #pragma unroll
     for (int m = 0; m < VPL; ++m) live[m] = !MASKED || (lane + WAVE * m < a.d);
 
+    // per-lane loss / metric partials (reduced across the wave once, at the end)
     float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
 
     for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; b < a.batch; b += n_waves) {
-        const int64_t cid = centre_id<FROM_WALKS>(a, b);
+        const int32_t *walk = nullptr;
+        int64_t i = 0, cid;
+        if (FROM_WALKS) {
+            const int64_t per = a.L - 2 * a.R;
+            const int64_t w = b / per;
+            i = a.R + (b - w * per);
+            walk = a.walks + w * a.L;
+            cid = walk[i];
+        } else {
+            cid = a.inputs[b];
+        }
         const bool centre_ok = cid >= 0 && cid < a.V;
         if (!centre_ok) {
             if (lane == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
@@ -132,87 +163,89 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
             c[m] = live[m] ? crow[WAVE * m] : 0.f;
             gc[m] = 0.f;
         }
-        for (int r0 = 0; r0 < n_rows; r0 += CHUNK) {
-            int64_t id[CHUNK];
-            bool pos[CHUNK], ok[CHUNK];
-            float o[CHUNK][VPL], dot[CHUNK];
+        for (int g0 = 0; g0 < n_rows; g0 += WAVE) {
+            const int g_rows = (n_rows - g0 < WAVE) ? n_rows - g0 : WAVE;
+            // this lane's output row: id, kind, validity
+            const int t = g0 + lane;
+            int32_t my_id = 0;
+            bool my_ok = false;
+            const bool my_pos = (t % rows_per_ctx) == 0;
+            if (lane < g_rows) {
+                const int64_t id = row_id<FROM_WALKS>(a, b, walk, i, t);
+                my_ok = id >= 0 && id < a.V;
+                if (!my_ok) dw::status_or(a.status, DW_S_BAD_INDEX);
+                my_id = my_ok ? static_cast<int32_t>(id) : 0;
+            }
+            float my_coef = 0.f;
+            for (int r0 = 0; r0 < g_rows; r0 += CH) {
+                int32_t id[CH];
+                float o[CH][VPL], dot[CH];
 #pragma unroll
-            for (int u = 0; u < CHUNK; ++u) {
-                const int r = r0 + u;
-                ok[u] = r < n_rows;
-                pos[u] = false;
-                id[u] = 0;
-                if (ok[u]) {
-                    const int j = r / rows_per_ctx, k = r - j * rows_per_ctx - 1;
-                    pos[u] = k < 0;
-                    id[u] = pos[u] ? context_id<FROM_WALKS>(a, b, j) : noise_id(a, b, j, k);
-                    if (id[u] < 0 || id[u] >= a.V) {
-                        if (lane == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
-                        ok[u] = false;
-                        if (RECORDS && lane == 0) {
-                            s_key[wv][r] = 0u;
-                            s_val[wv][r] = 0ull;
-                        }
+                for (int u = 0; u < CH; ++u) {
+                    const int src = (r0 + u < g_rows) ? r0 + u : 0;
+                    id[u] = __builtin_amdgcn_readlane(my_id, src);
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const bool in = r0 + u < g_rows;
+                    const float *row = a.w_out + static_cast<int64_t>(id[u]) * a.d + lane;
+#pragma unroll
+                    for (int m = 0; m < VPL; ++m) o[u][m] = (in && live[m]) ? row[WAVE * m] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int m = 0; m < VPL; ++m) s += c[m] * o[u][m];
+                    dot[u] = s;
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+                    for (int u = 0; u < CH; ++u) dot[u] += __shfl_xor(dot[u], off, WAVE);
+                }
+                // lane r0+u owns row r0+u of this chunk: its logit, loss terms and coefficient
+                float x = 0.f;
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (lane == r0 + u) x = dot[u];
+                const bool mine = lane >= r0 && lane < r0 + CH && lane < g_rows && my_ok;
+                float coef = 0.f;
+                if (mine) {
+                    if (my_pos) {
+                        // -log(clamp(sigmoid(s), 1e-6)); d/ds = sigmoid(s) - 1 where unclamped
+                        const float sg = sigmoidf(x);
+                        acc_pos += -logf(fmaxf(sg, 1e-6f));
+                        acc_rec += (sg >= 0.5f) ? 1.f : 0.f;
+                        coef = (sg >= 1e-6f) ? (sg - 1.0f) * a.scale : 0.f;
+                    } else {
+                        // -log(clamp(sigmoid(-t), 1e-6)); d/dt = 1 - sigmoid(-t) where unclamped
+                        const float sn = sigmoidf(-x);
+                        acc_neg += -logf(fmaxf(sn, 1e-6f));
+                        acc_prec += (sigmoidf(x) >= 0.5f) ? 1.f : 0.f;
+                        coef = (sn >= 1e-6f) ? (1.0f - sn) * a.scale : 0.f;
+                    }
+                    my_coef = coef;
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    if (r0 + u >= g_rows) continue;
+                    const float gs =
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(coef), r0 + u));
+#pragma unroll
+                    for (int m = 0; m < VPL; ++m) gc[m] += gs * o[u][m];
+                    if (!RECORDS && gs != 0.f) {
+                        float *grow = a.g_out + static_cast<int64_t>(id[u]) * a.d + lane;
+#pragma unroll
+                        for (int m = 0; m < VPL; ++m)
+                            if (live[m]) atomicAdd(grow + WAVE * m, gs * c[m]);
                     }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < CHUNK; ++u) {
-                const float *row = a.w_out + (ok[u] ? id[u] : 0) * a.d + lane;
-#pragma unroll
-                for (int m = 0; m < VPL; ++m) o[u][m] = (ok[u] && live[m]) ? row[WAVE * m] : 0.f;
+            if (RECORDS && lane < g_rows) {  // lane t writes row t's record (coalesced)
+                a.rec_key[b * n_rows + t] = static_cast<uint32_t>(my_id);
+                a.rec_val[b * n_rows + t] = pack_record(my_ok ? my_coef : 0.f, cid);
             }
-#pragma unroll
-            for (int u = 0; u < CHUNK; ++u) {
-                float s = 0.f;
-#pragma unroll
-                for (int m = 0; m < VPL; ++m) s += c[m] * o[u][m];
-                dot[u] = s;
-            }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-                for (int u = 0; u < CHUNK; ++u) dot[u] += __shfl_xor(dot[u], off, WAVE);
-            }
-#pragma unroll
-            for (int u = 0; u < CHUNK; ++u) {
-                if (!ok[u]) continue;
-                float gscal;
-                if (pos[u]) {
-                    // -log(clamp(sigmoid(s), 1e-6)); d/ds = sigmoid(s) - 1 where unclamped
-                    const float sg = sigmoidf(dot[u]);
-                    acc_pos += -logf(fmaxf(sg, 1e-6f));
-                    acc_rec += (sg >= 0.5f) ? 1.f : 0.f;
-                    gscal = (sg >= 1e-6f) ? (sg - 1.0f) * a.scale : 0.f;
-                } else {
-                    // -log(clamp(sigmoid(-t), 1e-6)); d/dt = 1 - sigmoid(-t) where unclamped
-                    const float sn = sigmoidf(-dot[u]);
-                    acc_neg += -logf(fmaxf(sn, 1e-6f));
-                    acc_prec += (sigmoidf(dot[u]) >= 0.5f) ? 1.f : 0.f;
-                    gscal = (sn >= 1e-6f) ? (1.0f - sn) * a.scale : 0.f;
-                }
-#pragma unroll
-                for (int m = 0; m < VPL; ++m) gc[m] += gscal * o[u][m];
-                if (RECORDS) {
-                    if (lane == 0) {
-                        s_key[wv][r0 + u] = static_cast<uint32_t>(id[u]);
-                        s_val[wv][r0 + u] = pack_record(gscal, cid);
-                    }
-                } else if (gscal != 0.f) {
-                    float *grow = a.g_out + id[u] * a.d + lane;
-#pragma unroll
-                    for (int m = 0; m < VPL; ++m)
-                        if (live[m]) atomicAdd(grow + WAVE * m, gscal * c[m]);
-                }
-            }
-        }
-        if (RECORDS) {  // one coalesced record store per centre
-            dw::wave_lds_sync();
-            for (int t = lane; t < n_rows; t += WAVE) {
-                a.rec_key[b * n_rows + t] = s_key[wv][t];
-                a.rec_val[b * n_rows + t] = s_val[wv][t];
-            }
-            dw::wave_lds_sync();
         }
         float *gcrow = a.g_in + cid * a.d + lane;
 #pragma unroll
@@ -220,12 +253,219 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
             if (live[m]) atomicAdd(gcrow + WAVE * m, gc[m]);
     }
 
-    // loss partials: the four scalars are wave-uniform; one double atomic per wave and value
-    if (a.loss_acc && lane == 0) {
-        if (acc_pos != 0.f) atomicAdd(a.loss_acc + 0, (double)acc_pos);
-        if (acc_neg != 0.f) atomicAdd(a.loss_acc + 1, (double)acc_neg);
-        if (acc_rec != 0.f) atomicAdd(a.loss_acc + 2, (double)acc_rec);
-        if (acc_prec != 0.f) atomicAdd(a.loss_acc + 3, (double)acc_prec);
+    // loss partials: wave-reduce the per-lane sums, one double atomic per wave and value
+    if (a.loss_acc) {
+        acc_pos = dw::wave_sum(acc_pos);
+        acc_neg = dw::wave_sum(acc_neg);
+        acc_rec = dw::wave_sum(acc_rec);
+        acc_prec = dw::wave_sum(acc_prec);
+        if (lane == 0) {
+            if (acc_pos != 0.f) atomicAdd(a.loss_acc + 0, (double)acc_pos);
+            if (acc_neg != 0.f) atomicAdd(a.loss_acc + 1, (double)acc_neg);
+            if (acc_rec != 0.f) atomicAdd(a.loss_acc + 2, (double)acc_rec);
+            if (acc_prec != 0.f) atomicAdd(a.loss_acc + 3, (double)acc_prec);
+        }
+    }
+}
+
+// ---- pass 1, 16-lane-group form (records mode, d = 64 * F4, T <= 64) -------------------------
+// One centre per 16-lane group, four centres per wave: lane gl of group q holds elements
+// [4gl + 64f, 4gl + 64f + 4) of every row (float4 loads: one wave-instruction moves 1 KiB =
+// four 256-B row pieces), so a logit is 4*F4 FMAs and a 16-lane DPP row-rotate reduction
+// (no LDS permutes). Each group's 2R(1+K) row ids are drawn once into LDS (lane gl draws rows
+// gl, gl+16, ...); per chunk of CHR rows the group loads CHR rows, lanes gl < CHR evaluate the
+// loss / clamp mask / coefficient of row gl (one transcendental pass per chunk, not per row)
+// and the coefficients come back by ds_bpermute. The centre gradient is staged in LDS and
+// added as full 256-B wave-instruction atomics; records are written by their owning lanes.
+constexpr int G16_TMAX = 64;
+#ifndef G16_MIN_WAVES
+#define G16_MIN_WAVES 4  // waves per SIMD the register allocation must allow (no spills)
+#endif
+
+template <int N>
+__device__ __forceinline__ float row_ror(float x) {  // lane i <- lane (i +- N) mod 16 of its row
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float row_sum16(float x) {
+    x += row_ror<8>(x);
+    x += row_ror<4>(x);
+    x += row_ror<2>(x);
+    x += row_ror<1>(x);
+    return x;
+}
+
+template <int F4, bool FROM_WALKS, int CHR>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, G16_MIN_WAVES) k_sgns_g16(SgnsArgs a) {
+    constexpr int D = 64 * F4;
+    __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
+    __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
+    __shared__ float4 s_g[WAVES_PER_BLOCK][4][16 * F4];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    const int q = lane >> 4, gl = lane & 15;
+    const int rows_per_ctx = 1 + a.K;
+    const int T = a.C * rows_per_ctx;
+    const int64_t n_slots = (int64_t)gridDim.x * WAVES_PER_BLOCK * 4;
+    float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
+
+    for (int64_t base = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * 4; base < a.batch;
+         base += n_slots) {
+        const int64_t b = base + q;
+        const bool active = b < a.batch;
+        const int32_t *walk = nullptr;
+        int64_t i = 0, cid = -1;
+        if (active) {
+            if (FROM_WALKS) {
+                const int64_t per = a.L - 2 * a.R;
+                const int64_t w = b / per;
+                i = a.R + (b - w * per);
+                walk = a.walks + w * a.L;
+                cid = walk[i];
+            } else {
+                cid = a.inputs[b];
+            }
+        }
+        const bool ok_c = active && cid >= 0 && cid < a.V;
+        if (active && !ok_c && gl == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
+        // the group's row ids (-1 = invalid row: zero coefficient); not unrolled: one Philox
+        // draw at a time keeps the register peak low
+#pragma unroll 1
+        for (int k = 0; k < G16_TMAX / 16; ++k) {
+            const int t = gl + 16 * k;
+            if (t < T) {
+                int32_t id = -1;
+                if (ok_c) {
+                    const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, t);
+                    if (r >= 0 && r < a.V)
+                        id = static_cast<int32_t>(r);
+                    else
+                        dw::status_or(a.status, DW_S_BAD_INDEX);
+                }
+                s_id[wv][q][t] = id;
+                s_coef[wv][q][t] = 0.f;
+            }
+        }
+        float4 c4[F4], g4[F4];
+        const float *crow = a.w_in + (ok_c ? cid : 0) * D + 4 * gl;
+#pragma unroll
+        for (int f = 0; f < F4; ++f) {
+            c4[f] = ok_c ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            g4[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        dw::wave_lds_sync();
+        for (int t0 = 0; t0 < T; t0 += CHR) {
+            float4 o4[CHR][F4];
+            int32_t rid[CHR];
+#pragma unroll
+            for (int u = 0; u < CHR; ++u) {
+                const int t = t0 + u;
+                rid[u] = (t < T) ? s_id[wv][q][t] : -1;
+                const float *row = a.w_out + static_cast<int64_t>(rid[u] < 0 ? 0 : rid[u]) * D +
+                                   4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+                    o4[u][f] = rid[u] >= 0 ? *reinterpret_cast<const float4 *>(row + 64 * f)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            float dot[CHR];
+#pragma unroll
+            for (int u = 0; u < CHR; ++u) {
+                float p = 0.f;
+#pragma unroll
+                for (int f = 0; f < F4; ++f) {
+                    p = fmaf(c4[f].x, o4[u][f].x, p);
+                    p = fmaf(c4[f].y, o4[u][f].y, p);
+                    p = fmaf(c4[f].z, o4[u][f].z, p);
+                    p = fmaf(c4[f].w, o4[u][f].w, p);
+                }
+                dot[u] = row_sum16(p);
+            }
+            // lane gl < CHR owns row t0 + gl of its group
+            float x = 0.f;
+            int32_t xid = -1;
+#pragma unroll
+            for (int u = 0; u < CHR; ++u)
+                if (gl == u) {
+                    x = dot[u];
+                    xid = rid[u];
+                }
+            float coef = 0.f;
+            const int t = t0 + gl;
+            if (gl < CHR && t < T && xid >= 0) {
+                if ((t % rows_per_ctx) == 0) {
+                    // -log(clamp(sigmoid(s), 1e-6)); d/ds = sigmoid(s) - 1 where unclamped
+                    const float sg = sigmoidf(x);
+                    acc_pos += -logf(fmaxf(sg, 1e-6f));
+                    acc_rec += (sg >= 0.5f) ? 1.f : 0.f;
+                    coef = (sg >= 1e-6f) ? (sg - 1.0f) * a.scale : 0.f;
+                } else {
+                    // -log(clamp(sigmoid(-t), 1e-6)); d/dt = 1 - sigmoid(-t) where unclamped
+                    const float sn = sigmoidf(-x);
+                    acc_neg += -logf(fmaxf(sn, 1e-6f));
+                    acc_prec += (sigmoidf(x) >= 0.5f) ? 1.f : 0.f;
+                    coef = (sn >= 1e-6f) ? (1.0f - sn) * a.scale : 0.f;
+                }
+                s_coef[wv][q][t] = coef;
+            }
+#pragma unroll
+            for (int u = 0; u < CHR; ++u) {
+                const float cu = __shfl(coef, (q << 4) | u, WAVE);
+#pragma unroll
+                for (int f = 0; f < F4; ++f) {
+                    g4[f].x = fmaf(cu, o4[u][f].x, g4[f].x);
+                    g4[f].y = fmaf(cu, o4[u][f].y, g4[f].y);
+                    g4[f].z = fmaf(cu, o4[u][f].z, g4[f].z);
+                    g4[f].w = fmaf(cu, o4[u][f].w, g4[f].w);
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
+        dw::wave_lds_sync();
+        if (active) {  // records: lane gl writes rows gl, gl+16, ... of its centre
+#pragma unroll
+            for (int k = 0; k < G16_TMAX / 16; ++k) {
+                const int tt = gl + 16 * k;
+                if (tt < T) {
+                    const int32_t id = s_id[wv][q][tt];
+                    a.rec_key[b * T + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                    a.rec_val[b * T + tt] = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
+                }
+            }
+        }
+        // centre gradients: per centre, 64 lanes x dword = 256 contiguous bytes per atomic
+        const float *sg_flat = reinterpret_cast<const float *>(&s_g[wv][0][0]);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int32_t cq = __builtin_amdgcn_readlane(ok_c ? static_cast<int32_t>(cid) : -1,
+                                                         qq * 16);
+            if (cq >= 0) {
+                float *dst = a.g_in + static_cast<int64_t>(cq) * D;
+                // s_g[qq] holds float4 slot j = gl + 16f -> elements 4gl + 64f .. +3
+#pragma unroll
+                for (int e0 = 0; e0 < D; e0 += WAVE) {
+                    const int e = e0 + lane;
+                    const int f = e >> 6, g = (e & 63) >> 2, comp = e & 3;
+                    atomicAdd(dst + e, sg_flat[qq * 16 * F4 * 4 + (g + 16 * f) * 4 + comp]);
+                }
+            }
+        }
+        dw::wave_lds_sync();
+    }
+    if (a.loss_acc) {
+        acc_pos = dw::wave_sum(acc_pos);
+        acc_neg = dw::wave_sum(acc_neg);
+        acc_rec = dw::wave_sum(acc_rec);
+        acc_prec = dw::wave_sum(acc_prec);
+        if (lane == 0) {
+            if (acc_pos != 0.f) atomicAdd(a.loss_acc + 0, (double)acc_pos);
+            if (acc_neg != 0.f) atomicAdd(a.loss_acc + 1, (double)acc_neg);
+            if (acc_rec != 0.f) atomicAdd(a.loss_acc + 2, (double)acc_rec);
+            if (acc_prec != 0.f) atomicAdd(a.loss_acc + 3, (double)acc_prec);
+        }
     }
 }
 
@@ -338,17 +578,33 @@ int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStrea
     return DW_OK;
 }
 
+int chunk_rows() {  // rows in flight per wave; DW_SGNS_CHUNK=6|8|12 (tuning knob)
+    static int v = [] {
+        const char *e = getenv("DW_SGNS_CHUNK");
+        const int x = e ? atoi(e) : CHUNK;
+        return (x == 6 || x == 8 || x == 12) ? x : CHUNK;
+    }();
+    return v;
+}
+
 template <bool FROM_WALKS, bool RECORDS>
 int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    const int ch = chunk_rows();
+#define DW_SGNS_LAUNCH(VPL, M, CHV) \
+    hipLaunchKernelGGL((k_sgns<VPL, M, FROM_WALKS, RECORDS, CHV>), g, bl, 0, st, a)
 #define DW_SGNS_CASE(VPL)                                                                    \
     if (a.d <= 64 * VPL) {                                                                    \
-        if (a.d == 64 * VPL)                                                                  \
-            hipLaunchKernelGGL((k_sgns<VPL, false, FROM_WALKS, RECORDS>), g, bl, 0, st, a);  \
-        else                                                                                  \
-            hipLaunchKernelGGL((k_sgns<VPL, true, FROM_WALKS, RECORDS>), g, bl, 0, st, a);   \
+        const bool exact = a.d == 64 * VPL;                                                   \
+        if (ch == 6) {                                                                        \
+            if (exact) DW_SGNS_LAUNCH(VPL, false, 6); else DW_SGNS_LAUNCH(VPL, true, 6);      \
+        } else if (ch == 8) {                                                                 \
+            if (exact) DW_SGNS_LAUNCH(VPL, false, 8); else DW_SGNS_LAUNCH(VPL, true, 8);      \
+        } else {                                                                              \
+            if (exact) DW_SGNS_LAUNCH(VPL, false, 12); else DW_SGNS_LAUNCH(VPL, true, 12);    \
+        }                                                                                     \
         DW_LAUNCH_CHECK("dw_sgns");                                                           \
         return DW_OK;                                                                         \
     }
@@ -357,8 +613,33 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     DW_SGNS_CASE(4)
     DW_SGNS_CASE(8)
 #undef DW_SGNS_CASE
+#undef DW_SGNS_LAUNCH
     dw::set_error("dw_sgns: dim %d > 512 is not supported", a.d);
     return DW_E_UNSUPPORTED;
+}
+
+// 16-lane-group pass 1 when d is a multiple of 64 (<= 512) and 2R(1+K) <= 64; otherwise
+// DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns). DW_SGNS_G16=0 disables it.
+template <bool FROM_WALKS>
+int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
+    static const bool enabled = [] {
+        const char *e = getenv("DW_SGNS_G16");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t T = (int64_t)a.C * (1 + a.K);
+    if (!enabled || a.d % 64 != 0 || a.d > 512 || T > G16_TMAX) return DW_E_UNSUPPORTED;
+    int64_t blocks = (a.batch + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
+    if (blocks > 65536) blocks = 65536;
+    const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    switch (a.d / 64) {
+        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8>), g, bl, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4>), g, bl, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2>), g, bl, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1>), g, bl, 0, st, a); break;
+        default: return DW_E_UNSUPPORTED;
+    }
+    DW_LAUNCH_CHECK("dw_sgns/g16");
+    return DW_OK;
 }
 
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
@@ -404,7 +685,8 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t
                workspace_bytes, ws.total);
     a.rec_key = ws.k0;
     a.rec_val = ws.v0;
-    rc = launch_pass1<FROM_WALKS, true>(a, st);
+    rc = launch_pass1_g16<FROM_WALKS>(a, st);
+    if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
     if (rc != DW_OK) return rc;
     hipcub::DoubleBuffer<uint32_t> kb(ws.k0, ws.k1);
     hipcub::DoubleBuffer<uint64_t> vb(ws.v0, ws.v1);
