@@ -58,7 +58,8 @@ def assert_within_envelope(got, exp, exact, lr, rtol=1e-5, atol=1e-6):
     trajectory does (fraction of entries outside (rtol, atol) and max |diff|)."""
     bad_exact = (~np.isclose(exact, exp, rtol=rtol, atol=atol)).mean()
     max_exact = float(np.abs(exact - exp).max())
-    assert_params_close(got, exp, lr, rtol, atol, max_frac=4 * bad_exact + 1e-3,
+    assert_params_close(got, exp, lr, rtol, atol,
+                        max_frac=4 * bad_exact + max(1e-3, 2.0 / got.size),
                         max_abs=4 * max_exact + lr / 100)
 
 
