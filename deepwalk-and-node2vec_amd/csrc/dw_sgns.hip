@@ -278,6 +278,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
 // and the coefficients come back by ds_bpermute. The centre gradient is staged in LDS and
 // added as full 256-B wave-instruction atomics; records are written by their owning lanes.
 constexpr int G16_TMAX = 64;
+#ifndef G16_DEFAULT_VARIANT
+#define G16_DEFAULT_VARIANT 0
+#endif
 #ifndef G16_MIN_WAVES
 #define G16_MIN_WAVES 4  // waves per SIMD the register allocation must allow (no spills)
 #endif
@@ -296,8 +299,9 @@ __device__ __forceinline__ float row_sum16(float x) {
     return x;
 }
 
-template <int F4, bool FROM_WALKS, int CHR>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, G16_MIN_WAVES) k_sgns_g16(SgnsArgs a) {
+template <int F4, bool FROM_WALKS, int CHR, bool PF>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : G16_MIN_WAVES)
+    k_sgns_g16(SgnsArgs a) {
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
@@ -356,9 +360,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, G16_MIN_WAVES) k_sgns_g
             g4[f] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         dw::wave_lds_sync();
-        for (int t0 = 0; t0 < T; t0 += CHR) {
-            float4 o4[CHR][F4];
-            int32_t rid[CHR];
+        auto load_chunk = [&](float4(&o4)[CHR][F4], int32_t(&rid)[CHR], int t0) {
 #pragma unroll
             for (int u = 0; u < CHR; ++u) {
                 const int t = t0 + u;
@@ -370,6 +372,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, G16_MIN_WAVES) k_sgns_g
                     o4[u][f] = rid[u] >= 0 ? *reinterpret_cast<const float4 *>(row + 64 * f)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
             }
+        };
+        auto compute_chunk = [&](const float4(&o4)[CHR][F4], const int32_t(&rid)[CHR],
+                                 int t0) {
             float dot[CHR];
 #pragma unroll
             for (int u = 0; u < CHR; ++u) {
@@ -420,6 +425,25 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, G16_MIN_WAVES) k_sgns_g
                     g4[f].z = fmaf(cu, o4[u][f].z, g4[f].z);
                     g4[f].w = fmaf(cu, o4[u][f].w, g4[f].w);
                 }
+            }
+        };
+        if (PF) {  // software pipeline: the next chunk is in flight while this one computes
+            float4 oA[CHR][F4], oB[CHR][F4];
+            int32_t ridA[CHR], ridB[CHR];
+            load_chunk(oA, ridA, 0);
+            for (int t0 = 0; t0 < T; t0 += 2 * CHR) {
+                if (t0 + CHR < T) load_chunk(oB, ridB, t0 + CHR);
+                compute_chunk(oA, ridA, t0);
+                if (t0 + CHR >= T) break;
+                if (t0 + 2 * CHR < T) load_chunk(oA, ridA, t0 + 2 * CHR);
+                compute_chunk(oB, ridB, t0 + CHR);
+            }
+        } else {
+            for (int t0 = 0; t0 < T; t0 += CHR) {
+                float4 o4[CHR][F4];
+                int32_t rid[CHR];
+                load_chunk(o4, rid, t0);
+                compute_chunk(o4, rid, t0);
             }
         }
 #pragma unroll
@@ -631,11 +655,24 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     int64_t blocks = (a.batch + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    static const int variant = [] {  // DW_G16_VARIANT (tuning, d=128): 0 4n, 1 4p, 2 8n, 3 2p
+        const char *e = getenv("DW_G16_VARIANT");
+        return e ? atoi(e) : G16_DEFAULT_VARIANT;
+    }();
     switch (a.d / 64) {
-        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8>), g, bl, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4>), g, bl, 0, st, a); break;
-        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2>), g, bl, 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1>), g, bl, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, false>), g, bl, 0, st, a); break;
+        case 2:
+            if (variant == 1)
+                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true>), g, bl, 0, st, a);
+            else if (variant == 2)
+                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 8, false>), g, bl, 0, st, a);
+            else if (variant == 3)
+                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 2, true>), g, bl, 0, st, a);
+            else
+                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, false>), g, bl, 0, st, a);
+            break;
+        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, false>), g, bl, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, false>), g, bl, 0, st, a); break;
         default: return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns/g16");
