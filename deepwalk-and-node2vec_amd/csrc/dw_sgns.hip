@@ -38,6 +38,59 @@ constexpr uint32_t TAG_SGNS = 0x53470000u;  // 'SG'
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Loss terms and gradient coefficient of one output row (loss.py:14-22 + its autograd):
+//   positive row: -log(clamp(sigmoid(x), 1e-6)),  d/dx = sigmoid(x) - 1  where unclamped;
+//   negative row: -log(clamp(sigmoid(-x), 1e-6)), d/dx = 1 - sigmoid(-x) where unclamped;
+// recall counts positives with sigmoid(x) >= 0.5, the precision tally negatives with it.
+// One exp(-|x|) and one reciprocal give sigmoid(|x|) and sigmoid(-|x|) together (finite for
+// every x); the hardware exp / rcp / log (a few ulp) keep the per-row dependency chain short —
+// this chain, not memory, bounded pass 1 with the libm versions. The (s - 1) / (1 - s) forms
+// keep the reference's rounding structure.
+__device__ __forceinline__ float row_coef(float x, bool pos, float scale, float &acc_pos,
+                                          float &acc_neg, float &acc_rec, float &acc_prec) {
+    const float e = __expf(-fabsf(x));
+    const float hi = __builtin_amdgcn_rcpf(1.0f + e);  // sigmoid(|x|)
+    const float lo = e * hi;                            // sigmoid(-|x|)
+    const float sp = x >= 0.f ? hi : lo;                // sigmoid(x)
+    const float sy = pos ? sp : (x >= 0.f ? lo : hi);   // sigmoid(x) / sigmoid(-x)
+    const float loss = -__logf(fmaxf(sy, 1e-6f));
+    const float hit = sp >= 0.5f ? 1.f : 0.f;
+    if (pos) {
+        acc_pos += loss;
+        acc_rec += hit;
+    } else {
+        acc_neg += loss;
+        acc_prec += hit;
+    }
+    return sy >= 1e-6f ? (pos ? sy - 1.0f : 1.0f - sy) * scale : 0.f;
+}
+
+// Loss sums leave each block as ONE fp64 atomic per term. The four terms share one cache line,
+// so same-address atomics serialise on a single L2 channel (~9 ns each measured on MI355X):
+// one per wave over ~10^5 waves cost ~5 ms per batch, more than the whole row traffic. The
+// launchers also cap the grid (grid-stride loops), so a batch issues a few thousand.
+// Every thread of the block must reach this (no early exits in the kernels).
+__device__ void flush_loss(double *acc, float p, float n, float r, float pr) {
+    __shared__ float s_loss[WAVES_PER_BLOCK][4];
+    p = dw::wave_sum(p);
+    n = dw::wave_sum(n);
+    r = dw::wave_sum(r);
+    pr = dw::wave_sum(pr);
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    if (lane == 0) {
+        s_loss[wv][0] = p;
+        s_loss[wv][1] = n;
+        s_loss[wv][2] = r;
+        s_loss[wv][3] = pr;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double t = 0.0;
+        for (int w = 0; w < WAVES_PER_BLOCK; ++w) t += s_loss[w][threadIdx.x];
+        if (t != 0.0) atomicAdd(acc + threadIdx.x, t);
+    }
+}
+
 struct SgnsArgs {
     // source of centres / contexts
     const int32_t *walks;     // walks mode
@@ -60,27 +113,6 @@ struct SgnsArgs {
     uint32_t *rec_key;        // records mode: [batch * T]
     uint64_t *rec_val;        //   {coef bits << 32 | centre id}
 };
-
-template <bool FROM_WALKS>
-__device__ __forceinline__ int64_t centre_id(const SgnsArgs &a, int64_t b) {
-    if (FROM_WALKS) {
-        const int64_t per = a.L - 2 * a.R;
-        const int64_t w = b / per, i = a.R + (b - w * per);
-        return a.walks[w * a.L + i];
-    }
-    return a.inputs[b];
-}
-
-template <bool FROM_WALKS>
-__device__ __forceinline__ int64_t context_id(const SgnsArgs &a, int64_t b, int j) {
-    if (FROM_WALKS) {
-        const int64_t per = a.L - 2 * a.R;
-        const int64_t w = b / per, i = a.R + (b - w * per);
-        const int64_t pos = (j < a.R) ? (i - a.R + j) : (i + 1 + (j - a.R));
-        return a.walks[w * a.L + pos];
-    }
-    return a.targets[b * a.C + j];
-}
 
 __device__ __forceinline__ int64_t noise_id(const SgnsArgs &a, int64_t b, int j, int k) {
     if (a.noise) return a.noise[(b * a.C + j) * a.K + k];
@@ -212,19 +244,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                 const bool mine = lane >= r0 && lane < r0 + CH && lane < g_rows && my_ok;
                 float coef = 0.f;
                 if (mine) {
-                    if (my_pos) {
-                        // -log(clamp(sigmoid(s), 1e-6)); d/ds = sigmoid(s) - 1 where unclamped
-                        const float sg = sigmoidf(x);
-                        acc_pos += -logf(fmaxf(sg, 1e-6f));
-                        acc_rec += (sg >= 0.5f) ? 1.f : 0.f;
-                        coef = (sg >= 1e-6f) ? (sg - 1.0f) * a.scale : 0.f;
-                    } else {
-                        // -log(clamp(sigmoid(-t), 1e-6)); d/dt = 1 - sigmoid(-t) where unclamped
-                        const float sn = sigmoidf(-x);
-                        acc_neg += -logf(fmaxf(sn, 1e-6f));
-                        acc_prec += (sigmoidf(x) >= 0.5f) ? 1.f : 0.f;
-                        coef = (sn >= 1e-6f) ? (1.0f - sn) * a.scale : 0.f;
-                    }
+                    coef = row_coef(x, my_pos, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
                     my_coef = coef;
                 }
 #pragma unroll
@@ -254,18 +274,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
     }
 
     // loss partials: wave-reduce the per-lane sums, one double atomic per wave and value
-    if (a.loss_acc) {
-        acc_pos = dw::wave_sum(acc_pos);
-        acc_neg = dw::wave_sum(acc_neg);
-        acc_rec = dw::wave_sum(acc_rec);
-        acc_prec = dw::wave_sum(acc_prec);
-        if (lane == 0) {
-            if (acc_pos != 0.f) atomicAdd(a.loss_acc + 0, (double)acc_pos);
-            if (acc_neg != 0.f) atomicAdd(a.loss_acc + 1, (double)acc_neg);
-            if (acc_rec != 0.f) atomicAdd(a.loss_acc + 2, (double)acc_rec);
-            if (acc_prec != 0.f) atomicAdd(a.loss_acc + 3, (double)acc_prec);
-        }
-    }
+    if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
 
 // ---- pass 1, 16-lane-group form (records mode, d = 64 * F4, T <= 64) -------------------------
@@ -333,9 +342,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : 
         }
         const bool ok_c = active && cid >= 0 && cid < a.V;
         if (active && !ok_c && gl == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
-        // the group's row ids (-1 = invalid row: zero coefficient); not unrolled: one Philox
-        // draw at a time keeps the register peak low
-#pragma unroll 1
+        // the group's row ids (-1 = invalid row: zero coefficient); two Philox draws overlap
+#pragma unroll 2
         for (int k = 0; k < G16_TMAX / 16; ++k) {
             const int t = gl + 16 * k;
             if (t < T) {
@@ -400,19 +408,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : 
             float coef = 0.f;
             const int t = t0 + gl;
             if (gl < CHR && t < T && xid >= 0) {
-                if ((t % rows_per_ctx) == 0) {
-                    // -log(clamp(sigmoid(s), 1e-6)); d/ds = sigmoid(s) - 1 where unclamped
-                    const float sg = sigmoidf(x);
-                    acc_pos += -logf(fmaxf(sg, 1e-6f));
-                    acc_rec += (sg >= 0.5f) ? 1.f : 0.f;
-                    coef = (sg >= 1e-6f) ? (sg - 1.0f) * a.scale : 0.f;
-                } else {
-                    // -log(clamp(sigmoid(-t), 1e-6)); d/dt = 1 - sigmoid(-t) where unclamped
-                    const float sn = sigmoidf(-x);
-                    acc_neg += -logf(fmaxf(sn, 1e-6f));
-                    acc_prec += (sigmoidf(x) >= 0.5f) ? 1.f : 0.f;
-                    coef = (sn >= 1e-6f) ? (1.0f - sn) * a.scale : 0.f;
-                }
+                coef = row_coef(x, (t % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg, acc_rec,
+                                acc_prec);
                 s_coef[wv][q][t] = coef;
             }
 #pragma unroll
@@ -479,18 +476,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : 
         }
         dw::wave_lds_sync();
     }
-    if (a.loss_acc) {
-        acc_pos = dw::wave_sum(acc_pos);
-        acc_neg = dw::wave_sum(acc_neg);
-        acc_rec = dw::wave_sum(acc_rec);
-        acc_prec = dw::wave_sum(acc_prec);
-        if (lane == 0) {
-            if (acc_pos != 0.f) atomicAdd(a.loss_acc + 0, (double)acc_pos);
-            if (acc_neg != 0.f) atomicAdd(a.loss_acc + 1, (double)acc_neg);
-            if (acc_rec != 0.f) atomicAdd(a.loss_acc + 2, (double)acc_rec);
-            if (acc_prec != 0.f) atomicAdd(a.loss_acc + 3, (double)acc_prec);
-        }
-    }
+    if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
 
 // Pass 2: records sorted by output row -> g_out[row] += sum coef * w_in[centre].
@@ -602,6 +588,22 @@ int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStrea
     return DW_OK;
 }
 
+// Grid cap for the grid-stride SGNS kernels: `per_cu` blocks per compute unit (a couple of
+// resident rounds), so per-block epilogues (loss atomics) stay in the thousands.
+int64_t grid_cap(int per_cu) {
+    static int n_cu[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 65536;
+    if (n_cu[dev] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v <= 0)
+            v = 256;
+        n_cu[dev] = v;
+    }
+    return (int64_t)n_cu[dev] * per_cu;
+}
+
 int chunk_rows() {  // rows in flight per wave; DW_SGNS_CHUNK=6|8|12 (tuning knob)
     static int v = [] {
         const char *e = getenv("DW_SGNS_CHUNK");
@@ -614,7 +616,8 @@ int chunk_rows() {  // rows in flight per wave; DW_SGNS_CHUNK=6|8|12 (tuning kno
 template <bool FROM_WALKS, bool RECORDS>
 int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    if (blocks > 65536) blocks = 65536;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     const int ch = chunk_rows();
 #define DW_SGNS_LAUNCH(VPL, M, CHV) \
@@ -653,7 +656,8 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     const int64_t T = (int64_t)a.C * (1 + a.K);
     if (!enabled || a.d % 64 != 0 || a.d > 512 || T > G16_TMAX) return DW_E_UNSUPPORTED;
     int64_t blocks = (a.batch + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
-    if (blocks > 65536) blocks = 65536;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     static const int variant = [] {  // DW_G16_VARIANT (tuning, d=128): 0 4n, 1 4p, 2 8n, 3 2p
         const char *e = getenv("DW_G16_VARIANT");
