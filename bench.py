@@ -40,6 +40,22 @@ def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     return 8 * d * (1 + K) + 8 * d / (2 * R) + 8 * (1 + K) + 8 / (2 * R)
 
 
+def sgns_phase_bytes(n_walks, L, R, K, d, V, scatter):
+    """Implementation byte model of each SGNS phase per call: rows of 4d B,
+    12-B records {row u32 | coef f32, centre u32}, one centre-gradient RMW row per centre."""
+    centres = n_walks * (L - 2 * R)
+    T = 2 * R * (1 + K)
+    n_rec = centres * T
+    if scatter != 'sorted':
+        return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 8 * d * T) + n_walks * L * 4,
+                'sort': 0, 'pass2': 0}
+    bits = max(1, math.ceil(math.log2(V)))
+    touched = V * (1.0 - math.exp(-n_rec / V))   # expected distinct output rows
+    return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 12 * T) + n_walks * L * 4,
+            'sort': n_rec * (4 + 24 * math.ceil(bits / 8)),
+            'pass2': n_rec * (12 + 4 * d) + touched * 8 * d}
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -120,7 +136,7 @@ def main():
     from shallow_encoders import _native
     from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
     from shallow_encoders.graph.rmat import rmat_graph
-    from shallow_encoders.word2vec.sgns import loss_terms, sgns_accumulate
+    from shallow_encoders.word2vec.sgns import loss_terms, phase_ms, phase_timing, sgns_accumulate
     from shallow_encoders.word2vec.sharding import ShardedTables
     _native.require_device(dev)
 
@@ -182,10 +198,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    phase_timing(True)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
     torch.cuda.synchronize(dev)
+    phases = phase_ms()
+    phase_timing(False)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
@@ -201,7 +220,12 @@ def main():
     total_pairs = pairs_per_step * args.steps * world
     value = total_pairs / elapsed
     bpp = sgns_bytes_per_pair(d, K, R)
-    sgns_gbs = pairs_per_step * bpp / (kern_ms['sgns'] * 1e-3) / 1e9
+    sgns_ms = phases['pass1'] + phases['sort'] + phases['pass2']
+    sgns_gbs = pairs_per_step * bpp / (sgns_ms * 1e-3) / 1e9
+    phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter)
+    phase_info = {k: {'ms': phases[k], 'bytes_model': phase_bytes[k],
+                      'GBps': phase_bytes[k] / (phases[k] * 1e-3) / 1e9 if phases[k] else None}
+                  for k in ('pass1', 'sort', 'pass2')}
 
     # ---- walker alone: walks/s (DeepWalk over one walk per node; node2vec sample) ------------
     walk_stats = {}
@@ -252,11 +276,13 @@ def main():
         'kernel_ms': kern_ms,
         'mean_loss': mean_loss,
         'roofline': {
-            'kernel': ('dw_sgns_walks: k_sgns + hipcub radix sort + k_rec_gather, timed together'
+            'kernel': ('dw_sgns_walks = k_sgns_g16 + hipcub radix sort + k_rec_gather'
                        if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
             'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,
+            'ms_per_launch': sgns_ms, 'launches_timed': phases['calls'],
+            'phases': phase_info,
         },
         'cpu_baseline': None,
     }
@@ -265,8 +291,13 @@ def main():
         try:
             with open(prof) as f:
                 pmc = json.load(f)
-            if pmc.get('pairs_per_launch') == pairs_per_step:
+            if (pmc.get('pairs_per_launch') == pairs_per_step and
+                    pmc.get('scatter', 'atomic') == args.scatter):
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
+                result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"
+                per_k = pmc.get('hbm_bytes_per_kernel') or {}
+                for k in ('pass1', 'sort', 'pass2'):
+                    result['roofline']['phases'][k]['traffic'] = per_k.get('sgns_' + k)
         except (OSError, ValueError):
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -22,6 +22,8 @@
 //     gathered bytes move at read speed, not atomic speed.
 #include <stdlib.h>
 
+#include <vector>
+
 #include <hipcub/hipcub.hpp>
 
 #include "dw_common.h"
@@ -709,9 +711,55 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     return DW_E_UNSUPPORTED;
 }
 
+// Per-phase HIP-event timing of dw_sgns_* calls (bench / profiling; off by default). Each
+// recorded call holds 4 events: start | pass 1 | sort | pass 2 (sort and pass 2 are empty
+// in atomic mode). Host-side state, not thread-safe: one profiling caller per process.
+struct PhaseTimer {
+    static constexpr size_t MAX_CALLS = 4096;
+    bool on = false;
+    size_t calls = 0;
+    std::vector<hipEvent_t> ev;
+    bool active() const { return on && calls < MAX_CALLS; }
+    void mark(int slot, hipStream_t st) {
+        if (!active()) return;
+        const size_t i = 4 * calls + slot;
+        while (ev.size() <= i) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) {
+                on = false;
+                return;
+            }
+            ev.push_back(e);
+        }
+        hipEventRecord(ev[i], st);
+        if (slot == 3) ++calls;
+    }
+};
+PhaseTimer g_timer;
+
+template <bool FROM_WALKS>
+int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st);
+
 template <bool FROM_WALKS>
 int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st) {
-    if (a.batch == 0) return DW_OK;
+    g_timer.mark(0, st);
+    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, st);
+    if (rc == DW_OK && workspace == nullptr) {
+        g_timer.mark(1, st);
+        g_timer.mark(2, st);
+    }
+    if (rc == DW_OK) g_timer.mark(3, st);
+    else if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
+    return rc;
+}
+
+template <bool FROM_WALKS>
+int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st) {
+    if (a.batch == 0) {
+        g_timer.mark(1, st);
+        g_timer.mark(2, st);
+        return DW_OK;
+    }
     const int64_t T = (int64_t)a.C * (1 + a.K);
     if (workspace == nullptr) return launch_pass1<FROM_WALKS, false>(a, st);
     DW_REQUIRE(T <= TMAX, "dw_sgns: records mode needs 2R(1+K) <= %d (got %lld)", TMAX,
@@ -729,6 +777,7 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t
     rc = launch_pass1_g16<FROM_WALKS>(a, st);
     if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
     if (rc != DW_OK) return rc;
+    g_timer.mark(1, st);
     hipcub::DoubleBuffer<uint32_t> kb(ws.k0, ws.k1);
     hipcub::DoubleBuffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
@@ -738,6 +787,7 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t
         dw::set_error("dw_sgns: hipcub sort failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
     }
+    g_timer.mark(2, st);
     return launch_pass2(kb.Current(), vb.Current(), n_rec, a.w_in, a.g_out, a.d, st);
 }
 
@@ -823,6 +873,33 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 }  // namespace
 
 extern "C" {
+
+int dw_sgns_timing(int32_t enable) {
+    g_timer.on = enable != 0;
+    if (enable) g_timer.calls = 0;
+    return DW_OK;
+}
+
+int dw_sgns_phase_ms(double *ms, int64_t *n_calls) {
+    DW_REQUIRE(ms && n_calls, "dw_sgns_phase_ms: null pointer");
+    ms[0] = ms[1] = ms[2] = 0.0;
+    *n_calls = static_cast<int64_t>(g_timer.calls);
+    if (g_timer.calls == 0) return DW_OK;
+    hipError_t e = hipEventSynchronize(g_timer.ev[4 * g_timer.calls - 1]);
+    for (size_t c = 0; c < g_timer.calls && e == hipSuccess; ++c) {
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) {
+            float t = 0.f;
+            e = hipEventElapsedTime(&t, g_timer.ev[4 * c + k], g_timer.ev[4 * c + k + 1]);
+            ms[k] += t;
+        }
+    }
+    if (e != hipSuccess) {
+        dw::set_error("dw_sgns_phase_ms: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    for (int k = 0; k < 3; ++k) ms[k] /= static_cast<double>(g_timer.calls);
+    return DW_OK;
+}
 
 int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
                             int64_t vocab_size, size_t *bytes) {

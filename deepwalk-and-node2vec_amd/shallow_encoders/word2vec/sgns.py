@@ -130,6 +130,20 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
     return loss_acc
 
 
+def phase_timing(enable: bool) -> None:
+    """Start (and reset) / stop per-phase HIP-event timing of later SGNS calls (profiling)."""
+    _native.call('dw_sgns_timing', 1 if enable else 0)
+
+
+def phase_ms() -> Dict[str, float]:
+    """Mean ms per recorded SGNS call: pass 1, records sort, pass 2 (waits for the last call)."""
+    import ctypes
+    ms = (ctypes.c_double * 3)()
+    n = ctypes.c_int64(0)
+    _native.call('dw_sgns_phase_ms', ms, ctypes.byref(n))
+    return {'pass1': ms[0], 'sort': ms[1], 'pass2': ms[2], 'calls': int(n.value)}
+
+
 class SGNSLoss(torch.autograd.Function):
     """loss = NegativeSamplingLoss(SkipGram(in, out), SkipGram(in, noise))['loss'], fused.
 

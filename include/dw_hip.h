@@ -149,6 +149,15 @@ int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, 
 int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
                             int64_t vocab_size, size_t *bytes);
 
+/* Profiling aid (bench.py): enable != 0 starts (and resets) per-phase HIP-event timing of every
+ * later dw_sgns_walks / dw_sgns_pairs call on this process; enable == 0 stops it.
+ * dw_sgns_phase_ms waits for the last recorded call and returns the mean milliseconds of
+ * ms[0] pass 1 (k_sgns*: logits, loss, centre gradients, records), ms[1] the radix sort of the
+ * records, ms[2] pass 2 (k_rec_gather: output-table gradients) over *n_calls calls (ms[1],
+ * ms[2] are 0 in atomic mode). No reference counterpart (measurement only). */
+int dw_sgns_timing(int32_t enable);
+int dw_sgns_phase_ms(double *ms, int64_t *n_calls);
+
 /* SkipGram.forward(inputs, outputs, proba) (model.py:79-91): logits[b, n] =
  * <w_in[inputs[b]], w_out[outputs[b, n]]>, sigmoid applied when proba != 0. */
 int dw_skipgram_logits(const int64_t *inputs, const int64_t *outputs, int64_t batch,

@@ -2,14 +2,22 @@
 
     python scripts/rocprof_summary.py <round-tag> [pairs_per_launch]
 
-Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim), profiles/<tag>_pmc.json
-(per-kernel mean FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC_sum per dispatch) and
-profiles/sgns_pmc.json (what bench.py reads for roofline.traffic).
+Writes
+  profiles/<tag>_kernel_stats.csv  rocprofv3 --stats, verbatim;
+  profiles/<tag>_pmc.json          per kernel class: dispatches, mean duration, HBM bytes per
+                                   dispatch and per SGNS call (FETCH_SIZE / WRITE_SIZE /
+                                   TCC_EA0_ATOMIC_sum passes);
+  profiles/sgns_pmc.json           what bench.py reads for roofline.traffic: HBM bytes of one
+                                   dw_sgns_walks call (pass 1 + sort + pass 2).
 
-HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB;
-FETCH_SIZE reads 1/2 of a wide coalesced stream's bytes on gfx950 (doubled here — calibrated
-on k_adam, whose 4 x 1 GiB read stream reports 2 GiB), WRITE_SIZE is exact for float atomics
-and 16-B streaming stores; TCC_EA0_ATOMIC_sum counts 64-B atomic requests.
+Kernel classes: one dw_sgns_walks call = one pass-1 dispatch (k_sgns_g16 / k_sgns) + the hipcub
+radix-sort dispatches + one k_rec_gather dispatch, so per-call figures divide a class's total
+by the number of pass-1 dispatches.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE
+reports 1/2 of a wide coalesced stream's bytes on gfx950 (doubled here — calibrated on k_adam,
+whose 4 x 1 GiB read stream reports 2 GiB), WRITE_SIZE is exact for float atomics and 16-B
+streaming stores; TCC_EA0_ATOMIC_sum counts 64-B atomic requests.
 """
 import collections
 import csv
@@ -22,15 +30,21 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, 'gpurun_out')
 PROF = os.path.join(REPO, 'profiles')
-KERNELS = {'k_sgns': 'dw_sgns_walks', 'k_adam': 'dw_adam_dense',
-           'k_walk_deepwalk_fast': 'dw_walk_fast/deepwalk',
-           'k_walk_node2vec_fast': 'dw_walk_fast/node2vec', 'k_sgns_rec': 'dw_sgns_records',
-           'k_out_adam': 'dw_adam_out_gather'}
+SGNS_CLASSES = ('sgns_pass1', 'sgns_sort', 'sgns_pass2')
 
 
-def short(name):
-    for k in sorted(KERNELS, key=len, reverse=True):
-        if k + '<' in name or k + '(' in name:
+def kernel_class(name: str):
+    if 'k_sgns_g16' in name or 'k_sgns<' in name or 'k_sgns(' in name:
+        return 'sgns_pass1'
+    if 'k_rec_gather' in name:
+        return 'sgns_pass2'
+    if 'radix_sort' in name or 'onesweep' in name:
+        # the SGNS records sort: u32 row keys, u64 {coef, centre} values; the CSR copy sort
+        # (dw_csr_sort_copy, u64 keys only) runs once at setup
+        return 'sgns_sort' if 'unsigned int, unsigned long' in name else 'csr_sort'
+    for k in ('k_adam', 'k_scale', 'k_walk_deepwalk_fast', 'k_walk_node2vec_fast',
+              'k_walk_replay', 'k_logits'):
+        if k in name:
             return k
     return None
 
@@ -40,49 +54,77 @@ def main():
     pairs = int(sys.argv[2]) if len(sys.argv) > 2 else None
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, 'prof_trace', '**', '*kernel_stats.csv'), recursive=True)
+    dur = collections.defaultdict(lambda: [0, 0.0])   # class -> [calls, total ns]
     if stats:
         shutil.copy(stats[0], os.path.join(PROF, f'{tag}_kernel_stats.csv'))
-    avg_ns = {}
-    if stats:
         for r in csv.DictReader(open(stats[0])):
-            k = short(r['Name'])
+            k = kernel_class(r['Name'])
             if k:
-                avg_ns[k] = float(r['AverageNs'])
-    pmc = collections.defaultdict(dict)
+                dur[k][0] += int(r['Calls'])
+                dur[k][1] += float(r['TotalDurationNs'])
+    # counter passes: one file per counter group; totals per class and dispatch counts
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(lambda: collections.defaultdict(set))
     for path in glob.glob(os.path.join(OUT, 'prof_pmc_*', '**', '*counter_collection.csv'),
                           recursive=True):
-        vals = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(path)):
-            k = short(r['Kernel_Name'])
-            if k:
-                vals[k][r['Counter_Name']].append(float(r['Counter_Value']))
-        for k, d in vals.items():
-            for ctr, v in d.items():
-                pmc[k][ctr] = sum(v) / len(v)
+            k = kernel_class(r['Kernel_Name'])
+            if not k:
+                continue
+            ctr = r['Counter_Name']
+            tot[k][ctr] += float(r['Counter_Value'])
+            disp[k][ctr].add((path, r.get('Dispatch_Id', r.get('Correlation_Id', ''))))
     summary = {}
-    for k, d in pmc.items():
-        e = dict(d)
-        fetch, write = d.get('FETCH_SIZE'), d.get('WRITE_SIZE')
-        if fetch is not None and write is not None:
-            e['hbm_bytes_per_launch'] = 2 * fetch * 1024 + write * 1024
-        if 'TCC_EA0_ATOMIC_sum' in d:
-            e['atomic_bytes_per_launch'] = d['TCC_EA0_ATOMIC_sum'] * 64
-        if k in avg_ns:
-            e['avg_ns'] = avg_ns[k]
-            if 'hbm_bytes_per_launch' in e:
-                e['hbm_GBps'] = e['hbm_bytes_per_launch'] / avg_ns[k]
-            if 'atomic_bytes_per_launch' in e:
-                e['atomic_GBps'] = e['atomic_bytes_per_launch'] / avg_ns[k]
-        summary[KERNELS.get(k, k)] = e
+    n_calls_pmc = {}
+    for k in set(tot) | set(dur):
+        e = {}
+        if k in dur:
+            e['trace_dispatches'] = dur[k][0]
+            e['avg_ns_per_dispatch'] = dur[k][1] / max(dur[k][0], 1)
+        per_disp = {}
+        for ctr, v in tot[k].items():
+            n = len(disp[k][ctr])
+            per_disp[ctr] = v / max(n, 1)
+            n_calls_pmc[(k, ctr)] = n
+        e['counters_per_dispatch'] = per_disp
+        if 'FETCH_SIZE' in per_disp and 'WRITE_SIZE' in per_disp:
+            e['hbm_bytes_per_dispatch'] = (2 * per_disp['FETCH_SIZE'] +
+                                           per_disp['WRITE_SIZE']) * 1024
+        if 'TCC_EA0_ATOMIC_sum' in per_disp:
+            e['atomic_bytes_per_dispatch'] = per_disp['TCC_EA0_ATOMIC_sum'] * 64
+        summary[k] = e
+    # per SGNS call: class totals / pass-1 dispatches
+    p1 = summary.get('sgns_pass1', {})
+    calls_trace = p1.get('trace_dispatches', 0)
+    call = {'ms': 0.0, 'hbm_bytes': 0.0}
+    ok = calls_trace > 0
+    for k in SGNS_CLASSES:
+        e = summary.get(k)
+        if not e:
+            continue
+        if k in dur and calls_trace:
+            e['ms_per_sgns_call'] = dur[k][1] / calls_trace / 1e6
+            call['ms'] += e['ms_per_sgns_call']
+        if 'hbm_bytes_per_dispatch' in e:
+            ratio = (n_calls_pmc.get((k, 'FETCH_SIZE'), 0) /
+                     max(n_calls_pmc.get(('sgns_pass1', 'FETCH_SIZE'), 0), 1))
+            e['hbm_bytes_per_sgns_call'] = e['hbm_bytes_per_dispatch'] * ratio
+            call['hbm_bytes'] += e['hbm_bytes_per_sgns_call']
+        else:
+            ok = False
+    summary['dw_sgns_walks_call'] = call
     with open(os.path.join(PROF, f'{tag}_pmc.json'), 'w') as f:
         json.dump(summary, f, indent=2)
-    s = summary.get('dw_sgns_walks')
-    if s and 'hbm_bytes_per_launch' in s and pairs:
+    if ok and pairs:
+        per_kernel = {k: summary[k].get('hbm_bytes_per_sgns_call') for k in SGNS_CLASSES
+                      if k in summary}
         with open(os.path.join(PROF, 'sgns_pmc.json'), 'w') as f:
             json.dump({'round': tag, 'pairs_per_launch': pairs,
-                       'hbm_bytes_per_launch': s['hbm_bytes_per_launch'],
-                       'atomic_bytes_per_launch': s.get('atomic_bytes_per_launch'),
-                       'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B); see scripts/rocprof_summary.py'},
+                       'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
+                       'hbm_bytes_per_launch': call['hbm_bytes'],
+                       'hbm_bytes_per_kernel': per_kernel,
+                       'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of '
+                               'one dw_sgns_walks call; see scripts/rocprof_summary.py'},
                       f, indent=2)
     print(json.dumps(summary, indent=2))
 
