@@ -11,9 +11,12 @@
 //     against N(prev) staged sorted in LDS), then ONE lane reproduces CPython's left-to-right
 //     fp64 sum / accumulate / bisect_right serially — a parallel scan would round differently.
 //     This file is compiled with -ffp-contract=off so no mul+add pair fuses into an FMA.
-//   * fast: Philox4x32-10 keyed by (seed, global walk id, step, lane/round).
-//     DeepWalk: one lane per walker. node2vec: one wave per walker, 64 proposals per round,
-//     exact rejection against alpha/alpha_max, lowest accepting lane wins (ballot).
+//   * fast: Philox4x32-10 keyed by (seed, global walk id, step, proposal/round).
+//     DeepWalk: one lane per walker. node2vec: 8 lanes per walker, 64 proposals per round
+//     evaluated 8 at a time, exact rejection against alpha/alpha_max, lowest accepting
+//     proposal wins (ballot); adjacency tests only where the uniform leaves the outcome open.
+#include <stdlib.h>
+
 #include "dw_common.h"
 
 namespace {
@@ -264,13 +267,51 @@ __global__ void __launch_bounds__(256)
     for (; s < L; ++s) o[s] = -1;
 }
 
-constexpr int N2V_WAVES = 4;     // waves per block, each owns one walker at a time
-constexpr int N2V_NCAP = 1024;   // staged N(prev) entries per wave (int32): 4 KiB
+constexpr int N2V_WAVES = 4;     // waves per block
 
 struct N2VThr {
     uint32_t p, q, one;  // accept iff r < thr (ALWAYS = unconditional)
 };
 
+// The G-bit slice of a wave ballot that belongs to this lane's group.
+template <int G>
+__device__ __forceinline__ uint32_t group_ballot(bool pred, int q) {
+    return static_cast<uint32_t>((__ballot(pred) >> (G * q)) & ((1ull << G) - 1ull));
+}
+
+// Membership of a group-uniform key in a sorted int32 list [0, n), the N2V_G lanes of a group
+// cooperating: N2V_G-ary search — lane j reads splitter j of the current range, one ballot picks
+// the segment, until <= N2V_G entries remain and one load + ballot decides. ceil(log_G n)
+// dependent loads (6 at G=8 for the largest C3 hub, 44,848 neighbours), no LDS staging.
+template <int N2V_G>
+__device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list, int64_t n,
+                                               int32_t key, int gl, int q) {
+    int64_t lo = 0, len = n;
+    while (len > N2V_G) {
+        const int64_t idx = lo + (static_cast<int64_t>(gl) * len) / N2V_G;
+        const int32_t sv = list[idx];
+        if (group_ballot<N2V_G>(sv == key, q)) return true;
+        const int c = __popc(group_ballot<N2V_G>(sv < key, q));  // splitters below key: 0 .. c-1
+        if (c == 0) return false;                          // key < list[lo]
+        const int64_t s0 = lo + (static_cast<int64_t>(c - 1) * len) / N2V_G;
+        const int64_t s1 = (c == N2V_G) ? lo + len : lo + (static_cast<int64_t>(c) * len) / N2V_G;
+        lo = s0;
+        len = s1 - s0;
+    }
+    const bool hit = gl < len && list[lo + gl] == key;
+    return group_ballot<N2V_G>(hit, q) != 0u;
+}
+
+// N2V_G lanes per walker (8 by default: 8 walkers per wave — the walk is latency-bound, so
+// walkers in flight matter more than proposals per instruction). A rejection round draws
+// proposals j = 0..63 (Philox counter lane field j; oracle/philox.py fast_walks) and picks the
+// LOWEST accepting j; the group evaluates them N2V_G at a time in j order and stops at the first block holding an
+// acceptance, which selects the same j as evaluating all 64 at once. A proposal x != prev is
+// accepted iff r < thr(x in N(prev) ? q : one); when r is below both thresholds (accept) or
+// not below either (reject) the adjacency test cannot change the outcome, so only the
+// "ambiguous" proposals BELOW the block's first certain acceptance are tested, in j order,
+// each by one group-cooperative search of N(prev).
+template <int N2V_G>
 __global__ void __launch_bounds__(N2V_WAVES *WAVE)
     k_walk_node2vec_fast(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
                          const int32_t *__restrict__ col_sorted,
@@ -278,29 +319,39 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                          int32_t L, N2VThr thr, uint32_t k0, uint32_t k1, uint64_t walk_id0,
                          int32_t *__restrict__ out, int32_t *status) {
-    __shared__ int32_t s_nprev[N2V_WAVES][N2V_NCAP];
     const int lane = threadIdx.x & (WAVE - 1);
+    const int q = lane / N2V_G, gl = lane & (N2V_G - 1);
     const int wv = threadIdx.x / WAVE;
-    int32_t *nprev = s_nprev[wv];
-    const int64_t n_waves = (int64_t)gridDim.x * N2V_WAVES;
+    constexpr int GPW = WAVE / N2V_G;  // walkers per wave
+    const int64_t n_slots = (int64_t)gridDim.x * N2V_WAVES * GPW;
+    // thresholds as 33-bit bounds: accept iff r < T (ALWAYS -> 2^32)
+    const uint64_t Tp = thr.p == ALWAYS ? (1ull << 32) : thr.p;
+    const uint64_t Tq = thr.q == ALWAYS ? (1ull << 32) : thr.q;
+    const uint64_t T1 = thr.one == ALWAYS ? (1ull << 32) : thr.one;
+    const uint64_t Tlo = Tq < T1 ? Tq : T1, Thi = Tq < T1 ? T1 : Tq;
+    const bool adj_wins = Tq > T1;  // in the ambiguous band: accept iff (x in N(prev)) == adj_wins
 
-    for (int64_t w = (int64_t)blockIdx.x * N2V_WAVES + wv; w < n_walks; w += n_waves) {
+    for (int64_t base = ((int64_t)blockIdx.x * N2V_WAVES + wv) * GPW; base < n_walks;
+         base += n_slots) {
+        const int64_t w = base + q;
+        if (w >= n_walks) continue;
         const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
         const uint32_t c0 = static_cast<uint32_t>(wid), c1 = static_cast<uint32_t>(wid >> 32);
         int32_t *o = out + w * (int64_t)L;
         int32_t v = starts[w];
         int32_t prev = -1;
-        if (lane == 0) o[0] = v;
+        int64_t pa = 0, pn = 0;  // CSR range of prev (carried from the previous step)
+        if (gl == 0) o[0] = v;
         int32_t s = 1;
         for (; s < L; ++s) {
             if (v < 0 || (int64_t)v >= n_rows) {
-                if (lane == 0) dw::status_or(status, DW_S_BAD_CSR);
+                if (gl == 0) dw::status_or(status, DW_S_BAD_CSR);
                 break;
             }
             const int64_t a = row_ptr[v];
             const int64_t n = row_ptr[v + 1] - a;
             if (n <= 0) {
-                if (lane == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
+                if (gl == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
                 break;
             }
             int32_t nxt;
@@ -309,46 +360,50 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                     dw::U4{c0, c1, static_cast<uint32_t>(s) << 8, dw::TAG_NODE2VEC}, k0, k1);
                 nxt = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
             } else {
-                const int64_t pa = row_ptr[prev];
-                const int64_t pn = row_ptr[prev + 1] - pa;
-                const bool staged = pn <= N2V_NCAP;
-                if (staged) {
-                    for (int64_t e = lane; e < pn; e += WAVE) nprev[e] = col_sorted[pa + e];
-                    dw::wave_lds_sync();
-                }
                 nxt = -1;
-                for (uint32_t round = 0; round < DW_MAX_REJECTION_ROUNDS; ++round) {
-                    const dw::U4 r = dw::philox(
-                        dw::U4{c0, c1, (static_cast<uint32_t>(s) << 8) | static_cast<uint32_t>(lane),
-                               dw::TAG_NODE2VEC ^ round},
-                        k0, k1);
-                    const int32_t x = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
-                    uint32_t t;
-                    if (x == prev)
-                        t = thr.p;
-                    else if (staged ? contains_lds(nprev, static_cast<int>(pn), x)
-                                    : contains_global(col_sorted + pa, pn, x))
-                        t = thr.q;
-                    else
-                        t = thr.one;
-                    const bool acc = (t == ALWAYS) || (r.z < t);
-                    const unsigned long long m = __ballot(acc);
-                    if (m) {
-                        nxt = __shfl(x, __ffsll(static_cast<long long>(m)) - 1, WAVE);
-                        break;
+                for (uint32_t round = 0; round < DW_MAX_REJECTION_ROUNDS && nxt < 0; ++round) {
+                    for (int blk = 0; blk < WAVE / N2V_G; ++blk) {
+                        const uint32_t j = static_cast<uint32_t>(blk * N2V_G + gl);
+                        const dw::U4 r = dw::philox(
+                            dw::U4{c0, c1, (static_cast<uint32_t>(s) << 8) | j,
+                                   dw::TAG_NODE2VEC ^ round},
+                            k0, k1);
+                        const int32_t x = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+                        const uint64_t u = r.z;
+                        const bool sure = (x == prev) ? (u < Tp) : (u < Tlo);
+                        const bool amb = x != prev && u >= Tlo && u < Thi;
+                        const uint32_t m_sure = group_ballot<N2V_G>(sure, q);
+                        const int f = m_sure ? __ffs(m_sure) - 1 : N2V_G;
+                        uint32_t m_amb = group_ballot<N2V_G>(amb, q);
+                        if (f < N2V_G) m_amb &= (1u << f) - 1u;
+                        int win = f;
+                        while (m_amb) {  // group-uniform loop over the candidates that matter
+                            const int l = __ffs(m_amb) - 1;
+                            const int32_t xl = __shfl(x, q * N2V_G + l, WAVE);
+                            if (group_contains<N2V_G>(col_sorted + pa, pn, xl, gl, q) == adj_wins) {
+                                win = l;
+                                break;
+                            }
+                            m_amb &= m_amb - 1u;
+                        }
+                        if (win < N2V_G) {
+                            nxt = __shfl(x, q * N2V_G + win, WAVE);
+                            break;
+                        }
                     }
                 }
-                if (staged) dw::wave_lds_sync();  // WAR on nprev before the next staging
                 if (nxt < 0) {
-                    if (lane == 0) dw::status_or(status, DW_S_REJECTION_CAP);
+                    if (gl == 0) dw::status_or(status, DW_S_REJECTION_CAP);
                     break;
                 }
             }
-            if (lane == 0) o[s] = nxt;
+            if (gl == 0) o[s] = nxt;
             prev = v;
+            pa = a;
+            pn = n;
             v = nxt;
         }
-        if (lane == 0)
+        if (gl == 0)
             for (; s < L; ++s) o[s] = -1;
     }
 }
@@ -429,11 +484,24 @@ int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_
     if (ip > amax) amax = ip;
     if (iq > amax) amax = iq;
     N2VThr thr{accept_threshold(ip, amax), accept_threshold(iq, amax), accept_threshold(1.0, amax)};
-    int64_t blocks = (n_walks + N2V_WAVES - 1) / N2V_WAVES;
+    static const int group = [] {  // lanes per walker (tuning knob DW_N2V_GROUP = 8 | 16)
+        const char *e = getenv("DW_N2V_GROUP");
+        const int g = e ? atoi(e) : 8;
+        return (g == 8 || g == 16) ? g : 8;
+    }();
+    const int64_t per_block = N2V_WAVES * (WAVE / group);
+    int64_t blocks = (n_walks + per_block - 1) / per_block;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_walk_node2vec_fast, dim3((unsigned)blocks), dim3(N2V_WAVES * WAVE), 0,
-                       dw::as_stream(stream), row_ptr, col, col_sorted, prob_thr, alias, n_rows,
-                       starts, n_walks, walk_length, thr, k0, k1, walk_id0, out, status);
+    if (group == 8)
+        hipLaunchKernelGGL(k_walk_node2vec_fast<8>, dim3((unsigned)blocks), dim3(N2V_WAVES * WAVE),
+                           0, dw::as_stream(stream), row_ptr, col, col_sorted, prob_thr, alias,
+                           n_rows, starts, n_walks, walk_length, thr, k0, k1, walk_id0, out,
+                           status);
+    else
+        hipLaunchKernelGGL(k_walk_node2vec_fast<16>, dim3((unsigned)blocks),
+                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col,
+                           col_sorted, prob_thr, alias, n_rows, starts, n_walks, walk_length, thr,
+                           k0, k1, walk_id0, out, status);
     DW_LAUNCH_CHECK("dw_walk_fast/node2vec");
     return DW_OK;
 }
