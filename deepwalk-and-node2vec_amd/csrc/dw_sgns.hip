@@ -16,7 +16,8 @@
 //   * atomic: g_out[row] += coef * centre, float atomics (1.3 TB/s chip-wide ceiling on MI355X;
 //     the output-table scatter is ~90% of the SGNS bytes, so this mode is atomic-bound);
 //   * records (workspace given): each output row's coefficient is written as a 12-byte record
-//     {row, centre, coef} (coalesced), the records are radix-sorted by row (hipcub, stable), and
+//     {row, centre, coef} (coalesced), the records are radix-sorted by row (rocprim onesweep,
+//     stable, 11-bit digits), and
 //     pass 2 (k_rec_gather) gathers the centre rows and sums every output row's records in
 //     registers. No float atomics except where a row straddles two fixed-size chunks; the
 //     gathered bytes move at read speed, not atomic speed.
@@ -24,7 +25,7 @@
 
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "dw_common.h"
 
@@ -568,14 +569,23 @@ struct Workspace {
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Records sort: onesweep with 11-bit digits on 1024 x 16 tiles — 2 passes for C3's 21-bit row
+// ids (the gfx950 default, 8-bit digits on 1024 x 8, needs 3): 0.79 ms vs 1.09 ms for 34.4M
+// records on MI355X (scripts/microbench/sort_bench.hip).
+using RecordSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>,
+                                        rocprim::kernel_config<1024, 16>, 11,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStream_t st) {
     size_t cub_bytes = 0;
-    hipcub::DoubleBuffer<uint32_t> kb(nullptr, nullptr);
-    hipcub::DoubleBuffer<uint64_t> vb(nullptr, nullptr);
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, kb, vb, (int)n_rec, 0,
-                                                      end_bit_for(V), st);
+    rocprim::double_buffer<uint32_t> kb(nullptr, nullptr);
+    rocprim::double_buffer<uint64_t> vb(nullptr, nullptr);
+    hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
+        nullptr, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(V), st);
     if (e != hipSuccess) {
-        dw::set_error("dw_sgns: hipcub size query failed: %s", hipGetErrorString(e));
+        dw::set_error("dw_sgns: sort size query failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
     }
     const size_t kbytes = align256((size_t)n_rec * 4), vbytes = align256((size_t)n_rec * 8);
@@ -731,7 +741,7 @@ struct PhaseTimer {
             }
             ev.push_back(e);
         }
-        hipEventRecord(ev[i], st);
+        (void)hipEventRecord(ev[i], st);
         if (slot == 3) ++calls;
     }
 };
@@ -778,17 +788,17 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStr
     if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
     if (rc != DW_OK) return rc;
     g_timer.mark(1, st);
-    hipcub::DoubleBuffer<uint32_t> kb(ws.k0, ws.k1);
-    hipcub::DoubleBuffer<uint64_t> vb(ws.v0, ws.v1);
+    rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
+    rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws.cub, cub_bytes, kb, vb, (int)n_rec, 0,
-                                                      end_bit_for(a.V), st);
+    hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
+        ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(a.V), st);
     if (e != hipSuccess) {
-        dw::set_error("dw_sgns: hipcub sort failed: %s", hipGetErrorString(e));
+        dw::set_error("dw_sgns: records sort failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
     }
     g_timer.mark(2, st);
-    return launch_pass2(kb.Current(), vb.Current(), n_rec, a.w_in, a.g_out, a.d, st);
+    return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, st);
 }
 
 // ---- SkipGram.forward logits and its backward (autograd path of the reference API) ----------
