@@ -7,7 +7,7 @@
 // arguments are:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2);
 //   denom = (v.sqrt() / bias_correction2_sqrt).add_(eps); p.addcdiv_(m, denom, value=-step_size)
-// Streaming: 16 B per lane per tensor; p, g, m, v read once, p, m, v (and g=0) written once.
+// Streaming: 16-B accesses; p, g, m, v read once, p, m, v (and g=0) written once.
 #include "dw_common.h"
 
 namespace {
@@ -27,28 +27,64 @@ __device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v
     p = p + s.nstep * (m / denom);
 }
 
-template <bool ZERO>
+// Every byte is touched once per step, so loads and stores are non-temporal (they neither
+// allocate in L2 / the Infinity Cache nor evict the embedding rows the next SGNS pass gathers),
+// and each lane keeps U = 2 float4 groups of all four tensors in flight. Measured on MI355X,
+// same box, C3 tables (2 x 1,048,577 x 128): 1.75 ms vs 2.02 ms for plain loads / stores with
+// one group per lane (scripts/gpu_tune.sh, DW_ADAM_VARIANT sweep of round 1).
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld(const float4 *p, bool nt) {
+    if (!nt) return *p;
+    const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void st(float4 *p, float4 v, bool nt) {
+    if (!nt) {
+        *p = v;
+        return;
+    }
+    const f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f4v *>(p));
+}
+
+template <bool ZERO, bool NT, int U, bool NTS = NT>
 __global__ void __launch_bounds__(256)
     k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
-           float *__restrict__ v, int64_t n, AdamScalars s) {
+             float *__restrict__ v, int64_t n, AdamScalars s) {
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     float4 *p4 = reinterpret_cast<float4 *>(p);
     float4 *g4 = reinterpret_cast<float4 *>(g);
     float4 *m4 = reinterpret_cast<float4 *>(m);
     float4 *v4 = reinterpret_cast<float4 *>(v);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
-        adam_elem(pp.x, gg.x, mm.x, vv.x, s);
-        adam_elem(pp.y, gg.y, mm.y, vv.y, s);
-        adam_elem(pp.z, gg.z, mm.z, vv.z, s);
-        adam_elem(pp.w, gg.w, mm.w, vv.w, s);
-        p4[i] = pp;
-        m4[i] = mm;
-        v4[i] = vv;
-        if (ZERO) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n4;
+         i0 += stride * U) {
+        float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < n4) {
+                pp[u] = ld(p4 + i, NT);
+                gg[u] = ld(g4 + i, NT);
+                mm[u] = ld(m4 + i, NT);
+                vv[u] = ld(v4 + i, NT);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < n4) {
+                adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, s);
+                adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, s);
+                adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, s);
+                adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, s);
+                st(p4 + i, pp[u], NTS);
+                st(m4 + i, mm[u], NTS);
+                st(v4 + i, vv[u], NTS);
+                if (ZERO) st(g4 + i, make_float4(0.f, 0.f, 0.f, 0.f), NTS);
+            }
+        }
     }
-    // tail (n % 4 elements)
     for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += stride) {
         adam_elem(p[i], g[i], m[i], v[i], s);
@@ -85,10 +121,10 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
     if (blocks < 1) blocks = 1;
     if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond
     if (zero_grad)
-        hipLaunchKernelGGL(k_adam<true>, dim3((unsigned)blocks), dim3(256), 0,
+        hipLaunchKernelGGL((k_adam<true, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
     else
-        hipLaunchKernelGGL(k_adam<false>, dim3((unsigned)blocks), dim3(256), 0,
+        hipLaunchKernelGGL((k_adam<false, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
     DW_LAUNCH_CHECK("dw_adam_dense");
     return DW_OK;
