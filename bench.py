@@ -177,13 +177,18 @@ def main():
         walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
         if record:
             e[1].record()
-        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K,
-                        walks=walks_buf, context_radius=R, noise=None, seed=99,
-                        noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale,
-                        loss_acc=loss_acc, status=status, scatter=args.scatter)
+        kw = dict(walks=walks_buf, context_radius=R, noise=None, seed=99,
+                  noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale, loss_acc=loss_acc,
+                  status=status, scatter=args.scatter)
+        # pass 1 (g_in final) -> in-table exchange on a side stream (N > 1) while the
+        # output-table phase runs -> out-table exchange -> wait for both all-gathers
+        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
+        tables.exchange_in()
+        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2, **kw)
         if record:
             e[2].record()
-        tables.step()
+        tables.exchange_out()
+        tables.sync()
         if record:
             e[3].record()
             ev['walk'].append((e[0], e[1]))

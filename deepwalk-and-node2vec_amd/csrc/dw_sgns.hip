@@ -747,31 +747,41 @@ struct PhaseTimer {
 };
 PhaseTimer g_timer;
 
+// phase 0: the whole call. phase 1: pass 1 only (centre-table gradients, loss sums, records).
+// phase 2: the records sort + pass 2 (output-table gradients) of a preceding phase-1 call with
+// the same arguments and workspace. Atomic mode (no workspace) completes in phase 1; its
+// phase 2 is empty. The split lets a caller start the centre-table gradient exchange while
+// the output-table phase runs (ShardedTables.exchange_in).
 template <bool FROM_WALKS>
-int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st);
+int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
+                     hipStream_t st);
 
 template <bool FROM_WALKS>
-int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st) {
-    g_timer.mark(0, st);
-    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, st);
-    if (rc == DW_OK && workspace == nullptr) {
-        g_timer.mark(1, st);
-        g_timer.mark(2, st);
+int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, hipStream_t st) {
+    if (phase != 2) g_timer.mark(0, st);
+    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st);
+    if (rc != DW_OK) {
+        if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
+        return rc;
     }
-    if (rc == DW_OK) g_timer.mark(3, st);
-    else if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
-    return rc;
+    if (phase != 1) g_timer.mark(3, st);
+    return DW_OK;
 }
 
 template <bool FROM_WALKS>
-int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStream_t st) {
-    if (a.batch == 0) {
-        g_timer.mark(1, st);
-        g_timer.mark(2, st);
+int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
+                     hipStream_t st) {
+    const bool do1 = phase != 2, do2 = phase != 1;
+    if (a.batch == 0 || workspace == nullptr) {
+        if (do1 && a.batch > 0) {
+            const int rc = launch_pass1<FROM_WALKS, false>(a, st);
+            if (rc != DW_OK) return rc;
+        }
+        if (do1) g_timer.mark(1, st);
+        if (do2) g_timer.mark(2, st);
         return DW_OK;
     }
     const int64_t T = (int64_t)a.C * (1 + a.K);
-    if (workspace == nullptr) return launch_pass1<FROM_WALKS, false>(a, st);
     DW_REQUIRE(T <= TMAX, "dw_sgns: records mode needs 2R(1+K) <= %d (got %lld)", TMAX,
                (long long)T);
     DW_REQUIRE(a.V <= 0x7FFFFFFF, "dw_sgns: records mode needs vocab_size < 2^31");
@@ -782,12 +792,15 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, hipStr
     if (rc != DW_OK) return rc;
     DW_REQUIRE(workspace_bytes >= ws.total, "dw_sgns: workspace too small (%zu < %zu)",
                workspace_bytes, ws.total);
-    a.rec_key = ws.k0;
-    a.rec_val = ws.v0;
-    rc = launch_pass1_g16<FROM_WALKS>(a, st);
-    if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
-    if (rc != DW_OK) return rc;
-    g_timer.mark(1, st);
+    if (do1) {
+        a.rec_key = ws.k0;
+        a.rec_val = ws.v0;
+        rc = launch_pass1_g16<FROM_WALKS>(a, st);
+        if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
+        if (rc != DW_OK) return rc;
+        g_timer.mark(1, st);
+    }
+    if (!do2) return DW_OK;
     rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
     rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
@@ -926,12 +939,14 @@ int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_sample
     return DW_OK;
 }
 
-int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                  int32_t context_radius, int32_t neg_samples, int64_t vocab_size, int32_t dim,
-                  const float *w_in, const float *w_out, float *g_in, float *g_out,
-                  const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
-                  double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
-                  void *stream) {
+namespace {
+int sgns_walks(int phase, const int32_t *walks, int64_t n_walks, int32_t walk_length,
+               int32_t context_radius, int32_t neg_samples, int64_t vocab_size, int32_t dim,
+               const float *w_in, const float *w_out, float *g_in, float *g_out,
+               const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
+               double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
+               void *stream) {
+    DW_REQUIRE(phase >= 0 && phase <= 2, "dw_sgns_walks_phase: phase must be 0, 1 or 2");
     DW_REQUIRE(context_radius >= 1, "dw_sgns_walks: context_radius must be >= 1");
     DW_REQUIRE(walk_length >= 2 * context_radius + 1,
                "dw_sgns_walks: walk_length %d < 2R+1 (Text is too short!)", walk_length);
@@ -945,7 +960,31 @@ int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
     a.R = context_radius;
     a.batch = n_walks * (walk_length - 2 * context_radius);
     a.C = 2 * context_radius;
-    return launch_sgns<true>(a, workspace, workspace_bytes, dw::as_stream(stream));
+    return launch_sgns<true>(a, workspace, workspace_bytes, phase, dw::as_stream(stream));
+}
+}  // namespace
+
+int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                  int32_t context_radius, int32_t neg_samples, int64_t vocab_size, int32_t dim,
+                  const float *w_in, const float *w_out, float *g_in, float *g_out,
+                  const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
+                  double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
+                  void *stream) {
+    return sgns_walks(0, walks, n_walks, walk_length, context_radius, neg_samples, vocab_size,
+                      dim, w_in, w_out, g_in, g_out, noise, seed, noise_offset, grad_scale,
+                      loss_acc, status, workspace, workspace_bytes, stream);
+}
+
+int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
+                        int32_t walk_length, int32_t context_radius, int32_t neg_samples,
+                        int64_t vocab_size, int32_t dim, const float *w_in, const float *w_out,
+                        float *g_in, float *g_out, const int64_t *noise, uint64_t seed,
+                        uint64_t noise_offset, float grad_scale, double *loss_acc,
+                        int32_t *status, void *workspace, size_t workspace_bytes,
+                        void *stream) {
+    return sgns_walks(phase, walks, n_walks, walk_length, context_radius, neg_samples,
+                      vocab_size, dim, w_in, w_out, g_in, g_out, noise, seed, noise_offset,
+                      grad_scale, loss_acc, status, workspace, workspace_bytes, stream);
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,
@@ -964,7 +1003,7 @@ int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, 
     a.targets = targets;
     a.batch = batch;
     a.C = n_ctx;
-    return launch_sgns<false>(a, workspace, workspace_bytes, dw::as_stream(stream));
+    return launch_sgns<false>(a, workspace, workspace_bytes, 0, dw::as_stream(stream));
 }
 
 int dw_skipgram_logits(const int64_t *inputs, const int64_t *outputs, int64_t batch,

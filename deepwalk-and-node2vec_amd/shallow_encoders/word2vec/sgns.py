@@ -68,7 +68,8 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                     targets: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                     seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                     loss_acc: Optional[torch.Tensor] = None,
-                    status: Optional[torch.Tensor] = None, scatter: str = 'sorted') -> torch.Tensor:
+                    status: Optional[torch.Tensor] = None, scatter: str = 'sorted',
+                    phase: int = 0) -> torch.Tensor:
     """Launch the fused SGNS kernel(s); returns the float64[4] loss accumulator.
 
     Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B,1]) +
@@ -76,6 +77,8 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
     Philox keyed by (seed, noise_offset + centre)). ``grad_scale`` defaults to 1/(B'*C).
     ``scatter``: 'sorted' (records + radix sort + per-row gather, no output-table atomics) or
     'atomic' (float atomics straight into g_out).
+    ``phase`` (walks only): 0 = the whole update; 1 = pass 1 (g_in final, loss sums, records);
+    2 = the output-table phase (g_out) of the preceding phase-1 call with the same arguments.
     """
     dev = w_in.device
     V, d = w_in.shape
@@ -105,7 +108,7 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
             scale = 1.0 / max(n_centres * C, 1) if grad_scale is None else grad_scale
             ws = workspace_for(n_centres, C, K, V, dev) \
                 if _use_records(scatter, C, K, V) else None
-            _native.call('dw_sgns_walks', _native.ptr(walks), n, L, R, K, V, d,
+            _native.call('dw_sgns_walks_phase', int(phase), _native.ptr(walks), n, L, R, K, V, d,
                          _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_in),
                          _native.ptr(g_out), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), float(scale), _native.ptr(loss_acc),
@@ -113,6 +116,8 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
         else:
             if inputs is None or targets is None:
                 raise ValueError('give walks, or inputs and targets')
+            if phase != 0:
+                raise ValueError('the two-phase form takes walks')
             inputs = inputs.reshape(-1)
             B, C = targets.shape
             if inputs.numel() != B:

@@ -1,23 +1,38 @@
 """Embedding tables sharded by node-id range across the GPUs of one node.
 
-The reference trains on one device (``devices: '1'`` in every config). Data-parallel SGNS
-with dense Adam semantics is laid out here ZeRO-1 style, one process per GPU:
+The reference trains on one device (``devices: '1'`` in every config). Here data-parallel SGNS
+with dense Adam semantics is laid out ZeRO-1 style, one process per GPU. Every rank scales its
+local gradient by 1/M_global (the mean over the GLOBAL batch), so the result equals
+single-device training on the concatenated batch (DDP semantics). Walk generation needs no
+communication, because walks are keyed by the global walk id.
 
-  params  float32 [2, V_pad, d]   both tables (in, out) in ONE flat buffer, replicated
-  grads   float32 [2, V_pad, d]   local dense gradients (the fused SGNS kernel adds into them)
-  m, v    float32 [2*V_pad*d / world]  Adam state for THIS rank's contiguous slice only
+Layout (S = V_pad / world rows; rank r owns rows [r*S, (r+1)*S) of BOTH tables):
 
-Per optimizer step (all collectives over RCCL = torch.distributed 'nccl' on ROCm, xGMI):
-  1. reduce-scatter(sum) of the flat gradient: rank r receives the global gradient of its
-     slice — a contiguous node-id range of the stacked [in; out] tables;
-  2. dense Adam on that slice only (dw_adam_dense): 1/world of the optimizer's HBM traffic;
-  3. all-gather of the updated parameter slices back into every rank's replica.
-Every rank scales its local gradient by 1/M_global (the mean over the GLOBAL batch), so the
-result equals single-device training on the concatenated batch (DDP semantics).
-Walk generation needs no communication (walks are keyed by global walk id).
+  params  float32 [2 or 3, V_pad, d]   slot 1 = out table; slot 0 = in table, and slot 2 =
+                                       its second buffer when world > 1 (see below)
+  grads   float32 [2, V_pad, d]        local dense gradients (in, out)
+  m, v    float32 [2, S, d]            Adam state of this rank's rows only
 
-The Adam update is injectable (``adam_impl``) so the exchange logic can be tested with gloo
-on CPU; the default is the HIP kernel and refuses host tensors.
+Per optimizer step, all collectives run over RCCL (torch.distributed 'nccl' on ROCm, xGMI),
+one table at a time:
+  1. reduce-scatter(sum) of the table's gradient: rank r receives the global gradient of its
+     rows;
+  2. dense Adam on those rows only (dw_adam_dense): 1/world of the optimizer's HBM traffic;
+  3. all-gather of the updated rows back into every rank's replica.
+
+Overlapped form (``exchange_in`` / ``exchange_out`` / ``sync``):
+  * The in-table gradient is final after SGNS pass 1 (dw_sgns_walks_phase 1).
+  * So ``exchange_in`` runs the in-table's reduce-scatter, Adam and all-gather on a side
+    stream while the output-table phase (records sort + gather) still runs on the main stream.
+  * That phase reads the current in table, so the update goes into the idle buffer: copy own
+    rows, Adam in place, all-gather into the buffer. The two buffers swap at ``sync``.
+  * ``exchange_out`` does the out table after phase 2.
+  * ``sync`` makes the main stream wait for both all-gathers before the next pass 1.
+``step()`` is the same update done serially.
+
+The Adam update is injectable (``adam_impl``), so the exchange logic can be tested with gloo
+on the CPU (there the overlapped form runs its collectives synchronously). The default is the
+HIP kernel, which refuses host tensors.
 """
 import math
 from typing import Callable, Optional
@@ -54,24 +69,30 @@ class ShardedTables:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.V, self.d = int(vocab_size), int(dim)
         self.V_pad = int(math.ceil(self.V / self.world)) * self.world
+        self.S = self.V_pad // self.world
         self.device = torch.device(device)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.adam_impl = adam_impl or hip_adam
         self.step_count = 0
-        self.params = torch.zeros((2, self.V_pad, self.d), dtype=torch.float32, device=self.device)
-        self.grads = torch.zeros_like(self.params)
-        n = self.params.numel()
-        self.shard_elems = n // self.world
-        self.m = torch.zeros(self.shard_elems, dtype=torch.float32, device=self.device)
+        n_slots = 3 if self.world > 1 else 2
+        self.params = torch.zeros((n_slots, self.V_pad, self.d), dtype=torch.float32,
+                                  device=self.device)
+        self.grads = torch.zeros((2, self.V_pad, self.d), dtype=torch.float32, device=self.device)
+        self.m = torch.zeros((2, self.S, self.d), dtype=torch.float32, device=self.device)
         self.v = torch.zeros_like(self.m)
         self.grad_shard = torch.empty_like(self.m) if self.world > 1 else None
+        self._cur_in = 0
+        self._next_in = 0
+        self._ag = []          # pending all-gathers (overlapped form)
+        self._cuda = self.device.type == 'cuda'
+        self._side = torch.cuda.Stream(self.device) if (self._cuda and self.world > 1) else None
         if init_seed is not None:
             self.xavier_(init_seed)
 
     # ---- views -------------------------------------------------------------------------------
     @property
     def w_in(self) -> torch.Tensor:
-        return self.params[0, :self.V]
+        return self.params[self._cur_in, :self.V]
 
     @property
     def w_out(self) -> torch.Tensor:
@@ -86,38 +107,96 @@ class ShardedTables:
         return self.grads[1, :self.V]
 
     def shard_range(self):
-        """[start, end) of this rank's slice in the flat [2*V_pad*d] parameter buffer."""
-        return self.rank * self.shard_elems, (self.rank + 1) * self.shard_elems
+        """[start, end) rows of this rank's node range (the same in both tables)."""
+        return self.rank * self.S, (self.rank + 1) * self.S
 
     def xavier_(self, seed: int) -> None:
         """W2VBase init (model.py:26-27): U(-a, a), a = sqrt(6/(V+d)); identical on all ranks."""
         g = torch.Generator(device='cpu').manual_seed(int(seed))
         a = math.sqrt(6.0 / (self.V + self.d))
-        for t in range(2):
+        for t in (self._cur_in, 1):
             w = torch.rand((self.V, self.d), generator=g) * (2 * a) - a
             self.params[t, :self.V].copy_(w)
 
     def load_(self, w_in: torch.Tensor, w_out: torch.Tensor) -> None:
-        self.params[0, :self.V].copy_(w_in)
+        self.params[self._cur_in, :self.V].copy_(w_in)
         self.params[1, :self.V].copy_(w_out)
 
-    # ---- optimizer step ---------------------------------------------------------------------------
-    def step(self) -> None:
-        """Exchange gradients, update this rank's slice, gather parameters; grads end zeroed."""
-        self.step_count += 1
-        flat_p = self.params.view(-1)
-        flat_g = self.grads.view(-1)
-        if self.world == 1:
-            self.adam_impl(flat_p, flat_g, self.m, self.v, self.step_count, self.lr, self.betas,
-                           self.eps, self.weight_decay, True)
-            return
-        dist.reduce_scatter_tensor(self.grad_shard, flat_g, op=dist.ReduceOp.SUM,
-                                   group=self.group)
-        flat_g.zero_()
+    # ---- one table's exchange -------------------------------------------------------------------
+    def _adam(self, p, g, t: int, zero_grad: bool) -> None:
+        self.adam_impl(p, g, self.m[t].view(-1), self.v[t].view(-1), self.step_count, self.lr,
+                       self.betas, self.eps, self.weight_decay, zero_grad)
+
+    def _exchange(self, t: int, src_slot: int, dst_slot: int, async_op: bool):
+        """reduce-scatter grads[t] -> Adam on own rows of params[dst_slot] (starting from
+        params[src_slot]) -> all-gather into params[dst_slot]; grads[t] ends zeroed.
+        Returns the all-gather work handle when async_op."""
         a, b = self.shard_range()
-        p_shard = flat_p[a:b]
-        self.adam_impl(p_shard, self.grad_shard, self.m, self.v, self.step_count, self.lr,
-                       self.betas, self.eps, self.weight_decay, False)
-        backend = dist.get_backend(self.group)
-        src = p_shard if backend == 'nccl' else p_shard.clone()  # RCCL all-gather is in-place safe
-        dist.all_gather_into_tensor(flat_p, src, group=self.group)
+        w = dist.reduce_scatter_tensor(self.grad_shard[t].view(-1), self.grads[t].view(-1),
+                                       op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=async_op)
+        if async_op:
+            w.wait()            # the current (side) stream waits for the reduce-scatter
+        self.grads[t].zero_()
+        own = self.params[dst_slot, a:b]
+        if src_slot != dst_slot:
+            own.copy_(self.params[src_slot, a:b])
+        self._adam(own.view(-1), self.grad_shard[t].view(-1), t, False)
+        nccl = dist.get_backend(self.group) == 'nccl'
+        src = own.view(-1) if nccl else own.reshape(-1).clone()   # RCCL all-gather is in-place safe
+        return dist.all_gather_into_tensor(self.params[dst_slot].view(-1), src, group=self.group,
+                                           async_op=async_op)
+
+    # ---- serial step ------------------------------------------------------------------------------
+    def step(self) -> None:
+        """Exchange gradients, update this rank's rows, gather parameters; grads end zeroed."""
+        self.sync()
+        self.step_count += 1
+        if self.world == 1:
+            self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
+                           self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
+                           self.weight_decay, True)
+            return
+        self._exchange(0, self._cur_in, self._cur_in, False)
+        self._exchange(1, 1, 1, False)
+
+    # ---- overlapped step --------------------------------------------------------------------------
+    def exchange_in(self) -> None:
+        """Call right after SGNS pass 1 is enqueued (g_in final): the in-table update starts on a
+        side stream while the output-table phase runs on the current stream."""
+        self.step_count += 1
+        if self.world == 1:
+            return                              # nothing to overlap: exchange_out does Adam
+        self._next_in = 2 - self._cur_in
+        if not self._cuda:
+            self._exchange(0, self._cur_in, self._next_in, False)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ev)
+            self._ag.append(self._exchange(0, self._cur_in, self._next_in, True))
+
+    def exchange_out(self) -> None:
+        """Call right after SGNS phase 2 is enqueued (g_out final)."""
+        if self.world == 1:
+            self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
+                           self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
+                           self.weight_decay, True)
+            return
+        if not self._cuda:
+            self._exchange(1, 1, 1, False)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ev)
+            self._ag.append(self._exchange(1, 1, 1, True))
+
+    def sync(self) -> None:
+        """The current stream waits for pending all-gathers; the new in table becomes current.
+        Call before the next SGNS pass 1 (and before reading the tables)."""
+        for w in self._ag:
+            w.wait()
+        self._ag = []
+        self._cur_in = self._next_in

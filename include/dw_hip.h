@@ -135,6 +135,20 @@ int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                   double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
                   void *stream);
 
+/* Two-phase form of dw_sgns_walks (same arguments, plus phase): phase 1 runs pass 1 — the
+ * centre-table gradient g_in, the loss sums and the output-row records in the workspace —
+ * and phase 2 sorts the records and accumulates g_out. A phase-2 call must follow the phase-1
+ * call with identical arguments on the same stream; between the two, g_in is final and may be
+ * read (the multi-GPU exchange starts its reduce-scatter there, overlapping phase 2). phase 0
+ * is dw_sgns_walks. In atomic mode (workspace NULL) phase 1 does everything. */
+int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
+                        int32_t walk_length, int32_t context_radius, int32_t neg_samples,
+                        int64_t vocab_size, int32_t dim, const float *w_in, const float *w_out,
+                        float *g_in, float *g_out, const int64_t *noise, uint64_t seed,
+                        uint64_t noise_offset, float grad_scale, double *loss_acc,
+                        int32_t *status, void *workspace, size_t workspace_bytes,
+                        void *stream);
+
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

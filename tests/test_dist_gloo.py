@@ -1,10 +1,13 @@
-"""The N>1 exchange (node-id-range sharded Adam: reduce-scatter -> Adam slice -> all-gather)
-with world_size 2 over gloo on the CPU.
+"""The N>1 exchange (node-id-range sharded Adam: reduce-scatter -> Adam on own rows ->
+all-gather, per table) with world_size 2 over gloo on the CPU.
 
 Two ranks each take half of the batch (DDP semantics: local gradient scaled by 1/M_global);
 after several steps their replicated tables must equal single-process training on the whole
-batch. The gradient and Adam math here is the oracle's (CPU); on the GPU the same
-ShardedTables object drives dw_sgns_walks + dw_adam_dense over RCCL (bench.py).
+batch. Both forms are checked: the serial ``step()`` and the overlapped protocol bench.py uses
+(``exchange_in`` after pass 1 -> output-table gradient computed from ``w_in`` -> ``exchange_out``
+-> ``sync``), where the in-table update must land in the second buffer so the output-table
+phase still sees the old in table. The gradient and Adam math here is the oracle's (CPU); on
+the GPU the same ShardedTables object drives dw_sgns_walks_phase + dw_adam_dense over RCCL.
 """
 import os
 import socket
@@ -45,26 +48,42 @@ def batches():
     return out
 
 
-def add_grads(tables, ins, tgt, noise, share):
+def grads(tables, ins, tgt, noise, share):
     _, gi, go = sgns_ref.sgns_grads_closed_form(tables.w_in.numpy(), tables.w_out.numpy(), ins,
                                                 tgt, noise)
-    tables.g_in.add_(torch.as_tensor(gi * share, dtype=torch.float32))
-    tables.g_out.add_(torch.as_tensor(go * share, dtype=torch.float32))
+    return (torch.as_tensor(gi * share, dtype=torch.float32),
+            torch.as_tensor(go * share, dtype=torch.float32))
 
 
-def _worker(rank, world, port, q):
+def train(t, rank, world, mode):
+    for ins, tgt, noise in batches():
+        half = len(ins) // world
+        sl = slice(rank * half, (rank + 1) * half)
+        gi, go = grads(t, ins[sl], tgt[sl], noise[sl], 1.0 / world)
+        if mode == 'serial':
+            t.g_in.add_(gi)
+            t.g_out.add_(go)
+            t.step()
+        else:
+            w_in_before = t.w_in.clone()
+            t.g_in.add_(gi)                      # pass 1: centre-table gradient final
+            t.exchange_in()
+            assert torch.equal(t.w_in, w_in_before)  # output-table phase sees the old in table
+            t.g_out.add_(go)                     # pass 2
+            t.exchange_out()
+            t.sync()
+        assert float(t.grads.abs().max()) == 0.0
+
+
+def _worker(rank, world, port, mode, q):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from shallow_encoders.word2vec.sharding import ShardedTables
     t = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
-    for ins, tgt, noise in batches():
-        half = len(ins) // world
-        sl = slice(rank * half, (rank + 1) * half)
-        add_grads(t, ins[sl], tgt[sl], noise[sl], 1.0 / world)
-        t.step()
-        assert float(t.grads.abs().max()) == 0.0
-    q.put((rank, t.params.numpy().copy(), t.shard_range(), t.m.numpy().copy()))
+    train(t, rank, world, mode)
+    q.put((rank, t.w_in.numpy().copy(), t.w_out.numpy().copy(), t.shard_range(),
+           t.m.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -78,26 +97,27 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_sharded_adam_world2_equals_single_process():
+@pytest.mark.parametrize('mode', ['serial', 'overlap'])
+def test_sharded_adam_world2_equals_single_process(mode):
     from shallow_encoders.word2vec.sharding import ShardedTables
     ref = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
     assert ref.world == 1
-    for ins, tgt, noise in batches():
-        add_grads(ref, ins, tgt, noise, 1.0)
-        ref.step()
+    train(ref, 0, 1, 'serial')
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, r0, m0), (_, p1, r1, m1) = res
-    np.testing.assert_array_equal(p0, p1)                 # replicas identical after all-gather
-    assert r0 == (0, p0.size // 2) and r1 == (p0.size // 2, p0.size)  # node-id-range slices
-    np.testing.assert_allclose(p0[:, :V], ref.params.numpy()[:, :V], rtol=1e-5, atol=1e-6)
-    full_m = ref.m.numpy()
-    np.testing.assert_allclose(np.concatenate([m0, m1]), full_m, rtol=1e-4, atol=1e-9)
+    (_, i0, o0, r0, m0), (_, i1, o1, r1, m1) = res
+    np.testing.assert_array_equal(i0, i1)                 # replicas identical after all-gather
+    np.testing.assert_array_equal(o0, o1)
+    assert r0 == (0, V // 2) and r1 == (V // 2, V)        # node-id-range rows of both tables
+    np.testing.assert_allclose(i0, ref.w_in.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(o0, ref.w_out.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np.concatenate([m0, m1], axis=1), ref.m.numpy(), rtol=1e-4,
+                               atol=1e-9)

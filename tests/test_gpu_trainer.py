@@ -46,7 +46,7 @@ def _reference_run(f, manual_grads=True):
             out['loss'].backward()
         opt.step()
         opt.zero_grad()
-        losses.append(float(out['loss']))
+        losses.append(float(out['loss'].detach()))
     return model, losses
 
 
