@@ -181,6 +181,10 @@ class ModelAnalysisConfig:
         default_factory=ModelSemanticsTestAnalysisConfig)
 
 
+DEFAULT_SPLIT_ALGORITHM = {'_target_': 'shallow_encoders.split.TrainTestRatioSplit',
+                           'random_state': 42, 'train_ratio': 0.5, 'stratify': False}
+
+
 @dataclass
 class GraphDownstreamNodeClassificationConfig:
     enable: bool = True
@@ -188,6 +192,14 @@ class GraphDownstreamNodeClassificationConfig:
     visualize: bool = True
     split_algorithm: Optional[dict] = None
     classifier_params: Optional[dict] = None
+
+    def instantiate_split_algorithm(self):
+        """The configured split (reference: config_parser/core.py:217-232). Without one, the
+        reference's intended default (train_ratio 0.5, seed 42, not stratified) is used; the
+        reference records that default but then instantiates the missing entry."""
+        if self.split_algorithm is None:
+            self.split_algorithm = dict(DEFAULT_SPLIT_ALGORITHM)
+        return instantiate(self.split_algorithm)
 
 
 @dataclass

@@ -1,6 +1,6 @@
 """Generate the golden fixtures from the REFERENCE itself (run in the build container only).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [downstream]
 
 Imports the importable pieces of /root/reference: the walkers
 (graph/random_walk_generator.py), the datasets (graph/datasets.py), SkipGram (word2vec/model.py),
@@ -280,7 +280,47 @@ def trajectory_fixture(name, seed, walks_per_node, walk_length, d, R, K, lr, bat
          w_out=model._output_embedding.weight.detach().numpy())
 
 
+SPLIT_CASES = [  # (class name, kwargs) of the reference's split algorithms
+    ('TrainTestRatioSplit', {'train_ratio': 0.5}),
+    ('TrainTestRatioSplit', {'train_ratio': 0.7, 'stratify': True}),
+    ('TrainTestRatioSplit', {'train_ratio': 0.5, 'test_all': True}),
+    ('TrainValTestRatioSplit', {'train_ratio': 0.6, 'val_ratio': 0.8}),
+    ('TrainValTestRatioSplit', {'train_ratio': 0.5, 'val_ratio': 0.7, 'stratify': True}),
+    ('TrainValTestStratifiedNSamplesSplit', {'train_samples': 3, 'val_samples': 2,
+                                             'test_samples': 4}),
+    ('TrainValTestStratifiedNSamplesSplit', {'train_samples': 3, 'val_samples': 2}),
+]
+SPLIT_SEEDS = (0, 7, 42)
+
+
+def downstream_fixture(name):
+    """Outputs of the reference's split algorithms (shallow_encoders/split/core.py) and edge
+    operators (shallow_encoders/graph/edge_operators.py) on fixed inputs."""
+    import shallow_encoders.split as ref_split
+    from shallow_encoders.graph import edge_operators as ref_ops
+    X = np.arange(40 * 3, dtype=np.float64).reshape(40, 3)
+    y = np.asarray([0] * 14 + [1] * 13 + [2] * 13, dtype=np.float32)
+    y = y[np.random.default_rng(3).permutation(40)]
+    arrays = {'X': X, 'y': y}
+    for i, (cls, kw) in enumerate(SPLIT_CASES):
+        for seed in SPLIT_SEEDS:
+            algo = getattr(ref_split, cls)(**kw)
+            algo.random_state = seed
+            for k, v in algo(X, y).items():
+                arrays[f'split{i}_seed{seed}_{k}'] = v
+    rng = np.random.default_rng(9)
+    a, b = rng.normal(size=(6, 5)), rng.normal(size=(6, 5))
+    arrays['op_lhs'], arrays['op_rhs'] = a, b
+    for op in ('average', 'hadamard', 'weighted_l1', 'weighted_l2'):
+        arrays[f'op_{op}'] = np.stack([ref_ops.edge_operator_factory(op)(a[j], b[j])
+                                       for j in range(6)])
+    save(name, **arrays)
+
+
 def main():
+    if sys.argv[1:] == ['downstream']:
+        downstream_fixture('downstream_split_ops.npz')
+        return
     info = {'python': sys.version, 'torch': torch.__version__, 'networkx': nx.__version__}
     # F1/F4 karate node2vec (configs/sge_sg_karate_club.yaml walker) and a strongly biased p,q
     dataset_fixture('walks_karate_node2vec_p1_q0.5.npz', ref_ds.KarateClubDataset, seed=11,
@@ -313,6 +353,8 @@ def main():
     # F7 trajectory with StepLR
     trajectory_fixture('traj_karate_node2vec.npz', seed=31, walks_per_node=8, walk_length=10,
                        d=2, R=2, K=1, lr=0.1, batch_walks=64, epochs=3, step_size=1, gamma=0.5)
+    # §8f 3: downstream split algorithms + edge operators
+    downstream_fixture('downstream_split_ops.npz')
     with open(os.path.join(HERE, 'golden_info.json'), 'w') as f:
         json.dump(info, f, indent=2)
 

@@ -105,3 +105,22 @@ def test_training_reduces_loss_on_triplets(tmp_path, hip_device):
     more = train_tool.main(['--config-name', 'sge_sg_graph_triplets', f'path.output_dir={out}',
                             f'output_dir={out}', 'train.max_epochs=5'])
     assert more['train-epoch/loss'] < first['train-epoch/loss'] + 0.05
+
+
+def test_downstream_quality_karate(tmp_path, hip_device):
+    """Train karate with the reference config (node2vec p=1 q=0.5, d=2, 50 epochs) and run the
+    downstream tool: README.md:276-281 reports 98.06% node / 69.52% edge accuracy (means over
+    100 / 1000 experiments) for the reference's own training."""
+    from tools import graph_model_downstream_classification as downstream
+    from tools import train as train_tool
+    out = str(tmp_path / 'runs')
+    base = [f'path.output_dir={out}', f'output_dir={out}']
+    train_tool.main(['--config-name', 'sge_sg_karate_club'] + base)
+    res = downstream.main(['--config-name', 'sge_sg_karate_club'] + base + [
+        'downstream.node_classification.n_experiments=20',
+        'downstream.edge_classification.n_experiments=100'])
+    print(res)
+    assert res['node_accuracy'] >= 0.85, res
+    assert res['edge_accuracy'] >= 0.55, res
+    assert os.path.exists(os.path.join(out, 'graph_karate_club', 'SG_exp01_baseline', 'analysis',
+                                       'downstream-node-classification.jpg'))
