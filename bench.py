@@ -126,10 +126,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    # rehearsal knobs (not for measurements): DW_BENCH_BACKEND=gloo and DW_BENCH_ONE_DEVICE=1
+    # run N ranks on one GPU to exercise the multi-rank flow on a 1-GPU box
+    backend = os.environ.get('DW_BENCH_BACKEND', 'nccl')
+    if os.environ.get('DW_BENCH_ONE_DEVICE') == '1':
+        local_rank = 0
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local_rank)
     torch.cuda.set_device(dev)
 
@@ -274,14 +282,16 @@ def main():
                          f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU; '
                          f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
-            'parallelism': f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather)',
+            'parallelism': (f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather, '
+                            f'in-table exchange overlapped)' if backend == 'nccl' else
+                            f'REHEARSAL dp{world} over {backend}, all ranks on one device'),
         },
         'walks_per_s': walk_stats.get('deepwalk'),
         'walks_per_s_node2vec_p0.25_q4': walk_stats.get('node2vec'),
         'kernel_ms': kern_ms,
         'mean_loss': mean_loss,
         'roofline': {
-            'kernel': ('dw_sgns_walks = k_sgns_g16 + hipcub radix sort + k_rec_gather'
+            'kernel': ('dw_sgns_walks = k_sgns_g16 + rocprim onesweep radix sort + k_rec_gather'
                        if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
