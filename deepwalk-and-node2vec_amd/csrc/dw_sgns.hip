@@ -94,11 +94,32 @@ __device__ void flush_loss(double *acc, float p, float n, float r, float pr) {
     }
 }
 
+// Pooled input vector of row b for lane element e: the mean of P input rows (P = 1: the
+// centre row itself) — torch.mean over dim 1 (model.py:104), a sequential sum then / P.
+__device__ __forceinline__ float pooled(const int64_t *__restrict__ inputs, int64_t b, int32_t P,
+                                        const float *__restrict__ w_in, int32_t d, int e) {
+    if (P == 1) return w_in[inputs[b] * d + e];
+    float h = 0.f;
+    for (int p = 0; p < P; ++p) h += w_in[inputs[b * P + p] * d + e];
+    return h / static_cast<float>(P);
+}
+
+__device__ __forceinline__ bool inputs_ok(const int64_t *__restrict__ inputs, int64_t b,
+                                          int32_t P, int64_t V) {
+    bool ok = true;
+    for (int p = 0; p < P; ++p) {
+        const int64_t c = inputs[b * P + p];
+        ok = ok && c >= 0 && c < V;
+    }
+    return ok;
+}
+
 struct SgnsArgs {
     // source of centres / contexts
     const int32_t *walks;     // walks mode
     int32_t L, R;
-    const int64_t *inputs;    // pairs mode
+    const int64_t *inputs;    // pairs mode: [batch, n_in] (n_in > 1: mean-pooled, CBOW)
+    int32_t n_in;
     const int64_t *targets;
     int64_t batch;            // number of centres B'
     int32_t C;                // contexts per centre
@@ -178,9 +199,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
             walk = a.walks + w * a.L;
             cid = walk[i];
         } else {
-            cid = a.inputs[b];
+            cid = a.inputs[b * a.n_in];
         }
-        const bool centre_ok = cid >= 0 && cid < a.V;
+        const bool pool = !FROM_WALKS && a.n_in > 1;  // CBOW: mean of n_in input rows
+        const bool centre_ok =
+            pool ? inputs_ok(a.inputs, b, a.n_in, a.V) : (cid >= 0 && cid < a.V);
         if (!centre_ok) {
             if (lane == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
             if (RECORDS) {  // keep the record array well-formed: zero-coefficient records
@@ -195,7 +218,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
         const float *crow = a.w_in + cid * a.d + lane;
 #pragma unroll
         for (int m = 0; m < VPL; ++m) {
-            c[m] = live[m] ? crow[WAVE * m] : 0.f;
+            c[m] = !live[m] ? 0.f
+                   : pool   ? pooled(a.inputs, b, a.n_in, a.w_in, a.d, lane + WAVE * m)
+                            : crow[WAVE * m];
             gc[m] = 0.f;
         }
         for (int g0 = 0; g0 < n_rows; g0 += WAVE) {
@@ -270,10 +295,19 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                 a.rec_val[b * n_rows + t] = pack_record(my_ok ? my_coef : 0.f, cid);
             }
         }
-        float *gcrow = a.g_in + cid * a.d + lane;
+        if (pool) {  // mean backward: each pooled input row receives gc / n_in
+            for (int p = 0; p < a.n_in; ++p) {
+                float *grow = a.g_in + a.inputs[b * a.n_in + p] * a.d + lane;
 #pragma unroll
-        for (int m = 0; m < VPL; ++m)
-            if (live[m]) atomicAdd(gcrow + WAVE * m, gc[m]);
+                for (int m = 0; m < VPL; ++m)
+                    if (live[m]) atomicAdd(grow + WAVE * m, gc[m] / static_cast<float>(a.n_in));
+            }
+        } else {
+            float *gcrow = a.g_in + cid * a.d + lane;
+#pragma unroll
+            for (int m = 0; m < VPL; ++m)
+                if (live[m]) atomicAdd(gcrow + WAVE * m, gc[m]);
+        }
     }
 
     // loss partials: wave-reduce the per-lane sums, one double atomic per wave and value
@@ -815,22 +849,25 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
 }
 
 // ---- SkipGram.forward logits and its backward (autograd path of the reference API) ----------
+// logits[b, n] = <mean_p w_in[inputs[b, p]], w_out[outputs[b, n]]> (SkipGram: P = 1; CBOW:
+// P = the context width). One wave per row b.
 __global__ void __launch_bounds__(256)
-    k_logits(const int64_t *__restrict__ inputs, const int64_t *__restrict__ outputs, int64_t B,
-             int32_t N, int64_t V, int32_t d, const float *__restrict__ w_in,
+    k_logits(const int64_t *__restrict__ inputs, int32_t P, const int64_t *__restrict__ outputs,
+             int64_t B, int32_t N, int64_t V, int32_t d, const float *__restrict__ w_in,
              const float *__restrict__ w_out, int32_t proba, float *__restrict__ logits,
              int32_t *status) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
     for (int64_t b = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; b < B;
          b += n_waves) {
-        const int64_t c = inputs[b];
+        const bool in_ok = inputs_ok(inputs, b, P, V);
         for (int n = 0; n < N; ++n) {
             const int64_t o = outputs[b * N + n];
             float s = 0.f;
-            const bool ok = c >= 0 && c < V && o >= 0 && o < V;
+            const bool ok = in_ok && o >= 0 && o < V;
             if (ok)
-                for (int e = lane; e < d; e += WAVE) s += w_in[c * d + e] * w_out[o * d + e];
+                for (int e = lane; e < d; e += WAVE)
+                    s += pooled(inputs, b, P, w_in, d, e) * w_out[o * d + e];
             s = dw::wave_sum(s);
             if (lane == 0) {
                 if (!ok) dw::status_or(status, DW_S_BAD_INDEX);
@@ -841,41 +878,100 @@ __global__ void __launch_bounds__(256)
 }
 
 __global__ void __launch_bounds__(256)
-    k_logits_bwd(const int64_t *__restrict__ inputs, const int64_t *__restrict__ outputs,
-                 int64_t B, int32_t N, int64_t V, int32_t d, const float *__restrict__ w_in,
-                 const float *__restrict__ w_out, const float *__restrict__ dl,
-                 float *__restrict__ g_in, float *__restrict__ g_out, int32_t *status) {
+    k_logits_bwd(const int64_t *__restrict__ inputs, int32_t P,
+                 const int64_t *__restrict__ outputs, int64_t B, int32_t N, int64_t V, int32_t d,
+                 const float *__restrict__ w_in, const float *__restrict__ w_out,
+                 const float *__restrict__ dl, float *__restrict__ g_in,
+                 float *__restrict__ g_out, int32_t *status) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
     for (int64_t b = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; b < B;
          b += n_waves) {
-        const int64_t c = inputs[b];
-        if (c < 0 || c >= V) {
+        if (!inputs_ok(inputs, b, P, V)) {
             if (lane == 0) dw::status_or(status, DW_S_BAD_INDEX);
             continue;
         }
         for (int e0 = 0; e0 < d; e0 += WAVE) {
             const int e = e0 + lane;
-            float gc = 0.f;
-            const float ce = e < d ? w_in[c * d + e] : 0.f;
+            float gh = 0.f;
+            const float he = e < d ? pooled(inputs, b, P, w_in, d, e) : 0.f;
             for (int n = 0; n < N; ++n) {
                 const int64_t o = outputs[b * N + n];
                 if (o < 0 || o >= V) continue;
                 const float g = dl[b * N + n];
                 if (e < d) {
-                    gc += g * w_out[o * d + e];
-                    atomicAdd(g_out + o * d + e, g * ce);
+                    gh += g * w_out[o * d + e];
+                    atomicAdd(g_out + o * d + e, g * he);
                 }
             }
-            if (e < d) atomicAdd(g_in + c * d + e, gc);
+            if (e < d) {  // mean backward: every pooled input row receives gh / P
+                const float gi = P == 1 ? gh : gh / static_cast<float>(P);
+                for (int p = 0; p < P; ++p) atomicAdd(g_in + inputs[b * P + p] * d + e, gi);
+            }
         }
     }
 }
+
+// ---- max_norm renormalisation (nn.Embedding(max_norm=...), torch embedding_renorm_) ----------
+// The referenced ids are sorted (duplicates adjacent) so each distinct row is renormalised once:
+// norm = ||row||_2 (float); if norm > max_norm: row *= float(max_norm / (norm + 1e-7)) with the
+// ratio in double, as the reference's CPU kernel computes it.
+__global__ void __launch_bounds__(256)
+    k_renorm_keys(const int64_t *__restrict__ ids, int64_t n, int64_t V,
+                  uint32_t *__restrict__ keys, int32_t *status) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t id = ids[i];
+    const bool ok = id >= 0 && id < V;
+    if (!ok) dw::status_or(status, DW_S_BAD_INDEX);
+    keys[i] = static_cast<uint32_t>(ok ? id : V);  // V = "skip"
+}
+
+__global__ void __launch_bounds__(256)
+    k_renorm_rows(const uint32_t *__restrict__ keys, int64_t n, int64_t V, float *__restrict__ w,
+                  int32_t d, double max_norm) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+    for (int64_t i = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; i < n;
+         i += n_waves) {
+        const uint32_t k = keys[i];
+        if (k >= V || (i > 0 && keys[i - 1] == k)) continue;
+        float *row = w + static_cast<int64_t>(k) * d;
+        float ss = 0.f;
+        for (int e = lane; e < d; e += WAVE) ss += row[e] * row[e];
+        const float norm = sqrtf(dw::wave_sum(ss));
+        if (static_cast<double>(norm) > max_norm) {
+            const float scale = static_cast<float>(max_norm / (static_cast<double>(norm) + 1e-7));
+            for (int e = lane; e < d; e += WAVE) row[e] *= scale;
+        }
+    }
+}
+
+// Device negatives exactly as the fused kernels draw them (noise_id): ids[(b*C + j)*K + k].
+__global__ void __launch_bounds__(256)
+    k_noise_fill(int64_t batch, int32_t C, int32_t K, int64_t V, uint32_t k0, uint32_t k1,
+                 uint64_t noise_offset, int64_t *__restrict__ out) {
+    const int64_t n = batch * C * K;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t b = i / (static_cast<int64_t>(C) * K);
+        const int slot = static_cast<int>(i - b * C * K);  // j*K + k
+        const uint64_t g = noise_offset + static_cast<uint64_t>(b);
+        const dw::U4 r = dw::philox(
+            dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
+                   static_cast<uint32_t>(slot), TAG_SGNS},
+            k0, k1);
+        out[i] = static_cast<int64_t>(dw::bounded64(r.x, r.y, static_cast<uint64_t>(V)));
+    }
+}
+
+using RenormSortConfig = RecordSortConfig;
 
 SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const float *w_out,
                    float *g_in, float *g_out, const int64_t *noise, uint64_t seed,
                    uint64_t noise_offset, float grad_scale, double *loss_acc, int32_t *status) {
     SgnsArgs a{};
+    a.n_in = 1;
     a.K = K;
     a.V = V;
     a.d = dim;
@@ -1006,38 +1102,146 @@ int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, 
     return launch_sgns<false>(a, workspace, workspace_bytes, 0, dw::as_stream(stream));
 }
 
+int dw_sgns_pooled_pairs(const int64_t *inputs, int32_t n_in, const int64_t *targets,
+                         int64_t batch, int32_t n_ctx, int32_t neg_samples, int64_t vocab_size,
+                         int32_t dim, const float *w_in, const float *w_out, float *g_in,
+                         float *g_out, const int64_t *noise, uint64_t seed,
+                         uint64_t noise_offset, float grad_scale, double *loss_acc,
+                         int32_t *status, void *stream) {
+    DW_REQUIRE(n_in >= 1 && n_ctx >= 1 && neg_samples >= 0 && dim >= 1 && vocab_size >= 1 &&
+                   batch >= 0,
+               "dw_sgns_pooled_pairs: bad sizes");
+    DW_REQUIRE(inputs && targets && w_in && w_out && g_in && g_out && status,
+               "dw_sgns_pooled_pairs: null pointer");
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out, g_in, g_out, noise, seed,
+                           noise_offset, grad_scale, loss_acc, status);
+    a.inputs = inputs;
+    a.n_in = n_in;
+    a.targets = targets;
+    a.batch = batch;
+    a.C = n_ctx;
+    return launch_sgns<false>(a, nullptr, 0, 0, dw::as_stream(stream));  // atomic mode
+}
+
+int dw_sgns_noise(int64_t batch, int32_t n_ctx, int32_t neg_samples, int64_t vocab_size,
+                  uint64_t seed, uint64_t noise_offset, int64_t *noise, void *stream) {
+    DW_REQUIRE(batch >= 0 && n_ctx >= 0 && neg_samples >= 0 && vocab_size >= 1,
+               "dw_sgns_noise: bad sizes");
+    const int64_t n = batch * n_ctx * neg_samples;
+    if (n == 0) return DW_OK;
+    DW_REQUIRE(noise, "dw_sgns_noise: null pointer");
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_noise_fill, dim3((unsigned)blocks), dim3(256), 0,
+                       dw::as_stream(stream), batch, n_ctx, neg_samples, vocab_size,
+                       static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32),
+                       noise_offset, noise);
+    DW_LAUNCH_CHECK("dw_sgns_noise");
+    return DW_OK;
+}
+
+int dw_embedding_renorm_workspace_bytes(int64_t n_ids, int64_t vocab_size, size_t *bytes) {
+    DW_REQUIRE(bytes && n_ids >= 0 && vocab_size >= 1 && vocab_size < 0x7FFFFFFF,
+               "dw_embedding_renorm_workspace_bytes: bad arguments");
+    size_t tmp = 0;
+    rocprim::double_buffer<uint32_t> kb(nullptr, nullptr);
+    hipError_t e = rocprim::radix_sort_keys<RenormSortConfig>(
+        nullptr, tmp, kb, static_cast<uint32_t>(n_ids > 0 ? n_ids : 1), 0,
+        end_bit_for(vocab_size + 1), nullptr);
+    if (e != hipSuccess) {
+        dw::set_error("dw_embedding_renorm: sort size query failed: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    *bytes = 2 * align256(static_cast<size_t>(n_ids) * 4) + align256(tmp);
+    return DW_OK;
+}
+
+int dw_embedding_renorm(float *weight, int64_t vocab_size, int32_t dim, const int64_t *ids,
+                        int64_t n_ids, double max_norm, void *workspace, size_t workspace_bytes,
+                        int32_t *status, void *stream) {
+    DW_REQUIRE(dim >= 1 && vocab_size >= 1 && vocab_size < 0x7FFFFFFF && n_ids >= 0,
+               "dw_embedding_renorm: bad sizes");
+    if (n_ids == 0) return DW_OK;
+    DW_REQUIRE(weight && ids && workspace && status, "dw_embedding_renorm: null pointer");
+    DW_REQUIRE(n_ids < 0x7FFFFFFF, "dw_embedding_renorm: too many ids");
+    size_t need = 0;
+    int rc = dw_embedding_renorm_workspace_bytes(n_ids, vocab_size, &need);
+    if (rc != DW_OK) return rc;
+    DW_REQUIRE(workspace_bytes >= need, "dw_embedding_renorm: workspace too small (%zu < %zu)",
+               workspace_bytes, need);
+    hipStream_t st = dw::as_stream(stream);
+    char *p = static_cast<char *>(workspace);
+    const size_t kbytes = align256(static_cast<size_t>(n_ids) * 4);
+    uint32_t *k0 = reinterpret_cast<uint32_t *>(p), *k1 = reinterpret_cast<uint32_t *>(p + kbytes);
+    hipLaunchKernelGGL(k_renorm_keys, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, st,
+                       ids, n_ids, vocab_size, k0, status);
+    DW_LAUNCH_CHECK("dw_embedding_renorm/keys");
+    rocprim::double_buffer<uint32_t> kb(k0, k1);
+    size_t tmp = need - 2 * kbytes;
+    hipError_t e = rocprim::radix_sort_keys<RenormSortConfig>(
+        p + 2 * kbytes, tmp, kb, static_cast<uint32_t>(n_ids), 0, end_bit_for(vocab_size + 1),
+        st);
+    if (e != hipSuccess) {
+        dw::set_error("dw_embedding_renorm: sort failed: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    int64_t blocks = (n_ids + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_renorm_rows, dim3((unsigned)blocks), dim3(256), 0, st, kb.current(),
+                       n_ids, vocab_size, weight, dim, max_norm);
+    DW_LAUNCH_CHECK("dw_embedding_renorm/rows");
+    return DW_OK;
+}
+
+int dw_pooled_logits(const int64_t *inputs, int32_t n_in, const int64_t *outputs,
+                     int64_t batch, int32_t n_out, int64_t vocab_size, int32_t dim,
+                     const float *w_in, const float *w_out, int32_t proba, float *logits,
+                     int32_t *status, void *stream) {
+    DW_REQUIRE(batch >= 0 && n_out >= 0 && n_in >= 1 && dim >= 1, "dw_pooled_logits: bad sizes");
+    if (batch == 0 || n_out == 0) return DW_OK;
+    DW_REQUIRE(inputs && outputs && w_in && w_out && logits && status,
+               "dw_pooled_logits: null pointer");
+    int64_t blocks = (batch + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_logits, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       inputs, n_in, outputs, batch, n_out, vocab_size, dim, w_in, w_out, proba,
+                       logits, status);
+    DW_LAUNCH_CHECK("dw_pooled_logits");
+    return DW_OK;
+}
+
+int dw_pooled_logits_backward(const int64_t *inputs, int32_t n_in, const int64_t *outputs,
+                              int64_t batch, int32_t n_out, int64_t vocab_size, int32_t dim,
+                              const float *w_in, const float *w_out, const float *dlogits,
+                              float *g_in, float *g_out, int32_t *status, void *stream) {
+    DW_REQUIRE(batch >= 0 && n_out >= 0 && n_in >= 1 && dim >= 1,
+               "dw_pooled_logits_backward: bad sizes");
+    if (batch == 0 || n_out == 0) return DW_OK;
+    DW_REQUIRE(inputs && outputs && w_in && w_out && dlogits && g_in && g_out && status,
+               "dw_pooled_logits_backward: null pointer");
+    int64_t blocks = (batch + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_logits_bwd, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       inputs, n_in, outputs, batch, n_out, vocab_size, dim, w_in, w_out, dlogits,
+                       g_in, g_out, status);
+    DW_LAUNCH_CHECK("dw_pooled_logits_backward");
+    return DW_OK;
+}
+
 int dw_skipgram_logits(const int64_t *inputs, const int64_t *outputs, int64_t batch,
                        int32_t n_out, int64_t vocab_size, int32_t dim, const float *w_in,
                        const float *w_out, int32_t proba, float *logits, int32_t *status,
                        void *stream) {
-    DW_REQUIRE(batch >= 0 && n_out >= 0 && dim >= 1, "dw_skipgram_logits: bad sizes");
-    if (batch == 0 || n_out == 0) return DW_OK;
-    DW_REQUIRE(inputs && outputs && w_in && w_out && logits && status,
-               "dw_skipgram_logits: null pointer");
-    int64_t blocks = (batch + 3) / 4;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_logits, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
-                       inputs, outputs, batch, n_out, vocab_size, dim, w_in, w_out, proba, logits,
-                       status);
-    DW_LAUNCH_CHECK("dw_skipgram_logits");
-    return DW_OK;
+    return dw_pooled_logits(inputs, 1, outputs, batch, n_out, vocab_size, dim, w_in, w_out, proba,
+                            logits, status, stream);
 }
 
 int dw_skipgram_logits_backward(const int64_t *inputs, const int64_t *outputs, int64_t batch,
                                 int32_t n_out, int64_t vocab_size, int32_t dim,
                                 const float *w_in, const float *w_out, const float *dlogits,
                                 float *g_in, float *g_out, int32_t *status, void *stream) {
-    DW_REQUIRE(batch >= 0 && n_out >= 0 && dim >= 1, "dw_skipgram_logits_backward: bad sizes");
-    if (batch == 0 || n_out == 0) return DW_OK;
-    DW_REQUIRE(inputs && outputs && w_in && w_out && dlogits && g_in && g_out && status,
-               "dw_skipgram_logits_backward: null pointer");
-    int64_t blocks = (batch + 3) / 4;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_logits_bwd, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
-                       inputs, outputs, batch, n_out, vocab_size, dim, w_in, w_out, dlogits, g_in,
-                       g_out, status);
-    DW_LAUNCH_CHECK("dw_skipgram_logits_backward");
-    return DW_OK;
+    return dw_pooled_logits_backward(inputs, 1, outputs, batch, n_out, vocab_size, dim, w_in,
+                                     w_out, dlogits, g_in, g_out, status, stream);
 }
 
 }  // extern "C"

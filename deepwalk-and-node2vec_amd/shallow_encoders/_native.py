@@ -62,6 +62,16 @@ SIGNATURES = {
     'dw_sgns_pairs': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),
+    'dw_sgns_pooled_pairs': (ctypes.c_int, [_p, _i32, _p, _i64, _i32, _i32, _i64, _i32, _p, _p,
+                                            _p, _p, _p, _u64, _u64, _f32, _p, _p, _p]),
+    'dw_sgns_noise': (ctypes.c_int, [_i64, _i32, _i32, _i64, _u64, _u64, _p, _p]),
+    'dw_embedding_renorm_workspace_bytes': (ctypes.c_int, [_i64, _i64, _szp]),
+    'dw_embedding_renorm': (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _f64, _p, ctypes.c_size_t,
+                                           _p, _p]),
+    'dw_pooled_logits': (ctypes.c_int, [_p, _i32, _p, _i64, _i32, _i64, _i32, _p, _p, _i32, _p,
+                                        _p, _p]),
+    'dw_pooled_logits_backward': (ctypes.c_int, [_p, _i32, _p, _i64, _i32, _i64, _i32, _p, _p,
+                                                 _p, _p, _p, _p, _p]),
     'dw_sgns_timing': (ctypes.c_int, [_i32]),
     'dw_sgns_phase_ms': (ctypes.c_int, [ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64)]),

@@ -20,6 +20,7 @@ import dataclasses
 import importlib
 import logging
 import os
+import re
 from dataclasses import dataclass, field
 from typing import Any, Dict, Iterator, List, Optional, Union
 
@@ -284,12 +285,31 @@ def _from_dict(cls, data):
     return cls(**kwargs)
 
 
+class _ConfigLoader(yaml.SafeLoader):
+    """SafeLoader whose floats follow YAML 1.2 / OmegaConf (the reference's loader): ``1e-3``
+    and ``1E+2`` are floats, not strings."""
+
+
+_ConfigLoader.add_implicit_resolver(
+    'tag:yaml.org,2002:float',
+    re.compile(r'''^(?:[-+]?(?:[0-9][0-9_]*)\.[0-9_]*(?:[eE][-+]?[0-9]+)?
+                |[-+]?(?:[0-9][0-9_]*)(?:[eE][-+]?[0-9]+)
+                |\.[0-9_]+(?:[eE][-+]?[0-9]+)?
+                |[-+]?\.(?:inf|Inf|INF)
+                |\.(?:nan|NaN|NAN))$''', re.X),
+    list('-+0123456789.'))
+
+
+def _yaml(text_or_stream):
+    return yaml.load(text_or_stream, Loader=_ConfigLoader)
+
+
 def _resolve_type(name: str):
     return globals().get(name, object)
 
 
 def _parse_value(text: str):
-    return yaml.safe_load(text)
+    return _yaml(text)
 
 
 def apply_overrides(cfg: Dict[str, Any], overrides: List[str]) -> Dict[str, Any]:
@@ -312,7 +332,7 @@ def load_config_dict(config_name: str, config_path: str = CONFIG_PATH,
     name = config_name if config_name.endswith('.yaml') else config_name + '.yaml'
     path = name if os.path.isabs(name) else os.path.join(config_path, name)
     with open(path, 'r', encoding='utf-8') as f:
-        raw = yaml.safe_load(f) or {}
+        raw = _yaml(f) or {}
     defaults = raw.pop('defaults', [])
     for d in defaults:
         if d not in ('w2v_config', '_self_'):

@@ -1,6 +1,8 @@
-"""Walk corpus -> training batches (reference: word2vec/dataloader/torch_dataset.py:23-322).
+"""Corpora -> training batches (reference: word2vec/dataloader/torch_dataset.py:23-322).
 
-Graph path only (the text corpora and lemmatisation are out of scope).
+``W2VDataset`` is the text corpus: sentences -> tokenize -> vocabulary in
+torchtext ``build_vocab_from_iterator`` order -> int64 id tensors per sentence. Lemmatisation
+needs nltk's WordNet, which this image lacks: ``lemmatize=True`` raises.
 
 ``GraphDataset`` builds the vocabulary straight from the graph — ``<unk>`` = 0, then node
 tokens in lexicographic order, the result of the reference's torchtext
@@ -17,7 +19,8 @@ Iteration:
 """
 import logging
 import re
-from typing import Dict, Iterator, List, Optional, Tuple
+from collections import Counter
+from typing import Dict, Iterable, Iterator, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -25,6 +28,7 @@ from torch.utils.data import IterableDataset
 
 from shallow_encoders.graph.datasets import RandomWalkDataset
 from shallow_encoders.graph.rng import skip_uniforms
+from shallow_encoders.word2vec.dataloader import w2v_datasets  # noqa: F401 (registers corpora)
 from shallow_encoders.word2vec.dataloader.registry import DATASET_REGISTRY
 
 logger = logging.getLogger('W2VDataset')
@@ -73,14 +77,88 @@ class Vocab:
         self._default = index
 
 
+def build_vocab(token_lists: Iterable[List[str]], specials: List[str], min_freq: int) -> Vocab:
+    """torchtext 0.15 ``build_vocab_from_iterator`` order (pinned version of the reference's
+    requirements; torchtext itself is absent here): specials first, then the other tokens with
+    frequency >= min_freq by descending frequency, ties alphabetical."""
+    counter: Counter = Counter()
+    for tokens in token_lists:
+        counter.update(tokens)
+    for sp in specials:
+        counter.pop(sp, None)
+    ordered = sorted(counter.items(), key=lambda kv: (-kv[1], kv[0]))
+    return Vocab(list(specials) + [t for t, f in ordered if f >= min_freq])
+
+
 class W2VDataset(IterableDataset):
-    """Text word2vec corpus — outside the graph hot path (OUT OF SCOPE)."""
+    """Text word2vec corpus (torch_dataset.py:61-213): iterates sentences as int64 id tensors.
+
+    Sentences shorter than 2R+1 tokens are dropped (not counted for the vocabulary filter
+    either way: the vocabulary pass reads every sentence, the iteration skips short ones).
+    """
 
     def __init__(self, dataset_name: str, context_radius: int = 5, min_word_frequency: int = 20,
                  lemmatize: bool = False, sort_by_frequency: bool = True,
                  additional_parameters: Optional[dict] = None):
-        raise NotImplementedError('text word2vec datasets are not part of the MI355X build; '
-                                  'use GraphDataset')
+        assert dataset_name in DATASET_REGISTRY, \
+            f'Dataset "{dataset_name}" is not supported. Supported: {list(DATASET_REGISTRY.keys())}'
+        if lemmatize:
+            raise NotImplementedError('lemmatize=True needs nltk WordNet (not in this image)')
+        self._context_radius = context_radius
+        self._dataset = DATASET_REGISTRY[dataset_name](**(additional_parameters or {}))
+        token_lists = list(self.get_iterator(apply_filter=False))
+        if sort_by_frequency:
+            vocab_source = token_lists
+        else:  # every token counted once: alphabetical order after the specials
+            vocab_source = [[t] for t in {t for tokens in token_lists for t in tokens}]
+        self._vocab = build_vocab(vocab_source, ['<unk>'], min_word_frequency)
+        logger.info(f'Vocabulary size: {len(self._vocab)}')
+        freq: Counter = Counter()
+        for tokens in token_lists:
+            freq.update(t for t in tokens if t in self._vocab)
+        self._word_frequency = dict(freq)
+
+    def sentence_pipeline(self, sentence: str, apply_filter: bool = True) -> Optional[List[str]]:
+        tokens = tokenize(sentence)
+        if apply_filter and len(tokens) < 2 * self._context_radius + 1:
+            return None
+        return tokens
+
+    def get_iterator(self, apply_filter: bool = True) -> Iterator[List[str]]:
+        for sentence in self._dataset:
+            tokens = self.sentence_pipeline(sentence, apply_filter=apply_filter)
+            if tokens is not None:
+                yield tokens
+
+    def get_n_most_frequent_words(self, n: int) -> Tuple[List[str], List[int]]:
+        """The n most frequent vocabulary words (ties in first-occurrence order) and their ids."""
+        words = [w for w, _ in sorted(self._word_frequency.items(), key=lambda x: x[1],
+                                      reverse=True)[:n]]
+        return words, [self._vocab[w] for w in words]
+
+    @property
+    def vocab(self) -> Vocab:
+        return self._vocab
+
+    @property
+    def context_radius(self) -> int:
+        return self._context_radius
+
+    @property
+    def has_labels(self) -> bool:
+        return False
+
+    @property
+    def labels(self) -> Dict[str, str]:
+        raise NotImplementedError('This function is not implemented!')
+
+    @property
+    def has_features(self) -> bool:
+        return False
+
+    def __iter__(self) -> Iterator[torch.Tensor]:
+        for tokens in self.get_iterator():
+            yield torch.tensor(self._vocab(tokens), dtype=torch.long)
 
 
 class GraphDataset(IterableDataset):

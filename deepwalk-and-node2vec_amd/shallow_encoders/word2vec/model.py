@@ -62,17 +62,19 @@ class W2VBase(nn.Module):
 
 
 class _Logits(torch.autograd.Function):
-    """logits[b, n] = <w_in[inputs[b]], w_out[outputs[b, n]]> on gfx950 (model.py:85-88)."""
+    """logits[b, n] = <mean_p w_in[inputs[b, p]], w_out[outputs[b, n]]> on gfx950
+    (SkipGram: P = 1, model.py:85-88; CBOW: P = context width, model.py:104-107)."""
 
     @staticmethod
     def forward(ctx, w_in, w_out, inputs, outputs):
         B, N = outputs.shape
+        P = inputs.shape[1]
         V, d = w_in.shape
         logits = torch.empty((B, N), dtype=torch.float32, device=w_in.device)
         status = torch.zeros(1, dtype=torch.int32, device=w_in.device)
         with torch.cuda.device(w_in.device):
-            _native.call('dw_skipgram_logits', _native.ptr(inputs), _native.ptr(outputs), B, N, V,
-                         d, _native.ptr(w_in.detach()), _native.ptr(w_out.detach()), 0,
+            _native.call('dw_pooled_logits', _native.ptr(inputs), P, _native.ptr(outputs), B, N,
+                         V, d, _native.ptr(w_in.detach()), _native.ptr(w_out.detach()), 0,
                          _native.ptr(logits), _native.ptr(status), _native.stream(w_in.device))
         ctx.save_for_backward(w_in, w_out, inputs, outputs, status)
         return logits
@@ -81,15 +83,36 @@ class _Logits(torch.autograd.Function):
     def backward(ctx, dlogits):
         w_in, w_out, inputs, outputs, status = ctx.saved_tensors
         B, N = outputs.shape
+        P = inputs.shape[1]
         V, d = w_in.shape
         g_in = torch.zeros_like(w_in)
         g_out = torch.zeros_like(w_out)
         with torch.cuda.device(w_in.device):
-            _native.call('dw_skipgram_logits_backward', _native.ptr(inputs), _native.ptr(outputs),
-                         B, N, V, d, _native.ptr(w_in.detach()), _native.ptr(w_out.detach()),
-                         _native.ptr(dlogits.contiguous().float()), _native.ptr(g_in),
-                         _native.ptr(g_out), _native.ptr(status), _native.stream(w_in.device))
+            _native.call('dw_pooled_logits_backward', _native.ptr(inputs), P,
+                         _native.ptr(outputs), B, N, V, d, _native.ptr(w_in.detach()),
+                         _native.ptr(w_out.detach()), _native.ptr(dlogits.contiguous().float()),
+                         _native.ptr(g_in), _native.ptr(g_out), _native.ptr(status),
+                         _native.stream(w_in.device))
         return g_in, g_out, None, None
+
+
+def _hip_logits(model: 'W2VBase', inputs: torch.Tensor, outputs: torch.Tensor,
+                proba: bool) -> torch.Tensor:
+    w_in, w_out = model.input_weight, model.output_weight
+    if w_in.device.type != 'cuda':
+        raise NotImplementedError(
+            f'{type(model).__name__}.forward runs on the HIP device only (move the model with '
+            '.cuda()); the CPU restatement of the reference lives in oracle/ for tests')
+    dev = w_in.device
+    B = outputs.shape[0]
+    inputs = inputs.to(dev, torch.long).reshape(B, -1).contiguous()
+    outputs = outputs.to(dev, torch.long).contiguous()
+    if model.max_norm is not None:   # nn.Embedding(max_norm): renormalise looked-up rows first
+        from shallow_encoders.word2vec.sgns import renorm_
+        renorm_(w_in, inputs, model.max_norm)
+        renorm_(w_out, outputs, model.max_norm)
+    scalars = _Logits.apply(w_in, w_out, inputs, outputs)
+    return torch.sigmoid(scalars) if proba else scalars
 
 
 class SkipGram(W2VBase):
@@ -97,27 +120,13 @@ class SkipGram(W2VBase):
 
     def forward(self, inputs: torch.Tensor, outputs: torch.Tensor, proba: bool = True) -> torch.Tensor:
         # inputs: (B, 1) centre ids; outputs: (B, N) context / noise ids
-        if self._input_embedding.weight.device.type != 'cuda':
-            raise NotImplementedError(
-                'SkipGram.forward runs on the HIP device only (move the model with .cuda()); '
-                'the CPU restatement of the reference lives in oracle/ for tests')
-        if self.max_norm is not None:
-            raise NotImplementedError('max_norm renormalisation is not supported on the HIP path '
-                                      '(every graph config uses max_norm: null)')
-        dev = self._input_embedding.weight.device
-        inputs = inputs.reshape(-1).to(dev, torch.long).contiguous()
-        outputs = outputs.to(dev, torch.long).contiguous()
-        scalars = _Logits.apply(self._input_embedding.weight, self._output_embedding.weight,
-                                inputs, outputs)
-        if proba:
-            scalars = torch.sigmoid(scalars)
-        return scalars
+        return _hip_logits(self, inputs.reshape(-1, 1), outputs, proba)
 
 
 class CBOW(W2VBase):
-    """Continuous bag of words (model.py:94-110) — text word2vec, outside the graph hot path.
-
-    Not implemented on the HIP path yet."""
+    """Continuous bag of words (model.py:94-110): the input vector is the MEAN of the input
+    rows (inputs (B, N), e.g. the 2R context words in 'cbow' collate mode), scored against
+    every output row (outputs (B, M)). With (B, 1) inputs it computes what SkipGram does."""
 
     def forward(self, inputs: torch.Tensor, outputs: torch.Tensor, proba: bool = True) -> torch.Tensor:
-        raise NotImplementedError('CBOW is not implemented on the MI355X path yet')
+        return _hip_logits(self, inputs, outputs, proba)

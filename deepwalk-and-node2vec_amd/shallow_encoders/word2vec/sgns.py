@@ -72,8 +72,8 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                     phase: int = 0) -> torch.Tensor:
     """Launch the fused SGNS kernel(s); returns the float64[4] loss accumulator.
 
-    Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B,1]) +
-    ``targets`` (int64 [B, C]). ``noise``: int64 [B', C, K] replayed negatives or None (device
+    Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B, 1];
+    [B, P] with P > 1 = CBOW, the mean of P input rows) + ``targets`` (int64 [B, C]). ``noise``: int64 [B', C, K] replayed negatives or None (device
     Philox keyed by (seed, noise_offset + centre)). ``grad_scale`` defaults to 1/(B'*C).
     ``scatter``: 'sorted' (records + radix sort + per-row gather, no output-table atomics) or
     'atomic' (float atomics straight into g_out).
@@ -118,13 +118,21 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                 raise ValueError('give walks, or inputs and targets')
             if phase != 0:
                 raise ValueError('the two-phase form takes walks')
-            inputs = inputs.reshape(-1)
             B, C = targets.shape
-            if inputs.numel() != B:
+            P = 1 if inputs.dim() == 1 else inputs.shape[1]
+            if inputs.numel() != B * P:
                 raise ValueError('inputs and targets disagree on the batch size')
             if noise is not None and noise.numel() != B * C * K:
                 raise ValueError('noise must have B * C * K entries')
             scale = 1.0 / max(B * C, 1) if grad_scale is None else grad_scale
+            if P > 1:
+                _native.call('dw_sgns_pooled_pairs', _native.ptr(inputs.contiguous()), P,
+                             _native.ptr(targets.contiguous()), B, C, K, V, d, _native.ptr(w_in),
+                             _native.ptr(w_out), _native.ptr(g_in), _native.ptr(g_out),
+                             _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
+                             float(scale), _native.ptr(loss_acc), _native.ptr(status), s)
+                return loss_acc
+            inputs = inputs.reshape(-1)
             ws = workspace_for(B, C, K, V, dev) if _use_records(scatter, C, K, V) else None
             _native.call('dw_sgns_pairs', _native.ptr(inputs.contiguous()),
                          _native.ptr(targets.contiguous()), B, C, K, V, d, _native.ptr(w_in),
@@ -133,6 +141,46 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                          float(scale), _native.ptr(loss_acc), _native.ptr(status),
                          _native.ptr(ws), 0 if ws is None else ws.numel(), s)
     return loss_acc
+
+
+def device_noise(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int, seed: int,
+                 noise_offset: int, device) -> torch.Tensor:
+    """int64 [B, C, K]: the negatives the fused kernels draw for ``noise=None`` (same Philox
+    keys), materialised — needed when rows must be renormalised before the step (max_norm)."""
+    out = torch.empty((n_centres, n_ctx, neg_samples), dtype=torch.int64, device=device)
+    with torch.cuda.device(device):
+        _native.call('dw_sgns_noise', int(n_centres), int(n_ctx), int(neg_samples),
+                     int(vocab_size), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
+                     _native.ptr(out), _native.stream(device))
+    return out
+
+
+_RENORM_WS: Dict[torch.device, torch.Tensor] = {}
+
+
+def renorm_(weight: torch.Tensor, ids: torch.Tensor, max_norm: float,
+            status: Optional[torch.Tensor] = None) -> None:
+    """nn.Embedding(max_norm) lookup side effect on the device: rows ``ids`` (any shape,
+    duplicates allowed) with L2 norm > max_norm are scaled to max_norm / (norm + 1e-7)."""
+    import ctypes
+    V, d = weight.shape
+    ids = ids.reshape(-1).to(weight.device, torch.long).contiguous()
+    n = ids.numel()
+    if n == 0:
+        return
+    nbytes = ctypes.c_size_t(0)
+    _native.call('dw_embedding_renorm_workspace_bytes', n, V, ctypes.byref(nbytes))
+    ws = _RENORM_WS.get(weight.device)
+    if ws is None or ws.numel() < nbytes.value:
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=weight.device)
+        _RENORM_WS[weight.device] = ws
+    st = torch.zeros(1, dtype=torch.int32, device=weight.device) if status is None else status
+    with torch.cuda.device(weight.device):
+        _native.call('dw_embedding_renorm', _native.ptr(weight.detach()), V, d, _native.ptr(ids),
+                     n, float(max_norm), _native.ptr(ws), ws.numel(), _native.ptr(st),
+                     _native.stream(weight.device))
+    if status is None:
+        _native.check_status(st, 'embedding renorm')
 
 
 def phase_timing(enable: bool) -> None:

@@ -30,8 +30,10 @@ from typing import Dict, List, Union
 import torch
 from torch.optim import Optimizer
 
+from shallow_encoders import _native
 from shallow_encoders.word2vec.model import W2VBase
-from shallow_encoders.word2vec.sgns import SGNSLoss, loss_terms, sgns_accumulate
+from shallow_encoders.word2vec.sgns import (SGNSLoss, device_noise, loss_terms, renorm_,
+                                            sgns_accumulate)
 from shallow_encoders.word2vec.utils import torch_helper
 from shallow_encoders.word2vec.utils.meter import MetricMeter
 from shallow_encoders.word2vec.utils.sampling import generate_noise_batch
@@ -112,6 +114,13 @@ class Word2VecTrainer(_Base):
         return self._model(inputs, outputs, proba=proba)
 
     # ---- training -----------------------------------------------------------------------------
+    def _status(self, device) -> torch.Tensor:
+        st = getattr(self, '_renorm_status', None)
+        if st is None or st.device != device:
+            st = torch.zeros(1, dtype=torch.int32, device=device)
+            self._renorm_status = st
+        return st
+
     def _noise(self, n_centres: int, n_ctx: int, device) -> Union[torch.Tensor, None]:
         if self._noise_mode == 'device':
             return None
@@ -132,14 +141,31 @@ class Word2VecTrainer(_Base):
             n_centres, C = n * (L - 2 * R), 2 * R
             src, targets = walks, None
         else:                                         # (inputs, targets) from the collate fn
-            inputs, targets = batch
-            src = inputs.reshape(-1).to(dev, torch.long).contiguous()
+            inputs, targets = batch                   # sg: (B, 1), (B, 2R); cbow: (B, 2R), (B, 1)
             targets = targets.to(dev, torch.long).contiguous()
             n_centres, C = targets.shape
+            src = inputs.to(dev, torch.long).reshape(n_centres, -1).contiguous()
+            if src.shape[1] == 1:
+                src = src.reshape(-1)
             R = C // 2
         noise = self._noise(n_centres, C, dev)
         offset = self._noise_offset
         self._noise_offset += n_centres
+        max_norm = self._model.max_norm
+        if max_norm is not None:
+            # nn.Embedding(max_norm) renormalises every row the reference's two forwards look
+            # up (inputs in the in table; targets and negatives in the out table) before the
+            # loss: materialise the device negatives, renormalise, then run the fused step
+            if targets is None:
+                raise NotImplementedError('max_norm with device walk batches: use the collate '
+                                          '(pairs) dataloader')
+            if noise is None:
+                noise = device_noise(n_centres, C, self._neg_samples, self._vocab_size,
+                                     self._seed, offset, dev)
+            st = self._status(dev)
+            renorm_(w_in, src, max_norm, st)
+            renorm_(w_out, targets, max_norm, st)
+            renorm_(w_out, noise, max_norm, st)
         if self.manual_grads:
             for p in (w_in, w_out):
                 if p.grad is None:
@@ -168,6 +194,9 @@ class Word2VecTrainer(_Base):
 
     def on_train_epoch_end(self) -> Dict[str, float]:
         """Log the epoch means; one host synchronisation per epoch (NaN check included)."""
+        st = getattr(self, '_renorm_status', None)
+        if st is not None:
+            _native.check_status(st, 'max_norm renormalisation')
         if self._meter.is_empty:
             return {}
         out = {}

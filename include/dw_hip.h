@@ -158,6 +158,35 @@ int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, 
                   double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
                   void *stream);
 
+/* Pooled-input (CBOW) form of dw_sgns_pairs (model.py:94-110 CBOW.forward + loss.py:14-22 +
+ * trainer.py:131-152): the input vector of sample b is the mean of w_in rows inputs[b, 0..n_in)
+ * (torch.mean over dim 1); targets int64 [batch, n_ctx] are the positive output rows and the
+ * noise [batch, n_ctx, neg_samples] (or device Philox, NULL) the negatives. Each of the n_in
+ * input rows receives 1/n_in of the input-vector gradient (mean backward). n_in = 1 computes
+ * what dw_sgns_pairs computes. Always the atomic output-table scatter (text-corpus batches). */
+int dw_sgns_pooled_pairs(const int64_t *inputs, int32_t n_in, const int64_t *targets,
+                         int64_t batch, int32_t n_ctx, int32_t neg_samples, int64_t vocab_size,
+                         int32_t dim, const float *w_in, const float *w_out, float *g_in,
+                         float *g_out, const int64_t *noise, uint64_t seed,
+                         uint64_t noise_offset, float grad_scale, double *loss_acc,
+                         int32_t *status, void *stream);
+
+/* The device negatives dw_sgns_* draw when noise == NULL, written out: noise[(b*n_ctx + j)*K + k]
+ * for b < batch (centre counter noise_offset + b). Replaces generate_noise_batch
+ * (utils/sampling.py:7-21) where the ids must exist before the step (max_norm renormalisation).*/
+int dw_sgns_noise(int64_t batch, int32_t n_ctx, int32_t neg_samples, int64_t vocab_size,
+                  uint64_t seed, uint64_t noise_offset, int64_t *noise, void *stream);
+
+/* nn.Embedding(max_norm=...) lookup side effect (model.py:24-25 with max_norm set; torch
+ * embedding_renorm_): every DISTINCT row among ids[0..n_ids) whose L2 norm exceeds max_norm is
+ * scaled by max_norm / (norm + 1e-7), in place. Ids are deduplicated on the device (radix sort
+ * in the caller's workspace, >= dw_embedding_renorm_workspace_bytes). Out-of-range ids set
+ * DW_S_BAD_INDEX and are skipped. */
+int dw_embedding_renorm_workspace_bytes(int64_t n_ids, int64_t vocab_size, size_t *bytes);
+int dw_embedding_renorm(float *weight, int64_t vocab_size, int32_t dim, const int64_t *ids,
+                        int64_t n_ids, double max_norm, void *workspace, size_t workspace_bytes,
+                        int32_t *status, void *stream);
+
 /* Bytes of device workspace the records path needs for n_centres centres with n_ctx contexts
  * and neg_samples negatives each over a vocabulary of vocab_size rows. */
 int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
@@ -171,6 +200,19 @@ int dw_sgns_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_sample
  * ms[2] are 0 in atomic mode). No reference counterpart (measurement only). */
 int dw_sgns_timing(int32_t enable);
 int dw_sgns_phase_ms(double *ms, int64_t *n_calls);
+
+/* CBOW.forward(inputs, outputs, proba) (model.py:98-110): logits[b, n] =
+ * <mean_p w_in[inputs[b, p]], w_out[outputs[b, n]]>, p < n_in; dw_skipgram_logits is n_in = 1.
+ * The backward adds dlogits[b,n] * pooled_b into g_out[outputs[b,n]] and (sum_n dlogits[b,n] *
+ * w_out[outputs[b,n]]) / n_in into each g_in[inputs[b, p]]. */
+int dw_pooled_logits(const int64_t *inputs, int32_t n_in, const int64_t *outputs,
+                     int64_t batch, int32_t n_out, int64_t vocab_size, int32_t dim,
+                     const float *w_in, const float *w_out, int32_t proba, float *logits,
+                     int32_t *status, void *stream);
+int dw_pooled_logits_backward(const int64_t *inputs, int32_t n_in, const int64_t *outputs,
+                              int64_t batch, int32_t n_out, int64_t vocab_size, int32_t dim,
+                              const float *w_in, const float *w_out, const float *dlogits,
+                              float *g_in, float *g_out, int32_t *status, void *stream);
 
 /* SkipGram.forward(inputs, outputs, proba) (model.py:79-91): logits[b, n] =
  * <w_in[inputs[b]], w_out[outputs[b, n]]>, sigmoid applied when proba != 0. */

@@ -1,6 +1,6 @@
 """Generate the golden fixtures from the REFERENCE itself (run in the build container only).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [downstream]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [downstream | cbow]
 
 Imports the importable pieces of /root/reference: the walkers
 (graph/random_walk_generator.py), the datasets (graph/datasets.py), SkipGram (word2vec/model.py),
@@ -182,6 +182,12 @@ def sg_windows(walks, R):
     return np.stack(ins).astype(np.int64), np.stack(tgts).astype(np.int64)
 
 
+def cbow_windows(walks, R):
+    """torch_dataset.py:311-315 (cbow): inputs text[i-R:i] | text[i+1:i+1+R], target text[i]."""
+    ins, tgts = sg_windows(walks, R)
+    return tgts, ins
+
+
 def reference_step(model, loss_fn, inputs, targets, noise):
     """trainer.py:131-152 wiring around the reference's own SkipGram / loss."""
     inputs_t = torch.as_tensor(inputs)
@@ -195,19 +201,23 @@ def reference_step(model, loss_fn, inputs, targets, noise):
     return loss, recall, precision
 
 
-def sgns_fixture(name, walks, V, d, R, K, lr, init_seed, noise_seed, n_steps=5, scale=1.0):
-    """F6: grads of one step, then params after 1 and n_steps Adam steps (new noise per step)."""
+def sgns_fixture(name, walks, V, d, R, K, lr, init_seed, noise_seed, n_steps=5, scale=1.0,
+                 model_cls=None, mode='sg', max_norm=None):
+    """F6: grads of one step, then params after 1 and n_steps Adam steps (new noise per step).
+    model_cls / mode / max_norm: CBOW (model.py:94-110) with 'cbow' windows, and
+    nn.Embedding(max_norm) renormalisation inside the reference's forwards."""
     torch.manual_seed(init_seed)
-    model = SkipGram(vocab_size=V, embedding_size=d, max_norm=None)
+    model = (model_cls or SkipGram)(vocab_size=V, embedding_size=d, max_norm=max_norm)
     if scale != 1.0:
         with torch.no_grad():
             model._input_embedding.weight.mul_(scale)
             model._output_embedding.weight.mul_(scale)
     w_in0 = model._input_embedding.weight.detach().numpy().copy()
     w_out0 = model._output_embedding.weight.detach().numpy().copy()
-    inputs, targets = sg_windows(walks, R)
+    inputs, targets = (cbow_windows if mode == 'cbow' else sg_windows)(walks, R)
     B, C = targets.shape
     opt = torch.optim.Adam(model.parameters(), lr=lr)
+    renormed = None
     loss_fn = NegativeSamplingLoss()
     torch.manual_seed(noise_seed)
     noises, losses, recalls, precisions = [], [], [], []
@@ -222,6 +232,8 @@ def sgns_fixture(name, walks, V, d, R, K, lr, init_seed, noise_seed, n_steps=5, 
         if step == 0:
             g_in = model._input_embedding.weight.grad.numpy().copy()
             g_out = model._output_embedding.weight.grad.numpy().copy()
+            renormed = (model._input_embedding.weight.detach().numpy().copy(),
+                        model._output_embedding.weight.detach().numpy().copy())
         losses.append([float(loss['loss']), float(loss['positive-loss']),
                        float(loss['negative-loss'])])
         recalls.append(rec)
@@ -235,6 +247,8 @@ def sgns_fixture(name, walks, V, d, R, K, lr, init_seed, noise_seed, n_steps=5, 
          g_in=g_in, g_out=g_out, w_in1=p1[0], w_out1=p1[1],
          w_in_n=model._input_embedding.weight.detach().numpy(),
          w_out_n=model._output_embedding.weight.detach().numpy(),
+         w_in0r=renormed[0], w_out0r=renormed[1], mode=mode,
+         max_norm=np.nan if max_norm is None else max_norm,
          losses=np.array(losses), recall=np.array(recalls), precision=np.array(precisions))
 
 
@@ -317,9 +331,25 @@ def downstream_fixture(name):
     save(name, **arrays)
 
 
+def cbow_fixtures():
+    """§8f 4: CBOW steps and max_norm renormalisation (reference model.py + nn.Embedding)."""
+    from shallow_encoders.word2vec.model import CBOW
+    rng = np.random.default_rng(41)
+    sgns_fixture('sgns_cbow_d16_k3.npz', rng.integers(1, 40, size=(12, 9)), V=40, d=16, R=2,
+                 K=3, lr=0.05, init_seed=8, noise_seed=9, model_cls=CBOW, mode='cbow')
+    sgns_fixture('sgns_sg_maxnorm_d8_k2.npz', rng.integers(1, 30, size=(10, 8)), V=30, d=8, R=2,
+                 K=2, lr=0.1, init_seed=10, noise_seed=11, scale=8.0, max_norm=1.0)
+    sgns_fixture('sgns_cbow_maxnorm_d2_k1.npz', rng.integers(1, 6, size=(9, 8)), V=6, d=2, R=1,
+                 K=1, lr=0.1, init_seed=12, noise_seed=13, scale=3.0, model_cls=CBOW,
+                 mode='cbow', max_norm=1.0)
+
+
 def main():
     if sys.argv[1:] == ['downstream']:
         downstream_fixture('downstream_split_ops.npz')
+        return
+    if sys.argv[1:] == ['cbow']:
+        cbow_fixtures()
         return
     info = {'python': sys.version, 'torch': torch.__version__, 'networkx': nx.__version__}
     # F1/F4 karate node2vec (configs/sge_sg_karate_club.yaml walker) and a strongly biased p,q
@@ -355,6 +385,7 @@ def main():
                        d=2, R=2, K=1, lr=0.1, batch_walks=64, epochs=3, step_size=1, gamma=0.5)
     # §8f 3: downstream split algorithms + edge operators
     downstream_fixture('downstream_split_ops.npz')
+    cbow_fixtures()
     with open(os.path.join(HERE, 'golden_info.json'), 'w') as f:
         json.dump(info, f, indent=2)
 

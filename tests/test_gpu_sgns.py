@@ -19,7 +19,10 @@ from shallow_encoders.word2vec.sgns import SGNSLoss, loss_terms, sgns_accumulate
 
 pytestmark = pytest.mark.gpu
 
-SGNS_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'sgns_*.npz')))
+ALL_SGNS = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'sgns_*.npz')))
+# skip-gram, no max_norm (the records / walks paths); CBOW and max_norm fixtures below
+SGNS_FIXTURES = [n for n in ALL_SGNS if 'cbow' not in n and 'maxnorm' not in n]
+POOLED_FIXTURES = [n for n in ALL_SGNS if n not in SGNS_FIXTURES]
 RTOL = 1e-5          # fp32 gradients / losses
 ATOL_REL = 2e-6      # absolute slack, relative to the largest gradient entry (cancellations)
 
@@ -257,3 +260,121 @@ def test_autograd_path_equals_manual_path(hip_device):
     (outs[0] * 3.0).backward()
     np.testing.assert_allclose(w_in.grad.cpu().numpy(), 3.0 * f['g_in'], rtol=1e-5, atol=1e-8)
     np.testing.assert_allclose(w_out.grad.cpu().numpy(), 3.0 * f['g_out'], rtol=1e-5, atol=1e-8)
+
+
+# ---- CBOW (pooled inputs) and nn.Embedding(max_norm) renormalisation -------
+def _max_norm(f):
+    return None if np.isnan(float(f['max_norm'])) else float(f['max_norm'])
+
+
+@pytest.mark.parametrize('name', POOLED_FIXTURES)
+def test_cbow_and_max_norm_step_vs_reference(name, hip_device):
+    """Renormalise the looked-up rows like the reference's two forwards, then one fused step
+    (dw_sgns_pooled_pairs for CBOW) — loss, metrics, renormalised tables and gradients."""
+    from shallow_encoders.word2vec.sgns import renorm_
+    f = golden(name)
+    mn = _max_norm(f)
+    w_in, w_out = _dev(f['w_in0']), _dev(f['w_out0'])
+    inputs, targets = _dev(f['inputs'], torch.long), _dev(f['targets'], torch.long)
+    noise = _dev(f['noise'][0], torch.long)
+    B, C = targets.shape
+    K = int(f['K'])
+    if mn is not None:
+        renorm_(w_in, inputs, mn)
+        renorm_(w_out, targets, mn)
+        renorm_(w_out, noise, mn)
+    # norms: wave-order float sum vs torch's; the renormalised rows agree to a few ulp
+    np.testing.assert_allclose(w_in.cpu().numpy(), f['w_in0r'], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(w_out.cpu().numpy(), f['w_out0r'], rtol=1e-6, atol=1e-7)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, inputs=inputs, targets=targets,
+                          noise=noise)
+    t = loss_terms(acc, B * C, K)
+    np.testing.assert_allclose([float(t['loss']), float(t['positive-loss']),
+                                float(t['negative-loss'])], f['losses'][0], rtol=1e-5)
+    assert float(t['recall']) == pytest.approx(float(f['recall'][0]), abs=1e-6)
+    assert float(t['precision']) == pytest.approx(float(f['precision'][0]), abs=1e-6)
+    assert_grad_close(g_in.cpu().numpy(), f['g_in'])
+    assert_grad_close(g_out.cpu().numpy(), f['g_out'])
+
+
+@pytest.mark.parametrize('name', POOLED_FIXTURES)
+def test_cbow_and_max_norm_adam_steps_vs_reference(name, hip_device):
+    """Renormalise + fused step + HIP dense Adam for every recorded batch: parameters after the
+    first step and the loss of every step against the reference's own training."""
+    from shallow_encoders.word2vec.sgns import renorm_
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    f = golden(name)
+    mn = _max_norm(f)
+    V, d, K, lr = int(f['V']), int(f['d']), int(f['K']), float(f['lr'])
+    t = ShardedTables(V, d, hip_device, lr=lr, init_seed=None)
+    t.load_(torch.as_tensor(f['w_in0']), torch.as_tensor(f['w_out0']))
+    inputs, targets = _dev(f['inputs'], torch.long), _dev(f['targets'], torch.long)
+    B, C = targets.shape
+    for step in range(f['noise'].shape[0]):
+        noise = _dev(f['noise'][step], torch.long)
+        if mn is not None:
+            renorm_(t.w_in, inputs, mn)
+            renorm_(t.w_out, targets, mn)
+            renorm_(t.w_out, noise, mn)
+        acc = sgns_accumulate(t.w_in, t.w_out, t.g_in, t.g_out, K, inputs=inputs,
+                              targets=targets, noise=noise)
+        assert float(loss_terms(acc, B * C, K)['loss']) == pytest.approx(
+            float(f['losses'][step][0]), rel=1e-4)
+        t.step()
+        if step == 0:   # tiny tables: allow 2 sign-flipped near-zero-gradient entries
+            frac = max(1e-3, 2.0 / t.w_in.numel())
+            assert_params_close(t.w_in.cpu().numpy(), f['w_in1'], lr, max_frac=frac,
+                                max_abs=2.05 * lr)
+            assert_params_close(t.w_out.cpu().numpy(), f['w_out1'], lr, max_frac=frac,
+                                max_abs=2.05 * lr)
+
+
+def test_cbow_forward_backward_vs_oracle(hip_device):
+    """CBOW.forward (dw_pooled_logits) and its backward against model.py:102-107 on the CPU."""
+    from shallow_encoders.word2vec.model import CBOW
+    f = golden('sgns_cbow_d16_k3.npz')
+    V, d = int(f['V']), int(f['d'])
+    model = CBOW(V, d).to(hip_device)
+    with torch.no_grad():
+        model.input_weight.copy_(torch.as_tensor(f['w_in0']))
+        model.output_weight.copy_(torch.as_tensor(f['w_out0']))
+    inputs = torch.as_tensor(f['inputs'])
+    outputs = torch.as_tensor(f['noise'][0]).reshape(inputs.shape[0], -1)
+    logits = model(inputs, outputs, proba=False)
+    (logits * torch.linspace(-1, 1, logits.numel(), device=hip_device).view_as(logits)).sum() \
+        .backward()
+    win = torch.tensor(f['w_in0'], requires_grad=True)
+    wout = torch.tensor(f['w_out0'], requires_grad=True)
+    ref = sgns_ref.pooled_logits(win, wout, inputs, outputs)
+    (ref * torch.linspace(-1, 1, ref.numel()).view_as(ref)).sum().backward()
+    np.testing.assert_allclose(logits.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5,
+                               atol=1e-7)
+    np.testing.assert_allclose(model.input_weight.grad.cpu().numpy(), win.grad.numpy(),
+                               rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(model.output_weight.grad.cpu().numpy(), wout.grad.numpy(),
+                               rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(model(inputs, outputs).detach().cpu().numpy(),
+                               torch.sigmoid(ref).detach().numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_device_noise_fill_matches_in_kernel_draws(hip_device):
+    """dw_sgns_noise writes exactly the negatives the fused kernel draws for noise=None."""
+    from shallow_encoders.word2vec.sgns import device_noise
+    f = golden('sgns_d128_k5.npz')
+    w_in, w_out = _dev(f['w_in0']), _dev(f['w_out0'])
+    inputs, targets = _dev(f['inputs'], torch.long), _dev(f['targets'], torch.long)
+    B, C = targets.shape
+    K, V = int(f['K']), int(f['V'])
+    outs = []
+    for noise in (None, device_noise(B, C, K, V, 17, 1000, hip_device)):
+        g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+        acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, inputs=inputs, targets=targets,
+                              noise=noise, seed=17, noise_offset=1000, scatter='atomic')
+        outs.append((acc.cpu().numpy(), g_in.cpu().numpy(), g_out.cpu().numpy()))
+    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6)
+    assert_grad_close(outs[1][1], outs[0][1])
+    assert_grad_close(outs[1][2], outs[0][2])
+    ref = ph.device_noise(17, 1000, B, C, K, V)
+    np.testing.assert_array_equal(device_noise(B, C, K, V, 17, 1000, hip_device).cpu().numpy(),
+                                  ref.reshape(B, C, K))

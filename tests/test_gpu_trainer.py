@@ -124,3 +124,29 @@ def test_downstream_quality_karate(tmp_path, hip_device):
     assert res['edge_accuracy'] >= 0.55, res
     assert os.path.exists(os.path.join(out, 'graph_karate_club', 'SG_exp01_baseline', 'analysis',
                                        'downstream-node-classification.jpg'))
+
+
+@pytest.mark.parametrize('config,mode', [('w2v_cbow_abcde', 'cbow'), ('w2v_sg_abcde', 'sg')])
+def test_text_word2vec_abcde(tmp_path, hip_device, config, mode):
+    """Text word2vec through tools/train.py: the reference's abcde configs
+    (max_norm 1.0, renormalised on every lookup; the per-step parity of that is in
+    test_gpu_sgns.py) — CBOW over real (B, 2R) -> (B, 1) batches and skip-gram: the loss falls
+    and co-occurring words score higher than words that never meet (README.md:127-147: `a`
+    goes with `b`, `c` with `d`)."""
+    from tools import train as train_tool
+    out = str(tmp_path / 'runs')
+    last = train_tool.main(['--config-name', config, f'path.output_dir={out}',
+                            f'output_dir={out}', f'datamodule.mode={mode}',
+                            'datamodule.num_workers=0', 'train.max_epochs=40'])
+    assert last['train-epoch/loss'] < 1.3, last
+    ck = os.path.join(out, 'abcde', 'CBOW_exp01_baseline' if 'cbow' in config
+                      else 'SG_exp01_baseline', 'checkpoints', 'last.ckpt')
+    sd = torch.load(ck, weights_only=True)['state_dict']
+    w_in = sd['_model._input_embedding.weight'].numpy()
+    w_out = sd['_model._output_embedding.weight'].numpy()
+    from shallow_encoders.config_parser import load_config
+    vocab = load_config(config).datamodule.instantiate_dataset().vocab
+    i = {t: w_in[vocab[t]] for t in 'abcd'}
+    o = {t: w_out[vocab[t]] for t in 'abcd'}
+    assert np.dot(i['a'], o['b']) > np.dot(i['a'], o['c'])
+    assert np.dot(i['c'], o['d']) > np.dot(i['c'], o['a'])

@@ -54,19 +54,32 @@ def test_oracle_transition_law_matches_reference(name):
     assert k == len(offs) - 1
 
 
+def _max_norm(f):
+    if 'max_norm' not in f.files or np.isnan(float(f['max_norm'])):
+        return None
+    return float(f['max_norm'])
+
+
 @pytest.mark.parametrize('name', SGNS_FIXTURES)
 def test_oracle_sgns_matches_reference(name):
     f = golden(name)
-    loss, g_in, g_out, rec, prec = sgns_ref.sgns_forward_backward(
-        f['w_in0'], f['w_out0'], f['inputs'], f['targets'], f['noise'][0])
+    mn = _max_norm(f)
+    loss, g_in, g_out, rec, prec, w_in_r, w_out_r = sgns_ref.sgns_forward_backward(
+        f['w_in0'], f['w_out0'], f['inputs'], f['targets'], f['noise'][0], max_norm=mn,
+        return_tables=True)
+    if 'w_in0r' in f.files:   # the tables the reference's forwards renormalised (max_norm)
+        np.testing.assert_array_equal(w_in_r, f['w_in0r'])
+        np.testing.assert_array_equal(w_out_r, f['w_out0r'])
     np.testing.assert_allclose([loss['loss'], loss['positive-loss'], loss['negative-loss']],
                                f['losses'][0], rtol=1e-6)
     np.testing.assert_allclose(g_in, f['g_in'], rtol=1e-5, atol=1e-9)
     np.testing.assert_allclose(g_out, f['g_out'], rtol=1e-5, atol=1e-9)
     assert rec == pytest.approx(float(f['recall'][0]))
     assert prec == pytest.approx(float(f['precision'][0]))
+    if f['inputs'].reshape(len(f['targets']), -1).shape[1] != 1:
+        return   # the closed form below is the skip-gram one
     # independent float64 closed form of the same gradient (clamp mask + batch mean)
-    l64, gi64, go64 = sgns_ref.sgns_grads_closed_form(f['w_in0'], f['w_out0'], f['inputs'],
+    l64, gi64, go64 = sgns_ref.sgns_grads_closed_form(w_in_r, w_out_r, f['inputs'],
                                                       f['targets'], f['noise'][0])
     assert l64 == pytest.approx(float(f['losses'][0][0]), rel=1e-5)
     np.testing.assert_allclose(gi64, f['g_in'], rtol=1e-4, atol=1e-8)
@@ -78,7 +91,7 @@ def test_oracle_adam_trajectory_matches_reference(name):
     f = golden(name)
     ref = sgns_ref.TorchAdamRef(f['w_in0'], f['w_out0'], lr=float(f['lr']))
     for step in range(f['noise'].shape[0]):
-        loss = ref.train_step(f['inputs'], f['targets'], f['noise'][step])
+        loss = ref.train_step(f['inputs'], f['targets'], f['noise'][step], max_norm=_max_norm(f))
         assert loss['loss'] == pytest.approx(float(f['losses'][step][0]), rel=1e-6)
         if step == 0:
             w_in, w_out = ref.tables()
@@ -92,7 +105,8 @@ def test_oracle_adam_trajectory_matches_reference(name):
 @pytest.mark.parametrize('name', SGNS_FIXTURES)
 def test_oracle_windows_match_reference_collate(name):
     f = golden(name)
-    ins, tgt = sgns_ref.sg_windows(f['walks'], int(f['R']))
+    cbow = 'mode' in f.files and str(f['mode']) == 'cbow'
+    ins, tgt = (sgns_ref.cbow_windows if cbow else sgns_ref.sg_windows)(f['walks'], int(f['R']))
     np.testing.assert_array_equal(ins, f['inputs'])
     np.testing.assert_array_equal(tgt, f['targets'])
 
