@@ -34,6 +34,12 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+CONFIGS = {
+    'c3': dict(scale=20, edges=10_000_000, dim=128, method='deepwalk', p=1.0, q=1.0),
+    'c5': dict(scale=24, edges=256_000_000, dim=256, method='node2vec', p=0.25, q=4.0),
+}
+
+
 def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     """Algorithmic HBM bytes per positive pair: every gathered fp32 row read
     once and its gradient written once; int64 ids. 6,295 B at d=128, K=5, R=5."""
@@ -81,7 +87,7 @@ def cpu_baseline(csr, args, budget_s: float):
     sgns_dt = time.perf_counter() - t0
     pairs_per_s = steps * tgt.size / sgns_dt
     # walker: the reference's per-step algorithm (Python, one process)
-    g = walk_ref.CSR(csr.row_ptr, csr.col)
+    g = walk_ref.CSR(csr.row_ptr, csr.host_col())
     n_w, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s * 0.3 or n_w < 1:
         s = int(rng.integers(1, V))
@@ -105,12 +111,16 @@ def main():
     ap.add_argument('--steps', type=int, default=30)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch-walks', type=int, default=8192)
-    ap.add_argument('--method', default='deepwalk', choices=['deepwalk', 'node2vec'])
-    ap.add_argument('--p', type=float, default=1.0)
-    ap.add_argument('--q', type=float, default=1.0)
-    ap.add_argument('--scale', type=int, default=20)
-    ap.add_argument('--edges', type=int, default=10_000_000)
-    ap.add_argument('--dim', type=int, default=128)
+    ap.add_argument('--config', default='c3', choices=sorted(CONFIGS),
+                    help='BASELINE workload preset: c3 = R-MAT 20 / 10M draws, d=128, DeepWalk '
+                         '(the metric\'s config); c5 = R-MAT 24 / 256M draws, d=256, node2vec '
+                         'p=0.25 q=4 (BASELINE configs[4], here per GPU)')
+    ap.add_argument('--method', default=None, choices=['deepwalk', 'node2vec'])
+    ap.add_argument('--p', type=float, default=None)
+    ap.add_argument('--q', type=float, default=None)
+    ap.add_argument('--scale', type=int, default=None)
+    ap.add_argument('--edges', type=int, default=None)
+    ap.add_argument('--dim', type=int, default=None)
     ap.add_argument('--neg', type=int, default=5)
     ap.add_argument('--radius', type=int, default=5)
     ap.add_argument('--walk-length', type=int, default=80)
@@ -122,6 +132,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-walk-bench', action='store_true')
     args = ap.parse_args()
+    for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -149,7 +162,7 @@ def main():
     _native.require_device(dev)
 
     t0 = time.time()
-    csr = rmat_graph(args.scale, args.edges, 0)
+    csr = rmat_graph(args.scale, args.edges, 0, device=dev)   # built in HBM (dw_rmat_edges)
     V = csr.vocab_size
     N = V - 1
     log(rank, f'[bench] R-MAT scale {args.scale}: {N} nodes, {csr.nnz // 2} edges '
@@ -275,10 +288,11 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'fp32',
-        'data': 'synthetic (R-MAT scale 20 graph, Philox walks, uniform device negatives, '
-                'random Xavier init)',
+        'data': f'synthetic (R-MAT scale {args.scale} graph built on the device, Philox walks, '
+                f'uniform device negatives, random Xavier init)',
         'config': {
-            'workload': (f'C3: R-MAT {N} nodes / {csr.nnz // 2} edges, {args.method} L={L}, '
+            'workload': (f'{args.config.upper()}: R-MAT {N} nodes / {csr.nnz // 2} edges, '
+                         f'{args.method}{f" p={args.p} q={args.q}" if args.method == "node2vec" else ""} L={L}, '
                          f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU; '
                          f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
@@ -307,7 +321,8 @@ def main():
             with open(prof) as f:
                 pmc = json.load(f)
             if (pmc.get('pairs_per_launch') == pairs_per_step and
-                    pmc.get('scatter', 'atomic') == args.scatter):
+                    pmc.get('scatter', 'atomic') == args.scatter and
+                    pmc.get('dim', 128) == d and pmc.get('vocab_size', 1048577) == V):
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
                 result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"
                 per_k = pmc.get('hbm_bytes_per_kernel') or {}
@@ -315,7 +330,7 @@ def main():
                     result['roofline']['phases'][k]['traffic'] = per_k.get('sgns_' + k)
         except (OSError, ValueError):
             pass
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 'c3':
         cb = cpu_baseline(csr, args, args.cpu_budget)
         result['cpu_baseline'] = cb
     if rank == 0:

@@ -50,6 +50,11 @@ SIGNATURES = {
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
     'dw_alias_build': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
+    'dw_ingest_workspace_bytes': (ctypes.c_int, [_i32, _i64, _i64, _szp]),
+    'dw_rmat_edges': (ctypes.c_int, [_i32, _i64, _p, _p, _u64, _u64, _f64, _f64, _f64, _p, _p, _p,
+                                     ctypes.c_size_t, _p]),
+    'dw_graph_isolated': (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
+    'dw_csr_from_edges': (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_walk_replay': (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i64, _i32, _i32, _f64, _f64,
                                       _p, _p, _p, _p]),
     'dw_walk_fast': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _i32, _f64, _f64,

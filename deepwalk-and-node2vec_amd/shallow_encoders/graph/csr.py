@@ -39,6 +39,38 @@ def node_token(name) -> str:
     return toks[0]
 
 
+class NodeNames(Sequence):
+    """``['<unk>', 'n0000000', 'n0000001', ...]`` computed on demand (synthetic graphs: node i
+    is named n%0{width}d and has vocabulary id i + 1), so a 16.8M-node graph does not hold
+    16.8M Python strings."""
+
+    def __init__(self, n_nodes: int, width: int):
+        self.n, self.width = int(n_nodes), int(width)
+
+    def __len__(self) -> int:
+        return self.n + 1
+
+    def _name(self, i: int) -> str:
+        return UNK if i == 0 else f'n{i - 1:0{self.width}d}'
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self._name(j) for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        return self._name(i)
+
+    def index(self, token, *args) -> int:
+        m = re.fullmatch(r'n(\d+)', str(token))
+        if token == UNK:
+            return 0
+        if m is None or len(m.group(1)) != self.width or int(m.group(1)) >= self.n:
+            raise ValueError(f'{token!r} is not a node name')
+        return int(m.group(1)) + 1
+
+
 @dataclass
 class CSRGraph:
     """Host (numpy) CSR plus lazily built device copies."""
@@ -97,12 +129,30 @@ class CSRGraph:
         if itos is None:
             width = max(7, len(str(V - 1)))
             itos = [UNK] + [f'n{i:0{width}d}' for i in range(V - 1)]
-        itos = list(itos)
+        if not isinstance(itos, NodeNames):
+            itos = list(itos)
         if names is None:
-            names = [None] + itos[1:]
+            names = itos if isinstance(itos, NodeNames) else [None] + itos[1:]
         if len(itos) != V:
             raise ValueError('itos length must equal the number of CSR rows')
-        return CSRGraph(row_ptr, col, weights, itos, list(names))
+        return CSRGraph(row_ptr, col, weights, itos,
+                        names if isinstance(names, NodeNames) else list(names))
+
+    @staticmethod
+    def from_device(row_ptr: torch.Tensor, col: torch.Tensor, itos: Sequence[str]) -> 'CSRGraph':
+        """A CSR built in HBM (dw_csr_from_edges): row_ptr is copied to the host (V+1 int64),
+        col stays on the device only (``col`` is None until ``host_col()``)."""
+        g = CSRGraph(row_ptr.cpu().numpy(), None, None, itos, itos)
+        g._dev_device = col.device
+        g._dev = {'row_ptr': row_ptr, 'col': col, 'weights': None,
+                  'status': torch.zeros(1, dtype=torch.int32, device=col.device)}
+        return g
+
+    def host_col(self) -> np.ndarray:
+        """The column array on the host (downloaded once for device-built graphs)."""
+        if self.col is None:
+            self.col = self._dev['col'].cpu().numpy()
+        return self.col
 
     # ------------------------------------------------------------------ host helpers
     @property
@@ -121,13 +171,15 @@ class CSRGraph:
         return np.diff(self.row_ptr)
 
     def neighbors(self, i: int) -> np.ndarray:
-        return self.col[self.row_ptr[i]:self.row_ptr[i + 1]]
+        return self.host_col()[self.row_ptr[i]:self.row_ptr[i + 1]]
 
     def stoi(self) -> Dict[str, int]:
         return {t: i for i, t in enumerate(self.itos)}
 
     def node_id(self, node) -> int:
         tok = node_token(node)
+        if isinstance(self.itos, NodeNames):
+            return self.itos.index(tok)
         sto = self.__dict__.setdefault('_stoi_cache', None)
         if sto is None:
             sto = self.stoi()
@@ -140,12 +192,14 @@ class CSRGraph:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables on the device)."""
         dev = _native.require_device(device)
         if self._dev_device != dev:
+            if self.col is None and 'col' in self._dev:   # device-built: keep a host copy
+                self.col = self._dev['col'].cpu().numpy()
             self._dev = {}
             self._dev_device = dev
         d = self._dev
         if 'row_ptr' not in d:
             d['row_ptr'] = torch.from_numpy(self.row_ptr).to(dev)
-            d['col'] = torch.from_numpy(self.col).to(dev)
+            d['col'] = torch.from_numpy(self.host_col()).to(dev)
             d['weights'] = None if self.weights is None else torch.from_numpy(self.weights).to(dev)
             d['status'] = torch.zeros(1, dtype=torch.int32, device=dev)
             st = d['status']

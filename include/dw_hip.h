@@ -82,6 +82,33 @@ int dw_alias_build(const int64_t *row_ptr, const double *weights, int64_t n_rows
 
 /* ---- walks -------------------------------------------------------------------------------- */
 
+/* ---- Graph ingestion on the device (shallow_encoders/graph/rmat.py) ----
+ * R-MAT edge draws replacing rmat.py:rmat_edges' numpy loop: the uniforms are numpy's
+ * default_rng PCG64 stream, draw index level * n_edges + edge. The host supplies level_state
+ * (2*scale uint64: lo, hi of the 128-bit state before level l's first draw), jump (64 x 4
+ * uint64: multiplier lo/hi, increment lo/hi of 2^i steps), the stream increment and the
+ * thresholds t1 = a, t2 = a + b, t3 = a + b + c. Output: edges packed (src << 32 | dst),
+ * self-loops dropped, undirected duplicates removed keeping the first draw, in draw order;
+ * *n_unique (device int64) = their count. Workspace >= dw_ingest_workspace_bytes. */
+int dw_ingest_workspace_bytes(int32_t scale, int64_t n_edges, int64_t n_nodes, size_t *bytes);
+int dw_rmat_edges(int32_t scale, int64_t n_edges, const uint64_t *level_state,
+                  const uint64_t *jump, uint64_t inc_lo, uint64_t inc_hi, double t1, double t2,
+                  double t3, uint64_t *edges, int64_t *n_unique, void *workspace,
+                  size_t workspace_bytes, void *stream);
+
+/* Nodes of [0, n_nodes) that no edge touches, increasing (rmat.py's isolated-node patch list);
+ * *n_isolated is a device int64. Endpoints >= n_nodes set DW_S_BAD_CSR. */
+int dw_graph_isolated(const uint64_t *edges, int64_t n_edges, int64_t n_nodes,
+                      int32_t *isolated, int64_t *n_isolated, int32_t *status, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
+/* CSR of an undirected packed edge list (rmat.py:csr_from_edges / networkx add_edges_from
+ * order): row_ptr int64 [n_nodes + 2] (row 0 = <unk>, row i+1 = node i), col int32
+ * [2 n_edges] holding vocabulary ids (node + 1); each row lists its edges in edge order. */
+int dw_csr_from_edges(const uint64_t *edges, int64_t n_edges, int64_t n_nodes,
+                      int64_t *row_ptr, int32_t *col, int32_t *status, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
 /* Exact replay walker — bit-exact with DeepWalk.walk / Node2Vec.walk
  * (random_walk_generator.py:61-72 / 94-119) given the uniforms random.random() would return.
  * uniforms: float64[n_walks, L-1], consumed in the reference's order (one per step).

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output (gpurun_out/prof_*) into profiles/ (committed evidence).
 
-    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch]
+    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch [dim vocab_size]]
 
 Writes
   profiles/<tag>_kernel_stats.csv  rocprofv3 --stats, verbatim;
@@ -52,6 +52,8 @@ def kernel_class(name: str):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else 'r01'
     pairs = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    dim = int(sys.argv[3]) if len(sys.argv) > 3 else 128          # C3 defaults
+    vocab = int(sys.argv[4]) if len(sys.argv) > 4 else 1048577
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, 'prof_trace', '**', '*kernel_stats.csv'), recursive=True)
     dur = collections.defaultdict(lambda: [0, 0.0])   # class -> [calls, total ns]
@@ -119,7 +121,7 @@ def main():
         per_kernel = {k: summary[k].get('hbm_bytes_per_sgns_call') for k in SGNS_CLASSES
                       if k in summary}
         with open(os.path.join(PROF, 'sgns_pmc.json'), 'w') as f:
-            json.dump({'round': tag, 'pairs_per_launch': pairs,
+            json.dump({'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
                        'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
                        'hbm_bytes_per_launch': call['hbm_bytes'],
                        'hbm_bytes_per_kernel': per_kernel,

@@ -196,3 +196,27 @@ def test_fast_walks_rmat20_properties(hip_device):
             for a, b in zip(row[:-1], row[1:]):
                 nb = csr.col[csr.row_ptr[a]:csr.row_ptr[a + 1]]
                 assert b in nb
+
+
+@pytest.mark.parametrize('scale,n_edges', [(12, 40_000), (16, 600_000), (20, 10_000_000)])
+def test_device_rmat_csr_equals_host_build(hip_device, scale, n_edges):
+    """Graph ingestion on the device (dw_rmat_edges -> dw_graph_isolated -> host patch draws
+    -> dw_csr_from_edges) reproduces the numpy generator's CSR exactly: same uniforms (numpy
+    PCG64 on the device), first-occurrence dedupe, patch edges and networkx row order. At
+    scale 20 (C3) it must also give SURVEY.md §8d's check values."""
+    import time
+    from shallow_encoders.graph.rmat import rmat_edges, rmat_graph
+    t0 = time.perf_counter()
+    host = rmat_graph(scale, n_edges, 0)
+    t1 = time.perf_counter()
+    dev = rmat_graph(scale, n_edges, 0, device=hip_device)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f'scale {scale}: host {t1 - t0:.2f}s, device {t2 - t1:.2f}s')
+    np.testing.assert_array_equal(dev.row_ptr, host.row_ptr)
+    np.testing.assert_array_equal(dev.host_col(), host.col)
+    assert len(dev.itos) == len(host.itos) and dev.itos[1] == host.itos[1]
+    if scale == 20:
+        edges, n_patched = rmat_edges(scale, n_edges, 0)
+        assert len(edges) == 10_013_665 and n_patched == 475_918
+        assert host.nnz == 2 * 10_013_665
