@@ -46,9 +46,11 @@ def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     return 8 * d * (1 + K) + 8 * d / (2 * R) + 8 * (1 + K) + 8 / (2 * R)
 
 
-def sgns_phase_bytes(n_walks, L, R, K, d, V, scatter):
+def sgns_phase_bytes(n_walks, L, R, K, d, V, scatter, fused=False):
     """Implementation byte model of each SGNS phase per call: rows of 4d B,
-    12-B records {row u32 | coef f32, centre u32}, one centre-gradient RMW row per centre."""
+    12-B records {row u32 | coef f32, centre u32}, one centre-gradient RMW row per centre.
+    fused: pass 2 also runs the out table's Adam (p, m, v read + written for every row) instead
+    of the g_out read-modify-write."""
     centres = n_walks * (L - 2 * R)
     T = 2 * R * (1 + K)
     n_rec = centres * T
@@ -58,8 +60,8 @@ def sgns_phase_bytes(n_walks, L, R, K, d, V, scatter):
     bits = max(1, math.ceil(math.log2(V)))
     touched = V * (1.0 - math.exp(-n_rec / V))   # expected distinct output rows
     return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 12 * T) + n_walks * L * 4,
-            'sort': n_rec * (4 + 24 * math.ceil(bits / 8)),
-            'pass2': n_rec * (12 + 4 * d) + touched * 8 * d}
+            'sort': n_rec * (4 + 24 * math.ceil(bits / 11)),
+            'pass2': n_rec * (12 + 4 * d) + (V * d * 24 if fused else touched * 8 * d)}
 
 
 def log(rank, *a):
@@ -131,6 +133,8 @@ def main():
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-walk-bench', action='store_true')
+    ap.add_argument('--no-fuse-adam', action='store_true',
+                    help='N=1: run the output table\'s Adam as its own pass (unfused)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
@@ -183,6 +187,8 @@ def main():
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
+    fuse = (not args.no_fuse_adam and args.scatter == 'sorted' and
+            tables.out_adam_spec() is not None)
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
 
     def one_step(record: bool):
@@ -205,10 +211,13 @@ def main():
         # output-table phase runs -> out-table exchange -> wait for both all-gathers
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
         tables.exchange_in()
-        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2, **kw)
+        # one device: the output table's Adam is fused into the output-table phase
+        spec = tables.out_adam_spec() if fuse else None
+        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
+                        out_adam=spec, **kw)
         if record:
             e[2].record()
-        tables.exchange_out()
+        tables.exchange_out(fused_out=spec is not None)
         tables.sync()
         if record:
             e[3].record()
@@ -247,8 +256,11 @@ def main():
     value = total_pairs / elapsed
     bpp = sgns_bytes_per_pair(d, K, R)
     sgns_ms = phases['pass1'] + phases['sort'] + phases['pass2']
-    sgns_gbs = pairs_per_step * bpp / (sgns_ms * 1e-3) / 1e9
-    phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter)
+    # algorithmic bytes of the timed op: SURVEY §8d's per-pair SGNS figure, plus its dense-Adam
+    # figure for one table (V*d*4 B x 7) when the out table's Adam is fused into pass 2
+    out_adam_bytes = V * d * 4 * 7 if fuse else 0
+    sgns_gbs = (pairs_per_step * bpp + out_adam_bytes) / (sgns_ms * 1e-3) / 1e9
+    phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     phase_info = {k: {'ms': phases[k], 'bytes_model': phase_bytes[k],
                       'GBps': phase_bytes[k] / (phases[k] * 1e-3) / 1e9 if phases[k] else None}
                   for k in ('pass1', 'sort', 'pass2')}
@@ -305,11 +317,15 @@ def main():
         'kernel_ms': kern_ms,
         'mean_loss': mean_loss,
         'roofline': {
-            'kernel': ('dw_sgns_walks = k_sgns_g16 + rocprim onesweep radix sort + k_rec_gather'
+            'kernel': (('dw_sgns_walks_phase 1 + dw_sgns_walks_phase2_adam = k_sgns_g16 + rocprim '
+                        'onesweep radix sort + k_rec_gather with the out-table Adam fused + '
+                        'k_adam_rest') if fuse else
+                       'dw_sgns_walks = k_sgns_g16 + rocprim onesweep radix sort + k_rec_gather'
                        if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
             'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,
+            'out_table_adam_bytes': out_adam_bytes,
             'ms_per_launch': sgns_ms, 'launches_timed': phases['calls'],
             'phases': phase_info,
         },
@@ -322,7 +338,8 @@ def main():
                 pmc = json.load(f)
             if (pmc.get('pairs_per_launch') == pairs_per_step and
                     pmc.get('scatter', 'atomic') == args.scatter and
-                    pmc.get('dim', 128) == d and pmc.get('vocab_size', 1048577) == V):
+                    pmc.get('dim', 128) == d and pmc.get('vocab_size', 1048577) == V and
+                    bool(pmc.get('fused_out_adam', False)) == fuse):
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
                 result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"
                 per_k = pmc.get('hbm_bytes_per_kernel') or {}

@@ -12,21 +12,6 @@
 
 namespace {
 
-struct AdamScalars {
-    float w1, b2, omb2, bc2s, nstep, eps, wd;
-};
-
-__device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
-                                          const AdamScalars &s) {
-    float gg = g;
-    if (s.wd != 0.f) gg = gg + s.wd * p;
-    m = fmaf(s.w1, gg - m, m);  // lerp with weight < 0.5: self + weight * (end - self)
-    v = v * s.b2;
-    v = v + s.omb2 * gg * gg;
-    const float denom = sqrtf(v) / s.bc2s + s.eps;
-    p = p + s.nstep * (m / denom);
-}
-
 // Every byte is touched once per step, so loads and stores are non-temporal (they neither
 // allocate in L2 / the Infinity Cache nor evict the embedding rows the next SGNS pass gathers),
 // and each lane keeps U = 2 float4 groups of all four tensors in flight. Measured on MI355X,
@@ -50,7 +35,7 @@ __device__ __forceinline__ void st(float4 *p, float4 v, bool nt) {
 template <bool ZERO, bool NT, int U, bool NTS = NT>
 __global__ void __launch_bounds__(256)
     k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
-             float *__restrict__ v, int64_t n, AdamScalars s) {
+             float *__restrict__ v, int64_t n, dw::AdamScalars s) {
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     float4 *p4 = reinterpret_cast<float4 *>(p);
@@ -74,10 +59,10 @@ __global__ void __launch_bounds__(256)
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i < n4) {
-                adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, s);
-                adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, s);
-                adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, s);
-                adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, s);
+                dw::adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, s);
+                dw::adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, s);
+                dw::adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, s);
+                dw::adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, s);
                 st(p4 + i, pp[u], NTS);
                 st(m4 + i, mm[u], NTS);
                 st(v4 + i, vv[u], NTS);
@@ -87,7 +72,7 @@ __global__ void __launch_bounds__(256)
     }
     for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += stride) {
-        adam_elem(p[i], g[i], m[i], v[i], s);
+        dw::adam_elem(p[i], g[i], m[i], v[i], s);
         if (ZERO) g[i] = 0.f;
     }
 }
@@ -115,7 +100,7 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
                        16 == 0,
                "dw_adam_dense: buffers must be 16-byte aligned");
     DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_adam_dense: bias_correction2_sqrt must be > 0");
-    AdamScalars s{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size,
+    dw::AdamScalars s{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size,
                   eps, weight_decay};
     int64_t blocks = ((n_elem >> 2) + 255) / 256;
     if (blocks < 1) blocks = 1;

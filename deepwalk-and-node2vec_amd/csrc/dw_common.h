@@ -87,4 +87,22 @@ __device__ __forceinline__ double wave_sum_d(double x) {
     return x;
 }
 
+// torch.optim.Adam single-tensor update of one element (dw_adam.hip; also fused into the SGNS
+// output-table pass). Scalars precomputed on the host in float64, cast to float32.
+struct AdamScalars {
+    float w1, b2, omb2, bc2s, nstep, eps, wd;
+};
+
+__device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
+                                          const AdamScalars &s) {
+    float gg = g;
+    if (s.wd != 0.f) gg = gg + s.wd * p;
+    m = fmaf(s.w1, gg - m, m);  // lerp with weight < 0.5: self + weight * (end - self)
+    v = v * s.b2;
+    v = v + s.omb2 * gg * gg;
+    const float denom = sqrtf(v) / s.bc2s + s.eps;
+    p = p + s.nstep * (m / denom);
+}
+
+
 }  // namespace dw

@@ -521,11 +521,22 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : 
 // hub rows hold thousands). A row wholly inside the chunk is summed in registers and added
 // with a plain read-modify-write (the chunk is its only writer); the first / last row of a
 // chunk may continue in the neighbouring chunk and is added with float atomics.
-template <int VPL, bool MASKED>
+// Output-table Adam fused in (ADAM, one device: dw_sgns_walks_phase2_adam): a row wholly
+// inside the chunk has its complete gradient in registers, so it is updated right there
+// (torch Adam, dw::adam_elem, the same code as dw_adam_dense) and flagged; g_out is never
+// touched for it. Boundary rows still accumulate into g_out and are updated, with the rows no
+// record touched (g = 0), by k_adam_rest.
+struct OutAdam {
+    float *p, *m, *v;
+    uint8_t *flags;
+    dw::AdamScalars s;
+};
+
+template <int VPL, bool MASKED, bool ADAM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
-                 int32_t d) {
+                 int32_t d, OutAdam oa) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t n_chunks = (n_rec + GCH - 1) / GCH;
@@ -547,9 +558,24 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         auto flush = [&](uint32_t row) {
             float *dst = g_out + static_cast<int64_t>(row) * d + lane;
             if (row != before && row != after) {
+                if (ADAM) {
+                    const int64_t o = static_cast<int64_t>(row) * d + lane;
 #pragma unroll
-                for (int m = 0; m < VPL; ++m)
-                    if (live[m]) dst[WAVE * m] += g[m];
+                    for (int m = 0; m < VPL; ++m) {
+                        if (!live[m]) continue;
+                        const int64_t i = o + WAVE * m;
+                        float pp = oa.p[i], gg = g[m], mm = oa.m[i], vv = oa.v[i];
+                        dw::adam_elem(pp, gg, mm, vv, oa.s);
+                        oa.p[i] = pp;
+                        oa.m[i] = mm;
+                        oa.v[i] = vv;
+                    }
+                    if (lane == 0) oa.flags[row] = 1;
+                } else {
+#pragma unroll
+                    for (int m = 0; m < VPL; ++m)
+                        if (live[m]) dst[WAVE * m] += g[m];
+                }
             } else {
 #pragma unroll
                 for (int m = 0; m < VPL; ++m)
@@ -729,30 +755,74 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     return DW_OK;
 }
 
+// Rows the fused gather did not update: boundary rows (g in g_out) and rows no record touched
+// (g_out = 0) — Adam with g_out, which is left zeroed. Flags are cleared afterwards.
+__global__ void __launch_bounds__(256)
+    k_adam_rest(int64_t n_rows, int32_t d, const uint8_t *__restrict__ flags,
+                float *__restrict__ g, OutAdam oa) {
+    const int64_t n = n_rows * d;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (flags[i / d]) continue;
+        float pp = oa.p[i], gg = g[i], mm = oa.m[i], vv = oa.v[i];
+        dw::adam_elem(pp, gg, mm, vv, oa.s);
+        oa.p[i] = pp;
+        oa.m[i] = mm;
+        oa.v[i] = vv;
+        g[i] = 0.f;
+    }
+}
+
+template <int VPL>
+void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const uint64_t *vals,
+                   int64_t n_rec, const float *w_in, float *g_out, int32_t d,
+                   const OutAdam *oa) {
+    const bool exact = d == 64 * VPL;
+    if (oa) {
+        if (exact)
+            hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
+                               w_in, g_out, d, *oa);
+        else
+            hipLaunchKernelGGL((k_rec_gather<VPL, true, true>), g, bl, 0, st, keys, vals, n_rec,
+                               w_in, g_out, d, *oa);
+    } else {
+        if (exact)
+            hipLaunchKernelGGL((k_rec_gather<VPL, false, false>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, OutAdam{});
+        else
+            hipLaunchKernelGGL((k_rec_gather<VPL, true, false>), g, bl, 0, st, keys, vals, n_rec,
+                               w_in, g_out, d, OutAdam{});
+    }
+}
+
+// oa != NULL: the fused output-table Adam (rows 0..V of the out table) — gather, then the
+// rest-of-rows update, then the row flags cleared.
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
-                 float *g_out, int32_t d, hipStream_t st) {
+                 float *g_out, int32_t d, const OutAdam *oa, int64_t V, hipStream_t st) {
     const int64_t n_chunks = (n_rec + GCH - 1) / GCH;
     int64_t blocks = (n_chunks + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-#define DW_GATHER_CASE(VPL)                                                                      \
-    if (d <= 64 * VPL) {                                                                          \
-        if (d == 64 * VPL)                                                                        \
-            hipLaunchKernelGGL((k_rec_gather<VPL, false>), g, bl, 0, st, keys, vals, n_rec, w_in, \
-                               g_out, d);                                                         \
-        else                                                                                      \
-            hipLaunchKernelGGL((k_rec_gather<VPL, true>), g, bl, 0, st, keys, vals, n_rec, w_in,  \
-                               g_out, d);                                                         \
-        DW_LAUNCH_CHECK("dw_sgns/gather");                                                        \
-        return DW_OK;                                                                             \
+    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
+    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
+    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
+    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
+    else return DW_E_UNSUPPORTED;
+    DW_LAUNCH_CHECK("dw_sgns/gather");
+    if (oa) {
+        int64_t rb = (V * d + 255) / 256;
+        if (rb > grid_cap(8)) rb = grid_cap(8);
+        if (rb < 1) rb = 1;
+        hipLaunchKernelGGL(k_adam_rest, dim3((unsigned)rb), dim3(256), 0, st, V, d, oa->flags,
+                           g_out, *oa);
+        DW_LAUNCH_CHECK("dw_sgns/adam_rest");
+        if (hipMemsetAsync(oa->flags, 0, static_cast<size_t>(V), st) != hipSuccess) {
+            dw::set_error("dw_sgns: flag reset failed");
+            return DW_E_HIP;
+        }
     }
-    DW_GATHER_CASE(1)
-    DW_GATHER_CASE(2)
-    DW_GATHER_CASE(4)
-    DW_GATHER_CASE(8)
-#undef DW_GATHER_CASE
-    return DW_E_UNSUPPORTED;
+    return DW_OK;
 }
 
 // Per-phase HIP-event timing of dw_sgns_* calls (bench / profiling; off by default). Each
@@ -788,12 +858,13 @@ PhaseTimer g_timer;
 // the output-table phase runs (ShardedTables.exchange_in).
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st);
+                     hipStream_t st, const OutAdam *oa);
 
 template <bool FROM_WALKS>
-int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, hipStream_t st) {
+int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, hipStream_t st,
+                const OutAdam *oa = nullptr) {
     if (phase != 2) g_timer.mark(0, st);
-    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st);
+    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st, oa);
     if (rc != DW_OK) {
         if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
         return rc;
@@ -804,8 +875,13 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, 
 
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st) {
+                     hipStream_t st, const OutAdam *oa) {
     const bool do1 = phase != 2, do2 = phase != 1;
+    if (a.batch == 0 && do2 && oa) {  // no records: every out row gets Adam with g = g_out
+        if (do1) g_timer.mark(1, st);
+        g_timer.mark(2, st);
+        return launch_pass2(nullptr, nullptr, 0, a.w_in, a.g_out, a.d, oa, a.V, st);
+    }
     if (a.batch == 0 || workspace == nullptr) {
         if (do1 && a.batch > 0) {
             const int rc = launch_pass1<FROM_WALKS, false>(a, st);
@@ -845,7 +921,7 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
         return DW_E_HIP;
     }
     g_timer.mark(2, st);
-    return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, st);
+    return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, oa, a.V, st);
 }
 
 // ---- SkipGram.forward logits and its backward (autograd path of the reference API) ----------
@@ -1069,6 +1145,34 @@ int dw_sgns_walks(const int32_t *walks, int64_t n_walks, int32_t walk_length,
     return sgns_walks(0, walks, n_walks, walk_length, context_radius, neg_samples, vocab_size,
                       dim, w_in, w_out, g_in, g_out, noise, seed, noise_offset, grad_scale,
                       loss_acc, status, workspace, workspace_bytes, stream);
+}
+
+int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                              int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                              int32_t dim, const float *w_in, float *w_out, float *g_out,
+                              float *m_out, float *v_out, uint8_t *row_flags,
+                              float one_minus_beta1, float beta2, float one_minus_beta2,
+                              float bias_correction2_sqrt, float neg_step_size, float eps,
+                              float weight_decay, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream) {
+    DW_REQUIRE(workspace && m_out && v_out && row_flags && w_out && g_out,
+               "dw_sgns_walks_phase2_adam: needs the records workspace and the Adam state");
+    DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_sgns_walks_phase2_adam: bad Adam scalars");
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0,
+               "dw_sgns_walks_phase2_adam: bad sizes");
+    DW_REQUIRE(walks && w_in && status, "dw_sgns_walks_phase2_adam: null pointer");
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out, nullptr, g_out, nullptr,
+                           0, 0, 1.f, nullptr, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    OutAdam oa{w_out, m_out, v_out, row_flags,
+               dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
+                               neg_step_size, eps, weight_decay}};
+    return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
 }
 
 int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,

@@ -69,7 +69,7 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                     seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                     loss_acc: Optional[torch.Tensor] = None,
                     status: Optional[torch.Tensor] = None, scatter: str = 'sorted',
-                    phase: int = 0) -> torch.Tensor:
+                    phase: int = 0, out_adam: Optional[dict] = None) -> torch.Tensor:
     """Launch the fused SGNS kernel(s); returns the float64[4] loss accumulator.
 
     Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B, 1];
@@ -79,6 +79,9 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
     'atomic' (float atomics straight into g_out).
     ``phase`` (walks only): 0 = the whole update; 1 = pass 1 (g_in final, loss sums, records);
     2 = the output-table phase (g_out) of the preceding phase-1 call with the same arguments.
+    ``out_adam`` (phase 2, records path, one device): ``{'m', 'v', 'flags', 'scalars'}`` — the
+    output table's Adam step is fused into the phase (w_out updated in place, g_out left zero;
+    ShardedTables.out_adam_spec()).
     """
     dev = w_in.device
     V, d = w_in.shape
@@ -108,6 +111,16 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
             scale = 1.0 / max(n_centres * C, 1) if grad_scale is None else grad_scale
             ws = workspace_for(n_centres, C, K, V, dev) \
                 if _use_records(scatter, C, K, V) else None
+            if out_adam is not None:
+                if phase != 2 or ws is None:
+                    raise ValueError('out_adam fuses the output-table Adam into phase 2 of the '
+                                     'records (sorted) path')
+                _native.call('dw_sgns_walks_phase2_adam', _native.ptr(walks), n, L, R, K, V, d,
+                             _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_out),
+                             _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
+                             _native.ptr(out_adam['flags']), *out_adam['scalars'],
+                             _native.ptr(status), _native.ptr(ws), ws.numel(), s)
+                return loss_acc
             _native.call('dw_sgns_walks_phase', int(phase), _native.ptr(walks), n, L, R, K, V, d,
                          _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_in),
                          _native.ptr(g_out), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,

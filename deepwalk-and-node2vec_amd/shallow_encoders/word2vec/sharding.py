@@ -43,17 +43,23 @@ import torch.distributed as dist
 from shallow_encoders import _native
 
 
-def hip_adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
-             lr: float, betas, eps: float, weight_decay: float, zero_grad: bool) -> None:
-    """One dense Adam step on flat fp32 buffers with torch.optim.Adam's scalar math."""
+def adam_scalars(step: int, lr: float, betas, eps: float, weight_decay: float):
+    """dw_adam_dense's scalar arguments for torch.optim.Adam step ``step`` (float64 on the host,
+    as torch computes them): (1-b1, b2, 1-b2, sqrt(bias_correction2), -lr/bias_correction1,
+    eps, weight_decay)."""
     beta1, beta2 = betas
     bias_correction1 = 1 - beta1 ** step
     bias_correction2 = 1 - beta2 ** step
-    step_size = lr / bias_correction1
+    return (1 - beta1, beta2, 1 - beta2, bias_correction2 ** 0.5, -(lr / bias_correction1), eps,
+            weight_decay)
+
+
+def hip_adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
+             lr: float, betas, eps: float, weight_decay: float, zero_grad: bool) -> None:
+    """One dense Adam step on flat fp32 buffers with torch.optim.Adam's scalar math."""
     with torch.cuda.device(p.device):
         _native.call('dw_adam_dense', _native.ptr(p), _native.ptr(g), _native.ptr(m),
-                     _native.ptr(v), p.numel(), 1 - beta1, beta2, 1 - beta2,
-                     bias_correction2 ** 0.5, -step_size, eps, weight_decay,
+                     _native.ptr(v), p.numel(), *adam_scalars(step, lr, betas, eps, weight_decay),
                      1 if zero_grad else 0, _native.stream(p.device))
 
 
@@ -86,6 +92,7 @@ class ShardedTables:
         self._ag = []          # pending all-gathers (overlapped form)
         self._cuda = self.device.type == 'cuda'
         self._side = torch.cuda.Stream(self.device) if (self._cuda and self.world > 1) else None
+        self._row_flags = None   # fused output-table Adam scratch (one device)
         if init_seed is not None:
             self.xavier_(init_seed)
 
@@ -177,8 +184,26 @@ class ShardedTables:
             self._side.wait_event(ev)
             self._ag.append(self._exchange(0, self._cur_in, self._next_in, True))
 
-    def exchange_out(self) -> None:
-        """Call right after SGNS phase 2 is enqueued (g_out final)."""
+    def out_adam_spec(self) -> Optional[dict]:
+        """For SGNS phase 2 with the output table's Adam fused in (sgns_accumulate out_adam=):
+        one device and the HIP Adam only; call after exchange_in (this step's scalars), then
+        exchange_out(fused_out=True). None where the fusion does not apply."""
+        if self.world != 1 or not self._cuda or self.adam_impl is not hip_adam:
+            return None
+        if self._row_flags is None:
+            self._row_flags = torch.zeros(self.V_pad, dtype=torch.uint8, device=self.device)
+        return {'m': self.m[1], 'v': self.v[1], 'flags': self._row_flags,
+                'scalars': adam_scalars(self.step_count, self.lr, self.betas, self.eps,
+                                        self.weight_decay)}
+
+    def exchange_out(self, fused_out: bool = False) -> None:
+        """Call right after SGNS phase 2 is enqueued (g_out final). ``fused_out``: phase 2
+        already applied the output table's Adam (out_adam_spec), only the in table remains."""
+        if self.world == 1 and fused_out:
+            self.adam_impl(self.params[0].view(-1), self.grads[0].view(-1), self.m[0].view(-1),
+                           self.v[0].view(-1), self.step_count, self.lr, self.betas, self.eps,
+                           self.weight_decay, True)
+            return
         if self.world == 1:
             self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
                            self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,

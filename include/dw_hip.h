@@ -176,6 +176,23 @@ int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
                         int32_t *status, void *workspace, size_t workspace_bytes,
                         void *stream);
 
+/* Phase 2 of dw_sgns_walks_phase fused with the output table's dense Adam step (one device):
+ * the same records sort + gather, but every out row is updated in place with torch.optim.Adam
+ * (single-tensor semantics, the scalars of dw_adam_dense) using its complete gradient —
+ * rows wholly inside one gather chunk straight from registers, the rest (chunk-boundary rows,
+ * rows without records: g = 0) from g_out. Equals phase 2 followed by dw_adam_dense(w_out,
+ * g_out, m_out, v_out, ..., zero_grad = 1); g_out must be zero on entry and is left zero;
+ * row_flags: vocab_size bytes, zero on entry, left zero. Arguments as dw_sgns_walks_phase
+ * (g_in, noise, seed, loss_acc are not used by phase 2). */
+int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                              int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                              int32_t dim, const float *w_in, float *w_out, float *g_out,
+                              float *m_out, float *v_out, uint8_t *row_flags,
+                              float one_minus_beta1, float beta2, float one_minus_beta2,
+                              float bias_correction2_sqrt, float neg_step_size, float eps,
+                              float weight_decay, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream);
+
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

@@ -36,7 +36,7 @@ SGNS_CLASSES = ('sgns_pass1', 'sgns_sort', 'sgns_pass2')
 def kernel_class(name: str):
     if 'k_sgns_g16' in name or 'k_sgns<' in name or 'k_sgns(' in name:
         return 'sgns_pass1'
-    if 'k_rec_gather' in name:
+    if 'k_rec_gather' in name or 'k_adam_rest' in name:   # pass 2 (+ the fused out-table Adam)
         return 'sgns_pass2'
     if 'radix_sort' in name or 'onesweep' in name:
         # the SGNS records sort: u32 row keys, u64 {coef, centre} values; the CSR copy sort
@@ -76,6 +76,8 @@ def main():
             ctr = r['Counter_Name']
             tot[k][ctr] += float(r['Counter_Value'])
             disp[k][ctr].add((path, r.get('Dispatch_Id', r.get('Correlation_Id', ''))))
+    fused = any('k_adam_rest' in r['Name'] for r in csv.DictReader(open(stats[0]))) \
+        if stats else False
     summary = {}
     n_calls_pmc = {}
     for k in set(tot) | set(dur):
@@ -123,6 +125,7 @@ def main():
         with open(os.path.join(PROF, 'sgns_pmc.json'), 'w') as f:
             json.dump({'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
                        'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
+                       'fused_out_adam': fused,
                        'hbm_bytes_per_launch': call['hbm_bytes'],
                        'hbm_bytes_per_kernel': per_kernel,
                        'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of '
