@@ -187,8 +187,7 @@ def main():
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
-    fuse = (not args.no_fuse_adam and args.scatter == 'sorted' and
-            tables.out_adam_spec() is not None)
+    fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
 
     def one_step(record: bool):

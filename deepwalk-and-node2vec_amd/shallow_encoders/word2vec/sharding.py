@@ -184,12 +184,18 @@ class ShardedTables:
             self._side.wait_event(ev)
             self._ag.append(self._exchange(0, self._cur_in, self._next_in, True))
 
+    def can_fuse_out_adam(self) -> bool:
+        """The output table's Adam can run inside SGNS phase 2: one device, HIP Adam."""
+        return self.world == 1 and self._cuda and self.adam_impl is hip_adam
+
     def out_adam_spec(self) -> Optional[dict]:
         """For SGNS phase 2 with the output table's Adam fused in (sgns_accumulate out_adam=):
-        one device and the HIP Adam only; call after exchange_in (this step's scalars), then
-        exchange_out(fused_out=True). None where the fusion does not apply."""
-        if self.world != 1 or not self._cuda or self.adam_impl is not hip_adam:
+        call after exchange_in (this step's scalars), then exchange_out(fused_out=True). None
+        where the fusion does not apply (can_fuse_out_adam)."""
+        if not self.can_fuse_out_adam():
             return None
+        if self.step_count < 1:
+            raise RuntimeError('out_adam_spec() before exchange_in(): no step to fuse')
         if self._row_flags is None:
             self._row_flags = torch.zeros(self.V_pad, dtype=torch.uint8, device=self.device)
         return {'m': self.m[1], 'v': self.v[1], 'flags': self._row_flags,
