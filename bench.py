@@ -334,11 +334,12 @@ def main():
     if os.path.exists(prof):
         try:
             with open(prof) as f:
-                pmc = json.load(f)
-            if (pmc.get('pairs_per_launch') == pairs_per_step and
-                    pmc.get('scatter', 'atomic') == args.scatter and
-                    pmc.get('dim', 128) == d and pmc.get('vocab_size', 1048577) == V and
-                    bool(pmc.get('fused_out_adam', False)) == fuse):
+                doc = json.load(f)
+            want = (pairs_per_step, args.scatter, d, V, fuse)
+            pmc = next((e for e in doc.get('entries', []) if
+                        (e.get('pairs_per_launch'), e.get('scatter'), e.get('dim'),
+                         e.get('vocab_size'), bool(e.get('fused_out_adam'))) == want), None)
+            if pmc is not None:
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
                 result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"
                 per_k = pmc.get('hbm_bytes_per_kernel') or {}

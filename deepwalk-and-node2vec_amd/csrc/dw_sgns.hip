@@ -756,20 +756,35 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
 }
 
 // Rows the fused gather did not update: boundary rows (g in g_out) and rows no record touched
-// (g_out = 0) — Adam with g_out, which is left zeroed. Flags are cleared afterwards.
+// (g_out = 0) — Adam with g_out, which is left zeroed. Each wave reads the flags of 64 rows in
+// one load, ballots the unflagged ones and updates only those (lane-coalesced rows), so the
+// common case at C3 — almost every row already updated — costs one byte per row.
+template <int VPL, bool MASKED>
 __global__ void __launch_bounds__(256)
     k_adam_rest(int64_t n_rows, int32_t d, const uint8_t *__restrict__ flags,
                 float *__restrict__ g, OutAdam oa) {
-    const int64_t n = n_rows * d;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (flags[i / d]) continue;
-        float pp = oa.p[i], gg = g[i], mm = oa.m[i], vv = oa.v[i];
-        dw::adam_elem(pp, gg, mm, vv, oa.s);
-        oa.p[i] = pp;
-        oa.m[i] = mm;
-        oa.v[i] = vv;
-        g[i] = 0.f;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+    for (int64_t base = (blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE) * WAVE;
+         base < n_rows; base += n_waves * WAVE) {
+        const int64_t r = base + lane;
+        unsigned long long todo = __ballot(r < n_rows && flags[r] == 0);
+        while (todo) {
+            const int l = __ffsll(static_cast<long long>(todo)) - 1;
+            todo &= todo - 1ull;
+            const int64_t o = (base + l) * d + lane;
+#pragma unroll
+            for (int m = 0; m < VPL; ++m) {
+                if (MASKED && lane + WAVE * m >= d) continue;
+                const int64_t i = o + WAVE * m;
+                float pp = oa.p[i], gg = g[i], mm = oa.m[i], vv = oa.v[i];
+                dw::adam_elem(pp, gg, mm, vv, oa.s);
+                oa.p[i] = pp;
+                oa.m[i] = mm;
+                oa.v[i] = vv;
+                g[i] = 0.f;
+            }
+        }
     }
 }
 
@@ -795,6 +810,19 @@ void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const 
     }
 }
 
+template <int VPL>
+void launch_rest(hipStream_t st, int64_t V, int32_t d, float *g_out, const OutAdam &oa) {
+    int64_t rb = (V + 255) / 256;   // 4 waves x 64 rows per block
+    if (rb > grid_cap(8)) rb = grid_cap(8);
+    if (rb < 1) rb = 1;
+    if (d == 64 * VPL)
+        hipLaunchKernelGGL((k_adam_rest<VPL, false>), dim3((unsigned)rb), dim3(256), 0, st, V, d,
+                           oa.flags, g_out, oa);
+    else
+        hipLaunchKernelGGL((k_adam_rest<VPL, true>), dim3((unsigned)rb), dim3(256), 0, st, V, d,
+                           oa.flags, g_out, oa);
+}
+
 // oa != NULL: the fused output-table Adam (rows 0..V of the out table) — gather, then the
 // rest-of-rows update, then the row flags cleared.
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
@@ -811,11 +839,10 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     else return DW_E_UNSUPPORTED;
     DW_LAUNCH_CHECK("dw_sgns/gather");
     if (oa) {
-        int64_t rb = (V * d + 255) / 256;
-        if (rb > grid_cap(8)) rb = grid_cap(8);
-        if (rb < 1) rb = 1;
-        hipLaunchKernelGGL(k_adam_rest, dim3((unsigned)rb), dim3(256), 0, st, V, d, oa->flags,
-                           g_out, *oa);
+        if (d <= 64) launch_rest<1>(st, V, d, g_out, *oa);
+        else if (d <= 128) launch_rest<2>(st, V, d, g_out, *oa);
+        else if (d <= 256) launch_rest<4>(st, V, d, g_out, *oa);
+        else launch_rest<8>(st, V, d, g_out, *oa);
         DW_LAUNCH_CHECK("dw_sgns/adam_rest");
         if (hipMemsetAsync(oa->flags, 0, static_cast<size_t>(V), st) != hipSuccess) {
             dw::set_error("dw_sgns: flag reset failed");

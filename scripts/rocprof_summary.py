@@ -8,7 +8,8 @@ Writes
                                    dispatch and per SGNS call (FETCH_SIZE / WRITE_SIZE /
                                    TCC_EA0_ATOMIC_sum passes);
   profiles/sgns_pmc.json           what bench.py reads for roofline.traffic: HBM bytes of one
-                                   dw_sgns_walks call (pass 1 + sort + pass 2).
+                                   SGNS step op (pass 1 + sort + pass 2), one entry per
+                                   workload (pairs, d, V, scatter, fused out-table Adam).
 
 Kernel classes: one dw_sgns_walks call = one pass-1 dispatch (k_sgns_g16 / k_sgns) + the hipcub
 radix-sort dispatches + one k_rec_gather dispatch, so per-call figures divide a class's total
@@ -122,15 +123,23 @@ def main():
     if ok and pairs:
         per_kernel = {k: summary[k].get('hbm_bytes_per_sgns_call') for k in SGNS_CLASSES
                       if k in summary}
-        with open(os.path.join(PROF, 'sgns_pmc.json'), 'w') as f:
-            json.dump({'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
-                       'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
-                       'fused_out_adam': fused,
-                       'hbm_bytes_per_launch': call['hbm_bytes'],
-                       'hbm_bytes_per_kernel': per_kernel,
-                       'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of '
-                               'one dw_sgns_walks call; see scripts/rocprof_summary.py'},
-                      f, indent=2)
+        entry = {'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
+                 'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
+                 'fused_out_adam': fused,
+                 'hbm_bytes_per_launch': call['hbm_bytes'],
+                 'hbm_bytes_per_kernel': per_kernel,
+                 'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of one '
+                         'SGNS step op; see scripts/rocprof_summary.py'}
+        path = os.path.join(PROF, 'sgns_pmc.json')
+        entries = []
+        if os.path.exists(path):
+            old = json.load(open(path))
+            entries = old.get('entries', [old] if 'pairs_per_launch' in old else [])
+        key = ('pairs_per_launch', 'dim', 'vocab_size', 'scatter', 'fused_out_adam')
+        entries = [e for e in entries if tuple(e.get(k) for k in key) !=
+                   tuple(entry[k] for k in key)] + [entry]
+        with open(path, 'w') as f:
+            json.dump({'entries': entries}, f, indent=2)
     print(json.dumps(summary, indent=2))
 
 
