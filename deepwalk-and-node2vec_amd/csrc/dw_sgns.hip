@@ -324,9 +324,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
 // and the coefficients come back by ds_bpermute. The centre gradient is staged in LDS and
 // added as full 256-B wave-instruction atomics; records are written by their owning lanes.
 constexpr int G16_TMAX = 64;
-#ifndef G16_DEFAULT_VARIANT
-#define G16_DEFAULT_VARIANT 0
-#endif
 #ifndef G16_MIN_WAVES
 #define G16_MIN_WAVES 4  // waves per SIMD the register allocation must allow (no spills)
 #endif
@@ -345,8 +342,8 @@ __device__ __forceinline__ float row_sum16(float x) {
     return x;
 }
 
-template <int F4, bool FROM_WALKS, int CHR, bool PF>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : G16_MIN_WAVES)
+template <int F4, bool FROM_WALKS, int CHR>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
@@ -461,24 +458,13 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, (PF || CHR >= 8) ? 3 : 
                 }
             }
         };
-        if (PF) {  // software pipeline: the next chunk is in flight while this one computes
-            float4 oA[CHR][F4], oB[CHR][F4];
-            int32_t ridA[CHR], ridB[CHR];
-            load_chunk(oA, ridA, 0);
-            for (int t0 = 0; t0 < T; t0 += 2 * CHR) {
-                if (t0 + CHR < T) load_chunk(oB, ridB, t0 + CHR);
-                compute_chunk(oA, ridA, t0);
-                if (t0 + CHR >= T) break;
-                if (t0 + 2 * CHR < T) load_chunk(oA, ridA, t0 + 2 * CHR);
-                compute_chunk(oB, ridB, t0 + CHR);
-            }
-        } else {
-            for (int t0 = 0; t0 < T; t0 += CHR) {
-                float4 o4[CHR][F4];
-                int32_t rid[CHR];
-                load_chunk(o4, rid, t0);
-                compute_chunk(o4, rid, t0);
-            }
+        // (a software-pipelined variant — next chunk in flight — and 2- / 8-row chunks measured
+        // the same on MI355X: the kernel is HBM-bound once the loss atomics were removed)
+        for (int t0 = 0; t0 < T; t0 += CHR) {
+            float4 o4[CHR][F4];
+            int32_t rid[CHR];
+            load_chunk(o4, rid, t0);
+            compute_chunk(o4, rid, t0);
         }
 #pragma unroll
         for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
@@ -676,34 +662,20 @@ int64_t grid_cap(int per_cu) {
     return (int64_t)n_cu[dev] * per_cu;
 }
 
-int chunk_rows() {  // rows in flight per wave; DW_SGNS_CHUNK=6|8|12 (tuning knob)
-    static int v = [] {
-        const char *e = getenv("DW_SGNS_CHUNK");
-        const int x = e ? atoi(e) : CHUNK;
-        return (x == 6 || x == 8 || x == 12) ? x : CHUNK;
-    }();
-    return v;
-}
-
 template <bool FROM_WALKS, bool RECORDS>
 int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    const int ch = chunk_rows();
-#define DW_SGNS_LAUNCH(VPL, M, CHV) \
-    hipLaunchKernelGGL((k_sgns<VPL, M, FROM_WALKS, RECORDS, CHV>), g, bl, 0, st, a)
 #define DW_SGNS_CASE(VPL)                                                                    \
     if (a.d <= 64 * VPL) {                                                                    \
-        const bool exact = a.d == 64 * VPL;                                                   \
-        if (ch == 6) {                                                                        \
-            if (exact) DW_SGNS_LAUNCH(VPL, false, 6); else DW_SGNS_LAUNCH(VPL, true, 6);      \
-        } else if (ch == 8) {                                                                 \
-            if (exact) DW_SGNS_LAUNCH(VPL, false, 8); else DW_SGNS_LAUNCH(VPL, true, 8);      \
-        } else {                                                                              \
-            if (exact) DW_SGNS_LAUNCH(VPL, false, 12); else DW_SGNS_LAUNCH(VPL, true, 12);    \
-        }                                                                                     \
+        if (a.d == 64 * VPL)                                                                  \
+            hipLaunchKernelGGL((k_sgns<VPL, false, FROM_WALKS, RECORDS, CHUNK>), g, bl, 0, st, \
+                               a);                                                            \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_sgns<VPL, true, FROM_WALKS, RECORDS, CHUNK>), g, bl, 0, st, \
+                               a);                                                            \
         DW_LAUNCH_CHECK("dw_sgns");                                                           \
         return DW_OK;                                                                         \
     }
@@ -712,7 +684,6 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     DW_SGNS_CASE(4)
     DW_SGNS_CASE(8)
 #undef DW_SGNS_CASE
-#undef DW_SGNS_LAUNCH
     dw::set_error("dw_sgns: dim %d > 512 is not supported", a.d);
     return DW_E_UNSUPPORTED;
 }
@@ -731,24 +702,11 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    static const int variant = [] {  // DW_G16_VARIANT (tuning, d=128): 0 4n, 1 4p, 2 8n, 3 2p
-        const char *e = getenv("DW_G16_VARIANT");
-        return e ? atoi(e) : G16_DEFAULT_VARIANT;
-    }();
-    switch (a.d / 64) {
-        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, false>), g, bl, 0, st, a); break;
-        case 2:
-            if (variant == 1)
-                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true>), g, bl, 0, st, a);
-            else if (variant == 2)
-                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 8, false>), g, bl, 0, st, a);
-            else if (variant == 3)
-                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 2, true>), g, bl, 0, st, a);
-            else
-                hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, false>), g, bl, 0, st, a);
-            break;
-        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, false>), g, bl, 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, false>), g, bl, 0, st, a); break;
+    switch (a.d / 64) {  // rows per chunk: CHR * F4 float4 registers per lane
+        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8>), g, bl, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4>), g, bl, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2>), g, bl, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1>), g, bl, 0, st, a); break;
         default: return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns/g16");
