@@ -97,3 +97,16 @@ def test_edge_classification_and_negative_sampler():
     emb = np.random.default_rng(2).normal(size=(35, 8))
     mean, best = edge_classification(emb, g, stoi, 0.5, 5, 'hadamard')
     assert 0.0 <= mean <= best <= 1.0
+
+
+def test_text_corpus_vocab_and_ids_like_reference_run_test():
+    """The reference's only test-like code, torch_dataset.py:323-336 run_test():
+    W2VDataset('test', min_word_frequency=2, context_radius=1). Expected values follow
+    torchtext 0.15's build_vocab_from_iterator rule (specials first, then by descending
+    frequency, ties alphabetical; torchtext itself is not importable here, so the rule — not
+    its code — pins this) and the collate length filter (2R + 1 = 3 tokens)."""
+    from shallow_encoders.word2vec.dataloader.torch_dataset import W2VDataset
+    ds = W2VDataset(dataset_name='test', min_word_frequency=2, context_radius=1)
+    assert ds.vocab.get_itos() == ['<unk>', 'a', 'b', 'hello', 'here', 'test', 'there', 'world']
+    assert [t.tolist() for t in ds] == [[1, 1, 0, 2, 2], [3, 7, 3, 7], [5, 4, 5, 6, 4, 6]]
+    assert ds.get_n_most_frequent_words(2) == (['a', 'b'], [1, 2])
