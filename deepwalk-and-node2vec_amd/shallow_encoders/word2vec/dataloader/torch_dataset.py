@@ -220,9 +220,13 @@ class GraphDataset(IterableDataset):
         return self._dataset.graph
 
     def get_n_most_frequent_words(self, n: int) -> Tuple[List[str], List[int]]:
-        """Every node occurs equally often in the vocabulary pass: the first n nodes by id."""
-        words = self._vocab.get_itos()[1:1 + n]
-        return words, [self._vocab[w] for w in words]
+        """The n most frequent nodes. The reference counts node visits over its random vocabulary
+        epoch of walks (torch_dataset.py:113-119); a walk visits a node about in proportion to its
+        degree, so the deterministic order here is descending degree (ties by id)."""
+        deg = np.diff(self._dataset.csr.row_ptr)
+        deg[0] = -1                                    # never <unk>
+        ids = np.lexsort((np.arange(len(deg)), -deg))[:min(n, len(deg) - 1)]
+        return [self._vocab.lookup_token(int(i)) for i in ids], [int(i) for i in ids]
 
     def sentence_pipeline(self, sentence: str, apply_filter: bool = True) -> Optional[List[str]]:
         tokens = tokenize(sentence)

@@ -2,6 +2,7 @@
 fixtures recorded from the reference (tests/golden/make_golden.py downstream), and the node /
 edge classification tasks of tools/graph_model_downstream_classification.py on synthetic
 embeddings (CPU; the trained-embedding run is in test_gpu_trainer.py)."""
+import os
 import random
 
 import networkx as nx
@@ -110,3 +111,35 @@ def test_text_corpus_vocab_and_ids_like_reference_run_test():
     assert ds.vocab.get_itos() == ['<unk>', 'a', 'b', 'hello', 'here', 'test', 'there', 'world']
     assert [t.tolist() for t in ds] == [[1, 1, 0, 2, 2], [3, 7, 3, 7], [5, 4, 5, 6, 4, 6]]
     assert ds.get_n_most_frequent_words(2) == (['a', 'b'], [1, 2])
+
+
+def test_model_analysis_tool(tmp_path):
+    """tools/model_analysis.py on a checkpoint: closest pairs (cosine of input rows vs output
+    rows), the projected-embedding figure (t-SNE when d > 2) and the graph dataset's
+    most-frequent order (by degree)."""
+    import torch
+    from shallow_encoders.config_parser import load_config
+    from tools import conventions
+    from tools import model_analysis
+    out = str(tmp_path / 'runs')
+    cfg = load_config('sge_sg_karate_club', overrides=[f'path.output_dir={out}'])
+    ds = cfg.datamodule.instantiate_dataset()
+    V = len(ds.vocab)
+    rng = np.random.default_rng(0)
+    w_in, w_out = rng.normal(size=(V, 4)).astype(np.float32), rng.normal(size=(V, 4))
+    w_out = w_out.astype(np.float32)
+    w_out[5] = w_in[3] * 2.0                     # word 3's closest context word is 5
+    ck = conventions.get_checkpoint_path(out, cfg.datamodule.dataset_name, cfg.train.experiment,
+                                         'last.ckpt')
+    os.makedirs(os.path.dirname(ck))
+    torch.save({'state_dict': {'_model._input_embedding.weight': torch.from_numpy(w_in),
+                               '_model._output_embedding.weight': torch.from_numpy(w_out)}}, ck)
+    res = model_analysis.main(['--config-name', 'sge_sg_karate_club', f'path.output_dir={out}',
+                               f'output_dir={out}'])
+    itos = ds.vocab.get_itos()
+    assert res['closest_pairs'][itos[3]][0] == itos[5]
+    assert os.path.exists(res['figure'])
+    words, ids = ds.get_n_most_frequent_words(3)
+    deg = np.diff(ds.dataset.csr.row_ptr)
+    assert list(ids) == sorted(range(1, V), key=lambda i: (-deg[i], i))[:3]
+    assert words == [itos[i] for i in ids]
