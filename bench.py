@@ -46,24 +46,6 @@ def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     return 8 * d * (1 + K) + 8 * d / (2 * R) + 8 * (1 + K) + 8 / (2 * R)
 
 
-def sgns_phase_bytes(n_walks, L, R, K, d, V, scatter, fused=False):
-    """Implementation byte model of each SGNS phase per call: rows of 4d B,
-    12-B records {row u32 | coef f32, centre u32}, one centre-gradient RMW row per centre.
-    fused: pass 2 also runs the out table's Adam (p, m, v read + written for every row) instead
-    of the g_out read-modify-write."""
-    centres = n_walks * (L - 2 * R)
-    T = 2 * R * (1 + K)
-    n_rec = centres * T
-    if scatter != 'sorted':
-        return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 8 * d * T) + n_walks * L * 4,
-                'sort': 0, 'pass2': 0}
-    bits = max(1, math.ceil(math.log2(V)))
-    touched = V * (1.0 - math.exp(-n_rec / V))   # expected distinct output rows
-    return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 12 * T) + n_walks * L * 4,
-            'sort': n_rec * (4 + 24 * math.ceil(bits / 11)),
-            'pass2': n_rec * (12 + 4 * d) + (V * d * 24 if fused else touched * 8 * d)}
-
-
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -135,6 +117,8 @@ def main():
     ap.add_argument('--no-walk-bench', action='store_true')
     ap.add_argument('--no-fuse-adam', action='store_true',
                     help='N=1: run the output table\'s Adam as its own pass (unfused)')
+    ap.add_argument('--no-overlap-in', action='store_true',
+                    help='N=1: run the in-table Adam after the output-table phase (serial)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
@@ -161,7 +145,8 @@ def main():
     from shallow_encoders import _native
     from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
     from shallow_encoders.graph.rmat import rmat_graph
-    from shallow_encoders.word2vec.sgns import loss_terms, phase_ms, phase_timing, sgns_accumulate
+    from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
+                                               sgns_phase_bytes)
     from shallow_encoders.word2vec.sharding import ShardedTables
     _native.require_device(dev)
 
@@ -177,7 +162,8 @@ def main():
         walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
-    tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0)
+    tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
+                           overlap_in=not args.no_overlap_in)
     centres = B * (L - 2 * R)
     pairs_per_step = centres * 2 * R
     grad_scale = 1.0 / (pairs_per_step * world)   # mean over the GLOBAL batch
@@ -189,6 +175,8 @@ def main():
     step_idx = [0]
     fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
+    pb = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
+    p2_bytes = pb['sort'] + pb['pass2']        # the phase the in-table Adam overlaps
 
     def one_step(record: bool):
         s = step_idx[0]
@@ -209,7 +197,7 @@ def main():
         # pass 1 (g_in final) -> in-table exchange on a side stream (N > 1) while the
         # output-table phase runs -> out-table exchange -> wait for both all-gathers
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
-        tables.exchange_in()
+        tables.exchange_in(overlap_bytes=p2_bytes)
         # one device: the output table's Adam is fused into the output-table phase
         spec = tables.out_adam_spec() if fuse else None
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,

@@ -34,11 +34,14 @@ __device__ __forceinline__ void st(float4 *p, float4 v, bool nt) {
 
 template <bool ZERO, bool NT, int U, bool NTS = NT>
 __global__ void __launch_bounds__(256)
-    k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
-             float *__restrict__ v, int64_t n, dw::AdamScalars s) {
+    k_adam(const float *p, float *pd, float *__restrict__ g, float *__restrict__ m,
+           float *__restrict__ v, int64_t n, dw::AdamScalars s) {
+    // p: parameters read; pd: parameters written (== p in place, or the other buffer of a
+    // double-buffered table)
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    float4 *p4 = reinterpret_cast<float4 *>(p);
+    const float4 *p4 = reinterpret_cast<const float4 *>(p);
+    float4 *pd4 = reinterpret_cast<float4 *>(pd);
     float4 *g4 = reinterpret_cast<float4 *>(g);
     float4 *m4 = reinterpret_cast<float4 *>(m);
     float4 *v4 = reinterpret_cast<float4 *>(v);
@@ -63,7 +66,7 @@ __global__ void __launch_bounds__(256)
                 dw::adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, s);
                 dw::adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, s);
                 dw::adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, s);
-                st(p4 + i, pp[u], NTS);
+                st(pd4 + i, pp[u], NTS);
                 st(m4 + i, mm[u], NTS);
                 st(v4 + i, vv[u], NTS);
                 if (ZERO) st(g4 + i, make_float4(0.f, 0.f, 0.f, 0.f), NTS);
@@ -72,7 +75,9 @@ __global__ void __launch_bounds__(256)
     }
     for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += stride) {
-        dw::adam_elem(p[i], g[i], m[i], v[i], s);
+        float pp = p[i];
+        dw::adam_elem(pp, g[i], m[i], v[i], s);
+        pd[i] = pp;
         if (ZERO) g[i] = 0.f;
     }
 }
@@ -89,30 +94,44 @@ __global__ void __launch_bounds__(256)
 
 extern "C" {
 
+int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, float *exp_avg,
+                     float *exp_avg_sq, int64_t n_elem, float one_minus_beta1, float beta2,
+                     float one_minus_beta2, float bias_correction2_sqrt, float neg_step_size,
+                     float eps, float weight_decay, int32_t zero_grad, int64_t max_blocks,
+                     void *stream) {
+    DW_REQUIRE(n_elem >= 0, "dw_adam_dense: negative size");
+    if (n_elem == 0) return DW_OK;
+    DW_REQUIRE(param_src && param_dst && grad && exp_avg && exp_avg_sq,
+               "dw_adam_dense: null pointer");
+    DW_REQUIRE(((uintptr_t)param_src | (uintptr_t)param_dst | (uintptr_t)grad |
+                (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+               "dw_adam_dense: buffers must be 16-byte aligned");
+    DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_adam_dense: bias_correction2_sqrt must be > 0");
+    dw::AdamScalars s{one_minus_beta1, beta2,         one_minus_beta2, bias_correction2_sqrt,
+                      neg_step_size,   eps,           weight_decay};
+    int64_t blocks = ((n_elem >> 2) + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond
+    if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+    if (zero_grad)
+        hipLaunchKernelGGL((k_adam<true, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param_src, param_dst, grad, exp_avg,
+                           exp_avg_sq, n_elem, s);
+    else
+        hipLaunchKernelGGL((k_adam<false, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param_src, param_dst, grad, exp_avg,
+                           exp_avg_sq, n_elem, s);
+    DW_LAUNCH_CHECK("dw_adam_dense");
+    return DW_OK;
+}
+
 int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n_elem,
                   float one_minus_beta1, float beta2, float one_minus_beta2,
                   float bias_correction2_sqrt, float neg_step_size, float eps,
                   float weight_decay, int32_t zero_grad, void *stream) {
-    DW_REQUIRE(n_elem >= 0, "dw_adam_dense: negative size");
-    if (n_elem == 0) return DW_OK;
-    DW_REQUIRE(param && grad && exp_avg && exp_avg_sq, "dw_adam_dense: null pointer");
-    DW_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) %
-                       16 == 0,
-               "dw_adam_dense: buffers must be 16-byte aligned");
-    DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_adam_dense: bias_correction2_sqrt must be > 0");
-    dw::AdamScalars s{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size,
-                  eps, weight_decay};
-    int64_t blocks = ((n_elem >> 2) + 255) / 256;
-    if (blocks < 1) blocks = 1;
-    if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond
-    if (zero_grad)
-        hipLaunchKernelGGL((k_adam<true, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
-                           dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
-    else
-        hipLaunchKernelGGL((k_adam<false, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
-                           dw::as_stream(stream), param, grad, exp_avg, exp_avg_sq, n_elem, s);
-    DW_LAUNCH_CHECK("dw_adam_dense");
-    return DW_OK;
+    return dw_adam_dense_to(param, param, grad, exp_avg, exp_avg_sq, n_elem, one_minus_beta1,
+                            beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size, eps,
+                            weight_decay, zero_grad, 0, stream);
 }
 
 int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream) {

@@ -95,6 +95,9 @@ struct AdamScalars {
 
 __device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
                                           const AdamScalars &s) {
+    // No implicit FMA contraction: each element rounds the same way whichever unrolled slot,
+    // grid size or fused kernel (k_rec_gather) updates it; the lerp's fmaf is explicit.
+#pragma clang fp contract(off)
     float gg = g;
     if (s.wd != 0.f) gg = gg + s.wd * p;
     m = fmaf(s.w1, gg - m, m);  // lerp with weight < 0.5: self + weight * (end - self)

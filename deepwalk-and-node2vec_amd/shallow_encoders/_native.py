@@ -89,6 +89,8 @@ SIGNATURES = {
                                                    _p, _p, _p, _p]),
     'dw_adam_dense': (ctypes.c_int, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _f32,
                                      _f32, _i32, _p]),
+    'dw_adam_dense_to': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32,
+                                         _f32, _f32, _i32, _i64, _p]),
     'dw_scale': (ctypes.c_int, [_p, _i64, _f32, _p, _p]),
 }
 

@@ -13,6 +13,7 @@ Two call styles:
   * ``SGNSLoss.apply(...)``: an autograd Function returning the loss, for callers that drive
     ``loss.backward()`` themselves (e.g. a Lightning loop).
 """
+import math
 from typing import Dict, Optional
 
 import torch
@@ -194,6 +195,25 @@ def renorm_(weight: torch.Tensor, ids: torch.Tensor, max_norm: float,
                      _native.stream(weight.device))
     if status is None:
         _native.check_status(st, 'embedding renorm')
+
+
+def sgns_phase_bytes(n_walks: int, L: int, R: int, K: int, d: int, V: int, scatter: str,
+                     fused: bool = False) -> Dict[str, float]:
+    """Implementation byte model of each SGNS phase per call of dw_sgns_walks: rows of 4d B,
+    12-B records {row u32 | coef f32, centre u32}, one centre-gradient RMW row per centre.
+    fused: pass 2 also runs the out table's Adam (p, m, v read + written for every row) instead
+    of the g_out read-modify-write."""
+    centres = n_walks * (L - 2 * R)
+    T = 2 * R * (1 + K)
+    n_rec = centres * T
+    if scatter != 'sorted':
+        return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 8 * d * T) + n_walks * L * 4,
+                'sort': 0, 'pass2': 0}
+    bits = max(1, math.ceil(math.log2(V)))
+    touched = V * (1.0 - math.exp(-n_rec / V))   # expected distinct output rows
+    return {'pass1': centres * (4 * d * (1 + T) + 8 * d + 12 * T) + n_walks * L * 4,
+            'sort': n_rec * (4 + 24 * math.ceil(bits / 11)),
+            'pass2': n_rec * (12 + 4 * d) + (V * d * 24 if fused else touched * 8 * d)}
 
 
 def phase_timing(enable: bool) -> None:

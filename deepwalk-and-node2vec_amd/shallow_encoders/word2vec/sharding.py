@@ -9,7 +9,8 @@ communication, because walks are keyed by the global walk id.
 Layout (S = V_pad / world rows; rank r owns rows [r*S, (r+1)*S) of BOTH tables):
 
   params  float32 [2 or 3, V_pad, d]   slot 1 = out table; slot 0 = in table, and slot 2 =
-                                       its second buffer when world > 1 (see below)
+                                       its second buffer when world > 1 or, on one GPU, when
+                                       the in-table Adam overlaps (see below)
   grads   float32 [2, V_pad, d]        local dense gradients (in, out)
   m, v    float32 [2, S, d]            Adam state of this rank's rows only
 
@@ -29,6 +30,11 @@ Overlapped form (``exchange_in`` / ``exchange_out`` / ``sync``):
   * ``exchange_out`` does the out table after phase 2.
   * ``sync`` makes the main stream wait for both all-gathers before the next pass 1.
 ``step()`` is the same update done serially.
+
+On one GPU there is nothing to exchange, but the in-table Adam (1/2 of the optimizer traffic) still
+overlaps the output-table phase the same way (``overlap_in``, default on with the HIP Adam):
+``exchange_in`` runs dw_adam_dense_to from the current in table into the idle buffer on the side
+stream, and the radix sort of that phase leaves the HBM bandwidth it needs.
 
 The Adam update is injectable (``adam_impl``), so the exchange logic can be tested with gloo
 on the CPU (there the overlapped form runs its collectives synchronously). The default is the
@@ -63,13 +69,47 @@ def hip_adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      1 if zero_grad else 0, _native.stream(p.device))
 
 
+def hip_adam_to(p_src: torch.Tensor, p_dst: torch.Tensor, g: torch.Tensor, m: torch.Tensor,
+                v: torch.Tensor, step: int, lr: float, betas, eps: float, weight_decay: float,
+                zero_grad: bool, max_blocks: int = 0) -> None:
+    """hip_adam reading the parameters from p_src and writing them to p_dst (dw_adam_dense_to);
+    max_blocks > 0 caps the grid."""
+    assert p_src.numel() == p_dst.numel() == g.numel() == m.numel() == v.numel()
+    with torch.cuda.device(p_src.device):
+        _native.call('dw_adam_dense_to', _native.ptr(p_src), _native.ptr(p_dst), _native.ptr(g),
+                     _native.ptr(m), _native.ptr(v), p_src.numel(),
+                     *adam_scalars(step, lr, betas, eps, weight_decay), 1 if zero_grad else 0,
+                     int(max_blocks), _native.stream(p_src.device))
+
+
+# One GPU, in-table Adam on the side stream: its grid is sized so that it just finishes inside
+# the overlapped phase (records sort + gather) and leaves the other CUs to that phase. The sort
+# is latency-bound (~2 TB/s); a full-grid Adam takes every CU and doubles it, one capped to the
+# rate it needs fills the unused bandwidth instead. Constants measured on MI355X at C3
+# (profiles/r01_overlap_sweep.txt): the phase runs at ~5 TB/s of its byte model; one 256-thread
+# Adam block moves ~22 GB/s next to it; 25% margin.
+OVERLAP_PHASE_BPS = 5.0e12
+ADAM_BLOCK_BPS = 22e9
+OVERLAP_MARGIN = 1.25
+
+
+def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> int:
+    """Grid cap for an Adam of ``adam_bytes`` overlapping a phase of ``overlap_bytes``
+    (0 = full grid, when no estimate is given)."""
+    if not overlap_bytes:
+        return 0
+    t = overlap_bytes / OVERLAP_PHASE_BPS
+    need = OVERLAP_MARGIN * adam_bytes / t / ADAM_BLOCK_BPS
+    return int(min(8192, max(32, math.ceil(need))))
+
+
 class ShardedTables:
     """In/out embedding tables + dense gradients + node-range-sharded Adam state."""
 
     def __init__(self, vocab_size: int, dim: int, device, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  group=None, init_seed: Optional[int] = 0,
-                 adam_impl: Optional[Callable] = None):
+                 adam_impl: Optional[Callable] = None, overlap_in: Optional[bool] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -80,7 +120,13 @@ class ShardedTables:
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.adam_impl = adam_impl or hip_adam
         self.step_count = 0
-        n_slots = 3 if self.world > 1 else 2
+        self._cuda = self.device.type == 'cuda'
+        if overlap_in is None:
+            overlap_in = True
+        # one GPU: the in-table Adam overlaps only with the HIP kernel (out of place)
+        self.overlap_in = bool(overlap_in and self.world == 1 and self._cuda
+                               and self.adam_impl is hip_adam)
+        n_slots = 3 if (self.world > 1 or self.overlap_in) else 2
         self.params = torch.zeros((n_slots, self.V_pad, self.d), dtype=torch.float32,
                                   device=self.device)
         self.grads = torch.zeros((2, self.V_pad, self.d), dtype=torch.float32, device=self.device)
@@ -89,9 +135,9 @@ class ShardedTables:
         self.grad_shard = torch.empty_like(self.m) if self.world > 1 else None
         self._cur_in = 0
         self._next_in = 0
-        self._ag = []          # pending all-gathers (overlapped form)
-        self._cuda = self.device.type == 'cuda'
-        self._side = torch.cuda.Stream(self.device) if (self._cuda and self.world > 1) else None
+        self._ag = []          # pending all-gathers / side-stream events (overlapped form)
+        self._side = (torch.cuda.Stream(self.device)
+                      if (self._cuda and (self.world > 1 or self.overlap_in)) else None)
         self._row_flags = None   # fused output-table Adam scratch (one device)
         if init_seed is not None:
             self.xavier_(init_seed)
@@ -134,6 +180,16 @@ class ShardedTables:
         self.adam_impl(p, g, self.m[t].view(-1), self.v[t].view(-1), self.step_count, self.lr,
                        self.betas, self.eps, self.weight_decay, zero_grad)
 
+    def _adam_both(self) -> None:
+        """One device: Adam on both tables in place (one launch when they are adjacent)."""
+        if self.params.shape[0] == 2 and self._cur_in == 0:
+            self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
+                           self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
+                           self.weight_decay, True)
+            return
+        self._adam(self.params[self._cur_in].view(-1), self.grads[0].view(-1), 0, True)
+        self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
+
     def _exchange(self, t: int, src_slot: int, dst_slot: int, async_op: bool):
         """reduce-scatter grads[t] -> Adam on own rows of params[dst_slot] (starting from
         params[src_slot]) -> all-gather into params[dst_slot]; grads[t] ends zeroed.
@@ -160,21 +216,34 @@ class ShardedTables:
         self.sync()
         self.step_count += 1
         if self.world == 1:
-            self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
-                           self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
-                           self.weight_decay, True)
+            self._adam_both()
             return
         self._exchange(0, self._cur_in, self._cur_in, False)
         self._exchange(1, 1, 1, False)
 
     # ---- overlapped step --------------------------------------------------------------------------
-    def exchange_in(self) -> None:
+    def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
         """Call right after SGNS pass 1 is enqueued (g_in final): the in-table update starts on a
-        side stream while the output-table phase runs on the current stream."""
+        side stream while the output-table phase runs on the current stream. ``overlap_bytes``
+        (one GPU): HBM bytes of that phase (sgns_phase_bytes sort + pass2), to size the Adam's
+        grid (overlap_adam_blocks); None = full grid."""
         self.step_count += 1
-        if self.world == 1:
-            return                              # nothing to overlap: exchange_out does Adam
+        if self.world == 1 and not self.overlap_in:
+            return                              # exchange_out does the Adam
         self._next_in = 2 - self._cur_in
+        if self.world == 1:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(ev)
+                blocks = overlap_adam_blocks(self.V_pad * self.d * 4 * 7, overlap_bytes)
+                hip_adam_to(self.params[self._cur_in], self.params[self._next_in],
+                            self.grads[0], self.m[0], self.v[0], self.step_count, self.lr,
+                            self.betas, self.eps, self.weight_decay, True, blocks)
+                done = torch.cuda.Event()
+                done.record(self._side)
+            self._ag.append(done)
+            return
         if not self._cuda:
             self._exchange(0, self._cur_in, self._next_in, False)
             return
@@ -205,15 +274,15 @@ class ShardedTables:
     def exchange_out(self, fused_out: bool = False) -> None:
         """Call right after SGNS phase 2 is enqueued (g_out final). ``fused_out``: phase 2
         already applied the output table's Adam (out_adam_spec), only the in table remains."""
+        if self.world == 1 and self.overlap_in:
+            if not fused_out:       # the in table is done on the side stream (exchange_in)
+                self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
+            return
         if self.world == 1 and fused_out:
-            self.adam_impl(self.params[0].view(-1), self.grads[0].view(-1), self.m[0].view(-1),
-                           self.v[0].view(-1), self.step_count, self.lr, self.betas, self.eps,
-                           self.weight_decay, True)
+            self._adam(self.params[self._cur_in].view(-1), self.grads[0].view(-1), 0, True)
             return
         if self.world == 1:
-            self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
-                           self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
-                           self.weight_decay, True)
+            self._adam_both()
             return
         if not self._cuda:
             self._exchange(1, 1, 1, False)
@@ -228,6 +297,9 @@ class ShardedTables:
         """The current stream waits for pending all-gathers; the new in table becomes current.
         Call before the next SGNS pass 1 (and before reading the tables)."""
         for w in self._ag:
-            w.wait()
+            if isinstance(w, torch.cuda.Event):
+                torch.cuda.current_stream(self.device).wait_event(w)
+            else:
+                w.wait()
         self._ag = []
         self._cur_in = self._next_in

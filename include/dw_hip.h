@@ -285,6 +285,17 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
                   float bias_correction2_sqrt, float neg_step_size, float eps,
                   float weight_decay, int32_t zero_grad, void *stream);
 
+/* dw_adam_dense reading the parameters from param_src and writing them to param_dst (the other
+ * buffer of a double-buffered table, so readers of the current values can run concurrently);
+ * param_src == param_dst is dw_adam_dense. max_blocks > 0 caps the grid (256-thread blocks,
+ * grid-stride): a concurrent kernel on another stream keeps the rest of the CUs; <= 0 = the
+ * full grid. */
+int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, float *exp_avg,
+                     float *exp_avg_sq, int64_t n_elem, float one_minus_beta1, float beta2,
+                     float one_minus_beta2, float bias_correction2_sqrt, float neg_step_size,
+                     float eps, float weight_decay, int32_t zero_grad, int64_t max_blocks,
+                     void *stream);
+
 /* Scale a float32 buffer in place: x *= alpha * (*alpha_dev) (alpha_dev NULL -> 1). Used by the
  * autograd path to apply the device-resident grad_output without a host synchronisation. */
 int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream);

@@ -155,6 +155,66 @@ def test_adam_kernel_vs_torch_adam_random_grads(hip_device):
                                ropt.state[ref]['exp_avg_sq'].numpy(), rtol=1e-5, atol=1e-10)
 
 
+@pytest.mark.parametrize('max_blocks', [0, 32, 47])
+def test_adam_dense_to_equals_in_place(hip_device, max_blocks):
+    """dw_adam_dense_to (read one buffer, write another; capped grid-stride grids) is
+    bit-identical to the in-place dw_adam_dense and leaves the source untouched; both zero the
+    gradient."""
+    from shallow_encoders.word2vec.sharding import hip_adam, hip_adam_to
+    rng = np.random.default_rng(1)
+    n = 4096 * 64 + 7
+    p0, g0, m0, v0 = (rng.standard_normal(n).astype(np.float32) for _ in range(4))
+    v0 = np.abs(v0)
+    a = [_dev(x, torch.float32) for x in (p0, g0, m0, v0)]
+    b = [_dev(x, torch.float32) for x in (p0, g0, m0, v0)]
+    dst = torch.full_like(b[0], float('nan'))
+    hp = (3, 0.01, (0.9, 0.999), 1e-8, 0.01)
+    hip_adam(*a, *hp, True)
+    hip_adam_to(b[0], dst, b[1], b[2], b[3], *hp, True, max_blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, a[0])
+    assert torch.equal(b[0].cpu(), torch.tensor(p0))
+    for x, y in zip(a[1:], b[1:]):
+        assert torch.equal(x, y)
+    assert float(b[1].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize('fuse', [True, False])
+def test_overlapped_in_table_adam_equals_serial(hip_device, fuse):
+    """One GPU: the in-table Adam on the side stream into the second buffer (overlap_in) gives
+    the tables of the serial in-place update, with and without the fused out-table Adam."""
+    from shallow_encoders.graph.random_walk_generator import DeepWalk
+    from shallow_encoders.graph.rmat import rmat_graph
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    csr = rmat_graph(12, 40_000, 0, device=hip_device)
+    walker = DeepWalk(csr, 40, rng='philox', seed=3, device=hip_device)
+    V, R, K, nw, d = csr.vocab_size, 3, 4, 256, 128
+    ov = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5, overlap_in=True)
+    se = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5, overlap_in=False)
+    assert ov.overlap_in and not se.overlap_in and ov.params.shape[0] == 3
+    for step in range(4):
+        starts = torch.randint(1, V, (nw,), generator=torch.Generator().manual_seed(step),
+                               dtype=torch.int32).to(hip_device)
+        walks = walker.walk_batch(starts, walk_id0=step * nw)
+        for t in (ov, se):
+            kw = dict(walks=walks, context_radius=R, seed=7, noise_offset=step * nw * 34)
+            sgns_accumulate(t.w_in, t.w_out, t.g_in, t.g_out, K, phase=1, **kw)
+            t.exchange_in()
+            spec = t.out_adam_spec() if fuse else None
+            sgns_accumulate(t.w_in, t.w_out, t.g_in, t.g_out, K, phase=2, out_adam=spec, **kw)
+            t.exchange_out(fused_out=fuse)
+            t.sync()
+    torch.cuda.synchronize()
+    assert ov._cur_in == 0 and float(ov.grads.abs().max()) == 0.0
+    for a, b in ((ov.w_in, se.w_in), (ov.w_out, se.w_out)):
+        assert_params_close(a.cpu().numpy(), b.cpu().numpy(), 0.02, max_frac=5e-3,
+                            max_abs=2.05 * 0.02 * 4)
+    # the serial step() path on the 3-slot layout
+    ov.step()
+    torch.cuda.synchronize()
+    assert float(ov.grads.abs().max()) == 0.0
+
+
 @pytest.mark.parametrize('d,hub', [(100, False), (128, False), (256, False), (300, False),
                                    (128, True), (64, True)])
 def test_fused_sgns_random_case_vs_oracle(d, hub, hip_device):
