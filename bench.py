@@ -147,7 +147,7 @@ def main():
     from shallow_encoders.graph.rmat import rmat_graph
     from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
                                                sgns_phase_bytes)
-    from shallow_encoders.word2vec.sharding import ShardedTables
+    from shallow_encoders.word2vec.sharding import ShardedTables, overlap_adam_blocks
     _native.require_device(dev)
 
     t0 = time.time()
@@ -246,7 +246,12 @@ def main():
     # algorithmic bytes of the timed op: SURVEY §8d's per-pair SGNS figure, plus its dense-Adam
     # figure for one table (V*d*4 B x 7) when the out table's Adam is fused into pass 2
     out_adam_bytes = V * d * 4 * 7 if fuse else 0
-    sgns_gbs = (pairs_per_step * bpp + out_adam_bytes) / (sgns_ms * 1e-3) / 1e9
+    # one GPU, overlap_in: the in-table Adam (the other V*d*4 B x 7) runs on a side stream
+    # inside the output-table phase; the window then ends when both streams are done
+    overlap_in = world == 1 and tables.overlap_in
+    in_adam_bytes = V * d * 4 * 7 if overlap_in else 0
+    op_ms = sgns_ms + (kern_ms['adam'] if overlap_in else 0.0)
+    sgns_gbs = (pairs_per_step * bpp + out_adam_bytes + in_adam_bytes) / (op_ms * 1e-3) / 1e9
     phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     phase_info = {k: {'ms': phases[k], 'bytes_model': phase_bytes[k],
                       'GBps': phase_bytes[k] / (phases[k] * 1e-3) / 1e9 if phases[k] else None}
@@ -306,14 +311,17 @@ def main():
         'roofline': {
             'kernel': (('dw_sgns_walks_phase 1 + dw_sgns_walks_phase2_adam = k_sgns_g16 + rocprim '
                         'onesweep radix sort + k_rec_gather with the out-table Adam fused + '
-                        'k_adam_rest') if fuse else
+                        'k_adam_rest' + (' || in-table k_adam (dw_adam_dense_to, side stream)'
+                                         if overlap_in else '')) if fuse else
                        'dw_sgns_walks = k_sgns_g16 + rocprim onesweep radix sort + k_rec_gather'
                        if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
             'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,
-            'out_table_adam_bytes': out_adam_bytes,
-            'ms_per_launch': sgns_ms, 'launches_timed': phases['calls'],
+            'out_table_adam_bytes': out_adam_bytes, 'in_table_adam_bytes': in_adam_bytes,
+            'in_table_adam_blocks': (overlap_adam_blocks(V * d * 4 * 7, p2_bytes)
+                                     if overlap_in else None),
+            'ms_per_launch': op_ms, 'launches_timed': phases['calls'],
             'phases': phase_info,
         },
         'cpu_baseline': None,
@@ -323,10 +331,11 @@ def main():
         try:
             with open(prof) as f:
                 doc = json.load(f)
-            want = (pairs_per_step, args.scatter, d, V, fuse)
+            want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in)
             pmc = next((e for e in doc.get('entries', []) if
                         (e.get('pairs_per_launch'), e.get('scatter'), e.get('dim'),
-                         e.get('vocab_size'), bool(e.get('fused_out_adam'))) == want), None)
+                         e.get('vocab_size'), bool(e.get('fused_out_adam')),
+                         bool(e.get('overlap_in'))) == want), None)
             if pmc is not None:
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
                 result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output (gpurun_out/prof_*) into profiles/ (committed evidence).
 
-    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch [dim vocab_size]]
+    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch [dim vocab_size [overlap_in]]]
 
 Writes
   profiles/<tag>_kernel_stats.csv  rocprofv3 --stats, verbatim;
@@ -9,7 +9,9 @@ Writes
                                    TCC_EA0_ATOMIC_sum passes);
   profiles/sgns_pmc.json           what bench.py reads for roofline.traffic: HBM bytes of one
                                    SGNS step op (pass 1 + sort + pass 2), one entry per
-                                   workload (pairs, d, V, scatter, fused out-table Adam).
+                                   workload (pairs, d, V, scatter, fused out-table Adam,
+                                   overlap_in: the in-table k_adam runs inside the op on a
+                                   side stream and its bytes count, one dispatch per step).
 
 Kernel classes: one dw_sgns_walks call = one pass-1 dispatch (k_sgns_g16 / k_sgns) + the hipcub
 radix-sort dispatches + one k_rec_gather dispatch, so per-call figures divide a class's total
@@ -55,6 +57,7 @@ def main():
     pairs = int(sys.argv[2]) if len(sys.argv) > 2 else None
     dim = int(sys.argv[3]) if len(sys.argv) > 3 else 128          # C3 defaults
     vocab = int(sys.argv[4]) if len(sys.argv) > 4 else 1048577
+    overlap_in = bool(int(sys.argv[5])) if len(sys.argv) > 5 else True
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, 'prof_trace', '**', '*kernel_stats.csv'), recursive=True)
     dur = collections.defaultdict(lambda: [0, 0.0])   # class -> [calls, total ns]
@@ -103,7 +106,8 @@ def main():
     calls_trace = p1.get('trace_dispatches', 0)
     call = {'ms': 0.0, 'hbm_bytes': 0.0}
     ok = calls_trace > 0
-    for k in SGNS_CLASSES:
+    op_classes = SGNS_CLASSES + (('k_adam',) if overlap_in else ())
+    for k in op_classes:
         e = summary.get(k)
         if not e:
             continue
@@ -121,11 +125,11 @@ def main():
     with open(os.path.join(PROF, f'{tag}_pmc.json'), 'w') as f:
         json.dump(summary, f, indent=2)
     if ok and pairs:
-        per_kernel = {k: summary[k].get('hbm_bytes_per_sgns_call') for k in SGNS_CLASSES
+        per_kernel = {k: summary[k].get('hbm_bytes_per_sgns_call') for k in op_classes
                       if k in summary}
         entry = {'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
                  'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
-                 'fused_out_adam': fused,
+                 'fused_out_adam': fused, 'overlap_in': overlap_in,
                  'hbm_bytes_per_launch': call['hbm_bytes'],
                  'hbm_bytes_per_kernel': per_kernel,
                  'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of one '
@@ -135,7 +139,7 @@ def main():
         if os.path.exists(path):
             old = json.load(open(path))
             entries = old.get('entries', [old] if 'pairs_per_launch' in old else [])
-        key = ('pairs_per_launch', 'dim', 'vocab_size', 'scatter', 'fused_out_adam')
+        key = ('pairs_per_launch', 'dim', 'vocab_size', 'scatter', 'fused_out_adam', 'overlap_in')
         entries = [e for e in entries if tuple(e.get(k) for k in key) !=
                    tuple(entry[k] for k in key)] + [entry]
         with open(path, 'w') as f:
