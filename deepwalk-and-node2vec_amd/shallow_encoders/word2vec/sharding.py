@@ -74,12 +74,18 @@ def hip_adam_to(p_src: torch.Tensor, p_dst: torch.Tensor, g: torch.Tensor, m: to
                 zero_grad: bool, max_blocks: int = 0) -> None:
     """hip_adam reading the parameters from p_src and writing them to p_dst (dw_adam_dense_to);
     max_blocks > 0 caps the grid."""
+    adam_to_scalars(p_src, p_dst, g, m, v, adam_scalars(step, lr, betas, eps, weight_decay),
+                    zero_grad, max_blocks)
+
+
+def adam_to_scalars(p_src: torch.Tensor, p_dst: torch.Tensor, g: torch.Tensor, m: torch.Tensor,
+                    v: torch.Tensor, scalars: tuple, zero_grad: bool, max_blocks: int = 0) -> None:
+    """dw_adam_dense_to with precomputed scalars (adam_scalars order), on the current stream."""
     assert p_src.numel() == p_dst.numel() == g.numel() == m.numel() == v.numel()
     with torch.cuda.device(p_src.device):
         _native.call('dw_adam_dense_to', _native.ptr(p_src), _native.ptr(p_dst), _native.ptr(g),
-                     _native.ptr(m), _native.ptr(v), p_src.numel(),
-                     *adam_scalars(step, lr, betas, eps, weight_decay), 1 if zero_grad else 0,
-                     int(max_blocks), _native.stream(p_src.device))
+                     _native.ptr(m), _native.ptr(v), p_src.numel(), *scalars,
+                     1 if zero_grad else 0, int(max_blocks), _native.stream(p_src.device))
 
 
 # One GPU, in-table Adam on the side stream: its grid is sized so that it just finishes inside

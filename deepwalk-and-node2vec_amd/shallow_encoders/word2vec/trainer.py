@@ -18,6 +18,18 @@ Gradient delivery:
   * ``manual_grads = False`` (default; a Lightning-style loop calling ``loss.backward()``):
     the returned ``loss`` carries a grad_fn whose backward hands over the same gradients.
 
+Fused step (``manual_grads`` + walk batches + the HIP Adam holding exactly the two tables, one
+device, records path): ``training_step`` also applies the optimizer update, the way bench.py's
+step does. The three pieces run as follows:
+  * SGNS pass 1 runs first, after which the input-table gradient is final.
+  * The input table's Adam then runs on a side stream, out of place into the table's second
+    buffer, overlapping the output-table phase, which still reads the current input table.
+  * The output table's Adam is fused into that phase's records gather
+    (dw_sgns_walks_phase2_adam).
+The optimizer's ``step()`` that follows is then a no-op for the two tables (Adam.begin_fused_step).
+Same update as SGNS + ``optimizer.step()`` up to float-atomic summation order
+(test_gpu_trainer.py::test_fused_trainer_step_equals_unfused).
+
 Noise: ``noise='torch'`` draws the reference's uniform negatives with torch's global CPU
 generator (generate_noise_batch, exact under ``torch.manual_seed``); ``noise='device'`` draws
 the same law on the device (Philox keyed by ``seed`` and the running centre counter).
@@ -32,8 +44,8 @@ from torch.optim import Optimizer
 
 from shallow_encoders import _native
 from shallow_encoders.word2vec.model import W2VBase
-from shallow_encoders.word2vec.sgns import (SGNSLoss, device_noise, loss_terms, renorm_,
-                                            sgns_accumulate)
+from shallow_encoders.word2vec.sgns import (SGNSLoss, _use_records, device_noise, loss_terms,
+                                            renorm_, sgns_accumulate, sgns_phase_bytes)
 from shallow_encoders.word2vec.utils import torch_helper
 from shallow_encoders.word2vec.utils.meter import MetricMeter
 from shallow_encoders.word2vec.utils.sampling import generate_noise_batch
@@ -67,6 +79,8 @@ class Word2VecTrainer(_Base):
         self._context_radius = context_radius
         self.manual_grads = False
         self.logged: Dict[str, object] = {}
+        self._side = None          # side stream of the fused step (input-table Adam)
+        self._row_flags = None     # fused output-table Adam scratch
 
     # ---- reference properties -------------------------------------------------------------
     @property
@@ -170,7 +184,9 @@ class Word2VecTrainer(_Base):
             for p in (w_in, w_out):
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
-            if targets is None:
+            if targets is None and self._can_fuse_step(w_in, w_out, C):
+                acc = self._fused_walk_step(w_in, w_out, src, R, noise, offset)
+            elif targets is None:
                 acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
                                       self._neg_samples, walks=src, context_radius=R, noise=noise,
                                       seed=self._seed, noise_offset=offset)
@@ -191,6 +207,53 @@ class Word2VecTrainer(_Base):
         self._meter.push('train-metrics/recall', recall)
         self._meter.push('train-metrics/precision', precision)
         return loss
+
+    # ---- fused step -----------------------------------------------------------------------------
+    def _can_fuse_step(self, w_in, w_out, n_ctx: int) -> bool:
+        from shallow_encoders.word2vec.optim import Adam
+        opt = self._optimizer
+        return (isinstance(opt, Adam) and w_in.device.type == 'cuda'
+                and _use_records('sorted', n_ctx, self._neg_samples, w_in.shape[0])
+                and opt.can_fuse([w_in, w_out]))
+
+    def _fused_walk_step(self, w_in, w_out, walks, R: int, noise, offset: int) -> torch.Tensor:
+        """Pass 1 -> input-table Adam on the side stream (into the second buffer) || output-table
+        phase with its Adam fused -> join -> swap the input table's buffers."""
+        from shallow_encoders.word2vec.sharding import adam_to_scalars, overlap_adam_blocks
+        opt = self._optimizer
+        (st_in, sc_in), (st_out, sc_out) = opt.begin_fused_step([w_in, w_out])
+        dev = w_in.device
+        K = self._neg_samples
+        V, d = w_in.shape
+        n, L = walks.shape
+        kw = dict(walks=walks, context_radius=R, noise=noise, seed=self._seed,
+                  noise_offset=offset)
+        acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad, K,
+                              phase=1, **kw)
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        if self._row_flags is None or self._row_flags.numel() != V or \
+                self._row_flags.device != dev:
+            self._row_flags = torch.zeros(V, dtype=torch.uint8, device=dev)
+        alt = opt.alt_buffer(w_in)
+        main = torch.cuda.current_stream(dev)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        pb = sgns_phase_bytes(n, L, R, K, d, V, 'sorted', True)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            adam_to_scalars(w_in.detach(), alt, w_in.grad, st_in['exp_avg'],
+                            st_in['exp_avg_sq'], sc_in, True,
+                            overlap_adam_blocks(V * d * 4 * 7, pb['sort'] + pb['pass2']))
+            done = torch.cuda.Event()
+            done.record(self._side)
+        sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad, K, phase=2,
+                        loss_acc=acc,
+                        out_adam={'m': st_out['exp_avg'], 'v': st_out['exp_avg_sq'],
+                                  'flags': self._row_flags, 'scalars': sc_out}, **kw)
+        main.wait_event(done)
+        opt.swap_alt(w_in)
+        return acc
 
     def on_train_epoch_end(self) -> Dict[str, float]:
         """Log the epoch means; one host synchronisation per epoch (NaN check included)."""

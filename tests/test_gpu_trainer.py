@@ -150,3 +150,50 @@ def test_text_word2vec_abcde(tmp_path, hip_device, config, mode):
     o = {t: w_out[vocab[t]] for t in 'abcd'}
     assert np.dot(i['a'], o['b']) > np.dot(i['a'], o['c'])
     assert np.dot(i['c'], o['d']) > np.dot(i['c'], o['a'])
+
+
+@pytest.mark.parametrize('d', [64, 128])
+def test_fused_trainer_step_equals_unfused(hip_device, d):
+    """Walk batches with the HIP Adam: training_step applies the update itself (output-table
+    Adam fused into the records gather, input-table Adam overlapped on a side stream into a
+    second buffer), and the tables, Adam state and losses equal SGNS + optimizer.step() (the
+    unfused form, fuse_into_sgns=False) up to float-atomic summation order."""
+    from shallow_encoders.graph.random_walk_generator import DeepWalk
+    from shallow_encoders.graph.rmat import rmat_graph
+    from test_gpu_sgns import assert_params_close
+    csr = rmat_graph(12, 40_000, 0, device=hip_device)
+    walker = DeepWalk(csr, 30, rng='philox', seed=3, device=hip_device)
+    V, R, K, lr = csr.vocab_size, 3, 4, 0.02
+    runs = []
+    for fuse in (True, False):
+        torch.manual_seed(11)
+        model = SkipGram(V, d).cuda()
+        opt = Adam(model.parameters(), lr=lr, fuse_into_sgns=fuse)
+        sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+        tr = Word2VecTrainer(model, opt, sched, neg_samples=K, vocab_size=V, noise='device',
+                             seed=5, context_radius=R)
+        tr.manual_grads = True
+        losses = []
+        for step in range(5):
+            if step == 3:
+                sched.step()                       # lr change between steps
+            starts = torch.randint(1, V, (300,), generator=torch.Generator().manual_seed(step),
+                                   dtype=torch.int32).to(hip_device)
+            out = tr.training_step(walker.walk_batch(starts, walk_id0=step * 300))
+            opt.step()
+            opt.zero_grad()
+            losses.append(out['loss'])
+        torch.cuda.synchronize()
+        assert bool(opt._alt) == fuse               # the fused path ran (second buffer exists)
+        assert float(model.input_weight.grad.abs().max()) == 0.0
+        assert float(model.output_weight.grad.abs().max()) == 0.0
+        runs.append((model, opt, [float(x) for x in losses]))
+    (mf, of, lf), (mu, ou, lu) = runs
+    np.testing.assert_allclose(lf, lu, rtol=1e-4)
+    for a, b in ((mf.input_weight, mu.input_weight), (mf.output_weight, mu.output_weight)):
+        assert_params_close(a.detach().cpu().numpy(), b.detach().cpu().numpy(), lr,
+                            max_frac=5e-3, max_abs=2.05 * lr * 5)
+    for pf, pu in zip(mf.parameters(), mu.parameters()):
+        assert float(of.state[pf]['step']) == float(ou.state[pu]['step']) == 5.0
+        np.testing.assert_allclose(of.state[pf]['exp_avg'].cpu().numpy(),
+                                   ou.state[pu]['exp_avg'].cpu().numpy(), rtol=1e-3, atol=1e-6)
