@@ -15,6 +15,8 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
+from shallow_encoders import _native
+
 from shallow_encoders.common.path import ASSETS_PATH
 from shallow_encoders.graph.csr import CSRGraph
 from shallow_encoders.graph.random_walk_generator import RandomWalk, random_walk_factory
@@ -59,8 +61,7 @@ class RandomWalkDataset:
         perm = list(range(len(base_nodes)))
         random.shuffle(perm)
         self._base_nodes = base_nodes
-        self._perm = np.asarray(perm, dtype=np.int64)
-        self._nodes = [base_nodes[i] for i in perm]
+        self._perm = np.asarray(perm, dtype=np.int64)   # epoch order, as base_nodes indices
 
         method_params = {} if method_params is None else method_params
         self._walk_generator: RandomWalk = random_walk_factory(
@@ -103,21 +104,24 @@ class RandomWalkDataset:
         return self._walk_generator.length
 
     def _get_current_node(self):
-        return self._nodes[self._index // self._walks_per_node]
+        return self._base_nodes[self._perm[self._index // self._walks_per_node]]
 
     def __len__(self) -> int:
-        return len(self._nodes) * self._walks_per_node
+        return len(self._base_nodes) * self._walks_per_node
 
     def __iter__(self) -> 'RandomWalkDataset':
         self._index = 0
         return self
 
     def _reshuffle(self) -> None:
-        perm = list(range(len(self._nodes)))
+        # the reference re-shuffles its node list in place (same draws as shuffling indices);
+        # names are looked up through the permutation instead of rebuilding a list of them
+        perm = list(range(len(self._base_nodes)))
         random.shuffle(perm)
         p = np.asarray(perm, dtype=np.int64)
-        self._nodes = [self._nodes[i] for i in perm]
+        self._perm = self._perm[p]
         self._node_ids = self._node_ids[p]
+        self._dev_starts = None
         self._epoch += 1
 
     def __next__(self):
@@ -135,6 +139,20 @@ class RandomWalkDataset:
         idx = np.arange(first, first + count, dtype=np.int64) // self._walks_per_node
         return self._node_ids[idx]
 
+    def _device_starts(self) -> Optional[torch.Tensor]:
+        """The epoch's start ids (int32, one per walk) on the walker's device, copied once per
+        epoch, so that a batch needs no host-to-device copy: a copy from pageable host memory
+        waits for the stream to drain, which would stall the training pipeline every batch."""
+        if not torch.cuda.is_available():
+            return None
+        dev = _native.require_device(self._walk_generator._device)
+        st = getattr(self, '_dev_starts', None)
+        if st is None or st.device != dev:
+            ids = torch.from_numpy(self._node_ids.astype(np.int32))
+            st = ids.to(dev).repeat_interleave(self._walks_per_node)
+            self._dev_starts = st
+        return st
+
     def next_walk_batch(self, max_walks: int, check: bool = True) -> Optional[torch.Tensor]:
         """The next <= max_walks walks of the epoch as device int32 [n, L]; None at epoch end
         (which reshuffles, as ``StopIteration`` does, and rewinds like ``__iter__``)."""
@@ -143,7 +161,11 @@ class RandomWalkDataset:
             self._index = 0
             return None
         n = min(int(max_walks), len(self) - self._index)
-        starts = torch.from_numpy(self.start_ids(self._index, n))
+        starts = self._device_starts()
+        if starts is not None:          # a slice of the epoch's start ids, already on the device
+            starts = starts[self._index:self._index + n]
+        else:
+            starts = torch.from_numpy(self.start_ids(self._index, n))
         walk_id0 = self._epoch * len(self) + self._index
         out = self._walk_generator.walk_batch(starts, walk_id0=walk_id0, check=check)
         self._index += n

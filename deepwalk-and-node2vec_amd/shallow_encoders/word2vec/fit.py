@@ -14,6 +14,8 @@ directory layout of tools/conventions.py.
 """
 import csv
 import os
+import shutil
+import threading
 import time
 from typing import Dict, Iterable, Optional
 
@@ -22,10 +24,48 @@ import torch
 from shallow_encoders.word2vec.trainer import Word2VecTrainer
 
 
-def save_checkpoint(path: str, trainer: Word2VecTrainer, epoch: int, global_step: int) -> None:
+def _snapshot(trainer: Word2VecTrainer, epoch: int, global_step: int) -> dict:
     state = {f'_model.{k}': v.detach().cpu() for k, v in trainer.model.state_dict().items()}
-    torch.save({'epoch': epoch, 'global_step': global_step, 'state_dict': state,
-                'pytorch-lightning_version': None}, path)
+    return {'epoch': epoch, 'global_step': global_step, 'state_dict': state,
+            'pytorch-lightning_version': None}
+
+
+def save_checkpoint(path: str, trainer: Word2VecTrainer, epoch: int, global_step: int) -> None:
+    torch.save(_snapshot(trainer, epoch, global_step), path)
+
+
+class _CheckpointWriter:
+    """Epoch checkpoints written on a background thread: the tables are copied to the host at
+    the epoch boundary (the values of that step), the file writes overlap the next epoch.
+    ``last.ckpt`` is a copy of the epoch file, not a second serialisation."""
+
+    def __init__(self, dirpath: str):
+        self.dirpath = dirpath
+        self._thread = None
+        self._error = None
+
+    def _write(self, snap: dict, name: str) -> None:
+        try:
+            path = os.path.join(self.dirpath, name)
+            torch.save(snap, path)
+            shutil.copyfile(path, os.path.join(self.dirpath, 'last.ckpt'))
+        except BaseException as e:  # re-raised in the training thread by join()
+            self._error = e
+
+    def submit(self, trainer: Word2VecTrainer, epoch: int, global_step: int) -> None:
+        self.join()
+        snap = _snapshot(trainer, epoch, global_step)
+        name = f'checkpoint_epoch={epoch:06d}_step={global_step:09d}.ckpt'
+        self._thread = threading.Thread(target=self._write, args=(snap, name), daemon=False)
+        self._thread.start()
+
+    def join(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise e
 
 
 class CSVMetricLogger:
@@ -64,8 +104,10 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
     step_sched = isinstance(sched, dict) and sched.get('interval', 'epoch') == 'step'
     sched_obj = sched['scheduler'] if isinstance(sched, dict) else sched
     logger = CSVMetricLogger(log_dir)
+    writer = None
     if checkpoint_dir:
         os.makedirs(checkpoint_dir, exist_ok=True)
+        writer = _CheckpointWriter(checkpoint_dir)
     global_step = 0
     last = {}
     for epoch in range(max_epochs):
@@ -81,18 +123,20 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
                 logger.log(global_step, epoch, {f'train/{k}': v for k, v in loss.items()})
             global_step += 1
             n_batches += 1
+        last = trainer.on_train_epoch_end()         # synchronises with the device
+        t_loop = time.perf_counter() - t0
         if not step_sched and sched_obj is not None:
             sched_obj.step()
-        last = trainer.on_train_epoch_end()
         last['epoch/lr'] = float(opt.param_groups[0]['lr'])
         logger.log(global_step, epoch, last)
         logger.flush()
-        if checkpoint_dir:
-            name = f'checkpoint_epoch={epoch:06d}_step={global_step:09d}.ckpt'
-            save_checkpoint(os.path.join(checkpoint_dir, name), trainer, epoch, global_step)
-            save_checkpoint(os.path.join(checkpoint_dir, 'last.ckpt'), trainer, epoch, global_step)
+        if writer is not None:
+            writer.submit(trainer, epoch, global_step)
         if verbose:
             dt = time.perf_counter() - t0
             msg = ' '.join(f'{k}={v:.4f}' for k, v in last.items() if k.endswith('loss'))
-            print(f'epoch {epoch}: {n_batches} batches in {dt:.2f}s {msg}', flush=True)
+            print(f'epoch {epoch}: {n_batches} batches in {dt:.2f}s (training loop {t_loop:.2f}s) '
+                  f'{msg}', flush=True)
+    if writer is not None:
+        writer.join()
     return last
