@@ -117,6 +117,10 @@ def main():
     ap.add_argument('--no-walk-bench', action='store_true')
     ap.add_argument('--no-fuse-adam', action='store_true',
                     help='N=1: run the output table\'s Adam as its own pass (unfused)')
+    ap.add_argument('--no-out-pieces', action='store_true',
+                    help='N>1: exchange the output table after the whole output-table phase')
+    ap.add_argument('--out-pieces', type=int, default=None,
+                    help='N>1: output-table pieces (default sharding.DEFAULT_OUT_PIECES)')
     ap.add_argument('--no-overlap-in', action='store_true',
                     help='N=1: run the in-table Adam after the output-table phase (serial)')
     args = ap.parse_args()
@@ -146,7 +150,7 @@ def main():
     from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
     from shallow_encoders.graph.rmat import rmat_graph
     from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
-                                               sgns_phase_bytes)
+                                               sgns_phase2_pieces, sgns_phase_bytes)
     from shallow_encoders.word2vec.sharding import ShardedTables, overlap_adam_blocks
     _native.require_device(dev)
 
@@ -163,7 +167,8 @@ def main():
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
     tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
-                           overlap_in=not args.no_overlap_in)
+                           overlap_in=not args.no_overlap_in,
+                           out_pieces=None if args.no_out_pieces else args.out_pieces)
     centres = B * (L - 2 * R)
     pairs_per_step = centres * 2 * R
     grad_scale = 1.0 / (pairs_per_step * world)   # mean over the GLOBAL batch
@@ -174,6 +179,7 @@ def main():
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
     fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
+    pieces = world > 1 and not args.no_out_pieces
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
     pb = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     p2_bytes = pb['sort'] + pb['pass2']        # the phase the in-table Adam overlaps
@@ -198,10 +204,18 @@ def main():
         # output-table phase runs -> out-table exchange -> wait for both all-gathers
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
         tables.exchange_in(overlap_bytes=p2_bytes)
-        # one device: the output table's Adam is fused into the output-table phase
+        # one device: the output table's Adam is fused into the output-table phase; N > 1:
+        # that phase runs in row pieces, each exchanged behind the next piece's gather
         spec = tables.out_adam_spec() if fuse else None
-        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
-                        out_adam=spec, **kw)
+        if pieces:
+            n_pieces, rows = tables.out_pieces_spec()
+            sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks_buf, context_radius=R,
+                               n_pieces=n_pieces, piece_rows=rows,
+                               on_piece=tables.exchange_out_piece, status=status,
+                               scatter=args.scatter)
+        else:
+            sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
+                            out_adam=spec, **kw)
         if record:
             e[2].record()
         tables.exchange_out(fused_out=spec is not None)
@@ -301,7 +315,9 @@ def main():
                          f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
             'parallelism': (f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather, '
-                            f'in-table exchange overlapped)' if backend == 'nccl' else
+                            f'in-table exchange overlapped'
+                            + (f', out table in {tables.P} pieces pipelined' if pieces else '')
+                            + ')' if backend == 'nccl' else
                             f'REHEARSAL dp{world} over {backend}, all ranks on one device'),
         },
         'walks_per_s': walk_stats.get('deepwalk'),

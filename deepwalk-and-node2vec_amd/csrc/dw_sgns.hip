@@ -23,6 +23,8 @@
 //     gathered bytes move at read speed, not atomic speed.
 #include <stdlib.h>
 
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -518,24 +520,28 @@ struct OutAdam {
     dw::AdamScalars s;
 };
 
+// range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
+// records of whole rows, so a piece's rows never continue in another piece's chunks.
 template <int VPL, bool MASKED, bool ADAM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
-                 int32_t d, OutAdam oa) {
+                 int32_t d, OutAdam oa, const int64_t *__restrict__ range) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-    const int64_t n_chunks = (n_rec + GCH - 1) / GCH;
+    const int64_t lo = range ? range[0] : 0;
+    const int64_t hi = range ? range[1] : n_rec;
+    const int64_t n_chunks = (hi - lo + GCH - 1) / GCH;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     bool live[VPL];
 #pragma unroll
     for (int m = 0; m < VPL; ++m) live[m] = !MASKED || (lane + WAVE * m < d);
 
     for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
-        const int64_t e0 = ch * GCH;
-        const int64_t e1 = (e0 + GCH < n_rec) ? e0 + GCH : n_rec;
-        const uint32_t before = e0 > 0 ? keys[e0 - 1] : 0xFFFFFFFFu;
-        const uint32_t after = e1 < n_rec ? keys[e1] : 0xFFFFFFFFu;
+        const int64_t e0 = lo + ch * GCH;
+        const int64_t e1 = (e0 + GCH < hi) ? e0 + GCH : hi;
+        const uint32_t before = e0 > lo ? keys[e0 - 1] : 0xFFFFFFFFu;
+        const uint32_t after = e1 < hi ? keys[e1] : 0xFFFFFFFFu;
         uint32_t cur = keys[e0];
         float g[VPL];
 #pragma unroll
@@ -605,9 +611,12 @@ int end_bit_for(int64_t V) {
     return bits;
 }
 
+constexpr int MAX_PIECES = 1024;  // row pieces of dw_sgns_walks_phase2_piece
+
 struct Workspace {
     uint32_t *k0, *k1;
     uint64_t *v0, *v1;
+    int64_t *bounds;  // [MAX_PIECES + 1] record bounds of the row pieces
     void *cub;
     size_t cub_bytes;
     size_t total;
@@ -640,9 +649,11 @@ int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStrea
     ws->k1 = reinterpret_cast<uint32_t *>(p + kbytes);
     ws->v0 = reinterpret_cast<uint64_t *>(p + 2 * kbytes);
     ws->v1 = reinterpret_cast<uint64_t *>(p + 2 * kbytes + vbytes);
-    ws->cub = p + 2 * kbytes + 2 * vbytes;
+    const size_t bbytes = align256(sizeof(int64_t) * (MAX_PIECES + 1));
+    ws->bounds = reinterpret_cast<int64_t *>(p + 2 * kbytes + 2 * vbytes);
+    ws->cub = p + 2 * kbytes + 2 * vbytes + bbytes;
     ws->cub_bytes = cub_bytes;
-    ws->total = 2 * kbytes + 2 * vbytes + align256(cub_bytes);
+    ws->total = 2 * kbytes + 2 * vbytes + bbytes + align256(cub_bytes);
     return DW_OK;
 }
 
@@ -749,22 +760,22 @@ __global__ void __launch_bounds__(256)
 template <int VPL>
 void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const uint64_t *vals,
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
-                   const OutAdam *oa) {
+                   const OutAdam *oa, const int64_t *range) {
     const bool exact = d == 64 * VPL;
     if (oa) {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa);
+                               w_in, g_out, d, *oa, range);
         else
             hipLaunchKernelGGL((k_rec_gather<VPL, true, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa);
+                               w_in, g_out, d, *oa, range);
     } else {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, false>), g, bl, 0, st, keys, vals,
-                               n_rec, w_in, g_out, d, OutAdam{});
+                               n_rec, w_in, g_out, d, OutAdam{}, range);
         else
             hipLaunchKernelGGL((k_rec_gather<VPL, true, false>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, OutAdam{});
+                               w_in, g_out, d, OutAdam{}, range);
     }
 }
 
@@ -783,17 +794,20 @@ void launch_rest(hipStream_t st, int64_t V, int32_t d, float *g_out, const OutAd
 
 // oa != NULL: the fused output-table Adam (rows 0..V of the out table) — gather, then the
 // rest-of-rows update, then the row flags cleared.
+// range != NULL: one row piece (records [range[0], range[1]), read on the device); the grid is
+// sized for `share` of the records (grid-stride beyond).
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
-                 float *g_out, int32_t d, const OutAdam *oa, int64_t V, hipStream_t st) {
+                 float *g_out, int32_t d, const OutAdam *oa, int64_t V, hipStream_t st,
+                 const int64_t *range = nullptr, double share = 1.0) {
     const int64_t n_chunks = (n_rec + GCH - 1) / GCH;
-    int64_t blocks = (n_chunks + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    int64_t blocks = (int64_t)((double)(n_chunks + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK * share);
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
-    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
-    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
-    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa);
+    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
+    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
+    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
+    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
     else return DW_E_UNSUPPORTED;
     DW_LAUNCH_CHECK("dw_sgns/gather");
     if (oa) {
@@ -907,6 +921,90 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     }
     g_timer.mark(2, st);
     return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, oa, a.V, st);
+}
+
+// ---- output-table phase in row pieces (N > 1: exchange a piece while the next one runs) -------
+// bounds[p] = first record whose row >= p * piece_rows (lower bound in the sorted keys).
+__global__ void k_piece_bounds(const uint32_t *__restrict__ keys, int64_t n_rec, int32_t n_pieces,
+                               int64_t piece_rows, int64_t *__restrict__ bounds) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > n_pieces) return;
+    if (p == n_pieces) {
+        bounds[p] = n_rec;
+        return;
+    }
+    const uint64_t target = static_cast<uint64_t>(p) * static_cast<uint64_t>(piece_rows);
+    int64_t lo = 0, hi = n_rec;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (static_cast<uint64_t>(keys[mid]) < target) lo = mid + 1;
+        else hi = mid;
+    }
+    bounds[p] = lo;
+}
+
+// Which buffer of the workspace holds the sorted records after the piece == -1 call (rocprim's
+// double buffer tells the host only): recorded per workspace for the piece calls that follow.
+std::mutex g_sorted_mu;
+std::unordered_map<const void *, bool> g_sorted_in_k1;
+
+int launch_pieces(SgnsArgs a, void *workspace, size_t workspace_bytes, int piece, int n_pieces,
+                  int64_t piece_rows, hipStream_t st) {
+    DW_REQUIRE(workspace != nullptr, "dw_sgns_walks_phase2_piece: needs the records workspace");
+    DW_REQUIRE(n_pieces >= 1 && n_pieces <= MAX_PIECES && piece >= -1 && piece < n_pieces,
+               "dw_sgns_walks_phase2_piece: piece %d of %d (at most %d pieces)", piece, n_pieces,
+               MAX_PIECES);
+    DW_REQUIRE(piece_rows >= 1 && piece_rows * (int64_t)n_pieces >= a.V,
+               "dw_sgns_walks_phase2_piece: %d pieces of %lld rows do not cover %lld rows",
+               n_pieces, (long long)piece_rows, (long long)a.V);
+    const int64_t T = (int64_t)a.C * (1 + a.K);
+    DW_REQUIRE(T <= TMAX && a.V <= 0x7FFFFFFF, "dw_sgns_walks_phase2_piece: records mode limits");
+    const int64_t n_rec = a.batch * T;
+    DW_REQUIRE(n_rec < 0x7FFFFFFF, "dw_sgns_walks_phase2_piece: too many records");
+    Workspace ws;
+    int rc = plan_workspace(n_rec > 0 ? n_rec : 1, a.V, workspace, &ws, st);
+    if (rc != DW_OK) return rc;
+    DW_REQUIRE(workspace_bytes >= ws.total, "dw_sgns: workspace too small (%zu < %zu)",
+               workspace_bytes, ws.total);
+    if (piece == -1) {
+        bool in_k1 = false;
+        if (n_rec > 0) {
+            rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
+            rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
+            size_t cub_bytes = ws.cub_bytes;
+            hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
+                ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(a.V), st);
+            if (e != hipSuccess) {
+                dw::set_error("dw_sgns: records sort failed: %s", hipGetErrorString(e));
+                return DW_E_HIP;
+            }
+            in_k1 = kb.current() == ws.k1;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_sorted_mu);
+            g_sorted_in_k1[workspace] = in_k1;
+        }
+        hipLaunchKernelGGL(k_piece_bounds, dim3((n_pieces + 256) / 256), dim3(256), 0, st,
+                           in_k1 ? ws.k1 : ws.k0, n_rec, n_pieces, piece_rows, ws.bounds);
+        DW_LAUNCH_CHECK("dw_sgns/piece_bounds");
+        g_timer.mark(2, st);
+        return DW_OK;
+    }
+    bool in_k1;
+    {
+        std::lock_guard<std::mutex> lk(g_sorted_mu);
+        auto it = g_sorted_in_k1.find(workspace);
+        DW_REQUIRE(it != g_sorted_in_k1.end(),
+                   "dw_sgns_walks_phase2_piece: piece %d before the sort call (piece -1)", piece);
+        in_k1 = it->second;
+    }
+    if (n_rec > 0) {
+        rc = launch_pass2(in_k1 ? ws.k1 : ws.k0, in_k1 ? ws.v1 : ws.v0, n_rec, a.w_in, a.g_out,
+                          a.d, nullptr, a.V, st, ws.bounds + piece, 2.0 / n_pieces);
+        if (rc != DW_OK) return rc;
+    }
+    if (piece == n_pieces - 1) g_timer.mark(3, st);
+    return DW_OK;
 }
 
 // ---- SkipGram.forward logits and its backward (autograd path of the reference API) ----------
@@ -1158,6 +1256,26 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
                                neg_step_size, eps, weight_decay}};
     return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
+}
+
+int dw_sgns_walks_phase2_piece(int32_t piece, int32_t n_pieces, int64_t piece_rows,
+                               const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                               int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                               int32_t dim, const float *w_in, float *g_out, int32_t *status,
+                               void *workspace, size_t workspace_bytes, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0,
+               "dw_sgns_walks_phase2_piece: bad sizes");
+    DW_REQUIRE(walks && w_in && g_out && status, "dw_sgns_walks_phase2_piece: null pointer");
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, nullptr, nullptr, g_out, nullptr,
+                           0, 0, 1.f, nullptr, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    return launch_pieces(a, workspace, workspace_bytes, piece, n_pieces, piece_rows,
+                         dw::as_stream(stream));
 }
 
 int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,

@@ -14,7 +14,7 @@ Two call styles:
     ``loss.backward()`` themselves (e.g. a Lightning loop).
 """
 import math
-from typing import Dict, Optional
+from typing import Callable, Dict, Optional
 
 import torch
 
@@ -155,6 +155,44 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                          float(scale), _native.ptr(loss_acc), _native.ptr(status),
                          _native.ptr(ws), 0 if ws is None else ws.numel(), s)
     return loss_acc
+
+
+def sgns_phase2_pieces(w_in: torch.Tensor, g_out: torch.Tensor, neg_samples: int, *,
+                       walks: torch.Tensor, context_radius: int, n_pieces: int,
+                       piece_rows: int, on_piece: Optional[Callable[[int], None]] = None,
+                       status: Optional[torch.Tensor] = None, scatter: str = 'sorted') -> None:
+    """Phase 2 of ``sgns_accumulate(walks=...)`` in output-row pieces (after its phase 1 with the
+    same walks): the records sort, then piece by piece the gather of rows [p*piece_rows,
+    (p+1)*piece_rows) into g_out, calling ``on_piece(p)`` right after each launch — the caller
+    can start exchanging those rows while the next pieces run (ShardedTables.exchange_out_piece).
+    Atomic mode: phase 1 already completed g_out; on_piece is called for every piece."""
+    dev = w_in.device
+    V, d = w_in.shape
+    if g_out.shape != (V, d):
+        raise ValueError('w_in and g_out must both be (V, d)')
+    if walks.dtype != torch.int32 or walks.dim() != 2:
+        raise TypeError('walks must be int32 [n_walks, L]')
+    if n_pieces * piece_rows < V:
+        raise ValueError('the pieces must cover every output row')
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    C = 2 * R
+    if not _use_records(scatter, C, K, V):
+        for p in range(n_pieces):
+            if on_piece is not None:
+                on_piece(p)
+        return
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = workspace_for(n * (L - 2 * R), C, K, V, dev)
+    with torch.cuda.device(dev):
+        for p in range(-1, n_pieces):
+            _native.call('dw_sgns_walks_phase2_piece', p, int(n_pieces), int(piece_rows),
+                         _native.ptr(walks), n, L, R, K, V, d, _native.ptr(w_in),
+                         _native.ptr(g_out), _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         _native.stream(dev))
+            if p >= 0 and on_piece is not None:
+                on_piece(p)
 
 
 def device_noise(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int, seed: int,

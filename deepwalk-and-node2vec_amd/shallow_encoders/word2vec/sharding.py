@@ -6,7 +6,7 @@ local gradient by 1/M_global (the mean over the GLOBAL batch), so the result equ
 single-device training on the concatenated batch (DDP semantics). Walk generation needs no
 communication, because walks are keyed by the global walk id.
 
-Layout (S = V_pad / world rows; rank r owns rows [r*S, (r+1)*S) of BOTH tables):
+Layout (P out-table pieces; V_pad = V rounded up to a multiple of world * P; S = V_pad / world):
 
   params  float32 [2 or 3, V_pad, d]   slot 1 = out table; slot 0 = in table, and slot 2 =
                                        its second buffer when world > 1 or, on one GPU, when
@@ -14,27 +14,35 @@ Layout (S = V_pad / world rows; rank r owns rows [r*S, (r+1)*S) of BOTH tables):
   grads   float32 [2, V_pad, d]        local dense gradients (in, out)
   m, v    float32 [2, S, d]            Adam state of this rank's rows only
 
+Row ownership: in table, rank r owns rows [r*S, (r+1)*S). Out table, cut into P pieces of
+PL = V_pad / P rows: rank r owns sub-range r (SL = PL / world rows) of every piece; m[1], v[1]
+hold those rows piece by piece. With P = 1 both tables have the same node-id ranges.
+
 Per optimizer step, all collectives run over RCCL (torch.distributed 'nccl' on ROCm, xGMI),
-one table at a time:
-  1. reduce-scatter(sum) of the table's gradient: rank r receives the global gradient of its
-     rows;
+per table (per piece for the out table):
+  1. reduce-scatter(sum) of the gradient: rank r receives the global gradient of its rows;
   2. dense Adam on those rows only (dw_adam_dense): 1/world of the optimizer's HBM traffic;
   3. all-gather of the updated rows back into every rank's replica.
 
-Overlapped form (``exchange_in`` / ``exchange_out`` / ``sync``):
-  * The in-table gradient is final after SGNS pass 1 (dw_sgns_walks_phase 1).
-  * So ``exchange_in`` runs the in-table's reduce-scatter, Adam and all-gather on a side
-    stream while the output-table phase (records sort + gather) still runs on the main stream.
-  * That phase reads the current in table, so the update goes into the idle buffer: copy own
-    rows, Adam in place, all-gather into the buffer. The two buffers swap at ``sync``.
-  * ``exchange_out`` does the out table after phase 2.
-  * ``sync`` makes the main stream wait for both all-gathers before the next pass 1.
+Overlapped form (``exchange_in`` / ``exchange_out_piece`` / ``exchange_out`` / ``sync``):
+  * The in-table gradient is final after SGNS pass 1 (dw_sgns_walks_phase 1). ``exchange_in``
+    runs the in-table's exchange on a side stream while the output-table phase (records sort +
+    gather) still runs on the main stream. That phase reads the current in table, so the
+    update goes into the idle buffer: copy own rows, Adam in place, all-gather into the
+    buffer. The two buffers swap at ``sync``.
+  * The output-table phase runs in row pieces (dw_sgns_walks_phase2_piece, sgns_phase2_pieces):
+    piece p's gradient rows are final once its gather is done, and nothing in the phase reads
+    the out table, so ``exchange_out_piece(p)`` exchanges piece p on the side stream while the
+    gathers of the next pieces run. Only the last piece's exchange is exposed.
+  * ``exchange_out`` exchanges the pieces not yet exchanged (all of them after an unpieced
+    phase 2); ``sync`` makes the main stream wait for every all-gather before the next pass 1.
 ``step()`` is the same update done serially.
 
 On one GPU there is nothing to exchange, but the in-table Adam (1/2 of the optimizer traffic) still
 overlaps the output-table phase the same way (``overlap_in``, default on with the HIP Adam):
 ``exchange_in`` runs dw_adam_dense_to from the current in table into the idle buffer on the side
-stream, and the radix sort of that phase leaves the HBM bandwidth it needs.
+stream, and the radix sort of that phase leaves the HBM bandwidth it needs. The out table's Adam
+is fused into the phase itself (``out_adam_spec``).
 
 The Adam update is injectable (``adam_impl``), so the exchange logic can be tested with gloo
 on the CPU (there the overlapped form runs its collectives synchronously). The default is the
@@ -98,6 +106,10 @@ OVERLAP_PHASE_BPS = 5.0e12
 ADAM_BLOCK_BPS = 22e9
 OVERLAP_MARGIN = 1.25
 
+# N > 1: out-table pieces exchanged behind the output-table phase; 8 keeps each collective at
+# 1/8 of the table (64 MB at C3) while exposing only the last piece's exchange.
+DEFAULT_OUT_PIECES = 8
+
 
 def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> int:
     """Grid cap for an Adam of ``adam_bytes`` overlapping a phase of ``overlap_bytes``
@@ -115,13 +127,21 @@ class ShardedTables:
     def __init__(self, vocab_size: int, dim: int, device, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  group=None, init_seed: Optional[int] = 0,
-                 adam_impl: Optional[Callable] = None, overlap_in: Optional[bool] = None):
+                 adam_impl: Optional[Callable] = None, overlap_in: Optional[bool] = None,
+                 out_pieces: Optional[int] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.V, self.d = int(vocab_size), int(dim)
-        self.V_pad = int(math.ceil(self.V / self.world)) * self.world
+        # out-table pieces: one per exchange pipelined behind the output-table phase (N > 1)
+        self.P = int(out_pieces) if out_pieces else (DEFAULT_OUT_PIECES if self.world > 1 else 1)
+        if not 1 <= self.P <= 1024:
+            raise ValueError('out_pieces must be in [1, 1024]')
+        unit = self.world * self.P
+        self.V_pad = int(math.ceil(self.V / unit)) * unit
         self.S = self.V_pad // self.world
+        self.PL = self.V_pad // self.P          # rows per out-table piece
+        self.SL = self.PL // self.world         # rows per rank per piece
         self.device = torch.device(device)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.adam_impl = adam_impl or hip_adam
@@ -142,6 +162,7 @@ class ShardedTables:
         self._cur_in = 0
         self._next_in = 0
         self._ag = []          # pending all-gathers / side-stream events (overlapped form)
+        self._out_done = set()  # out-table pieces already exchanged this step
         self._side = (torch.cuda.Stream(self.device)
                       if (self._cuda and (self.world > 1 or self.overlap_in)) else None)
         self._row_flags = None   # fused output-table Adam scratch (one device)
@@ -166,8 +187,20 @@ class ShardedTables:
         return self.grads[1, :self.V]
 
     def shard_range(self):
-        """[start, end) rows of this rank's node range (the same in both tables)."""
+        """[start, end) rows of this rank's node range of the in table."""
         return self.rank * self.S, (self.rank + 1) * self.S
+
+    def out_piece_rows(self, p: int):
+        """[start, end) rows of out-table piece p, and of this rank's share of it."""
+        a = p * self.PL
+        return (a, a + self.PL), (a + self.rank * self.SL, a + (self.rank + 1) * self.SL)
+
+    def state_rows(self, t: int) -> torch.Tensor:
+        """Global row of each row of m[t] / v[t] (this rank's rows of table t, in order)."""
+        if t == 0:
+            a, b = self.shard_range()
+            return torch.arange(a, b)
+        return torch.cat([torch.arange(*self.out_piece_rows(p)[1]) for p in range(self.P)])
 
     def xavier_(self, seed: int) -> None:
         """W2VBase init (model.py:26-27): U(-a, a), a = sqrt(6/(V+d)); identical on all ranks."""
@@ -196,25 +229,45 @@ class ShardedTables:
         self._adam(self.params[self._cur_in].view(-1), self.grads[0].view(-1), 0, True)
         self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
 
-    def _exchange(self, t: int, src_slot: int, dst_slot: int, async_op: bool):
-        """reduce-scatter grads[t] -> Adam on own rows of params[dst_slot] (starting from
-        params[src_slot]) -> all-gather into params[dst_slot]; grads[t] ends zeroed.
+    def _all_gather(self, dst: torch.Tensor, own: torch.Tensor, async_op: bool):
+        nccl = dist.get_backend(self.group) == 'nccl'
+        src = own.view(-1) if nccl else own.reshape(-1).clone()   # RCCL all-gather is in-place safe
+        return dist.all_gather_into_tensor(dst.view(-1), src, group=self.group, async_op=async_op)
+
+    def _exchange_in(self, src_slot: int, dst_slot: int, async_op: bool):
+        """reduce-scatter grads[0] -> Adam on own rows of params[dst_slot] (starting from
+        params[src_slot]) -> all-gather into params[dst_slot]; grads[0] ends zeroed.
         Returns the all-gather work handle when async_op."""
         a, b = self.shard_range()
-        w = dist.reduce_scatter_tensor(self.grad_shard[t].view(-1), self.grads[t].view(-1),
+        w = dist.reduce_scatter_tensor(self.grad_shard[0].view(-1), self.grads[0].view(-1),
                                        op=dist.ReduceOp.SUM, group=self.group,
                                        async_op=async_op)
         if async_op:
             w.wait()            # the current (side) stream waits for the reduce-scatter
-        self.grads[t].zero_()
+        self.grads[0].zero_()
         own = self.params[dst_slot, a:b]
         if src_slot != dst_slot:
             own.copy_(self.params[src_slot, a:b])
-        self._adam(own.view(-1), self.grad_shard[t].view(-1), t, False)
-        nccl = dist.get_backend(self.group) == 'nccl'
-        src = own.view(-1) if nccl else own.reshape(-1).clone()   # RCCL all-gather is in-place safe
-        return dist.all_gather_into_tensor(self.params[dst_slot].view(-1), src, group=self.group,
-                                           async_op=async_op)
+        self._adam(own.view(-1), self.grad_shard[0].view(-1), 0, False)
+        return self._all_gather(self.params[dst_slot], own, async_op)
+
+    def _exchange_out_piece(self, p: int, async_op: bool):
+        """The same for out-table piece p (rows out_piece_rows(p)); grads of the piece end
+        zeroed. Returns the all-gather work handle when async_op."""
+        (a, b), (oa, ob) = self.out_piece_rows(p)
+        gp = self.grads[1, a:b]
+        gs = self.grad_shard[1].view(self.P, self.SL, self.d)[p]
+        w = dist.reduce_scatter_tensor(gs.view(-1), gp.reshape(-1), op=dist.ReduceOp.SUM,
+                                       group=self.group, async_op=async_op)
+        if async_op:
+            w.wait()
+        gp.zero_()
+        own = self.params[1, oa:ob]
+        self.adam_impl(own.view(-1), gs.view(-1),
+                       self.m[1].view(self.P, self.SL, self.d)[p].view(-1),
+                       self.v[1].view(self.P, self.SL, self.d)[p].view(-1), self.step_count,
+                       self.lr, self.betas, self.eps, self.weight_decay, False)
+        return self._all_gather(self.params[1, a:b], own, async_op)
 
     # ---- serial step ------------------------------------------------------------------------------
     def step(self) -> None:
@@ -224,40 +277,62 @@ class ShardedTables:
         if self.world == 1:
             self._adam_both()
             return
-        self._exchange(0, self._cur_in, self._cur_in, False)
-        self._exchange(1, 1, 1, False)
+        self._exchange_in(self._cur_in, self._cur_in, False)
+        for p in range(self.P):
+            self._exchange_out_piece(p, False)
 
     # ---- overlapped step --------------------------------------------------------------------------
+    def _on_side(self, fn) -> None:
+        """Run fn on the side stream after the work enqueued so far on the current stream (CPU:
+        now). fn returns a work handle / event that ``sync`` waits for, or None."""
+        if not self._cuda:
+            fn(False)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ev)
+            w = fn(True)
+            if w is not None:
+                self._ag.append(w)
+
     def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
         """Call right after SGNS pass 1 is enqueued (g_in final): the in-table update starts on a
         side stream while the output-table phase runs on the current stream. ``overlap_bytes``
         (one GPU): HBM bytes of that phase (sgns_phase_bytes sort + pass2), to size the Adam's
         grid (overlap_adam_blocks); None = full grid."""
         self.step_count += 1
+        self._out_done = set()
         if self.world == 1 and not self.overlap_in:
             return                              # exchange_out does the Adam
         self._next_in = 2 - self._cur_in
         if self.world == 1:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._side):
-                self._side.wait_event(ev)
+            def adam_to(_async):
                 blocks = overlap_adam_blocks(self.V_pad * self.d * 4 * 7, overlap_bytes)
                 hip_adam_to(self.params[self._cur_in], self.params[self._next_in],
                             self.grads[0], self.m[0], self.v[0], self.step_count, self.lr,
                             self.betas, self.eps, self.weight_decay, True, blocks)
                 done = torch.cuda.Event()
                 done.record(self._side)
-            self._ag.append(done)
+                return done
+            self._on_side(adam_to)
             return
-        if not self._cuda:
-            self._exchange(0, self._cur_in, self._next_in, False)
+        self._on_side(lambda a: self._exchange_in(self._cur_in, self._next_in, a))
+
+    def out_pieces_spec(self):
+        """(n_pieces, piece_rows) for sgns_phase2_pieces."""
+        return self.P, self.PL
+
+    def exchange_out_piece(self, p: int) -> None:
+        """Call right after the gather of out-table piece p is enqueued (its gradient rows
+        final): its reduce-scatter / Adam / all-gather run on the side stream while the next
+        pieces' gathers run. One GPU: nothing to exchange (exchange_out does the Adam)."""
+        if self.world == 1:
             return
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._side):
-            self._side.wait_event(ev)
-            self._ag.append(self._exchange(0, self._cur_in, self._next_in, True))
+        if p in self._out_done:
+            raise RuntimeError(f'out-table piece {p} exchanged twice in one step')
+        self._out_done.add(p)
+        self._on_side(lambda a: self._exchange_out_piece(p, a))
 
     def can_fuse_out_adam(self) -> bool:
         """The output table's Adam can run inside SGNS phase 2: one device, HIP Adam."""
@@ -278,26 +353,21 @@ class ShardedTables:
                                         self.weight_decay)}
 
     def exchange_out(self, fused_out: bool = False) -> None:
-        """Call right after SGNS phase 2 is enqueued (g_out final). ``fused_out``: phase 2
-        already applied the output table's Adam (out_adam_spec), only the in table remains."""
-        if self.world == 1 and self.overlap_in:
-            if not fused_out:       # the in table is done on the side stream (exchange_in)
-                self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
-            return
-        if self.world == 1 and fused_out:
-            self._adam(self.params[self._cur_in].view(-1), self.grads[0].view(-1), 0, True)
-            return
+        """Call right after SGNS phase 2 is enqueued (g_out final): exchanges the out-table
+        pieces exchange_out_piece has not. ``fused_out``: phase 2 already applied the output
+        table's Adam (out_adam_spec, one GPU)."""
         if self.world == 1:
-            self._adam_both()
+            if self.overlap_in:
+                if not fused_out:       # the in table is done on the side stream (exchange_in)
+                    self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
+            elif fused_out:
+                self._adam(self.params[self._cur_in].view(-1), self.grads[0].view(-1), 0, True)
+            else:
+                self._adam_both()
             return
-        if not self._cuda:
-            self._exchange(1, 1, 1, False)
-            return
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._side):
-            self._side.wait_event(ev)
-            self._ag.append(self._exchange(1, 1, 1, True))
+        for p in range(self.P):
+            if p not in self._out_done:
+                self.exchange_out_piece(p)
 
     def sync(self) -> None:
         """The current stream waits for pending all-gathers; the new in table becomes current.

@@ -176,6 +176,21 @@ int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
                         int32_t *status, void *workspace, size_t workspace_bytes,
                         void *stream);
 
+/* Phase 2 of dw_sgns_walks_phase in row pieces (N > 1: ShardedTables pipelines each piece's
+ * output-table exchange behind the next piece's gather). Piece p covers output rows
+ * [p * piece_rows, (p+1) * piece_rows); n_pieces * piece_rows >= vocab_size, n_pieces <= 1024.
+ *   piece == -1: the records sort of the preceding phase-1 call and the record bounds of the
+ *                pieces (in the workspace);
+ *   piece in [0, n_pieces): g_out += the gradient of piece p's rows (complete when it returns
+ *                in stream order; other rows untouched).
+ * Calls -1, 0, ..., n_pieces-1 in order equal phase 2. Arguments as dw_sgns_walks_phase, same
+ * workspace (a workspace holds one sorted batch at a time). */
+int dw_sgns_walks_phase2_piece(int32_t piece, int32_t n_pieces, int64_t piece_rows,
+                               const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                               int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                               int32_t dim, const float *w_in, float *g_out, int32_t *status,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
 /* Phase 2 of dw_sgns_walks_phase fused with the output table's dense Adam step (one device):
  * the same records sort + gather, but every out row is updated in place with torch.optim.Adam
  * (single-tensor semantics, the scalars of dw_adam_dense) using its complete gradient —

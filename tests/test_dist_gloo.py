@@ -6,8 +6,12 @@ after several steps their replicated tables must equal single-process training o
 batch. Both forms are checked: the serial ``step()`` and the overlapped protocol bench.py uses
 (``exchange_in`` after pass 1 -> output-table gradient computed from ``w_in`` -> ``exchange_out``
 -> ``sync``), where the in-table update must land in the second buffer so the output-table
-phase still sees the old in table. The gradient and Adam math here is the oracle's (CPU); on
-the GPU the same ShardedTables object drives dw_sgns_walks_phase + dw_adam_dense over RCCL.
+phase still sees the old in table. The 'pieces' form hands the output-table gradient over in
+row pieces, each exchanged (exchange_out_piece) before the next piece's rows are added, as
+bench.py does at N > 1 behind dw_sgns_walks_phase2_piece; it also runs with a piece count that
+does not divide the vocabulary (padding rows). The gradient and Adam math here is the
+oracle's (CPU); on the GPU the same ShardedTables object drives dw_sgns_walks_phase +
+dw_adam_dense over RCCL.
 """
 import os
 import socket
@@ -56,6 +60,7 @@ def grads(tables, ins, tgt, noise, share):
 
 
 def train(t, rank, world, mode):
+    """mode: 'serial' | 'overlap' | 'pieces'."""
     for ins, tgt, noise in batches():
         half = len(ins) // world
         sl = slice(rank * half, (rank + 1) * half)
@@ -69,21 +74,33 @@ def train(t, rank, world, mode):
             t.g_in.add_(gi)                      # pass 1: centre-table gradient final
             t.exchange_in()
             assert torch.equal(t.w_in, w_in_before)  # output-table phase sees the old in table
-            t.g_out.add_(go)                     # pass 2
+            if mode == 'pieces':
+                n_pieces, rows = t.out_pieces_spec()
+                for p in range(n_pieces):        # pass 2, piece by piece
+                    a, b = p * rows, min((p + 1) * rows, t.V)
+                    w_out_before = t.w_out[a:b].clone()
+                    if a < b:
+                        t.g_out[a:b].add_(go[a:b])
+                    t.exchange_out_piece(p)
+                    if world > 1 and a < b:
+                        assert not torch.equal(t.w_out[a:b], w_out_before)  # piece updated
+            else:
+                t.g_out.add_(go)                 # pass 2
             t.exchange_out()
             t.sync()
         assert float(t.grads.abs().max()) == 0.0
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, port, mode, pieces, q):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from shallow_encoders.word2vec.sharding import ShardedTables
-    t = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    t = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam, out_pieces=pieces)
     train(t, rank, world, mode)
-    q.put((rank, t.w_in.numpy().copy(), t.w_out.numpy().copy(), t.shard_range(),
-           t.m.numpy().copy()))
+    q.put((rank, t.w_in.numpy().copy(), t.w_out.numpy().copy(),
+           (t.shard_range(), t.P, t.S, t.V_pad),
+           [(t.state_rows(k).numpy(), t.m[k].numpy().copy()) for k in (0, 1)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -97,8 +114,9 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('mode', ['serial', 'overlap'])
-def test_sharded_adam_world2_equals_single_process(mode):
+@pytest.mark.parametrize('mode,pieces', [('serial', None), ('overlap', None), ('serial', 3),
+                                         ('pieces', None), ('pieces', 3)])
+def test_sharded_adam_world2_equals_single_process(mode, pieces):
     from shallow_encoders.word2vec.sharding import ShardedTables
     ref = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
     assert ref.world == 1
@@ -106,18 +124,25 @@ def test_sharded_adam_world2_equals_single_process(mode):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, pieces, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, i0, o0, r0, m0), (_, i1, o1, r1, m1) = res
+    (_, i0, o0, g0, st0), (_, i1, o1, g1, st1) = res
     np.testing.assert_array_equal(i0, i1)                 # replicas identical after all-gather
     np.testing.assert_array_equal(o0, o1)
-    assert r0 == (0, V // 2) and r1 == (V // 2, V)        # node-id-range rows of both tables
+    (r0, P, S, V_pad), (r1, _, _, _) = g0, g1
+    assert P == (pieces or 8) and V_pad % (2 * P) == 0 and V_pad >= V
+    assert r0 == (0, S) and r1 == (S, 2 * S)              # node-id ranges of the in table
     np.testing.assert_allclose(i0, ref.w_in.numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(o0, ref.w_out.numpy(), rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(np.concatenate([m0, m1], axis=1), ref.m.numpy(), rtol=1e-4,
-                               atol=1e-9)
+    for k in (0, 1):                                      # Adam state, by global row
+        rows = np.concatenate([st0[k][0], st1[k][0]])
+        m = np.concatenate([st0[k][1], st1[k][1]])
+        assert sorted(rows.tolist()) == list(range(V_pad))   # every row owned exactly once
+        keep = rows < V
+        np.testing.assert_allclose(m[keep][np.argsort(rows[keep])], ref.m[k].numpy(),
+                                   rtol=1e-4, atol=1e-9)

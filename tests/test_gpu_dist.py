@@ -4,8 +4,11 @@ dw_sgns_walks_phase + ShardedTables.exchange_in / exchange_out / sync with the H
 This exercises the side-stream ordering: the in-table reduce-scatter / Adam / all-gather is
 issued after pass 1 while pass 2 still reads the old in table from the other buffer. After a
 few steps both replicas must equal a single-process run (world 1, serial step) over the whole
-batch. The RCCL variant of the same code runs in bench.py at N > 1; RCCL refuses two ranks on
-one device, so gloo carries the collectives here.
+batch. The 'pieces' form runs the output-table phase in row pieces (sgns_phase2_pieces ->
+dw_sgns_walks_phase2_piece) with each piece exchanged on the side stream behind the next
+piece's gather (ShardedTables.exchange_out_piece), as bench.py does at N > 1. The RCCL variant
+of the same code runs in bench.py at N > 1; RCCL refuses two ranks on one device, so gloo
+carries the collectives here.
 """
 import os
 import socket
@@ -26,8 +29,9 @@ def walks_all():
     return torch.randint(1, V, (STEPS, NW, L), generator=g, dtype=torch.int32)
 
 
-def run(tables, walks, rank, world, overlapped):
-    from shallow_encoders.word2vec.sgns import sgns_accumulate
+def run(tables, walks, rank, world, mode):
+    """mode: 'serial' | 'overlap' | 'pieces'."""
+    from shallow_encoders.word2vec.sgns import sgns_accumulate, sgns_phase2_pieces
     dev = tables.device
     per = L - 2 * R
     scale = 1.0 / (NW * per * 2 * R)
@@ -36,10 +40,17 @@ def run(tables, walks, rank, world, overlapped):
         w = walks[s, rank * half:(rank + 1) * half].to(dev)
         kw = dict(walks=w, context_radius=R, seed=11, noise_offset=s * NW * per + rank * half * per,
                   grad_scale=scale)
-        if overlapped:
+        if mode != 'serial':
             sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
             tables.exchange_in()
-            sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2, **kw)
+            if mode == 'pieces':
+                n_pieces, rows = tables.out_pieces_spec()
+                sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=w, context_radius=R,
+                                   n_pieces=n_pieces, piece_rows=rows,
+                                   on_piece=tables.exchange_out_piece)
+            else:
+                sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K,
+                                phase=2, **kw)
             tables.exchange_out()
             tables.sync()
         else:
@@ -49,14 +60,14 @@ def run(tables, walks, rank, world, overlapped):
     return tables.w_in.cpu().numpy().copy(), tables.w_out.cpu().numpy().copy()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, mode, pieces, q):
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
         dist.init_process_group('gloo', rank=rank, world_size=world)
         from shallow_encoders.word2vec.sharding import ShardedTables
-        t = ShardedTables(V, D, 'cuda:0', lr=LR, init_seed=4)
-        wi, wo = run(t, walks_all(), rank, world, True)
+        t = ShardedTables(V, D, 'cuda:0', lr=LR, init_seed=4, out_pieces=pieces)
+        wi, wo = run(t, walks_all(), rank, world, mode)
         q.put((rank, wi, wo, None))
         dist.barrier()
         dist.destroy_process_group()
@@ -73,14 +84,15 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-def test_overlapped_exchange_two_ranks_equals_single_process(hip_device):
+@pytest.mark.parametrize('mode,pieces', [('overlap', None), ('pieces', None), ('pieces', 7)])
+def test_overlapped_exchange_two_ranks_equals_single_process(hip_device, mode, pieces):
     from shallow_encoders.word2vec.sharding import ShardedTables
     ref = ShardedTables(V, D, hip_device, lr=LR, init_seed=4)
-    ri, ro = run(ref, walks_all(), 0, 1, False)
+    ri, ro = run(ref, walks_all(), 0, 1, 'serial')
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, pieces, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda x: x[0])

@@ -155,6 +155,45 @@ def test_adam_kernel_vs_torch_adam_random_grads(hip_device):
                                ropt.state[ref]['exp_avg_sq'].numpy(), rtol=1e-5, atol=1e-10)
 
 
+@pytest.mark.parametrize('n_pieces,extra', [(1, 0), (3, 0), (8, 5), (64, 0), (1024, 0)])
+def test_phase2_pieces_equal_phase2(hip_device, n_pieces, extra):
+    """dw_sgns_walks_phase2_piece: the sort call then the gathers of n_pieces row pieces (some
+    empty, piece_rows over-covering V by `extra` rows per piece) give phase 2's g_out (float
+    atomic order aside: chunk boundaries move with the pieces), and each piece call touches
+    only its own rows."""
+    from shallow_encoders.word2vec.sgns import sgns_phase2_pieces
+    g = torch.Generator().manual_seed(n_pieces)
+    V, d, R, K, n, L = 3000, 128, 3, 4, 200, 30
+    walks = torch.randint(0, V, (n, L), generator=g, dtype=torch.int32)
+    walks[:, ::4] = 5                                   # a hub row spanning many chunks
+    walks = walks.to(hip_device)
+    w_in = (torch.rand((V, d), generator=g) - 0.5).to(hip_device)
+    w_out = (torch.rand((V, d), generator=g) - 0.5).to(hip_device)
+    kw = dict(walks=walks, context_radius=R, seed=3)
+    ref_in, ref_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    sgns_accumulate(w_in, w_out, ref_in, ref_out, K, **kw)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    sgns_accumulate(w_in, w_out, g_in, g_out, K, phase=1, **kw)
+    rows = -(-V // n_pieces) + extra
+    seen = []
+
+    def on_piece(p):
+        torch.cuda.synchronize()
+        done = g_out.abs().sum(dim=1) > 0
+        lo, hi = p * rows, min((p + 1) * rows, V)
+        assert not bool(done[hi:].any()), f'piece {p} wrote rows of later pieces'
+        seen.append(p)
+
+    sgns_phase2_pieces(w_in, g_out, K, walks=walks, context_radius=R, n_pieces=n_pieces,
+                       piece_rows=rows, on_piece=on_piece)
+    torch.cuda.synchronize()
+    assert seen == list(range(n_pieces))
+    np.testing.assert_allclose(g_in.cpu().numpy(), ref_in.cpu().numpy(), rtol=1e-5,
+                               atol=1e-7 * float(ref_in.abs().max()))
+    np.testing.assert_allclose(g_out.cpu().numpy(), ref_out.cpu().numpy(), rtol=1e-5,
+                               atol=1e-7 * float(ref_out.abs().max()))
+
+
 @pytest.mark.parametrize('max_blocks', [0, 32, 47])
 def test_adam_dense_to_equals_in_place(hip_device, max_blocks):
     """dw_adam_dense_to (read one buffer, write another; capped grid-stride grids) is
