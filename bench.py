@@ -123,6 +123,15 @@ def main():
                     help='N>1: output-table pieces (default sharding.DEFAULT_OUT_PIECES)')
     ap.add_argument('--no-overlap-in', action='store_true',
                     help='N=1: run the in-table Adam after the output-table phase (serial)')
+    ap.add_argument('--dist-mode', default='owner', choices=['owner', 'replicated'],
+                    help='N>1 layout: owner = out table sharded by row owner, every rank forms '
+                         'the whole global batch and computes its own rows\' slots, only the in '
+                         'table is exchanged (OwnerTables); replicated = both tables replicated, '
+                         'both exchanged (ShardedTables)')
+    ap.add_argument('--emulate-world', type=int, default=0,
+                    help='one GPU, measurement only: run rank 0\'s share of an owner-mode job of '
+                         'this many ranks (its walks, slots, Adam rows) without the collectives; '
+                         'value is then a projection (comm assumed hidden)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
@@ -151,7 +160,8 @@ def main():
     from shallow_encoders.graph.rmat import rmat_graph
     from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
                                                sgns_phase2_pieces, sgns_phase_bytes)
-    from shallow_encoders.word2vec.sharding import ShardedTables, overlap_adam_blocks
+    from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
+    from shallow_encoders.word2vec.sharding import OwnerTables, ShardedTables, overlap_adam_blocks
     _native.require_device(dev)
 
     t0 = time.time()
@@ -166,25 +176,77 @@ def main():
         walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
-    tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
-                           overlap_in=not args.no_overlap_in,
-                           out_pieces=None if args.no_out_pieces else args.out_pieces)
+    emulate = args.emulate_world if (world == 1 and args.emulate_world > 1) else 0
+    owner = emulate > 0 or (world > 1 and args.dist_mode == 'owner')
+    if owner and not (args.scatter == 'sorted' and d % 64 == 0 and d <= 512
+                      and 2 * R * (1 + K) <= 64):
+        raise SystemExit('owner mode needs the sorted path, d a multiple of 64 (<= 512) and '
+                         '2R(1+K) <= 64; use --dist-mode replicated')
+    W_eff = emulate or world            # ranks of the (possibly emulated) job
+    if owner:
+        tables = OwnerTables(V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
+    else:
+        tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
+                               overlap_in=not args.no_overlap_in,
+                               out_pieces=None if args.no_out_pieces else args.out_pieces)
     centres = B * (L - 2 * R)
     pairs_per_step = centres * 2 * R
-    grad_scale = 1.0 / (pairs_per_step * world)   # mean over the GLOBAL batch
+    grad_scale = 1.0 / (pairs_per_step * W_eff)   # mean over the GLOBAL batch
     walks_total = N * args.walks_per_node
-    walks_buf = torch.empty((B, L), dtype=torch.int32, device=dev)
-    starts_buf = torch.empty(B, dtype=torch.int32, device=dev)
+    BG = B * W_eff if owner else B      # walks each rank generates per step (owner: all ranks')
+    walks_buf = torch.empty((BG, L), dtype=torch.int32, device=dev)
+    starts_buf = torch.empty(BG, dtype=torch.int32, device=dev)
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
     fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
-    pieces = world > 1 and not args.no_out_pieces
+    pieces = world > 1 and not args.no_out_pieces and not owner
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
     pb = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     p2_bytes = pb['sort'] + pb['pass2']        # the phase the in-table Adam overlaps
 
+    def owner_one_step(record: bool):
+        # every rank: the whole global batch's walks -> its own slots (pass 1) -> in-table
+        # exchange on the side stream -> records sort + gather with the slice's Adam fused
+        s = step_idx[0]
+        step_idx[0] += 1
+        g0 = s * BG                                   # global walk id of the step's batch
+        ids = (torch.arange(g0, g0 + BG, device=dev, dtype=torch.int64) % walks_total)
+        torch.floor_divide(ids, args.walks_per_node, out=ids)
+        starts_buf.copy_(ids + 1)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
+        if record:
+            e[1].record()
+        sgns_owner_pass1(tables.w_in, tables.w_out, tables.grads_in, K, walks=walks_buf,
+                         context_radius=R, owner=tables.rank, n_owners=tables.world,
+                         vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
+                         grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+        tables.exchange_in(overlap_bytes=owner_p2_bytes)
+        spec = tables.out_adam_spec() if fuse else None
+        n_rec[0] = sgns_owner_pass2(tables.w_in, tables.w_out, tables.g_out, K, walks=walks_buf,
+                                    context_radius=R, out_adam=spec, status=status)
+        if spec is None:
+            tables.out_step()
+        if record:
+            e[2].record()
+        tables.sync()
+        if record:
+            e[3].record()
+            ev['walk'].append((e[0], e[1]))
+            ev['sgns'].append((e[1], e[2]))
+            ev['adam'].append((e[2], e[3]))
+
+    n_rec = [0]
+    # the owner output-table phase (sort + gather + slice Adam), for the in-table Adam's grid:
+    # ~1/W of the one-GPU phase's records
+    owner_p2_bytes = (p2_bytes / W_eff + V * d * 24 / W_eff) if owner else None
+
     def one_step(record: bool):
+        if owner:
+            return owner_one_step(record)
         s = step_idx[0]
         step_idx[0] += 1
         g0 = (s * world + rank) * B                   # global walk id of this rank's batch
@@ -250,10 +312,14 @@ def main():
         elapsed = float(t)
     _native.check_status(status, 'bench')
     kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
-    terms = loss_terms(loss_acc, pairs_per_step * args.steps, K)
-    mean_loss = float(terms['loss'])
+    if owner and world > 1:             # each rank summed the loss terms of its own slots
+        dist.all_reduce(loss_acc)
+    terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
+    mean_loss = None if emulate else float(terms['loss'])
 
-    total_pairs = pairs_per_step * args.steps * world
+    # weak scaling: the job processes B walks per rank per step (owner: W*B walks, each rank a
+    # 1/W share of their slots)
+    total_pairs = pairs_per_step * args.steps * W_eff
     value = total_pairs / elapsed
     bpp = sgns_bytes_per_pair(d, K, R)
     sgns_ms = phases['pass1'] + phases['sort'] + phases['pass2']
@@ -262,11 +328,27 @@ def main():
     out_adam_bytes = V * d * 4 * 7 if fuse else 0
     # one GPU, overlap_in: the in-table Adam (the other V*d*4 B x 7) runs on a side stream
     # inside the output-table phase; the window then ends when both streams are done
-    overlap_in = world == 1 and tables.overlap_in
+    overlap_in = world == 1 and not owner and tables.overlap_in
     in_adam_bytes = V * d * 4 * 7 if overlap_in else 0
     op_ms = sgns_ms + (kern_ms['adam'] if overlap_in else 0.0)
+    if owner:
+        # this rank's share of the job's algorithmic bytes: 1/W of the pairs' SGNS bytes and of
+        # both tables' dense Adam (out slice fused in pass 2, own in-table rows on the side
+        # stream); the window runs to the end of the in-table update
+        out_adam_bytes = V * d * 4 * 7 // W_eff
+        in_adam_bytes = V * d * 4 * 7 // W_eff
+        op_ms = sgns_ms + kern_ms['adam']
     sgns_gbs = (pairs_per_step * bpp + out_adam_bytes + in_adam_bytes) / (op_ms * 1e-3) / 1e9
     phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
+    if owner:
+        # implementation byte model of one rank's owner passes: every centre of the global
+        # batch reads its in row and adds its partial gradient row; n_rec owned slots each
+        # gather an out row (pass 1) and a centre row (pass 2) with 12-B records; the slice Adam
+        c_all, rows4 = BG * (L - 2 * R), 4 * d
+        bits = max(1, math.ceil(math.log2(tables.S)))
+        phase_bytes = {'pass1': c_all * 2 * rows4 + n_rec[0] * (rows4 + 12) + BG * L * 4,
+                       'sort': n_rec[0] * (4 + 24 * math.ceil(bits / 11)),
+                       'pass2': n_rec[0] * (12 + rows4) + tables.S * d * 24}
     phase_info = {k: {'ms': phases[k], 'bytes_model': phase_bytes[k],
                       'GBps': phase_bytes[k] / (phases[k] * 1e-3) / 1e9 if phases[k] else None}
                   for k in ('pass1', 'sort', 'pass2')}
@@ -313,19 +395,30 @@ def main():
                          f'{args.method}{f" p={args.p} q={args.q}" if args.method == "node2vec" else ""} L={L}, '
                          f'R={R}, K={K}, d={d}, dense Adam; {B} walks/step/GPU; '
                          f'{args.scatter} output-table scatter'),
-            'global_batch_walks': B * world, 'positive_pairs_per_step_per_gpu': pairs_per_step,
-            'parallelism': (f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather, '
-                            f'in-table exchange overlapped'
-                            + (f', out table in {tables.P} pieces pipelined' if pieces else '')
-                            + ')' if backend == 'nccl' else
-                            f'REHEARSAL dp{world} over {backend}, all ranks on one device'),
+            'global_batch_walks': B * W_eff, 'positive_pairs_per_step_per_gpu': pairs_per_step,
+            'parallelism': (
+                f'EMULATED rank 0 of {W_eff} on one GPU (owner-computes; no collectives run, '
+                f'value is a projection assuming the in-table exchange stays hidden)' if emulate
+                else f'REHEARSAL dp{world} over {backend}, all ranks on one device'
+                if backend != 'nccl' and world > 1 else
+                f'dp{world} owner-computes (out table sharded by row owner o % {world}, no '
+                f'out-table collective; in table replicated, RCCL reduce-scatter / all-gather '
+                f'overlapped with the output-table phase)' if owner else
+                f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather, '
+                f'in-table exchange overlapped'
+                + (f', out table in {tables.P} pieces pipelined' if pieces else '') + ')'),
         },
         'walks_per_s': walk_stats.get('deepwalk'),
         'walks_per_s_node2vec_p0.25_q4': walk_stats.get('node2vec'),
         'kernel_ms': kern_ms,
+        'records_per_step_per_gpu': n_rec[0] if owner else pairs_per_step * (1 + K),
         'mean_loss': mean_loss,
         'roofline': {
-            'kernel': (('dw_sgns_walks_phase 1 + dw_sgns_walks_phase2_adam = k_sgns_g16 + rocprim '
+            'kernel': ('dw_sgns_owner_pass1 + dw_sgns_owner_pass2 = k_sgns_g16<owner> + rocprim '
+                       'onesweep radix sort + k_rec_gather with the out-slice Adam fused + '
+                       'k_adam_rest || own in-table rows: reduce-scatter, k_adam, all-gather '
+                       '(side stream)') if owner else
+                      (('dw_sgns_walks_phase 1 + dw_sgns_walks_phase2_adam = k_sgns_g16 + rocprim '
                         'onesweep radix sort + k_rec_gather with the out-table Adam fused + '
                         'k_adam_rest' + (' || in-table k_adam (dw_adam_dense_to, side stream)'
                                          if overlap_in else '')) if fuse else
@@ -347,11 +440,12 @@ def main():
         try:
             with open(prof) as f:
                 doc = json.load(f)
-            want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in)
+            want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in, W_eff if owner else 0)
             pmc = next((e for e in doc.get('entries', []) if
                         (e.get('pairs_per_launch'), e.get('scatter'), e.get('dim'),
                          e.get('vocab_size'), bool(e.get('fused_out_adam')),
-                         bool(e.get('overlap_in'))) == want), None)
+                         bool(e.get('overlap_in')), int(e.get('owner_world') or 0)) == want),
+                       None)
             if pmc is not None:
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')
                 result['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({pmc.get('round')})"

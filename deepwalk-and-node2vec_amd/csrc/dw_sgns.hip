@@ -138,6 +138,12 @@ struct SgnsArgs {
     int32_t *status;
     uint32_t *rec_key;        // records mode: [batch * T]
     uint64_t *rec_val;        //   {coef bits << 32 | centre id}
+    // owner-computes form (dw_sgns_owner_pass1): only output rows o with o % n_owners == owner,
+    // addressed as local row o / n_owners of w_out; wave g appends its records to its own region
+    // [g * region, (g+1) * region) of rec_key / rec_val and leaves the count in rec_counts[g]
+    int32_t owner, n_owners;
+    uint32_t *rec_counts;
+    int64_t region;
 };
 
 __device__ __forceinline__ int64_t noise_id(const SgnsArgs &a, int64_t b, int j, int k) {
@@ -344,12 +350,20 @@ __device__ __forceinline__ float row_sum16(float x) {
     return x;
 }
 
-template <int F4, bool FROM_WALKS, int CHR>
+// OWNER (dw_sgns_owner_pass1, N > 1): the group keeps only the output rows this rank owns
+// (o % n_owners == owner), compacted to the front of its id list in slot order (s_t keeps each
+// one's slot t for the positive / negative rule), so the chunk loop gathers ~T / n_owners rows
+// from the rank's local slice of the out table. Each wave appends its records to a region of
+// its own (sized for every slot of its grid-stride iterations), counted in a register: no
+// atomics (a shared counter took one same-address atomic per wave iteration — ~12 ns each,
+// serialised: 14 ms per pass at 8 owners); k_rec_compact packs the regions afterwards.
+template <int F4, bool FROM_WALKS, int CHR, bool OWNER>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
+    __shared__ uint8_t s_t[WAVES_PER_BLOCK][4][OWNER ? G16_TMAX : 1];
     __shared__ float4 s_g[WAVES_PER_BLOCK][4][16 * F4];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
@@ -358,6 +372,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
     const int T = a.C * rows_per_ctx;
     const int64_t n_slots = (int64_t)gridDim.x * WAVES_PER_BLOCK * 4;
     float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
+    int64_t filled = 0;  // OWNER: records in this wave's region so far (wave-uniform)
 
     for (int64_t base = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * 4; base < a.batch;
          base += n_slots) {
@@ -379,21 +394,42 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         const bool ok_c = active && cid >= 0 && cid < a.V;
         if (active && !ok_c && gl == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
         // the group's row ids (-1 = invalid row: zero coefficient); two Philox draws overlap
+        int n_own = T;  // rows in the group's list (OWNER: the owned ones, compacted)
+        if constexpr (OWNER) n_own = 0;
 #pragma unroll 2
         for (int k = 0; k < G16_TMAX / 16; ++k) {
             const int t = gl + 16 * k;
-            if (t < T) {
-                int32_t id = -1;
-                if (ok_c) {
-                    const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, t);
-                    if (r >= 0 && r < a.V)
-                        id = static_cast<int32_t>(r);
-                    else
-                        dw::status_or(a.status, DW_S_BAD_INDEX);
+            int32_t id = -1;
+            if (t < T && ok_c) {
+                const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, t);
+                if (r >= 0 && r < a.V)
+                    id = static_cast<int32_t>(r);
+                else
+                    dw::status_or(a.status, DW_S_BAD_INDEX);
+            }
+            if constexpr (OWNER) {
+                const bool own = id >= 0 && (id % a.n_owners) == a.owner;
+                const uint32_t grp =
+                    static_cast<uint32_t>(__ballot(own) >> (16 * q)) & 0xFFFFu;
+                if (own) {
+                    const int pos = n_own + __popc(grp & ((1u << gl) - 1u));
+                    s_id[wv][q][pos] = id / a.n_owners;
+                    s_t[wv][q][pos] = static_cast<uint8_t>(t);
                 }
+                n_own += __popc(grp);
+            } else if (t < T) {
                 s_id[wv][q][t] = id;
                 s_coef[wv][q][t] = 0.f;
             }
+        }
+        // rows the chunk loop runs over: wave-uniform (the longest of the four groups' lists)
+        int n_loop = T;
+        if constexpr (OWNER) {
+            const int c0 = __builtin_amdgcn_readlane(n_own, 0);
+            const int c1 = __builtin_amdgcn_readlane(n_own, 16);
+            const int c2 = __builtin_amdgcn_readlane(n_own, 32);
+            const int c3 = __builtin_amdgcn_readlane(n_own, 48);
+            n_loop = max(max(c0, c1), max(c2, c3));
         }
         float4 c4[F4], g4[F4];
         const float *crow = a.w_in + (ok_c ? cid : 0) * D + 4 * gl;
@@ -408,7 +444,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 #pragma unroll
             for (int u = 0; u < CHR; ++u) {
                 const int t = t0 + u;
-                rid[u] = (t < T) ? s_id[wv][q][t] : -1;
+                rid[u] = (t < n_own) ? s_id[wv][q][t] : -1;
                 const float *row = a.w_out + static_cast<int64_t>(rid[u] < 0 ? 0 : rid[u]) * D +
                                    4 * gl;
 #pragma unroll
@@ -443,8 +479,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 }
             float coef = 0.f;
             const int t = t0 + gl;
-            if (gl < CHR && t < T && xid >= 0) {
-                coef = row_coef(x, (t % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg, acc_rec,
+            if (gl < CHR && t < n_own && xid >= 0) {
+                const int slot = OWNER ? static_cast<int>(s_t[wv][q][t]) : t;
+                coef = row_coef(x, (slot % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg, acc_rec,
                                 acc_prec);
                 s_coef[wv][q][t] = coef;
             }
@@ -462,7 +499,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         };
         // (a software-pipelined variant — next chunk in flight — and 2- / 8-row chunks measured
         // the same on MI355X: the kernel is HBM-bound once the loss atomics were removed)
-        for (int t0 = 0; t0 < T; t0 += CHR) {
+        for (int t0 = 0; t0 < n_loop; t0 += CHR) {
             float4 o4[CHR][F4];
             int32_t rid[CHR];
             load_chunk(o4, rid, t0);
@@ -471,7 +508,23 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 #pragma unroll
         for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
         dw::wave_lds_sync();
-        if (active) {  // records: lane gl writes rows gl, gl+16, ... of its centre
+        if constexpr (OWNER) {  // the wave's owned records, appended to its region
+            const int c0 = __builtin_amdgcn_readlane(n_own, 0);
+            const int c1 = __builtin_amdgcn_readlane(n_own, 16);
+            const int c2 = __builtin_amdgcn_readlane(n_own, 32);
+            const int c3 = __builtin_amdgcn_readlane(n_own, 48);
+            const int64_t at = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * a.region + filled +
+                               (q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2);
+#pragma unroll
+            for (int k = 0; k < G16_TMAX / 16; ++k) {
+                const int tt = gl + 16 * k;
+                if (tt < n_own) {
+                    a.rec_key[at + tt] = static_cast<uint32_t>(s_id[wv][q][tt]);
+                    a.rec_val[at + tt] = pack_record(s_coef[wv][q][tt], cid);
+                }
+            }
+            filled += c0 + c1 + c2 + c3;
+        } else if (active) {  // records: lane gl writes rows gl, gl+16, ... of its centre
 #pragma unroll
             for (int k = 0; k < G16_TMAX / 16; ++k) {
                 const int tt = gl + 16 * k;
@@ -486,8 +539,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         const float *sg_flat = reinterpret_cast<const float *>(&s_g[wv][0][0]);
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-            const int32_t cq = __builtin_amdgcn_readlane(ok_c ? static_cast<int32_t>(cid) : -1,
-                                                         qq * 16);
+            const int32_t cq = __builtin_amdgcn_readlane(
+                ok_c && n_own > 0 ? static_cast<int32_t>(cid) : -1, qq * 16);
             if (cq >= 0) {
                 float *dst = a.g_in + static_cast<int64_t>(cq) * D;
                 // s_g[qq] holds float4 slot j = gl + 16f -> elements 4gl + 64f .. +3
@@ -500,6 +553,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             }
         }
         dw::wave_lds_sync();
+    }
+    if constexpr (OWNER) {
+        if (lane == 0) a.rec_counts[(int64_t)blockIdx.x * WAVES_PER_BLOCK + wv] =
+            static_cast<uint32_t>(filled);
     }
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
@@ -542,6 +599,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         const int64_t e1 = (e0 + GCH < hi) ? e0 + GCH : hi;
         const uint32_t before = e0 > lo ? keys[e0 - 1] : 0xFFFFFFFFu;
         const uint32_t after = e1 < hi ? keys[e1] : 0xFFFFFFFFu;
+        // lanes past the chunk's end repeat its LAST key: a partial final group must not switch
+        // `cur` back to an earlier row (that flushed the row a second time, with g = 0 — an extra
+        // Adam step in the fused form)
+        const uint32_t last = keys[e1 - 1];
         uint32_t cur = keys[e0];
         float g[VPL];
 #pragma unroll
@@ -583,7 +644,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             for (int u = 0; u < GU; ++u) {
                 const bool in = e + u < e1;
                 const uint64_t v = in ? vals[e + u] : 0ull;
-                k[u] = in ? keys[e + u] : cur;
+                k[u] = in ? keys[e + u] : last;
                 coef[u] = in ? __uint_as_float(static_cast<uint32_t>(v >> 32)) : 0.f;
                 const float *src = w_in + static_cast<int64_t>(static_cast<uint32_t>(v)) * d + lane;
 #pragma unroll
@@ -612,11 +673,15 @@ int end_bit_for(int64_t V) {
 }
 
 constexpr int MAX_PIECES = 1024;  // row pieces of dw_sgns_walks_phase2_piece
+constexpr int MAX_OWNER_WAVES = 1 << 16;  // pass-1 waves of the owner form (grid_cap(8) * 4)
 
 struct Workspace {
     uint32_t *k0, *k1;
     uint64_t *v0, *v1;
     int64_t *bounds;  // [MAX_PIECES + 1] record bounds of the row pieces
+    uint32_t *count;  // records of the owner form (dw_sgns_owner_pass1), after compaction
+    uint32_t *wave_counts;   // [MAX_OWNER_WAVES] records per pass-1 wave region (owner form)
+    int64_t *wave_offsets;   // [MAX_OWNER_WAVES] their exclusive prefix sums
     void *cub;
     size_t cub_bytes;
     size_t total;
@@ -649,8 +714,17 @@ int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStrea
     ws->k1 = reinterpret_cast<uint32_t *>(p + kbytes);
     ws->v0 = reinterpret_cast<uint64_t *>(p + 2 * kbytes);
     ws->v1 = reinterpret_cast<uint64_t *>(p + 2 * kbytes + vbytes);
-    const size_t bbytes = align256(sizeof(int64_t) * (MAX_PIECES + 1));
-    ws->bounds = reinterpret_cast<int64_t *>(p + 2 * kbytes + 2 * vbytes);
+    const size_t wbytes = align256(sizeof(uint32_t) * MAX_OWNER_WAVES) +
+                          align256(sizeof(int64_t) * MAX_OWNER_WAVES);
+    const size_t bbytes = align256(sizeof(int64_t) * (MAX_PIECES + 1)) + 256 + wbytes;
+    char *q = p + 2 * kbytes + 2 * vbytes;
+    ws->bounds = reinterpret_cast<int64_t *>(q);
+    q += align256(sizeof(int64_t) * (MAX_PIECES + 1));
+    ws->count = reinterpret_cast<uint32_t *>(q);
+    q += 256;
+    ws->wave_counts = reinterpret_cast<uint32_t *>(q);
+    q += align256(sizeof(uint32_t) * MAX_OWNER_WAVES);
+    ws->wave_offsets = reinterpret_cast<int64_t *>(q);
     ws->cub = p + 2 * kbytes + 2 * vbytes + bbytes;
     ws->cub_bytes = cub_bytes;
     ws->total = 2 * kbytes + 2 * vbytes + bbytes + align256(cub_bytes);
@@ -701,7 +775,7 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
 
 // 16-lane-group pass 1 when d is a multiple of 64 (<= 512) and 2R(1+K) <= 64; otherwise
 // DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns). DW_SGNS_G16=0 disables it.
-template <bool FROM_WALKS>
+template <bool FROM_WALKS, bool OWNER = false>
 int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     static const bool enabled = [] {
         const char *e = getenv("DW_SGNS_G16");
@@ -714,10 +788,10 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     switch (a.d / 64) {  // rows per chunk: CHR * F4 float4 registers per lane
-        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8>), g, bl, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4>), g, bl, 0, st, a); break;
-        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2>), g, bl, 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1>), g, bl, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, OWNER>), g, bl, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER>), g, bl, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, OWNER>), g, bl, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER>), g, bl, 0, st, a); break;
         default: return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns/g16");
@@ -1007,6 +1081,171 @@ int launch_pieces(SgnsArgs a, void *workspace, size_t workspace_bytes, int piece
     return DW_OK;
 }
 
+// ---- owner-computes form (N > 1: the out table sharded by row owner, no out-table exchange) ---
+// Every rank forms ALL the global batch's windows but keeps only the output slots whose row it
+// owns (o % n_owners == owner). Pass 1 writes their records (local row o / n_owners) into one
+// region per wave and adds the centre-table gradient of those slots into the full g_in
+// (reduce-scattered by the caller); k_wave_scan + k_rec_compact pack the regions in wave order
+// (so the records, and pass 2's per-row sums, come out in the same order every run). Pass 2
+// sorts them by local row and gathers, with the slice's Adam fused in or not. The regions are
+// sized for every slot of a wave's iterations, so they can never overflow.
+struct OwnerLayout {
+    int64_t blocks, n_waves, region, total;
+};
+
+OwnerLayout owner_layout(int64_t n_centres, int64_t T) {
+    OwnerLayout l;
+    l.blocks = (n_centres + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);  // = launch_pass1_g16
+    if (l.blocks > grid_cap(8)) l.blocks = grid_cap(8);
+    if (l.blocks < 1) l.blocks = 1;
+    l.n_waves = l.blocks * WAVES_PER_BLOCK;
+    const int64_t per_sweep = l.n_waves * 4;  // centres per grid-stride iteration
+    const int64_t iters = (n_centres + per_sweep - 1) / per_sweep;
+    l.region = iters * 4 * T;
+    l.total = l.n_waves * l.region;
+    return l;
+}
+
+// exclusive prefix sums of the per-wave record counts (one block; n <= MAX_OWNER_WAVES); the
+// total goes to *count
+__global__ void __launch_bounds__(1024)
+    k_wave_scan(const uint32_t *__restrict__ counts, int64_t n, int64_t *__restrict__ offsets,
+                uint32_t *__restrict__ count) {
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024;
+    const int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
+    int64_t sum = 0;
+    for (int64_t i = lo; i < hi; ++i) sum += counts[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the partials
+        const int64_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int64_t run = part[t] - sum;  // exclusive prefix of this thread's first count
+    for (int64_t i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+    if (t == 1023) *count = static_cast<uint32_t>(part[1023]);
+}
+
+// wave g's region [g * region, g * region + counts[g]) of (k_src, v_src) -> offsets[g] of (k_dst,
+// v_dst); one block per region (grid-stride beyond the grid)
+__global__ void __launch_bounds__(256)
+    k_rec_compact(const uint32_t *__restrict__ counts, const int64_t *__restrict__ offsets,
+                  int64_t n_waves, int64_t region, const uint32_t *__restrict__ k_src,
+                  const uint64_t *__restrict__ v_src, uint32_t *__restrict__ k_dst,
+                  uint64_t *__restrict__ v_dst) {
+    for (int64_t g = blockIdx.x; g < n_waves; g += gridDim.x) {
+        const int64_t n = counts[g], src = g * region, dst = offsets[g];
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            k_dst[dst + i] = k_src[src + i];
+            v_dst[dst + i] = v_src[src + i];
+        }
+    }
+}
+
+int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *workspace,
+                    size_t workspace_bytes, Workspace *ws, OwnerLayout *lay, hipStream_t st,
+                    const char *what) {
+    *lay = owner_layout(n_centres, T);
+    DW_REQUIRE(lay->total < 0x7FFFFFFF, "%s: too many records (%lld)", what,
+               (long long)lay->total);
+    DW_REQUIRE(lay->n_waves <= MAX_OWNER_WAVES, "%s: %lld pass-1 waves > %d", what,
+               (long long)lay->n_waves, MAX_OWNER_WAVES);
+    DW_REQUIRE(workspace != nullptr, "%s: needs the records workspace", what);
+    int rc = plan_workspace(lay->total, local_rows, workspace, ws, st);
+    if (rc != DW_OK) return rc;
+    DW_REQUIRE(workspace_bytes >= ws->total, "%s: workspace too small (%zu < %zu)", what,
+               workspace_bytes, ws->total);
+    return DW_OK;
+}
+
+int launch_owner_pass1(SgnsArgs a, int64_t local_rows, void *workspace, size_t workspace_bytes,
+                       hipStream_t st) {
+    const int64_t T = (int64_t)a.C * (1 + a.K);
+    DW_REQUIRE(a.n_owners >= 1 && a.owner >= 0 && a.owner < a.n_owners,
+               "dw_sgns_owner_pass1: owner %d of %d", a.owner, a.n_owners);
+    DW_REQUIRE(local_rows * a.n_owners >= a.V, "dw_sgns_owner_pass1: %lld local rows x %d owners "
+               "do not cover %lld rows", (long long)local_rows, a.n_owners, (long long)a.V);
+    DW_REQUIRE(a.V <= 0x7FFFFFFF, "dw_sgns_owner_pass1: vocab_size must be < 2^31");
+    DW_REQUIRE(a.d % 64 == 0 && a.d <= 512 && T <= G16_TMAX,
+               "dw_sgns_owner_pass1: needs d a multiple of 64 (<= 512) and 2R(1+K) <= %d",
+               G16_TMAX);
+    Workspace ws;
+    OwnerLayout lay;
+    int rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
+                             "dw_sgns_owner_pass1");
+    if (rc != DW_OK) return rc;
+    g_timer.mark(0, st);
+    a.rec_key = ws.k0;
+    a.rec_val = ws.v0;
+    a.rec_counts = ws.wave_counts;
+    a.region = lay.region;
+    if (a.batch > 0) {
+        rc = launch_pass1_g16<true, true>(a, st);
+        if (rc != DW_OK) return rc;
+        hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts, lay.n_waves,
+                           ws.wave_offsets, ws.count);
+        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/scan");
+        int64_t cb = lay.n_waves < 65536 ? lay.n_waves : 65536;
+        hipLaunchKernelGGL(k_rec_compact, dim3((unsigned)cb), dim3(256), 0, st, ws.wave_counts,
+                           ws.wave_offsets, lay.n_waves, lay.region, ws.k0, ws.v0, ws.k1, ws.v1);
+        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/compact");
+    } else if (hipMemsetAsync(ws.count, 0, sizeof(uint32_t), st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner_pass1: counter reset failed");
+        return DW_E_HIP;
+    }
+    g_timer.mark(1, st);
+    return DW_OK;
+}
+
+int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
+                       const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
+                       size_t workspace_bytes, int64_t *n_records, hipStream_t st) {
+    Workspace ws;
+    OwnerLayout lay;
+    int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
+                             "dw_sgns_owner_pass2");
+    if (rc != DW_OK) return rc;
+    // the record count decides the sort's size on the host: one stream synchronisation
+    uint32_t n = 0;
+    if (hipMemcpyAsync(&n, ws.count, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner_pass2: reading the record count failed");
+        return DW_E_HIP;
+    }
+    const int64_t n_rec = static_cast<int64_t>(n) < n_centres * T ? n : n_centres * T;
+    if (n_records) *n_records = n_rec;
+    const uint32_t *keys = ws.k1;  // compacted by pass 1
+    const uint64_t *vals = ws.v1;
+    if (n_rec > 0) {
+        rocprim::double_buffer<uint32_t> kb(ws.k1, ws.k0);
+        rocprim::double_buffer<uint64_t> vb(ws.v1, ws.v0);
+        size_t cub_bytes = ws.cub_bytes;
+        hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
+            ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(local_rows),
+            st);
+        if (e != hipSuccess) {
+            dw::set_error("dw_sgns_owner_pass2: records sort failed: %s", hipGetErrorString(e));
+            return DW_E_HIP;
+        }
+        keys = kb.current();
+        vals = vb.current();
+    }
+    g_timer.mark(2, st);
+    if (n_rec > 0 || oa) {
+        rc = launch_pass2(keys, vals, n_rec, w_in, g_out, d, oa, local_rows, st);
+        if (rc != DW_OK) return rc;
+    }
+    g_timer.mark(3, st);
+    return DW_OK;
+}
+
 // ---- SkipGram.forward logits and its backward (autograd path of the reference API) ----------
 // logits[b, n] = <mean_p w_in[inputs[b, p]], w_out[outputs[b, n]]> (SkipGram: P = 1; CBOW:
 // P = the context width). One wave per row b.
@@ -1288,6 +1527,68 @@ int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
     return sgns_walks(phase, walks, n_walks, walk_length, context_radius, neg_samples,
                       vocab_size, dim, w_in, w_out, g_in, g_out, noise, seed, noise_offset,
                       grad_scale, loss_acc, status, workspace, workspace_bytes, stream);
+}
+
+int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
+                                  int64_t local_rows, size_t *bytes) {
+    DW_REQUIRE(bytes, "dw_sgns_owner_workspace_bytes: bytes is null");
+    DW_REQUIRE(n_centres >= 0 && n_ctx >= 1 && neg_samples >= 0 && local_rows >= 1,
+               "dw_sgns_owner_workspace_bytes: bad sizes");
+    const OwnerLayout lay = owner_layout(n_centres, (int64_t)n_ctx * (1 + neg_samples));
+    DW_REQUIRE(lay.total < 0x7FFFFFFF, "dw_sgns_owner_workspace_bytes: too many records");
+    Workspace ws;
+    char dummy;
+    int rc = plan_workspace(lay.total > 0 ? lay.total : 1, local_rows, &dummy, &ws, nullptr);
+    if (rc != DW_OK) return rc;
+    *bytes = ws.total;
+    return DW_OK;
+}
+
+int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                        int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                        int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                        const float *w_in, const float *w_out_local, float *g_in,
+                        const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                        float grad_scale, double *loss_acc, int32_t *status, void *workspace,
+                        size_t workspace_bytes, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0,
+               "dw_sgns_owner_pass1: bad sizes");
+    DW_REQUIRE((walks || n_walks == 0) && w_in && w_out_local && g_in && status,
+               "dw_sgns_owner_pass1: null pointer");
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out_local, g_in, nullptr, noise,
+                           seed, noise_offset, grad_scale, loss_acc, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    a.owner = owner;
+    a.n_owners = n_owners;
+    return launch_owner_pass1(a, local_rows, workspace, workspace_bytes, dw::as_stream(stream));
+}
+
+int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_radius,
+                        int32_t neg_samples, int64_t local_rows, int32_t dim, const float *w_in,
+                        float *w_out_local, float *g_out_local, float *m_out, float *v_out,
+                        uint8_t *row_flags, float one_minus_beta1, float beta2,
+                        float one_minus_beta2, float bias_correction2_sqrt, float neg_step_size,
+                        float eps, float weight_decay, int32_t *status, void *workspace,
+                        size_t workspace_bytes, int64_t *n_records, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && local_rows >= 1 && neg_samples >= 0,
+               "dw_sgns_owner_pass2: bad sizes");
+    DW_REQUIRE(w_in && g_out_local && status, "dw_sgns_owner_pass2: null pointer");
+    const bool adam = m_out != nullptr;
+    DW_REQUIRE(!adam || (v_out && row_flags && w_out_local && bias_correction2_sqrt > 0.f),
+               "dw_sgns_owner_pass2: the fused Adam needs w_out_local, m, v, flags, scalars");
+    OutAdam oa{w_out_local, m_out, v_out, row_flags,
+               dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
+                               neg_step_size, eps, weight_decay}};
+    const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
+    return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
+                              w_in, g_out_local, adam ? &oa : nullptr, workspace,
+                              workspace_bytes, n_records, dw::as_stream(stream));
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

@@ -28,11 +28,12 @@ DW_S_ZERO_WEIGHT = 2
 DW_S_REJECTION_CAP = 4
 DW_S_BAD_CSR = 8
 DW_S_BAD_INDEX = 16
+DW_S_RECORDS_FULL = 32
 
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -67,6 +68,13 @@ SIGNATURES = {
     'dw_sgns_walks_phase2_piece': (ctypes.c_int, [_i32, _i32, _i64, _p, _i64, _i32, _i32, _i32,
                                                    _i64, _i32, _p, _p, _p, _p, ctypes.c_size_t,
                                                    _p]),
+    'dw_sgns_owner_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),
+    'dw_sgns_owner_pass1': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32,
+                                           _i64, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p, _p,
+                                           ctypes.c_size_t, _p]),
+    'dw_sgns_owner_pass2': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p, _p,
+                                           _p, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p,
+                                           ctypes.c_size_t, _p, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                                  _f32, _f32, _p, _p, ctypes.c_size_t, _p]),
@@ -191,4 +199,6 @@ def check_status(status: torch.Tensor, what: str) -> None:
         raise ValueError(f'{what}: malformed CSR graph')
     if s & DW_S_BAD_INDEX:
         raise IndexError(f'{what}: index out of range [0, vocab_size)')
+    if s & DW_S_RECORDS_FULL:
+        raise RuntimeError(f'{what}: SGNS records exceeded the workspace')
     raise RuntimeError(f'{what}: device status {s:#x}')

@@ -48,13 +48,15 @@ def _use_records(scatter: str, n_ctx: int, neg_samples: int, vocab_size: int) ->
 
 
 def workspace_for(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int,
-                  device: torch.device) -> torch.Tensor:
+                  device: torch.device, owner: bool = False) -> torch.Tensor:
     """Device workspace of the atomic-free (records) output-table path, cached per device and
-    grown on demand (allocated outside any timed region after the first call)."""
+    grown on demand (allocated outside any timed region after the first call). ``owner``: sized
+    for dw_sgns_owner_pass1 (vocab_size = the local rows)."""
     import ctypes
     nbytes = ctypes.c_size_t(0)
-    _native.call('dw_sgns_workspace_bytes', int(n_centres), int(n_ctx), int(neg_samples),
-                 int(vocab_size), ctypes.byref(nbytes))
+    _native.call('dw_sgns_owner_workspace_bytes' if owner else 'dw_sgns_workspace_bytes',
+                 int(n_centres), int(n_ctx), int(neg_samples), int(vocab_size),
+                 ctypes.byref(nbytes))
     ws = _WORKSPACES.get(device)
     if ws is None or ws.numel() < nbytes.value:
         _WORKSPACES.pop(device, None)
@@ -309,3 +311,83 @@ class SGNSLoss(torch.autograd.Function):
                 _native.call('dw_scale', _native.ptr(g_out), g_out.numel(), 1.0, _native.ptr(go),
                              s)
         return g_in, g_out, None, None, None, None, None, None, None
+
+
+def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.Tensor,
+                     neg_samples: int, *, walks: torch.Tensor, context_radius: int, owner: int,
+                     n_owners: int, vocab_size: int, noise: Optional[torch.Tensor] = None,
+                     seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
+                     loss_acc: Optional[torch.Tensor] = None,
+                     status: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
+    batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
+    ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
+    partial centre-table gradient of the owned slots; returns the float64[4] loss accumulator
+    (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2."""
+    dev = w_in.device
+    d = w_in.shape[1]
+    local_rows = w_out_local.shape[0]
+    if w_out_local.shape[1] != d or g_in.shape[1] != d or g_in.shape[0] < vocab_size \
+            or w_in.shape[0] < vocab_size:
+        raise ValueError('w_in / g_in must be (>= V, d) and w_out_local (local_rows, d)')
+    if local_rows * n_owners < vocab_size:
+        raise ValueError('the owners\' local rows do not cover the vocabulary')
+    for t in (w_in, w_out_local, g_in):
+        if t.dtype != torch.float32:
+            raise TypeError('embedding tables and gradients must be float32')
+    if walks.dtype != torch.int32 or walks.dim() != 2:
+        raise TypeError('walks must be int32 [n_walks, L]')
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    n_centres = n * (L - 2 * R)
+    if noise is not None and noise.numel() != n_centres * 2 * R * K:
+        raise ValueError('noise must have B\' * 2R * K entries')
+    scale = 1.0 / max(n_centres * 2 * R, 1) if grad_scale is None else grad_scale
+    if loss_acc is None:
+        loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = workspace_for(n_centres, 2 * R, K, local_rows, dev, owner=True)
+    with torch.cuda.device(dev):
+        _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
+                     int(owner), int(n_owners), local_rows, _native.ptr(w_in),
+                     _native.ptr(w_out_local), _native.ptr(g_in), _native.ptr(noise),
+                     seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),
+                     _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws), ws.numel(),
+                     _native.stream(dev))
+    return loss_acc
+
+
+def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local: torch.Tensor,
+                     neg_samples: int, *, walks: torch.Tensor, context_radius: int,
+                     out_adam: Optional[dict] = None,
+                     status: Optional[torch.Tensor] = None) -> int:
+    """Pass 2 of the owner-computes step (dw_sgns_owner_pass2) after sgns_owner_pass1 with the
+    same walks: the records sort and gather over the local slice. ``out_adam`` ({'m', 'v',
+    'flags', 'scalars'}, OwnerTables.out_adam_spec()) fuses the slice's Adam step in (w_out_local
+    updated, g_out_local left zero); None accumulates g_out_local. Returns the record count
+    (the call synchronises the current stream once to read it)."""
+    import ctypes
+    dev = w_in.device
+    d = w_in.shape[1]
+    local_rows = w_out_local.shape[0]
+    if g_out_local.shape != w_out_local.shape or w_out_local.shape[1] != d:
+        raise ValueError('w_out_local and g_out_local must both be (local_rows, d)')
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = workspace_for(n * (L - 2 * R), 2 * R, K, local_rows, dev, owner=True)
+    n_rec = ctypes.c_int64(0)
+    if out_adam is not None:
+        m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
+                           _native.ptr(out_adam['flags']), out_adam['scalars'])
+    else:
+        m = v = flags = None
+        sc = (0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0)
+    with torch.cuda.device(dev):
+        _native.call('dw_sgns_owner_pass2', n, L, R, K, local_rows, d, _native.ptr(w_in),
+                     _native.ptr(w_out_local), _native.ptr(g_out_local), m, v, flags, *sc,
+                     _native.ptr(status), _native.ptr(ws), ws.numel(), ctypes.byref(n_rec),
+                     _native.stream(dev))
+    return int(n_rec.value)

@@ -379,3 +379,251 @@ class ShardedTables:
                 w.wait()
         self._ag = []
         self._cur_in = self._next_in
+
+
+class OwnerTables:
+    """N > 1, owner-computes layout (the multi-GPU default of bench.py).
+
+    The output ("context") table never crosses ranks: rank r holds only the rows o with
+    o % world == r (local row o // world; interleaved ownership spreads R-MAT's low-id hubs over
+    all ranks), with their Adam state, and updates them itself. Every rank forms the windows of
+    the WHOLE global batch (walks are keyed by the global walk id, so it generates them all)
+    and computes only the output slots whose row it owns (dw_sgns_owner_pass1 / _pass2); summed
+    over the ranks that is exactly the single-device computation, so this is DDP-equivalent
+    training of the global batch with no output-table collective at all.
+
+    The in table is replicated and double-buffered as in ShardedTables: each rank's pass 1 adds
+    the partial centre gradient of its owned slots into the dense g_in, and ``exchange_in``
+    reduce-scatters it by node-id range (rank r owns rows [r*S, (r+1)*S)), applies Adam to the
+    own rows and all-gathers them into the idle buffer, on a side stream behind the
+    output-table phase. Per step that is the in table's 2 x V*d*4 B over xGMI and nothing else
+    (ShardedTables moves both tables: twice that).
+
+      params_in  float32 [2, V_pad, d]   replicated in table, two buffers
+      g_in       float32 [V_pad, d]      partial (this rank's slots) centre gradient
+      m_in, v_in float32 [S, d]          Adam state of the own in-table rows
+      w_out      float32 [S, d]          local out-table slice (global row r + world*j)
+      g_out      float32 [S, d]          its gradient (zero between steps)
+      m_out, v_out float32 [S, d]        its Adam state
+
+    V_pad = V rounded up to a multiple of world, S = V_pad / world. ``adam_impl`` is injectable
+    as in ShardedTables (CPU tests over gloo).
+    """
+
+    def __init__(self, vocab_size: int, dim: int, device, lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 group=None, init_seed: Optional[int] = 0,
+                 adam_impl: Optional[Callable] = None, emulate_world: Optional[int] = None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # emulate_world (one process, measurement only: bench.py --emulate-world): act as rank 0
+        # of that many ranks — the same per-rank kernels and Adam shares, no collectives (the
+        # in-table rows of the other ranks are then never refreshed)
+        self.emulated = bool(emulate_world) and self.world == 1
+        if self.emulated:
+            self.world, self.rank = int(emulate_world), 0
+        self.V, self.d = int(vocab_size), int(dim)
+        self.V_pad = int(math.ceil(self.V / self.world)) * self.world
+        self.S = self.V_pad // self.world
+        self.device = torch.device(device)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.adam_impl = adam_impl or hip_adam
+        self.step_count = 0
+        self._cuda = self.device.type == 'cuda'
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.params_in = torch.zeros((2, self.V_pad, self.d), **f32)
+        self.grads_in = torch.zeros((self.V_pad, self.d), **f32)
+        self.m_in = torch.zeros((self.S, self.d), **f32)
+        self.v_in = torch.zeros_like(self.m_in)
+        self.grad_shard = (torch.empty_like(self.m_in) if self.world > 1 and not self.emulated
+                           else None)
+        self.w_out = torch.zeros((self.S, self.d), **f32)
+        self.g_out = torch.zeros_like(self.w_out)
+        self.m_out = torch.zeros_like(self.w_out)
+        self.v_out = torch.zeros_like(self.w_out)
+        self._flags = torch.zeros(self.S, dtype=torch.uint8, device=self.device)
+        self._cur_in = 0
+        self._next_in = 0
+        self._ag = []
+        self._overlap_bytes = None
+        self._side = torch.cuda.Stream(self.device) if self._cuda else None
+        if init_seed is not None:
+            self.xavier_(init_seed)
+
+    # ---- views -------------------------------------------------------------------------------
+    @property
+    def w_in(self) -> torch.Tensor:
+        return self.params_in[self._cur_in, :self.V]
+
+    @property
+    def g_in(self) -> torch.Tensor:
+        return self.grads_in[:self.V]
+
+    def shard_range(self):
+        """[start, end) rows of this rank's node range of the in table."""
+        return self.rank * self.S, (self.rank + 1) * self.S
+
+    def out_rows(self) -> torch.Tensor:
+        """Global row of each local out-table row (r, r + world, ...; some >= V are padding)."""
+        return torch.arange(self.S) * self.world + self.rank
+
+    def xavier_(self, seed: int) -> None:
+        """The same initial tables as ShardedTables.xavier_ (model.py:26-27), this rank's slice of
+        the out table."""
+        g = torch.Generator(device='cpu').manual_seed(int(seed))
+        a = math.sqrt(6.0 / (self.V + self.d))
+        w_in = torch.rand((self.V, self.d), generator=g) * (2 * a) - a
+        w_out = torch.rand((self.V, self.d), generator=g) * (2 * a) - a
+        self.load_(w_in, w_out)
+
+    def load_(self, w_in: torch.Tensor, w_out: torch.Tensor) -> None:
+        """Set the tables from full (V, d) tensors (every rank passes the same ones)."""
+        self.params_in[self._cur_in, :self.V].copy_(w_in)
+        rows = self.out_rows()
+        keep = rows < self.V
+        self.w_out.zero_()
+        self.w_out[keep] = w_out[rows[keep]].to(self.device)
+
+    def full_w_out(self) -> torch.Tensor:
+        """The whole (V, d) out table, gathered from every rank's slice (collective when N > 1)."""
+        if self.emulated:
+            raise RuntimeError('an emulated rank holds only its own slice')
+        if self.world == 1:
+            return self.w_out[:self.V].clone()
+        parts = torch.empty((self.world, self.S, self.d), dtype=torch.float32, device=self.device)
+        if dist.get_backend(self.group) == 'nccl':
+            dist.all_gather_into_tensor(parts.view(-1), self.w_out.view(-1), group=self.group)
+        else:
+            dist.all_gather(list(parts.unbind(0)), self.w_out.clone(), group=self.group)
+        # local row j of rank r is global row r + world * j
+        return parts.transpose(0, 1).reshape(self.V_pad, self.d)[:self.V].clone()
+
+    def out_state_full(self):
+        """(m, v) of the out table as full (V, d) tensors (gathered, as full_w_out)."""
+        res = []
+        for t in (self.m_out, self.v_out):
+            w, self.w_out = self.w_out, t
+            try:
+                res.append(self.full_w_out())
+            finally:
+                self.w_out = w
+        return tuple(res)
+
+    # ---- the step ------------------------------------------------------------------------------
+    def _adam(self, p, g, m, v, zero_grad: bool) -> None:
+        self.adam_impl(p, g, m, v, self.step_count, self.lr, self.betas, self.eps,
+                       self.weight_decay, zero_grad)
+
+    def _adam_own(self, src: torch.Tensor, dst: torch.Tensor, g: torch.Tensor) -> None:
+        """Adam on the own in-table rows from the current buffer into the idle one: one
+        out-of-place HIP pass (dw_adam_dense_to, grid capped to the overlapped phase) or copy +
+        the injected update."""
+        if self.adam_impl is hip_adam:
+            blocks = overlap_adam_blocks(self.S * self.d * 4 * 7, self._overlap_bytes)
+            adam_to_scalars(src, dst, g, self.m_in, self.v_in,
+                            adam_scalars(self.step_count, self.lr, self.betas, self.eps,
+                                         self.weight_decay), False, blocks)
+            return
+        dst.copy_(src)
+        self._adam(dst.view(-1), g.reshape(-1), self.m_in.view(-1), self.v_in.view(-1), False)
+
+    def _exchange_in(self, async_op: bool):
+        """reduce-scatter g_in -> Adam on own rows of the idle buffer -> all-gather into it;
+        g_in ends zeroed. One rank: Adam over the whole in table into the idle buffer."""
+        src, dst = self.params_in[self._cur_in], self.params_in[self._next_in]
+        if self.world == 1:
+            dst.copy_(src)
+            self._adam(dst.view(-1), self.grads_in.view(-1), self.m_in.view(-1),
+                       self.v_in.view(-1), True)
+            return None
+        a, b = self.shard_range()
+        if self.emulated:   # this rank's share of the work, without the collectives
+            self._adam_own(src[a:b], dst[a:b], self.grads_in[a:b])
+            self.grads_in.zero_()
+            return None
+        w = dist.reduce_scatter_tensor(self.grad_shard.view(-1), self.grads_in.view(-1),
+                                       op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+        if async_op:
+            w.wait()
+        self.grads_in.zero_()
+        own = dst[a:b]
+        self._adam_own(src[a:b], own, self.grad_shard)
+        nccl = dist.get_backend(self.group) == 'nccl'
+        send = own.view(-1) if nccl else own.reshape(-1).clone()
+        return dist.all_gather_into_tensor(dst.view(-1), send, group=self.group,
+                                           async_op=async_op)
+
+    def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
+        """Call right after pass 1 is enqueued (this rank's g_in final): the in-table update
+        runs on a side stream into the idle buffer while the output-table phase reads the
+        current one. Also starts the step (the Adam step count). ``overlap_bytes``: HBM bytes of
+        that phase, to cap the own-rows Adam's grid (overlap_adam_blocks); None = full grid."""
+        self.step_count += 1
+        self._overlap_bytes = overlap_bytes
+        self._next_in = 1 - self._cur_in
+        if not self._cuda:
+            self._exchange_in(False)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ev)
+            w = self._exchange_in(True)
+            done = torch.cuda.Event()
+            done.record(self._side)
+            self._ag.append(w if w is not None else done)
+            if w is not None:
+                self._ag.append(done)
+
+    def can_fuse_out_adam(self) -> bool:
+        return self._cuda and self.adam_impl is hip_adam
+
+    def out_adam_spec(self) -> Optional[dict]:
+        """The slice's Adam for sgns_owner_pass2 (after exchange_in: this step's scalars); None
+        where it cannot be fused (then call out_step after the gradient is in g_out)."""
+        if not self.can_fuse_out_adam():
+            return None
+        if self.step_count < 1:
+            raise RuntimeError('out_adam_spec() before exchange_in(): no step to fuse')
+        return {'m': self.m_out, 'v': self.v_out, 'flags': self._flags,
+                'scalars': adam_scalars(self.step_count, self.lr, self.betas, self.eps,
+                                        self.weight_decay)}
+
+    def out_step(self) -> None:
+        """Unfused: Adam on the local slice from g_out (zeroed)."""
+        self._adam(self.w_out.view(-1), self.g_out.view(-1), self.m_out.view(-1),
+                   self.v_out.view(-1), True)
+
+    def sync(self) -> None:
+        """The current stream waits for the in-table update; the new in table becomes current.
+        Call before the next pass 1 (and before reading w_in)."""
+        for w in self._ag:
+            if isinstance(w, torch.cuda.Event):
+                torch.cuda.current_stream(self.device).wait_event(w)
+            else:
+                w.wait()
+        self._ag = []
+        self._cur_in = self._next_in
+
+
+def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
+               neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
+               loss_acc: torch.Tensor, status: torch.Tensor,
+               overlap_bytes: Optional[float] = None) -> int:
+    """One owner-computes training step over the global batch ``walks`` (every rank passes the
+    same walks): pass 1 (owned slots) -> in-table exchange on the side stream -> pass 2 with the
+    slice's Adam fused -> sync. Returns this rank's record count."""
+    from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
+    sgns_owner_pass1(tables.w_in, tables.w_out, tables.grads_in, neg_samples, walks=walks,
+                     context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
+                     vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+    tables.exchange_in(overlap_bytes)
+    spec = tables.out_adam_spec()
+    n = sgns_owner_pass2(tables.w_in, tables.w_out, tables.g_out, neg_samples, walks=walks,
+                         context_radius=context_radius, out_adam=spec, status=status)
+    if spec is None:
+        tables.out_step()
+    tables.sync()
+    return n

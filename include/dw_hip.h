@@ -47,6 +47,7 @@ extern "C" {
 #define DW_S_REJECTION_CAP   4   /* node2vec rejection exceeded DW_MAX_REJECTION_ROUNDS              */
 #define DW_S_BAD_CSR         8   /* row_ptr not monotone / col out of range                          */
 #define DW_S_BAD_INDEX      16   /* an index outside [0, V) reached the SGNS kernel                  */
+#define DW_S_RECORDS_FULL   32   /* owner-form SGNS records exceeded the workspace (not expected)    */
 
 #define DW_METHOD_DEEPWALK   0   /* random_walk_generator.py:56-72 ('deepwalk' and 'dfs')          */
 #define DW_METHOD_NODE2VEC   1   /* random_walk_generator.py:75-119                                  */
@@ -207,6 +208,43 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                               float bias_correction2_sqrt, float neg_step_size, float eps,
                               float weight_decay, int32_t *status, void *workspace,
                               size_t workspace_bytes, void *stream);
+
+/* Owner-computes form of the walks SGNS step for N > 1 (ShardedTables(mode='owner'), bench.py).
+ * The output ("context") table is sharded by row owner: rank `owner` of `n_owners` holds only
+ * rows o with o % n_owners == owner, as local row o / n_owners of w_out_local
+ * (float32[local_rows, d], local_rows * n_owners >= vocab_size). Every rank passes the WHOLE
+ * global batch of walks (walks are keyed by global id, so each rank forms them itself) and the
+ * full, replicated in table; it computes only the output slots it owns, so no output-table
+ * gradient or parameter ever crosses ranks. Replaces the reference's single-device step
+ * (trainer.py:131-152 + the dense Adam of config_parser/core.py:43-53) at N > 1; summed over the
+ * owners, the work is exactly dw_sgns_walks_phase's.
+ * pass 1: g_in += the centre-table gradient of the owned slots (a PARTIAL sum: the caller
+ *         reduces it across ranks), loss_acc += their loss terms, records kept in the
+ *         workspace (>= dw_sgns_owner_workspace_bytes(n_walks*(L-2R), 2R, K, local_rows)),
+ *         packed in a fixed order (deterministic).
+ *         Needs dim a multiple of 64 (<= 512) and 2R(1+K) <= 64 (else DW_E_UNSUPPORTED).
+ * pass 2: sorts the records by local row and accumulates the slice's gradient: with m_out
+ *         non-NULL, the slice's torch.optim.Adam step is fused in exactly as in
+ *         dw_sgns_walks_phase2_adam (g_out_local zero on entry and left zero, row_flags
+ *         local_rows bytes); with m_out NULL, g_out_local += the gradient. It reads the record
+ *         count back to the host (ONE synchronisation of `stream`); *n_records (optional)
+ *         receives it. Same walk sizes and workspace as the pass-1 call. */
+int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
+                                  int64_t local_rows, size_t *bytes);
+int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                        int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                        int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                        const float *w_in, const float *w_out_local, float *g_in,
+                        const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                        float grad_scale, double *loss_acc, int32_t *status, void *workspace,
+                        size_t workspace_bytes, void *stream);
+int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_radius,
+                        int32_t neg_samples, int64_t local_rows, int32_t dim, const float *w_in,
+                        float *w_out_local, float *g_out_local, float *m_out, float *v_out,
+                        uint8_t *row_flags, float one_minus_beta1, float beta2,
+                        float one_minus_beta2, float bias_correction2_sqrt, float neg_step_size,
+                        float eps, float weight_decay, int32_t *status, void *workspace,
+                        size_t workspace_bytes, int64_t *n_records, void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */

@@ -1,0 +1,259 @@
+"""Owner-computes SGNS (N > 1 layout) on the GPU: dw_sgns_owner_pass1 / dw_sgns_owner_pass2.
+
+Rank r of W holds the out-table rows o with o % W == r and computes only those output slots of
+the whole global batch. Checked here on one device by running every owner in turn:
+  * each owner's gradients equal the oracle's owner split (sgns_grads_closed_form(owner=r));
+  * the owners' parts add up to the single-device step (dw_sgns_walks_phase): the partial
+    g_in's sum to g_in, the local g_out slices are g_out's rows r, r+W, ...; loss sums add up;
+    the record counts add up to every slot;
+  * the slice's fused Adam equals pass 2 followed by dw_adam_dense on the slice;
+  * an empty batch still gives every slice row its g = 0 Adam step; bad ids are reported;
+  * two ranks (gloo, both on cuda:0) training with OwnerTables + owner_step equal one process
+    training the whole batch (ShardedTables).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import sgns_ref
+from shallow_encoders import _native
+from shallow_encoders.word2vec.sgns import (loss_terms, sgns_accumulate, sgns_owner_pass1,
+                                           sgns_owner_pass2)
+from test_gpu_sgns import assert_no_row_drift, assert_params_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _owner_parts(w_in, w_out, walks, R, K, W, noise=None, seed=9, noise_offset=0, scale=None):
+    """Every owner's (partial g_in, local g_out, loss_acc, n_records) for the same batch."""
+    V, d = w_out.shape
+    S = -(-V // W)
+    parts = []
+    for r in range(W):
+        rows = torch.arange(S, device=w_out.device) * W + r
+        w_loc = torch.zeros((S, d), dtype=torch.float32, device=w_out.device)
+        keep = rows < V
+        w_loc[keep] = w_out[rows[keep]]
+        g_in = torch.zeros_like(w_in)
+        g_loc = torch.zeros_like(w_loc)
+        acc = sgns_owner_pass1(w_in, w_loc, g_in, K, walks=walks, context_radius=R, owner=r,
+                               n_owners=W, vocab_size=V, noise=noise, seed=seed,
+                               noise_offset=noise_offset, grad_scale=scale)
+        n = sgns_owner_pass2(w_in, w_loc, g_loc, K, walks=walks, context_radius=R)
+        parts.append((g_in, g_loc, acc, n, rows, keep))
+    return parts
+
+
+@pytest.mark.parametrize('d,W', [(128, 1), (128, 2), (128, 3), (64, 8), (256, 5)])
+def test_owner_parts_vs_oracle_and_full_step(hip_device, d, W):
+    rng = np.random.default_rng(d + W)
+    V, R, K, L, n = 3001, 3, 4, 24, 40
+    w_in0, w_out0 = sgns_ref.xavier_tables(V, d, seed=d)
+    walks = rng.integers(0, V, size=(n, L)).astype(np.int32)
+    walks[:, ::4] = 11                      # a hub row straddling many gather chunks
+    ins, tgt = sgns_ref.sg_windows(walks, R)
+    noise = rng.integers(0, V, size=(len(ins), 2 * R, K))
+    w_in = torch.as_tensor(w_in0).cuda()
+    w_out = torch.as_tensor(w_out0).cuda()
+    wk = torch.as_tensor(walks).cuda()
+    nz = torch.as_tensor(noise).cuda()
+    parts = _owner_parts(w_in, w_out, wk, R, K, W, noise=nz)
+    # the single-device step over the same batch
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=wk, context_radius=R, noise=nz)
+    full_loss, gi_full, go_full = sgns_ref.sgns_grads_closed_form(w_in0, w_out0, ins, tgt, noise)
+    scale = float(np.abs(gi_full).max())
+    T = 2 * R * (1 + K)
+    assert sum(p[3] for p in parts) == len(ins) * T        # every slot owned exactly once
+    sum_gin = torch.zeros_like(w_in)
+    sum_acc = torch.zeros(4, dtype=torch.float64, device='cuda')
+    for r, (gi_r, go_r, acc_r, n_r, rows, keep) in enumerate(parts):
+        loss_r, gi_o, go_o = sgns_ref.sgns_grads_closed_form(w_in0, w_out0, ins, tgt, noise,
+                                                             owner=r, n_owners=W)
+        np.testing.assert_allclose(gi_r.cpu().numpy(), gi_o, rtol=1e-4, atol=1e-6 * scale)
+        rk = rows[keep].cpu().numpy()
+        np.testing.assert_allclose(go_r[keep].cpu().numpy(), go_o[rk], rtol=1e-4,
+                                   atol=1e-6 * scale)
+        if (~keep).any():
+            assert float(go_r[~keep].abs().max()) == 0.0         # padding rows untouched
+        torch.testing.assert_close(go_r[keep], g_out[rows[keep]], rtol=1e-4,
+                                   atol=1e-6 * scale)
+        assert float(loss_terms(acc_r, tgt.size, K)['loss']) == pytest.approx(loss_r, rel=1e-4,
+                                                                              abs=1e-6)
+        sum_gin += gi_r
+        sum_acc += acc_r
+    torch.testing.assert_close(sum_gin, g_in, rtol=1e-4, atol=1e-6 * scale)
+    torch.testing.assert_close(sum_acc, acc, rtol=1e-5, atol=1e-6)
+    assert float(loss_terms(sum_acc, tgt.size, K)['loss']) == pytest.approx(full_loss, rel=1e-5)
+
+
+def test_owner_device_noise_equals_replayed(hip_device):
+    """noise=None draws the same Philox negatives as dw_sgns_walks_phase (keyed by the global
+    centre), so the owners' parts of a device-noise step add up to that step."""
+    rng = np.random.default_rng(3)
+    V, d, R, K, L, n, W = 5000, 128, 5, 5, 30, 32, 4
+    w_in0, w_out0 = sgns_ref.xavier_tables(V, d, seed=1)
+    w_in, w_out = torch.as_tensor(w_in0).cuda(), torch.as_tensor(w_out0).cuda()
+    wk = torch.as_tensor(rng.integers(1, V, size=(n, L)).astype(np.int32)).cuda()
+    parts = _owner_parts(w_in, w_out, wk, R, K, W, seed=77, noise_offset=12345)
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    acc = sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=wk, context_radius=R, seed=77,
+                          noise_offset=12345)
+    scale = float(g_in.abs().max())
+    torch.testing.assert_close(sum(p[0] for p in parts), g_in, rtol=1e-4, atol=1e-6 * scale)
+    torch.testing.assert_close(sum(p[2] for p in parts), acc, rtol=1e-5, atol=1e-6)
+    for g_in_r, g_loc, _, _, rows, keep in parts:
+        torch.testing.assert_close(g_loc[keep], g_out[rows[keep]], rtol=1e-4, atol=1e-6 * scale)
+
+
+@pytest.mark.parametrize('d', [64, 128])
+def test_owner_fused_slice_adam_equals_unfused(hip_device, d):
+    from shallow_encoders.word2vec.sharding import adam_scalars, hip_adam
+    rng = np.random.default_rng(d)
+    V, R, K, L, n, W, lr = 4000, 2, 3, 16, 64, 3, 0.02
+    S = -(-V // W)
+    w_in = torch.as_tensor(sgns_ref.xavier_tables(V, d, seed=2)[0]).cuda()
+    base = torch.randn((S, d), generator=torch.Generator().manual_seed(1)).cuda() * 0.1
+    fused = [base.clone(), torch.zeros_like(base), torch.zeros_like(base), torch.zeros_like(base)]
+    plain = [base.clone(), torch.zeros_like(base), torch.zeros_like(base), torch.zeros_like(base)]
+    flags = torch.zeros(S, dtype=torch.uint8, device='cuda')
+    for step in range(1, 4):
+        wk = torch.as_tensor(rng.integers(0, V, size=(n, L)).astype(np.int32)).cuda()
+        for tabs, fuse in ((fused, True), (plain, False)):
+            w, g, m, v = tabs
+            g_in = torch.zeros_like(w_in)
+            sgns_owner_pass1(w_in, w, g_in, K, walks=wk, context_radius=R, owner=1, n_owners=W,
+                             vocab_size=V, seed=step, noise_offset=0)
+            spec = ({'m': m, 'v': v, 'flags': flags,
+                     'scalars': adam_scalars(step, lr, (0.9, 0.999), 1e-8, 0.0)}
+                    if fuse else None)
+            sgns_owner_pass2(w_in, w, g, K, walks=wk, context_radius=R, out_adam=spec)
+            if not fuse:
+                hip_adam(w.view(-1), g.view(-1), m.view(-1), v.view(-1), step, lr,
+                         (0.9, 0.999), 1e-8, 0.0, True)
+    torch.cuda.synchronize()
+    assert float(fused[1].abs().max()) == 0.0 and int(flags.max()) == 0
+    assert_params_close(fused[0].cpu().numpy(), plain[0].cpu().numpy(), lr, max_frac=5e-3,
+                        max_abs=2.05 * lr * 3)
+    assert_no_row_drift(fused[0].cpu().numpy(), plain[0].cpu().numpy())
+    np.testing.assert_allclose(fused[2].cpu().numpy(), plain[2].cpu().numpy(), rtol=1e-3,
+                               atol=1e-6)
+
+
+def test_owner_empty_batch_and_bad_index(hip_device):
+    from shallow_encoders.word2vec.sharding import adam_scalars, hip_adam
+    V, d, R, K, W = 1000, 64, 2, 2, 2
+    S = V // W
+    w_in = torch.randn((V, d), device='cuda')
+    w = torch.randn((S, d), device='cuda')
+    w2 = w.clone()
+    m, v = torch.zeros_like(w), torch.zeros_like(w)
+    m2, v2 = torch.zeros_like(w), torch.zeros_like(w)
+    g = torch.zeros_like(w)
+    flags = torch.zeros(S, dtype=torch.uint8, device='cuda')
+    empty = torch.zeros((0, 10), dtype=torch.int32, device='cuda')
+    g_in = torch.zeros_like(w_in)
+    sgns_owner_pass1(w_in, w, g_in, K, walks=empty, context_radius=R, owner=0, n_owners=W,
+                     vocab_size=V)
+    n = sgns_owner_pass2(w_in, w, g, K, walks=empty, context_radius=R,
+                         out_adam={'m': m, 'v': v, 'flags': flags,
+                                   'scalars': adam_scalars(1, 0.1, (0.9, 0.999), 1e-8, 0.0)})
+    assert n == 0
+    hip_adam(w2.view(-1), torch.zeros_like(w2).view(-1), m2.view(-1), v2.view(-1), 1, 0.1,
+             (0.9, 0.999), 1e-8, 0.0, True)
+    torch.testing.assert_close(w, w2, rtol=0, atol=0)
+    # an id outside [0, V) is reported through the status word, not a fault
+    bad = torch.randint(0, V, (4, 10), dtype=torch.int32, device='cuda')
+    bad[2, 5] = V + 3
+    status = torch.zeros(1, dtype=torch.int32, device='cuda')
+    sgns_owner_pass1(w_in, w, g_in, K, walks=bad, context_radius=R, owner=0, n_owners=W,
+                     vocab_size=V, status=status)
+    sgns_owner_pass2(w_in, w, torch.zeros_like(w), K, walks=bad, context_radius=R, status=status)
+    with pytest.raises(IndexError):
+        _native.check_status(status, 'owner sgns')
+    # widths the 16-lane kernel does not cover are refused, not mis-computed
+    with pytest.raises(Exception):
+        sgns_owner_pass1(torch.zeros((V, 96), device='cuda'), torch.zeros((S, 96), device='cuda'),
+                         torch.zeros((V, 96), device='cuda'), K, walks=bad[:1] % V,
+                         context_radius=R, owner=0, n_owners=W, vocab_size=V)
+
+
+# ---- two ranks on one GPU (gloo carries the collectives; RCCL refuses two ranks per device) ----
+V2, D2, R2, K2, L2, NW2, STEPS2, LR2 = 700, 64, 2, 3, 12, 48, 3, 1e-3
+
+
+def _walks_all():
+    g = torch.Generator().manual_seed(8)
+    return torch.randint(1, V2, (STEPS2, NW2, L2), generator=g, dtype=torch.int32)
+
+
+def _owner_run(rank, world, port, q):
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from shallow_encoders.word2vec.sharding import OwnerTables, owner_step
+        t = OwnerTables(V2, D2, 'cuda:0', lr=LR2, init_seed=4)
+        walks = _walks_all()
+        per = L2 - 2 * R2
+        acc = torch.zeros(4, dtype=torch.float64, device='cuda:0')
+        status = torch.zeros(1, dtype=torch.int32, device='cuda:0')
+        for s in range(STEPS2):
+            owner_step(t, walks[s].cuda(), R2, K2, seed=11, noise_offset=s * NW2 * per,
+                       grad_scale=1.0 / (NW2 * per * 2 * R2), loss_acc=acc, status=status)
+        torch.cuda.synchronize()
+        _native.check_status(status, 'owner_step')
+        q.put((rank, t.w_in.cpu().numpy().copy(), t.full_w_out().cpu().numpy(),
+               acc.cpu().numpy(), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report, the parent asserts
+        q.put((rank, None, None, None, repr(e)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.timeout(600)
+def test_owner_tables_two_ranks_equal_single_process(hip_device):
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    ref = ShardedTables(V2, D2, hip_device, lr=LR2, init_seed=4)
+    walks = _walks_all()
+    per = L2 - 2 * R2
+    acc_ref = torch.zeros(4, dtype=torch.float64, device=hip_device)
+    for s in range(STEPS2):
+        sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K2, walks=walks[s].cuda(),
+                        context_radius=R2, seed=11, noise_offset=s * NW2 * per,
+                        loss_acc=acc_ref)
+        ref.step()
+    torch.cuda.synchronize()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_run, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs
+    (_, i0, o0, a0, _), (_, i1, o1, a1, _) = res
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_allclose(a0 + a1, acc_ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    for got, exp in ((i0, ref.w_in.cpu().numpy()), (o0, ref.w_out.cpu().numpy())):
+        bad = ~np.isclose(got, exp, rtol=1e-4, atol=1e-6)
+        assert bad.mean() < 1e-3, bad.mean()
+        assert_no_row_drift(got, exp, rtol=1e-4)
+        assert np.abs(got - exp).max() <= 2.05 * LR2 * STEPS2

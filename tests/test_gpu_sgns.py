@@ -42,6 +42,16 @@ def assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3, max_a
     assert np.abs(got - exp).max() <= lim, (np.abs(got - exp).max(), lim)
 
 
+def assert_no_row_drift(got, exp, rtol=1e-5, atol=1e-6, max_row_frac=0.25):
+    """Adam amplifies accumulation-order noise only in isolated entries (gradients ~0); an extra
+    or missing update of a row moves (nearly) all of its entries. No row may have more than
+    ``max_row_frac`` of its entries outside (rtol, atol)."""
+    bad = ~np.isclose(got, exp, rtol=rtol, atol=atol)
+    frac = bad.mean(axis=1)
+    rows = np.nonzero(frac > max_row_frac)[0]
+    assert rows.size == 0, f'rows drifted as a whole: {rows[:10].tolist()} ({frac[rows[:10]]})'
+
+
 def reference_envelope(w_in0, w_out0, lr, batches, rtol=1e-5, atol=1e-6):
     """How far the REFERENCE's own trajectory moves when its gradients are summed exactly
     (float64 closed form, rounded to float32) instead of in torch's order: the fp32
@@ -479,8 +489,8 @@ def test_device_noise_fill_matches_in_kernel_draws(hip_device):
                                   ref.reshape(B, C, K))
 
 
-@pytest.mark.parametrize('d', [64, 100, 128])
-def test_fused_out_table_adam_equals_unfused(hip_device, d):
+@pytest.mark.parametrize('d,nw', [(64, 256), (100, 256), (128, 256), (128, 255)])
+def test_fused_out_table_adam_equals_unfused(hip_device, d, nw):
     """dw_sgns_walks_phase2_adam (the output table's Adam fused into the records gather) gives
     the tables that phase 2 + dw_adam_dense give, over several steps; g_out and the row flags
     are left zeroed. Float atomics (g_in, chunk-boundary rows) make two runs of either path
@@ -491,7 +501,7 @@ def test_fused_out_table_adam_equals_unfused(hip_device, d):
     from shallow_encoders.word2vec.sharding import ShardedTables
     csr = rmat_graph(12, 40_000, 0, device=hip_device)
     walker = DeepWalk(csr, 40, rng='philox', seed=3, device=hip_device)
-    V, R, K, nw = csr.vocab_size, 3, 4, 256
+    V, R, K = csr.vocab_size, 3, 4   # nw = 255: records % 8 != 0 (a partial last group)
     fused = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5)
     plain = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5)
     for step in range(3):
@@ -513,5 +523,6 @@ def test_fused_out_table_adam_equals_unfused(hip_device, d):
     for a, b in ((fused.w_in, plain.w_in), (fused.w_out, plain.w_out)):
         assert_params_close(a.cpu().numpy(), b.cpu().numpy(), 0.02, max_frac=5e-3,
                             max_abs=2.05 * 0.02 * 3)
+        assert_no_row_drift(a.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_allclose(fused.m.cpu().numpy(), plain.m.cpu().numpy(), rtol=1e-3,
                                atol=1e-6)
