@@ -144,6 +144,8 @@ struct SgnsArgs {
     int32_t owner, n_owners;
     uint32_t *rec_counts;
     int64_t region;
+    const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
+    int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
 };
 
 __device__ __forceinline__ int64_t noise_id(const SgnsArgs &a, int64_t b, int j, int k) {
@@ -354,9 +356,13 @@ __device__ __forceinline__ float row_sum16(float x) {
 // (o % n_owners == owner), compacted to the front of its id list in slot order (s_t keeps each
 // one's slot t for the positive / negative rule), so the chunk loop gathers ~T / n_owners rows
 // from the rank's local slice of the out table. Each wave appends its records to a region of
-// its own (sized for every slot of its grid-stride iterations), counted in a register: no
-// atomics (a shared counter took one same-address atomic per wave iteration — ~12 ns each,
-// serialised: 14 ms per pass at 8 owners); k_rec_compact packs the regions afterwards.
+// its own (sized for every slot of its iterations), counted in a register: no atomics (a
+// shared counter took one same-address atomic per wave iteration — ~12 ns each, serialised:
+// 14 ms per pass at 8 owners); k_rec_compact packs the regions afterwards.
+// Every rank forms every centre of the global batch, so at W owners the centre-gradient atomics
+// grow W-fold (2.35 GB per pass at W = 8, C3). The owner form therefore takes the centres in
+// node order (a sorted occurrence list, contiguous per wave): consecutive occurrences of one
+// node are summed in registers (pend) and leave as ONE atomic row per run.
 template <int F4, bool FROM_WALKS, int CHR, bool OWNER>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
@@ -373,11 +379,22 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
     const int64_t n_slots = (int64_t)gridDim.x * WAVES_PER_BLOCK * 4;
     float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
     int64_t filled = 0;  // OWNER: records in this wave's region so far (wave-uniform)
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+    int64_t o_end = a.batch, step = n_slots, base0 = gw * 4;
+    if constexpr (OWNER) {  // this wave's slice of the node-ordered occurrences
+        base0 = gw * a.occ_per_wave;
+        o_end = base0 + a.occ_per_wave < a.batch ? base0 + a.occ_per_wave : a.batch;
+        step = 4;
+    }
+    int32_t pend_c = -1;  // OWNER: node whose centre gradient is being summed (wave-uniform)
+    float pend[F4];
+#pragma unroll
+    for (int f = 0; f < F4; ++f) pend[f] = 0.f;
 
-    for (int64_t base = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * 4; base < a.batch;
-         base += n_slots) {
-        const int64_t b = base + q;
-        const bool active = b < a.batch;
+    for (int64_t base = base0; base < o_end; base += step) {
+        const int64_t jb = base + q;
+        const bool active = jb < o_end;
+        const int64_t b = OWNER ? (active ? static_cast<int64_t>(a.occ[jb]) : 0) : jb;
         const int32_t *walk = nullptr;
         int64_t i = 0, cid = -1;
         if (active) {
@@ -541,6 +558,24 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         for (int qq = 0; qq < 4; ++qq) {
             const int32_t cq = __builtin_amdgcn_readlane(
                 ok_c && n_own > 0 ? static_cast<int32_t>(cid) : -1, qq * 16);
+            if constexpr (OWNER) {  // sum runs of one node, one atomic row per run
+                if (cq < 0) continue;
+                if (cq != pend_c) {
+                    if (pend_c >= 0) {
+                        float *dst = a.g_in + static_cast<int64_t>(pend_c) * D + lane;
+#pragma unroll
+                        for (int f = 0; f < F4; ++f) atomicAdd(dst + 64 * f, pend[f]);
+                    }
+                    pend_c = cq;
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) pend[f] = 0.f;
+                }
+                // element 64f + lane sits in float4 slot (lane >> 2) + 16f, component lane & 3
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+                    pend[f] += sg_flat[qq * 16 * F4 * 4 + ((lane >> 2) + 16 * f) * 4 + (lane & 3)];
+                continue;
+            }
             if (cq >= 0) {
                 float *dst = a.g_in + static_cast<int64_t>(cq) * D;
                 // s_g[qq] holds float4 slot j = gl + 16f -> elements 4gl + 64f .. +3
@@ -555,8 +590,12 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         dw::wave_lds_sync();
     }
     if constexpr (OWNER) {
-        if (lane == 0) a.rec_counts[(int64_t)blockIdx.x * WAVES_PER_BLOCK + wv] =
-            static_cast<uint32_t>(filled);
+        if (pend_c >= 0) {
+            float *dst = a.g_in + static_cast<int64_t>(pend_c) * D + lane;
+#pragma unroll
+            for (int f = 0; f < F4; ++f) atomicAdd(dst + 64 * f, pend[f]);
+        }
+        if (lane == 0) a.rec_counts[gw] = static_cast<uint32_t>(filled);
     }
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
@@ -1149,9 +1188,49 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// occurrence b (centre position of the walks) keyed by its node, for the node-order sort
+__global__ void __launch_bounds__(256)
+    k_occ_keys(const int32_t *__restrict__ walks, int64_t n_centres, int32_t L, int32_t R,
+               uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const int64_t per = L - 2 * R;
+    for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < n_centres;
+         b += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w = b / per;
+        keys[b] = static_cast<uint32_t>(walks[w * L + R + (b - w * per)]);
+        vals[b] = static_cast<uint32_t>(b);
+    }
+}
+
+// the owner form's tail of the workspace (after the records part): the occurrence sort
+struct OccSpace {
+    uint32_t *k0, *k1, *v0, *v1;
+    void *tmp;
+    size_t tmp_bytes, total;
+};
+
+int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t st) {
+    size_t tmp = 0;
+    rocprim::double_buffer<uint32_t> kb(nullptr, nullptr), vb(nullptr, nullptr);
+    if (rocprim::radix_sort_pairs(nullptr, tmp, kb, vb, static_cast<uint32_t>(n_centres), 0,
+                                  end_bit_for(V), st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner: occurrence sort size query failed");
+        return DW_E_HIP;
+    }
+    const size_t a = align256((size_t)n_centres * 4);
+    char *p = static_cast<char *>(base);
+    o->k0 = reinterpret_cast<uint32_t *>(p);
+    o->k1 = reinterpret_cast<uint32_t *>(p + a);
+    o->v0 = reinterpret_cast<uint32_t *>(p + 2 * a);
+    o->v1 = reinterpret_cast<uint32_t *>(p + 3 * a);
+    o->tmp = p + 4 * a;
+    o->tmp_bytes = tmp;
+    o->total = 4 * a + align256(tmp);
+    return DW_OK;
+}
+
 int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *workspace,
                     size_t workspace_bytes, Workspace *ws, OwnerLayout *lay, hipStream_t st,
-                    const char *what) {
+                    const char *what, int64_t V = 0, OccSpace *occ = nullptr) {
     *lay = owner_layout(n_centres, T);
     DW_REQUIRE(lay->total < 0x7FFFFFFF, "%s: too many records (%lld)", what,
                (long long)lay->total);
@@ -1160,8 +1239,15 @@ int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *work
     DW_REQUIRE(workspace != nullptr, "%s: needs the records workspace", what);
     int rc = plan_workspace(lay->total, local_rows, workspace, ws, st);
     if (rc != DW_OK) return rc;
-    DW_REQUIRE(workspace_bytes >= ws->total, "%s: workspace too small (%zu < %zu)", what,
-               workspace_bytes, ws->total);
+    size_t need = ws->total;
+    if (occ) {
+        rc = plan_occ(n_centres > 0 ? n_centres : 1, V, static_cast<char *>(workspace) + ws->total,
+                      occ, st);
+        if (rc != DW_OK) return rc;
+        need += occ->total;
+    }
+    DW_REQUIRE(workspace_bytes >= need, "%s: workspace too small (%zu < %zu)", what,
+               workspace_bytes, need);
     return DW_OK;
 }
 
@@ -1178,15 +1264,31 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, void *workspace, size_t w
                G16_TMAX);
     Workspace ws;
     OwnerLayout lay;
+    OccSpace occ;
     int rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
-                             "dw_sgns_owner_pass1");
+                             "dw_sgns_owner_pass1", a.V, &occ);
     if (rc != DW_OK) return rc;
     g_timer.mark(0, st);
     a.rec_key = ws.k0;
     a.rec_val = ws.v0;
     a.rec_counts = ws.wave_counts;
     a.region = lay.region;
+    a.occ_per_wave = lay.region / T;
     if (a.batch > 0) {
+        // the centres in node order (stable: walk order within a node)
+        int64_t ob = (a.batch + 255) / 256;
+        if (ob > grid_cap(8)) ob = grid_cap(8);
+        hipLaunchKernelGGL(k_occ_keys, dim3((unsigned)ob), dim3(256), 0, st, a.walks, a.batch,
+                           a.L, a.R, occ.k0, occ.v0);
+        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/occ_keys");
+        rocprim::double_buffer<uint32_t> kb(occ.k0, occ.k1), vb(occ.v0, occ.v1);
+        size_t tb = occ.tmp_bytes;
+        if (rocprim::radix_sort_pairs(occ.tmp, tb, kb, vb, static_cast<uint32_t>(a.batch), 0,
+                                      end_bit_for(a.V), st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner_pass1: occurrence sort failed");
+            return DW_E_HIP;
+        }
+        a.occ = vb.current();
         rc = launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
         hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts, lay.n_waves,
@@ -1530,17 +1632,21 @@ int dw_sgns_walks_phase(int32_t phase, const int32_t *walks, int64_t n_walks,
 }
 
 int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
-                                  int64_t local_rows, size_t *bytes) {
+                                  int64_t vocab_size, int64_t local_rows, size_t *bytes) {
     DW_REQUIRE(bytes, "dw_sgns_owner_workspace_bytes: bytes is null");
-    DW_REQUIRE(n_centres >= 0 && n_ctx >= 1 && neg_samples >= 0 && local_rows >= 1,
+    DW_REQUIRE(n_centres >= 0 && n_ctx >= 1 && neg_samples >= 0 && local_rows >= 1 &&
+                   vocab_size >= 1,
                "dw_sgns_owner_workspace_bytes: bad sizes");
     const OwnerLayout lay = owner_layout(n_centres, (int64_t)n_ctx * (1 + neg_samples));
     DW_REQUIRE(lay.total < 0x7FFFFFFF, "dw_sgns_owner_workspace_bytes: too many records");
     Workspace ws;
+    OccSpace occ;
     char dummy;
     int rc = plan_workspace(lay.total > 0 ? lay.total : 1, local_rows, &dummy, &ws, nullptr);
     if (rc != DW_OK) return rc;
-    *bytes = ws.total;
+    rc = plan_occ(n_centres > 0 ? n_centres : 1, vocab_size, &dummy, &occ, nullptr);
+    if (rc != DW_OK) return rc;
+    *bytes = ws.total + occ.total;
     return DW_OK;
 }
 

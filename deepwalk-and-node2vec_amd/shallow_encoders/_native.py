@@ -68,7 +68,7 @@ SIGNATURES = {
     'dw_sgns_walks_phase2_piece': (ctypes.c_int, [_i32, _i32, _i64, _p, _i64, _i32, _i32, _i32,
                                                    _i64, _i32, _p, _p, _p, _p, ctypes.c_size_t,
                                                    _p]),
-    'dw_sgns_owner_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),
+    'dw_sgns_owner_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _i64, _szp]),
     'dw_sgns_owner_pass1': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32,
                                            _i64, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p, _p,
                                            ctypes.c_size_t, _p]),

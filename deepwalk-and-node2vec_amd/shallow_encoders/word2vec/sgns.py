@@ -48,15 +48,18 @@ def _use_records(scatter: str, n_ctx: int, neg_samples: int, vocab_size: int) ->
 
 
 def workspace_for(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int,
-                  device: torch.device, owner: bool = False) -> torch.Tensor:
+                  device: torch.device, local_rows: Optional[int] = None) -> torch.Tensor:
     """Device workspace of the atomic-free (records) output-table path, cached per device and
-    grown on demand (allocated outside any timed region after the first call). ``owner``: sized
-    for dw_sgns_owner_pass1 (vocab_size = the local rows)."""
+    grown on demand (allocated outside any timed region after the first call). ``local_rows``:
+    sized for dw_sgns_owner_pass1 (records keyed by the rank's local out-table rows)."""
     import ctypes
     nbytes = ctypes.c_size_t(0)
-    _native.call('dw_sgns_owner_workspace_bytes' if owner else 'dw_sgns_workspace_bytes',
-                 int(n_centres), int(n_ctx), int(neg_samples), int(vocab_size),
-                 ctypes.byref(nbytes))
+    if local_rows is None:
+        _native.call('dw_sgns_workspace_bytes', int(n_centres), int(n_ctx), int(neg_samples),
+                     int(vocab_size), ctypes.byref(nbytes))
+    else:
+        _native.call('dw_sgns_owner_workspace_bytes', int(n_centres), int(n_ctx),
+                     int(neg_samples), int(vocab_size), int(local_rows), ctypes.byref(nbytes))
     ws = _WORKSPACES.get(device)
     if ws is None or ws.numel() < nbytes.value:
         _WORKSPACES.pop(device, None)
@@ -347,7 +350,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
         loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = workspace_for(n_centres, 2 * R, K, local_rows, dev, owner=True)
+    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows, _native.ptr(w_in),
@@ -377,7 +380,7 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
     R, K = int(context_radius), int(neg_samples)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = workspace_for(n * (L - 2 * R), 2 * R, K, local_rows, dev, owner=True)
+    ws = workspace_for(n * (L - 2 * R), 2 * R, K, w_in.shape[0], dev, local_rows=local_rows)
     n_rec = ctypes.c_int64(0)
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),

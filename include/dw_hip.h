@@ -220,7 +220,7 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
  * owners, the work is exactly dw_sgns_walks_phase's.
  * pass 1: g_in += the centre-table gradient of the owned slots (a PARTIAL sum: the caller
  *         reduces it across ranks), loss_acc += their loss terms, records kept in the
- *         workspace (>= dw_sgns_owner_workspace_bytes(n_walks*(L-2R), 2R, K, local_rows)),
+ *         workspace (>= dw_sgns_owner_workspace_bytes(n_walks*(L-2R), 2R, K, V, local_rows)),
  *         packed in a fixed order (deterministic).
  *         Needs dim a multiple of 64 (<= 512) and 2R(1+K) <= 64 (else DW_E_UNSUPPORTED).
  * pass 2: sorts the records by local row and accumulates the slice's gradient: with m_out
@@ -230,7 +230,7 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
  *         count back to the host (ONE synchronisation of `stream`); *n_records (optional)
  *         receives it. Same walk sizes and workspace as the pass-1 call. */
 int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
-                                  int64_t local_rows, size_t *bytes);
+                                  int64_t vocab_size, int64_t local_rows, size_t *bytes);
 int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                         int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                         int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
