@@ -132,10 +132,24 @@ def main():
                     help='one GPU, measurement only: run rank 0\'s share of an owner-mode job of '
                          'this many ranks (its walks, slots, Adam rows) without the collectives; '
                          'value is then a projection (comm assumed hidden)')
+    ap.add_argument('--owner-walks', default=None, choices=['all', 'gather'],
+                    help='owner mode: every rank generates the whole global batch of walks '
+                         '(all; default for DeepWalk, whose walker is cheap) or its own B walks '
+                         'and all-gathers them (gather; default for node2vec)')
+    ap.add_argument('--in-exchange', default=None, choices=['sharded', 'lazy'],
+                    help='owner mode, in table: sharded = dense reduce-scatter / own-rows Adam / '
+                         'all-gather (OwnerTables; default at C3); lazy = only the rows the '
+                         'batch touched are all-reduced and updated, the others\' g = 0 Adam '
+                         'steps replayed exactly when next touched (OwnerLazyTables; default at '
+                         'C5, where the dense exchange is 2 x 17 GB per step)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
             setattr(args, k, v)
+    if args.owner_walks is None:
+        args.owner_walks = 'gather' if args.method == 'node2vec' else 'all'
+    if args.in_exchange is None:
+        args.in_exchange = 'lazy' if args.config == 'c5' else 'sharded'
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -161,7 +175,8 @@ def main():
     from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
                                                sgns_phase2_pieces, sgns_phase_bytes)
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
-    from shallow_encoders.word2vec.sharding import OwnerTables, ShardedTables, overlap_adam_blocks
+    from shallow_encoders.word2vec.sharding import (OwnerLazyTables, OwnerTables, ShardedTables,
+                                                    overlap_adam_blocks)
     _native.require_device(dev)
 
     t0 = time.time()
@@ -183,8 +198,10 @@ def main():
         raise SystemExit('owner mode needs the sorted path, d a multiple of 64 (<= 512) and '
                          '2R(1+K) <= 64; use --dist-mode replicated')
     W_eff = emulate or world            # ranks of the (possibly emulated) job
+    lazy = owner and args.in_exchange == 'lazy'
     if owner:
-        tables = OwnerTables(V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
+        tables = (OwnerLazyTables if lazy else OwnerTables)(
+            V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
     else:
         tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
                                overlap_in=not args.no_overlap_in,
@@ -211,28 +228,51 @@ def main():
         s = step_idx[0]
         step_idx[0] += 1
         g0 = s * BG                                   # global walk id of the step's batch
-        ids = (torch.arange(g0, g0 + BG, device=dev, dtype=torch.int64) % walks_total)
+        # gather: this rank's B walks are global ids g0 + rank*B ... (the same global batch);
+        # emulated, all W*B walks are generated here (no collective to time: conservative)
+        gather = args.owner_walks == 'gather' and not emulate
+        a0 = g0 + tables.rank * B if gather else g0
+        nb = B if gather else BG
+        ids = (torch.arange(a0, a0 + nb, device=dev, dtype=torch.int64) % walks_total)
         torch.floor_divide(ids, args.walks_per_node, out=ids)
-        starts_buf.copy_(ids + 1)
+        starts_buf[:nb].copy_(ids + 1)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         if record:
             e[0].record()
-        walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
+        if gather:
+            own = walks_buf[tables.rank * B:(tables.rank + 1) * B]
+            walker.walk_batch(starts_buf[:B], walk_id0=a0, out=own, check=False)
+            send = own if backend == 'nccl' else own.clone()
+            dist.all_gather_into_tensor(walks_buf.view(-1), send.reshape(-1))
+        else:
+            walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
         if record:
             e[1].record()
-        sgns_owner_pass1(tables.w_in, tables.w_out, tables.grads_in, K, walks=walks_buf,
+        if lazy:
+            tables.begin_step()
+            tables.prepare(walks_buf, R, K)
+            tables.catch_up()
+        sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks_buf,
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
-                         grad_scale=grad_scale, loss_acc=loss_acc, status=status)
-        tables.exchange_in(overlap_bytes=owner_p2_bytes)
+                         grad_scale=grad_scale, loss_acc=loss_acc, status=status,
+                         order_ready=lazy)
+        if lazy:
+            tables.exchange_touched()
+        else:
+            tables.exchange_in()        # full grid: 1/W of the in table, between RS and AG
         spec = tables.out_adam_spec() if fuse else None
-        n_rec[0] = sgns_owner_pass2(tables.w_in, tables.w_out, tables.g_out, K, walks=walks_buf,
-                                    context_radius=R, out_adam=spec, status=status)
+        n_rec[0] = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, K,
+                                    walks=walks_buf, context_radius=R, out_adam=spec,
+                                    status=status)
         if spec is None:
             tables.out_step()
         if record:
             e[2].record()
-        tables.sync()
+        if lazy:
+            tables.update_touched()
+        else:
+            tables.sync()
         if record:
             e[3].record()
             ev['walk'].append((e[0], e[1]))
@@ -240,9 +280,6 @@ def main():
             ev['adam'].append((e[2], e[3]))
 
     n_rec = [0]
-    # the owner output-table phase (sort + gather + slice Adam), for the in-table Adam's grid:
-    # ~1/W of the one-GPU phase's records
-    owner_p2_bytes = (p2_bytes / W_eff + V * d * 24 / W_eff) if owner else None
 
     def one_step(record: bool):
         if owner:
@@ -338,6 +375,8 @@ def main():
         out_adam_bytes = V * d * 4 * 7 // W_eff
         in_adam_bytes = V * d * 4 * 7 // W_eff
         op_ms = sgns_ms + kern_ms['adam']
+        if lazy:   # + the centre order, touched-row catch-up and gather outside the pass events
+            op_ms = kern_ms['sgns'] + kern_ms['adam']
     sgns_gbs = (pairs_per_step * bpp + out_adam_bytes + in_adam_bytes) / (op_ms * 1e-3) / 1e9
     phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     if owner:
@@ -397,13 +436,18 @@ def main():
                          f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * W_eff, 'positive_pairs_per_step_per_gpu': pairs_per_step,
             'parallelism': (
-                f'EMULATED rank 0 of {W_eff} on one GPU (owner-computes; no collectives run, '
-                f'value is a projection assuming the in-table exchange stays hidden)' if emulate
+                f'EMULATED rank 0 of {W_eff} on one GPU (owner-computes, in table '
+                f'{args.in_exchange}; no collectives run, '
+                f'value is a projection assuming the in-table exchange stays hidden; walks: '
+                f'{args.owner_walks})' if emulate
                 else f'REHEARSAL dp{world} over {backend}, all ranks on one device'
                 if backend != 'nccl' and world > 1 else
                 f'dp{world} owner-computes (out table sharded by row owner o % {world}, no '
-                f'out-table collective; in table replicated, RCCL reduce-scatter / all-gather '
-                f'overlapped with the output-table phase)' if owner else
+                f'out-table collective; in table replicated: '
+                + ('touched rows all-reduced over RCCL, lazy exact Adam' if lazy else
+                   'RCCL reduce-scatter / all-gather')
+                + f' overlapped with the output-table phase; walks: {args.owner_walks})' if owner
+                else
                 f'dp{world} (node-id-range sharded Adam, RCCL reduce-scatter/all-gather, '
                 f'in-table exchange overlapped'
                 + (f', out table in {tables.P} pieces pipelined' if pieces else '') + ')'),

@@ -82,6 +82,84 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ---- lazy exact Adam over selected rows (the touched-row in-table exchange, N > 1) ------------
+// A row that no centre of a batch touched has g = 0 for that step, and torch's update with
+// g = 0 is a fixed recurrence in (p, m, v) driven by the step's scalars. OwnerLazyTables defers
+// those updates and replays them here, one step at a time through the same adam_elem, when the
+// row is next read or at a flush: every element goes through the same fp32 operations in the
+// same order as under the dense update, so the tables are bit-for-bit the dense ones.
+//   hist[8 s + k]: step s's scalars (AdamScalars order, one pad), s >= 1
+//   last[r]:       the step up to which row r's (p, m, v) are current
+__device__ __forceinline__ dw::AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
+    const float *h = hist + 8 * s;
+    return dw::AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6]};
+}
+
+// One wave per row (lanes over the row's elements). STEP: replay the missed steps up to
+// step - 1, then apply `step` with the row's gradient g_rows[i]; else replay up to `step`.
+template <bool STEP>
+__global__ void __launch_bounds__(256)
+    k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
+                int32_t *__restrict__ last, int64_t n_table, int32_t d,
+                const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
+                int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
+                int32_t step) {
+    const int lane = threadIdx.x & 63;
+    int64_t n = n_max;
+    if (n_dev) {
+        const int64_t c = *n_dev;
+        n = c < n_max ? c : n_max;
+    }
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; i < n;
+         i += n_waves) {
+        const int64_t r = rows ? static_cast<int64_t>(rows[i]) : i;
+        if (r >= n_table) continue;  // an out-of-range centre: reported by the SGNS pass
+        const int32_t from = __builtin_amdgcn_readfirstlane(last[r]);
+        const int32_t upto = STEP ? step - 1 : step;
+        if (from >= (STEP ? step : upto)) continue;  // already current (or already stepped)
+        for (int64_t e = lane; e < d; e += 64) {
+            const int64_t o = r * d + e;
+            float pp = p[o], mm = m[o], vv = v[o];
+            for (int32_t s = from + 1; s <= upto; ++s) {
+                float z = 0.f;
+                dw::adam_elem(pp, z, mm, vv, hist_at(hist, s));
+            }
+            if (STEP) {
+                float gg = g_rows[i * d + e];
+                dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
+            }
+            p[o] = pp;
+            m[o] = mm;
+            v[o] = vv;
+        }
+        if (lane == 0) last[r] = STEP ? step : upto;
+    }
+}
+
+// out[i] = table[rows[i]] (one wave per row); zero: the source rows are cleared in the same pass
+__global__ void __launch_bounds__(256)
+    k_rows_gather(float *__restrict__ table, int64_t n_table, int32_t d,
+                  const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
+                  int64_t n_max, float *__restrict__ out, int32_t zero) {
+    const int lane = threadIdx.x & 63;
+    int64_t n = n_max;
+    if (n_dev) {
+        const int64_t c = *n_dev;
+        n = c < n_max ? c : n_max;
+    }
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; i < n;
+         i += n_waves) {
+        const int64_t r = static_cast<int64_t>(rows[i]);
+        const bool ok = r < n_table;
+        for (int64_t e = lane; e < d; e += 64) {
+            out[i * d + e] = ok ? table[r * d + e] : 0.f;
+            if (zero && ok) table[r * d + e] = 0.f;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256)
     k_scale(float *__restrict__ x, int64_t n, float alpha, const float *__restrict__ alpha_dev) {
     if (alpha_dev) alpha *= *alpha_dev;
@@ -132,6 +210,44 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
     return dw_adam_dense_to(param, param, grad, exp_avg, exp_avg_sq, n_elem, one_minus_beta1,
                             beta2, one_minus_beta2, bias_correction2_sqrt, neg_step_size, eps,
                             weight_decay, zero_grad, 0, stream);
+}
+
+int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
+                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
+                 const float *hist, int32_t step, void *stream) {
+    DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0 && step >= 0,
+               "dw_adam_rows: bad sizes");
+    if (n_rows_max == 0) return DW_OK;
+    DW_REQUIRE(param && exp_avg && exp_avg_sq && last_step && hist, "dw_adam_rows: null pointer");
+    DW_REQUIRE(rows || !n_rows_dev, "dw_adam_rows: a device row count needs a row list");
+    DW_REQUIRE(!grad_rows || step >= 1, "dw_adam_rows: a gradient step needs step >= 1");
+    int64_t blocks = (n_rows_max + 3) / 4;  // one wave per row, 4 waves per block
+    if (blocks > 8192) blocks = 8192;
+    if (grad_rows)
+        hipLaunchKernelGGL(k_rows_adam<true>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
+    else
+        hipLaunchKernelGGL(k_rows_adam<false>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
+    DW_LAUNCH_CHECK("dw_adam_rows");
+    return DW_OK;
+}
+
+int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                   const int64_t *n_rows_dev, int64_t n_rows_max, float *out,
+                   int32_t zero_source, void *stream) {
+    DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0, "dw_rows_gather: bad sizes");
+    if (n_rows_max == 0) return DW_OK;
+    DW_REQUIRE(table && rows && out, "dw_rows_gather: null pointer");
+    int64_t blocks = (n_rows_max + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       table, n_table_rows, dim, rows, n_rows_dev, n_rows_max, out, zero_source);
+    DW_LAUNCH_CHECK("dw_rows_gather");
+    return DW_OK;
 }
 
 int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream) {

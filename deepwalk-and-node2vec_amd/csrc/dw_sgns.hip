@@ -28,6 +28,7 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include "dw_common.h"
 
@@ -142,6 +143,7 @@ struct SgnsArgs {
     // addressed as local row o / n_owners of w_out; wave g appends its records to its own region
     // [g * region, (g+1) * region) of rec_key / rec_val and leaves the count in rec_counts[g]
     int32_t owner, n_owners;
+    int32_t own_shift;        //   log2(n_owners) when a power of two (mask / shift), else -1
     uint32_t *rec_counts;
     int64_t region;
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
@@ -425,12 +427,15 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                     dw::status_or(a.status, DW_S_BAD_INDEX);
             }
             if constexpr (OWNER) {
-                const bool own = id >= 0 && (id % a.n_owners) == a.owner;
+                // owner o % W, local row o / W (shift and mask for the usual W = 2, 4, 8)
+                const int32_t lrow = a.own_shift >= 0 ? (id >> a.own_shift) : id / a.n_owners;
+                const int32_t orow = id - lrow * a.n_owners;
+                const bool own = id >= 0 && orow == a.owner;
                 const uint32_t grp =
                     static_cast<uint32_t>(__ballot(own) >> (16 * q)) & 0xFFFFu;
                 if (own) {
                     const int pos = n_own + __popc(grp & ((1u << gl) - 1u));
-                    s_id[wv][q][pos] = id / a.n_owners;
+                    s_id[wv][q][pos] = lrow;
                     s_t[wv][q][pos] = static_cast<uint8_t>(t);
                 }
                 n_own += __popc(grp);
@@ -1209,13 +1214,18 @@ struct OccSpace {
 };
 
 int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t st) {
-    size_t tmp = 0;
+    size_t tmp = 0, utmp = 0;
     rocprim::double_buffer<uint32_t> kb(nullptr, nullptr), vb(nullptr, nullptr);
     if (rocprim::radix_sort_pairs(nullptr, tmp, kb, vb, static_cast<uint32_t>(n_centres), 0,
-                                  end_bit_for(V), st) != hipSuccess) {
-        dw::set_error("dw_sgns_owner: occurrence sort size query failed");
+                                  end_bit_for(V), st) != hipSuccess ||
+        rocprim::unique(nullptr, utmp, static_cast<const uint32_t *>(nullptr),
+                        static_cast<uint32_t *>(nullptr), static_cast<int64_t *>(nullptr),
+                        static_cast<size_t>(n_centres), rocprim::equal_to<uint32_t>(),
+                        st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner: occurrence sort / unique size query failed");
         return DW_E_HIP;
     }
+    if (utmp > tmp) tmp = utmp;
     const size_t a = align256((size_t)n_centres * 4);
     char *p = static_cast<char *>(base);
     o->k0 = reinterpret_cast<uint32_t *>(p);
@@ -1251,8 +1261,63 @@ int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *work
     return DW_OK;
 }
 
-int launch_owner_pass1(SgnsArgs a, int64_t local_rows, void *workspace, size_t workspace_bytes,
-                       hipStream_t st) {
+// The global batch's centres in node order into occ.v0 (their nodes in occ.k0); touched != NULL:
+// also the distinct nodes, sorted, and their count (device int64).
+int owner_order(const SgnsArgs &a, const OccSpace &occ, uint32_t *touched, int64_t *n_touched,
+                hipStream_t st) {
+    int64_t ob = (a.batch + 255) / 256;
+    if (ob > grid_cap(8)) ob = grid_cap(8);
+    hipLaunchKernelGGL(k_occ_keys, dim3((unsigned)ob), dim3(256), 0, st, a.walks, a.batch, a.L,
+                       a.R, occ.k0, occ.v0);
+    DW_LAUNCH_CHECK("dw_sgns_owner/occ_keys");
+    rocprim::double_buffer<uint32_t> kb(occ.k0, occ.k1), vb(occ.v0, occ.v1);
+    size_t tb = occ.tmp_bytes;
+    if (rocprim::radix_sort_pairs(occ.tmp, tb, kb, vb, static_cast<uint32_t>(a.batch), 0,
+                                  end_bit_for(a.V), st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner: occurrence sort failed");
+        return DW_E_HIP;
+    }
+    if (kb.current() != occ.k0) {  // keep the order where pass 1 and the unique step read it
+        const size_t nb = static_cast<size_t>(a.batch) * sizeof(uint32_t);
+        if (hipMemcpyAsync(occ.k0, kb.current(), nb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(occ.v0, vb.current(), nb, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner: occurrence copy failed");
+            return DW_E_HIP;
+        }
+    }
+    if (touched) {
+        size_t ub = occ.tmp_bytes;
+        if (rocprim::unique(occ.tmp, ub, static_cast<const uint32_t *>(occ.k0), touched, n_touched,
+                            static_cast<size_t>(a.batch), rocprim::equal_to<uint32_t>(),
+                            st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner: distinct centres failed");
+            return DW_E_HIP;
+        }
+    }
+    return DW_OK;
+}
+
+int launch_owner_prepare(SgnsArgs a, int64_t local_rows, uint32_t *touched, int64_t *n_touched,
+                         void *workspace, size_t workspace_bytes, hipStream_t st) {
+    const int64_t T = (int64_t)a.C * (1 + a.K);
+    Workspace ws;
+    OwnerLayout lay;
+    OccSpace occ;
+    int rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
+                             "dw_sgns_owner_prepare", a.V, &occ);
+    if (rc != DW_OK) return rc;
+    if (a.batch == 0) {
+        if (n_touched && hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner_prepare: count reset failed");
+            return DW_E_HIP;
+        }
+        return DW_OK;
+    }
+    return owner_order(a, occ, touched, n_touched, st);
+}
+
+int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void *workspace,
+                       size_t workspace_bytes, hipStream_t st) {
     const int64_t T = (int64_t)a.C * (1 + a.K);
     DW_REQUIRE(a.n_owners >= 1 && a.owner >= 0 && a.owner < a.n_owners,
                "dw_sgns_owner_pass1: owner %d of %d", a.owner, a.n_owners);
@@ -1275,20 +1340,11 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, void *workspace, size_t w
     a.region = lay.region;
     a.occ_per_wave = lay.region / T;
     if (a.batch > 0) {
-        // the centres in node order (stable: walk order within a node)
-        int64_t ob = (a.batch + 255) / 256;
-        if (ob > grid_cap(8)) ob = grid_cap(8);
-        hipLaunchKernelGGL(k_occ_keys, dim3((unsigned)ob), dim3(256), 0, st, a.walks, a.batch,
-                           a.L, a.R, occ.k0, occ.v0);
-        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/occ_keys");
-        rocprim::double_buffer<uint32_t> kb(occ.k0, occ.k1), vb(occ.v0, occ.v1);
-        size_t tb = occ.tmp_bytes;
-        if (rocprim::radix_sort_pairs(occ.tmp, tb, kb, vb, static_cast<uint32_t>(a.batch), 0,
-                                      end_bit_for(a.V), st) != hipSuccess) {
-            dw::set_error("dw_sgns_owner_pass1: occurrence sort failed");
-            return DW_E_HIP;
+        if (!order_ready) {  // the centres in node order (stable: walk order within a node)
+            rc = owner_order(a, occ, nullptr, nullptr, st);
+            if (rc != DW_OK) return rc;
         }
-        a.occ = vb.current();
+        a.occ = occ.v0;
         rc = launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
         hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts, lay.n_waves,
@@ -1650,10 +1706,31 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
     return DW_OK;
 }
 
+int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          int64_t local_rows, uint32_t *touched, int64_t *n_touched,
+                          void *workspace, size_t workspace_bytes, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   vocab_size >= 1 && local_rows >= 1 && neg_samples >= 0,
+               "dw_sgns_owner_prepare: bad sizes");
+    DW_REQUIRE((walks || n_walks == 0) && (!touched || n_touched),
+               "dw_sgns_owner_prepare: null pointer");
+    SgnsArgs a = base_args(vocab_size, 64, neg_samples, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, 0, 0, 1.f, nullptr, nullptr);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    return launch_owner_prepare(a, local_rows, touched, n_touched, workspace, workspace_bytes,
+                                dw::as_stream(stream));
+}
+
 int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                         int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                         int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
-                        const float *w_in, const float *w_out_local, float *g_in,
+                        int32_t order_ready, const float *w_in, const float *w_out_local,
+                        float *g_in,
                         const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                         float grad_scale, double *loss_acc, int32_t *status, void *workspace,
                         size_t workspace_bytes, void *stream) {
@@ -1671,7 +1748,11 @@ int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_leng
     a.C = 2 * context_radius;
     a.owner = owner;
     a.n_owners = n_owners;
-    return launch_owner_pass1(a, local_rows, workspace, workspace_bytes, dw::as_stream(stream));
+    a.own_shift = -1;
+    for (int sh = 0; sh < 31; ++sh)
+        if ((1 << sh) == n_owners) a.own_shift = sh;
+    return launch_owner_pass1(a, local_rows, order_ready, workspace, workspace_bytes,
+                              dw::as_stream(stream));
 }
 
 int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_radius,

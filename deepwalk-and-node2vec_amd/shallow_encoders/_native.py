@@ -33,7 +33,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -69,9 +69,13 @@ SIGNATURES = {
                                                    _i64, _i32, _p, _p, _p, _p, ctypes.c_size_t,
                                                    _p]),
     'dw_sgns_owner_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _i64, _szp]),
+    'dw_sgns_owner_prepare': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i64, _p, _p,
+                                             _p, ctypes.c_size_t, _p]),
     'dw_sgns_owner_pass1': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32,
-                                           _i64, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p, _p,
-                                           ctypes.c_size_t, _p]),
+                                           _i64, _i32, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p,
+                                           _p, ctypes.c_size_t, _p]),
+    'dw_adam_rows': (ctypes.c_int, [_p, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _p, _i32, _p]),
+    'dw_rows_gather': (ctypes.c_int, [_p, _i64, _i32, _p, _p, _i64, _p, _i32, _p]),
     'dw_sgns_owner_pass2': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p, _p,
                                            _p, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p,
                                            ctypes.c_size_t, _p, _p]),

@@ -321,12 +321,14 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      n_owners: int, vocab_size: int, noise: Optional[torch.Tensor] = None,
                      seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                      loss_acc: Optional[torch.Tensor] = None,
-                     status: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     status: Optional[torch.Tensor] = None,
+                     order_ready: bool = False) -> torch.Tensor:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
     partial centre-table gradient of the owned slots; returns the float64[4] loss accumulator
-    (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2."""
+    (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
+    ``order_ready``: sgns_owner_prepare already built the centre order for these walks."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -353,12 +355,36 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
-                     int(owner), int(n_owners), local_rows, _native.ptr(w_in),
+                     int(owner), int(n_owners), local_rows, 1 if order_ready else 0,
+                     _native.ptr(w_in),
                      _native.ptr(w_out_local), _native.ptr(g_in), _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),
                      _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws), ws.numel(),
                      _native.stream(dev))
     return loss_acc
+
+
+def sgns_owner_prepare(walks: torch.Tensor, context_radius: int, neg_samples: int,
+                       vocab_size: int, local_rows: int, *,
+                       touched: Optional[torch.Tensor] = None,
+                       n_touched: Optional[torch.Tensor] = None) -> None:
+    """dw_sgns_owner_prepare: the centre order of ``walks`` for sgns_owner_pass1(order_ready=True)
+    and, with ``touched`` (int32 [>= n_centres], read as uint32) and ``n_touched`` (int64 [1]),
+    the sorted distinct centre nodes and their count, on the device."""
+    dev = walks.device
+    if walks.dtype != torch.int32 or walks.dim() != 2:
+        raise TypeError('walks must be int32 [n_walks, L]')
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    n_centres = n * (L - 2 * R)
+    if touched is not None and (touched.numel() < n_centres or touched.dtype != torch.int32
+                                or n_touched is None or n_touched.dtype != torch.int64):
+        raise ValueError('touched must be int32 [>= n_centres] with an int64 n_touched')
+    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
+    with torch.cuda.device(dev):
+        _native.call('dw_sgns_owner_prepare', _native.ptr(walks), n, L, R, K, int(vocab_size),
+                     int(local_rows), _native.ptr(touched), _native.ptr(n_touched),
+                     _native.ptr(ws), ws.numel(), _native.stream(dev))
 
 
 def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local: torch.Tensor,

@@ -432,12 +432,7 @@ class OwnerTables:
         self.step_count = 0
         self._cuda = self.device.type == 'cuda'
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.params_in = torch.zeros((2, self.V_pad, self.d), **f32)
-        self.grads_in = torch.zeros((self.V_pad, self.d), **f32)
-        self.m_in = torch.zeros((self.S, self.d), **f32)
-        self.v_in = torch.zeros_like(self.m_in)
-        self.grad_shard = (torch.empty_like(self.m_in) if self.world > 1 and not self.emulated
-                           else None)
+        self._alloc_in(f32)
         self.w_out = torch.zeros((self.S, self.d), **f32)
         self.g_out = torch.zeros_like(self.w_out)
         self.m_out = torch.zeros_like(self.w_out)
@@ -451,9 +446,23 @@ class OwnerTables:
         if init_seed is not None:
             self.xavier_(init_seed)
 
+    def _alloc_in(self, f32: dict) -> None:
+        """The in table (two buffers), its dense partial gradient and the own rows' Adam state."""
+        self.params_in = torch.zeros((2, self.V_pad, self.d), **f32)
+        self.grads_in = torch.zeros((self.V_pad, self.d), **f32)
+        self.m_in = torch.zeros((self.S, self.d), **f32)
+        self.v_in = torch.zeros_like(self.m_in)
+        self.grad_shard = (torch.empty_like(self.m_in) if self.world > 1 and not self.emulated
+                           else None)
+
     # ---- views -------------------------------------------------------------------------------
     @property
     def w_in(self) -> torch.Tensor:
+        return self.params_in[self._cur_in, :self.V]
+
+    @property
+    def w_in_raw(self) -> torch.Tensor:
+        """The in table as the SGNS passes read it (the same as w_in here)."""
         return self.params_in[self._cur_in, :self.V]
 
     @property
@@ -626,4 +635,226 @@ def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
     if spec is None:
         tables.out_step()
     tables.sync()
+    return n
+
+
+HIST_CAP0 = 1024   # initial rows of OwnerLazyTables' Adam-scalar history (doubled on demand)
+
+
+def hip_rows_adam(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor,
+                  rows: Optional[torch.Tensor], n_dev: Optional[torch.Tensor], n_max: int,
+                  g_rows: Optional[torch.Tensor], hist: torch.Tensor, step: int) -> None:
+    """dw_adam_rows on [n_table, d] tables (see include/dw_hip.h)."""
+    with torch.cuda.device(p.device):
+        _native.call('dw_adam_rows', _native.ptr(p), _native.ptr(m), _native.ptr(v),
+                     _native.ptr(last), p.shape[0], p.shape[1], _native.ptr(rows),
+                     _native.ptr(n_dev), int(n_max), _native.ptr(g_rows), _native.ptr(hist),
+                     int(step), _native.stream(p.device))
+
+
+class OwnerLazyTables(OwnerTables):
+    """Owner-computes layout with the touched-row in-table exchange (``bench.py --in-exchange
+    lazy``): SURVEY.md §8e's "throughput mode" — traffic proportional to the rows a step touches,
+    not to V — kept exact.
+
+    The out table is OwnerTables' owner slice. The in table, its Adam state and the step each row
+    is current to (``last_in``) are replicated on every rank. A step reads and updates only the
+    in rows of the global batch's centres, U (every rank holds the same walks, so every rank
+    builds the same sorted U). Every other row has g = 0 for the step, and torch's Adam with
+    g = 0 is a fixed recurrence in (p, m, v): it is deferred and replayed exactly (dw_adam_rows:
+    the same adam_elem, step by step) when the row is next in U or the table is read (``flush``;
+    the ``w_in`` property flushes). Per step (owner_lazy_step):
+      begin_step        records the step's Adam scalars (the replays use them later);
+      prepare           the batch's centre order and U (dw_sgns_owner_prepare);
+      catch_up          the rows of U replay their missed steps, up to step - 1;
+      (pass 1)          the partial centre gradient of the owned slots into g_in (rows of U);
+      exchange_touched  G = g_in[U] (those rows cleared) and all-reduce(SUM) of G on a side
+                        stream while pass 2 runs: |U| x d x 4 B per step instead of the dense
+                        reduce-scatter + all-gather of 2 x V x d x 4 B;
+      (pass 2)          the out slice's records with its Adam fused, as OwnerTables;
+      update_touched    step t on the rows of U with G, on every rank from identical inputs, so
+                        the replicas stay bit-identical.
+    On the CPU (gloo tests, ``adam_impl`` injected) the same protocol runs with torch ops, and
+    ``set_touched`` stands in for ``prepare``.
+
+      params_in  float32 [1, V_pad, d]  replicated in table
+      m_in, v_in float32 [V_pad, d]     its Adam state, replicated
+      last_in    int32 [V_pad]          step each row is current to
+    """
+
+    def _alloc_in(self, f32: dict) -> None:
+        self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
+        self.grads_in = torch.zeros((self.V_pad, self.d), **f32)
+        self.m_in = torch.zeros((self.V_pad, self.d), **f32)
+        self.v_in = torch.zeros_like(self.m_in)
+        self.grad_shard = None
+        self.last_in = torch.zeros(self.V_pad, dtype=torch.int32, device=self.device)
+        pin = self.device.type == 'cuda'
+        self._hist = torch.zeros((HIST_CAP0, 8), **f32)
+        self._hist_host = torch.zeros((HIST_CAP0, 8), dtype=torch.float32, pin_memory=pin)
+        self._lr_hist = [0.0]
+        self._touched = None
+        self._n_max = 0
+        self._n_touched = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._n_host = torch.zeros(1, dtype=torch.int64, pin_memory=pin)
+        self._n_event = None
+        self._G = None
+        self._ar = None
+
+    # ---- views -------------------------------------------------------------------------------
+    @property
+    def w_in(self) -> torch.Tensor:
+        """The in table with every deferred update applied (flushes)."""
+        self.flush()
+        return self.params_in[0, :self.V]
+
+    @property
+    def w_in_raw(self) -> torch.Tensor:
+        """The in table as stored: the rows of the current U are current, others may lag."""
+        return self.params_in[0, :self.V]
+
+    def _hip(self) -> bool:
+        return self._cuda and self.adam_impl is hip_adam
+
+    # ---- the step ------------------------------------------------------------------------------
+    def begin_step(self) -> None:
+        """Starts Adam step t and records its scalars for the replays."""
+        self.step_count += 1
+        s = self.step_count
+        if s >= self._hist.shape[0]:
+            cap = 2 * self._hist.shape[0]
+            h = torch.zeros((cap, 8), dtype=torch.float32, device=self.device)
+            h[:self._hist.shape[0]] = self._hist
+            hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
+            hh[:self._hist_host.shape[0]] = self._hist_host
+            self._hist, self._hist_host = h, hh
+        sc = adam_scalars(s, self.lr, self.betas, self.eps, self.weight_decay)
+        self._hist_host[s, :7] = torch.tensor(sc, dtype=torch.float32)
+        self._hist[s].copy_(self._hist_host[s], non_blocking=True)
+        self._lr_hist.append(self.lr)
+
+    def prepare(self, walks: torch.Tensor, context_radius: int, neg_samples: int) -> None:
+        """The batch's centre order (for pass 1 with order_ready) and its touched rows U."""
+        from shallow_encoders.word2vec.sgns import sgns_owner_prepare
+        n = walks.shape[0] * (walks.shape[1] - 2 * int(context_radius))
+        if self._touched is None or self._touched.numel() < max(n, 1):
+            self._touched = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
+                           touched=self._touched, n_touched=self._n_touched)
+        self._n_max = n
+        self._n_host.copy_(self._n_touched, non_blocking=True)
+        self._n_event = torch.cuda.Event()
+        self._n_event.record(torch.cuda.current_stream(self.device))
+
+    def set_touched(self, rows: torch.Tensor) -> None:
+        """CPU protocol (tests): the step's touched rows (distinct centre ids)."""
+        self._touched = rows.to(device=self.device, dtype=torch.int64)
+        self._n_max = int(rows.numel())
+
+    def _rows(self, g_rows: Optional[torch.Tensor], step: int, all_rows: bool = False) -> None:
+        """Replay the listed rows (all rows / the touched ones) up to ``step`` (g = 0), or up to
+        step - 1 and then apply ``step`` with g_rows."""
+        if self._hip():
+            if all_rows:
+                hip_rows_adam(self.params_in[0], self.m_in, self.v_in, self.last_in, None, None,
+                              self.V_pad, None, self._hist, step)
+            else:
+                hip_rows_adam(self.params_in[0], self.m_in, self.v_in, self.last_in,
+                              self._touched, self._n_touched, self._n_max, g_rows, self._hist,
+                              step)
+            return
+        rows = torch.arange(self.V_pad, device=self.device) if all_rows else self._touched
+        upto = step - 1 if g_rows is not None else step
+        last = self.last_in[rows]
+        lo = int(last.min()) + 1 if rows.numel() else upto + 1
+        for s in range(lo, upto + 1):
+            sel = rows[last < s]
+            if sel.numel():
+                self._cpu_adam_rows(sel, None, s)
+        if g_rows is not None and rows.numel():
+            self._cpu_adam_rows(rows, g_rows, step)
+        self.last_in[rows] = torch.clamp(self.last_in[rows], min=step)
+
+    def _cpu_adam_rows(self, rows: torch.Tensor, g: Optional[torch.Tensor], s: int) -> None:
+        p, m, v = self.params_in[0][rows], self.m_in[rows], self.v_in[rows]
+        gg = torch.zeros_like(p) if g is None else g.clone()
+        self.adam_impl(p.view(-1), gg.view(-1), m.view(-1), v.view(-1), s, self._lr_hist[s],
+                       self.betas, self.eps, self.weight_decay, False)
+        self.params_in[0][rows] = p
+        self.m_in[rows] = m
+        self.v_in[rows] = v
+
+    def catch_up(self) -> None:
+        """Before pass 1: the touched rows replay their missed steps, up to step - 1."""
+        self._rows(None, self.step_count - 1)
+
+    def exchange_touched(self) -> None:
+        """After pass 1: G = g_in[U] (those rows cleared); N > 1: all-reduce(SUM) of G, on a side
+        stream behind the output-table phase."""
+        n_max = self._n_max
+        multi = self.world > 1 and not self.emulated
+        if self._hip():
+            if self._G is None or self._G.shape[0] < max(n_max, 1):
+                self._G = torch.empty((max(n_max, 1), self.d), dtype=torch.float32,
+                                      device=self.device)
+            with torch.cuda.device(self.device):
+                _native.call('dw_rows_gather', _native.ptr(self.grads_in), self.V_pad, self.d,
+                             _native.ptr(self._touched), _native.ptr(self._n_touched),
+                             int(n_max), _native.ptr(self._G), 1, _native.stream(self.device))
+            if multi:
+                self._n_event.synchronize()   # the batch's |U| (known since prepare)
+                n = int(self._n_host[0])
+                if n > 0:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self._side):
+                        self._side.wait_event(ev)
+                        self._ar = dist.all_reduce(self._G[:n], op=dist.ReduceOp.SUM,
+                                                   group=self.group, async_op=True)
+            return
+        rows = self._touched
+        self._G = self.grads_in[rows].clone()
+        self.grads_in[rows] = 0.0
+        if multi:
+            dist.all_reduce(self._G, op=dist.ReduceOp.SUM, group=self.group)
+
+    def update_touched(self) -> None:
+        """After pass 2 (which still reads the touched rows): Adam step t on them with G."""
+        if self._ar is not None:
+            self._ar.wait()            # the current stream waits for the all-reduce
+            self._ar = None
+        self._rows(self._G, self.step_count)
+
+    def flush(self) -> None:
+        """Every row up to the current step (before the table is read as a whole)."""
+        if self.step_count > 0:
+            self._rows(None, self.step_count, all_rows=True)
+
+    def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
+        raise RuntimeError('OwnerLazyTables steps through owner_lazy_step')
+
+    def sync(self) -> None:
+        """Nothing is pending between steps (update_touched waits for the all-reduce)."""
+
+
+def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
+                    neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
+                    loss_acc: torch.Tensor, status: torch.Tensor) -> int:
+    """One owner-computes step with the touched-row in-table exchange (every rank passes the
+    same global batch). Returns this rank's record count."""
+    from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
+    tables.begin_step()
+    tables.prepare(walks, context_radius, neg_samples)
+    tables.catch_up()
+    sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
+                     context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
+                     vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True)
+    tables.exchange_touched()
+    spec = tables.out_adam_spec()
+    n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,
+                         context_radius=context_radius, out_adam=spec, status=status)
+    if spec is None:
+        tables.out_step()
+    tables.update_touched()
     return n

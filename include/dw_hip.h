@@ -231,10 +231,20 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
  *         receives it. Same walk sizes and workspace as the pass-1 call. */
 int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
                                   int64_t vocab_size, int64_t local_rows, size_t *bytes);
+/* The owner form's centre order for a batch ahead of pass 1 (pass 1 with order_ready = 1 uses
+ * it instead of building its own): the centres sorted by node (stable). touched (optional,
+ * uint32[n_walks*(L-2R)]) receives the batch's distinct centre nodes in increasing order and
+ * *n_touched (device int64) their count — the rows a step reads and updates in the in table
+ * (OwnerLazyTables). Same workspace as the pass-1 / pass-2 calls that follow. */
+int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          int64_t local_rows, uint32_t *touched, int64_t *n_touched,
+                          void *workspace, size_t workspace_bytes, void *stream);
 int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                         int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                         int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
-                        const float *w_in, const float *w_out_local, float *g_in,
+                        int32_t order_ready, const float *w_in, const float *w_out_local,
+                        float *g_in,
                         const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                         float grad_scale, double *loss_acc, int32_t *status, void *workspace,
                         size_t workspace_bytes, void *stream);
@@ -351,6 +361,33 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
 
 /* Scale a float32 buffer in place: x *= alpha * (*alpha_dev) (alpha_dev NULL -> 1). Used by the
  * autograd path to apply the device-resident grad_output without a host synchronisation. */
+/* Lazy exact Adam over selected rows (OwnerLazyTables, the touched-row in-table exchange;
+ * torch.optim.Adam single-tensor semantics as dw_adam_dense). A row's update with g = 0 is a
+ * fixed recurrence, so rows no batch touched are brought up to date later by replaying each
+ * missed step through the same per-element arithmetic: the result is bit-identical to the
+ * dense update every step.
+ *   rows: uint32 row ids (NULL = rows 0 .. n_rows_max-1); n_rows_dev: device int64 count
+ *         (NULL = n_rows_max; clamped to n_rows_max); ids >= n_table_rows are skipped;
+ *   last_step: int32[n_table_rows], the step each row's (param, exp_avg, exp_avg_sq) are
+ *         current to; updated;
+ *   hist: float32[(step+1) * 8]: row s = Adam step s's scalars in dw_adam_dense's order
+ *         (1-beta1, beta2, 1-beta2, sqrt(bias_correction2), -lr/bias_correction1, eps,
+ *         weight_decay, unused);
+ *   grad_rows NULL: replay every listed row up to `step` (g = 0);
+ *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
+ *         gradient grad_rows[i]. */
+int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
+                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
+                 const float *hist, int32_t step, void *stream);
+
+/* out[i] = table[rows[i]] for i < min(*n_rows_dev, n_rows_max) (float32 rows of dim); with
+ * zero_source the table rows are cleared in the same pass (the touched rows of the in-table
+ * gradient, gathered for the all-reduce). */
+int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                   const int64_t *n_rows_dev, int64_t n_rows_max, float *out,
+                   int32_t zero_source, void *stream);
+
 int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream);
 
 #ifdef __cplusplus

@@ -108,3 +108,87 @@ def test_owner_tables_equal_single_process(world):
     owned = np.concatenate([r[6] for r in res])
     assert sorted(owned.tolist()) == list(range(S * world))
     np.testing.assert_allclose(res[0][5], ref.m[1].numpy()[:V], rtol=1e-4, atol=1e-9)
+
+
+# ---- the touched-row in-table exchange (OwnerLazyTables) -------------------------------------
+# sparse batches over a larger vocabulary: most rows miss several steps, so the deferred Adam
+# updates are replayed (catch_up / flush) rather than applied every step
+VL, NWL, LL, STEPS_L = 300, 4, 9, 5
+
+
+def lazy_batches():
+    rng = np.random.default_rng(7)
+    out = []
+    for _ in range(STEPS_L):
+        walks = rng.integers(1, VL, size=(NWL, LL))
+        ins, tgt = sgns_ref.sg_windows(walks, R)
+        noise = rng.integers(0, VL, size=(len(ins), 2 * R, K))
+        out.append((ins, tgt, noise))
+    return out
+
+
+def lazy_train(t, rank, world):
+    rows = t.out_rows().numpy()
+    keep = rows < t.V
+    for ins, tgt, noise in lazy_batches():
+        U = np.unique(ins.reshape(-1))
+        t.begin_step()
+        t.set_touched(torch.as_tensor(U))
+        t.catch_up()
+        _, gi, go = sgns_ref.sgns_grads_closed_form(t.w_in_raw.numpy(), t.full_w_out().numpy(),
+                                                    ins, tgt, noise, owner=rank, n_owners=world)
+        untouched = np.setdiff1d(np.arange(t.V), U)
+        assert np.abs(gi[untouched]).max(initial=0.0) == 0.0   # only centres get a gradient
+        t.g_in.add_(torch.as_tensor(gi, dtype=torch.float32))
+        t.exchange_touched()
+        t.g_out[keep] += torch.as_tensor(go[rows[keep]], dtype=torch.float32)
+        t.out_step()
+        t.update_touched()
+        assert float(t.grads_in.abs().max()) == 0.0
+        # rows outside U lag behind: the deferral is really exercised
+        assert int(t.last_in[torch.as_tensor(untouched)].min()) < t.step_count or t.step_count == 1
+
+
+def _lazy_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables
+    t = OwnerLazyTables(VL, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    lazy_train(t, rank, world)
+    w_in = t.w_in.numpy().copy()             # flushes every deferred update
+    assert int(t.last_in.min()) == t.step_count
+    q.put((rank, w_in, t.full_w_out().numpy(), t.m_in.numpy().copy(), t.v_in.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('world', [1, 2, 3])
+def test_owner_lazy_tables_equal_dense_single_process(world):
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    ref = ShardedTables(VL, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    for ins, tgt, noise in lazy_batches():
+        _, gi, go = sgns_ref.sgns_grads_closed_form(ref.w_in.numpy(), ref.w_out.numpy(), ins, tgt,
+                                                    noise)
+        ref.g_in.add_(torch.as_tensor(gi, dtype=torch.float32))
+        ref.g_out.add_(torch.as_tensor(go, dtype=torch.float32))
+        ref.step()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lazy_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(1, world):
+        np.testing.assert_array_equal(res[0][1], res[r][1])   # replicas identical
+        np.testing.assert_array_equal(res[0][3], res[r][3])
+    np.testing.assert_allclose(res[0][1], ref.w_in.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(res[0][2], ref.w_out.numpy(), rtol=1e-5, atol=1e-6)
+    # the replicated in-table Adam state after the flush equals the dense optimizer's
+    np.testing.assert_allclose(res[0][3][:VL], ref.m[0].numpy()[:VL], rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(res[0][4][:VL], ref.v[0].numpy()[:VL], rtol=1e-4, atol=1e-12)

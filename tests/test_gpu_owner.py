@@ -257,3 +257,141 @@ def test_owner_tables_two_ranks_equal_single_process(hip_device):
         assert bad.mean() < 1e-3, bad.mean()
         assert_no_row_drift(got, exp, rtol=1e-4)
         assert np.abs(got - exp).max() <= 2.05 * LR2 * STEPS2
+
+
+# ---- the touched-row in-table exchange: lazy exact Adam (dw_adam_rows, OwnerLazyTables) -------
+@pytest.mark.parametrize('d', [64, 96])
+def test_rows_adam_replay_is_bit_exact(hip_device, d):
+    """dw_adam_rows replaying a row's missed steps (g = 0, per-step lr) gives exactly what one
+    dense dw_adam_dense per step would have given; the gradient step on top matches too."""
+    from shallow_encoders.word2vec.sharding import adam_scalars, hip_adam, hip_rows_adam
+    g = torch.Generator().manual_seed(d)
+    V, S = 300, 7
+    betas, eps = (0.9, 0.999), 1e-8
+    lrs = [0.1, 0.1, 0.05, 0.05, 0.02, 0.01, 0.01, 0.01]       # step s uses lrs[s - 1]
+    hist = torch.zeros((S + 2, 8))
+    for s in range(1, S + 2):
+        hist[s, :7] = torch.tensor(adam_scalars(s, lrs[s - 1], betas, eps, 0.0))
+    hist = hist.cuda()
+    p0 = torch.randn((V, d), generator=g)
+    m0 = torch.randn((V, d), generator=g) * 1e-2
+    v0 = torch.rand((V, d), generator=g) * 1e-3
+    last0 = torch.randint(0, S + 1, (V,), generator=g, dtype=torch.int32)
+    # reference: every row behind step s gets a dense g = 0 step s (hip_adam on the gathered rows)
+    ref = [t.cuda().clone() for t in (p0, m0, v0)]
+    for s in range(1, S + 1):
+        rows = torch.nonzero(last0 < s).flatten().cuda()
+        pp, mm, vv = (t[rows].contiguous() for t in ref)
+        hip_adam(pp.view(-1), torch.zeros_like(pp).view(-1), mm.view(-1), vv.view(-1), s,
+                 lrs[s - 1], betas, eps, 0.0, False)
+        for t, u in zip(ref, (pp, mm, vv)):
+            t[rows] = u
+    p, m, v = (t.cuda().clone() for t in (p0, m0, v0))
+    last = last0.cuda().clone()
+    hip_rows_adam(p, m, v, last, None, None, V, None, hist, S)          # replay every row to S
+    torch.cuda.synchronize()
+    for a, b in zip((p, m, v), ref):
+        assert torch.equal(a, b)
+    assert int(last.min()) == S == int(last.max())
+    # a gradient step S + 1 on some rows (listed, with a device count) vs the dense kernel
+    rows = torch.tensor([3, 17, 18, 250, 299], dtype=torch.int32).cuda()
+    n_dev = torch.tensor([5], dtype=torch.int64).cuda()
+    gr = torch.randn((5, d), generator=g).cuda()
+    hip_rows_adam(p, m, v, last, rows, n_dev, 5, gr, hist, S + 1)
+    ri = rows.long()
+    pp, mm, vv = (t[ri].contiguous() for t in ref)
+    hip_adam(pp.view(-1), gr.clone().view(-1), mm.view(-1), vv.view(-1), S + 1, lrs[S], betas,
+             eps, 0.0, False)
+    torch.cuda.synchronize()
+    assert torch.equal(p[ri], pp) and torch.equal(m[ri], mm) and torch.equal(v[ri], vv)
+    assert (last[ri] == S + 1).all() and int((last == S + 1).sum()) == 5
+
+
+def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0):
+    """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L]."""
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4)
+    n, L = walks_all.shape[1:]
+    per = L - 2 * R
+    acc = torch.zeros(4, dtype=torch.float64, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    for s in range(walks_all.shape[0]):
+        owner_lazy_step(t, walks_all[s].to(device), R, K, seed=11, noise_offset=s * n * per,
+                        grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status)
+    torch.cuda.synchronize()
+    _native.check_status(status, 'owner_lazy_step')
+    return t, acc
+
+
+def test_owner_lazy_single_rank_equals_dense(hip_device):
+    """One rank: sparse batches (most rows untouched for several steps) through the lazy
+    protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush."""
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    V, d, R, K, L, n, steps, lr = 5000, 64, 2, 3, 12, 16, 6, 0.01
+    walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(3),
+                          dtype=torch.int32)
+    ref = ShardedTables(V, d, hip_device, lr=lr, init_seed=4)
+    per = L - 2 * R
+    acc_ref = torch.zeros(4, dtype=torch.float64, device=hip_device)
+    for s in range(steps):
+        sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
+                        context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
+        ref.step()
+    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr)
+    lag = int((t.last_in[:V] < steps).sum())
+    assert lag > V // 2                      # most rows were deferred before the flush
+    w_in = t.w_in.cpu().numpy()              # flush
+    assert int(t.last_in.min()) == steps
+    torch.testing.assert_close(acc, acc_ref, rtol=1e-5, atol=1e-6)
+    for got, exp in ((w_in, ref.w_in.cpu().numpy()), (t.full_w_out().cpu().numpy(),
+                                                      ref.w_out.cpu().numpy())):
+        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
+                            max_abs=2.05 * lr * steps)
+        assert_no_row_drift(got, exp)
+
+
+def _lazy_run(rank, world, port, q):
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        t, acc = _lazy_vs_dense('cuda:0', _walks_all(), V2, D2, R2, K2, LR2)
+        q.put((rank, t.w_in.cpu().numpy().copy(), t.full_w_out().cpu().numpy(),
+               acc.cpu().numpy(), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report, the parent asserts
+        q.put((rank, None, None, None, repr(e)))
+
+
+@pytest.mark.timeout(600)
+def test_owner_lazy_two_ranks_equal_single_process(hip_device):
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    ref = ShardedTables(V2, D2, hip_device, lr=LR2, init_seed=4)
+    walks = _walks_all()
+    per = L2 - 2 * R2
+    acc_ref = torch.zeros(4, dtype=torch.float64, device=hip_device)
+    for s in range(STEPS2):
+        sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K2, walks=walks[s].cuda(),
+                        context_radius=R2, seed=11, noise_offset=s * NW2 * per, loss_acc=acc_ref)
+        ref.step()
+    torch.cuda.synchronize()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lazy_run, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs
+    (_, i0, o0, a0, _), (_, i1, o1, a1, _) = res
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_allclose(a0 + a1, acc_ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    for got, exp in ((i0, ref.w_in.cpu().numpy()), (o0, ref.w_out.cpu().numpy())):
+        bad = ~np.isclose(got, exp, rtol=1e-4, atol=1e-6)
+        assert bad.mean() < 1e-3, bad.mean()
+        assert_no_row_drift(got, exp, rtol=1e-4)
