@@ -142,6 +142,10 @@ def main():
                          'batch touched are all-reduced and updated, the others\' g = 0 Adam '
                          'steps replayed exactly when next touched (OwnerLazyTables; default at '
                          'C5, where the dense exchange is 2 x 17 GB per step)')
+    ap.add_argument('--walk-prefetch', action='store_true',
+                    help='generate the next batch\'s walks on a side stream during this step\'s '
+                         'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
+                         'saves, 6.89 vs 6.89 ms/step at C3)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
@@ -213,6 +217,65 @@ def main():
     BG = B * W_eff if owner else B      # walks each rank generates per step (owner: all ranks')
     walks_buf = torch.empty((BG, L), dtype=torch.int32, device=dev)
     starts_buf = torch.empty(BG, dtype=torch.int32, device=dev)
+
+    class WalkFeed:
+        """The walks of step s, in buffer s % 2. With prefetch, step s+1's walks are generated
+        on a side stream while step s's SGNS runs (the reference's DataLoader workers produce
+        walks concurrently with training too); each timed step still generates exactly one
+        batch. The walker is latency-bound and leaves the bandwidth to the SGNS kernels."""
+
+        def __init__(self, n_walks, first_id, prefetch):
+            nb = 2 if prefetch else 1
+            self.prefetch, self.first_id = prefetch, first_id
+            self.walks = [walks_buf] + [torch.empty_like(walks_buf[:n_walks])
+                                        for _ in range(nb - 1)]
+            self.starts = [starts_buf] + [torch.empty_like(starts_buf[:n_walks])
+                                          for _ in range(nb - 1)]
+            self.n = n_walks
+            self.ready = [torch.cuda.Event() for _ in range(nb)]
+            self.free = [None] * nb
+            self.stream = torch.cuda.Stream(dev) if prefetch else None
+            self.launched = -1
+
+        def _gen(self, s):
+            i = s % len(self.walks)
+            g0 = self.first_id(s)
+            ids = (torch.arange(g0, g0 + self.n, device=dev, dtype=torch.int64) % walks_total)
+            torch.floor_divide(ids, args.walks_per_node, out=ids)
+            self.starts[i][:self.n].copy_(ids + 1)
+            walker.walk_batch(self.starts[i][:self.n], walk_id0=g0, out=self.walks[i][:self.n],
+                              check=False)
+
+        def _launch(self, s):
+            i = s % 2
+            with torch.cuda.stream(self.stream):
+                if self.free[i] is not None:
+                    self.stream.wait_event(self.free[i])
+                self._gen(s)
+                self.ready[i].record(self.stream)
+            self.launched = s
+
+        def get(self, s):
+            """On the current stream: step s's walks."""
+            if not self.prefetch:
+                self._gen(s)
+                return self.walks[0][:self.n]
+            if self.launched < s:
+                self._launch(s)
+            torch.cuda.current_stream(dev).wait_event(self.ready[s % 2])
+            return self.walks[s % 2][:self.n]
+
+        def next(self, s):
+            """After step s's walks are first read: start step s+1's."""
+            if self.prefetch:
+                self._launch(s + 1)
+
+        def release(self, s):
+            """After the last reader of step s's walks is enqueued."""
+            if self.prefetch:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                self.free[s % 2] = ev
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
@@ -231,40 +294,44 @@ def main():
         # gather: this rank's B walks are global ids g0 + rank*B ... (the same global batch);
         # emulated, all W*B walks are generated here (no collective to time: conservative)
         gather = args.owner_walks == 'gather' and not emulate
-        a0 = g0 + tables.rank * B if gather else g0
-        nb = B if gather else BG
-        ids = (torch.arange(a0, a0 + nb, device=dev, dtype=torch.int64) % walks_total)
-        torch.floor_divide(ids, args.walks_per_node, out=ids)
-        starts_buf[:nb].copy_(ids + 1)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         if record:
             e[0].record()
         if gather:
+            a0 = g0 + tables.rank * B
+            ids = (torch.arange(a0, a0 + B, device=dev, dtype=torch.int64) % walks_total)
+            torch.floor_divide(ids, args.walks_per_node, out=ids)
+            starts_buf[:B].copy_(ids + 1)
             own = walks_buf[tables.rank * B:(tables.rank + 1) * B]
             walker.walk_batch(starts_buf[:B], walk_id0=a0, out=own, check=False)
             send = own if backend == 'nccl' else own.clone()
             dist.all_gather_into_tensor(walks_buf.view(-1), send.reshape(-1))
+            walks = walks_buf
         else:
-            walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
+            walks = feed.get(s)
         if record:
             e[1].record()
         if lazy:
             tables.begin_step()
-            tables.prepare(walks_buf, R, K)
+            tables.prepare(walks, R, K)
             tables.catch_up()
-        sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks_buf,
+        sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks,
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
                          grad_scale=grad_scale, loss_acc=loss_acc, status=status,
                          order_ready=lazy)
+        if not gather:
+            feed.next(s)
         if lazy:
             tables.exchange_touched()
         else:
             tables.exchange_in()        # full grid: 1/W of the in table, between RS and AG
         spec = tables.out_adam_spec() if fuse else None
         n_rec[0] = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, K,
-                                    walks=walks_buf, context_radius=R, out_adam=spec,
+                                    walks=walks, context_radius=R, out_adam=spec,
                                     status=status)
+        if not gather:
+            feed.release(s)
         if spec is None:
             tables.out_step()
         if record:
@@ -280,6 +347,12 @@ def main():
             ev['adam'].append((e[2], e[3]))
 
     n_rec = [0]
+    # walks: one batch per step; prefetched on a side stream unless owner 'gather' (a collective)
+    prefetch = args.walk_prefetch and not (owner and args.owner_walks == 'gather'
+                                           and not emulate)
+    feed = WalkFeed(BG if owner else B,
+                    (lambda s: s * BG) if owner else (lambda s: (s * world + rank) * B),
+                    prefetch)
 
     def one_step(record: bool):
         if owner:
@@ -287,34 +360,33 @@ def main():
         s = step_idx[0]
         step_idx[0] += 1
         g0 = (s * world + rank) * B                   # global walk id of this rank's batch
-        ids = (torch.arange(g0, g0 + B, device=dev, dtype=torch.int64) % walks_total)
-        torch.floor_divide(ids, args.walks_per_node, out=ids)
-        starts_buf.copy_(ids + 1)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         if record:
             e[0].record()
-        walker.walk_batch(starts_buf, walk_id0=g0, out=walks_buf, check=False)
+        walks = feed.get(s)
         if record:
             e[1].record()
-        kw = dict(walks=walks_buf, context_radius=R, noise=None, seed=99,
+        kw = dict(walks=walks, context_radius=R, noise=None, seed=99,
                   noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale, loss_acc=loss_acc,
                   status=status, scatter=args.scatter)
         # pass 1 (g_in final) -> in-table exchange on a side stream (N > 1) while the
         # output-table phase runs -> out-table exchange -> wait for both all-gathers
         sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
+        feed.next(s)
         tables.exchange_in(overlap_bytes=p2_bytes)
         # one device: the output table's Adam is fused into the output-table phase; N > 1:
         # that phase runs in row pieces, each exchanged behind the next piece's gather
         spec = tables.out_adam_spec() if fuse else None
         if pieces:
             n_pieces, rows = tables.out_pieces_spec()
-            sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks_buf, context_radius=R,
+            sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks, context_radius=R,
                                n_pieces=n_pieces, piece_rows=rows,
                                on_piece=tables.exchange_out_piece, status=status,
                                scatter=args.scatter)
         else:
             sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
                             out_adam=spec, **kw)
+        feed.release(s)
         if record:
             e[2].record()
         tables.exchange_out(fused_out=spec is not None)
