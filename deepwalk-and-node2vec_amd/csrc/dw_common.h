@@ -37,11 +37,12 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+template <int ROUNDS = 10>
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < ROUNDS; ++r) {
         const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
         const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};

@@ -150,10 +150,13 @@ struct SgnsArgs {
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
 };
 
+#ifndef DW_NOISE_ROUNDS
+#define DW_NOISE_ROUNDS 10  // (timing experiments only: any other value changes the stream)
+#endif
 __device__ __forceinline__ int64_t noise_id(const SgnsArgs &a, int64_t b, int j, int k) {
     if (a.noise) return a.noise[(b * a.C + j) * a.K + k];
     const uint64_t g = a.noise_offset + static_cast<uint64_t>(b);
-    const dw::U4 r = dw::philox(
+    const dw::U4 r = dw::philox<DW_NOISE_ROUNDS>(
         dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
                static_cast<uint32_t>(j * a.K + k), TAG_SGNS},
         a.k0, a.k1);

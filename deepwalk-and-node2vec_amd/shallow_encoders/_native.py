@@ -16,7 +16,8 @@ from typing import Optional
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libdw_hip.so')
+LIB_PATH = os.environ.get(   # DW_LIB_PATH: an experimental build (timing studies only)
+    'DW_LIB_PATH', os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libdw_hip.so'))
 
 DW_OK = 0
 DW_E_INVALID_ARG = -1
