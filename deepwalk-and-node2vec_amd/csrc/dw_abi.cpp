@@ -21,7 +21,7 @@ extern "C" {
 
 const char *dw_last_error_string(void) { return dw::g_err; }
 
-int dw_abi_version(void) { return 4; }
+int dw_abi_version(void) { return 5; }
 
 int dw_device_sync(void *stream) {
     hipError_t e = hipStreamSynchronize(dw::as_stream(stream));

@@ -65,6 +65,16 @@ __device__ __forceinline__ uint64_t bounded64(uint32_t lo, uint32_t hi, uint64_t
     return __umul64hi(r, n);
 }
 
+// Per-row adjacency hash (dw_adj_hash_*): buckets of 16 int32 slots for a row of degree `deg`
+// (none up to DW_ADJ_HASH_MIN_DEG, else load <= 3/4), and the home bucket of neighbour x.
+__host__ __device__ __forceinline__ int64_t adj_buckets(int64_t deg) {
+    return deg > DW_ADJ_HASH_MIN_DEG ? (4 * deg + 47) / 48 : 0;
+}
+__device__ __forceinline__ uint32_t adj_bucket(int32_t x, uint32_t nb) {
+    return static_cast<uint32_t>(
+        (static_cast<uint64_t>(static_cast<uint32_t>(x) * 0x9E3779B1u) * nb) >> 32);
+}
+
 __device__ __forceinline__ void status_or(int32_t *status, int32_t bits) {
     if (status) atomicOr(status, bits);
 }

@@ -99,6 +99,51 @@ __global__ void k_alias_build(const int64_t *__restrict__ row_ptr, const double 
     }
 }
 
+
+// ---- per-row adjacency hash (node2vec "x in N(prev)" tests in one probe) ---------------------
+// Row u of degree > DW_ADJ_HASH_MIN_DEG owns nb(u) = ceil(4 deg / 48) buckets of 16 int32 slots
+// (load <= 3/4) at adj_off[u]; rows of lower degree own none (a single load of their unsorted
+// neighbour list decides). Key x goes to bucket dw::adj_bucket(x, nb) and the first free slot
+// of that bucket or the next ones (cyclically): slots only go empty -> full, so a bucket with a
+// free slot ends every probe sequence through it.
+__global__ void k_adj_counts(const int64_t *__restrict__ row_ptr, int64_t n_rows,
+                             int64_t *__restrict__ counts) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r <= n_rows; r += stride)
+        counts[r] = r < n_rows ? 16 * dw::adj_buckets(row_ptr[r + 1] - row_ptr[r]) : 0;
+}
+
+__global__ void k_adj_insert(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                             int64_t n_rows, const int64_t *__restrict__ adj_off,
+                             int32_t *__restrict__ tab, int32_t *status) {
+    const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + threadIdx.x / 64; r < n_rows;
+         r += stride) {
+        const int64_t off = adj_off[r];
+        const uint32_t nb = static_cast<uint32_t>((adj_off[r + 1] - off) / 16);
+        if (nb == 0) continue;
+        const int64_t a = row_ptr[r], b = row_ptr[r + 1];
+        for (int64_t e = a + lane; e < b; e += 64) {
+            const int32_t x = col[e];
+            uint32_t bk = dw::adj_bucket(x, nb);
+            bool done = false;
+            for (uint32_t t = 0; t < nb && !done; ++t) {
+                int32_t *slots = tab + off + (int64_t)bk * 16;
+                for (int j = 0; j < 16; ++j) {
+                    const int32_t old = atomicCAS(slots + j, -1, x);
+                    if (old == -1 || old == x) {   // inserted (or a duplicate edge entry)
+                        done = true;
+                        break;
+                    }
+                }
+                if (++bk == nb) bk = 0;
+            }
+            if (!done) dw::status_or(status, DW_S_BAD_CSR);   // cannot happen at load <= 3/4
+        }
+    }
+}
+
 inline int grid_for(int64_t work, int block, int cap = 8192) {
     int64_t g = (work + block - 1) / block;
     if (g < 1) g = 1;
@@ -163,6 +208,60 @@ int dw_csr_sort_copy(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
     hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(nnz, 256)), dim3(256), 0,
                        dw::as_stream(stream), k_out, nnz, col_sorted);
     DW_LAUNCH_CHECK("dw_csr_sort_copy/extract");
+    return DW_OK;
+}
+
+int dw_adj_hash_offsets(const int64_t *row_ptr, int64_t n_rows, int64_t *adj_off, void *temp,
+                        size_t *temp_bytes, void *stream) {
+    DW_REQUIRE(temp_bytes, "dw_adj_hash_offsets: temp_bytes is null");
+    DW_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31),
+               "dw_adj_hash_offsets: n_rows must be in [0, 2^31)");
+    const size_t cnt_bytes = ((size_t)(n_rows + 1) * sizeof(int64_t) + 255) & ~size_t(255);
+    size_t cub_bytes = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (int64_t *)nullptr,
+                                                    (int64_t *)nullptr, (int)(n_rows + 1),
+                                                    dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_adj_hash_offsets: hipcub size query: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    const size_t need = cnt_bytes + cub_bytes;
+    if (temp == nullptr) {
+        *temp_bytes = need;
+        return DW_OK;
+    }
+    DW_REQUIRE(*temp_bytes >= need, "dw_adj_hash_offsets: temp too small (%zu < %zu)",
+               *temp_bytes, need);
+    DW_REQUIRE(row_ptr && adj_off, "dw_adj_hash_offsets: null pointer");
+    int64_t *counts = static_cast<int64_t *>(temp);
+    hipLaunchKernelGGL(k_adj_counts, dim3(grid_for(n_rows + 1, 256)), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, n_rows, counts);
+    DW_LAUNCH_CHECK("dw_adj_hash_offsets/counts");
+    e = hipcub::DeviceScan::ExclusiveSum(static_cast<char *>(temp) + cnt_bytes, cub_bytes, counts,
+                                         adj_off, (int)(n_rows + 1), dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_adj_hash_offsets: hipcub scan: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    return DW_OK;
+}
+
+int dw_adj_hash_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                      const int64_t *adj_off, int64_t n_slots, int32_t *adj_hash, int32_t *status,
+                      void *stream) {
+    DW_REQUIRE(n_rows >= 0 && n_slots >= 0, "dw_adj_hash_build: negative size");
+    DW_REQUIRE(row_ptr && adj_off && status, "dw_adj_hash_build: null pointer");
+    if (n_slots == 0) return DW_OK;
+    DW_REQUIRE(col && adj_hash, "dw_adj_hash_build: null pointer");
+    hipError_t e = hipMemsetAsync(adj_hash, 0xFF, (size_t)n_slots * sizeof(int32_t),
+                                  dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_adj_hash_build: memset: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    hipLaunchKernelGGL(k_adj_insert, dim3(grid_for(n_rows * 64, 256)), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, col, n_rows, adj_off, adj_hash, status);
+    DW_LAUNCH_CHECK("dw_adj_hash_build");
     return DW_OK;
 }
 

@@ -268,6 +268,8 @@ __global__ void __launch_bounds__(256)
 }
 
 constexpr int N2V_WAVES = 4;     // waves per block
+// (Occupancy: the hashed variant compiles to 73 VGPRs, 6 waves/SIMD. Forcing 8 waves/SIMD
+// (amdgpu_waves_per_eu) spills to scratch and measured 16% slower at C3.)
 
 struct N2VThr {
     uint32_t p, q, one;  // accept iff r < thr (ALWAYS = unconditional)
@@ -302,6 +304,34 @@ __device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list,
     return group_ballot<N2V_G>(hit, q) != 0u;
 }
 
+// Membership of a group-uniform key in a row's adjacency hash (dw_adj_hash_build): the group
+// reads one 64-B bucket (16 slots, 16/N2V_G per lane); a hit -> true, a free slot -> false
+// (slots fill in probe order and never empty), else the next bucket. At load <= 3/4 the first
+// bucket almost always decides; nb probes bound the loop.
+template <int N2V_G>
+__device__ __forceinline__ bool group_hash_contains(const int32_t *__restrict__ tab, uint32_t nb,
+                                                    int32_t key, int gl, int q) {
+    constexpr int PER = 16 / N2V_G;
+    uint32_t b = dw::adj_bucket(key, nb);
+    for (uint32_t t = 0; t < nb; ++t) {
+        const int32_t *slot = tab + (int64_t)b * 16 + gl * PER;
+        bool hit = false, free_slot = false;
+        if constexpr (PER == 2) {
+            const int2 e = *reinterpret_cast<const int2 *>(slot);
+            hit = e.x == key || e.y == key;
+            free_slot = e.x < 0 || e.y < 0;
+        } else {
+            const int32_t e = *slot;
+            hit = e == key;
+            free_slot = e < 0;
+        }
+        if (group_ballot<N2V_G>(hit, q)) return true;
+        if (group_ballot<N2V_G>(free_slot, q)) return false;
+        if (++b == nb) b = 0;
+    }
+    return false;
+}
+
 // N2V_G lanes per walker (8 by default: 8 walkers per wave — the walk is latency-bound, so
 // walkers in flight matter more than proposals per instruction). A rejection round draws
 // proposals j = 0..63 (Philox counter lane field j; oracle/philox.py fast_walks) and picks the
@@ -310,11 +340,14 @@ __device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list,
 // accepted iff r < thr(x in N(prev) ? q : one); when r is below both thresholds (accept) or
 // not below either (reject) the adjacency test cannot change the outcome, so only the
 // "ambiguous" proposals BELOW the block's first certain acceptance are tested, in j order,
-// each by one group-cooperative search of N(prev).
-template <int N2V_G>
+// each by one group-cooperative search of N(prev): HASH = false, an N2V_G-ary search of the
+// sorted list `nbr` (col_sorted); HASH = true, one probe of prev's adjacency hash, or for a row
+// without one (degree <= DW_ADJ_HASH_MIN_DEG) one load of its list `nbr` (= col, unsorted).
+template <int N2V_G, bool HASH>
 __global__ void __launch_bounds__(N2V_WAVES *WAVE)
     k_walk_node2vec_fast(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-                         const int32_t *__restrict__ col_sorted,
+                         const int32_t *__restrict__ nbr, const int64_t *__restrict__ adj_off,
+                         const int32_t *__restrict__ adj_hash,
                          const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                          int32_t L, N2VThr thr, uint32_t k0, uint32_t k1, uint64_t walk_id0,
@@ -341,6 +374,8 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
         int32_t v = starts[w];
         int32_t prev = -1;
         int64_t pa = 0, pn = 0;  // CSR range of prev (carried from the previous step)
+        int64_t ph = 0;          // prev's adjacency-hash buckets (HASH), with their count pnb
+        uint32_t pnb = 0;
         if (gl == 0) o[0] = v;
         int32_t s = 1;
         for (; s < L; ++s) {
@@ -350,6 +385,12 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
             }
             const int64_t a = row_ptr[v];
             const int64_t n = row_ptr[v + 1] - a;
+            int64_t h = 0;
+            uint32_t nb = 0;
+            if constexpr (HASH) {   // independent of the row_ptr loads: same latency slot
+                h = adj_off[v];
+                nb = static_cast<uint32_t>((adj_off[v + 1] - h) >> 4);
+            }
             if (n <= 0) {
                 if (gl == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
                 break;
@@ -380,7 +421,12 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                         while (m_amb) {  // group-uniform loop over the candidates that matter
                             const int l = __ffs(m_amb) - 1;
                             const int32_t xl = __shfl(x, q * N2V_G + l, WAVE);
-                            if (group_contains<N2V_G>(col_sorted + pa, pn, xl, gl, q) == adj_wins) {
+                            bool adj;
+                            if (HASH && pnb > 0)
+                                adj = group_hash_contains<N2V_G>(adj_hash + ph, pnb, xl, gl, q);
+                            else
+                                adj = group_contains<N2V_G>(nbr + pa, pn, xl, gl, q);
+                            if (adj == adj_wins) {
                                 win = l;
                                 break;
                             }
@@ -401,6 +447,8 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
             prev = v;
             pa = a;
             pn = n;
+            ph = h;
+            pnb = nb;
             v = nxt;
         }
         if (gl == 0)
@@ -415,6 +463,40 @@ inline uint32_t accept_threshold(double alpha, double alpha_max) {
     if (t < 0.0) t = 0.0;
     if (t > 4294967294.0) t = 4294967294.0;
     return static_cast<uint32_t>(t);
+}
+
+template <bool HASH>
+int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *nbr,
+                    const int64_t *adj_off, const int32_t *adj_hash, const uint32_t *prob_thr,
+                    const int32_t *alias, int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                    int32_t walk_length, double p, double q, uint32_t k0, uint32_t k1,
+                    uint64_t walk_id0, int32_t *out, int32_t *status, void *stream) {
+    DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_fast: p and q must be positive");
+    const double ip = 1.0 / p, iq = 1.0 / q;
+    double amax = 1.0;
+    if (ip > amax) amax = ip;
+    if (iq > amax) amax = iq;
+    N2VThr thr{accept_threshold(ip, amax), accept_threshold(iq, amax), accept_threshold(1.0, amax)};
+    static const int group = [] {  // lanes per walker (tuning knob DW_N2V_GROUP = 8 | 16)
+        const char *e = getenv("DW_N2V_GROUP");
+        const int g = e ? atoi(e) : 8;
+        return (g == 8 || g == 16) ? g : 8;
+    }();
+    const int64_t per_block = N2V_WAVES * (WAVE / group);
+    int64_t blocks = (n_walks + per_block - 1) / per_block;
+    if (blocks > 8192) blocks = 8192;
+    if (group == 8)
+        hipLaunchKernelGGL((k_walk_node2vec_fast<8, HASH>), dim3((unsigned)blocks),
+                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,
+                           adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks,
+                           walk_length, thr, k0, k1, walk_id0, out, status);
+    else
+        hipLaunchKernelGGL((k_walk_node2vec_fast<16, HASH>), dim3((unsigned)blocks),
+                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,
+                           adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks,
+                           walk_length, thr, k0, k1, walk_id0, out, status);
+    DW_LAUNCH_CHECK(HASH ? "dw_walk_fast_adj/node2vec" : "dw_walk_fast/node2vec");
+    return DW_OK;
 }
 
 }  // namespace
@@ -478,32 +560,30 @@ int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_
         return DW_OK;
     }
     DW_REQUIRE(col_sorted, "dw_walk_fast: node2vec needs col_sorted");
-    DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_fast: p and q must be positive");
-    const double ip = 1.0 / p, iq = 1.0 / q;
-    double amax = 1.0;
-    if (ip > amax) amax = ip;
-    if (iq > amax) amax = iq;
-    N2VThr thr{accept_threshold(ip, amax), accept_threshold(iq, amax), accept_threshold(1.0, amax)};
-    static const int group = [] {  // lanes per walker (tuning knob DW_N2V_GROUP = 8 | 16)
-        const char *e = getenv("DW_N2V_GROUP");
-        const int g = e ? atoi(e) : 8;
-        return (g == 8 || g == 16) ? g : 8;
-    }();
-    const int64_t per_block = N2V_WAVES * (WAVE / group);
-    int64_t blocks = (n_walks + per_block - 1) / per_block;
-    if (blocks > 8192) blocks = 8192;
-    if (group == 8)
-        hipLaunchKernelGGL(k_walk_node2vec_fast<8>, dim3((unsigned)blocks), dim3(N2V_WAVES * WAVE),
-                           0, dw::as_stream(stream), row_ptr, col, col_sorted, prob_thr, alias,
-                           n_rows, starts, n_walks, walk_length, thr, k0, k1, walk_id0, out,
-                           status);
-    else
-        hipLaunchKernelGGL(k_walk_node2vec_fast<16>, dim3((unsigned)blocks),
-                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col,
-                           col_sorted, prob_thr, alias, n_rows, starts, n_walks, walk_length, thr,
-                           k0, k1, walk_id0, out, status);
-    DW_LAUNCH_CHECK("dw_walk_fast/node2vec");
-    return DW_OK;
+    return launch_node2vec<false>(row_ptr, col, col_sorted, nullptr, nullptr, prob_thr, alias,
+                                  n_rows, starts, n_walks, walk_length, p, q, k0, k1, walk_id0,
+                                  out, status, stream);
+}
+
+int dw_walk_fast_adj(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                     const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
+                     int64_t n_rows, const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                     int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
+                     int32_t *out, int32_t *status, void *stream) {
+    if (method != DW_METHOD_NODE2VEC || n_walks == 0)   // DeepWalk never tests adjacency
+        return dw_walk_fast(row_ptr, col, nullptr, prob_thr, alias, n_rows, starts, n_walks,
+                            walk_length, method, p, q, seed, walk_id0, out, status, stream);
+    DW_REQUIRE(walk_length >= 1, "dw_walk_fast_adj: Minimum walk length is 1!");
+    DW_REQUIRE(walk_length < (1 << 24), "dw_walk_fast_adj: walk_length too large");
+    DW_REQUIRE(n_walks > 0 && n_rows >= 0, "dw_walk_fast_adj: negative size");
+    DW_REQUIRE(row_ptr && col && adj_off && starts && out && status,
+               "dw_walk_fast_adj: null pointer");
+    DW_REQUIRE((prob_thr == nullptr) == (alias == nullptr),
+               "dw_walk_fast_adj: prob_thr and alias must be both set or both null");
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    return launch_node2vec<true>(row_ptr, col, col, adj_off, adj_hash, prob_thr, alias, n_rows,
+                                 starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
+                                 status, stream);
 }
 
 }  // extern "C"

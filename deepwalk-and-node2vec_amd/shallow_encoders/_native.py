@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -51,6 +51,8 @@ SIGNATURES = {
     'dw_device_sync': (ctypes.c_int, [_p]),
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
+    'dw_adj_hash_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),
+    'dw_adj_hash_build': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _p, _p]),
     'dw_alias_build': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
     'dw_ingest_workspace_bytes': (ctypes.c_int, [_i32, _i64, _i64, _szp]),
     'dw_rmat_edges': (ctypes.c_int, [_i32, _i64, _p, _p, _u64, _u64, _f64, _f64, _f64, _p, _p, _p,
@@ -61,6 +63,8 @@ SIGNATURES = {
                                       _p, _p, _p, _p]),
     'dw_walk_fast': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _i32, _f64, _f64,
                                     _u64, _u64, _p, _p, _p]),
+    'dw_walk_fast_adj': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _i32, _f64,
+                                        _f64, _u64, _u64, _p, _p, _p]),
     'dw_sgns_walks': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_walks_phase': (ctypes.c_int, [_i32, _p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,

@@ -188,8 +188,9 @@ class CSRGraph:
 
     # ------------------------------------------------------------------ device side
     def device_tensors(self, device=None, need_sorted: bool = False,
-                       need_alias: bool = False) -> Dict[str, torch.Tensor]:
-        """Copy the CSR to HBM once (and derive col_sorted / alias tables on the device)."""
+                       need_alias: bool = False, need_adj: bool = False) -> Dict[str, torch.Tensor]:
+        """Copy the CSR to HBM once (and derive col_sorted / alias tables / the per-row
+        adjacency hash on the device)."""
         dev = _native.require_device(device)
         if self._dev_device != dev:
             if self.col is None and 'col' in self._dev:   # device-built: keep a host copy
@@ -212,7 +213,33 @@ class CSRGraph:
             d['col_sorted'] = self._sorted_copy(dev)
         if need_alias and self.weights is not None and 'prob_thr' not in d:
             self._build_alias(dev)
+        if need_adj and 'adj_off' not in d:
+            self._build_adj_hash(dev)
         return d
+
+    def _build_adj_hash(self, dev) -> None:
+        """adj_off int64[V+1] / adj_hash int32[slots]: dw_adj_hash_offsets + dw_adj_hash_build
+        (rows of degree > 8 hashed; the fast node2vec walker's adjacency test in one probe)."""
+        import ctypes
+        d = self._dev
+        V = self.vocab_size
+        off = torch.empty(V + 1, dtype=torch.int64, device=dev)
+        nbytes = ctypes.c_size_t(0)
+        with torch.cuda.device(dev):
+            s = _native.stream(dev)
+            _native.call('dw_adj_hash_offsets', _native.ptr(d['row_ptr']), V, _native.ptr(off),
+                         None, ctypes.byref(nbytes), s)
+            tmp = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+            _native.call('dw_adj_hash_offsets', _native.ptr(d['row_ptr']), V, _native.ptr(off),
+                         _native.ptr(tmp), ctypes.byref(nbytes), s)
+            n_slots = int(off[V])          # synchronises: the table size
+            del tmp
+            tab = torch.empty(max(n_slots, 1), dtype=torch.int32, device=dev)
+            _native.call('dw_adj_hash_build', _native.ptr(d['row_ptr']),
+                         _native.ptr(d['col']) if self.nnz else None, V, _native.ptr(off),
+                         n_slots, _native.ptr(tab), _native.ptr(d['status']), s)
+        _native.check_status(d['status'], 'adjacency hash build')
+        d['adj_off'], d['adj_hash'] = off, tab
 
     def _sorted_copy(self, dev) -> torch.Tensor:
         d = self._dev

@@ -53,6 +53,7 @@ extern "C" {
 #define DW_METHOD_NODE2VEC   1   /* random_walk_generator.py:75-119                                  */
 
 #define DW_MAX_REJECTION_ROUNDS 65536
+#define DW_ADJ_HASH_MIN_DEG  8   /* rows of higher degree get an adjacency hash (dw_adj_hash_*)        */
 
 /* ---- library ---------------------------------------------------------------------------- */
 const char *dw_last_error_string(void);
@@ -71,6 +72,20 @@ int dw_csr_validate(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, 
  * Two-phase temp-storage protocol: call with temp==NULL to get *temp_bytes, then again. */
 int dw_csr_sort_copy(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
                      int32_t *col_sorted, void *temp, size_t *temp_bytes, void *stream);
+
+/* Per-row adjacency hash for the fast node2vec walker's test `prev_node in
+ * candidate_neighbors` (random_walk_generator.py:106-107): one probe of a 64-B bucket instead of
+ * a ceil(log8 deg)-load search of the sorted list. A row u of degree > DW_ADJ_HASH_MIN_DEG owns
+ * nb = ceil(4 deg / 48) buckets of 16 int32 slots (load <= 3/4) at adj_hash + adj_off[u]; rows
+ * of lower degree own none (their neighbour list itself is one load).
+ *   dw_adj_hash_offsets: adj_off int64[n_rows + 1] (exclusive scan of the per-row slot counts;
+ *     adj_off[n_rows] = total slots). Two-phase temp protocol as dw_csr_sort_copy.
+ *   dw_adj_hash_build: fills adj_hash int32[n_slots] (n_slots = adj_off[n_rows]). */
+int dw_adj_hash_offsets(const int64_t *row_ptr, int64_t n_rows, int64_t *adj_off, void *temp,
+                        size_t *temp_bytes, void *stream);
+int dw_adj_hash_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                      const int64_t *adj_off, int64_t n_slots, int32_t *adj_hash, int32_t *status,
+                      void *stream);
 
 /* Per-row Vose alias tables for first-order weighted sampling (the fast-mode replacement of
  * get_node_normalized_edge_weights + random.choices, random_walk_generator.py:50-53,68).
@@ -124,16 +139,25 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
 /* Fast walker (Philox4x32-10 keyed by (seed, walk_id0 + w, step, round/lane)); walks are a pure
  * function of (seed, global walk id), identical for any grid and any number of GPUs.
  *   DeepWalk: one lane per walker; uniform neighbour (unweighted) or alias table (weighted).
- *   node2vec: one wave (64 lanes) per walker; N(prev) staged sorted in LDS (HBM binary search
- *   for hubs); each lane proposes x ~ w(v,x), accepts with alpha(prev,x)/alpha_max using the
- *   reference's rule (x==prev -> 1/p, prev in N(x) -> 1/q, else 1; random_walk_generator.py:101-108);
- *   the lowest accepting lane (ballot) wins — an exact draw from the reference's step law.
- * prob_thr/alias: NULL for unweighted graphs. col_sorted: required for node2vec. */
+ *   node2vec: 8 lanes per walker; rejection rounds of 64 proposals x ~ w(v,x) (Philox counter
+ *   field j = 0..63), accepted with alpha(prev,x)/alpha_max under the reference's rule
+ *   (x==prev -> 1/p, prev in N(x) -> 1/q, else 1; random_walk_generator.py:101-108); the
+ *   lowest accepting j wins — an exact draw from the reference's step law. Proposals are
+ *   evaluated 8 at a time in j order; adjacency is tested only where the uniform leaves the
+ *   outcome open.
+ * prob_thr/alias: NULL for unweighted graphs. col_sorted: required for node2vec (8-ary search
+ * of the sorted list). dw_walk_fast_adj: the same walks (bit-identical), adjacency tested in
+ * the per-row hash instead (adj_off/adj_hash from dw_adj_hash_build; no col_sorted needed). */
 int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                  const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
                  const int32_t *starts, int64_t n_walks, int32_t walk_length, int32_t method,
                  double p, double q, uint64_t seed, uint64_t walk_id0, int32_t *out,
                  int32_t *status, void *stream);
+int dw_walk_fast_adj(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                     const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
+                     int64_t n_rows, const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                     int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
+                     int32_t *out, int32_t *status, void *stream);
 
 /* ---- SGNS (skip-gram negative sampling) ---------------------------------------------------------- */
 

@@ -112,15 +112,16 @@ def test_replay_hub_rows_vs_oracle(method, hip_device):
     assert (got == 1).sum() > 16
 
 
-@pytest.mark.parametrize('method,weighted', [('deepwalk', False), ('deepwalk', True),
-                                             ('node2vec', False), ('node2vec', True)])
-def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, hip_device):
+@pytest.mark.parametrize('method,weighted,adjacency', [
+    ('deepwalk', False, 'hash'), ('deepwalk', True, 'hash'), ('node2vec', False, 'hash'),
+    ('node2vec', True, 'hash'), ('node2vec', False, 'sorted'), ('node2vec', True, 'sorted')])
+def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, adjacency, hip_device):
     f = golden('walks_karate_deepwalk.npz')
     csr = _csr(f) if weighted else CSRGraph.from_arrays(f['row_ptr'], f['col'], None)
     L = 16
     starts = np.arange(1, 35, dtype=np.int32).repeat(3)
-    w = (Node2Vec(csr, L, p=0.25, q=4.0, rng='philox', seed=77) if method == 'node2vec'
-         else DeepWalk(csr, L, rng='philox', seed=77))
+    w = (Node2Vec(csr, L, p=0.25, q=4.0, rng='philox', seed=77, adjacency=adjacency)
+         if method == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=77))
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=1000).cpu().numpy()
     prob, alias = ph.alias_tables(csr.row_ptr, csr.weights) if weighted else (None, None)
     if weighted:
@@ -132,16 +133,56 @@ def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, hip_device):
     np.testing.assert_array_equal(got, exp)
 
 
-def test_fast_node2vec_hub_staging_vs_oracle(hip_device):
-    """deg(prev) > the LDS staging cap -> HBM binary search; same walks as the oracle."""
+@pytest.mark.parametrize('adjacency', ['hash', 'sorted'])
+def test_fast_node2vec_hub_staging_vs_oracle(adjacency, hip_device):
+    """A hub as prev (6-level 8-ary search / a 126-bucket hash row); same walks as the oracle."""
     csr = _hub_graph(n_leaves=1500, seed=3)
     L = 8
     starts = np.array([1] * 8 + [6] * 8, dtype=np.int32)   # vocab id 1 is the hub (node 0)
     assert csr.degree()[1] > 1024
-    w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5)
+    w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5, adjacency=adjacency)
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=0).cpu().numpy()
     exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, 'node2vec', 2.0, 0.5, seed=5, walk_id0=0)
     np.testing.assert_array_equal(got, exp)
+
+
+def _probe_ok(tab, nb, key):
+    """Host restatement of the kernel's probe (dw_walk.hip group_hash_contains)."""
+    b = ((key * 0x9E3779B1) & 0xFFFFFFFF) * nb >> 32
+    for _ in range(nb):
+        bk = tab[b * 16:(b + 1) * 16]
+        if (bk == key).any():
+            return True
+        if (bk < 0).any():
+            return False
+        b = (b + 1) % nb
+    return False
+
+
+@pytest.mark.parametrize('graph', ['rmat12', 'hub'])
+def test_adjacency_hash_tables(graph, hip_device):
+    """dw_adj_hash_offsets / _build: rows of degree > 8 hold exactly their neighbours in
+    ceil(4 deg / 48) buckets; every neighbour is found by the probe and non-neighbours are not."""
+    csr = (_csr(golden('walks_rmat12_node2vec_p0.25_q4.npz')) if graph == 'rmat12'
+           else _hub_graph(n_leaves=1500, seed=3))
+    d = csr.device_tensors(need_adj=True)
+    off = d['adj_off'].cpu().numpy()
+    tab = d['adj_hash'].cpu().numpy()
+    deg = np.diff(csr.row_ptr)
+    nb = np.where(deg > 8, (4 * deg + 47) // 48, 0)
+    np.testing.assert_array_equal(np.diff(off), 16 * nb)
+    assert off[0] == 0 and (deg > 8).any()
+    rng = np.random.default_rng(0)
+    for u in np.flatnonzero(deg > 8):
+        t = tab[off[u]:off[u + 1]]
+        nbrs = np.sort(csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]])
+        np.testing.assert_array_equal(np.sort(t[t >= 0]), nbrs)
+        assert (t >= 0).sum() <= 0.75 * t.size
+        for x in nbrs[:: max(1, len(nbrs) // 16)]:
+            assert _probe_ok(t, int(nb[u]), int(x))
+        others = np.setdiff1d(rng.integers(0, csr.vocab_size, 32), nbrs)
+        for x in others:
+            assert not _probe_ok(t, int(nb[u]), int(x))
 
 
 def test_fast_node2vec_statistics_vs_reference_law(hip_device):
@@ -189,6 +230,9 @@ def test_fast_walks_rmat20_properties(hip_device):
         out = w.walk_batch(starts[:m], walk_id0=0)
         again = w.walk_batch(starts[:m], walk_id0=0)
         assert torch.equal(out, again)
+        if method == 'node2vec':   # hashed adjacency (default) == sorted-list search, at scale
+            srt = Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1, adjacency='sorted')
+            assert torch.equal(out, srt.walk_batch(starts[:m], walk_id0=0))
         o = out.cpu().numpy()
         assert (o > 0).all()
         sample = o[:: max(1, m // 512)]
