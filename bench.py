@@ -136,12 +136,17 @@ def main():
                     help='owner mode: every rank generates the whole global batch of walks '
                          '(all; default for DeepWalk, whose walker is cheap) or its own B walks '
                          'and all-gathers them (gather; default for node2vec)')
-    ap.add_argument('--in-exchange', default=None, choices=['sharded', 'lazy'],
+    ap.add_argument('--in-exchange', default=None, choices=['sharded', 'lazy', 'auto'],
                     help='owner mode, in table: sharded = dense reduce-scatter / own-rows Adam / '
-                         'all-gather (OwnerTables; default at C3); lazy = only the rows the '
-                         'batch touched are all-reduced and updated, the others\' g = 0 Adam '
-                         'steps replayed exactly when next touched (OwnerLazyTables; default at '
-                         'C5, where the dense exchange is 2 x 17 GB per step)')
+                         'all-gather (OwnerTables); lazy = only the rows the batch touched are '
+                         'all-reduced and updated, the others\' g = 0 Adam steps replayed exactly '
+                         'when next touched (OwnerLazyTables; default at C5, where the dense '
+                         'exchange is 2 x 17 GB per step); auto = time --calib-steps of each on '
+                         'this job (max over ranks) before the warmup and keep the faster '
+                         '(default at C3 with N > 1: which one hides better behind the '
+                         'output-table phase depends on the xGMI / RCCL rate)')
+    ap.add_argument('--calib-steps', type=int, default=8,
+                    help='--in-exchange auto: timed steps per protocol')
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
@@ -153,7 +158,7 @@ def main():
     if args.owner_walks is None:
         args.owner_walks = 'gather' if args.method == 'node2vec' else 'all'
     if args.in_exchange is None:
-        args.in_exchange = 'lazy' if args.config == 'c5' else 'sharded'
+        args.in_exchange = 'lazy' if args.config == 'c5' else 'auto'
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -202,10 +207,18 @@ def main():
         raise SystemExit('owner mode needs the sorted path, d a multiple of 64 (<= 512) and '
                          '2R(1+K) <= 64; use --dist-mode replicated')
     W_eff = emulate or world            # ranks of the (possibly emulated) job
+    # auto (N > 1 only; one rank has no exchange to choose): both protocols are timed below
+    auto_in = owner and args.in_exchange == 'auto' and world > 1
+    if owner and args.in_exchange == 'auto' and not auto_in:
+        args.in_exchange = 'sharded'
     lazy = owner and args.in_exchange == 'lazy'
-    if owner:
-        tables = (OwnerLazyTables if lazy else OwnerTables)(
+
+    def owner_tables(lazy_mode: bool):
+        return (OwnerLazyTables if lazy_mode else OwnerTables)(
             V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
+
+    if owner:
+        tables = owner_tables(lazy)
     else:
         tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
                                overlap_in=not args.no_overlap_in,
@@ -397,6 +410,35 @@ def main():
             ev['sgns'].append((e[1], e[2]))
             ev['adam'].append((e[2], e[3]))
 
+    calib_ms = None
+    if auto_in:
+        # time each in-table protocol on this job (fresh tables, same init), keep the faster;
+        # every rank takes the same decision from the max-over-ranks times
+        calib_ms = {}
+        for mode in ('sharded', 'lazy'):
+            lazy = mode == 'lazy'
+            del tables
+            torch.cuda.empty_cache()
+            tables = owner_tables(lazy)
+            for _ in range(max(1, args.warmup)):
+                one_step(False)
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            a = time.perf_counter()
+            for _ in range(args.calib_steps):
+                one_step(False)
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - a], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            calib_ms[mode] = float(t) / args.calib_steps * 1e3
+        args.in_exchange = 'lazy' if calib_ms['lazy'] < calib_ms['sharded'] else 'sharded'
+        lazy = args.in_exchange == 'lazy'
+        del tables
+        torch.cuda.empty_cache()
+        tables = owner_tables(lazy)
+        log(rank, f'[bench] in-table exchange calibration (ms/step): {calib_ms} -> '
+                  f'{args.in_exchange}')
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize(dev)
@@ -526,6 +568,8 @@ def main():
                 f'in-table exchange overlapped'
                 + (f', out table in {tables.P} pieces pipelined' if pieces else '') + ')'),
         },
+        'in_exchange': args.in_exchange if owner else None,
+        'in_exchange_calibration_ms_per_step': calib_ms,
         'walks_per_s': walk_stats.get('deepwalk'),
         'walks_per_s_node2vec_p0.25_q4': walk_stats.get('node2vec'),
         'kernel_ms': kern_ms,
