@@ -194,7 +194,7 @@ def main():
     N = V - 1
     log(rank, f'[bench] R-MAT scale {args.scale}: {N} nodes, {csr.nnz // 2} edges '
               f'({time.time() - t0:.1f}s)')
-    csr.device_tensors(dev, need_sorted=True)
+    csr.device_tensors(dev)
     R, K, d, L, B = args.radius, args.neg, args.dim, args.walk_length, args.batch_walks
     if args.method == 'node2vec':
         walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)

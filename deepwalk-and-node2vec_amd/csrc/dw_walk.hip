@@ -267,6 +267,70 @@ __global__ void __launch_bounds__(256)
     for (; s < L; ++s) o[s] = -1;
 }
 
+// DeepWalk over the edge-inline CSR (dw_edges_inline_build): entry e of row u is the int4
+// {x, deg(x), row_ptr[x] (lo, hi)}, so the pick of the next node also yields its row — one
+// dependent load per step where the CSR walk needs two (row_ptr, then col). Same Philox draws
+// and picks as k_walk_deepwalk_fast: bit-identical walks.
+// DeepWalk, one lane per walker; the walk leaves in 16-B stores of 4 steps when L % 4 == 0.
+__global__ void __launch_bounds__(256)
+    k_walk_deepwalk_inline(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ edges,
+                           const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
+                           int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
+                           int32_t L, uint32_t k0, uint32_t k1, uint64_t walk_id0,
+                           int32_t *__restrict__ out, int32_t *status) {
+    const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (w >= n_walks) return;
+    const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
+    int32_t *o = out + w * (int64_t)L;
+    int32_t v = starts[w];
+    bool ok = v >= 0 && (int64_t)v < n_rows;
+    if (!ok) dw::status_or(status, DW_S_BAD_CSR);
+    int64_t a = ok ? row_ptr[v] : 0;
+    int64_t n = ok ? row_ptr[v + 1] - a : 0;
+    auto step = [&](int32_t s) -> int32_t {   // node at step s >= 1 (-1 once the walk aborted)
+        if (!ok) return -1;
+        if (n <= 0) {
+            dw::status_or(status, DW_S_ISOLATED_NODE);
+            ok = false;
+            return -1;
+        }
+        const dw::U4 r = dw::philox(dw::U4{static_cast<uint32_t>(wid),
+                                           static_cast<uint32_t>(wid >> 32),
+                                           static_cast<uint32_t>(s) << 8, dw::TAG_DEEPWALK},
+                                    k0, k1);
+        const int4 e = edges[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+        a = static_cast<int64_t>(static_cast<uint32_t>(e.z)) | (static_cast<int64_t>(e.w) << 32);
+        n = e.y;
+        return e.x;
+    };
+    if ((L & 3) == 0) {
+        int4 *o4 = reinterpret_cast<int4 *>(o);
+        for (int32_t s0 = 0; s0 < L; s0 += 4) {
+            int4 pk;
+            pk.x = s0 == 0 ? v : step(s0);
+            pk.y = step(s0 + 1);
+            pk.z = step(s0 + 2);
+            pk.w = step(s0 + 3);
+            o4[s0 >> 2] = pk;
+        }
+    } else {
+        o[0] = v;
+        for (int32_t s = 1; s < L; ++s) o[s] = step(s);
+    }
+}
+
+__global__ void k_edges_inline(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                               int64_t nnz, int4 *__restrict__ edges) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz; e += stride) {
+        const int32_t x = col[e];
+        const int64_t a = row_ptr[x];
+        edges[e] = int4{x, static_cast<int32_t>(row_ptr[x + 1] - a),
+                        static_cast<int32_t>(static_cast<uint32_t>(a)),
+                        static_cast<int32_t>(a >> 32)};
+    }
+}
+
 constexpr int N2V_WAVES = 4;     // waves per block
 // (Occupancy: the hashed variant compiles to 73 VGPRs, 6 waves/SIMD. Forcing 8 waves/SIMD
 // (amdgpu_waves_per_eu) spills to scratch and measured 16% slower at C3.)
@@ -495,7 +559,7 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
                            dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,
                            adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks,
                            walk_length, thr, k0, k1, walk_id0, out, status);
-    DW_LAUNCH_CHECK(HASH ? "dw_walk_fast_adj/node2vec" : "dw_walk_fast/node2vec");
+    DW_LAUNCH_CHECK(HASH ? "dw_walk_fast_indexed/node2vec" : "dw_walk_fast/node2vec");
     return DW_OK;
 }
 
@@ -565,25 +629,51 @@ int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_
                                   out, status, stream);
 }
 
-int dw_walk_fast_adj(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
-                     const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
-                     int64_t n_rows, const int32_t *starts, int64_t n_walks, int32_t walk_length,
-                     int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
-                     int32_t *out, int32_t *status, void *stream) {
-    if (method != DW_METHOD_NODE2VEC || n_walks == 0)   // DeepWalk never tests adjacency
-        return dw_walk_fast(row_ptr, col, nullptr, prob_thr, alias, n_rows, starts, n_walks,
-                            walk_length, method, p, q, seed, walk_id0, out, status, stream);
-    DW_REQUIRE(walk_length >= 1, "dw_walk_fast_adj: Minimum walk length is 1!");
-    DW_REQUIRE(walk_length < (1 << 24), "dw_walk_fast_adj: walk_length too large");
-    DW_REQUIRE(n_walks > 0 && n_rows >= 0, "dw_walk_fast_adj: negative size");
-    DW_REQUIRE(row_ptr && col && adj_off && starts && out && status,
-               "dw_walk_fast_adj: null pointer");
+int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *edges,
+                         const int64_t *adj_off, const int32_t *adj_hash,
+                         const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
+                         const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                         int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
+                         int32_t *out, int32_t *status, void *stream) {
+    DW_REQUIRE(walk_length >= 1 && walk_length < (1 << 24),
+               "dw_walk_fast_indexed: walk_length must be in [1, 2^24)");
+    DW_REQUIRE(method == DW_METHOD_DEEPWALK || method == DW_METHOD_NODE2VEC,
+               "dw_walk_fast_indexed: unknown method %d", method);
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_fast_indexed: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && starts && out && status, "dw_walk_fast_indexed: null pointer");
     DW_REQUIRE((prob_thr == nullptr) == (alias == nullptr),
-               "dw_walk_fast_adj: prob_thr and alias must be both set or both null");
+               "dw_walk_fast_indexed: prob_thr and alias must be both set or both null");
     const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    if (method == DW_METHOD_DEEPWALK) {
+        DW_REQUIRE(edges, "dw_walk_fast_indexed: DeepWalk needs edges (dw_edges_inline_build)");
+        const int64_t blocks = (n_walks + 255) / 256;
+        DW_REQUIRE(blocks < (int64_t(1) << 31), "dw_walk_fast_indexed: too many walks");
+        hipLaunchKernelGGL(k_walk_deepwalk_inline, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), row_ptr, reinterpret_cast<const int4 *>(edges),
+                           prob_thr, alias, n_rows, starts, n_walks, walk_length, k0, k1,
+                           walk_id0, out, status);
+        DW_LAUNCH_CHECK("dw_walk_fast_indexed/deepwalk");
+        return DW_OK;
+    }
+    DW_REQUIRE(col && adj_off && adj_hash,
+               "dw_walk_fast_indexed: node2vec needs col, adj_off and adj_hash");
     return launch_node2vec<true>(row_ptr, col, col, adj_off, adj_hash, prob_thr, alias, n_rows,
                                  starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
                                  status, stream);
+}
+
+int dw_edges_inline_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                          int32_t *edges, void *stream) {
+    DW_REQUIRE(n_rows >= 0 && nnz >= 0, "dw_edges_inline_build: negative size");
+    if (nnz == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && edges, "dw_edges_inline_build: null pointer");
+    int64_t blocks = (nnz + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_edges_inline, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       row_ptr, col, nnz, reinterpret_cast<int4 *>(edges));
+    DW_LAUNCH_CHECK("dw_edges_inline_build");
+    return DW_OK;
 }
 
 }  // extern "C"

@@ -188,9 +188,10 @@ class CSRGraph:
 
     # ------------------------------------------------------------------ device side
     def device_tensors(self, device=None, need_sorted: bool = False,
-                       need_alias: bool = False, need_adj: bool = False) -> Dict[str, torch.Tensor]:
-        """Copy the CSR to HBM once (and derive col_sorted / alias tables / the per-row
-        adjacency hash on the device)."""
+                       need_alias: bool = False, need_edges: bool = False,
+                       need_adj: bool = False) -> Dict[str, torch.Tensor]:
+        """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
+        the per-row adjacency hash on the device)."""
         dev = _native.require_device(device)
         if self._dev_device != dev:
             if self.col is None and 'col' in self._dev:   # device-built: keep a host copy
@@ -213,9 +214,21 @@ class CSRGraph:
             d['col_sorted'] = self._sorted_copy(dev)
         if need_alias and self.weights is not None and 'prob_thr' not in d:
             self._build_alias(dev)
+        if need_edges and 'edges' not in d:
+            self._build_edges(dev)
         if need_adj and 'adj_off' not in d:
             self._build_adj_hash(dev)
         return d
+
+    def _build_edges(self, dev) -> None:
+        """edges int32[nnz, 4] (dw_edges_inline_build): {x, deg(x), row_ptr[x] lo, hi}."""
+        d = self._dev
+        e = torch.empty((max(self.nnz, 1), 4), dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            _native.call('dw_edges_inline_build', _native.ptr(d['row_ptr']),
+                         _native.ptr(d['col']) if self.nnz else None, self.vocab_size, self.nnz,
+                         _native.ptr(e), _native.stream(dev))
+        d['edges'] = e
 
     def _build_adj_hash(self, dev) -> None:
         """adj_off int64[V+1] / adj_hash int32[slots]: dw_adj_hash_offsets + dw_adj_hash_build

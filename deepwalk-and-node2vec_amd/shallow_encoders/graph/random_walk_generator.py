@@ -7,9 +7,11 @@ Two sampling modes, one kernel family each (include/dw_hip.h):
   (random_walk_generator.py:68,113). The doubles are drawn on the host (rng.draw_uniforms) and
   the replay kernel ``dw_walk_replay`` reproduces CPython's fp64 arithmetic, so
   ``random.seed(s)`` yields the reference's walks bit for bit.
-* ``rng='philox'``: ``dw_walk_fast`` / ``dw_walk_fast_adj`` (node2vec adjacency tests in a
-  per-row hash), Philox4x32-10 keyed by (seed, global walk id); the walk law is the reference's
-  (including its inverted node2vec q rule), the stream is not.
+* ``rng='philox'``: ``dw_walk_fast_indexed`` (DeepWalk over the edge-inline CSR, node2vec
+  adjacency tests in a per-row hash; the default) or ``dw_walk_fast`` (plain CSR,
+  ``layout='csr'``), Philox4x32-10
+  keyed by (seed, global walk id); the walk law is the reference's (including its inverted
+  node2vec q rule), the stream is not.
 
 ``walk(node) -> str`` keeps the reference signature; ``walk_batch`` is the batched device API
 (int32 vocabulary ids, shape [n_walks, length]) that feeds the fused SGNS kernel.
@@ -44,7 +46,7 @@ class RandomWalk(ABC):
     METHOD = _native.DW_METHOD_DEEPWALK
 
     def __init__(self, graph, length: int, rng: str = 'python', seed: int = 0, device=None,
-                 adjacency: str = 'hash'):
+                 layout: str = 'indexed'):
         """
         Args:
             graph: ``networkx.Graph`` (or a prebuilt ``CSRGraph`` for large synthetic graphs)
@@ -52,16 +54,17 @@ class RandomWalk(ABC):
             rng: 'python' (bit-exact replay of the global ``random`` stream) or 'philox'
             seed: Philox key (rng='philox')
             device: HIP device (default: current)
-            adjacency: node2vec with rng='philox' — how ``prev in N(x)`` is tested: 'hash'
-                (per-row adjacency hash, dw_walk_fast_adj) or 'sorted' (search of the sorted
-                lists, dw_walk_fast). Both give the same walks bit for bit.
+            layout: rng='philox' — 'indexed' (default, dw_walk_fast_indexed: DeepWalk over the
+                edge-inline CSR, one dependent load per step; node2vec adjacency tests in the
+                per-row hash) or 'csr' (dw_walk_fast: row_ptr / col, node2vec tests by search of
+                the sorted lists). Both give the same walks bit for bit.
         """
         assert length >= 1, 'Minimum walk length is 1!'
         if rng not in ('python', 'philox'):
             raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
-        if adjacency not in ('hash', 'sorted'):
-            raise ValueError(f'unknown adjacency "{adjacency}" (expected "hash" or "sorted")')
-        self._adjacency = adjacency
+        if layout not in ('indexed', 'csr'):
+            raise ValueError(f'unknown layout "{layout}" (expected "indexed" or "csr")')
+        self._layout = layout
         self._graph = graph
         self._length = length
         self._rng = rng
@@ -121,11 +124,13 @@ class RandomWalk(ABC):
         n = int(starts.numel())
         L = self._length
         n2v = self.METHOD == _native.DW_METHOD_NODE2VEC
-        # replay: adjacency by search of the sorted lists; philox: by the per-row hash (the same
-        # walks as dw_walk_fast over col_sorted, bit for bit; adjacency='sorted' selects that)
-        hashed = n2v and self._rng == 'philox' and self._adjacency == 'hash'
-        d = self._csr.device_tensors(dev, need_sorted=n2v and not hashed,
-                                     need_alias=self._rng == 'philox', need_adj=hashed)
+        # replay: the CSR, adjacency by search of the sorted lists; philox: DeepWalk over the
+        # edge-inline CSR, node2vec with the per-row adjacency hash (the same walks as
+        # dw_walk_fast, bit for bit; layout='csr' selects that one)
+        indexed = self._rng == 'philox' and self._layout == 'indexed'
+        d = self._csr.device_tensors(dev, need_sorted=n2v and not indexed,
+                                     need_alias=self._rng == 'philox',
+                                     need_edges=indexed and not n2v, need_adj=indexed and n2v)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -146,10 +151,11 @@ class RandomWalk(ABC):
                              _native.ptr(out), _native.ptr(status), s)
             else:
                 wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
-                if hashed:
-                    _native.call('dw_walk_fast_adj', _native.ptr(d['row_ptr']),
-                                 _native.ptr(d['col']), _native.ptr(d['adj_off']),
-                                 _native.ptr(d['adj_hash']), _native.ptr(d.get('prob_thr')),
+                if indexed:
+                    _native.call('dw_walk_fast_indexed', _native.ptr(d['row_ptr']),
+                                 _native.ptr(d['col']), _native.ptr(d.get('edges')),
+                                 _native.ptr(d.get('adj_off')), _native.ptr(d.get('adj_hash')),
+                                 _native.ptr(d.get('prob_thr')),
                                  _native.ptr(d.get('alias')), self._csr.vocab_size,
                                  _native.ptr(starts), n, L, self.METHOD, float(p), float(q),
                                  self._seed & 0xFFFFFFFFFFFFFFFF, wid0, _native.ptr(out),

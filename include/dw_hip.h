@@ -146,18 +146,27 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
  *   evaluated 8 at a time in j order; adjacency is tested only where the uniform leaves the
  *   outcome open.
  * prob_thr/alias: NULL for unweighted graphs. col_sorted: required for node2vec (8-ary search
- * of the sorted list). dw_walk_fast_adj: the same walks (bit-identical), adjacency tested in
- * the per-row hash instead (adj_off/adj_hash from dw_adj_hash_build; no col_sorted needed). */
+ * of the sorted list). dw_walk_fast_indexed: the same walks (bit-identical) over derived
+ * indexes — DeepWalk over the edge-inline CSR `edges` (dw_edges_inline_build; one dependent
+ * load per step, walks stored 4 steps per 16-B store), node2vec with its adjacency tests in the
+ * per-row hash (adj_off/adj_hash from dw_adj_hash_build; `col` for rows of degree <= 8). */
 int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                  const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
                  const int32_t *starts, int64_t n_walks, int32_t walk_length, int32_t method,
                  double p, double q, uint64_t seed, uint64_t walk_id0, int32_t *out,
                  int32_t *status, void *stream);
-int dw_walk_fast_adj(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
-                     const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
-                     int64_t n_rows, const int32_t *starts, int64_t n_walks, int32_t walk_length,
-                     int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
-                     int32_t *out, int32_t *status, void *stream);
+int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *edges,
+                         const int64_t *adj_off, const int32_t *adj_hash,
+                         const uint32_t *prob_thr, const int32_t *alias, int64_t n_rows,
+                         const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                         int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
+                         int32_t *out, int32_t *status, void *stream);
+
+/* Edge-inline CSR for DeepWalk in dw_walk_fast_indexed: edges int32[nnz][4], entry e of row u =
+ * {x = col[e], deg(x), row_ptr[x] low 32 bits, row_ptr[x] high 32 bits}. The pick of the next
+ * node then also yields its row: one dependent load per walk step instead of two. */
+int dw_edges_inline_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
+                          int32_t *edges, void *stream);
 
 /* ---- SGNS (skip-gram negative sampling) ---------------------------------------------------------- */
 

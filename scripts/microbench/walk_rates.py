@@ -29,16 +29,20 @@ def main():
     csr.device_tensors(dev, need_sorted=True)
     N = csr.vocab_size - 1
     t0 = time.perf_counter()
-    csr.device_tensors(dev, need_adj=True)
+    csr.device_tensors(dev, need_edges=True, need_adj=True)
     torch.cuda.synchronize()
-    print(f'adjacency hash built in {time.perf_counter() - t0:.3f} s '
-          f'({csr.device_tensors(dev)["adj_hash"].numel() * 4 / 2**20:.0f} MiB)', flush=True)
+    dd = csr.device_tensors(dev)
+    print(f'edge-inline CSR + adjacency hash built in {time.perf_counter() - t0:.3f} s '
+          f'({dd["edges"].numel() * 4 / 2**20:.0f} + {dd["adj_hash"].numel() * 4 / 2**20:.0f} MiB)',
+          flush=True)
     ref = {}
-    for name, mk in (('deepwalk', lambda: DeepWalk(csr, args.L, rng='philox', seed=7, device=dev)),
-                     ('n2v-hash', lambda: Node2Vec(csr, args.L, p=0.25, q=4.0, rng='philox',
-                                                   seed=7, device=dev, adjacency='hash')),
-                     ('n2v-sort', lambda: Node2Vec(csr, args.L, p=0.25, q=4.0, rng='philox',
-                                                   seed=7, device=dev, adjacency='sorted'))):
+    for name, mk in (('dw-indexed', lambda: DeepWalk(csr, args.L, rng='philox', seed=7, device=dev)),
+                     ('dw-csr', lambda: DeepWalk(csr, args.L, rng='philox', seed=7, device=dev,
+                                                 layout='csr')),
+                     ('n2v-indexed', lambda: Node2Vec(csr, args.L, p=0.25, q=4.0, rng='philox',
+                                                     seed=7, device=dev)),
+                     ('n2v-csr', lambda: Node2Vec(csr, args.L, p=0.25, q=4.0, rng='philox',
+                                                  seed=7, device=dev, layout='csr'))):
         w = mk()
         for n in (int(c) for c in args.counts.split(',')):
             st = (torch.arange(n, dtype=torch.int64, device=dev) % N + 1).to(torch.int32)
@@ -52,16 +56,14 @@ def main():
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - a
                 best = dt if best is None else min(best, dt)
-            if name.startswith('n2v'):   # both adjacency tests give the same walks
-                key = n
-                if key in ref:
-                    assert torch.equal(ref[key], out), 'hash and sorted walks differ'
-                else:
-                    ref[key] = out.clone()
-            print(f'{name:9s} n={n:8d}  {best * 1e3:8.2f} ms  {n / best:.3e} walks/s  '
+            key = (name.split('-')[0], n)   # both layouts give the same walks
+            if key in ref:
+                assert torch.equal(ref[key], out), 'inline and csr walks differ'
+            else:
+                ref[key] = out.clone()
+            print(f'{name:11s} n={n:8d}  {best * 1e3:8.2f} ms  {n / best:.3e} walks/s  '
                   f'{n * (args.L - 1) / best:.3e} steps/s', flush=True)
             del out
-        ref = {} if name == 'deepwalk' else ref
 
 
 if __name__ == '__main__':

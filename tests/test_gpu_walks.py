@@ -112,15 +112,17 @@ def test_replay_hub_rows_vs_oracle(method, hip_device):
     assert (got == 1).sum() > 16
 
 
-@pytest.mark.parametrize('method,weighted,adjacency', [
-    ('deepwalk', False, 'hash'), ('deepwalk', True, 'hash'), ('node2vec', False, 'hash'),
-    ('node2vec', True, 'hash'), ('node2vec', False, 'sorted'), ('node2vec', True, 'sorted')])
-def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, adjacency, hip_device):
+@pytest.mark.parametrize('layout,L', [('indexed', 16), ('csr', 16), ('indexed', 1),
+                                      ('indexed', 5), ('indexed', 11)])
+@pytest.mark.parametrize('method,weighted', [('deepwalk', False), ('deepwalk', True),
+                                             ('node2vec', False), ('node2vec', True)])
+def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, layout, L, hip_device):
+    """Fast walkers vs the Philox oracle, both layouts; the inline DeepWalk walker's packed
+    stores at walk lengths that are not multiples of 4."""
     f = golden('walks_karate_deepwalk.npz')
     csr = _csr(f) if weighted else CSRGraph.from_arrays(f['row_ptr'], f['col'], None)
-    L = 16
     starts = np.arange(1, 35, dtype=np.int32).repeat(3)
-    w = (Node2Vec(csr, L, p=0.25, q=4.0, rng='philox', seed=77, adjacency=adjacency)
+    w = (Node2Vec(csr, L, p=0.25, q=4.0, rng='philox', seed=77, layout=layout)
          if method == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=77))
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=1000).cpu().numpy()
     prob, alias = ph.alias_tables(csr.row_ptr, csr.weights) if weighted else (None, None)
@@ -133,14 +135,14 @@ def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, adjacency, hip
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize('adjacency', ['hash', 'sorted'])
-def test_fast_node2vec_hub_staging_vs_oracle(adjacency, hip_device):
+@pytest.mark.parametrize('layout', ['indexed', 'csr'])
+def test_fast_node2vec_hub_staging_vs_oracle(layout, hip_device):
     """A hub as prev (6-level 8-ary search / a 126-bucket hash row); same walks as the oracle."""
     csr = _hub_graph(n_leaves=1500, seed=3)
     L = 8
     starts = np.array([1] * 8 + [6] * 8, dtype=np.int32)   # vocab id 1 is the hub (node 0)
     assert csr.degree()[1] > 1024
-    w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5, adjacency=adjacency)
+    w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5, layout=layout)
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=0).cpu().numpy()
     exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, 'node2vec', 2.0, 0.5, seed=5, walk_id0=0)
     np.testing.assert_array_equal(got, exp)
@@ -165,13 +167,19 @@ def test_adjacency_hash_tables(graph, hip_device):
     ceil(4 deg / 48) buckets; every neighbour is found by the probe and non-neighbours are not."""
     csr = (_csr(golden('walks_rmat12_node2vec_p0.25_q4.npz')) if graph == 'rmat12'
            else _hub_graph(n_leaves=1500, seed=3))
-    d = csr.device_tensors(need_adj=True)
+    d = csr.device_tensors(need_adj=True, need_edges=True)
     off = d['adj_off'].cpu().numpy()
     tab = d['adj_hash'].cpu().numpy()
     deg = np.diff(csr.row_ptr)
     nb = np.where(deg > 8, (4 * deg + 47) // 48, 0)
     np.testing.assert_array_equal(np.diff(off), 16 * nb)
     assert off[0] == 0 and (deg > 8).any()
+    # edge-inline entries: {x, deg(x), row_ptr[x] as two int32 halves}
+    e = d['edges'].cpu().numpy()
+    x = csr.col
+    np.testing.assert_array_equal(e[:, 0], x)
+    np.testing.assert_array_equal(e[:, 1], deg[x])
+    np.testing.assert_array_equal(e[:, 2:4].copy().view(np.int64)[:, 0], csr.row_ptr[x])
     rng = np.random.default_rng(0)
     for u in np.flatnonzero(deg > 8):
         t = tab[off[u]:off[u + 1]]
@@ -230,9 +238,10 @@ def test_fast_walks_rmat20_properties(hip_device):
         out = w.walk_batch(starts[:m], walk_id0=0)
         again = w.walk_batch(starts[:m], walk_id0=0)
         assert torch.equal(out, again)
-        if method == 'node2vec':   # hashed adjacency (default) == sorted-list search, at scale
-            srt = Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1, adjacency='sorted')
-            assert torch.equal(out, srt.walk_batch(starts[:m], walk_id0=0))
+        # indexed layout (default) == plain CSR + sorted search, at scale
+        plain = (Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1, layout='csr')
+                 if method == 'node2vec' else DeepWalk(csr, 80, rng='philox', seed=1, layout='csr'))
+        assert torch.equal(out, plain.walk_batch(starts[:m], walk_id0=0))
         o = out.cpu().numpy()
         assert (o > 0).all()
         sample = o[:: max(1, m // 512)]
