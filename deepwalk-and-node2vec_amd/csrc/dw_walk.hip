@@ -380,7 +380,11 @@ __device__ __forceinline__ bool group_hash_contains(const int32_t *__restrict__ 
     for (uint32_t t = 0; t < nb; ++t) {
         const int32_t *slot = tab + (int64_t)b * 16 + gl * PER;
         bool hit = false, free_slot = false;
-        if constexpr (PER == 2) {
+        if constexpr (PER == 4) {
+            const int4 e = *reinterpret_cast<const int4 *>(slot);
+            hit = e.x == key || e.y == key || e.z == key || e.w == key;
+            free_slot = e.x < 0 || e.y < 0 || e.z < 0 || e.w < 0;
+        } else if constexpr (PER == 2) {
             const int2 e = *reinterpret_cast<const int2 *>(slot);
             hit = e.x == key || e.y == key;
             free_slot = e.x < 0 || e.y < 0;
@@ -394,6 +398,16 @@ __device__ __forceinline__ bool group_hash_contains(const int32_t *__restrict__ 
         if (++b == nb) b = 0;
     }
     return false;
+}
+
+// Membership in a short UNSORTED list (a row without an adjacency hash, degree <= 8): the group
+// reads it N2V_G entries at a time.
+template <int N2V_G>
+__device__ __forceinline__ bool small_contains(const int32_t *__restrict__ list, int64_t n,
+                                               int32_t key, int gl, int q) {
+    bool hit = false;
+    for (int64_t t = gl; t < n; t += N2V_G) hit = hit || list[t] == key;
+    return group_ballot<N2V_G>(hit, q) != 0u;
 }
 
 // N2V_G lanes per walker (8 by default: 8 walkers per wave — the walk is latency-bound, so
@@ -489,7 +503,8 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                             if (HASH && pnb > 0)
                                 adj = group_hash_contains<N2V_G>(adj_hash + ph, pnb, xl, gl, q);
                             else
-                                adj = group_contains<N2V_G>(nbr + pa, pn, xl, gl, q);
+                                adj = HASH ? small_contains<N2V_G>(nbr + pa, pn, xl, gl, q)
+                                           : group_contains<N2V_G>(nbr + pa, pn, xl, gl, q);
                             if (adj == adj_wins) {
                                 win = l;
                                 break;
@@ -529,6 +544,19 @@ inline uint32_t accept_threshold(double alpha, double alpha_max) {
     return static_cast<uint32_t>(t);
 }
 
+// Walkers of k_walk_node2vec_fast<G> the device keeps resident at once.
+inline int64_t node2vec_capacity(const void *kern, int g) {
+    int dev = 0, n_cu = 0, bpc = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+        n_cu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, N2V_WAVES * WAVE, 0) !=
+            hipSuccess || bpc <= 0)
+        bpc = 6;
+    return (int64_t)bpc * n_cu * N2V_WAVES * (WAVE / g);
+}
+
 template <bool HASH>
 int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *nbr,
                     const int64_t *adj_off, const int32_t *adj_hash, const uint32_t *prob_thr,
@@ -541,24 +569,37 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
     if (ip > amax) amax = ip;
     if (iq > amax) amax = iq;
     N2VThr thr{accept_threshold(ip, amax), accept_threshold(iq, amax), accept_threshold(1.0, amax)};
-    static const int group = [] {  // lanes per walker (tuning knob DW_N2V_GROUP = 8 | 16)
+    // Lanes per walker G (4, 8 or 16; the walks do not depend on it): the walker is
+    // latency-bound, so a batch that fits on the chip at 16 lanes per walker (fewer blocks of
+    // proposals per step) runs at 16, one that fits at 8 at 8, a larger one at 4 (the most
+    // walkers in flight). Measured at C3, 1M walks: G=4 116M, G=8 101M, G=16 79M walks/s;
+    // 8,192 walks: 17M / 27M / 32M. DW_N2V_GROUP=4|8|16 forces a size.
+    static const int forced = [] {
         const char *e = getenv("DW_N2V_GROUP");
-        const int g = e ? atoi(e) : 8;
-        return (g == 8 || g == 16) ? g : 8;
+        const int g = e ? atoi(e) : 0;
+        return (g == 4 || g == 8 || g == 16) ? g : 0;
     }();
+    // resident walkers at 16 and 8 lanes (occupancy query once per process: one GPU model)
+    static const int64_t cap16 = node2vec_capacity(
+        reinterpret_cast<const void *>(&k_walk_node2vec_fast<16, HASH>), 16);
+    static const int64_t cap8 = node2vec_capacity(
+        reinterpret_cast<const void *>(&k_walk_node2vec_fast<8, HASH>), 8);
+    const int group = forced ? forced : n_walks <= cap16 ? 16 : n_walks <= cap8 ? 8 : 4;
     const int64_t per_block = N2V_WAVES * (WAVE / group);
     int64_t blocks = (n_walks + per_block - 1) / per_block;
     if (blocks > 8192) blocks = 8192;
-    if (group == 8)
-        hipLaunchKernelGGL((k_walk_node2vec_fast<8, HASH>), dim3((unsigned)blocks),
-                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,
-                           adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks,
-                           walk_length, thr, k0, k1, walk_id0, out, status);
+#define DW_N2V_LAUNCH(G)                                                                       \
+    hipLaunchKernelGGL((k_walk_node2vec_fast<G, HASH>), dim3((unsigned)blocks),                \
+                       dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,    \
+                       adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks, walk_length, \
+                       thr, k0, k1, walk_id0, out, status)
+    if (group == 4)
+        DW_N2V_LAUNCH(4);
+    else if (group == 8)
+        DW_N2V_LAUNCH(8);
     else
-        hipLaunchKernelGGL((k_walk_node2vec_fast<16, HASH>), dim3((unsigned)blocks),
-                           dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,
-                           adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks,
-                           walk_length, thr, k0, k1, walk_id0, out, status);
+        DW_N2V_LAUNCH(16);
+#undef DW_N2V_LAUNCH
     DW_LAUNCH_CHECK(HASH ? "dw_walk_fast_indexed/node2vec" : "dw_walk_fast/node2vec");
     return DW_OK;
 }

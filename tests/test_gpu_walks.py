@@ -273,3 +273,19 @@ def test_device_rmat_csr_equals_host_build(hip_device, scale, n_edges):
         edges, n_patched = rmat_edges(scale, n_edges, 0)
         assert len(edges) == 10_013_665 and n_patched == 475_918
         assert host.nnz == 2 * 10_013_665
+
+
+def test_node2vec_lane_groups_give_identical_walks(hip_device):
+    """The node2vec walker picks 16, 8 or 4 lanes per walker from the batch size (resident
+    capacity); walks are pure functions of the walk id, so a walk is the same in every batch."""
+    csr = rmat_graph(16, 500_000, 0)
+    n_big = 300_000
+    starts = (torch.arange(n_big, dtype=torch.int64) % (csr.vocab_size - 1) + 1).to(torch.int32)
+    for layout in ('indexed', 'csr'):
+        w = Node2Vec(csr, 20, p=0.25, q=4.0, rng='philox', seed=3, layout=layout)
+        big = w.walk_batch(starts, walk_id0=0)               # 4 lanes per walker
+        mid = w.walk_batch(starts[:40_000], walk_id0=0)      # 8 (or 16) lanes
+        small = w.walk_batch(starts[:4096], walk_id0=0)      # 16 lanes
+        assert torch.equal(big[:40_000], mid)
+        assert torch.equal(big[:4096], small)
+        assert (big > 0).all()
