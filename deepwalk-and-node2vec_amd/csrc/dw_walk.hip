@@ -287,6 +287,12 @@ __global__ void __launch_bounds__(256)
     if (!ok) dw::status_or(status, DW_S_BAD_CSR);
     int64_t a = ok ? row_ptr[v] : 0;
     int64_t n = ok ? row_ptr[v + 1] - a : 0;
+    auto draw = [&](int32_t s) {
+        return dw::philox(dw::U4{static_cast<uint32_t>(wid), static_cast<uint32_t>(wid >> 32),
+                                 static_cast<uint32_t>(s) << 8, dw::TAG_DEEPWALK},
+                          k0, k1);
+    };
+    dw::U4 r = draw(1);   // the draw of the coming step: computed while the previous load flies
     auto step = [&](int32_t s) -> int32_t {   // node at step s >= 1 (-1 once the walk aborted)
         if (!ok) return -1;
         if (n <= 0) {
@@ -294,11 +300,8 @@ __global__ void __launch_bounds__(256)
             ok = false;
             return -1;
         }
-        const dw::U4 r = dw::philox(dw::U4{static_cast<uint32_t>(wid),
-                                           static_cast<uint32_t>(wid >> 32),
-                                           static_cast<uint32_t>(s) << 8, dw::TAG_DEEPWALK},
-                                    k0, k1);
         const int4 e = edges[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+        r = draw(s + 1);   // independent of e: overlaps the load's latency
         a = static_cast<int64_t>(static_cast<uint32_t>(e.z)) | (static_cast<int64_t>(e.w) << 32);
         n = e.y;
         return e.x;
