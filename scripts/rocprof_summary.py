@@ -45,7 +45,8 @@ def kernel_class(name: str):
         # the SGNS records sort: u32 row keys, u64 {coef, centre} values; the CSR copy sort
         # (dw_csr_sort_copy, u64 keys only) runs once at setup
         return 'sgns_sort' if 'unsigned int, unsigned long' in name else 'csr_sort'
-    for k in ('k_adam', 'k_scale', 'k_walk_deepwalk_fast', 'k_walk_node2vec_fast',
+    for k in ('k_adam', 'k_scale', 'k_walk_deepwalk_fast', 'k_walk_deepwalk_inline',
+              'k_walk_node2vec_fast',
               'k_walk_replay', 'k_logits'):
         if k in name:
             return k
