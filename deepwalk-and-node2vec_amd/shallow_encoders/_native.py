@@ -49,6 +49,7 @@ SIGNATURES = {
     'dw_last_error_string': (ctypes.c_char_p, []),
     'dw_abi_version': (ctypes.c_int, []),
     'dw_device_sync': (ctypes.c_int, [_p]),
+    'dw_host_shuffle': (ctypes.c_int, [_p, _p, _i64]),
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
     'dw_adj_hash_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),

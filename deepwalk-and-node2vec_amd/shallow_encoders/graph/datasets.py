@@ -9,7 +9,6 @@ continues the SAME iteration state and, in rng='python' mode, consumes the globa
 stream exactly as the same number of ``__next__`` calls would.
 """
 import os
-import random
 from typing import Dict, Optional
 
 import numpy as np
@@ -20,6 +19,7 @@ from shallow_encoders import _native
 from shallow_encoders.common.path import ASSETS_PATH
 from shallow_encoders.graph.csr import CSRGraph
 from shallow_encoders.graph.random_walk_generator import RandomWalk, random_walk_factory
+from shallow_encoders.graph.rng import shuffled_range
 from shallow_encoders.word2vec.dataloader.registry import register_dataset
 
 
@@ -57,11 +57,9 @@ class RandomWalkDataset:
         self._labels = labels
         self._features = features
         # the reference shuffles the node list in place; shuffling an index permutation with
-        # the same generator consumes the same draws and yields the same order
-        perm = list(range(len(base_nodes)))
-        random.shuffle(perm)
+        # the same generator consumes the same draws and yields the same order (native loop)
         self._base_nodes = base_nodes
-        self._perm = np.asarray(perm, dtype=np.int64)   # epoch order, as base_nodes indices
+        self._perm = shuffled_range(len(base_nodes))   # epoch order, as base_nodes indices
 
         method_params = {} if method_params is None else method_params
         self._walk_generator: RandomWalk = random_walk_factory(
@@ -116,9 +114,7 @@ class RandomWalkDataset:
     def _reshuffle(self) -> None:
         # the reference re-shuffles its node list in place (same draws as shuffling indices);
         # names are looked up through the permutation instead of rebuilding a list of them
-        perm = list(range(len(self._base_nodes)))
-        random.shuffle(perm)
-        p = np.asarray(perm, dtype=np.int64)
+        p = shuffled_range(len(self._base_nodes))
         self._perm = self._perm[p]
         self._node_ids = self._node_ids[p]
         self._dev_starts = None

@@ -40,3 +40,23 @@ def skip_uniforms(n: int, rng: random.Random = None) -> None:
         m = min(n, _CHUNK)
         draw_uniforms(m, rng)
         n -= m
+
+
+def shuffled_range(n: int, rng: random.Random = None) -> np.ndarray:
+    """``x = list(range(n)); rng.shuffle(x)`` as an int64 array, bit for bit, and ``rng`` left
+    where that shuffle leaves it (default: the global instance). The loop runs in native code
+    (dw_host_shuffle: CPython's MT19937 + ``_randbelow`` + ``shuffle``); ~0.5 s -> ~10 ms for 1M
+    nodes."""
+    rng = random._inst if rng is None else rng  # noqa: SLF001
+    n = int(n)
+    if n < 4096 or type(rng) is not random.Random:   # small, or a subclass with its own draws
+        x = list(range(n))
+        rng.shuffle(x)
+        return np.asarray(x, dtype=np.int64)
+    from shallow_encoders import _native
+    version, internal, gauss = rng.getstate()
+    state = np.asarray(internal, dtype=np.uint32)          # 624 words + index
+    perm = np.empty(n, dtype=np.int64)
+    _native.call('dw_host_shuffle', state.ctypes.data, perm.ctypes.data, n)
+    rng.setstate((version, tuple(int(v) for v in state), gauss))
+    return perm

@@ -60,6 +60,12 @@ const char *dw_last_error_string(void);
 int dw_abi_version(void);               /* bumps on any signature change */
 int dw_device_sync(void *stream);       /* hipStreamSynchronize(stream); used by the host mirror */
 
+/* Host-side (no device work): CPython 3.10 random.shuffle over range(n), bit for bit — the
+ * reference's start-node shuffle (datasets.py:45,86-88) in native code. mt_state: the 625 words
+ * of random.getstate()[1] (624-word MT19937 state + index), advanced in place exactly as
+ * Python's shuffle would; perm: int64[n] out. */
+int dw_host_shuffle(uint32_t *mt_state, int64_t *perm, int64_t n);
+
 /* ---- graph ------------------------------------------------------------------------------- */
 
 /* Validate a CSR on the device: row_ptr[0]==0, monotone, row_ptr[n_rows]==nnz, 0<=col<n_rows.

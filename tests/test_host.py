@@ -277,3 +277,22 @@ def test_device_noise_oracle_is_uniform():
     counts = np.bincount(nz.ravel(), minlength=7)
     from scipy.stats import chisquare
     assert chisquare(counts).pvalue > 1e-3
+
+
+@pytest.mark.parametrize('n,seed', [(4096, 0), (65_537, 1), (131_072, 2), (1_000_003, 3)])
+def test_native_shuffle_matches_cpython(n, seed):
+    """dw_host_shuffle (the start-node shuffle in native code) == random.shuffle bit for bit, and
+    the global stream continues where Python's own shuffle leaves it."""
+    import random
+    from shallow_encoders.graph.rng import shuffled_range
+    random.seed(seed)
+    random.random()                       # an arbitrary position inside the 624-word block
+    ref = list(range(n))
+    random.shuffle(ref)
+    after_ref = [random.random() for _ in range(5)]
+    random.seed(seed)
+    random.random()
+    got = shuffled_range(n)
+    after_got = [random.random() for _ in range(5)]
+    assert np.array_equal(got, np.asarray(ref, dtype=np.int64))
+    assert after_got == after_ref
