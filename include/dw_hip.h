@@ -170,7 +170,9 @@ int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32
 
 /* Edge-inline CSR for DeepWalk in dw_walk_fast_indexed: edges int32[nnz][4], entry e of row u =
  * {x = col[e], deg(x), row_ptr[x] low 32 bits, row_ptr[x] high 32 bits}. The pick of the next
- * node then also yields its row: one dependent load per walk step instead of two. */
+ * node then also yields its row: one dependent load per walk step instead of two — the
+ * `get_node_neighbors` + `random.choices` step of DeepWalk.walk (random_walk_generator.py:41-42,
+ * 61-72) as one 16-B read. */
 int dw_edges_inline_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
                           int32_t *edges, void *stream);
 
