@@ -200,7 +200,7 @@ def main():
         walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
-    emulate = args.emulate_world if (world == 1 and args.emulate_world > 1) else 0
+    emulate = args.emulate_world if (world == 1 and args.emulate_world >= 1) else 0
     owner = emulate > 0 or (world > 1 and args.dist_mode == 'owner')
     if owner and not (args.scatter == 'sorted' and d % 64 == 0 and d <= 512
                       and 2 * R * (1 + K) <= 64):
