@@ -153,14 +153,24 @@ struct SgnsArgs {
 #ifndef DW_NOISE_ROUNDS
 #define DW_NOISE_ROUNDS 10  // (timing experiments only: any other value changes the stream)
 #endif
+// Device negatives (noise == NULL): centre b's negative n = j*K + k comes from Philox call
+// m = n / 2 with counter (g, m, TAG_SGNS), g = noise_offset + b — words (x, y) for even n,
+// (z, w) for odd n, each through bounded64 (uniform over [0, V) like torch.randint;
+// oracle/philox.py device_noise). One call serves two negatives.
+__device__ __forceinline__ dw::U4 noise_pair(const SgnsArgs &a, int64_t b, int m) {
+    const uint64_t g = a.noise_offset + static_cast<uint64_t>(b);
+    return dw::philox<DW_NOISE_ROUNDS>(
+        dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32), static_cast<uint32_t>(m),
+               TAG_SGNS},
+        a.k0, a.k1);
+}
+
 __device__ __forceinline__ int64_t noise_id(const SgnsArgs &a, int64_t b, int j, int k) {
     if (a.noise) return a.noise[(b * a.C + j) * a.K + k];
-    const uint64_t g = a.noise_offset + static_cast<uint64_t>(b);
-    const dw::U4 r = dw::philox<DW_NOISE_ROUNDS>(
-        dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
-               static_cast<uint32_t>(j * a.K + k), TAG_SGNS},
-        a.k0, a.k1);
-    return static_cast<int64_t>(dw::bounded64(r.x, r.y, static_cast<uint64_t>(a.V)));
+    const int n = j * a.K + k;
+    const dw::U4 r = noise_pair(a, b, n >> 1);
+    const uint64_t V = static_cast<uint64_t>(a.V);
+    return static_cast<int64_t>((n & 1) ? dw::bounded64(r.z, r.w, V) : dw::bounded64(r.x, r.y, V));
 }
 
 __device__ __forceinline__ uint64_t pack_record(float coef, int64_t centre) {
@@ -415,21 +425,52 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         }
         const bool ok_c = active && cid >= 0 && cid < a.V;
         if (active && !ok_c && gl == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
-        // the group's row ids (-1 = invalid row: zero coefficient); two Philox draws overlap
+        // the group's row ids (-1 = invalid row: zero coefficient)
         int n_own = T;  // rows in the group's list (OWNER: the owned ones, compacted)
-        if constexpr (OWNER) n_own = 0;
+        if constexpr (OWNER) {
+            // staged in LDS by slot t first (in s_coef, free until the coefficients): contexts
+            // from the walk, negatives two per Philox call (noise_pair) — the 16 lanes draw the
+            // C*K/2 calls, so a centre costs ceil(C*K/32) Philox per lane, not ceil(T/16). Every
+            // rank draws every centre's negatives and keeps ~1/W of them: at W = 8 the draws are
+            // a visible share of pass 1.
+            int32_t *stage = reinterpret_cast<int32_t *>(&s_coef[wv][q][0]);
+            for (int t = gl; t < T; t += 16) stage[t] = -1;
+            if (ok_c) {
+                const int n_neg = a.C * a.K;
+                auto put = [&](int n, int64_t r) {   // negative n -> slot t
+                    const int jn = n / a.K;
+                    const int t = jn * rows_per_ctx + 1 + (n - jn * a.K);
+                    if (r >= 0 && r < a.V)
+                        stage[t] = static_cast<int32_t>(r);
+                    else
+                        dw::status_or(a.status, DW_S_BAD_INDEX);
+                };
+                for (int j = gl; j < a.C; j += 16) {   // contexts
+                    const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, j * rows_per_ctx);
+                    if (r >= 0 && r < a.V)
+                        stage[j * rows_per_ctx] = static_cast<int32_t>(r);
+                    else
+                        dw::status_or(a.status, DW_S_BAD_INDEX);
+                }
+                if (a.noise) {   // replayed negatives
+                    for (int n = gl; n < n_neg; n += 16) put(n, a.noise[b * n_neg + n]);
+                } else {
+                    const uint64_t Vu = static_cast<uint64_t>(a.V);
 #pragma unroll 2
-        for (int k = 0; k < G16_TMAX / 16; ++k) {
-            const int t = gl + 16 * k;
-            int32_t id = -1;
-            if (t < T && ok_c) {
-                const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, t);
-                if (r >= 0 && r < a.V)
-                    id = static_cast<int32_t>(r);
-                else
-                    dw::status_or(a.status, DW_S_BAD_INDEX);
+                    for (int m = gl; 2 * m < n_neg; m += 16) {
+                        const dw::U4 r = noise_pair(a, b, m);
+                        put(2 * m, static_cast<int64_t>(dw::bounded64(r.x, r.y, Vu)));
+                        if (2 * m + 1 < n_neg)
+                            put(2 * m + 1, static_cast<int64_t>(dw::bounded64(r.z, r.w, Vu)));
+                    }
+                }
             }
-            if constexpr (OWNER) {
+            dw::wave_lds_sync();
+            n_own = 0;
+#pragma unroll
+            for (int k = 0; k < G16_TMAX / 16; ++k) {
+                const int t = gl + 16 * k;
+                const int32_t id = t < T ? stage[t] : -1;
                 // owner o % W, local row o / W (shift and mask for the usual W = 2, 4, 8)
                 const int32_t lrow = a.own_shift >= 0 ? (id >> a.own_shift) : id / a.n_owners;
                 const int32_t orow = id - lrow * a.n_owners;
@@ -442,9 +483,24 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                     s_t[wv][q][pos] = static_cast<uint8_t>(t);
                 }
                 n_own += __popc(grp);
-            } else if (t < T) {
-                s_id[wv][q][t] = id;
-                s_coef[wv][q][t] = 0.f;
+            }
+        } else {
+            // one Philox per lane and row (two Philox draws overlap); one device, memory-bound
+#pragma unroll 2
+            for (int k = 0; k < G16_TMAX / 16; ++k) {
+                const int t = gl + 16 * k;
+                int32_t id = -1;
+                if (t < T && ok_c) {
+                    const int64_t r = row_id<FROM_WALKS>(a, b, walk, i, t);
+                    if (r >= 0 && r < a.V)
+                        id = static_cast<int32_t>(r);
+                    else
+                        dw::status_or(a.status, DW_S_BAD_INDEX);
+                }
+                if (t < T) {
+                    s_id[wv][q][t] = id;
+                    s_coef[wv][q][t] = 0.f;
+                }
             }
         }
         // rows the chunk loop runs over: wave-uniform (the longest of the four groups' lists)
@@ -1516,11 +1572,13 @@ __global__ void __launch_bounds__(256)
         const int64_t b = i / (static_cast<int64_t>(C) * K);
         const int slot = static_cast<int>(i - b * C * K);  // j*K + k
         const uint64_t g = noise_offset + static_cast<uint64_t>(b);
-        const dw::U4 r = dw::philox(
+        const dw::U4 r = dw::philox<DW_NOISE_ROUNDS>(   // the pair of slot (noise_pair)
             dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
-                   static_cast<uint32_t>(slot), TAG_SGNS},
+                   static_cast<uint32_t>(slot >> 1), TAG_SGNS},
             k0, k1);
-        out[i] = static_cast<int64_t>(dw::bounded64(r.x, r.y, static_cast<uint64_t>(V)));
+        const uint64_t Vu = static_cast<uint64_t>(V);
+        out[i] = static_cast<int64_t>((slot & 1) ? dw::bounded64(r.z, r.w, Vu)
+                                                 : dw::bounded64(r.x, r.y, Vu));
     }
 }
 

@@ -134,15 +134,23 @@ def fast_walks(row_ptr, col, starts: Sequence[int], length: int, method: str, p:
 
 def device_noise(seed: int, noise_offset: int, n_centres: int, n_ctx: int, k: int,
                  vocab_size: int) -> np.ndarray:
-    """The negatives dw_sgns_* draw when noise == NULL: int64 [B', C, K]."""
+    """The negatives dw_sgns_* draw when noise == NULL: int64 [B', C, K].
+
+    Centre b's negatives are numbered n = j*K + k (context j, k-th negative); Philox call
+    m = n // 2, counter (g lo, g hi, m, TAG_SGNS) with g = noise_offset + b, serves the pair
+    n = 2m (words x, y = lo, hi) and n = 2m + 1 (words z, w), each through bounded64 (dw_sgns.hip
+    noise_id / k_sgns_g16 / k_noise_fill)."""
     k0, k1 = seed & MASK, (seed >> 32) & MASK
     b = (np.arange(n_centres, dtype=np.uint64) + np.uint64(noise_offset))
     jk = np.arange(n_ctx * k, dtype=np.uint64)
     bb = np.repeat(b, n_ctx * k)
-    jj = np.tile(jk, n_centres)
-    r = philox(bb & np.uint64(MASK), bb >> np.uint64(32), jj, np.full(bb.shape, TAG_SGNS,
-                                                                      np.uint64), k0, k1)
-    return bounded64(r[0], r[1], vocab_size).reshape(n_centres, n_ctx, k)
+    nn = np.tile(jk, n_centres)
+    r = philox(bb & np.uint64(MASK), bb >> np.uint64(32), nn >> np.uint64(1),
+               np.full(bb.shape, TAG_SGNS, np.uint64), k0, k1)
+    odd = (nn & np.uint64(1)).astype(bool)
+    lo = np.where(odd, r[2], r[0])
+    hi = np.where(odd, r[3], r[1])
+    return bounded64(lo, hi, vocab_size).reshape(n_centres, n_ctx, k)
 
 
 def alias_tables(row_ptr, weights: Optional[np.ndarray]):
