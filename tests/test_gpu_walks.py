@@ -223,6 +223,9 @@ def test_isolated_node_raises_like_reference(hip_device):
     w2 = Node2Vec(g, 4, p=1, q=1, rng='philox')
     with pytest.raises(IndexError):
         w2.walk('c')
+    for layout in ('indexed', 'csr'):   # both Philox DeepWalk walkers report it too
+        with pytest.raises(IndexError):
+            DeepWalk(g, 4, rng='philox', layout=layout).walk('c')
     assert len(DeepWalk(g, 1).walk('c').split()) == 1
 
 
