@@ -602,11 +602,14 @@ def main():
         try:
             with open(prof) as f:
                 doc = json.load(f)
-            want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in, W_eff if owner else 0)
+            # (owner form: its own in-table rows' Adam runs on the side stream inside the op)
+            want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in or owner,
+                    W_eff if owner else 0, args.in_exchange if owner else None)
             pmc = next((e for e in doc.get('entries', []) if
                         (e.get('pairs_per_launch'), e.get('scatter'), e.get('dim'),
                          e.get('vocab_size'), bool(e.get('fused_out_adam')),
-                         bool(e.get('overlap_in')), int(e.get('owner_world') or 0)) == want),
+                         bool(e.get('overlap_in')), int(e.get('owner_world') or 0),
+                         e.get('in_exchange')) == want),
                        None)
             if pmc is not None:
                 result['roofline']['traffic'] = pmc.get('hbm_bytes_per_launch')

@@ -1,6 +1,12 @@
 """Summarise rocprofv3 output (gpurun_out/prof_*) into profiles/ (committed evidence).
 
-    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch [dim vocab_size [overlap_in]]]
+    python scripts/rocprof_summary.py <round-tag> [pairs_per_launch [dim vocab_size [overlap_in
+                                      [owner_world in_exchange]]]]
+
+owner_world > 0: a profile of `bench.py --emulate-world W` (rank 0's share of an owner-computes
+job of W ranks; the kernels of a real rank, without its collectives); the sgns_pmc.json entry is
+then keyed by (owner_world, in_exchange) too, and bench.py reports it as the N = W line's
+traffic.
 
 Writes
   profiles/<tag>_kernel_stats.csv  rocprofv3 --stats, verbatim;
@@ -44,7 +50,12 @@ def kernel_class(name: str):
     if 'radix_sort' in name or 'onesweep' in name:
         # the SGNS records sort: u32 row keys, u64 {coef, centre} values; the CSR copy sort
         # (dw_csr_sort_copy, u64 keys only) runs once at setup
+        # (the owner form's occurrence sort of the centres, u32/u32 with rocprim's default
+        # config, cannot be told from the graph-ingestion sorts by name; it is left out: < 1%
+        # of an owner step's bytes)
         return 'sgns_sort' if 'unsigned int, unsigned long' in name else 'csr_sort'
+    if 'k_occ_keys' in name or 'k_wave_scan' in name or 'k_rec_compact' in name:
+        return 'sgns_aux'        # owner-form pass-1 helpers (centre order, record compaction)
     for k in ('k_adam', 'k_scale', 'k_walk_deepwalk_fast', 'k_walk_deepwalk_inline',
               'k_walk_node2vec_fast',
               'k_walk_replay', 'k_logits'):
@@ -59,6 +70,8 @@ def main():
     dim = int(sys.argv[3]) if len(sys.argv) > 3 else 128          # C3 defaults
     vocab = int(sys.argv[4]) if len(sys.argv) > 4 else 1048577
     overlap_in = bool(int(sys.argv[5])) if len(sys.argv) > 5 else True
+    owner_world = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    in_exchange = sys.argv[7] if len(sys.argv) > 7 else None
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, 'prof_trace', '**', '*kernel_stats.csv'), recursive=True)
     dur = collections.defaultdict(lambda: [0, 0.0])   # class -> [calls, total ns]
@@ -107,7 +120,8 @@ def main():
     calls_trace = p1.get('trace_dispatches', 0)
     call = {'ms': 0.0, 'hbm_bytes': 0.0}
     ok = calls_trace > 0
-    op_classes = SGNS_CLASSES + (('k_adam',) if overlap_in else ())
+    op_classes = SGNS_CLASSES + (('k_adam',) if overlap_in else ()) + \
+        (('sgns_aux',) if owner_world else ())
     for k in op_classes:
         e = summary.get(k)
         if not e:
@@ -131,6 +145,7 @@ def main():
         entry = {'round': tag, 'pairs_per_launch': pairs, 'dim': dim, 'vocab_size': vocab,
                  'scatter': 'sorted' if 'sgns_sort' in summary else 'atomic',
                  'fused_out_adam': fused, 'overlap_in': overlap_in,
+                 'owner_world': owner_world, 'in_exchange': in_exchange,
                  'hbm_bytes_per_launch': call['hbm_bytes'],
                  'hbm_bytes_per_kernel': per_kernel,
                  'note': '2*FETCH_SIZE + WRITE_SIZE (KiB->B) summed over the kernels of one '
@@ -140,7 +155,8 @@ def main():
         if os.path.exists(path):
             old = json.load(open(path))
             entries = old.get('entries', [old] if 'pairs_per_launch' in old else [])
-        key = ('pairs_per_launch', 'dim', 'vocab_size', 'scatter', 'fused_out_adam', 'overlap_in')
+        key = ('pairs_per_launch', 'dim', 'vocab_size', 'scatter', 'fused_out_adam', 'overlap_in',
+               'owner_world', 'in_exchange')
         entries = [e for e in entries if tuple(e.get(k) for k in key) !=
                    tuple(entry[k] for k in key)] + [entry]
         with open(path, 'w') as f:
