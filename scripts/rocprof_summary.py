@@ -54,8 +54,11 @@ def kernel_class(name: str):
         # config, cannot be told from the graph-ingestion sorts by name; it is left out: < 1%
         # of an owner step's bytes)
         return 'sgns_sort' if 'unsigned int, unsigned long' in name else 'csr_sort'
-    if 'k_occ_keys' in name or 'k_wave_scan' in name or 'k_rec_compact' in name:
-        return 'sgns_aux'        # owner-form pass-1 helpers (centre order, record compaction)
+    if any(k in name for k in ('k_occ_keys', 'k_wave_scan', 'k_rec_compact', 'k_rows_adam',
+                                'k_rows_gather')):
+        # owner-form helpers: centre order, record compaction; lazy in-table exchange: the
+        # touched rows' catch-up / gradient gather / update
+        return 'sgns_aux'
     for k in ('k_adam', 'k_scale', 'k_walk_deepwalk_fast', 'k_walk_deepwalk_inline',
               'k_walk_node2vec_fast',
               'k_walk_replay', 'k_logits'):
