@@ -35,8 +35,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 CONFIGS = {
-    'c3': dict(scale=20, edges=10_000_000, dim=128, method='deepwalk', p=1.0, q=1.0),
-    'c5': dict(scale=24, edges=256_000_000, dim=256, method='node2vec', p=0.25, q=4.0),
+    # BASELINE C2 shape (Cora is not shipped): a 4,096-node R-MAT with Cora's 5,429 edges, the
+    # reference's Cora config (node2vec, L=10, R=2, 16 walks per node, 64-walk batches) at d=128
+    'c2': dict(scale=12, edges=5429, dim=128, method='node2vec', p=1.0, q=1.0, radius=2,
+               walk_length=10, batch_walks=64, walks_per_node=16),
+    'c3': dict(scale=20, edges=10_000_000, dim=128, method='deepwalk', p=1.0, q=1.0, radius=5,
+               walk_length=80, batch_walks=8192, walks_per_node=10),
+    'c5': dict(scale=24, edges=256_000_000, dim=256, method='node2vec', p=0.25, q=4.0, radius=5,
+               walk_length=80, batch_walks=8192, walks_per_node=10),
 }
 
 
@@ -94,9 +100,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=30)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch-walks', type=int, default=8192)
+    ap.add_argument('--batch-walks', type=int, default=None)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS),
-                    help='BASELINE workload preset: c3 = R-MAT 20 / 10M draws, d=128, DeepWalk '
+                    help='BASELINE workload preset: c2 = Cora-shaped R-MAT 12, node2vec, 64-walk batches; c3 = R-MAT 20 / 10M draws, d=128, DeepWalk '
                          '(the metric\'s config); c5 = R-MAT 24 / 256M draws, d=256, node2vec '
                          'p=0.25 q=4 (BASELINE configs[4], here per GPU)')
     ap.add_argument('--method', default=None, choices=['deepwalk', 'node2vec'])
@@ -106,9 +112,9 @@ def main():
     ap.add_argument('--edges', type=int, default=None)
     ap.add_argument('--dim', type=int, default=None)
     ap.add_argument('--neg', type=int, default=5)
-    ap.add_argument('--radius', type=int, default=5)
-    ap.add_argument('--walk-length', type=int, default=80)
-    ap.add_argument('--walks-per-node', type=int, default=10)
+    ap.add_argument('--radius', type=int, default=None)
+    ap.add_argument('--walk-length', type=int, default=None)
+    ap.add_argument('--walks-per-node', type=int, default=None)
     ap.add_argument('--lr', type=float, default=0.01)
     ap.add_argument('--scatter', default='sorted', choices=['sorted', 'atomic'],
                     help='output-table gradient: records+sort+gather (sorted) or float atomics')
@@ -619,7 +625,7 @@ def main():
                     result['roofline']['phases'][k]['traffic'] = per_k.get('sgns_' + k)
         except (OSError, ValueError):
             pass
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 'c3':
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ('c2', 'c3'):
         cb = cpu_baseline(csr, args, args.cpu_budget)
         result['cpu_baseline'] = cb
     if rank == 0:
