@@ -102,7 +102,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch-walks', type=int, default=None)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS),
-                    help='BASELINE workload preset: c2 = Cora-shaped R-MAT 12, node2vec, 64-walk batches; c3 = R-MAT 20 / 10M draws, d=128, DeepWalk '
+                    help='BASELINE workload preset: c2 = Cora-shaped R-MAT 12, node2vec, 64-walk '
+                         'batches; c3 = R-MAT 20 / 10M draws, d=128, DeepWalk '
                          '(the metric\'s config); c5 = R-MAT 24 / 256M draws, d=256, node2vec '
                          'p=0.25 q=4 (BASELINE configs[4], here per GPU)')
     ap.add_argument('--method', default=None, choices=['deepwalk', 'node2vec'])
