@@ -38,7 +38,7 @@ constexpr int WAVE = 64;
 constexpr int WAVES_PER_BLOCK = 4;
 constexpr int CHUNK = 12;            // output rows in flight per wave
 constexpr int TMAX = 256;            // max output rows per centre in records mode
-constexpr int GCH = 512;             // records per pass-2 wave chunk
+constexpr int GCH = 512;             // records per pass-2 wave chunk (large batches; pass2_chunk)
 constexpr int GU = 8;                // records in flight per pass-2 iteration
 constexpr uint32_t TAG_SGNS = 0x53470000u;  // 'SG'
 
@@ -665,8 +665,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 }
 
 // Pass 2: records sorted by output row -> g_out[row] += sum coef * w_in[centre].
-// Each wave owns a fixed chunk of GCH sorted records (balanced whatever the row lengths —
-// hub rows hold thousands). A row wholly inside the chunk is summed in registers and added
+// Each wave owns a fixed chunk of gch sorted records (GCH = 512; smaller for small batches),
+// balanced whatever the row lengths (hub rows hold thousands). A row wholly inside the chunk is summed in registers and added
 // with a plain read-modify-write (the chunk is its only writer); the first / last row of a
 // chunk may continue in the neighbouring chunk and is added with float atomics.
 // Output-table Adam fused in (ADAM, one device: dw_sgns_walks_phase2_adam): a row wholly
@@ -686,20 +686,20 @@ template <int VPL, bool MASKED, bool ADAM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
-                 int32_t d, OutAdam oa, const int64_t *__restrict__ range) {
+                 int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t lo = range ? range[0] : 0;
     const int64_t hi = range ? range[1] : n_rec;
-    const int64_t n_chunks = (hi - lo + GCH - 1) / GCH;
+    const int64_t n_chunks = (hi - lo + gch - 1) / gch;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     bool live[VPL];
 #pragma unroll
     for (int m = 0; m < VPL; ++m) live[m] = !MASKED || (lane + WAVE * m < d);
 
     for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
-        const int64_t e0 = lo + ch * GCH;
-        const int64_t e1 = (e0 + GCH < hi) ? e0 + GCH : hi;
+        const int64_t e0 = lo + ch * gch;
+        const int64_t e1 = (e0 + gch < hi) ? e0 + gch : hi;
         const uint32_t before = e0 > lo ? keys[e0 - 1] : 0xFFFFFFFFu;
         const uint32_t after = e1 < hi ? keys[e1] : 0xFFFFFFFFu;
         // lanes past the chunk's end repeat its LAST key: a partial final group must not switch
@@ -937,22 +937,22 @@ __global__ void __launch_bounds__(256)
 template <int VPL>
 void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const uint64_t *vals,
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
-                   const OutAdam *oa, const int64_t *range) {
+                   const OutAdam *oa, const int64_t *range, int32_t gch) {
     const bool exact = d == 64 * VPL;
     if (oa) {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa, range);
+                               w_in, g_out, d, *oa, range, gch);
         else
             hipLaunchKernelGGL((k_rec_gather<VPL, true, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa, range);
+                               w_in, g_out, d, *oa, range, gch);
     } else {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, false>), g, bl, 0, st, keys, vals,
-                               n_rec, w_in, g_out, d, OutAdam{}, range);
+                               n_rec, w_in, g_out, d, OutAdam{}, range, gch);
         else
             hipLaunchKernelGGL((k_rec_gather<VPL, true, false>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, OutAdam{}, range);
+                               w_in, g_out, d, OutAdam{}, range, gch);
     }
 }
 
@@ -976,15 +976,23 @@ void launch_rest(hipStream_t st, int64_t V, int32_t d, float *g_out, const OutAd
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
                  float *g_out, int32_t d, const OutAdam *oa, int64_t V, hipStream_t st,
                  const int64_t *range = nullptr, double share = 1.0) {
-    const int64_t n_chunks = (n_rec + GCH - 1) / GCH;
+    // chunk size: GCH for large batches (balanced, few boundary rows); halved down to 32 while
+    // the chunks would not give every SIMD of the chip a few waves — a 9K-record batch (C2 shape)
+    // in 512-record chunks ran as 18 waves, 240 us of latency-bound gathers
+    int32_t gch = GCH;
+    {
+        const int64_t want = grid_cap(16);   // 4 waves per SIMD
+        while (gch > 32 && (n_rec + gch - 1) / gch < want) gch >>= 1;
+    }
+    const int64_t n_chunks = (n_rec + gch - 1) / gch;
     int64_t blocks = (int64_t)((double)(n_chunks + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK * share);
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
-    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
-    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
-    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range);
+    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
+    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
+    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
+    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
     else return DW_E_UNSUPPORTED;
     DW_LAUNCH_CHECK("dw_sgns/gather");
     if (oa) {
