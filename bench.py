@@ -152,6 +152,13 @@ def main():
                          'this job (max over ranks) before the warmup and keep the faster '
                          '(default at C3 with N > 1: which one hides better behind the '
                          'output-table phase depends on the xGMI / RCCL rate)')
+    ap.add_argument('--n1-in-adam', default='auto', choices=['auto', 'dense', 'lazy'],
+                    help='one GPU, in-table Adam: dense (the overlapped dense update of the fused '
+                         'N=1 step) or lazy (the owner path on one rank with the lazy exact Adam: '
+                         'only the rows the batch touches are read and updated, deferred g = 0 '
+                         'steps replayed bit-exactly). auto = lazy when a step\'s centres are '
+                         'under 10%% of the rows of a table of >= 1 GB of Adam bytes (C5: 3.4%% '
+                         'of 16.8M rows; C3: 55%%, where dense measured faster)')
     ap.add_argument('--calib-steps', type=int, default=8,
                     help='--in-exchange auto: timed steps per protocol')
     ap.add_argument('--walk-prefetch', action='store_true',
@@ -208,6 +215,15 @@ def main():
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
     emulate = args.emulate_world if (world == 1 and args.emulate_world >= 1) else 0
+    # one GPU, sparse batches: the owner path on one rank with the lazy exact in-table Adam
+    # (auto: sparse batches over a large table — at C2 the table is 15 MB and the lazy path's
+    # extra launches cost more than its Adam saves: 0.35 vs 0.20 ms per step)
+    n1_lazy = (world == 1 and not emulate and args.dist_mode == 'owner'
+               and (args.n1_in_adam == 'lazy' or
+                    (args.n1_in_adam == 'auto' and B * (L - 2 * R) < 0.1 * V
+                     and V * args.dim * 4 * 7 >= 1e9)))
+    if n1_lazy:
+        emulate, args.in_exchange = 1, 'lazy'
     owner = emulate > 0 or (world > 1 and args.dist_mode == 'owner')
     if owner and not (args.scatter == 'sorted' and d % 64 == 0 and d <= 512
                       and 2 * R * (1 + K) <= 64):
@@ -473,7 +489,7 @@ def main():
     if owner and world > 1:             # each rank summed the loss terms of its own slots
         dist.all_reduce(loss_acc)
     terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
-    mean_loss = None if emulate else float(terms['loss'])
+    mean_loss = None if emulate > 1 else float(terms['loss'])   # one rank owns every slot at W=1
 
     # weak scaling: the job processes B walks per rank per step (owner: W*B walks, each rank a
     # 1/W share of their slots)
@@ -498,6 +514,9 @@ def main():
         op_ms = sgns_ms + kern_ms['adam']
         if lazy:   # + the centre order, touched-row catch-up and gather outside the pass events
             op_ms = kern_ms['sgns'] + kern_ms['adam']
+            # the lazy exact Adam needs the dense figure only on the rows the batch touches
+            # (every rank updates all of them); the last step's |U| stands for the steps
+            in_adam_bytes = int(tables._n_host[0]) * d * 4 * 7
     sgns_gbs = (pairs_per_step * bpp + out_adam_bytes + in_adam_bytes) / (op_ms * 1e-3) / 1e9
     phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     if owner:
@@ -559,6 +578,9 @@ def main():
                          f'{args.scatter} output-table scatter'),
             'global_batch_walks': B * W_eff, 'positive_pairs_per_step_per_gpu': pairs_per_step,
             'parallelism': (
+                'dp1 (one GPU; owner path on one rank with the lazy exact in-table Adam: only '
+                'the rows the batch touches are read and updated, deferred g = 0 steps replayed '
+                'bit-exactly)' if n1_lazy else
                 f'EMULATED rank 0 of {W_eff} on one GPU (owner-computes, in table '
                 f'{args.in_exchange}; no collectives run, '
                 f'value is a projection assuming the in-table exchange stays hidden; walks: '
