@@ -904,7 +904,9 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
 // Rows the fused gather did not update: boundary rows (g in g_out) and rows no record touched
 // (g_out = 0) — Adam with g_out, which is left zeroed. Each wave reads the flags of 64 rows in
 // one load, ballots the unflagged ones and updates only those (lane-coalesced rows), so the
-// common case at C3 — almost every row already updated — costs one byte per row.
+// common case at C3 — almost every row already updated — costs one byte per row. g is
+// re-zeroed only where it is non-zero (boundary rows): it never holds -0 (atomic sums from +0),
+// so the skipped store leaves the same bits.
 template <int VPL, bool MASKED>
 __global__ void __launch_bounds__(256)
     k_adam_rest(int64_t n_rows, int32_t d, const uint8_t *__restrict__ flags,
@@ -928,7 +930,7 @@ __global__ void __launch_bounds__(256)
                 oa.p[i] = pp;
                 oa.m[i] = mm;
                 oa.v[i] = vv;
-                g[i] = 0.f;
+                if (gg != 0.f) g[i] = 0.f;   // untouched rows' g is already 0: no write
             }
         }
     }
