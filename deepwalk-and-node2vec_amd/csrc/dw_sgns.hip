@@ -917,20 +917,36 @@ __global__ void __launch_bounds__(256)
          base < n_rows; base += n_waves * WAVE) {
         const int64_t r = base + lane;
         unsigned long long todo = __ballot(r < n_rows && flags[r] == 0);
+        // two rows per trip (wave-uniform): both rows' loads are issued before either's stores
         while (todo) {
-            const int l = __ffsll(static_cast<long long>(todo)) - 1;
+            const int l0 = __ffsll(static_cast<long long>(todo)) - 1;
             todo &= todo - 1ull;
-            const int64_t o = (base + l) * d + lane;
+            const bool two = todo != 0ull;
+            const int l1 = two ? __ffsll(static_cast<long long>(todo)) - 1 : l0;
+            if (two) todo &= todo - 1ull;
+            const int64_t o0 = (base + l0) * d + lane, o1 = (base + l1) * d + lane;
+            float pp[2][VPL], gg[2][VPL], mm[2][VPL], vv[2][VPL];
 #pragma unroll
             for (int m = 0; m < VPL; ++m) {
                 if (MASKED && lane + WAVE * m >= d) continue;
-                const int64_t i = o + WAVE * m;
-                float pp = oa.p[i], gg = g[i], mm = oa.m[i], vv = oa.v[i];
-                dw::adam_elem(pp, gg, mm, vv, oa.s);
-                oa.p[i] = pp;
-                oa.m[i] = mm;
-                oa.v[i] = vv;
-                if (gg != 0.f) g[i] = 0.f;   // untouched rows' g is already 0: no write
+                const int64_t i0 = o0 + WAVE * m, i1 = o1 + WAVE * m;
+                pp[0][m] = oa.p[i0]; gg[0][m] = g[i0]; mm[0][m] = oa.m[i0]; vv[0][m] = oa.v[i0];
+                pp[1][m] = oa.p[i1]; gg[1][m] = g[i1]; mm[1][m] = oa.m[i1]; vv[1][m] = oa.v[i1];
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (k == 1 && !two) break;
+                const int64_t o = k ? o1 : o0;
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) {
+                    if (MASKED && lane + WAVE * m >= d) continue;
+                    const int64_t i = o + WAVE * m;
+                    dw::adam_elem(pp[k][m], gg[k][m], mm[k][m], vv[k][m], oa.s);
+                    oa.p[i] = pp[k][m];
+                    oa.m[i] = mm[k][m];
+                    oa.v[i] = vv[k][m];
+                    if (gg[k][m] != 0.f) g[i] = 0.f;   // untouched rows' g is already 0: no write
+                }
             }
         }
     }
