@@ -195,11 +195,10 @@ def main():
     from shallow_encoders import _native
     from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
     from shallow_encoders.graph.rmat import rmat_graph
-    from shallow_encoders.word2vec.sgns import (loss_terms, phase_ms, phase_timing, sgns_accumulate,
-                                               sgns_phase2_pieces, sgns_phase_bytes)
+    from shallow_encoders.word2vec.sgns import loss_terms, phase_ms, phase_timing, sgns_phase_bytes
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     from shallow_encoders.word2vec.sharding import (OwnerLazyTables, OwnerTables, ShardedTables,
-                                                    overlap_adam_blocks)
+                                                    overlap_adam_blocks, replicated_step)
     _native.require_device(dev)
 
     t0 = time.time()
@@ -402,31 +401,18 @@ def main():
         walks = feed.get(s)
         if record:
             e[1].record()
-        kw = dict(walks=walks, context_radius=R, noise=None, seed=99,
-                  noise_offset=g0 * (L - 2 * R), grad_scale=grad_scale, loss_acc=loss_acc,
-                  status=status, scatter=args.scatter)
-        # pass 1 (g_in final) -> in-table exchange on a side stream (N > 1) while the
-        # output-table phase runs -> out-table exchange -> wait for both all-gathers
-        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
-        feed.next(s)
-        tables.exchange_in(overlap_bytes=p2_bytes)
-        # one device: the output table's Adam is fused into the output-table phase; N > 1:
-        # that phase runs in row pieces, each exchanged behind the next piece's gather
-        spec = tables.out_adam_spec() if fuse else None
-        if pieces:
-            n_pieces, rows = tables.out_pieces_spec()
-            sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks, context_radius=R,
-                               n_pieces=n_pieces, piece_rows=rows,
-                               on_piece=tables.exchange_out_piece, status=status,
-                               scatter=args.scatter)
-        else:
-            sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
-                            out_adam=spec, **kw)
-        feed.release(s)
-        if record:
-            e[2].record()
-        tables.exchange_out(fused_out=spec is not None)
-        tables.sync()
+
+        def phase2_done():
+            feed.release(s)
+            if record:
+                e[2].record()
+        # pass 1 (g_in final) -> in-table Adam / exchange on a side stream while the
+        # output-table phase runs (one device: the out table's Adam fused into it; N > 1: in
+        # row pieces, each exchanged behind the next piece's gather) -> join
+        replicated_step(tables, walks, R, K, seed=99, noise_offset=g0 * (L - 2 * R),
+                        grad_scale=grad_scale, loss_acc=loss_acc, status=status,
+                        scatter=args.scatter, fuse_out_adam=fuse, pieces=pieces,
+                        after_pass1=lambda: feed.next(s), after_phase2=phase2_done)
         if record:
             e[3].record()
             ev['walk'].append((e[0], e[1]))

@@ -381,6 +381,51 @@ class ShardedTables:
         self._cur_in = self._next_in
 
 
+def replicated_step(tables: ShardedTables, walks: torch.Tensor, context_radius: int,
+                    neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
+                    loss_acc: torch.Tensor, status: torch.Tensor, scatter: str = 'sorted',
+                    fuse_out_adam: bool = True, pieces: bool = False,
+                    after_pass1: Optional[Callable[[], None]] = None,
+                    after_phase2: Optional[Callable[[], None]] = None) -> None:
+    """One training step of ``tables`` over the batch ``walks`` — bench.py's step at N = 1 (and
+    the replicated layout at N > 1), also run at full C3 size by tests/test_gpu_c3_step.py:
+
+      SGNS pass 1 (g_in final; device negatives when ``noise`` is not given)
+      -> in-table Adam (N = 1: dw_adam_dense_to into the idle buffer on the side stream, grid
+         sized to the output-table phase; N > 1: reduce-scatter / Adam / all-gather)
+      -> output-table phase with the out table's Adam fused (N = 1, records path) or in pieces
+         exchanged behind the gathers (N > 1, ``pieces``)
+      -> remaining exchanges, then the main stream joins the side stream.
+
+    ``after_pass1`` / ``after_phase2``: host callbacks at those two points of the enqueue order
+    (bench.py records events and hands the walk buffer back there)."""
+    from shallow_encoders.word2vec.sgns import (sgns_accumulate, sgns_phase2_pieces,
+                                                sgns_phase_bytes)
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    kw = dict(walks=walks, context_radius=R, noise=None, seed=seed, noise_offset=noise_offset,
+              grad_scale=grad_scale, loss_acc=loss_acc, status=status, scatter=scatter)
+    fuse = fuse_out_adam and scatter == 'sorted' and tables.can_fuse_out_adam()
+    pb = sgns_phase_bytes(n, L, R, K, tables.d, tables.V, scatter, fuse)
+    sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
+    if after_pass1 is not None:
+        after_pass1()
+    tables.exchange_in(overlap_bytes=pb['sort'] + pb['pass2'])
+    spec = tables.out_adam_spec() if fuse else None
+    if pieces:
+        n_pieces, rows = tables.out_pieces_spec()
+        sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks, context_radius=R,
+                           n_pieces=n_pieces, piece_rows=rows,
+                           on_piece=tables.exchange_out_piece, status=status, scatter=scatter)
+    else:
+        sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=2,
+                        out_adam=spec, **kw)
+    if after_phase2 is not None:
+        after_phase2()
+    tables.exchange_out(fused_out=spec is not None)
+    tables.sync()
+
+
 class OwnerTables:
     """N > 1, owner-computes layout (the multi-GPU default of bench.py).
 

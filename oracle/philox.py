@@ -40,8 +40,8 @@ def bounded32(r, n):
     return (np.asarray(r, dtype=np.uint64) * np.uint64(n)) >> np.uint64(32)
 
 
-def bounded64(lo, hi, n: int) -> np.ndarray:
-    """floor(r64 * n / 2^64) with r64 = hi:lo, exact via Python integers."""
+def bounded64_int(lo, hi, n: int) -> np.ndarray:
+    """floor(r64 * n / 2^64) with r64 = hi:lo, by Python integers (the definition; slow)."""
     lo = np.asarray(lo, dtype=np.uint64).ravel()
     hi = np.asarray(hi, dtype=np.uint64).ravel()
     out = np.empty(lo.shape, dtype=np.int64)
@@ -49,6 +49,20 @@ def bounded64(lo, hi, n: int) -> np.ndarray:
         r = (int(hi[i]) << 32) | int(lo[i])
         out[i] = (r * n) >> 64
     return out
+
+
+def bounded64(lo, hi, n: int) -> np.ndarray:
+    """floor(r64 * n / 2^64) with r64 = hi:lo, n < 2^32, vectorised and exact:
+    r64 * n = hi*n*2^32 + lo*n, and with lo*n = A*2^32 + a (a < 2^32) the result is
+    floor((hi*n + A) / 2^32) — hi*n + A <= (2^32-1)^2 + 2^32 - 1 < 2^64 never wraps.
+    Equal to bounded64_int (tests/test_oracle_golden.py)."""
+    if not 0 < n < 2 ** 32:
+        raise ValueError('bounded64 needs 0 < n < 2^32')
+    lo = np.asarray(lo, dtype=np.uint64).ravel()
+    hi = np.asarray(hi, dtype=np.uint64).ravel()
+    nn = np.uint64(n)
+    s32 = np.uint64(32)
+    return ((hi * nn + ((lo * nn) >> s32)) >> s32).astype(np.int64)
 
 
 def accept_threshold(alpha: float, alpha_max: float) -> int:
@@ -151,6 +165,51 @@ def device_noise(seed: int, noise_offset: int, n_centres: int, n_ctx: int, k: in
     lo = np.where(odd, r[2], r[0])
     hi = np.where(odd, r[3], r[1])
     return bounded64(lo, hi, vocab_size).reshape(n_centres, n_ctx, k)
+
+
+def philox_torch(c0, c1, c2, c3, k0: int, k1: int):
+    """philox() over torch int64 tensors holding 32-bit words (any device; the full-size
+    checks run it on the GPU). A 32x32-bit product fits an int64 bit pattern; >> 32 of a
+    wrapped (negative) product is masked back to the unsigned high word."""
+    m32 = 0xFFFFFFFF
+    x0, x1, x2, x3 = (t & m32 for t in (c0, c1, c2, c3))
+    k0, k1 = k0 & m32, k1 & m32
+    for _ in range(10):
+        p0 = x0 * M0
+        p1 = x2 * M1
+        hi0, lo0 = (p0 >> 32) & m32, p0 & m32
+        hi1, lo1 = (p1 >> 32) & m32, p1 & m32
+        x0, x1, x2, x3 = (hi1 ^ x1 ^ k0), lo1, (hi0 ^ x3 ^ k1), lo0
+        k0 = (k0 + W0) & m32
+        k1 = (k1 + W1) & m32
+    return x0, x1, x2, x3
+
+
+def bounded64_torch(lo, hi, n: int):
+    """bounded64 over int64 tensors for n < 2^31 (then hi*n + A < 2^63: no signed wrap)."""
+    if not 0 < n < 2 ** 31:
+        raise ValueError('bounded64_torch needs 0 < n < 2^31')
+    return (hi * n + ((lo * n) >> 32)) >> 32
+
+
+def device_noise_torch(seed: int, noise_offset: int, n_centres: int, n_ctx: int, k: int,
+                       vocab_size: int, device=None):
+    """device_noise() as an int64 torch tensor [B', C, K] computed on ``device`` (one Philox
+    call per pair of negatives, as the kernels draw them). Equal to device_noise
+    (tests/test_oracle_golden.py); used where B'·C·K is in the tens of millions."""
+    import torch
+    k0, k1 = seed & MASK, (seed >> 32) & MASK
+    nk = n_ctx * k
+    calls = (nk + 1) // 2
+    b = torch.arange(n_centres, dtype=torch.int64, device=device) + int(noise_offset)
+    bb = b.repeat_interleave(calls)
+    mm = torch.arange(calls, dtype=torch.int64, device=device).repeat(n_centres)
+    r = philox_torch(bb & MASK, bb >> 32, mm, torch.full_like(bb, TAG_SGNS), k0, k1)
+    del bb, mm
+    even = bounded64_torch(r[0], r[1], vocab_size).view(n_centres, calls)
+    odd = bounded64_torch(r[2], r[3], vocab_size).view(n_centres, calls)
+    out = torch.stack([even, odd], dim=2).view(n_centres, 2 * calls)[:, :nk]
+    return out.reshape(n_centres, n_ctx, k).contiguous()
 
 
 def alias_tables(row_ptr, weights: Optional[np.ndarray]):

@@ -135,3 +135,58 @@ def test_oracle_trajectory_with_steplr():
     w_in, w_out = ref.tables()
     np.testing.assert_allclose(w_in, f['w_in'], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(w_out, f['w_out'], rtol=1e-5, atol=1e-6)
+
+
+# ---- the vectorised / torch forms the full-size checks use, against the definitions ----------
+
+def test_bounded64_vectorised_equals_integer_definition():
+    from oracle import philox as ph
+    rng = np.random.default_rng(3)
+    lo = np.concatenate([rng.integers(0, 2 ** 32, 4000, dtype=np.uint64),
+                         np.array([0, 2 ** 32 - 1, 0, 2 ** 32 - 1], np.uint64)])
+    hi = np.concatenate([rng.integers(0, 2 ** 32, 4000, dtype=np.uint64),
+                         np.array([0, 0, 2 ** 32 - 1, 2 ** 32 - 1], np.uint64)])
+    for n in (1, 35, 1_048_577, 16_777_217, 2 ** 31 - 1, 2 ** 32 - 1):
+        exp = ph.bounded64_int(lo, hi, n)
+        np.testing.assert_array_equal(ph.bounded64(lo, hi, n), exp)
+        if n < 2 ** 31:
+            import torch
+            got = ph.bounded64_torch(torch.as_tensor(lo.astype(np.int64)),
+                                     torch.as_tensor(hi.astype(np.int64)), n)
+            np.testing.assert_array_equal(got.numpy(), exp)
+
+
+def test_philox_torch_equals_numpy_and_device_noise_torch():
+    import torch
+    from oracle import philox as ph
+    rng = np.random.default_rng(4)
+    c = [rng.integers(0, 2 ** 32, 500, dtype=np.uint64) for _ in range(4)]
+    exp = ph.philox(*c, 0x12345678, 0x9ABCDEF0)
+    got = ph.philox_torch(*(torch.as_tensor(x.astype(np.int64)) for x in c),
+                          0x12345678, 0x9ABCDEF0)
+    for e, g in zip(exp, got):
+        np.testing.assert_array_equal(g.numpy().astype(np.uint64), e)
+    for (B, C, K, V, off) in ((37, 10, 5, 1_048_577, 123_456_789_012), (9, 4, 3, 35, 0),
+                              (5, 2, 1, 2 ** 31 - 1, 7)):
+        np.testing.assert_array_equal(ph.device_noise_torch(99, off, B, C, K, V).numpy(),
+                                      ph.device_noise(99, off, B, C, K, V))
+
+
+def test_closed_form_torch_and_windows_torch_equal_numpy_forms():
+    import torch
+    f = golden('sgns_d128_k5.npz')
+    R = int(f['R'])
+    ins_t, tgt_t = sgns_ref.sg_windows_torch(torch.as_tensor(f['walks']), R)
+    ins, tgt = sgns_ref.sg_windows(f['walks'], R)
+    np.testing.assert_array_equal(ins_t.numpy(), ins.reshape(-1))
+    np.testing.assert_array_equal(tgt_t.numpy(), tgt)
+    l64, gi64, go64 = sgns_ref.sgns_grads_closed_form(f['w_in0'], f['w_out0'], ins, tgt,
+                                                      f['noise'][0])
+    sums, gi, go = sgns_ref.sgns_grads_closed_form_torch(
+        torch.as_tensor(f['w_in0']), torch.as_tensor(f['w_out0']), ins_t, tgt_t,
+        torch.as_tensor(f['noise'][0]), chunk=7)
+    assert float(sums[0] + sums[1]) / tgt.size == pytest.approx(l64, rel=1e-12)
+    np.testing.assert_allclose(gi.numpy(), gi64, rtol=1e-12, atol=1e-18)
+    np.testing.assert_allclose(go.numpy(), go64, rtol=1e-12, atol=1e-18)
+    assert float(sums[0] + sums[1]) / tgt.size == pytest.approx(float(f['losses'][0][0]),
+                                                                rel=1e-5)
