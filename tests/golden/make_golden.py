@@ -1,6 +1,6 @@
 """Generate the golden fixtures from the REFERENCE itself (run in the build container only).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [downstream | cbow]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [downstream | cbow | cora | traj128]
 
 Imports the importable pieces of /root/reference: the walkers
 (graph/random_walk_generator.py), the datasets (graph/datasets.py), SkipGram (word2vec/model.py),
@@ -106,8 +106,10 @@ def save(name, **arrays):
 
 
 # ------------------------------------------------------------------------------- walks
-def dataset_fixture(name, ds_cls, seed, walks_per_node, walk_length, method, method_params=None):
-    """F1/F2/F4: one epoch of RandomWalkDataset iteration under random.seed(seed)."""
+def dataset_fixture(name, ds_cls, seed, walks_per_node, walk_length, method, method_params=None,
+                    extra=None):
+    """F1/F2/F4: one epoch of RandomWalkDataset iteration under random.seed(seed). ``extra``:
+    more arrays to store, or a function of the dataset returning them."""
     random.seed(seed)
     kwargs = dict(walks_per_node=walks_per_node, walk_length=walk_length, method=method)
     if method_params is not None:
@@ -130,7 +132,8 @@ def dataset_fixture(name, ds_cls, seed, walks_per_node, walk_length, method, met
     p = q = 1.0
     if method_params:
         p, q = float(method_params.get('p', 1.0)), float(method_params.get('q', 1.0))
-    save(name, seed=seed, walks_per_node=walks_per_node, walk_length=L,
+    more = extra(ds) if callable(extra) else (extra or {})
+    save(name, **more, seed=seed, walks_per_node=walks_per_node, walk_length=L,
          method=np.array(method), p=p, q=q, itos=np.array(itos), row_ptr=row_ptr, col=col,
          weights=w, weighted=weighted, order=order, order_after=order_after,
          starts=ids[:, 0].copy(), uniforms=u, walks=ids,
@@ -344,7 +347,98 @@ def cbow_fixtures():
                  mode='cbow', max_norm=1.0)
 
 
+def trajectory128_fixture(name='traj_d128_k5_r5.npz', V=1025, d=128, R=5, K=5, lr=0.01, L=40,
+                         batch_walks=16, steps=24, init_seed=51, noise_seed=52, walk_seed=53):
+    """§8c trajectory parity at the bench's shape: >= 20 reference Adam steps at d=128, K=5,
+    R=5, lr 0.01 (bench.py's lr) through the reference's SkipGram / NegativeSamplingLoss /
+    generate_noise_batch + torch.optim.Adam (trainer.py:131-152 wiring). Walks are uniform ids
+    (the SGNS step does not depend on where they come from); every step trains a new batch."""
+    torch.manual_seed(init_seed)
+    model = SkipGram(vocab_size=V, embedding_size=d, max_norm=None)
+    w_in0 = model._input_embedding.weight.detach().numpy().copy()
+    w_out0 = model._output_embedding.weight.detach().numpy().copy()
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    loss_fn = NegativeSamplingLoss()
+    walks = np.random.default_rng(walk_seed).integers(1, V, size=(steps, batch_walks, L))
+    torch.manual_seed(noise_seed)
+    noises, losses = [], []
+    for step in range(steps):
+        inputs, targets = sg_windows(walks[step], R)
+        B, C = targets.shape
+        noise = generate_noise_batch(B, C, K, V).numpy()
+        opt.zero_grad()
+        loss, _, _ = reference_step(model, loss_fn, inputs, targets, noise)
+        loss['loss'].backward()
+        opt.step()
+        noises.append(noise)
+        losses.append([float(loss['loss']), float(loss['positive-loss']),
+                       float(loss['negative-loss'])])
+    save(name, V=V, d=d, R=R, K=K, lr=lr, init_seed=init_seed, noise_seed=noise_seed,
+         walks=walks.astype(np.int16), noise=np.stack(noises).astype(np.int16), w_in0=w_in0,
+         w_out0=w_out0, w_in=model._input_embedding.weight.detach().numpy(),
+         w_out=model._output_embedding.weight.detach().numpy(), losses=np.array(losses))
+
+
+CORA_SUBJECTS = ['Case_Based', 'Genetic_Algorithms', 'Neural_Networks',
+                 'Probabilistic_Methods', 'Reinforcement_Learning', 'Rule_Learning', 'Theory']
+
+
+def synthetic_cora(n_papers=240, n_cites=520, seed=17):
+    """cora.cites / cora.content in the real files' format (tab-separated; content rows: paper
+    id, 1,433 binary word features, subject). Paper ids are sparse ints as in Cora; citations
+    include reverse duplicates (nx merges them) and every paper has at least one citation."""
+    rng = np.random.default_rng(seed)
+    ids = np.sort(rng.choice(np.arange(30, 1_200_000), size=n_papers, replace=False))
+    pairs = [(int(ids[i]), int(ids[rng.integers(n_papers)])) for i in range(n_papers)]
+    while len(pairs) < n_cites:
+        a, b = rng.integers(n_papers, size=2)
+        pairs.append((int(ids[a]), int(ids[b])))
+    pairs += [(b, a) for a, b in pairs[:12]]          # reverse duplicates
+    pairs = [(a, b) for a, b in pairs if a != b]
+    cites = ''.join(f'{a}\t{b}\n' for a, b in pairs)
+    rows = []
+    for pid in rng.permutation(ids):
+        feats = (rng.random(1433) < 0.013).astype(int)
+        rows.append('\t'.join([str(pid)] + [str(x) for x in feats]
+                              + [CORA_SUBJECTS[rng.integers(len(CORA_SUBJECTS))]]))
+    return cites, ''.join(r + '\n' for r in rows)
+
+
+def cora_fixture(name='walks_cora_node2vec_p1_q2.npz'):
+    """§8 C2's ingest path: the reference's CoraDataset (datasets.py:183-221) on synthetic
+    cora.cites / cora.content (the real files are not shipped), read through a temporary
+    ASSETS_PATH: one epoch of node2vec p=1 q=2 walks (configs/sge_sg_cora.yaml's walker),
+    the start order, the labels and a sample of the features."""
+    import tempfile
+    cites, content = synthetic_cora()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, 'cora'))
+        with open(os.path.join(tmp, 'cora', 'cora.cites'), 'w') as f:
+            f.write(cites)
+        with open(os.path.join(tmp, 'cora', 'cora.content'), 'w') as f:
+            f.write(content)
+        ref_ds.ASSETS_PATH = tmp
+
+        def extra(ds):
+            names = sorted(ds.labels)
+            feat = np.stack([ds.features[n] for n in names[:16]]).astype(np.uint8)
+            return dict(cites_txt=np.frombuffer(cites.encode(), np.uint8),
+                        content_txt=np.frombuffer(content.encode(), np.uint8),
+                        label_names=np.array(names), label_values=np.array(
+                            [ds.labels[n] for n in names]),
+                        feature_sample=feat, n_nodes=ds.graph.number_of_nodes(),
+                        n_edges=ds.graph.number_of_edges())
+        dataset_fixture(name, ref_ds.CoraDataset, seed=43, walks_per_node=2, walk_length=10,
+                        method='node2vec', method_params={'p': 1, 'q': 2}, extra=extra)
+
+
 def main():
+    if sys.argv[1:] == ['cora']:
+        cora_fixture()
+        return
+    if sys.argv[1:] == ['traj128']:
+        trajectory128_fixture()
+        return
     if sys.argv[1:] == ['downstream']:
         downstream_fixture('downstream_split_ops.npz')
         return
@@ -386,6 +480,8 @@ def main():
     # §8f 3: downstream split algorithms + edge operators
     downstream_fixture('downstream_split_ops.npz')
     cbow_fixtures()
+    cora_fixture()
+    trajectory128_fixture()
     with open(os.path.join(HERE, 'golden_info.json'), 'w') as f:
         json.dump(info, f, indent=2)
 

@@ -197,3 +197,54 @@ def test_fused_trainer_step_equals_unfused(hip_device, d):
         assert float(of.state[pf]['step']) == float(ou.state[pu]['step']) == 5.0
         np.testing.assert_allclose(of.state[pf]['exp_avg'].cpu().numpy(),
                                    ou.state[pu]['exp_avg'].cpu().numpy(), rtol=1e-3, atol=1e-6)
+
+
+def test_d128_trajectory_matches_reference(hip_device):
+    """24 reference training steps at the bench's shape (d=128, K=5, R=5, lr 0.01;
+    traj_d128_k5_r5.npz from the reference's SkipGram / loss / generate_noise_batch +
+    torch.optim.Adam) through the user-facing fused step: Word2VecTrainer.training_step on
+    device walk batches with noise='torch' (the reference's negative stream) and the HIP Adam
+    (out-table Adam fused into the records gather, in-table Adam on the side stream).
+
+    Stated tolerance: per-step loss rtol 1e-4; final tables rtol 1e-4 / atol 1e-5 on at least
+    99.99% of the entries and no entry off by more than lr / 10 (an entry whose gradient is a
+    near-cancelling sum can have its Adam step flipped by the summation order). The envelope
+    of the reference itself against its float64-exact-sum rerun is printed for comparison."""
+    from oracle import sgns_ref
+    f = golden('traj_d128_k5_r5.npz')
+    V, d, R, K, lr = int(f['V']), int(f['d']), int(f['R']), int(f['K']), float(f['lr'])
+    torch.manual_seed(int(f['init_seed']))
+    model = SkipGram(V, d)
+    np.testing.assert_array_equal(model.input_embedding.numpy(), f['w_in0'])
+    np.testing.assert_array_equal(model.output_embedding.numpy(), f['w_out0'])
+    model = model.cuda()
+    opt = Adam(model.parameters(), lr=lr)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1000, gamma=1.0)
+    tr = Word2VecTrainer(model, opt, sched, neg_samples=K, vocab_size=V, noise='torch',
+                         context_radius=R)
+    tr.manual_grads = True
+    torch.manual_seed(int(f['noise_seed']))
+    losses = []
+    for step in range(f['walks'].shape[0]):
+        walks = torch.as_tensor(f['walks'][step].astype(np.int32)).to(hip_device)
+        out = tr.training_step(walks)
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(out['loss']))
+    assert bool(opt._alt)                         # the fused step ran
+    np.testing.assert_allclose(losses, f['losses'][:, 0], rtol=1e-4)
+    batches = []
+    for step in range(f['walks'].shape[0]):
+        ins, tgt = sgns_ref.sg_windows(f['walks'][step].astype(np.int64), R)
+        batches.append((ins, tgt, f['noise'][step].astype(np.int64)))
+    from test_gpu_sgns import reference_envelope
+    ex_in, ex_out = reference_envelope(f['w_in0'], f['w_out0'], lr, batches)
+    for name, got, exp, ex in (('w_in', model.input_embedding.numpy(), f['w_in'], ex_in),
+                               ('w_out', model.output_embedding.numpy(), f['w_out'], ex_out)):
+        bad = ~np.isclose(got, exp, rtol=1e-4, atol=1e-5)
+        bad_ex = ~np.isclose(ex, exp, rtol=1e-4, atol=1e-5)
+        print(f'{name}: {bad.sum()} / {bad.size} outside rtol 1e-4 / atol 1e-5, max |diff| '
+              f'{np.abs(got - exp).max():.3e}; reference vs its exact-sum rerun: {bad_ex.sum()} '
+              f'outside, max |diff| {np.abs(ex - exp).max():.3e}')
+        assert bad.mean() <= 1e-4, f'{name}: {bad.sum()} entries outside tolerance'
+        assert np.abs(got - exp).max() <= lr / 10

@@ -292,3 +292,29 @@ def test_node2vec_lane_groups_give_identical_walks(hip_device):
         assert torch.equal(big[:40_000], mid)
         assert torch.equal(big[:4096], small)
         assert (big > 0).all()
+
+
+def test_cora_epoch_end_to_end_bit_exact(tmp_path, monkeypatch, hip_device):
+    """C2's real ingest path: CoraDataset parses the cora.cites / cora.content files the
+    reference parsed (synthetic, tests/golden/make_golden.py cora), then random.seed(s) gives
+    the reference's epoch of node2vec p=1 q=2 walks through the batched device path."""
+    import os
+    import shallow_encoders.graph.datasets as ds_mod
+    f = golden('walks_cora_node2vec_p1_q2.npz')
+    d = tmp_path / 'cora'
+    os.makedirs(d)
+    (d / 'cora.cites').write_bytes(f['cites_txt'].tobytes())
+    (d / 'cora.content').write_bytes(f['content_txt'].tobytes())
+    monkeypatch.setattr(ds_mod, 'ASSETS_PATH', str(tmp_path))
+    random.seed(int(f['seed']))
+    ds = ds_mod.CoraDataset(walks_per_node=int(f['walks_per_node']),
+                            walk_length=int(f['walk_length']), method='node2vec',
+                            method_params={'p': 1, 'q': 2})
+    got = []
+    while True:
+        b = ds.next_walk_batch(64)
+        if b is None:
+            break
+        got.append(b.cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate(got), f['walks'])
+    np.testing.assert_array_equal(ds._node_ids, f['order_after'])

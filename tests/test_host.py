@@ -296,3 +296,37 @@ def test_native_shuffle_matches_cpython(n, seed):
     after_got = [random.random() for _ in range(5)]
     assert np.array_equal(got, np.asarray(ref, dtype=np.int64))
     assert after_got == after_ref
+
+
+def _cora_assets(f, root):
+    d = os.path.join(root, 'cora')
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, 'cora.cites'), 'wb') as fh:
+        fh.write(f['cites_txt'].tobytes())
+    with open(os.path.join(d, 'cora.content'), 'wb') as fh:
+        fh.write(f['content_txt'].tobytes())
+    return root
+
+
+def test_cora_ingest_matches_reference(tmp_path, monkeypatch):
+    """C2's ingest path: CoraDataset (datasets.py:183-221) on the synthetic cora.cites /
+    cora.content the reference itself parsed (tests/golden/make_golden.py cora): the same graph,
+    vocabulary, CSR in networkx neighbour order, start-node order, labels and features."""
+    import shallow_encoders.graph.datasets as ds_mod
+    f = golden('walks_cora_node2vec_p1_q2.npz')
+    monkeypatch.setattr(ds_mod, 'ASSETS_PATH', _cora_assets(f, str(tmp_path)))
+    random.seed(int(f['seed']))
+    ds = ds_mod.CoraDataset(walks_per_node=int(f['walks_per_node']),
+                            walk_length=int(f['walk_length']), method='node2vec',
+                            method_params={'p': 1, 'q': 2})
+    assert ds.graph.number_of_nodes() == int(f['n_nodes'])
+    assert ds.graph.number_of_edges() == int(f['n_edges'])
+    assert list(ds.csr.itos) == list(f['itos'])
+    np.testing.assert_array_equal(ds.csr.row_ptr, f['row_ptr'])
+    np.testing.assert_array_equal(ds.csr.col, f['col'])
+    np.testing.assert_array_equal(ds._node_ids, f['order'])
+    names = list(f['label_names'])
+    assert sorted(ds.labels) == names
+    assert [ds.labels[n] for n in names] == list(f['label_values'])
+    np.testing.assert_array_equal(np.stack([ds.features[n] for n in names[:16]]),
+                                  f['feature_sample'])

@@ -190,3 +190,24 @@ def test_closed_form_torch_and_windows_torch_equal_numpy_forms():
     np.testing.assert_allclose(go.numpy(), go64, rtol=1e-12, atol=1e-18)
     assert float(sums[0] + sums[1]) / tgt.size == pytest.approx(float(f['losses'][0][0]),
                                                                 rel=1e-5)
+
+
+def test_oracle_d128_trajectory_matches_reference():
+    """24 reference Adam steps at d=128, K=5, R=5, lr 0.01 (traj_d128_k5_r5.npz): the oracle
+    replays the losses and final tables, and the fixture's negatives are torch's global stream
+    after manual_seed(noise_seed) (what Word2VecTrainer(noise='torch') draws)."""
+    import torch
+    from shallow_encoders.word2vec.utils.sampling import generate_noise_batch
+    f = golden('traj_d128_k5_r5.npz')
+    R, K, V = int(f['R']), int(f['K']), int(f['V'])
+    ref = sgns_ref.TorchAdamRef(f['w_in0'], f['w_out0'], lr=float(f['lr']))
+    torch.manual_seed(int(f['noise_seed']))
+    for step in range(f['walks'].shape[0]):
+        ins, tgt = sgns_ref.sg_windows(f['walks'][step].astype(np.int64), R)
+        noise = generate_noise_batch(len(ins), 2 * R, K, V).numpy()
+        np.testing.assert_array_equal(noise, f['noise'][step])
+        loss = ref.train_step(ins, tgt, noise)
+        assert loss['loss'] == pytest.approx(float(f['losses'][step][0]), rel=1e-6)
+    w_in, w_out = ref.tables()
+    np.testing.assert_allclose(w_in, f['w_in'], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(w_out, f['w_out'], rtol=1e-5, atol=1e-7)
