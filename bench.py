@@ -52,46 +52,101 @@ def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     return 8 * d * (1 + K) + 8 * d / (2 * R) + 8 * (1 + K) + 8 / (2 * R)
 
 
+def walk_line_rates(table_bytes: int):
+    """The random-line rates measured on MI355X by scripts/microbench/random_lines.hip
+    (profiles/r02_random_lines.json) for the table size nearest ``table_bytes``: independent
+    16-B gathers and 1M dependent chains over a table of 16-B entries."""
+    path = os.path.join(REPO, 'profiles', 'r02_random_lines.json')
+    try:
+        with open(path) as f:
+            rows = [json.loads(x) for x in f if x.strip().startswith('{')]
+    except OSError:
+        return None
+    if not rows:
+        return None
+    mib = table_bytes / 2 ** 20
+    r = min(rows, key=lambda x: abs(math.log(x['table_MiB'] / mib)))
+    return dict(r, source=f'profiles/r02_random_lines.json ({r["table_MiB"]} MiB table)')
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(csr, args, budget_s: float):
-    """The oracle (reference algorithm restated on the CPU) on a bounded sample."""
+def cpu_baseline(csr, args, budget_s: float, walk_methods):
+    """The oracle port of the reference's CPU path (cross-checked against the reference itself
+    in the build container: identical outputs; speed in profiles/r02_cpu_crosscheck.log), timed
+    on this host on bounded samples of the same workload:
+      * SGNS steps (torch-CPU restatement of model.py / loss.py + autograd + torch.optim.Adam,
+        the whole V x d tables) at the reference configs' 64 walks per step and at the GPU
+        line's batch (like-for-like: ``value``);
+      * the walkers, 1 core, with the reference's per-step work on networkx's adjacency layout
+        (oracle NxLikeGraph): DeepWalk and node2vec with the GPU walk bench's (p, q)."""
     from oracle import sgns_ref, walk_ref
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    V, d, R, K = csr.vocab_size, args.dim, args.radius, args.neg
+    V, d, R, K, L = csr.vocab_size, args.dim, args.radius, args.neg, args.walk_length
     rng = np.random.default_rng(0)
     w_in, w_out = sgns_ref.xavier_tables(V, d, seed=0)
     ref = sgns_ref.TorchAdamRef(w_in, w_out, lr=args.lr)
-    # the reference's own batch: 64 walks per step (configs: batch_size 64)
-    walks = rng.integers(1, V, size=(64, args.walk_length)).astype(np.int32)
-    ins, tgt = sgns_ref.sg_windows(walks, R)
-    ref.train_step(ins, tgt, rng.integers(0, V, size=(len(ins), 2 * R, K)))  # state alloc
-    t0, steps = time.perf_counter(), 0
-    while time.perf_counter() - t0 < budget_s * 0.7 or steps < 2:
-        ref.train_step(ins, tgt, rng.integers(0, V, size=(len(ins), 2 * R, K)))
-        steps += 1
-    sgns_dt = time.perf_counter() - t0
-    pairs_per_s = steps * tgt.size / sgns_dt
-    # walker: the reference's per-step algorithm (Python, one process)
-    g = walk_ref.CSR(csr.row_ptr, csr.host_col())
-    n_w, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s * 0.3 or n_w < 1:
-        s = int(rng.integers(1, V))
-        walk_ref.deepwalk_walk(g, s, args.walk_length, rng.random(args.walk_length - 1))
-        n_w += 1
-    walk_dt = time.perf_counter() - t0
+
+    def batch(bw):
+        walks = torch.from_numpy(rng.integers(1, V, size=(bw, L)).astype(np.int32))
+        ins, tgt = sgns_ref.sg_windows_torch(walks, R)
+        return ins.numpy(), tgt.numpy(), rng.integers(0, V, size=(ins.shape[0], 2 * R, K))
+
+    ref.train_step(*batch(64))                 # allocates the Adam state
+    samples = []
+    for bw in sorted({64, args.batch_walks}):
+        ins, tgt, noise = batch(bw)
+        steps, t = 0, 0.0
+        while steps < 1 or (bw == 64 and t < 0.3 * budget_s):
+            a = time.perf_counter()
+            ref.train_step(ins, tgt, noise)
+            t += time.perf_counter() - a
+            steps += 1
+            if bw == 64:
+                ins, tgt, noise = batch(bw)
+        samples.append({'batch_walks': bw, 'pairs_per_step': int(tgt.size), 'steps': steps,
+                        'seconds': t, 'pairs_per_s': steps * tgt.size / t})
+    del ref
+    a = time.perf_counter()
+    g = walk_ref.NxLikeGraph(csr.row_ptr, csr.host_col(), csr.itos)
+    build_s = time.perf_counter() - a
+    names = csr.itos
+    walkers = {}
+    for meth, p, q in walk_methods:
+        # node2vec at C3 costs seconds per walk (a hub step scans ~44K neighbour lists): time
+        # steps of length-10 walks from uniform starts and quote walks of L as steps / (L-1)
+        wl = L if meth == 'deepwalk' else min(L, 10)
+        steps, a = 0, time.perf_counter()
+        while steps == 0 or time.perf_counter() - a < 0.2 * budget_s:
+            s0 = names[int(rng.integers(1, V))]
+            u = rng.random(wl - 1).tolist()
+            if meth == 'deepwalk':
+                walk_ref.deepwalk_walk(g, s0, wl, u)
+            else:
+                walk_ref.node2vec_walk(g, s0, wl, p, q, u, listscan=True)
+            steps += wl - 1
+        dt = time.perf_counter() - a
+        walkers[meth] = {'p': p, 'q': q, 'sample_walk_length': wl, 'steps': steps,
+                         'seconds': dt, 'steps_per_s': steps / dt,
+                         'walks_per_s': steps / dt / (L - 1)}
+    del g
+    like = next(x for x in samples if x['batch_walks'] == args.batch_walks)
     return {
-        'value': pairs_per_s, 'unit': 'positive-pairs/s', 'cores': threads, 'kind': 'port',
+        'value': like['pairs_per_s'], 'unit': 'positive-pairs/s', 'cores': threads, 'kind': 'port',
         'sample': (f'oracle SGNS step (torch-CPU restatement of model.py/loss.py + autograd + '
-                   f'torch.optim.Adam, V={V}, d={d}, K={K}, R={R}, 64 walks x L={args.walk_length}'
-                   f' = {tgt.size} pairs/step) x {steps} steps in {sgns_dt:.1f}s, '
-                   f'{threads} torch threads; walker: {n_w} oracle DeepWalk walks (Python, 1 core)'
-                   f' in {walk_dt:.1f}s'),
-        'walks_per_s': n_w / walk_dt,
+                   f'torch.optim.Adam over the whole V={V} x d={d} tables, K={K}, R={R}, L={L}) at '
+                   f'the GPU line\'s {args.batch_walks} walks/step ({like["steps"]} step(s), '
+                   f'{like["seconds"]:.1f}s) and at the reference configs\' 64 walks/step, '
+                   f'{threads} torch threads; walkers: the reference\'s per-step algorithm on '
+                   f'networkx\'s adjacency layout (built in {build_s:.1f}s), 1 core, '
+                   f'{0.2 * budget_s:.0f}s each'),
+        'batches': samples,
+        'walkers': walkers,
+        'walks_per_s': {m: w['walks_per_s'] for m, w in walkers.items()},
     }
 
 
@@ -518,12 +573,16 @@ def main():
                       'GBps': phase_bytes[k] / (phases[k] * 1e-3) / 1e9 if phases[k] else None}
                   for k in ('pass1', 'sort', 'pass2')}
 
-    # ---- walker alone: walks/s (DeepWalk over one walk per node; node2vec sample) ------------
-    walk_stats = {}
+    # ---- walker alone: walks/s, roofline, and the bit-exact replay walker ---------------------
+    p2, q2 = (args.p, args.q) if args.method == 'node2vec' else (0.25, 4.0)
+    walk_methods = (('deepwalk', 1.0, 1.0), ('node2vec', p2, q2))
+    walk_stats, walk_roof, replay_stats = {}, {}, {}
+    line_rate = walk_line_rates(csr.nnz * 16)
     if not args.no_walk_bench:
         # one walk per node (N walks) for both: a sample far beyond the ~50K walkers the chip
         # keeps in flight, so no partial last round of walkers skews the rate
-        for meth, n_walks, p, q in (('deepwalk', N, 1.0, 1.0), ('node2vec', N, 0.25, 4.0)):
+        for meth, p, q in walk_methods:
+            n_walks = N
             w = (Node2Vec(csr, L, p=p, q=q, rng='philox', seed=7, device=dev)
                  if meth == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=7, device=dev))
             st = torch.arange(1, n_walks + 1, dtype=torch.int32, device=dev)
@@ -532,16 +591,65 @@ def main():
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a = time.perf_counter()
+            e0.record()
             w.walk_batch(st, walk_id0=rank * n_walks, out=out, check=False)
+            e1.record()
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - a
+            kern_s = e0.elapsed_time(e1) * 1e-3
             if world > 1:
                 t = torch.tensor([dt], dtype=torch.float64, device=dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 dt = float(t)
             walk_stats[meth] = n_walks * world / dt
+            steps = n_walks * (L - 1)
+            if meth == 'deepwalk':
+                # the edge-inline walker: the start's row_ptr pair, one 16-B entry per step
+                # (+ prob_thr / alias on weighted graphs), the walk's L int32 ids
+                per_step = 16 + (8 if csr.weights is not None else 0)
+                nbytes = n_walks * (16 + (L - 1) * per_step + 4 * L)
+                extra = {'bytes_per_step': per_step + 4.0, 'dependent_loads_per_step': 1}
+                if line_rate:
+                    extra['random_line_roofline'] = {
+                        'steps_per_s': steps / kern_s,
+                        'chase_lines_per_s': line_rate['chase_lines_per_s'],
+                        'gather_lines_per_s': line_rate['gather_lines_per_s'],
+                        'frac_of_chase': steps / kern_s / line_rate['chase_lines_per_s'],
+                        'frac_of_gather': steps / kern_s / line_rate['gather_lines_per_s'],
+                        'source': line_rate['source']}
+            else:
+                # realised traffic of the same walks (dw_walk_fast_counted, untimed launch)
+                c = w.count_traffic(st, walk_id0=rank * n_walks, out=out)
+                nbytes = c['bytes']
+                extra = {'bytes_per_step': c['bytes'] / max(c['steps'], 1),
+                         'proposal_blocks_per_step': c['blocks'] / max(c['steps'], 1),
+                         'adjacency_tests_per_step': c['tests'] / max(c['steps'], 1)}
+            gbs = nbytes / kern_s / 1e9
+            walk_roof[meth] = dict({'kernel_ms': kern_s * 1e3, 'walks': n_walks, 'bytes': nbytes,
+                                    'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                    'frac': gbs / HBM_PEAK_GBS, 'p': p, 'q': q}, **extra)
             del out
+        # the reference-exact walker (rng='python', dw_walk_replay): CPython's uniforms drawn on
+        # the host and copied in (8 B per step), fp64 choices arithmetic, a bounded sample
+        if rank == 0 and world == 1:
+            import random as _random
+            from shallow_encoders.graph.rng import draw_uniforms
+            for meth, p, q in walk_methods:
+                n_r = 65_536 if meth == 'deepwalk' else 4_096
+                w = (Node2Vec(csr, L, p=p, q=q, device=dev) if meth == 'node2vec'
+                     else DeepWalk(csr, L, device=dev))
+                gen = _random.Random(0)
+                st = torch.arange(1, n_r + 1, dtype=torch.int32)
+                w.walk_batch(st[:64], uniforms=draw_uniforms(64 * (L - 1), gen))
+                u = draw_uniforms(n_r * (L - 1), gen)
+                torch.cuda.synchronize(dev)
+                a = time.perf_counter()
+                w.walk_batch(st, uniforms=u)
+                torch.cuda.synchronize(dev)
+                replay_stats[meth] = {'walks': n_r, 'p': p, 'q': q,
+                                      'walks_per_s': n_r / (time.perf_counter() - a)}
 
     result = {
         'metric': 'positive-pairs/s + random-walks/s, 1M-node d=128 k=5, 1/2/4/8 MI355X',
@@ -586,7 +694,9 @@ def main():
         'in_exchange': args.in_exchange if owner else None,
         'in_exchange_calibration_ms_per_step': calib_ms,
         'walks_per_s': walk_stats.get('deepwalk'),
-        'walks_per_s_node2vec_p0.25_q4': walk_stats.get('node2vec'),
+        f'walks_per_s_node2vec_p{p2:g}_q{q2:g}': walk_stats.get('node2vec'),
+        'roofline_walk': walk_roof or None,
+        'walks_per_s_replay': replay_stats or None,
         'kernel_ms': kern_ms,
         'records_per_step_per_gpu': n_rec[0] if owner else pairs_per_step * (1 + K),
         'mean_loss': mean_loss,
@@ -635,7 +745,7 @@ def main():
         except (OSError, ValueError):
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ('c2', 'c3'):
-        cb = cpu_baseline(csr, args, args.cpu_budget)
+        cb = cpu_baseline(csr, args, args.cpu_budget, walk_methods)
         result['cpu_baseline'] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)

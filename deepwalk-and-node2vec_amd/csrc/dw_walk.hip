@@ -354,11 +354,12 @@ __device__ __forceinline__ uint32_t group_ballot(bool pred, int q) {
 // dependent loads (6 at G=8 for the largest C3 hub, 44,848 neighbours), no LDS staging.
 template <int N2V_G>
 __device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list, int64_t n,
-                                               int32_t key, int gl, int q) {
+                                               int32_t key, int gl, int q, uint32_t &bytes) {
     int64_t lo = 0, len = n;
     while (len > N2V_G) {
         const int64_t idx = lo + (static_cast<int64_t>(gl) * len) / N2V_G;
         const int32_t sv = list[idx];
+        bytes += 4 * N2V_G;
         if (group_ballot<N2V_G>(sv == key, q)) return true;
         const int c = __popc(group_ballot<N2V_G>(sv < key, q));  // splitters below key: 0 .. c-1
         if (c == 0) return false;                          // key < list[lo]
@@ -368,6 +369,7 @@ __device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list,
         len = s1 - s0;
     }
     const bool hit = gl < len && list[lo + gl] == key;
+    bytes += 4 * static_cast<uint32_t>(len);
     return group_ballot<N2V_G>(hit, q) != 0u;
 }
 
@@ -377,11 +379,12 @@ __device__ __forceinline__ bool group_contains(const int32_t *__restrict__ list,
 // bucket almost always decides; nb probes bound the loop.
 template <int N2V_G>
 __device__ __forceinline__ bool group_hash_contains(const int32_t *__restrict__ tab, uint32_t nb,
-                                                    int32_t key, int gl, int q) {
+                                                    int32_t key, int gl, int q, uint32_t &bytes) {
     constexpr int PER = 16 / N2V_G;
     uint32_t b = dw::adj_bucket(key, nb);
     for (uint32_t t = 0; t < nb; ++t) {
         const int32_t *slot = tab + (int64_t)b * 16 + gl * PER;
+        bytes += 64;
         bool hit = false, free_slot = false;
         if constexpr (PER == 4) {
             const int4 e = *reinterpret_cast<const int4 *>(slot);
@@ -407,7 +410,8 @@ __device__ __forceinline__ bool group_hash_contains(const int32_t *__restrict__ 
 // reads it N2V_G entries at a time.
 template <int N2V_G>
 __device__ __forceinline__ bool small_contains(const int32_t *__restrict__ list, int64_t n,
-                                               int32_t key, int gl, int q) {
+                                               int32_t key, int gl, int q, uint32_t &bytes) {
+    bytes += 4 * static_cast<uint32_t>(n);
     bool hit = false;
     for (int64_t t = gl; t < n; t += N2V_G) hit = hit || list[t] == key;
     return group_ballot<N2V_G>(hit, q) != 0u;
@@ -424,7 +428,10 @@ __device__ __forceinline__ bool small_contains(const int32_t *__restrict__ list,
 // each by one group-cooperative search of N(prev): HASH = false, an N2V_G-ary search of the
 // sorted list `nbr` (col_sorted); HASH = true, one probe of prev's adjacency hash, or for a row
 // without one (degree <= DW_ADJ_HASH_MIN_DEG) one load of its list `nbr` (= col, unsorted).
-template <int N2V_G, bool HASH>
+// STATS (dw_walk_fast_counted, a diagnostic launch; the walks are the same): every walker's
+// realised load/store bytes, steps, proposal blocks and adjacency tests, summed per wave and
+// added to counters[0..3] once per wave.
+template <int N2V_G, bool HASH, bool STATS>
 __global__ void __launch_bounds__(N2V_WAVES *WAVE)
     k_walk_node2vec_fast(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
                          const int32_t *__restrict__ nbr, const int64_t *__restrict__ adj_off,
@@ -432,7 +439,10 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                          const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                          int32_t L, N2VThr thr, uint32_t k0, uint32_t k1, uint64_t walk_id0,
-                         int32_t *__restrict__ out, int32_t *status) {
+                         int32_t *__restrict__ out, int32_t *status,
+                         unsigned long long *counters) {
+    uint32_t c_bytes = 0, c_steps = 0, c_blocks = 0, c_tests = 0;   // STATS only
+    const uint32_t pick_bytes = prob_thr ? 12u : 4u;   // col (+ prob_thr, alias) per proposal
     const int lane = threadIdx.x & (WAVE - 1);
     const int q = lane / N2V_G, gl = lane & (N2V_G - 1);
     const int wv = threadIdx.x / WAVE;
@@ -476,11 +486,16 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                 if (gl == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
                 break;
             }
+            if constexpr (STATS) {
+                c_steps += 1;
+                c_bytes += (HASH ? 32u : 16u) + 4u;   // row_ptr (+ adj_off) pairs, the output
+            }
             int32_t nxt;
             if (prev < 0) {  // first step: prev_node is None -> unbiased (random_walk_generator.py:97)
                 const dw::U4 r = dw::philox(
                     dw::U4{c0, c1, static_cast<uint32_t>(s) << 8, dw::TAG_NODE2VEC}, k0, k1);
                 nxt = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+                if constexpr (STATS) c_bytes += pick_bytes;
             } else {
                 nxt = -1;
                 for (uint32_t round = 0; round < DW_MAX_REJECTION_ROUNDS && nxt < 0; ++round) {
@@ -491,6 +506,10 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                                    dw::TAG_NODE2VEC ^ round},
                             k0, k1);
                         const int32_t x = col[a + first_order_pick(r.x, r.y, a, n, prob_thr, alias)];
+                        if constexpr (STATS) {
+                            c_blocks += 1;
+                            c_bytes += N2V_G * pick_bytes;
+                        }
                         const uint64_t u = r.z;
                         const bool sure = (x == prev) ? (u < Tp) : (u < Tlo);
                         const bool amb = x != prev && u >= Tlo && u < Thi;
@@ -503,11 +522,16 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                             const int l = __ffs(m_amb) - 1;
                             const int32_t xl = __shfl(x, q * N2V_G + l, WAVE);
                             bool adj;
+                            uint32_t tb = 0;
                             if (HASH && pnb > 0)
-                                adj = group_hash_contains<N2V_G>(adj_hash + ph, pnb, xl, gl, q);
+                                adj = group_hash_contains<N2V_G>(adj_hash + ph, pnb, xl, gl, q, tb);
                             else
-                                adj = HASH ? small_contains<N2V_G>(nbr + pa, pn, xl, gl, q)
-                                           : group_contains<N2V_G>(nbr + pa, pn, xl, gl, q);
+                                adj = HASH ? small_contains<N2V_G>(nbr + pa, pn, xl, gl, q, tb)
+                                           : group_contains<N2V_G>(nbr + pa, pn, xl, gl, q, tb);
+                            if constexpr (STATS) {
+                                c_tests += 1;
+                                c_bytes += tb;
+                            }
                             if (adj == adj_wins) {
                                 win = l;
                                 break;
@@ -535,6 +559,15 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
         }
         if (gl == 0)
             for (; s < L; ++s) o[s] = -1;
+    }
+    if constexpr (STATS) {   // one group lane counts; sum the wave, one atomic per counter
+        uint32_t v4[4] = {gl == 0 ? c_bytes : 0u, gl == 0 ? c_steps : 0u,
+                          gl == 0 ? c_blocks : 0u, gl == 0 ? c_tests : 0u};
+        for (int k = 0; k < 4; ++k) {
+            unsigned long long x = v4[k];
+            for (int off = WAVE / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, WAVE);
+            if (lane == 0) atomicAdd(counters + k, x);
+        }
     }
 }
 
@@ -565,7 +598,8 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
                     const int64_t *adj_off, const int32_t *adj_hash, const uint32_t *prob_thr,
                     const int32_t *alias, int64_t n_rows, const int32_t *starts, int64_t n_walks,
                     int32_t walk_length, double p, double q, uint32_t k0, uint32_t k1,
-                    uint64_t walk_id0, int32_t *out, int32_t *status, void *stream) {
+                    uint64_t walk_id0, int32_t *out, int32_t *status, void *stream,
+                    unsigned long long *counters = nullptr) {
     DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_fast: p and q must be positive");
     const double ip = 1.0 / p, iq = 1.0 / q;
     double amax = 1.0;
@@ -584,24 +618,31 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
     }();
     // resident walkers at 16 and 8 lanes (occupancy query once per process: one GPU model)
     static const int64_t cap16 = node2vec_capacity(
-        reinterpret_cast<const void *>(&k_walk_node2vec_fast<16, HASH>), 16);
+        reinterpret_cast<const void *>(&k_walk_node2vec_fast<16, HASH, false>), 16);
     static const int64_t cap8 = node2vec_capacity(
-        reinterpret_cast<const void *>(&k_walk_node2vec_fast<8, HASH>), 8);
+        reinterpret_cast<const void *>(&k_walk_node2vec_fast<8, HASH, false>), 8);
     const int group = forced ? forced : n_walks <= cap16 ? 16 : n_walks <= cap8 ? 8 : 4;
     const int64_t per_block = N2V_WAVES * (WAVE / group);
     int64_t blocks = (n_walks + per_block - 1) / per_block;
     if (blocks > 8192) blocks = 8192;
-#define DW_N2V_LAUNCH(G)                                                                       \
-    hipLaunchKernelGGL((k_walk_node2vec_fast<G, HASH>), dim3((unsigned)blocks),                \
+#define DW_N2V_LAUNCH(G, ST)                                                                   \
+    hipLaunchKernelGGL((k_walk_node2vec_fast<G, HASH, ST>), dim3((unsigned)blocks),            \
                        dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,    \
                        adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks, walk_length, \
-                       thr, k0, k1, walk_id0, out, status)
-    if (group == 4)
-        DW_N2V_LAUNCH(4);
+                       thr, k0, k1, walk_id0, out, status, counters)
+    if (counters) {
+        if (group == 4)
+            DW_N2V_LAUNCH(4, true);
+        else if (group == 8)
+            DW_N2V_LAUNCH(8, true);
+        else
+            DW_N2V_LAUNCH(16, true);
+    } else if (group == 4)
+        DW_N2V_LAUNCH(4, false);
     else if (group == 8)
-        DW_N2V_LAUNCH(8);
+        DW_N2V_LAUNCH(8, false);
     else
-        DW_N2V_LAUNCH(16);
+        DW_N2V_LAUNCH(16, false);
 #undef DW_N2V_LAUNCH
     DW_LAUNCH_CHECK(HASH ? "dw_walk_fast_indexed/node2vec" : "dw_walk_fast/node2vec");
     return DW_OK;
@@ -705,6 +746,27 @@ int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32
     return launch_node2vec<true>(row_ptr, col, col, adj_off, adj_hash, prob_thr, alias, n_rows,
                                  starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
                                  status, stream);
+}
+
+int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                         const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
+                         int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                         int32_t walk_length, double p, double q, uint64_t seed,
+                         uint64_t walk_id0, int32_t *out, int32_t *status,
+                         uint64_t *counters, void *stream) {
+    DW_REQUIRE(walk_length >= 1 && walk_length < (1 << 24),
+               "dw_walk_fast_counted: walk_length must be in [1, 2^24)");
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_fast_counted: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && starts && out && status && counters,
+               "dw_walk_fast_counted: null pointer");
+    DW_REQUIRE((prob_thr == nullptr) == (alias == nullptr),
+               "dw_walk_fast_counted: prob_thr and alias must be both set or both null");
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    return launch_node2vec<true>(row_ptr, col, col, adj_off, adj_hash, prob_thr, alias, n_rows,
+                                 starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
+                                 status, stream,
+                                 reinterpret_cast<unsigned long long *>(counters));
 }
 
 int dw_edges_inline_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,

@@ -66,6 +66,8 @@ SIGNATURES = {
                                     _u64, _u64, _p, _p, _p]),
     'dw_walk_fast_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i32,
                                             _i32, _f64, _f64, _u64, _u64, _p, _p, _p]),
+    'dw_walk_fast_counted': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _f64,
+                                            _f64, _u64, _u64, _p, _p, _p, _p]),
     'dw_edges_inline_build': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_sgns_walks': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),

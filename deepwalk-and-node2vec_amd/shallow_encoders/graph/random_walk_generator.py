@@ -172,6 +172,34 @@ class RandomWalk(ABC):
             _native.check_status(status, f'{type(self).__name__}.walk')
         return out
 
+    def count_traffic(self, start_ids: torch.Tensor, walk_id0: int,
+                      out: Optional[torch.Tensor] = None) -> dict:
+        """node2vec, rng='philox', layout='indexed': the same walks as ``walk_batch`` with the
+        walkers' realised memory traffic counted (dw_walk_fast_counted; a diagnostic launch):
+        {'bytes', 'steps', 'blocks', 'tests'} summed over the walks."""
+        if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'philox' \
+                or self._layout != 'indexed':
+            raise ValueError('count_traffic: node2vec with rng="philox", layout="indexed"')
+        dev = _native.require_device(self._device)
+        starts = torch.as_tensor(start_ids, dtype=torch.int32).to(dev).contiguous()
+        n, L = int(starts.numel()), self._length
+        d = self._csr.device_tensors(dev, need_alias=True, need_adj=True)
+        if out is None:
+            out = torch.empty((n, L), dtype=torch.int32, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        p, q = self._params()
+        with torch.cuda.device(dev):
+            _native.call('dw_walk_fast_counted', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                         _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                         _native.ptr(d.get('prob_thr')), _native.ptr(d.get('alias')),
+                         self._csr.vocab_size, _native.ptr(starts), n, L, float(p), float(q),
+                         self._seed & 0xFFFFFFFFFFFFFFFF, int(walk_id0), _native.ptr(out),
+                         _native.ptr(status), _native.ptr(counters), _native.stream(dev))
+        _native.check_status(status, f'{type(self).__name__}.count_traffic')
+        c = counters.cpu().tolist()
+        return {'bytes': c[0], 'steps': c[1], 'blocks': c[2], 'tests': c[3]}
+
 
 class DeepWalk(RandomWalk):
     """First-order walk (random_walk_generator.py:56-72). https://arxiv.org/pdf/1403.6652.pdf"""

@@ -168,6 +168,20 @@ int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32
                          int32_t method, double p, double q, uint64_t seed, uint64_t walk_id0,
                          int32_t *out, int32_t *status, void *stream);
 
+/* dw_walk_fast_indexed's node2vec walks (the same walks, bit for bit) with the walker's realised
+ * memory traffic counted, for the walk roofline (bench.py): counters[0..3] (uint64, caller-zeroed,
+ * accumulated) += load + store bytes the walkers issued (row_ptr / adj_off pairs, proposal picks,
+ * hash buckets or short-list scans, the output), steps, proposal blocks evaluated, adjacency
+ * tests. A diagnostic launch: one wave-summed atomic per counter and wave. Replaces no reference
+ * interface (the reference has no counters); its walks are Node2Vec.walk's law
+ * (random_walk_generator.py:94-119). */
+int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                         const int32_t *adj_hash, const uint32_t *prob_thr, const int32_t *alias,
+                         int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                         int32_t walk_length, double p, double q, uint64_t seed,
+                         uint64_t walk_id0, int32_t *out, int32_t *status,
+                         uint64_t *counters, void *stream);
+
 /* Edge-inline CSR for DeepWalk in dw_walk_fast_indexed: edges int32[nnz][4], entry e of row u =
  * {x = col[e], deg(x), row_ptr[x] low 32 bits, row_ptr[x] high 32 bits}. The pick of the next
  * node then also yields its row: one dependent load per walk step instead of two — the

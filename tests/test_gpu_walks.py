@@ -318,3 +318,19 @@ def test_cora_epoch_end_to_end_bit_exact(tmp_path, monkeypatch, hip_device):
         got.append(b.cpu().numpy())
     np.testing.assert_array_equal(np.concatenate(got), f['walks'])
     np.testing.assert_array_equal(ds._node_ids, f['order_after'])
+
+
+def test_counted_node2vec_walks_equal_and_count(hip_device):
+    """dw_walk_fast_counted (bench.py's walk roofline): the same walks as the indexed walker,
+    every step counted, at least the fixed per-step loads / store counted as bytes."""
+    csr = rmat_graph(16, 600_000, 0)
+    w = Node2Vec(csr, 20, p=0.25, q=4.0, rng='philox', seed=3)
+    for n in (4096, 200_000):                     # 16-lane and 4-lane groups
+        starts = (torch.arange(n, dtype=torch.int64) % (csr.vocab_size - 1) + 1).to(torch.int32)
+        ref = w.walk_batch(starts, walk_id0=5)
+        out = torch.empty_like(ref)
+        c = w.count_traffic(starts, walk_id0=5, out=out)
+        assert torch.equal(out, ref)
+        assert c['steps'] == n * 19
+        assert c['blocks'] >= c['steps'] - n        # >= one proposal block per biased step
+        assert c['bytes'] >= c['steps'] * 36 + c['blocks'] * 16

@@ -211,3 +211,15 @@ def test_oracle_d128_trajectory_matches_reference():
     w_in, w_out = ref.tables()
     np.testing.assert_allclose(w_in, f['w_in'], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(w_out, f['w_out'], rtol=1e-5, atol=1e-7)
+
+
+def test_listscan_node2vec_equals_reference_walks():
+    """The CPU baseline's node2vec (list membership at the reference's cost) replays the
+    reference's R-MAT 12 walks bit-exactly, like the set-based oracle."""
+    f = golden('walks_rmat12_node2vec_p0.25_q4.npz')
+    g = _graph(f)
+    L = int(f['walk_length'])
+    for k in range(0, len(f['starts']), 8):
+        w = walk_ref.node2vec_walk(g, int(f['starts'][k]), L, float(f['p']), float(f['q']),
+                                   f['uniforms'][k].tolist(), listscan=True)
+        np.testing.assert_array_equal(w, f['walks'][k])
