@@ -10,7 +10,8 @@ One step = one pass of the hot path over one batch of synthetic input, all on th
      dense gradient of the batch-mean loss into both tables;
   3. dense Adam over both full 1,048,577 x 128 tables (torch.optim.Adam semantics), with the
      node-id-range sharded reduce-scatter / all-gather exchange over RCCL when N > 1.
-Weak scaling: every rank processes B walks per step; `value` = positive pairs of ALL ranks / s.
+Weak scaling (default): every rank processes B walks per step; `--scaling strong`: the global
+batch is B walks and every rank trains 1/N of it. `value` = positive pairs of ALL ranks / s.
 
 Also reported: walks/s of the walker alone (DeepWalk and node2vec p=.25 q=4), the SGNS kernel
 against the HBM roofline (algorithmic bytes / live HIP-event kernel time), and the CPU
@@ -172,6 +173,10 @@ def main():
     ap.add_argument('--walk-length', type=int, default=None)
     ap.add_argument('--walks-per-node', type=int, default=None)
     ap.add_argument('--lr', type=float, default=0.01)
+    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'],
+                    help='weak: --batch-walks walks per rank per step (the global batch grows '
+                         'with N); strong: --batch-walks is the global batch, each rank trains '
+                         '1/N of it (SURVEY.md §8e parity mode)')
     ap.add_argument('--scatter', default='sorted', choices=['sorted', 'atomic'],
                     help='output-table gradient: records+sort+gather (sorted) or float atomics')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
@@ -214,6 +219,10 @@ def main():
                          'steps replayed bit-exactly). auto = lazy when a step\'s centres are '
                          'under 10%% of the rows of a table of >= 1 GB of Adam bytes (C5: 3.4%% '
                          'of 16.8M rows; C3: 55%%, where dense measured faster)')
+    ap.add_argument('--lazy-out', default='auto', choices=['auto', 'on', 'off'],
+                    help='lazy in-table exchange: keep the out slice\'s Adam lazy (exact) too; '
+                         'auto = when a step\'s records touch under ~half of the slice\'s rows '
+                         '(C3 at 64-walk batches)')
     ap.add_argument('--calib-steps', type=int, default=8,
                     help='--in-exchange auto: timed steps per protocol')
     ap.add_argument('--walk-prefetch', action='store_true',
@@ -291,8 +300,15 @@ def main():
     lazy = owner and args.in_exchange == 'lazy'
 
     def owner_tables(lazy_mode: bool):
-        return (OwnerLazyTables if lazy_mode else OwnerTables)(
-            V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
+        if not lazy_mode:
+            return OwnerTables(V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None)
+        # the out slice lazy too when a step's records touch under ~half of its rows
+        rec_rank = B * W_eff * (L - 2 * R) * 2 * R * (1 + K) / W_eff
+        s_rows = -(-V // W_eff)
+        lazy_out = (args.lazy_out == 'on' or
+                    (args.lazy_out == 'auto' and rec_rank < 0.7 * s_rows))
+        return OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None,
+                               lazy_out=lazy_out)
 
     if owner:
         tables = owner_tables(lazy)
@@ -300,6 +316,11 @@ def main():
         tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
                                overlap_in=not args.no_overlap_in,
                                out_pieces=None if args.no_out_pieces else args.out_pieces)
+    if args.scaling == 'strong':
+        # SURVEY §8e parity mode: the global batch is --batch-walks, each rank trains 1/W of it
+        if B % W_eff:
+            raise SystemExit(f'--scaling strong: --batch-walks {B} must divide by {W_eff} ranks')
+        B //= W_eff
     centres = B * (L - 2 * R)
     pairs_per_step = centres * 2 * R
     grad_scale = 1.0 / (pairs_per_step * W_eff)   # mean over the GLOBAL batch
@@ -405,6 +426,7 @@ def main():
             tables.begin_step()
             tables.prepare(walks, R, K)
             tables.catch_up()
+            tables.catch_up_out(walks, R, K, 99, g0 * (L - 2 * R), status)
         sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks,
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
@@ -558,6 +580,8 @@ def main():
             # the lazy exact Adam needs the dense figure only on the rows the batch touches
             # (every rank updates all of them); the last step's |U| stands for the steps
             in_adam_bytes = int(tables._n_host[0]) * d * 4 * 7
+            if tables.lazy_out:   # the out slice's rows its records touch (expected count)
+                out_adam_bytes = int(tables.S * -math.expm1(-n_rec[0] / tables.S)) * d * 4 * 7
     sgns_gbs = (pairs_per_step * bpp + out_adam_bytes + in_adam_bytes) / (op_ms * 1e-3) / 1e9
     phase_bytes = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     if owner:
@@ -660,7 +684,7 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': elapsed / args.steps * 1e3,
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': args.scaling,
         'vs_baseline': None,
         'dtype': 'fp32',
         'data': f'synthetic (R-MAT scale {args.scale} graph built on the device, Philox walks, '

@@ -90,10 +90,7 @@ __global__ void __launch_bounds__(256)
 // same order as under the dense update, so the tables are bit-for-bit the dense ones.
 //   hist[8 s + k]: step s's scalars (AdamScalars order, one pad), s >= 1
 //   last[r]:       the step up to which row r's (p, m, v) are current
-__device__ __forceinline__ dw::AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
-    const float *h = hist + 8 * s;
-    return dw::AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6]};
-}
+using dw::hist_at;
 
 // One wave per row (lanes over the row's elements). STEP: replay the missed steps up to
 // step - 1, then apply `step` with the row's gradient g_rows[i]; else replay up to `step`.

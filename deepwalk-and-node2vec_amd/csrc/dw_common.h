@@ -119,4 +119,10 @@ __device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v
 }
 
 
+// Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
+__device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
+    const float *h = hist + 8 * s;
+    return AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6]};
+}
+
 }  // namespace dw

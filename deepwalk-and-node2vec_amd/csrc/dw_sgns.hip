@@ -674,11 +674,43 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 // (torch Adam, dw::adam_elem, the same code as dw_adam_dense) and flagged; g_out is never
 // touched for it. Boundary rows still accumulate into g_out and are updated, with the rows no
 // record touched (g = 0), by k_adam_rest.
+// Lazy form (last != nullptr; dw_sgns_owner_pass2_lazy): rows no record touched are not
+// updated at all; a row's deferred g = 0 steps (last[row] + 1 .. step - 1, scalars from `hist`)
+// are replayed right before its update, through the same adam_elem — bit-identical to the dense
+// update (k_rows_adam's rule). Boundary rows then go through k_lazy_boundary, not k_adam_rest.
 struct OutAdam {
     float *p, *m, *v;
     uint8_t *flags;
     dw::AdamScalars s;
+    int32_t *last = nullptr;
+    const float *hist = nullptr;
+    int32_t step = 0;
 };
+
+// One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
+// `oa.step` with g (registers), record the step.
+template <int VPL, bool MASKED>
+__device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, int32_t d,
+                                              int lane, const float (&g)[VPL]) {
+    const int32_t from = oa.last[row];
+    const int64_t o = static_cast<int64_t>(row) * d + lane;
+#pragma unroll
+    for (int m = 0; m < VPL; ++m) {
+        if (MASKED && lane + WAVE * m >= d) continue;
+        const int64_t i = o + WAVE * m;
+        float pp = oa.p[i], mm = oa.m[i], vv = oa.v[i];
+        for (int32_t t = from + 1; t < oa.step; ++t) {
+            float z = 0.f;
+            dw::adam_elem(pp, z, mm, vv, dw::hist_at(oa.hist, t));
+        }
+        float gg = g[m];
+        dw::adam_elem(pp, gg, mm, vv, dw::hist_at(oa.hist, oa.step));
+        oa.p[i] = pp;
+        oa.m[i] = mm;
+        oa.v[i] = vv;
+    }
+    if (lane == 0) oa.last[row] = oa.step;
+}
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
 // records of whole rows, so a piece's rows never continue in another piece's chunks.
@@ -714,7 +746,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         auto flush = [&](uint32_t row) {
             float *dst = g_out + static_cast<int64_t>(row) * d + lane;
             if (row != before && row != after) {
-                if (ADAM) {
+                if (ADAM && oa.last) {
+                    lazy_row_step<VPL, MASKED>(oa, row, d, lane, g);
+                } else if (ADAM) {
                     const int64_t o = static_cast<int64_t>(row) * d + lane;
 #pragma unroll
                     for (int m = 0; m < VPL; ++m) {
@@ -952,6 +986,50 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// Lazy form, after k_rec_gather: the rows that straddle chunks (their gradient summed by
+// atomics into g_out). Chunk c's last row is updated here by the chunk where the row begins —
+// each straddling row exactly once — with g from g_out, which is re-zeroed.
+template <int VPL, bool MASKED>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
+    k_lazy_boundary(const uint32_t *__restrict__ keys, int64_t n_rec, int32_t gch,
+                    float *__restrict__ g_out, int32_t d, OutAdam oa) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_chunks = (n_rec + gch - 1) / gch;
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; ch < n_chunks;
+         ch += n_waves) {
+        const int64_t e0 = ch * gch;
+        const int64_t e1 = (e0 + gch < n_rec) ? e0 + gch : n_rec;
+        const uint32_t row = keys[e1 - 1];
+        if (e1 >= n_rec || keys[e1] != row) continue;               // does not continue
+        if (keys[e0] == row && e0 > 0 && keys[e0 - 1] == row) continue;   // began earlier
+        float g[VPL];
+        const int64_t o = static_cast<int64_t>(row) * d + lane;
+#pragma unroll
+        for (int m = 0; m < VPL; ++m) {
+            g[m] = 0.f;
+            if (MASKED && lane + WAVE * m >= d) continue;
+            g[m] = g_out[o + WAVE * m];
+            g_out[o + WAVE * m] = 0.f;
+        }
+        lazy_row_step<VPL, MASKED>(oa, row, d, lane, g);
+    }
+}
+
+template <int VPL>
+void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_t gch,
+                     float *g_out, int32_t d, const OutAdam &oa) {
+    int64_t blocks = ((n_rec + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 65536) blocks = 65536;
+    if (d == 64 * VPL)
+        hipLaunchKernelGGL((k_lazy_boundary<VPL, false>), dim3((unsigned)blocks),
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa);
+    else
+        hipLaunchKernelGGL((k_lazy_boundary<VPL, true>), dim3((unsigned)blocks),
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa);
+}
+
 template <int VPL>
 void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const uint64_t *vals,
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
@@ -1013,7 +1091,15 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
     else return DW_E_UNSUPPORTED;
     DW_LAUNCH_CHECK("dw_sgns/gather");
-    if (oa) {
+    if (oa && oa->last) {   // lazy: only the straddling rows remain; untouched rows wait
+        if (n_rec > 0) {
+            if (d <= 64) launch_boundary<1>(st, keys, n_rec, gch, g_out, d, *oa);
+            else if (d <= 128) launch_boundary<2>(st, keys, n_rec, gch, g_out, d, *oa);
+            else if (d <= 256) launch_boundary<4>(st, keys, n_rec, gch, g_out, d, *oa);
+            else launch_boundary<8>(st, keys, n_rec, gch, g_out, d, *oa);
+            DW_LAUNCH_CHECK("dw_sgns/lazy_boundary");
+        }
+    } else if (oa) {
         if (d <= 64) launch_rest<1>(st, V, d, g_out, *oa);
         else if (d <= 128) launch_rest<2>(st, V, d, g_out, *oa);
         else if (d <= 256) launch_rest<4>(st, V, d, g_out, *oa);
@@ -1632,9 +1718,97 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
     return a;
 }
 
+// Lazy out slice (dw_sgns_owner_out_catch_up), before pass 1: every owned output row a slot of
+// this batch references is brought current to step - 1 — its deferred g = 0 steps replayed
+// through adam_elem with hist's scalars — so pass 1 reads the rows the dense update would hold.
+// One wave per centre, lane t = slot t (T <= 64). A row is claimed by exactly one lane in the
+// whole launch: atomicMax(claim[row], step) returning < step; the claiming wave then replays the
+// row, lanes over its elements. Race-free: no other wave touches a claimed row in this launch.
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
+    k_out_catch_up(SgnsArgs a, float *__restrict__ p, float *__restrict__ m,
+                   float *__restrict__ v, int32_t *__restrict__ last,
+                   int32_t *__restrict__ claim, const float *__restrict__ hist, int32_t step) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int T = a.C * (1 + a.K);
+    const int64_t per = a.L - 2 * a.R;
+    for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; b < a.batch;
+         b += n_waves) {
+        const int64_t w = b / per, i = a.R + b % per;
+        const int32_t *walk = a.walks + w * a.L;
+        uint32_t mine = 0xFFFFFFFFu;
+        if (lane < T) {
+            const int64_t o = row_id<true>(a, b, walk, i, lane);
+            if (o < 0 || o >= a.V) {
+                dw::status_or(a.status, DW_S_BAD_INDEX);
+            } else if (o % a.n_owners == a.owner) {
+                const uint32_t lo = static_cast<uint32_t>(o / a.n_owners);
+                if (atomicMax(claim + lo, step) < step) mine = lo;
+            }
+        }
+        unsigned long long todo = __ballot(mine != 0xFFFFFFFFu);
+        while (todo) {
+            const int l = __ffsll(static_cast<long long>(todo)) - 1;
+            todo &= todo - 1ull;
+            const uint32_t row = __shfl(mine, l, WAVE);
+            const int32_t from = last[row];
+            if (from >= step - 1) continue;
+            for (int64_t e = lane; e < a.d; e += WAVE) {
+                const int64_t o = static_cast<int64_t>(row) * a.d + e;
+                float pp = p[o], mm = m[o], vv = v[o];
+                for (int32_t t = from + 1; t < step; ++t) {
+                    float z = 0.f;
+                    dw::adam_elem(pp, z, mm, vv, dw::hist_at(hist, t));
+                }
+                p[o] = pp;
+                m[o] = mm;
+                v[o] = vv;
+            }
+            if (lane == 0) last[row] = step - 1;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                               int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                               int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                               const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                               float *w_out_local, float *m_out, float *v_out,
+                               int32_t *last_step, int32_t *claim, const float *hist,
+                               int32_t step, int32_t *status, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
+                   owner >= 0 && owner < n_owners && step >= 1,
+               "dw_sgns_owner_out_catch_up: bad sizes");
+    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= WAVE,
+               "dw_sgns_owner_out_catch_up: 2R(1+K) must be <= 64");
+    DW_REQUIRE(local_rows * n_owners >= vocab_size,
+               "dw_sgns_owner_out_catch_up: the owners' rows do not cover the vocabulary");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && hist && status,
+               "dw_sgns_owner_out_catch_up: null pointer");
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, nullptr, w_out_local, nullptr, nullptr,
+                           noise, seed, noise_offset, 0.f, nullptr, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    a.owner = owner;
+    a.n_owners = n_owners;
+    int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_out_catch_up, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0,
+                       dw::as_stream(stream), a, w_out_local, m_out, v_out, last_step, claim,
+                       hist, step);
+    DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up");
+    return DW_OK;
+}
 
 int dw_sgns_timing(int32_t enable) {
     g_timer.on = enable != 0;
@@ -1863,6 +2037,25 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, adam ? &oa : nullptr, workspace,
                               workspace_bytes, n_records, dw::as_stream(stream));
+}
+
+int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
+                             int32_t neg_samples, int64_t local_rows, int32_t dim,
+                             const float *w_in, float *w_out_local, float *g_out_local,
+                             float *m_out, float *v_out, int32_t *last_step, const float *hist,
+                             int32_t step, int32_t *status, void *workspace,
+                             size_t workspace_bytes, int64_t *n_records, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
+               "dw_sgns_owner_pass2_lazy: bad sizes");
+    DW_REQUIRE(w_in && w_out_local && g_out_local && m_out && v_out && last_step && hist &&
+                   status,
+               "dw_sgns_owner_pass2_lazy: null pointer");
+    OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
+    const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
+    return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
+                              w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
+                              dw::as_stream(stream));
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

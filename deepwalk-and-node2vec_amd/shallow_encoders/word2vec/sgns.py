@@ -394,7 +394,8 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
     """Pass 2 of the owner-computes step (dw_sgns_owner_pass2) after sgns_owner_pass1 with the
     same walks: the records sort and gather over the local slice. ``out_adam`` ({'m', 'v',
     'flags', 'scalars'}, OwnerTables.out_adam_spec()) fuses the slice's Adam step in (w_out_local
-    updated, g_out_local left zero); None accumulates g_out_local. Returns the record count
+    updated, g_out_local left zero); {'m', 'v', 'last', 'hist', 'step'}
+    (OwnerLazyTables(lazy_out=True)) the lazy exact form; None accumulates g_out_local. Returns the record count
     (the call synchronises the current stream once to read it)."""
     import ctypes
     dev = w_in.device
@@ -408,6 +409,15 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
     ws = workspace_for(n * (L - 2 * R), 2 * R, K, w_in.shape[0], dev, local_rows=local_rows)
     n_rec = ctypes.c_int64(0)
+    if out_adam is not None and 'last' in out_adam:      # OwnerLazyTables(lazy_out=True)
+        with torch.cuda.device(dev):
+            _native.call('dw_sgns_owner_pass2_lazy', n, L, R, K, local_rows, d, _native.ptr(w_in),
+                         _native.ptr(w_out_local), _native.ptr(g_out_local),
+                         _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
+                         _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
+                         int(out_adam['step']), _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         ctypes.byref(n_rec), _native.stream(dev))
+        return int(n_rec.value)
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                            _native.ptr(out_adam['flags']), out_adam['scalars'])

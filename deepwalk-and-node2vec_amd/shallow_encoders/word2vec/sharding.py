@@ -712,6 +712,7 @@ class OwnerLazyTables(OwnerTables):
       begin_step        records the step's Adam scalars (the replays use them later);
       prepare           the batch's centre order and U (dw_sgns_owner_prepare);
       catch_up          the rows of U replay their missed steps, up to step - 1;
+      catch_up_out      (lazy_out) the out rows the batch's slots reference, likewise;
       (pass 1)          the partial centre gradient of the owned slots into g_in (rows of U);
       exchange_touched  G = g_in[U] (those rows cleared) and all-reduce(SUM) of G on a side
                         stream while pass 2 runs: |U| x d x 4 B per step instead of the dense
@@ -725,7 +726,38 @@ class OwnerLazyTables(OwnerTables):
       params_in  float32 [1, V_pad, d]  replicated in table
       m_in, v_in float32 [V_pad, d]     its Adam state, replicated
       last_in    int32 [V_pad]          step each row is current to
+
+    ``lazy_out`` (HIP only): the out slice's Adam is lazy too — pass 2 updates only the rows its
+    records touch, each after replaying its deferred g = 0 steps (dw_sgns_owner_pass2_lazy;
+    ``last_out`` int32 [S]); ``flush`` brings both tables current. It pays where a step's
+    records touch a small share of the slice (C3 at the reference's 64-walk batches: ~23% of
+    the rows), so the dense out-table Adam (V·d·4 B x 7 per step) is not paid for the rest.
     """
+
+    def __init__(self, *args, lazy_out: bool = False, **kwargs):
+        self.lazy_out = bool(lazy_out)
+        super().__init__(*args, **kwargs)
+        self.lazy_out = self.lazy_out and self._hip()
+        self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
+                         if self.lazy_out else None)
+        self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
+
+    def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
+                     seed: int, noise_offset: int, status: torch.Tensor,
+                     noise: Optional[torch.Tensor] = None) -> None:
+        """lazy_out, before pass 1 of the batch ``walks``: the owned out rows its slots
+        reference replay their deferred steps up to step - 1 (dw_sgns_owner_out_catch_up)."""
+        if not self.lazy_out:
+            return
+        n, L = walks.shape
+        with torch.cuda.device(self.device):
+            _native.call('dw_sgns_owner_out_catch_up', _native.ptr(walks), n, L,
+                         int(context_radius), int(neg_samples), self.V, self.d, self.rank,
+                         self.world, self.S, _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
+                         int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
+                         _native.ptr(self.v_out), _native.ptr(self.last_out),
+                         _native.ptr(self._claim_out), _native.ptr(self._hist),
+                         self.step_count, _native.ptr(status), _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -871,9 +903,28 @@ class OwnerLazyTables(OwnerTables):
         self._rows(self._G, self.step_count)
 
     def flush(self) -> None:
-        """Every row up to the current step (before the table is read as a whole)."""
+        """Every row up to the current step (before the table is read as a whole); with
+        lazy_out the out slice's deferred steps too."""
         if self.step_count > 0:
             self._rows(None, self.step_count, all_rows=True)
+            if self.lazy_out:
+                hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
+                              self.S, None, self._hist, self.step_count)
+
+    def out_adam_spec(self) -> Optional[dict]:
+        spec = super().out_adam_spec()
+        if spec is not None and self.lazy_out:
+            spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
+                    'step': self.step_count}
+        return spec
+
+    def full_w_out(self) -> torch.Tensor:
+        self.flush()
+        return super().full_w_out()
+
+    def out_state_full(self):
+        self.flush()
+        return super().out_state_full()
 
     def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
         raise RuntimeError('OwnerLazyTables steps through owner_lazy_step')
@@ -891,6 +942,7 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     tables.begin_step()
     tables.prepare(walks, context_radius, neg_samples)
     tables.catch_up()
+    tables.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,

@@ -311,6 +311,32 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
                         float eps, float weight_decay, int32_t *status, void *workspace,
                         size_t workspace_bytes, int64_t *n_records, void *stream);
 
+/* The lazy out slice's catch-up, before dw_sgns_owner_pass1 of the same batch: every owned
+ * output row a slot references (contexts from the walks, negatives as pass 1 draws them) is
+ * brought current to step - 1 (its deferred g = 0 steps replayed, hist as above), so pass 1 reads
+ * the rows the dense update holds. claim int32 [local_rows] (zero-initialised, never reset): a
+ * row is claimed by one wave per step via atomicMax(claim[row], step). 2R(1+K) <= 64. */
+int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                               int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                               int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                               const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                               float *w_out_local, float *m_out, float *v_out,
+                               int32_t *last_step, int32_t *claim, const float *hist,
+                               int32_t step, int32_t *status, void *stream);
+
+/* dw_sgns_owner_pass2 with the out slice's Adam kept LAZY and exact (OwnerLazyTables, small
+ * batches): a row no record touched is not read or written; its deferred g = 0 steps are
+ * replayed (scalars hist[t], fp32 [steps][8] as for dw_adam_rows) right before its next update,
+ * through the same adam_elem, so the slice equals the dense update bit for bit once flushed
+ * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
+ * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53). */
+int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
+                             int32_t neg_samples, int64_t local_rows, int32_t dim,
+                             const float *w_in, float *w_out_local, float *g_out_local,
+                             float *m_out, float *v_out, int32_t *last_step, const float *hist,
+                             int32_t step, int32_t *status, void *workspace,
+                             size_t workspace_bytes, int64_t *n_records, void *stream);
+
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

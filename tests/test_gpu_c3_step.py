@@ -39,9 +39,8 @@ from oracle import sgns_ref
 pytestmark = pytest.mark.gpu
 
 SCALE, EDGES = 20, 10_000_000
-B, L, R, K, D, LR, SEED, WALK_SEED, WPN = 8192, 80, 5, 5, 128, 0.01, 99, 1234, 10
+L, R, K, D, LR, SEED, WALK_SEED, WPN = 80, 5, 5, 128, 0.01, 99, 1234, 10
 BETAS, EPS = (0.9, 0.999), 1e-8
-STEPS = 3
 
 
 @pytest.fixture(scope='module')
@@ -54,7 +53,7 @@ def c3(hip_device):
     return csr, walker
 
 
-def _walks(csr, walker, s, dev):
+def _walks(csr, walker, s, dev, B):
     """Step s's batch as bench.py forms it: global walk ids s*B.., start = id // 10 + 1."""
     g0 = s * B
     n_total = (csr.vocab_size - 1) * WPN
@@ -84,10 +83,11 @@ class _Dense:
 
 
 class _Lazy:
-    def __init__(self, V, dev):
+    def __init__(self, V, dev, lazy_out=False):
         from shallow_encoders.word2vec.sharding import OwnerLazyTables
         self.t = OwnerLazyTables(V, D, dev, lr=LR, betas=BETAS, eps=EPS, init_seed=0,
-                                 emulate_world=1)
+                                 emulate_world=1, lazy_out=lazy_out)
+        assert self.t.lazy_out == lazy_out
         self.V = V
 
     def state(self):
@@ -100,9 +100,12 @@ class _Lazy:
         """The current state with every deferred step applied, leaving the tables as they were
         (rows outside the next batch keep lagging, so the step's catch-up is exercised)."""
         t = self.t
-        keep = [x.clone() for x in (t.params_in, t.m_in, t.v_in, t.last_in)]
+        lagging = [t.params_in, t.m_in, t.v_in, t.last_in]
+        if t.lazy_out:
+            lagging += [t.w_out, t.m_out, t.v_out, t.last_out]
+        keep = [x.clone() for x in lagging]
         snap = [x.clone() for x in self.state()]
-        for dst, src in zip((t.params_in, t.m_in, t.v_in, t.last_in), keep):
+        for dst, src in zip(lagging, keep):
             dst.copy_(src)
         return snap
 
@@ -124,22 +127,26 @@ def _close(name, got, exp, rtol, atol):
                        f'atol {atol:.3e} (worst err/limit {worst:.2f})'
 
 
-@pytest.mark.parametrize('composition', ['dense', 'lazy'])
-def test_c3_step_full_size_vs_float64_reference(c3, composition, hip_device):
+@pytest.mark.parametrize('composition,B,steps', [('dense', 8192, 3), ('lazy', 8192, 3),
+                                                 ('lazy_out', 64, 6)])
+def test_c3_step_full_size_vs_float64_reference(c3, composition, B, steps, hip_device):
+    """'lazy_out': the reference's 64-walk batch on the full C3 tables, both tables' Adam lazy
+    (a step touches ~23% of the out rows; the others' deferred steps are replayed exactly)."""
     from shallow_encoders import _native
     dev = hip_device
     csr, walker = c3
     V = csr.vocab_size
     assert V == 1_048_577
-    prod = (_Dense if composition == 'dense' else _Lazy)(V, dev)
+    prod = (_Dense(V, dev) if composition == 'dense' else
+            _Lazy(V, dev, lazy_out=composition == 'lazy_out'))
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     centres = B * (L - 2 * R)
     M = centres * 2 * R
     b1, b2 = BETAS
     w1 = np.float32(1 - b1)
-    for s in range(STEPS):
-        walks, g0 = _walks(csr, walker, s, dev)
+    for s in range(steps):
+        walks, g0 = _walks(csr, walker, s, dev, B)
         p_in0, p_out0, m_in0, v_in0, m_out0, v_out0 = prod.snapshot()
         torch.cuda.synchronize()
         loss_acc.zero_()

@@ -307,10 +307,10 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d):
     assert (last[ri] == S + 1).all() and int((last == S + 1).sum()) == 5
 
 
-def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0):
+def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False):
     """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L]."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
-    t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4)
+    t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
     n, L = walks_all.shape[1:]
     per = L - 2 * R
     acc = torch.zeros(4, dtype=torch.float64, device=device)
@@ -323,9 +323,11 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0):
     return t, acc
 
 
-def test_owner_lazy_single_rank_equals_dense(hip_device):
+@pytest.mark.parametrize('lazy_out', [False, True])
+def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
     """One rank: sparse batches (most rows untouched for several steps) through the lazy
-    protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush."""
+    protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush;
+    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary)."""
     from shallow_encoders.word2vec.sharding import ShardedTables
     V, d, R, K, L, n, steps, lr = 5000, 64, 2, 3, 12, 16, 6, 0.01
     walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(3),
@@ -337,11 +339,17 @@ def test_owner_lazy_single_rank_equals_dense(hip_device):
         sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
                         context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
         ref.step()
-    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr)
+    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out)
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
+    if lazy_out:
+        lag_out = int((t.last_out[:V] < steps).sum())
+        assert lag_out > V // 4, lag_out     # out rows deferred too
+        assert int(t.last_out.max()) == steps
     w_in = t.w_in.cpu().numpy()              # flush
     assert int(t.last_in.min()) == steps
+    if lazy_out:
+        assert int(t.last_out.min()) == steps
     torch.testing.assert_close(acc, acc_ref, rtol=1e-5, atol=1e-6)
     for got, exp in ((w_in, ref.w_in.cpu().numpy()), (t.full_w_out().cpu().numpy(),
                                                       ref.w_out.cpu().numpy())):
