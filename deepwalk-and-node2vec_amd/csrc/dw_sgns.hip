@@ -1719,15 +1719,15 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 }
 
 // Lazy out slice (dw_sgns_owner_out_catch_up), before pass 1: every owned output row a slot of
-// this batch references is brought current to step - 1 — its deferred g = 0 steps replayed
-// through adam_elem with hist's scalars — so pass 1 reads the rows the dense update would hold.
-// One wave per centre, lane t = slot t (T <= 64). A row is claimed by exactly one lane in the
-// whole launch: atomicMax(claim[row], step) returning < step; the claiming wave then replays the
-// row, lanes over its elements. Race-free: no other wave touches a claimed row in this launch.
+// this batch references must be brought current to step - 1 (its deferred g = 0 steps replayed
+// through adam_elem with hist's scalars), so pass 1 reads the rows the dense update would hold.
+// This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64); a row is
+// claimed by exactly one lane in the launch — atomicMax(claim[row], step) returning < step — and
+// the wave appends its claimed rows to `list` with one counter atomic. dw_adam_rows then
+// replays the listed rows, all in parallel.
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_out_catch_up(SgnsArgs a, float *__restrict__ p, float *__restrict__ m,
-                   float *__restrict__ v, int32_t *__restrict__ last,
-                   int32_t *__restrict__ claim, const float *__restrict__ hist, int32_t step) {
+    k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step,
+                uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int T = a.C * (1 + a.K);
@@ -1736,36 +1736,24 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
          b += n_waves) {
         const int64_t w = b / per, i = a.R + b % per;
         const int32_t *walk = a.walks + w * a.L;
-        uint32_t mine = 0xFFFFFFFFu;
+        bool mine = false;
+        uint32_t lo = 0;
         if (lane < T) {
             const int64_t o = row_id<true>(a, b, walk, i, lane);
             if (o < 0 || o >= a.V) {
                 dw::status_or(a.status, DW_S_BAD_INDEX);
             } else if (o % a.n_owners == a.owner) {
-                const uint32_t lo = static_cast<uint32_t>(o / a.n_owners);
-                if (atomicMax(claim + lo, step) < step) mine = lo;
+                lo = static_cast<uint32_t>(o / a.n_owners);
+                mine = atomicMax(claim + lo, step) < step;
             }
         }
-        unsigned long long todo = __ballot(mine != 0xFFFFFFFFu);
-        while (todo) {
-            const int l = __ffsll(static_cast<long long>(todo)) - 1;
-            todo &= todo - 1ull;
-            const uint32_t row = __shfl(mine, l, WAVE);
-            const int32_t from = last[row];
-            if (from >= step - 1) continue;
-            for (int64_t e = lane; e < a.d; e += WAVE) {
-                const int64_t o = static_cast<int64_t>(row) * a.d + e;
-                float pp = p[o], mm = m[o], vv = v[o];
-                for (int32_t t = from + 1; t < step; ++t) {
-                    float z = 0.f;
-                    dw::adam_elem(pp, z, mm, vv, dw::hist_at(hist, t));
-                }
-                p[o] = pp;
-                m[o] = mm;
-                v[o] = vv;
-            }
-            if (lane == 0) last[row] = step - 1;
-        }
+        const unsigned long long mask = __ballot(mine);
+        if (mask == 0ull) continue;
+        unsigned long long base = 0;
+        if (lane == __ffsll(static_cast<long long>(mask)) - 1)
+            base = atomicAdd(n_list, static_cast<unsigned long long>(__popcll(mask)));
+        base = __shfl(base, __ffsll(static_cast<long long>(mask)) - 1, WAVE);
+        if (mine) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = lo;
     }
 }
 
@@ -1778,8 +1766,9 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
-                               int32_t *last_step, int32_t *claim, const float *hist,
-                               int32_t step, int32_t *status, void *stream) {
+                               int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
+                               int64_t *n_rows, const float *hist, int32_t step,
+                               int32_t *status, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
                    owner >= 0 && owner < n_owners && step >= 1,
@@ -1789,8 +1778,10 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_REQUIRE(local_rows * n_owners >= vocab_size,
                "dw_sgns_owner_out_catch_up: the owners' rows do not cover the vocabulary");
     if (n_walks == 0) return DW_OK;
-    DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && hist && status,
+    DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && rows_buf &&
+                   n_rows && hist && status,
                "dw_sgns_owner_out_catch_up: null pointer");
+    hipStream_t st = dw::as_stream(stream);
     SgnsArgs a = base_args(vocab_size, dim, neg_samples, nullptr, w_out_local, nullptr, nullptr,
                            noise, seed, noise_offset, 0.f, nullptr, status);
     a.walks = walks;
@@ -1800,14 +1791,20 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     a.C = 2 * context_radius;
     a.owner = owner;
     a.n_owners = n_owners;
+    if (hipMemsetAsync(n_rows, 0, sizeof(int64_t), st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner_out_catch_up: counter reset failed");
+        return DW_E_HIP;
+    }
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_out_catch_up, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0,
-                       dw::as_stream(stream), a, w_out_local, m_out, v_out, last_step, claim,
-                       hist, step);
-    DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up");
-    return DW_OK;
+    hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
+                       a, claim, step, rows_buf, reinterpret_cast<unsigned long long *>(n_rows));
+    DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
+    // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
+    const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
+    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
+                        n_max, nullptr, hist, step - 1, stream);
 }
 
 int dw_sgns_timing(int32_t enable) {

@@ -741,6 +741,8 @@ class OwnerLazyTables(OwnerTables):
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
+        self._out_rows = None
+        self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
@@ -750,13 +752,18 @@ class OwnerLazyTables(OwnerTables):
         if not self.lazy_out:
             return
         n, L = walks.shape
+        slots = n * (L - 2 * int(context_radius)) * 2 * int(context_radius) * (1 + int(neg_samples))
+        cap = max(1, min(self.S, slots))
+        if self._out_rows is None or self._out_rows.numel() < cap:
+            self._out_rows = torch.empty(cap, dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_catch_up', _native.ptr(walks), n, L,
                          int(context_radius), int(neg_samples), self.V, self.d, self.rank,
                          self.world, self.S, _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._claim_out), _native.ptr(self._hist),
+                         _native.ptr(self._claim_out), _native.ptr(self._out_rows),
+                         _native.ptr(self._n_out), _native.ptr(self._hist),
                          self.step_count, _native.ptr(status), _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:

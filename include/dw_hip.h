@@ -315,14 +315,17 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
  * output row a slot references (contexts from the walks, negatives as pass 1 draws them) is
  * brought current to step - 1 (its deferred g = 0 steps replayed, hist as above), so pass 1 reads
  * the rows the dense update holds. claim int32 [local_rows] (zero-initialised, never reset): a
- * row is claimed by one wave per step via atomicMax(claim[row], step). 2R(1+K) <= 64. */
+ * row is listed once per step, claimed via atomicMax(claim[row], step); rows_buf uint32
+ * [min(local_rows, B' * 2R(1+K))] and n_rows (int64, device) receive the list, which
+ * dw_adam_rows then replays. 2R(1+K) <= 64, dim <= 512. */
 int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                                int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
-                               int32_t *last_step, int32_t *claim, const float *hist,
-                               int32_t step, int32_t *status, void *stream);
+                               int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
+                               int64_t *n_rows, const float *hist, int32_t step,
+                               int32_t *status, void *stream);
 
 /* dw_sgns_owner_pass2 with the out slice's Adam kept LAZY and exact (OwnerLazyTables, small
  * batches): a row no record touched is not read or written; its deferred g = 0 steps are

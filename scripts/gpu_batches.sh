@@ -17,7 +17,10 @@ run() {  # run <name> <args...>
   grep '^{' gpurun_out/b_$name.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); d['run']='$name'; print(json.dumps(d))" >> $OUT
   python -c "import json; d=json.loads(open('$OUT').read().splitlines()[-1]); print(d['run'], '%.4g pairs/s' % d['value'], '%.3f ms/step' % d['ms_per_step'], 'frac %.3f' % d['roofline']['frac'])"
 }
-for spec in ${BATCH_SPECS:-"c3_64:--batch-walks 64 --steps 200" "c3_1024:--batch-walks 1024 --steps 100" "c3_65536:--batch-walks 65536 --steps 5" "c2_sorted:--config c2 --steps 500" "c2_atomic:--config c2 --scatter atomic --steps 500"}; do
+SPECS=${BATCH_SPECS:-"c3_64:--batch-walks 64 --steps 200;c3_1024:--batch-walks 1024 --steps 100;c3_65536:--batch-walks 65536 --steps 5;c2_sorted:--config c2 --steps 500;c2_atomic:--config c2 --scatter atomic --steps 500"}
+IFS=';' read -ra ITEMS <<< "$SPECS"
+for spec in "${ITEMS[@]}"; do
   name=${spec%%:*}; args=${spec#*:}
-  run $name $args
+  IFS=' ' read -ra ARGV <<< "$args"
+  run $name "${ARGV[@]}"
 done
