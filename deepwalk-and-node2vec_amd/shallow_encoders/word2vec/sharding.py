@@ -914,9 +914,13 @@ class OwnerLazyTables(OwnerTables):
         lazy_out the out slice's deferred steps too."""
         if self.step_count > 0:
             self._rows(None, self.step_count, all_rows=True)
-            if self.lazy_out:
-                hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
-                              self.S, None, self._hist, self.step_count)
+            self._flush_out()
+
+    def _flush_out(self) -> None:
+        """lazy_out: every out-slice row up to the current step."""
+        if self.lazy_out and self.step_count > 0:
+            hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
+                          self.S, None, self._hist, self.step_count)
 
     def out_adam_spec(self) -> Optional[dict]:
         spec = super().out_adam_spec()
@@ -926,11 +930,11 @@ class OwnerLazyTables(OwnerTables):
         return spec
 
     def full_w_out(self) -> torch.Tensor:
-        self.flush()
+        self._flush_out()
         return super().full_w_out()
 
     def out_state_full(self):
-        self.flush()
+        self._flush_out()
         return super().out_state_full()
 
     def exchange_in(self, overlap_bytes: Optional[float] = None) -> None:
