@@ -939,8 +939,8 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
 // (g_out = 0) — Adam with g_out, which is left zeroed. Each wave reads the flags of 64 rows in
 // one load, ballots the unflagged ones and updates only those (lane-coalesced rows), so the
 // common case at C3 — almost every row already updated — costs one byte per row. g is
-// re-zeroed only where it is non-zero (boundary rows): it never holds -0 (atomic sums from +0),
-// so the skipped store leaves the same bits.
+// re-zeroed only where its bits are not +0 (boundary rows, and any -0 a caller left), so the
+// skipped store leaves the same bits.
 template <int VPL, bool MASKED>
 __global__ void __launch_bounds__(256)
     k_adam_rest(int64_t n_rows, int32_t d, const uint8_t *__restrict__ flags,
@@ -979,7 +979,8 @@ __global__ void __launch_bounds__(256)
                     oa.p[i] = pp[k][m];
                     oa.m[i] = mm[k][m];
                     oa.v[i] = vv[k][m];
-                    if (gg[k][m] != 0.f) g[i] = 0.f;   // untouched rows' g is already 0: no write
+                    // untouched rows' g is already +0: no write (-0 is cleared too)
+                    if (__float_as_uint(gg[k][m]) != 0u) g[i] = 0.f;
                 }
             }
         }

@@ -75,7 +75,7 @@ class TrainConfig:
     max_epochs: int
     accelerator: str
     devices: str
-    noise: str = 'device'
+    noise: str = 'torch'
     seed: int = 0
 
     def instantiate_optimizer(self, params: Iterator[nn.Parameter]) -> Optimizer:

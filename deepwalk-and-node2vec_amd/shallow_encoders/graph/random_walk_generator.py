@@ -16,6 +16,7 @@ Two sampling modes, one kernel family each (include/dw_hip.h):
 ``walk(node) -> str`` keeps the reference signature; ``walk_batch`` is the batched device API
 (int32 vocabulary ids, shape [n_walks, length]) that feeds the fused SGNS kernel.
 """
+import sys
 from abc import ABC
 from typing import List, Optional, Sequence, Union
 
@@ -29,15 +30,24 @@ from shallow_encoders.graph.rng import draw_uniforms
 _CSR_CACHE_ATTR = '_dw_csr_cache'
 
 
+def _graph_fingerprint(graph) -> int:
+    """Hash of the adjacency in insertion order with edge weights: a rewired edge or a changed
+    weight gives a new CSR (the reference reads the live graph on every step). O(E)."""
+    return hash(tuple((n, tuple((x, d.get('weight')) for x, d in nbrs.items()))
+                      for n, nbrs in graph.adj.items()))
+
+
 def _csr_of(graph) -> CSRGraph:
-    """CSR of a networkx graph, cached on the graph object (the walker borrows the graph)."""
+    """CSR of a networkx graph, cached on the graph object (the walker borrows the graph) and
+    rebuilt when the graph changed since (structure, neighbour order or weights)."""
     if isinstance(graph, CSRGraph):
         return graph
+    key = _graph_fingerprint(graph)
     cached = graph.graph.get(_CSR_CACHE_ATTR) if hasattr(graph, 'graph') else None
-    if cached is not None and cached[0] == (graph.number_of_nodes(), graph.number_of_edges()):
+    if cached is not None and cached[0] == key:
         return cached[1]
     csr = CSRGraph.from_networkx(graph)
-    graph.graph[_CSR_CACHE_ATTR] = ((graph.number_of_nodes(), graph.number_of_edges()), csr)
+    graph.graph[_CSR_CACHE_ATTR] = (key, csr)
     return csr
 
 
@@ -64,6 +74,12 @@ class RandomWalk(ABC):
             raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
         if layout not in ('indexed', 'csr'):
             raise ValueError(f'unknown layout "{layout}" (expected "indexed" or "csr")')
+        if rng == 'python' and sys.version_info >= (3, 12):
+            # the replay kernel sums the normalising weights left to right as CPython <= 3.11's
+            # sum() does; 3.12+ sums floats with compensation, so the walks would not be the
+            # reference's bit for bit
+            raise NotImplementedError("rng='python' (bit-exact replay) needs CPython < 3.12; "
+                                      "use rng='philox'")
         self._layout = layout
         self._graph = graph
         self._length = length

@@ -46,6 +46,9 @@ class Adam(Optimizer):
         self.fuse_into_sgns = fuse_into_sgns
         self._fused_done = set()   # ids of parameters whose update this step already applied
         self._alt: Dict[int, torch.Tensor] = {}   # second buffer of double-buffered parameters
+        # ids of parameters whose .grad is known to be all zero (a fresh buffer, or one a
+        # zeroing step consumed): the fused step needs it — its interior rows never read g
+        self._grads_clean = set()
 
     # ---- fused form ---------------------------------------------------------------------------
     def can_fuse(self, params: List[torch.Tensor]) -> bool:
@@ -57,7 +60,14 @@ class Adam(Optimizer):
         if len(mine) != len(params) or {id(p) for p in mine} != {id(p) for p in params}:
             return False
         return all(p.device.type == 'cuda' and p.dtype == torch.float32 and p.is_contiguous()
-                   and p.grad is not None and p.grad.is_contiguous() for p in params)
+                   and p.grad is not None and p.grad.is_contiguous()
+                   and id(p) in self._grads_clean for p in params)
+
+    def mark_grads(self, params: List[torch.Tensor], clean: bool) -> None:
+        """Record that the gradients of ``params`` are all zero (``clean``: a new zero buffer)
+        or may not be (something accumulated into them outside a fused step)."""
+        for p in params:
+            (self._grads_clean.add if clean else self._grads_clean.discard)(id(p))
 
     def begin_fused_step(self, params: List[torch.Tensor]) -> List[Tuple[dict, tuple]]:
         """Count one step for each of ``params`` (state created on first use) and return
@@ -69,6 +79,7 @@ class Adam(Optimizer):
             state['step'] += 1
             out.append((state, self._scalars(group, float(state['step'].item()))))
             self._fused_done.add(id(p))
+            self._grads_clean.add(id(p))     # the fused step leaves the gradient zero
         return out
 
     def alt_buffer(self, p: torch.Tensor) -> torch.Tensor:
@@ -130,6 +141,7 @@ class Adam(Optimizer):
                                  _native.ptr(state['exp_avg']), _native.ptr(state['exp_avg_sq']),
                                  p.numel(), *scalars, 1 if self.zero_grad_in_step else 0,
                                  _native.stream(p.device))
+                self.mark_grads([p], self.zero_grad_in_step)
         return loss
 
     def zero_grad(self, set_to_none: bool = True) -> None:

@@ -181,9 +181,12 @@ class Word2VecTrainer(_Base):
             renorm_(w_out, targets, max_norm, st)
             renorm_(w_out, noise, max_norm, st)
         if self.manual_grads:
-            for p in (w_in, w_out):
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
+            from shallow_encoders.word2vec.optim import Adam
+            fresh = [p for p in (w_in, w_out) if p.grad is None]
+            for p in fresh:
+                p.grad = torch.zeros_like(p)
+            if isinstance(self._optimizer, Adam):
+                self._optimizer.mark_grads(fresh, True)
             if targets is None and self._can_fuse_step(w_in, w_out, C):
                 acc = self._fused_walk_step(w_in, w_out, src, R, noise, offset)
             elif targets is None:
@@ -194,6 +197,8 @@ class Word2VecTrainer(_Base):
                 acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
                                       self._neg_samples, inputs=src, targets=targets, noise=noise,
                                       seed=self._seed, noise_offset=offset)
+            if isinstance(self._optimizer, Adam) and not self._optimizer._fused_done:
+                self._optimizer.mark_grads([w_in, w_out], False)   # accumulated, not consumed
             t = loss_terms(acc, n_centres * C, self._neg_samples)
             loss = {k: t[k] for k in ('loss', 'positive-loss', 'negative-loss')}
             recall, precision = t['recall'], t['precision']
