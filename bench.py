@@ -177,8 +177,11 @@ def main():
                     help='weak: --batch-walks walks per rank per step (the global batch grows '
                          'with N); strong: --batch-walks is the global batch, each rank trains '
                          '1/N of it (SURVEY.md §8e parity mode)')
-    ap.add_argument('--scatter', default='sorted', choices=['sorted', 'atomic'],
-                    help='output-table gradient: records+sort+gather (sorted) or float atomics')
+    ap.add_argument('--scatter', default='auto', choices=['auto', 'sorted', 'atomic'],
+                    help='output-table gradient: records+sort+gather (sorted) or float atomics; '
+                         'auto = atomic for batches of <= 65,536 records on the one-GPU '
+                         'replicated path (the C2 shape: the sort\'s launches cost more than '
+                         'the atomics), sorted otherwise')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-walk-bench', action='store_true')
@@ -219,6 +222,10 @@ def main():
                          'steps replayed bit-exactly). auto = lazy when a step\'s centres are '
                          'under 10%% of the rows of a table of >= 1 GB of Adam bytes (C5: 3.4%% '
                          'of 16.8M rows; C3: 55%%, where dense measured faster)')
+    ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
+                    help='one GPU, replicated step: replay it as a HIP graph with the per-step '
+                         'scalars in device memory (word2vec/graphed.py); auto = for batches of '
+                         '<= 100K centres, where the step is launch-bound (C2 shape)')
     ap.add_argument('--lazy-out', default='auto', choices=['auto', 'on', 'off'],
                     help='lazy in-table exchange: keep the out slice\'s Adam lazy (exact) too; '
                          'auto = when a step\'s records touch under ~half of the slice\'s rows '
@@ -288,6 +295,9 @@ def main():
     if n1_lazy:
         emulate, args.in_exchange = 1, 'lazy'
     owner = emulate > 0 or (world > 1 and args.dist_mode == 'owner')
+    if args.scatter == 'auto':
+        records = B * (L - 2 * R) * 2 * R * (1 + K)
+        args.scatter = 'atomic' if (world == 1 and not owner and records <= 65_536) else 'sorted'
     if owner and not (args.scatter == 'sorted' and d % 64 == 0 and d <= 512
                       and 2 * R * (1 + K) <= 64):
         raise SystemExit('owner mode needs the sorted path, d a multiple of 64 (<= 512) and '
@@ -529,14 +539,36 @@ def main():
         one_step(False)
     torch.cuda.synchronize(dev)
     _native.check_status(status, 'bench warmup')
+    # small batches on one GPU: the step replayed as a HIP graph (word2vec/graphed.py)
+    graphed = None
+    use_graph = (world == 1 and not owner and (fuse or args.scatter == 'atomic')
+                 and tables.overlap_in
+                 and args.method in ('deepwalk', 'node2vec') and not args.walk_prefetch
+                 and (args.graph == 'on' or (args.graph == 'auto' and centres <= 100_000)))
+    if use_graph:
+        from shallow_encoders.word2vec.graphed import GraphedStep, epoch_starts_node_order
+        graphed = GraphedStep(tables, walker, epoch_starts_node_order(N, args.walks_per_node, dev),
+                              B, R, K, seed=99, grad_scale=grad_scale, loss_acc=loss_acc,
+                              status=status, first_walk_id=step_idx[0] * B,
+                              n_steps=args.steps + 1, scatter=args.scatter)
     loss_acc.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    phase_timing(True)
+    phase_timing(graphed is None)
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        one_step(True)
+    if graphed is None:
+        for _ in range(args.steps):
+            one_step(True)
+    else:
+        for _ in range(args.steps):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record()
+            graphed.replay()
+            e[1].record()
+            ev['sgns'].append((e[0], e[1]))
+            ev['walk'].append((e[0], e[0]))
+            ev['adam'].append((e[1], e[1]))
     torch.cuda.synchronize(dev)
     phases = phase_ms()
     phase_timing(False)
@@ -568,6 +600,8 @@ def main():
     overlap_in = world == 1 and not owner and tables.overlap_in
     in_adam_bytes = V * d * 4 * 7 if overlap_in else 0
     op_ms = sgns_ms + (kern_ms['adam'] if overlap_in else 0.0)
+    if graphed is not None:     # one replay: walk + SGNS + both tables' Adam
+        op_ms = kern_ms['sgns']
     if owner:
         # this rank's share of the job's algorithmic bytes: 1/W of the pairs' SGNS bytes and of
         # both tables' dense Adam (out slice fused in pass 2, own in-table rows on the side
@@ -741,7 +775,11 @@ def main():
             'out_table_adam_bytes': out_adam_bytes, 'in_table_adam_bytes': in_adam_bytes,
             'in_table_adam_blocks': (overlap_adam_blocks(V * d * 4 * 7, p2_bytes)
                                      if overlap_in else None),
-            'ms_per_launch': op_ms, 'launches_timed': phases['calls'],
+            'ms_per_launch': op_ms,
+            'launches_timed': phases['calls'] if graphed is None else args.steps,
+            'graph': (None if graphed is None else
+                      'HIP graph replay of walk + SGNS + both Adams (word2vec/graphed.py); '
+                      'the window is the whole replay, phases are not split'),
             'phases': phase_info,
         },
         'cpu_baseline': None,

@@ -7,6 +7,9 @@
 namespace dw {
 
 static thread_local char g_err[512] = "";
+static thread_local const dw_step_scalars *g_step = nullptr;
+
+const dw_step_scalars *bound_step_scalars() { return g_step; }
 
 void set_error(const char *fmt, ...) {
     va_list ap;
@@ -22,6 +25,11 @@ extern "C" {
 const char *dw_last_error_string(void) { return dw::g_err; }
 
 int dw_abi_version(void) { return 5; }
+
+int dw_step_scalars_bind(const dw_step_scalars *dev) {
+    dw::g_step = dev;
+    return DW_OK;
+}
 
 int dw_device_sync(void *stream) {
     hipError_t e = hipStreamSynchronize(dw::as_stream(stream));

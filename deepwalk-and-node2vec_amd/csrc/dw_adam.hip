@@ -35,9 +35,11 @@ __device__ __forceinline__ void st(float4 *p, float4 v, bool nt) {
 template <bool ZERO, bool NT, int U, bool NTS = NT>
 __global__ void __launch_bounds__(256)
     k_adam(const float *p, float *pd, float *__restrict__ g, float *__restrict__ m,
-           float *__restrict__ v, int64_t n, dw::AdamScalars s) {
+           float *__restrict__ v, int64_t n, dw::AdamScalars s0,
+           const dw_step_scalars *__restrict__ dyn) {
     // p: parameters read; pd: parameters written (== p in place, or the other buffer of a
-    // double-buffered table)
+    // double-buffered table); dyn: the bound step block's scalars replace s0 (graph replay)
+    const dw::AdamScalars s = dw::step_adam(dyn, s0);
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const float4 *p4 = reinterpret_cast<const float4 *>(p);
@@ -218,11 +220,11 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
     if (zero_grad)
         hipLaunchKernelGGL((k_adam<true, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), param_src, param_dst, grad, exp_avg,
-                           exp_avg_sq, n_elem, s);
+                           exp_avg_sq, n_elem, s, dw::bound_step_scalars());
     else
         hipLaunchKernelGGL((k_adam<false, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), param_src, param_dst, grad, exp_avg,
-                           exp_avg_sq, n_elem, s);
+                           exp_avg_sq, n_elem, s, dw::bound_step_scalars());
     DW_LAUNCH_CHECK("dw_adam_dense");
     return DW_OK;
 }

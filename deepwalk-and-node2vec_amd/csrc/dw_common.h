@@ -12,6 +12,9 @@ namespace dw {
 // ---- error reporting across the C ABI ---------------------------------------------------------
 void set_error(const char *fmt, ...);
 
+// The dw_step_scalars block bound on this host thread (dw_step_scalars_bind), or NULL.
+const dw_step_scalars *bound_step_scalars();
+
 #define DW_REQUIRE(cond, ...)                 \
     do {                                      \
         if (!(cond)) {                        \
@@ -118,6 +121,15 @@ __device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v
     p = p + s.nstep * (m / denom);
 }
 
+
+// The Adam scalars a kernel uses: the bound step block's when there is one (graph replay),
+// else the launch's by-value ones.
+__device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
+                                                 const AdamScalars &s) {
+    if (!dyn) return s;
+    const float *h = dyn->adam;
+    return AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6]};
+}
 
 // Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
 __device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {

@@ -148,6 +148,7 @@ struct SgnsArgs {
     int64_t region;
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
+    const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
 };
 
 #ifndef DW_NOISE_ROUNDS
@@ -158,7 +159,7 @@ struct SgnsArgs {
 // (z, w) for odd n, each through bounded64 (uniform over [0, V) like torch.randint;
 // oracle/philox.py device_noise). One call serves two negatives.
 __device__ __forceinline__ dw::U4 noise_pair(const SgnsArgs &a, int64_t b, int m) {
-    const uint64_t g = a.noise_offset + static_cast<uint64_t>(b);
+    const uint64_t g = (a.dyn ? a.dyn->noise_offset : a.noise_offset) + static_cast<uint64_t>(b);
     return dw::philox<DW_NOISE_ROUNDS>(
         dw::U4{static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32), static_cast<uint32_t>(m),
                TAG_SGNS},
@@ -685,6 +686,7 @@ struct OutAdam {
     int32_t *last = nullptr;
     const float *hist = nullptr;
     int32_t step = 0;
+    const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -724,6 +726,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     const int64_t lo = range ? range[0] : 0;
     const int64_t hi = range ? range[1] : n_rec;
     const int64_t n_chunks = (hi - lo + gch - 1) / gch;
+    const dw::AdamScalars sc = ADAM ? dw::step_adam(oa.dyn, oa.s) : oa.s;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     bool live[VPL];
 #pragma unroll
@@ -755,7 +758,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                         if (!live[m]) continue;
                         const int64_t i = o + WAVE * m;
                         float pp = oa.p[i], gg = g[m], mm = oa.m[i], vv = oa.v[i];
-                        dw::adam_elem(pp, gg, mm, vv, oa.s);
+                        dw::adam_elem(pp, gg, mm, vv, sc);
                         oa.p[i] = pp;
                         oa.m[i] = mm;
                         oa.v[i] = vv;
@@ -947,10 +950,14 @@ __global__ void __launch_bounds__(256)
                 float *__restrict__ g, OutAdam oa) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+    const dw::AdamScalars sc = dw::step_adam(oa.dyn, oa.s);
     for (int64_t base = (blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE) * WAVE;
          base < n_rows; base += n_waves * WAVE) {
         const int64_t r = base + lane;
-        unsigned long long todo = __ballot(r < n_rows && flags[r] == 0);
+        const bool in = r < n_rows;
+        const uint8_t f = in ? flags[r] : 1;
+        if (in && f != 0) flags[r] = 0;     // the flags are left zero for the next step
+        unsigned long long todo = __ballot(in && f == 0);
         // two rows per trip (wave-uniform): both rows' loads are issued before either's stores
         while (todo) {
             const int l0 = __ffsll(static_cast<long long>(todo)) - 1;
@@ -975,7 +982,7 @@ __global__ void __launch_bounds__(256)
                 for (int m = 0; m < VPL; ++m) {
                     if (MASKED && lane + WAVE * m >= d) continue;
                     const int64_t i = o + WAVE * m;
-                    dw::adam_elem(pp[k][m], gg[k][m], mm[k][m], vv[k][m], oa.s);
+                    dw::adam_elem(pp[k][m], gg[k][m], mm[k][m], vv[k][m], sc);
                     oa.p[i] = pp[k][m];
                     oa.m[i] = mm[k][m];
                     oa.v[i] = vv[k][m];
@@ -1067,7 +1074,7 @@ void launch_rest(hipStream_t st, int64_t V, int32_t d, float *g_out, const OutAd
 }
 
 // oa != NULL: the fused output-table Adam (rows 0..V of the out table) — gather, then the
-// rest-of-rows update, then the row flags cleared.
+// rest-of-rows update, which also clears the row flags.
 // range != NULL: one row piece (records [range[0], range[1]), read on the device); the grid is
 // sized for `share` of the records (grid-stride beyond).
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
@@ -1105,11 +1112,7 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
         else if (d <= 128) launch_rest<2>(st, V, d, g_out, *oa);
         else if (d <= 256) launch_rest<4>(st, V, d, g_out, *oa);
         else launch_rest<8>(st, V, d, g_out, *oa);
-        DW_LAUNCH_CHECK("dw_sgns/adam_rest");
-        if (hipMemsetAsync(oa->flags, 0, static_cast<size_t>(V), st) != hipSuccess) {
-            dw::set_error("dw_sgns: flag reset failed");
-            return DW_E_HIP;
-        }
+        DW_LAUNCH_CHECK("dw_sgns/adam_rest");   // (k_adam_rest also clears the flags)
     }
     return DW_OK;
 }
@@ -1716,6 +1719,7 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
     a.scale = grad_scale;
     a.loss_acc = loss_acc;
     a.status = status;
+    a.dyn = dw::bound_step_scalars();
     return a;
 }
 
@@ -1911,6 +1915,7 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
     OutAdam oa{w_out, m_out, v_out, row_flags,
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
                                neg_step_size, eps, weight_decay}};
+    oa.dyn = dw::bound_step_scalars();
     return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
 }
 
@@ -2031,6 +2036,7 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
     OutAdam oa{w_out_local, m_out, v_out, row_flags,
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
                                neg_step_size, eps, weight_decay}};
+    oa.dyn = dw::bound_step_scalars();
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, adam ? &oa : nullptr, workspace,

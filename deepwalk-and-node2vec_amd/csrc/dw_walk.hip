@@ -238,10 +238,11 @@ __global__ void __launch_bounds__(256)
                          const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                          int32_t L, uint32_t k0, uint32_t k1, uint64_t walk_id0,
-                         int32_t *__restrict__ out, int32_t *status) {
+                         int32_t *__restrict__ out, int32_t *status,
+                         const dw_step_scalars *__restrict__ dyn) {
     const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (w >= n_walks) return;
-    const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
+    const uint64_t wid = (dyn ? dyn->walk_id0 : walk_id0) + static_cast<uint64_t>(w);
     int32_t *o = out + w * (int64_t)L;
     int32_t v = starts[w];
     o[0] = v;
@@ -277,10 +278,11 @@ __global__ void __launch_bounds__(256)
                            const uint32_t *__restrict__ prob_thr, const int32_t *__restrict__ alias,
                            int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                            int32_t L, uint32_t k0, uint32_t k1, uint64_t walk_id0,
-                           int32_t *__restrict__ out, int32_t *status) {
+                           int32_t *__restrict__ out, int32_t *status,
+                           const dw_step_scalars *__restrict__ dyn) {
     const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (w >= n_walks) return;
-    const uint64_t wid = walk_id0 + static_cast<uint64_t>(w);
+    const uint64_t wid = (dyn ? dyn->walk_id0 : walk_id0) + static_cast<uint64_t>(w);
     int32_t *o = out + w * (int64_t)L;
     int32_t v = starts[w];
     bool ok = v >= 0 && (int64_t)v < n_rows;
@@ -332,6 +334,29 @@ __global__ void k_edges_inline(const int64_t *__restrict__ row_ptr, const int32_
                         static_cast<int32_t>(static_cast<uint32_t>(a)),
                         static_cast<int32_t>(a >> 32)};
     }
+}
+
+// dw_step_starts / dw_step_scalars_advance: the per-step values of a replayed training step.
+__global__ void __launch_bounds__(256)
+    k_step_starts(const dw_step_scalars *__restrict__ dyn, const int32_t *__restrict__ epoch,
+                  int64_t n_epoch, int32_t *__restrict__ out, int64_t n) {
+    const uint64_t base = dyn->walk_id0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += stride)
+        out[k] = epoch[(base + static_cast<uint64_t>(k)) % static_cast<uint64_t>(n_epoch)];
+}
+
+__global__ void k_step_advance(dw_step_scalars *dyn, const float *__restrict__ hist,
+                               int64_t hist_rows, uint64_t walks_per_step,
+                               uint64_t centres_per_step, int32_t *status) {
+    dyn->walk_id0 += walks_per_step;
+    dyn->noise_offset += centres_per_step;
+    const int64_t s = ++dyn->step;
+    if (s >= hist_rows) {
+        dw::status_or(status, DW_S_BAD_INDEX);
+        return;
+    }
+    for (int k = 0; k < 8; ++k) dyn->adam[k] = hist[8 * s + k];
 }
 
 constexpr int N2V_WAVES = 4;     // waves per block
@@ -440,7 +465,8 @@ __global__ void __launch_bounds__(N2V_WAVES *WAVE)
                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                          int32_t L, N2VThr thr, uint32_t k0, uint32_t k1, uint64_t walk_id0,
                          int32_t *__restrict__ out, int32_t *status,
-                         unsigned long long *counters) {
+                         unsigned long long *counters, const dw_step_scalars *__restrict__ dyn) {
+    if (dyn) walk_id0 = dyn->walk_id0;
     uint32_t c_bytes = 0, c_steps = 0, c_blocks = 0, c_tests = 0;   // STATS only
     const uint32_t pick_bytes = prob_thr ? 12u : 4u;   // col (+ prob_thr, alias) per proposal
     const int lane = threadIdx.x & (WAVE - 1);
@@ -629,7 +655,7 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
     hipLaunchKernelGGL((k_walk_node2vec_fast<G, HASH, ST>), dim3((unsigned)blocks),            \
                        dim3(N2V_WAVES * WAVE), 0, dw::as_stream(stream), row_ptr, col, nbr,    \
                        adj_off, adj_hash, prob_thr, alias, n_rows, starts, n_walks, walk_length, \
-                       thr, k0, k1, walk_id0, out, status, counters)
+                       thr, k0, k1, walk_id0, out, status, counters, dw::bound_step_scalars())
     if (counters) {
         if (group == 4)
             DW_N2V_LAUNCH(4, true);
@@ -704,7 +730,8 @@ int dw_walk_fast(const int64_t *row_ptr, const int32_t *col, const int32_t *col_
         DW_REQUIRE(blocks < (int64_t(1) << 31), "dw_walk_fast: too many walks");
         hipLaunchKernelGGL(k_walk_deepwalk_fast, dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), row_ptr, col, prob_thr, alias, n_rows, starts,
-                           n_walks, walk_length, k0, k1, walk_id0, out, status);
+                           n_walks, walk_length, k0, k1, walk_id0, out, status,
+                           dw::bound_step_scalars());
         DW_LAUNCH_CHECK("dw_walk_fast/deepwalk");
         return DW_OK;
     }
@@ -737,7 +764,7 @@ int dw_walk_fast_indexed(const int64_t *row_ptr, const int32_t *col, const int32
         hipLaunchKernelGGL(k_walk_deepwalk_inline, dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), row_ptr, reinterpret_cast<const int4 *>(edges),
                            prob_thr, alias, n_rows, starts, n_walks, walk_length, k0, k1,
-                           walk_id0, out, status);
+                           walk_id0, out, status, dw::bound_step_scalars());
         DW_LAUNCH_CHECK("dw_walk_fast_indexed/deepwalk");
         return DW_OK;
     }
@@ -767,6 +794,29 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
                                  starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
                                  status, stream,
                                  reinterpret_cast<unsigned long long *>(counters));
+}
+
+int dw_step_starts(const dw_step_scalars *dev, const int32_t *epoch_starts, int64_t n_epoch,
+                   int32_t *starts_out, int64_t n, void *stream) {
+    DW_REQUIRE(n >= 0 && n_epoch >= 1, "dw_step_starts: bad sizes");
+    if (n == 0) return DW_OK;
+    DW_REQUIRE(dev && epoch_starts && starts_out, "dw_step_starts: null pointer");
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_step_starts, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       dev, epoch_starts, n_epoch, starts_out, n);
+    DW_LAUNCH_CHECK("dw_step_starts");
+    return DW_OK;
+}
+
+int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t hist_rows,
+                            uint64_t walks_per_step, uint64_t centres_per_step, int32_t *status,
+                            void *stream) {
+    DW_REQUIRE(dev && hist && status && hist_rows >= 1, "dw_step_scalars_advance: bad arguments");
+    hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(1), 0, dw::as_stream(stream), dev, hist,
+                       hist_rows, walks_per_step, centres_per_step, status);
+    DW_LAUNCH_CHECK("dw_step_scalars_advance");
+    return DW_OK;
 }
 
 int dw_edges_inline_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,

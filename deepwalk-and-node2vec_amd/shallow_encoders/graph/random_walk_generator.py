@@ -126,13 +126,15 @@ class RandomWalk(ABC):
 
     def walk_batch(self, start_ids: Union[torch.Tensor, Sequence[int]],
                    uniforms: Optional[np.ndarray] = None, walk_id0: Optional[int] = None,
-                   out: Optional[torch.Tensor] = None, check: bool = True) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, check: bool = True,
+                   status: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Walks from every start id (vocabulary ids) — int32 [n, length] on the device.
 
         rng='python': the next n*(length-1) doubles of the global ``random`` stream are used
         (or ``uniforms`` when given, shape [n, length-1]). rng='philox': walk ``k`` of this
         call has global walk id ``walk_id0 + k`` (default: continues the previous call).
-        ``check=False`` skips the synchronising status check (stream stays asynchronous).
+        ``check=False`` skips the synchronising status check (stream stays asynchronous);
+        ``status``: the caller's int32 status word to OR conditions into (default: a new one).
         """
         dev = _native.require_device(self._device)
         starts = torch.as_tensor(start_ids, dtype=torch.int32)
@@ -149,7 +151,8 @@ class RandomWalk(ABC):
                                      need_edges=indexed and not n2v, need_adj=indexed and n2v)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        if status is None:
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
         p, q = self._params()
         with torch.cuda.device(dev):
             s = _native.stream(dev)

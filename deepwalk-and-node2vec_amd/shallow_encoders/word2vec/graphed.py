@@ -1,0 +1,128 @@
+"""A training step replayed as a HIP graph (small batches: the step is launch-bound).
+
+At the reference's own batch shape (64 walks per step, configs/sge_sg_*.yaml) one step is a few
+dozen microseconds of kernels — walker, SGNS pass 1, records sort, gather with the output
+table's Adam fused, the input table's Adam on a side stream — and launching them one by one from
+Python costs more than running them. ``GraphedStep`` captures the one-GPU step once per parity
+of the input table's double buffer (two hipGraphs) and replays it.
+
+What changes from step to step is kept in device memory (include/dw_hip.h, dw_step_scalars):
+the walk id of the step's first walk (the Philox walker), the centre counter of its negatives
+(SGNS pass 1) and the Adam scalars (both tables' updates). While the block is bound during
+capture, those kernels read it instead of their by-value arguments; the captured step ends with
+``dw_step_scalars_advance``, which moves the block to the next step from a precomputed history of
+Adam scalars (float64 on the host, rounded to float32 exactly as the eager launches pass them).
+The start nodes come from the epoch's start list by walk id (``dw_step_starts``). The kernels and
+their results are those of the eager step (tests/test_gpu_graphed.py).
+"""
+from typing import Optional
+
+import numpy as np
+import torch
+
+from shallow_encoders import _native
+from shallow_encoders.word2vec.sharding import ShardedTables, adam_scalars, replicated_step
+
+_STEP_DTYPE = np.dtype([('walk_id0', '<u8'), ('noise_offset', '<u8'), ('step', '<i8'),
+                        ('adam', '<f4', (8,))])   # == dw_step_scalars (56 bytes)
+
+
+def adam_history(n_steps: int, lr: float, betas, eps: float, weight_decay: float) -> np.ndarray:
+    """float32 [n_steps + 1, 8]: row s = Adam step s's scalars (dw_adam_dense order)."""
+    h = np.zeros((n_steps + 1, 8), dtype=np.float32)
+    for s in range(1, n_steps + 1):
+        h[s, :7] = np.asarray(adam_scalars(s, lr, betas, eps, weight_decay), dtype=np.float32)
+    return h
+
+
+class GraphedStep:
+    """``replicated_step`` on one GPU (ShardedTables with the overlapped in-table Adam; the out
+    table's Adam fused into the records gather, or after the atomic scatter with
+    ``scatter='atomic'``), captured with the walker in front of it.
+
+    ``walker``: a Philox walker (rng='philox'); ``epoch_starts``: device int32 — walk w of the
+    epoch starts at epoch_starts[w mod len]; the step trains walks ``first_walk_id + k*B ..``.
+    ``n_steps``: how many replays the Adam-scalar history covers."""
+
+    def __init__(self, tables: ShardedTables, walker, epoch_starts: torch.Tensor, B: int,
+                 context_radius: int, neg_samples: int, *, seed: int, grad_scale: float,
+                 loss_acc: torch.Tensor, status: torch.Tensor, first_walk_id: int,
+                 n_steps: int, noise_offset: Optional[int] = None, scatter: str = 'sorted'):
+        if tables.world != 1 or not tables.overlap_in or not tables.can_fuse_out_adam():
+            raise ValueError('GraphedStep: one GPU, HIP Adam with the overlapped in-table update')
+        if epoch_starts.dtype != torch.int32 or epoch_starts.device != tables.device:
+            raise ValueError('GraphedStep: epoch_starts must be int32 on the tables\' device')
+        self.t, self.walker = tables, walker
+        dev = tables.device
+        L = walker.length
+        R, K = int(context_radius), int(neg_samples)
+        self.B, self.centres = int(B), int(B) * (L - 2 * R)
+        self.status, self.loss_acc = status, loss_acc
+        self.epoch_starts = epoch_starts
+        self.walks = torch.empty((self.B, L), dtype=torch.int32, device=dev)
+        self.starts = torch.empty(self.B, dtype=torch.int32, device=dev)
+        s1 = tables.step_count + 1                      # the Adam step the first replay applies
+        hist = adam_history(s1 + n_steps + 2, tables.lr, tables.betas, tables.eps,
+                            tables.weight_decay)
+        self.hist = torch.from_numpy(hist).to(dev)
+        blk = np.zeros(1, dtype=_STEP_DTYPE)
+        blk['walk_id0'] = first_walk_id
+        blk['noise_offset'] = (first_walk_id * (L - 2 * R) if noise_offset is None
+                               else noise_offset)
+        blk['step'] = s1
+        blk['adam'][0] = hist[s1]
+        self.block = torch.from_numpy(np.frombuffer(blk.tobytes(), dtype=np.uint8).copy()).to(dev)
+        self._args = dict(seed=seed, grad_scale=grad_scale, scatter=scatter,
+                          fuse_out_adam=scatter == 'sorted')
+        self.R, self.K = R, K
+        self.graphs = {}
+        torch.cuda.synchronize(dev)
+        for _ in range(2):                  # one graph per parity of the in-table buffers
+            parity = tables._cur_in
+            g = torch.cuda.CUDAGraph()
+            _native.call('dw_step_scalars_bind', _native.ptr(self.block))
+            try:
+                with torch.cuda.graph(g, capture_error_mode='relaxed'):
+                    self._body()
+            finally:
+                _native.call('dw_step_scalars_bind', None)
+            self.graphs[parity] = g
+        tables.step_count -= 2              # the captures ran no step (host bookkeeping only)
+        torch.cuda.synchronize(dev)
+
+    def _body(self) -> None:
+        t, dev = self.t, self.t.device
+        with torch.cuda.device(dev):
+            _native.call('dw_step_starts', _native.ptr(self.block), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
+                         _native.stream(dev))
+        self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
+                               status=self.status)
+        replicated_step(t, self.walks, self.R, self.K, noise_offset=0, loss_acc=self.loss_acc,
+                        status=self.status, **self._args)
+        with torch.cuda.device(dev):
+            _native.call('dw_step_scalars_advance', _native.ptr(self.block),
+                         _native.ptr(self.hist), self.hist.shape[0], self.B, self.centres,
+                         _native.ptr(self.status), _native.stream(dev))
+
+    def replay(self) -> None:
+        """One training step (enqueued on the current stream); the tables' host bookkeeping
+        (Adam step count, current in-table buffer) follows as the eager step's would."""
+        t = self.t
+        self.graphs[t._cur_in].replay()
+        t.step_count += 1
+        t._next_in = 2 - t._cur_in
+        t._cur_in = t._next_in
+
+    def scalars(self) -> dict:
+        """The device block (synchronises): walk_id0, noise_offset, step."""
+        b = np.frombuffer(self.block.cpu().numpy().tobytes(), dtype=_STEP_DTYPE)[0]
+        return {'walk_id0': int(b['walk_id0']), 'noise_offset': int(b['noise_offset']),
+                'step': int(b['step'])}
+
+
+def epoch_starts_node_order(n_nodes: int, walks_per_node: int, device) -> torch.Tensor:
+    """bench.py's start order: walk w starts at node w // walks_per_node + 1 (vocabulary id)."""
+    ids = torch.arange(1, n_nodes + 1, dtype=torch.int32, device=device)
+    return ids.repeat_interleave(walks_per_node)
+

@@ -474,6 +474,42 @@ int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32
 
 int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void *stream);
 
+/* ---- step scalars in device memory (HIP-graph replay of a training step) ------------------------
+ * A small-batch training step is a few dozen microseconds of kernels; launched one by one from
+ * the host it is launch-bound. To replay a captured step (hipGraph), the values that change from
+ * step to step live in device memory instead of kernel arguments: while a dw_step_scalars block
+ * is BOUND (dw_step_scalars_bind, per host thread), every launch of
+ *   dw_walk_fast / dw_walk_fast_indexed   reads walk_id0 from it,
+ *   dw_sgns_walks_phase (pass 1)          reads noise_offset from it,
+ *   dw_adam_dense(_to), dw_sgns_walks_phase2_adam   read the Adam scalars adam[0..6],
+ * and ignores the corresponding host arguments. dw_step_scalars_advance, the last node of a
+ * captured step, moves the block to the next step. Nothing else changes: the kernels and their
+ * results are those of the eager launches (the bench and tests compare the two). Replaces no
+ * reference interface: it is how trainer.py:131-152's per-batch step is replayed on the device. */
+typedef struct dw_step_scalars {
+    uint64_t walk_id0;      /* global walk id of the step's first walk */
+    uint64_t noise_offset;  /* centre counter of the step's device negatives */
+    int64_t step;           /* the Adam step this step applies (1-based) */
+    float adam[8];          /* its scalars, dw_adam_dense order (as a dw_adam_rows hist row) */
+} dw_step_scalars;
+
+/* Bind (dev != NULL) or unbind (NULL) a device dw_step_scalars for the launches this host
+ * thread makes next. */
+int dw_step_scalars_bind(const dw_step_scalars *dev);
+
+/* One thread: walk_id0 += walks_per_step, noise_offset += centres_per_step, step += 1,
+ * adam = hist[step] (hist: float32[hist_rows][8]; a step beyond hist_rows sets DW_S_BAD_INDEX
+ * in status and leaves adam unchanged). */
+int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t hist_rows,
+                            uint64_t walks_per_step, uint64_t centres_per_step, int32_t *status,
+                            void *stream);
+
+/* starts_out[k] = epoch_starts[(dev->walk_id0 + k) mod n_epoch] for k < n: the start nodes of
+ * a step's walks when walk w of the epoch starts at epoch_starts[w] (RandomWalkDataset's
+ * `_get_current_node`, datasets.py:69-76, with the walk ids of the epoch). */
+int dw_step_starts(const dw_step_scalars *dev, const int32_t *epoch_starts, int64_t n_epoch,
+                   int32_t *starts_out, int64_t n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,78 @@
+"""The small-batch step replayed as a HIP graph (word2vec/graphed.py) equals the eager step.
+
+C2's shape (a 4,096-node R-MAT with Cora's edge count, node2vec p=1 q=1, L=10, R=2, K=5, d=128,
+64-walk batches): the same walks bit for bit, the same negatives and Adam steps, so the losses
+agree to float64-atomic order and the tables to fp32 atomic-order noise (the bars of
+test_gpu_sgns.py: at most 0.1% of entries outside rtol 1e-5 / atol 1e-6, none by more than
+lr / 100, no row drifting as a whole)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_sgns import assert_no_row_drift, assert_params_close
+
+pytestmark = pytest.mark.gpu
+
+B, L, R, K, D, LR, WPN, SEED = 64, 10, 2, 5, 128, 0.01, 16, 99
+
+
+def _setup(dev):
+    from shallow_encoders.graph.random_walk_generator import Node2Vec
+    from shallow_encoders.graph.rmat import rmat_graph
+    from shallow_encoders.word2vec.graphed import epoch_starts_node_order
+    csr = rmat_graph(12, 5429, 0, device=dev)
+    walker = Node2Vec(csr, L, p=1.0, q=1.0, rng='philox', seed=1234, device=dev)
+    starts = epoch_starts_node_order(csr.vocab_size - 1, WPN, dev)
+    return csr, walker, starts
+
+
+@pytest.mark.parametrize('scatter', ['sorted', 'atomic'])
+def test_graphed_step_equals_eager(hip_device, scatter):
+    from shallow_encoders.word2vec.graphed import GraphedStep
+    from shallow_encoders.word2vec.sharding import ShardedTables, replicated_step
+    dev = hip_device
+    csr, walker, epoch = _setup(dev)
+    V = csr.vocab_size
+    grad_scale = 1.0 / (B * (L - 2 * R) * 2 * R)
+    warm, steps = 2, 7
+    runs = []
+    for mode in ('eager', 'graph'):
+        t = ShardedTables(V, D, dev, lr=LR, init_seed=0)
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def eager(s):
+            g0 = s * B
+            st = epoch[torch.arange(g0, g0 + B, device=dev) % epoch.numel()]
+            walks = walker.walk_batch(st, walk_id0=g0, check=False)
+            replicated_step(t, walks, R, K, seed=SEED, noise_offset=g0 * (L - 2 * R),
+                            grad_scale=grad_scale, loss_acc=acc, status=status, scatter=scatter,
+                            fuse_out_adam=scatter == 'sorted')
+            return walks
+        for s in range(warm):                   # allocates the workspaces, as bench.py does
+            eager(s)
+        if mode == 'eager':
+            for s in range(warm, warm + steps):
+                last = eager(s)
+        else:
+            gs = GraphedStep(t, walker, epoch, B, R, K, seed=SEED, grad_scale=grad_scale,
+                             loss_acc=acc, status=status, first_walk_id=warm * B,
+                             n_steps=steps, scatter=scatter)
+            for _ in range(steps):
+                gs.replay()
+            last = gs.walks
+            sc = gs.scalars()
+            assert sc == {'walk_id0': (warm + steps) * B,
+                          'noise_offset': (warm + steps) * B * (L - 2 * R),
+                          'step': warm + steps + 1}
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0
+        assert t.step_count == warm + steps
+        runs.append((t.w_in.cpu().numpy(), t.w_out.cpu().numpy(), acc.cpu().numpy(),
+                     last.cpu().numpy()))
+    (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
+    np.testing.assert_array_equal(walks_g, walks_e)        # same walk ids and starts
+    np.testing.assert_allclose(acc_g, acc_e, rtol=1e-9)
+    for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
+        assert_params_close(got, exp, LR)
+        assert_no_row_drift(got, exp)
