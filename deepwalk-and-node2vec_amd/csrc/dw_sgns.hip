@@ -946,7 +946,7 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
 // skipped store leaves the same bits.
 template <int VPL, bool MASKED>
 __global__ void __launch_bounds__(256)
-    k_adam_rest(int64_t n_rows, int32_t d, const uint8_t *__restrict__ flags,
+    k_adam_rest(int64_t n_rows, int32_t d, uint8_t *__restrict__ flags,
                 float *__restrict__ g, OutAdam oa) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / WAVE);

@@ -346,17 +346,30 @@ __global__ void __launch_bounds__(256)
         out[k] = epoch[(base + static_cast<uint64_t>(k)) % static_cast<uint64_t>(n_epoch)];
 }
 
-__global__ void k_step_advance(dw_step_scalars *dyn, const float *__restrict__ hist,
-                               int64_t hist_rows, uint64_t walks_per_step,
-                               uint64_t centres_per_step, int32_t *status) {
-    dyn->walk_id0 += walks_per_step;
-    dyn->noise_offset += centres_per_step;
-    const int64_t s = ++dyn->step;
-    if (s >= hist_rows) {
-        dw::status_or(status, DW_S_BAD_INDEX);
-        return;
+// One block: thread 0 moves the block to the next step; then (epoch != NULL) the block's
+// threads write that step's start nodes, as k_step_starts would (one launch instead of two).
+__global__ void __launch_bounds__(256)
+    k_step_advance(dw_step_scalars *dyn, const float *__restrict__ hist, int64_t hist_rows,
+                   uint64_t walks_per_step, uint64_t centres_per_step, int32_t *status,
+                   const int32_t *__restrict__ epoch, int64_t n_epoch,
+                   int32_t *__restrict__ starts_out, int64_t n) {
+    __shared__ uint64_t next_wid;
+    if (threadIdx.x == 0) {
+        const uint64_t wid = dyn->walk_id0 + walks_per_step;
+        dyn->walk_id0 = wid;
+        next_wid = wid;
+        dyn->noise_offset += centres_per_step;
+        const int64_t s = ++dyn->step;
+        if (s >= hist_rows)
+            dw::status_or(status, DW_S_BAD_INDEX);
+        else
+            for (int k = 0; k < 8; ++k) dyn->adam[k] = hist[8 * s + k];
     }
-    for (int k = 0; k < 8; ++k) dyn->adam[k] = hist[8 * s + k];
+    if (!epoch) return;
+    __syncthreads();
+    const uint64_t base = next_wid;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x)
+        starts_out[k] = epoch[(base + static_cast<uint64_t>(k)) % static_cast<uint64_t>(n_epoch)];
 }
 
 constexpr int N2V_WAVES = 4;     // waves per block
@@ -811,10 +824,14 @@ int dw_step_starts(const dw_step_scalars *dev, const int32_t *epoch_starts, int6
 
 int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t hist_rows,
                             uint64_t walks_per_step, uint64_t centres_per_step, int32_t *status,
-                            void *stream) {
+                            const int32_t *epoch_starts, int64_t n_epoch, int32_t *starts_out,
+                            int64_t n, void *stream) {
     DW_REQUIRE(dev && hist && status && hist_rows >= 1, "dw_step_scalars_advance: bad arguments");
-    hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(1), 0, dw::as_stream(stream), dev, hist,
-                       hist_rows, walks_per_step, centres_per_step, status);
+    DW_REQUIRE(!epoch_starts || (starts_out && n_epoch >= 1 && n >= 0),
+               "dw_step_scalars_advance: bad start-node arguments");
+    hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(256), 0, dw::as_stream(stream), dev, hist,
+                       hist_rows, walks_per_step, centres_per_step, status, epoch_starts, n_epoch,
+                       starts_out, n);
     DW_LAUNCH_CHECK("dw_step_scalars_advance");
     return DW_OK;
 }

@@ -123,7 +123,8 @@ SIGNATURES = {
                                          _f32, _f32, _i32, _i64, _p]),
     'dw_scale': (ctypes.c_int, [_p, _i64, _f32, _p, _p]),
     'dw_step_scalars_bind': (ctypes.c_int, [_p]),
-    'dw_step_scalars_advance': (ctypes.c_int, [_p, _p, _i64, _u64, _u64, _p, _p]),
+    'dw_step_scalars_advance': (ctypes.c_int, [_p, _p, _i64, _u64, _u64, _p, _p, _i64, _p,
+                                               _i64, _p]),
     'dw_step_starts': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),
 }
 

@@ -12,7 +12,8 @@ the walk id of the step's first walk (the Philox walker), the centre counter of 
 capture, those kernels read it instead of their by-value arguments; the captured step ends with
 ``dw_step_scalars_advance``, which moves the block to the next step from a precomputed history of
 Adam scalars (float64 on the host, rounded to float32 exactly as the eager launches pass them).
-The start nodes come from the epoch's start list by walk id (``dw_step_starts``). The kernels and
+The start nodes come from the epoch's start list by walk id (``dw_step_starts`` for the first
+step; the advance writes the next step's). The kernels and
 their results are those of the eager step (tests/test_gpu_graphed.py).
 """
 from typing import Optional
@@ -76,6 +77,11 @@ class GraphedStep:
                           fuse_out_adam=scatter == 'sorted')
         self.R, self.K = R, K
         self.graphs = {}
+        # the first step's start nodes; every replay then ends by writing the next step's
+        with torch.cuda.device(dev):
+            _native.call('dw_step_starts', _native.ptr(self.block), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
+                         _native.stream(dev))
         torch.cuda.synchronize(dev)
         for _ in range(2):                  # one graph per parity of the in-table buffers
             parity = tables._cur_in
@@ -92,10 +98,6 @@ class GraphedStep:
 
     def _body(self) -> None:
         t, dev = self.t, self.t.device
-        with torch.cuda.device(dev):
-            _native.call('dw_step_starts', _native.ptr(self.block), _native.ptr(self.epoch_starts),
-                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
-                         _native.stream(dev))
         self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
                                status=self.status)
         replicated_step(t, self.walks, self.R, self.K, noise_offset=0, loss_acc=self.loss_acc,
@@ -103,7 +105,9 @@ class GraphedStep:
         with torch.cuda.device(dev):
             _native.call('dw_step_scalars_advance', _native.ptr(self.block),
                          _native.ptr(self.hist), self.hist.shape[0], self.B, self.centres,
-                         _native.ptr(self.status), _native.stream(dev))
+                         _native.ptr(self.status), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
+                         _native.stream(dev))
 
     def replay(self) -> None:
         """One training step (enqueued on the current stream); the tables' host bookkeeping

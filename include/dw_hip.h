@@ -497,12 +497,14 @@ typedef struct dw_step_scalars {
  * thread makes next. */
 int dw_step_scalars_bind(const dw_step_scalars *dev);
 
-/* One thread: walk_id0 += walks_per_step, noise_offset += centres_per_step, step += 1,
- * adam = hist[step] (hist: float32[hist_rows][8]; a step beyond hist_rows sets DW_S_BAD_INDEX
- * in status and leaves adam unchanged). */
+/* walk_id0 += walks_per_step, noise_offset += centres_per_step, step += 1, adam = hist[step]
+ * (hist: float32[hist_rows][8]; a step beyond hist_rows sets DW_S_BAD_INDEX in status and
+ * leaves adam unchanged); then, with epoch_starts != NULL, the new step's start nodes into
+ * starts_out exactly as dw_step_starts (one launch for both). */
 int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t hist_rows,
                             uint64_t walks_per_step, uint64_t centres_per_step, int32_t *status,
-                            void *stream);
+                            const int32_t *epoch_starts, int64_t n_epoch, int32_t *starts_out,
+                            int64_t n, void *stream);
 
 /* starts_out[k] = epoch_starts[(dev->walk_id0 + k) mod n_epoch] for k < n: the start nodes of
  * a step's walks when walk w of the epoch starts at epoch_starts[w] (RandomWalkDataset's
