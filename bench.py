@@ -792,7 +792,7 @@ def main():
             # (owner form: its own in-table rows' Adam runs on the side stream inside the op)
             want = (pairs_per_step, args.scatter, d, V, fuse, overlap_in or owner,
                     W_eff if owner else 0, args.in_exchange if owner else None)
-            pmc = next((e for e in doc.get('entries', []) if
+            pmc = next((e for e in reversed(doc.get('entries', [])) if   # the latest round
                         (e.get('pairs_per_launch'), e.get('scatter'), e.get('dim'),
                          e.get('vocab_size'), bool(e.get('fused_out_adam')),
                          bool(e.get('overlap_in')), int(e.get('owner_world') or 0),
