@@ -154,8 +154,9 @@ def cpu_baseline(csr, args, budget_s: float, walk_methods):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=30)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=400,
+                    help='timed steps (C3: ~2.7 s of GPU time, so the job clock sees the GPU busy)')
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch-walks', type=int, default=None)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS),
                     help='BASELINE workload preset: c2 = Cora-shaped R-MAT 12, node2vec, 64-walk '
