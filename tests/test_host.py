@@ -330,3 +330,29 @@ def test_cora_ingest_matches_reference(tmp_path, monkeypatch):
     assert [ds.labels[n] for n in names] == list(f['label_values'])
     np.testing.assert_array_equal(np.stack([ds.features[n] for n in names[:16]]),
                                   f['feature_sample'])
+
+
+def test_step_scalars_layout_and_history():
+    """word2vec/graphed.py's dw_step_scalars block matches include/dw_hip.h's struct (56 bytes,
+    walk_id0 @0, noise_offset @8, step @16, adam[8] @24) and its Adam history rows equal the
+    scalars the eager launches pass (adam_scalars rounded to float32)."""
+    import ctypes
+    from shallow_encoders.word2vec.graphed import _STEP_DTYPE, adam_history
+    from shallow_encoders.word2vec.sharding import adam_scalars
+
+    class StepScalars(ctypes.Structure):
+        _fields_ = [('walk_id0', ctypes.c_uint64), ('noise_offset', ctypes.c_uint64),
+                    ('step', ctypes.c_int64), ('adam', ctypes.c_float * 8)]
+    assert ctypes.sizeof(StepScalars) == _STEP_DTYPE.itemsize == 56
+    for name in ('walk_id0', 'noise_offset', 'step', 'adam'):
+        assert getattr(StepScalars, name).offset == _STEP_DTYPE.fields[name][1]
+    header = open(os.path.join(REPO, 'include', 'dw_hip.h')).read()
+    body = header[header.index('typedef struct dw_step_scalars'):]
+    body = body[:body.index('} dw_step_scalars;')]
+    assert re.findall(r'(uint64_t|int64_t|float) (\w+)', body) == [
+        ('uint64_t', 'walk_id0'), ('uint64_t', 'noise_offset'), ('int64_t', 'step'),
+        ('float', 'adam')]
+    h = adam_history(5, 0.01, (0.9, 0.999), 1e-8, 0.0)
+    for s in range(1, 6):
+        exp = [ctypes.c_float(x).value for x in adam_scalars(s, 0.01, (0.9, 0.999), 1e-8, 0.0)]
+        assert h[s, :7].tolist() == exp and h[s, 7] == 0.0
