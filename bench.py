@@ -340,6 +340,19 @@ def main():
     walks_buf = torch.empty((BG, L), dtype=torch.int32, device=dev)
     starts_buf = torch.empty(BG, dtype=torch.int32, device=dev)
 
+    # walk w of the job starts at node w // walks_per_node + 1 (the epoch's start list, resident;
+    # a step's starts are a slice of it — no per-step kernels)
+    from shallow_encoders.word2vec.graphed import epoch_starts_node_order
+    epoch_starts = epoch_starts_node_order(N, args.walks_per_node, dev)
+
+    def step_starts(g0: int, n: int, buf: torch.Tensor) -> torch.Tensor:
+        a = g0 % walks_total
+        if a + n <= walks_total:
+            return epoch_starts[a:a + n]
+        ids = torch.arange(a, a + n, device=dev, dtype=torch.int64) % walks_total
+        torch.index_select(epoch_starts, 0, ids, out=buf[:n])
+        return buf[:n]
+
     class WalkFeed:
         """The walks of step s, in buffer s % 2. With prefetch, step s+1's walks are generated
         on a side stream while step s's SGNS runs (the reference's DataLoader workers produce
@@ -362,11 +375,8 @@ def main():
         def _gen(self, s):
             i = s % len(self.walks)
             g0 = self.first_id(s)
-            ids = (torch.arange(g0, g0 + self.n, device=dev, dtype=torch.int64) % walks_total)
-            torch.floor_divide(ids, args.walks_per_node, out=ids)
-            self.starts[i][:self.n].copy_(ids + 1)
-            walker.walk_batch(self.starts[i][:self.n], walk_id0=g0, out=self.walks[i][:self.n],
-                              check=False)
+            walker.walk_batch(step_starts(g0, self.n, self.starts[i]), walk_id0=g0,
+                              out=self.walks[i][:self.n], check=False)
 
         def _launch(self, s):
             i = s % 2
@@ -421,11 +431,8 @@ def main():
             e[0].record()
         if gather:
             a0 = g0 + tables.rank * B
-            ids = (torch.arange(a0, a0 + B, device=dev, dtype=torch.int64) % walks_total)
-            torch.floor_divide(ids, args.walks_per_node, out=ids)
-            starts_buf[:B].copy_(ids + 1)
             own = walks_buf[tables.rank * B:(tables.rank + 1) * B]
-            walker.walk_batch(starts_buf[:B], walk_id0=a0, out=own, check=False)
+            walker.walk_batch(step_starts(a0, B, starts_buf), walk_id0=a0, out=own, check=False)
             send = own if backend == 'nccl' else own.clone()
             dist.all_gather_into_tensor(walks_buf.view(-1), send.reshape(-1))
             walks = walks_buf
@@ -450,9 +457,11 @@ def main():
         else:
             tables.exchange_in()        # full grid: 1/W of the in table, between RS and AG
         spec = tables.out_adam_spec() if fuse else None
-        n_rec[0] = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, K,
-                                    walks=walks, context_radius=R, out_adam=spec,
-                                    status=status)
+        # one owner keeps every slot: no record-count readback (the host runs ahead)
+        n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, K, walks=walks,
+                             context_radius=R, out_adam=spec, status=status,
+                             read_count=tables.world > 1)
+        n_rec[0] = n if n is not None else BG * (L - 2 * R) * 2 * R * (1 + K)
         if not gather:
             feed.release(s)
         if spec is None:
@@ -547,8 +556,8 @@ def main():
                  and args.method in ('deepwalk', 'node2vec') and not args.walk_prefetch
                  and (args.graph == 'on' or (args.graph == 'auto' and centres <= 100_000)))
     if use_graph:
-        from shallow_encoders.word2vec.graphed import GraphedStep, epoch_starts_node_order
-        graphed = GraphedStep(tables, walker, epoch_starts_node_order(N, args.walks_per_node, dev),
+        from shallow_encoders.word2vec.graphed import GraphedStep
+        graphed = GraphedStep(tables, walker, epoch_starts,
                               B, R, K, seed=99, grad_scale=grad_scale, loss_acc=loss_acc,
                               status=status, first_walk_id=step_idx[0] * B,
                               n_steps=args.steps + 1, scatter=args.scatter)

@@ -832,18 +832,50 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // Records sort: onesweep with 11-bit digits on 1024 x 16 tiles — 2 passes for C3's 21-bit row
 // ids (the gfx950 default, 8-bit digits on 1024 x 8, needs 3): 0.79 ms vs 1.09 ms for 34.4M
 // records on MI355X (scripts/microbench/sort_bench.hip).
+// Merge-sort limit 0: rocprim's default sends up to 1M items through its merge sort, which at
+// the reference's batch shape (64 walks: 269K records) ran as 20 launches and 120 us.
 using RecordSortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>,
                                         rocprim::kernel_config<1024, 16>, 11,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+// Smaller sorts (under SMALL_SORT_MAX items): 16K-item tiles leave most of the chip idle (17
+// blocks for 269K records, ~30 us per pass), so 2K-item tiles with 8-bit digits; merge sort up
+// to 128K items (the C2 shape).
+using SmallSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>,
+                                        rocprim::kernel_config<256, 8>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    128 * 1024>;
+constexpr uint32_t SMALL_SORT_MAX = 4u << 20;
+
+// Stable LSD sort of (key, value) pairs on bits [0, end_bit), the config chosen by size. With
+// tmp == nullptr: *bytes = the larger of both configs' needs for n (so any n' <= n fits).
+template <class K, class Vt>
+hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
+                      rocprim::double_buffer<Vt> &vb, uint32_t n, int end_bit, hipStream_t st) {
+    if (tmp == nullptr) {
+        size_t a = 0, b = 0;
+        hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, kb, vb, n, 0,
+                                                                   end_bit, st);
+        if (e == hipSuccess)
+            e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, kb, vb, n, 0, end_bit, st);
+        bytes = a > b ? a : b;
+        return e;
+    }
+    if (n < SMALL_SORT_MAX)
+        return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
+    return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
+}
 
 int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStream_t st) {
     size_t cub_bytes = 0;
     rocprim::double_buffer<uint32_t> kb(nullptr, nullptr);
     rocprim::double_buffer<uint64_t> vb(nullptr, nullptr);
-    hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
-        nullptr, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(V), st);
+    hipError_t e = sort_pairs(nullptr, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
+                              end_bit_for(V), st);
     if (e != hipSuccess) {
         dw::set_error("dw_sgns: sort size query failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
@@ -1000,8 +1032,10 @@ __global__ void __launch_bounds__(256)
 template <int VPL, bool MASKED>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_lazy_boundary(const uint32_t *__restrict__ keys, int64_t n_rec, int32_t gch,
-                    float *__restrict__ g_out, int32_t d, OutAdam oa) {
+                    float *__restrict__ g_out, int32_t d, OutAdam oa,
+                    const int64_t *__restrict__ range) {
     const int lane = threadIdx.x & (WAVE - 1);
+    if (range) n_rec = range[1];   // (range[0] == 0: the padded owner sort, launch_owner_pass2)
     const int64_t n_chunks = (n_rec + gch - 1) / gch;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; ch < n_chunks;
@@ -1026,16 +1060,18 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 
 template <int VPL>
 void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_t gch,
-                     float *g_out, int32_t d, const OutAdam &oa) {
+                     float *g_out, int32_t d, const OutAdam &oa, const int64_t *range) {
     int64_t blocks = ((n_rec + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
     if (d == 64 * VPL)
         hipLaunchKernelGGL((k_lazy_boundary<VPL, false>), dim3((unsigned)blocks),
-                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa);
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa,
+                           range);
     else
         hipLaunchKernelGGL((k_lazy_boundary<VPL, true>), dim3((unsigned)blocks),
-                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa);
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa,
+                           range);
 }
 
 template <int VPL>
@@ -1085,7 +1121,12 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     // in 512-record chunks ran as 18 waves, 240 us of latency-bound gathers
     int32_t gch = GCH;
     {
-        const int64_t want = grid_cap(16);   // 4 waves per SIMD
+        static const int per_cu = [] {
+            const char *e = getenv("DW_GATHER_WAVES_PER_CU");
+            const int v = e ? atoi(e) : 0;
+            return v > 0 ? v : 16;
+        }();
+        const int64_t want = grid_cap(per_cu);   // 4 waves per SIMD
         while (gch > 32 && (n_rec + gch - 1) / gch < want) gch >>= 1;
     }
     const int64_t n_chunks = (n_rec + gch - 1) / gch;
@@ -1101,10 +1142,10 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     DW_LAUNCH_CHECK("dw_sgns/gather");
     if (oa && oa->last) {   // lazy: only the straddling rows remain; untouched rows wait
         if (n_rec > 0) {
-            if (d <= 64) launch_boundary<1>(st, keys, n_rec, gch, g_out, d, *oa);
-            else if (d <= 128) launch_boundary<2>(st, keys, n_rec, gch, g_out, d, *oa);
-            else if (d <= 256) launch_boundary<4>(st, keys, n_rec, gch, g_out, d, *oa);
-            else launch_boundary<8>(st, keys, n_rec, gch, g_out, d, *oa);
+            if (d <= 64) launch_boundary<1>(st, keys, n_rec, gch, g_out, d, *oa, range);
+            else if (d <= 128) launch_boundary<2>(st, keys, n_rec, gch, g_out, d, *oa, range);
+            else if (d <= 256) launch_boundary<4>(st, keys, n_rec, gch, g_out, d, *oa, range);
+            else launch_boundary<8>(st, keys, n_rec, gch, g_out, d, *oa, range);
             DW_LAUNCH_CHECK("dw_sgns/lazy_boundary");
         }
     } else if (oa) {
@@ -1206,8 +1247,8 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
     rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
-    hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
-        ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(a.V), st);
+    hipError_t e = sort_pairs(ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
+                              end_bit_for(a.V), st);
     if (e != hipSuccess) {
         dw::set_error("dw_sgns: records sort failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
@@ -1265,8 +1306,8 @@ int launch_pieces(SgnsArgs a, void *workspace, size_t workspace_bytes, int piece
             rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
             rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
             size_t cub_bytes = ws.cub_bytes;
-            hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
-                ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(a.V), st);
+            hipError_t e = sort_pairs(ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
+                                      end_bit_for(a.V), st);
             if (e != hipSuccess) {
                 dw::set_error("dw_sgns: records sort failed: %s", hipGetErrorString(e));
                 return DW_E_HIP;
@@ -1368,6 +1409,25 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// Pass 2 without the count readback (n_records NULL): the compacted records [0, *count) are
+// followed by sentinel keys up to the bound n_centres * T (all ones: with the sort's end bit they
+// rank after every row, and the stable sort keeps them behind equal low bits), and range =
+// {0, *count} limits the gather. With one owner every slot is kept and nothing is padded.
+__global__ void __launch_bounds__(256)
+    k_rec_pad(const uint32_t *__restrict__ count, int64_t bound, uint32_t *__restrict__ keys,
+              uint64_t *__restrict__ vals, int64_t *__restrict__ range) {
+    const int64_t n = *count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        range[0] = 0;
+        range[1] = n < bound ? n : bound;
+    }
+    for (int64_t i = n + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < bound;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        keys[i] = 0xFFFFFFFFu;
+        vals[i] = 0ull;
+    }
+}
+
 // occurrence b (centre position of the walks) keyed by its node, for the node-order sort
 __global__ void __launch_bounds__(256)
     k_occ_keys(const int32_t *__restrict__ walks, int64_t n_centres, int32_t L, int32_t R,
@@ -1391,8 +1451,8 @@ struct OccSpace {
 int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t st) {
     size_t tmp = 0, utmp = 0;
     rocprim::double_buffer<uint32_t> kb(nullptr, nullptr), vb(nullptr, nullptr);
-    if (rocprim::radix_sort_pairs(nullptr, tmp, kb, vb, static_cast<uint32_t>(n_centres), 0,
-                                  end_bit_for(V), st) != hipSuccess ||
+    if (sort_pairs(nullptr, tmp, kb, vb, static_cast<uint32_t>(n_centres), end_bit_for(V),
+                   st) != hipSuccess ||
         rocprim::unique(nullptr, utmp, static_cast<const uint32_t *>(nullptr),
                         static_cast<uint32_t *>(nullptr), static_cast<int64_t *>(nullptr),
                         static_cast<size_t>(n_centres), rocprim::equal_to<uint32_t>(),
@@ -1447,8 +1507,8 @@ int owner_order(const SgnsArgs &a, const OccSpace &occ, uint32_t *touched, int64
     DW_LAUNCH_CHECK("dw_sgns_owner/occ_keys");
     rocprim::double_buffer<uint32_t> kb(occ.k0, occ.k1), vb(occ.v0, occ.v1);
     size_t tb = occ.tmp_bytes;
-    if (rocprim::radix_sort_pairs(occ.tmp, tb, kb, vb, static_cast<uint32_t>(a.batch), 0,
-                                  end_bit_for(a.V), st) != hipSuccess) {
+    if (sort_pairs(occ.tmp, tb, kb, vb, static_cast<uint32_t>(a.batch), end_bit_for(a.V),
+                   st) != hipSuccess) {
         dw::set_error("dw_sgns_owner: occurrence sort failed");
         return DW_E_HIP;
     }
@@ -1545,24 +1605,36 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
                              "dw_sgns_owner_pass2");
     if (rc != DW_OK) return rc;
-    // the record count decides the sort's size on the host: one stream synchronisation
-    uint32_t n = 0;
-    if (hipMemcpyAsync(&n, ws.count, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-        dw::set_error("dw_sgns_owner_pass2: reading the record count failed");
-        return DW_E_HIP;
+    const int64_t bound = n_centres * T;
+    const int64_t *range = nullptr;
+    int64_t n_rec = bound;
+    if (n_records) {
+        // the record count decides the sort's size on the host: one stream synchronisation
+        uint32_t n = 0;
+        if (hipMemcpyAsync(&n, ws.count, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner_pass2: reading the record count failed");
+            return DW_E_HIP;
+        }
+        n_rec = static_cast<int64_t>(n) < bound ? n : bound;
+        *n_records = n_rec;
+    } else if (bound > 0) {
+        // no readback: sort the bound with the tail padded, gather [0, count) (k_rec_pad)
+        int64_t pb = (bound + 255) / 256;
+        if (pb > grid_cap(4)) pb = grid_cap(4);
+        hipLaunchKernelGGL(k_rec_pad, dim3((unsigned)pb), dim3(256), 0, st, ws.count, bound,
+                           ws.k1, ws.v1, ws.bounds);
+        DW_LAUNCH_CHECK("dw_sgns_owner_pass2/pad");
+        range = ws.bounds;
     }
-    const int64_t n_rec = static_cast<int64_t>(n) < n_centres * T ? n : n_centres * T;
-    if (n_records) *n_records = n_rec;
     const uint32_t *keys = ws.k1;  // compacted by pass 1
     const uint64_t *vals = ws.v1;
     if (n_rec > 0) {
         rocprim::double_buffer<uint32_t> kb(ws.k1, ws.k0);
         rocprim::double_buffer<uint64_t> vb(ws.v1, ws.v0);
         size_t cub_bytes = ws.cub_bytes;
-        hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(
-            ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec), 0, end_bit_for(local_rows),
-            st);
+        hipError_t e = sort_pairs(ws.cub, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
+                                  end_bit_for(local_rows), st);
         if (e != hipSuccess) {
             dw::set_error("dw_sgns_owner_pass2: records sort failed: %s", hipGetErrorString(e));
             return DW_E_HIP;
@@ -1572,7 +1644,7 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     }
     g_timer.mark(2, st);
     if (n_rec > 0 || oa) {
-        rc = launch_pass2(keys, vals, n_rec, w_in, g_out, d, oa, local_rows, st);
+        rc = launch_pass2(keys, vals, n_rec, w_in, g_out, d, oa, local_rows, st, range);
         if (rc != DW_OK) return rc;
     }
     g_timer.mark(3, st);

@@ -390,13 +390,16 @@ def sgns_owner_prepare(walks: torch.Tensor, context_radius: int, neg_samples: in
 def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local: torch.Tensor,
                      neg_samples: int, *, walks: torch.Tensor, context_radius: int,
                      out_adam: Optional[dict] = None,
-                     status: Optional[torch.Tensor] = None) -> int:
+                     status: Optional[torch.Tensor] = None,
+                     read_count: bool = True) -> Optional[int]:
     """Pass 2 of the owner-computes step (dw_sgns_owner_pass2) after sgns_owner_pass1 with the
     same walks: the records sort and gather over the local slice. ``out_adam`` ({'m', 'v',
     'flags', 'scalars'}, OwnerTables.out_adam_spec()) fuses the slice's Adam step in (w_out_local
     updated, g_out_local left zero); {'m', 'v', 'last', 'hist', 'step'}
     (OwnerLazyTables(lazy_out=True)) the lazy exact form; None accumulates g_out_local. Returns the record count
-    (the call synchronises the current stream once to read it)."""
+    (the call synchronises the current stream once to read it); ``read_count=False`` skips
+    that synchronisation and sorts the slot bound instead (one owner: every slot is kept, so
+    the bound is the count) and returns None."""
     import ctypes
     dev = w_in.device
     d = w_in.shape[1]
@@ -409,6 +412,7 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
     ws = workspace_for(n * (L - 2 * R), 2 * R, K, w_in.shape[0], dev, local_rows=local_rows)
     n_rec = ctypes.c_int64(0)
+    n_rec_p = ctypes.byref(n_rec) if read_count else None
     if out_adam is not None and 'last' in out_adam:      # OwnerLazyTables(lazy_out=True)
         with torch.cuda.device(dev):
             _native.call('dw_sgns_owner_pass2_lazy', n, L, R, K, local_rows, d, _native.ptr(w_in),
@@ -416,8 +420,8 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
                          int(out_adam['step']), _native.ptr(status), _native.ptr(ws), ws.numel(),
-                         ctypes.byref(n_rec), _native.stream(dev))
-        return int(n_rec.value)
+                         n_rec_p, _native.stream(dev))
+        return int(n_rec.value) if read_count else None
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                            _native.ptr(out_adam['flags']), out_adam['scalars'])
@@ -427,6 +431,6 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass2', n, L, R, K, local_rows, d, _native.ptr(w_in),
                      _native.ptr(w_out_local), _native.ptr(g_out_local), m, v, flags, *sc,
-                     _native.ptr(status), _native.ptr(ws), ws.numel(), ctypes.byref(n_rec),
+                     _native.ptr(status), _native.ptr(ws), ws.numel(), n_rec_p,
                      _native.stream(dev))
-    return int(n_rec.value)
+    return int(n_rec.value) if read_count else None

@@ -676,7 +676,11 @@ def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
     tables.exchange_in(overlap_bytes)
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in, tables.w_out, tables.g_out, neg_samples, walks=walks,
-                         context_radius=context_radius, out_adam=spec, status=status)
+                         context_radius=context_radius, out_adam=spec, status=status,
+                         read_count=tables.world > 1)
+    if n is None:   # one owner keeps every slot (no count readback)
+        n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
+            1 + neg_samples)
     if spec is None:
         tables.out_step()
     tables.sync()
@@ -684,6 +688,7 @@ def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
 
 
 HIST_CAP0 = 1024   # initial rows of OwnerLazyTables' Adam-scalar history (doubled on demand)
+HIST_AHEAD = 256   # history rows written per host-to-device copy (begin_step)
 
 
 def hip_rows_adam(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor,
@@ -777,6 +782,7 @@ class OwnerLazyTables(OwnerTables):
         self._hist = torch.zeros((HIST_CAP0, 8), **f32)
         self._hist_host = torch.zeros((HIST_CAP0, 8), dtype=torch.float32, pin_memory=pin)
         self._lr_hist = [0.0]
+        self._hist_ready, self._hist_key = 0, None
         self._touched = None
         self._n_max = 0
         self._n_touched = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -802,19 +808,26 @@ class OwnerLazyTables(OwnerTables):
 
     # ---- the step ------------------------------------------------------------------------------
     def begin_step(self) -> None:
-        """Starts Adam step t and records its scalars for the replays."""
+        """Starts Adam step t and records its scalars for the replays. The rows are written
+        HIST_AHEAD steps at a time (one host-to-device copy per block, not per step) for the
+        current hyper-parameters; a change of lr (a scheduler) rewrites them from step t."""
         self.step_count += 1
         s = self.step_count
-        if s >= self._hist.shape[0]:
-            cap = 2 * self._hist.shape[0]
-            h = torch.zeros((cap, 8), dtype=torch.float32, device=self.device)
-            h[:self._hist.shape[0]] = self._hist
-            hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
-            hh[:self._hist_host.shape[0]] = self._hist_host
-            self._hist, self._hist_host = h, hh
-        sc = adam_scalars(s, self.lr, self.betas, self.eps, self.weight_decay)
-        self._hist_host[s, :7] = torch.tensor(sc, dtype=torch.float32)
-        self._hist[s].copy_(self._hist_host[s], non_blocking=True)
+        key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
+        if s > self._hist_ready or key != self._hist_key:
+            hi = s + HIST_AHEAD - 1
+            if hi >= self._hist.shape[0]:
+                cap = max(2 * self._hist.shape[0], hi + 1)
+                h = torch.zeros((cap, 8), dtype=torch.float32, device=self.device)
+                h[:self._hist.shape[0]] = self._hist
+                hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
+                hh[:self._hist_host.shape[0]] = self._hist_host
+                self._hist, self._hist_host = h, hh
+            rows = [adam_scalars(t, self.lr, self.betas, self.eps, self.weight_decay)
+                    for t in range(s, hi + 1)]
+            self._hist_host[s:hi + 1, :7] = torch.tensor(rows, dtype=torch.float32)
+            self._hist[s:hi + 1].copy_(self._hist_host[s:hi + 1], non_blocking=True)
+            self._hist_ready, self._hist_key = hi, key
         self._lr_hist.append(self.lr)
 
     def prepare(self, walks: torch.Tensor, context_radius: int, neg_samples: int) -> None:
@@ -826,9 +839,10 @@ class OwnerLazyTables(OwnerTables):
         sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
                            touched=self._touched, n_touched=self._n_touched)
         self._n_max = n
-        self._n_host.copy_(self._n_touched, non_blocking=True)
-        self._n_event = torch.cuda.Event()
-        self._n_event.record(torch.cuda.current_stream(self.device))
+        if self.world > 1 and not self.emulated:   # |U| sizes the all-reduce (exchange_touched)
+            self._n_host.copy_(self._n_touched, non_blocking=True)
+            self._n_event = torch.cuda.Event()
+            self._n_event.record(torch.cuda.current_stream(self.device))
 
     def set_touched(self, rows: torch.Tensor) -> None:
         """CPU protocol (tests): the step's touched rows (distinct centre ids)."""
@@ -961,7 +975,11 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,
-                         context_radius=context_radius, out_adam=spec, status=status)
+                         context_radius=context_radius, out_adam=spec, status=status,
+                         read_count=tables.world > 1)
+    if n is None:   # one owner keeps every slot (no count readback)
+        n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
+            1 + neg_samples)
     if spec is None:
         tables.out_step()
     tables.update_touched()

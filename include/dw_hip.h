@@ -281,9 +281,13 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
  * pass 2: sorts the records by local row and accumulates the slice's gradient: with m_out
  *         non-NULL, the slice's torch.optim.Adam step is fused in exactly as in
  *         dw_sgns_walks_phase2_adam (g_out_local zero on entry and left zero, row_flags
- *         local_rows bytes); with m_out NULL, g_out_local += the gradient. It reads the record
- *         count back to the host (ONE synchronisation of `stream`); *n_records (optional)
- *         receives it. Same walk sizes and workspace as the pass-1 call. */
+ *         local_rows bytes); with m_out NULL, g_out_local += the gradient. With n_records
+ *         non-NULL it reads the record count back to the host (ONE synchronisation of
+ *         `stream`) into *n_records and sorts exactly that many; with n_records NULL there is
+ *         no synchronisation: the sort runs over the bound n_walks*(L-2R)*2R(1+K) with the
+ *         tail padded past every row and the gather limited on the device — the choice for
+ *         n_owners = 1, where every slot is kept and the bound is the count. Same walk sizes
+ *         and workspace as the pass-1 call. */
 int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_samples,
                                   int64_t vocab_size, int64_t local_rows, size_t *bytes);
 /* The owner form's centre order for a batch ahead of pass 1 (pass 1 with order_ready = 1 uses

@@ -403,3 +403,58 @@ def test_owner_lazy_two_ranks_equal_single_process(hip_device):
         bad = ~np.isclose(got, exp, rtol=1e-4, atol=1e-6)
         assert bad.mean() < 1e-3, bad.mean()
         assert_no_row_drift(got, exp, rtol=1e-4)
+
+
+@pytest.mark.parametrize('W,mode', [(1, 'acc'), (1, 'fused'), (1, 'lazy'), (3, 'acc'),
+                                    (3, 'fused'), (3, 'lazy'), (1, 'bad')])
+def test_owner_pass2_without_count_readback(hip_device, W, mode):
+    """read_count=False (n_records NULL): no host synchronisation — the sort runs over the slot
+    bound with the tail padded past every row and the gather is limited on the device
+    (k_rec_pad). One owner keeps every slot, so the records and their chunking are those of the
+    counted call: bit-exact, but for the hub row, whose records span several gather chunks and
+    are summed by atomics in no fixed order (so two counted calls differ there as well). With
+    W = 3 (or dropped bad ids) the tail is padded and the chunk size follows the bound: equal up
+    to the boundary rows' summation order."""
+    from shallow_encoders.word2vec.sharding import adam_scalars
+    from shallow_encoders.word2vec.graphed import adam_history
+    rng = np.random.default_rng(W * 7 + len(mode))
+    V, d, R, K, L, n = 2500, 128, 3, 4, 20, 48
+    S = -(-V // W)
+    w_in = torch.as_tensor(sgns_ref.xavier_tables(V, d, seed=4)[0]).cuda()
+    base = torch.randn((S, d), generator=torch.Generator().manual_seed(2)).cuda() * 0.1
+    walks = torch.as_tensor(rng.integers(0, V, size=(n, L)).astype(np.int32)).cuda()
+    walks[:, ::5] = 17                      # a hub row straddling gather chunks
+    if mode == 'bad':
+        walks[3, 7] = V + 5
+    hist = torch.as_tensor(adam_history(4, 0.02, (0.9, 0.999), 1e-8, 0.0)).cuda()
+    outs = []
+    for read in (True, False):
+        w, g = base.clone(), torch.zeros_like(base)
+        m, v = torch.zeros_like(base), torch.zeros_like(base)
+        flags = torch.zeros(S, dtype=torch.uint8, device='cuda')
+        last = torch.zeros(S, dtype=torch.int32, device='cuda')
+        status = torch.zeros(1, dtype=torch.int32, device='cuda')
+        g_in = torch.zeros_like(w_in)
+        sgns_owner_pass1(w_in, w, g_in, K, walks=walks, context_radius=R, owner=W - 1,
+                         n_owners=W, vocab_size=V, seed=5, noise_offset=0, status=status)
+        spec = {'acc': None, 'bad': None,
+                'fused': {'m': m, 'v': v, 'flags': flags,
+                          'scalars': adam_scalars(1, 0.02, (0.9, 0.999), 1e-8, 0.0)},
+                'lazy': {'m': m, 'v': v, 'last': last, 'hist': hist, 'step': 1}}[mode]
+        r = sgns_owner_pass2(w_in, w, g, K, walks=walks, context_radius=R, out_adam=spec,
+                             status=status, read_count=read)
+        torch.cuda.synchronize()
+        assert (r is None) == (not read)
+        outs.append((w, g, m, v, flags, last, int(status.item())))
+    (w1, g1, m1, v1, f1, l1, s1), (w2, g2, m2, v2, f2, l2, s2) = outs
+    assert s1 == s2 and ((s1 != 0) == (mode == 'bad'))
+    assert torch.equal(f1, f2) and torch.equal(l1, l2)
+    if W == 1 and mode != 'bad':
+        rest = torch.ones(S, dtype=torch.bool, device='cuda')
+        rest[17] = False
+        for a, b in ((w1, w2), (g1, g2), (m1, m2), (v1, v2)):
+            assert torch.equal(a[rest], b[rest])
+    scale = float(g1.abs().max()) + 1e-30
+    torch.testing.assert_close(g2, g1, rtol=1e-5, atol=1e-6 * scale)
+    torch.testing.assert_close(m2, m1, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(w2, w1, rtol=1e-5, atol=1e-5 * 0.02)
