@@ -126,33 +126,48 @@ __global__ void __launch_bounds__(256)
             from[k] = r[k] < n_table ? __builtin_amdgcn_readfirstlane(last[r[k]]) : step;
             go[k] = from[k] < (STEP ? step : upto);   // not already current (or stepped)
         }
+        // lanes past d hold zeros and run the updates harmlessly (uniform replay loops: the
+        // step scalars come through the scalar cache, the loop is pure ALU)
         float pp[2][VPL], mm[2][VPL], vv[2][VPL], gg[2][VPL];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
 #pragma unroll
             for (int q = 0; q < VPL; ++q) {
                 const int e = lane + 64 * q;
-                if (!go[k] || e >= d) continue;
+                const bool ld = go[k] && e < d;
                 const int64_t o = r[k] * d + e;
-                pp[k][q] = p[o];
-                mm[k][q] = m[o];
-                vv[k][q] = v[o];
-                if (STEP) gg[k][q] = g_rows[(i0 + k) * d + e];
+                pp[k][q] = ld ? p[o] : 0.f;
+                mm[k][q] = ld ? m[o] : 0.f;
+                vv[k][q] = ld ? v[o] : 0.f;
+                gg[k][q] = (STEP && ld) ? g_rows[(i0 + k) * d + e] : 0.f;
             }
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (!go[k]) continue;
+            for (int32_t s = from[k] + 1; s <= upto; ++s) {
+                const dw::AdamScalars h = hist_at(hist, s);
+                if (h.wd == 0.f) {
+#pragma unroll
+                    for (int q = 0; q < VPL; ++q) dw::adam_elem_g0(pp[k][q], mm[k][q], vv[k][q], h);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < VPL; ++q) {
+                        float z = 0.f;
+                        dw::adam_elem(pp[k][q], z, mm[k][q], vv[k][q], h);
+                    }
+                }
+            }
+            if (STEP) {
+                const dw::AdamScalars h = hist_at(hist, step);
+#pragma unroll
+                for (int q = 0; q < VPL; ++q)
+                    dw::adam_elem(pp[k][q], gg[k][q], mm[k][q], vv[k][q], h);
+            }
 #pragma unroll
             for (int q = 0; q < VPL; ++q) {
                 const int e = lane + 64 * q;
                 if (e >= d) continue;
-                for (int32_t s = from[k] + 1; s <= upto; ++s) {
-                    float z = 0.f;
-                    dw::adam_elem(pp[k][q], z, mm[k][q], vv[k][q], hist_at(hist, s));
-                }
-                if (STEP) dw::adam_elem(pp[k][q], gg[k][q], mm[k][q], vv[k][q],
-                                        hist_at(hist, step));
                 const int64_t o = r[k] * d + e;
                 p[o] = pp[k][q];
                 m[o] = mm[k][q];

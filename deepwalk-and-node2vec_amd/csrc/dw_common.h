@@ -121,6 +121,18 @@ __device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v
     p = p + s.nstep * (m / denom);
 }
 
+// adam_elem with g = 0 when weight_decay == 0 (the lazy replays' deferred steps; callers test
+// wd once per step, uniformly). The same IEEE operations give the same bits: gg - m is -m
+// exactly (for m = +-0 both forms make fmaf's result +0), omb2 * 0 * 0 is +0 and v + (+0) is v
+// for every v the update can hold (v >= +0, or NaN / inf) — minus the dead operations and the
+// per-lane weight-decay select, which the replay loops, ALU-bound, otherwise pay every step.
+__device__ __forceinline__ void adam_elem_g0(float &p, float &m, float &v, const AdamScalars &s) {
+#pragma clang fp contract(off)
+    m = fmaf(s.w1, -m, m);
+    v = v * s.b2;
+    const float denom = sqrtf(v) / s.bc2s + s.eps;
+    p = p + s.nstep * (m / denom);
+}
 
 // The Adam scalars a kernel uses: the bound step block's when there is one (graph replay),
 // else the launch's by-value ones.

@@ -694,22 +694,41 @@ struct OutAdam {
 template <int VPL, bool MASKED>
 __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, int32_t d,
                                               int lane, const float (&g)[VPL]) {
-    const int32_t from = oa.last[row];
+    // (row is wave-uniform; lanes past d carry zeros through a uniform replay loop)
+    const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
     const int64_t o = static_cast<int64_t>(row) * d + lane;
+    float pp[VPL], mm[VPL], vv[VPL], gg[VPL];
+#pragma unroll
+    for (int m = 0; m < VPL; ++m) {
+        const bool live = !MASKED || lane + WAVE * m < d;
+        const int64_t i = o + WAVE * m;
+        pp[m] = live ? oa.p[i] : 0.f;
+        mm[m] = live ? oa.m[i] : 0.f;
+        vv[m] = live ? oa.v[i] : 0.f;
+        gg[m] = g[m];
+    }
+    for (int32_t t = from + 1; t < oa.step; ++t) {
+        const dw::AdamScalars h = dw::hist_at(oa.hist, t);
+        if (h.wd == 0.f) {
+#pragma unroll
+            for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
+        } else {
+#pragma unroll
+            for (int m = 0; m < VPL; ++m) {
+                float z = 0.f;
+                dw::adam_elem(pp[m], z, mm[m], vv[m], h);
+            }
+        }
+    }
+    const dw::AdamScalars h = dw::hist_at(oa.hist, oa.step);
 #pragma unroll
     for (int m = 0; m < VPL; ++m) {
         if (MASKED && lane + WAVE * m >= d) continue;
+        dw::adam_elem(pp[m], gg[m], mm[m], vv[m], h);
         const int64_t i = o + WAVE * m;
-        float pp = oa.p[i], mm = oa.m[i], vv = oa.v[i];
-        for (int32_t t = from + 1; t < oa.step; ++t) {
-            float z = 0.f;
-            dw::adam_elem(pp, z, mm, vv, dw::hist_at(oa.hist, t));
-        }
-        float gg = g[m];
-        dw::adam_elem(pp, gg, mm, vv, dw::hist_at(oa.hist, oa.step));
-        oa.p[i] = pp;
-        oa.m[i] = mm;
-        oa.v[i] = vv;
+        oa.p[i] = pp[m];
+        oa.m[i] = mm[m];
+        oa.v[i] = vv[m];
     }
     if (lane == 0) oa.last[row] = oa.step;
 }
