@@ -94,87 +94,54 @@ __global__ void __launch_bounds__(256)
 //   last[r]:       the step up to which row r's (p, m, v) are current
 using dw::hist_at;
 
-// One wave per row (lanes over the row's elements, VPL per lane: d <= 64 * VPL), two rows per
-// trip with all six of their loads issued before any replay (the rows are independent; a
-// latency-bound kernel otherwise). STEP: replay the missed steps up to step - 1, then apply
-// `step` with the row's gradient g_rows[i]; else replay up to `step`.
-template <bool STEP, int VPL>
-__global__ void __launch_bounds__(256)
+// One block per row, one element per thread (blockDim = 64 * ceil(d / 64)): the replays are
+// ALU-bound dependent chains (correctly rounded sqrt and two divisions per element-step), so the
+// row is spread over as many waves as it has 64-element pieces — at C3's 64-walk batch the
+// in-table catch-up replays ~234 steps on 4,480 rows, and 2 waves per row fill the SIMDs where
+// one wave per row (two rows per trip) left them latency-bound. Every wave reads last[r] before
+// the barrier; thread 0 writes it after. STEP: replay the missed steps up to step - 1, then
+// apply `step` with the row's gradient g_rows[i]; else replay up to `step`. The step loop is
+// uniform: lanes past d carry zeros and are not stored.
+template <bool STEP>
+__global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
                 int32_t *__restrict__ last, int64_t n_table, int32_t d,
                 const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
                 int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
                 int32_t step) {
-    const int lane = threadIdx.x & 63;
+    const int e = threadIdx.x;
+    const bool live = e < d;
     int64_t n = n_max;
     if (n_dev) {
         const int64_t c = *n_dev;
         n = c < n_max ? c : n_max;
     }
     const int32_t upto = STEP ? step - 1 : step;
-    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / 64);
-    for (int64_t i0 = 2 * ((int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); i0 < n;
-         i0 += 2 * n_waves) {
-        int64_t r[2];
-        int32_t from[2];
-        bool go[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int64_t i = i0 + k;
-            r[k] = i < n ? (rows ? static_cast<int64_t>(rows[i]) : i) : n_table;
-            // an out-of-range centre is reported by the SGNS pass
-            from[k] = r[k] < n_table ? __builtin_amdgcn_readfirstlane(last[r[k]]) : step;
-            go[k] = from[k] < (STEP ? step : upto);   // not already current (or stepped)
-        }
-        // lanes past d hold zeros and run the updates harmlessly (uniform replay loops: the
-        // step scalars come through the scalar cache, the loop is pure ALU)
-        float pp[2][VPL], mm[2][VPL], vv[2][VPL], gg[2][VPL];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-#pragma unroll
-            for (int q = 0; q < VPL; ++q) {
-                const int e = lane + 64 * q;
-                const bool ld = go[k] && e < d;
-                const int64_t o = r[k] * d + e;
-                pp[k][q] = ld ? p[o] : 0.f;
-                mm[k][q] = ld ? m[o] : 0.f;
-                vv[k][q] = ld ? v[o] : 0.f;
-                gg[k][q] = (STEP && ld) ? g_rows[(i0 + k) * d + e] : 0.f;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t r = rows ? static_cast<int64_t>(rows[i]) : i;
+        // an out-of-range centre is reported by the SGNS pass
+        const int32_t from = r < n_table ? __builtin_amdgcn_readfirstlane(last[r]) : step;
+        __syncthreads();   // every wave has read last[r] before thread 0 advances it
+        if (from >= (STEP ? step : upto)) continue;   // already current (or stepped)
+        const int64_t o = r * d + e;
+        float pp = live ? p[o] : 0.f, mm = live ? m[o] : 0.f, vv = live ? v[o] : 0.f;
+        float gg = (STEP && live) ? g_rows[i * d + e] : 0.f;
+        for (int32_t s = from + 1; s <= upto; ++s) {
+            const dw::AdamScalars h = hist_at(hist, s);
+            if (h.wd == 0.f) {
+                dw::adam_elem_g0(pp, mm, vv, h);
+            } else {
+                float z = 0.f;
+                dw::adam_elem(pp, z, mm, vv, h);
             }
         }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (!go[k]) continue;
-            for (int32_t s = from[k] + 1; s <= upto; ++s) {
-                const dw::AdamScalars h = hist_at(hist, s);
-                if (h.wd == 0.f) {
-#pragma unroll
-                    for (int q = 0; q < VPL; ++q) dw::adam_elem_g0(pp[k][q], mm[k][q], vv[k][q], h);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < VPL; ++q) {
-                        float z = 0.f;
-                        dw::adam_elem(pp[k][q], z, mm[k][q], vv[k][q], h);
-                    }
-                }
-            }
-            if (STEP) {
-                const dw::AdamScalars h = hist_at(hist, step);
-#pragma unroll
-                for (int q = 0; q < VPL; ++q)
-                    dw::adam_elem(pp[k][q], gg[k][q], mm[k][q], vv[k][q], h);
-            }
-#pragma unroll
-            for (int q = 0; q < VPL; ++q) {
-                const int e = lane + 64 * q;
-                if (e >= d) continue;
-                const int64_t o = r[k] * d + e;
-                p[o] = pp[k][q];
-                m[o] = mm[k][q];
-                v[o] = vv[k][q];
-            }
-            if (lane == 0) last[r[k]] = STEP ? step : upto;
+        if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
+        if (live) {
+            p[o] = pp;
+            m[o] = mm;
+            v[o] = vv;
         }
+        if (e == 0) last[r] = STEP ? step : upto;
     }
 }
 
@@ -264,27 +231,17 @@ int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_
     DW_REQUIRE(rows || !n_rows_dev, "dw_adam_rows: a device row count needs a row list");
     DW_REQUIRE(!grad_rows || step >= 1, "dw_adam_rows: a gradient step needs step >= 1");
     DW_REQUIRE(dim <= 512, "dw_adam_rows: dim > 512 is not supported");
-    int64_t blocks = (n_rows_max + 7) / 8;  // one wave per row, two rows per trip, 4 waves
-    if (blocks > 8192) blocks = 8192;
-    const int vpl = dim <= 64 ? 1 : dim <= 128 ? 2 : dim <= 256 ? 4 : 8;
-#define DW_ROWS_ADAM(ST, V)                                                                    \
-    hipLaunchKernelGGL((k_rows_adam<ST, V>), dim3((unsigned)blocks), dim3(256), 0,             \
-                       dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,           \
-                       n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step)
-#define DW_ROWS_ADAM_V(ST)                                                                     \
-    switch (vpl) {                                                                             \
-        case 1: DW_ROWS_ADAM(ST, 1); break;                                                   \
-        case 2: DW_ROWS_ADAM(ST, 2); break;                                                   \
-        case 4: DW_ROWS_ADAM(ST, 4); break;                                                   \
-        default: DW_ROWS_ADAM(ST, 8); break;                                                  \
-    }
-    if (grad_rows) {
-        DW_ROWS_ADAM_V(true)
-    } else {
-        DW_ROWS_ADAM_V(false)
-    }
-#undef DW_ROWS_ADAM_V
-#undef DW_ROWS_ADAM
+    int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
+    if (blocks > 65536) blocks = 65536;
+    const int threads = 64 * ((dim + 63) / 64);
+    if (grad_rows)
+        hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0,
+                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
+    else
+        hipLaunchKernelGGL((k_rows_adam<false>), dim3((unsigned)blocks), dim3(threads), 0,
+                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
 }
