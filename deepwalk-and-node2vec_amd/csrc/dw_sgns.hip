@@ -1824,18 +1824,22 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
+    // one centre per wave; the block's claimed rows are appended with ONE counter atomic (a
+    // same-address atomic per wave serialised: 4,480 of them were ~40 us at the 64-walk batch)
+    __shared__ uint32_t s_cnt[WAVES_PER_BLOCK];
+    __shared__ unsigned long long s_base;
     const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int T = a.C * (1 + a.K);
     const int64_t per = a.L - 2 * a.R;
-    for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; b < a.batch;
-         b += n_waves) {
-        const int64_t w = b / per, i = a.R + b % per;
-        const int32_t *walk = a.walks + w * a.L;
+    for (int64_t b0 = (int64_t)blockIdx.x * WAVES_PER_BLOCK; b0 < a.batch; b0 += n_waves) {
+        const int64_t b = b0 + wv;   // block-uniform trip count (barriers below)
         bool mine = false;
         uint32_t lo = 0;
-        if (lane < T) {
-            const int64_t o = row_id<true>(a, b, walk, i, lane);
+        if (b < a.batch && lane < T) {
+            const int64_t w = b / per, i = a.R + b % per;
+            const int64_t o = row_id<true>(a, b, a.walks + w * a.L, i, lane);
             if (o < 0 || o >= a.V) {
                 dw::status_or(a.status, DW_S_BAD_INDEX);
             } else if (o % a.n_owners == a.owner) {
@@ -1844,12 +1848,18 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             }
         }
         const unsigned long long mask = __ballot(mine);
-        if (mask == 0ull) continue;
-        unsigned long long base = 0;
-        if (lane == __ffsll(static_cast<long long>(mask)) - 1)
-            base = atomicAdd(n_list, static_cast<unsigned long long>(__popcll(mask)));
-        base = __shfl(base, __ffsll(static_cast<long long>(mask)) - 1, WAVE);
+        if (lane == 0) s_cnt[wv] = static_cast<uint32_t>(__popcll(mask));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int k = 0; k < WAVES_PER_BLOCK; ++k) tot += s_cnt[k];
+            s_base = tot ? atomicAdd(n_list, static_cast<unsigned long long>(tot)) : 0ull;
+        }
+        __syncthreads();
+        unsigned long long base = s_base;
+        for (int k = 0; k < wv; ++k) base += s_cnt[k];
         if (mine) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = lo;
+        __syncthreads();   // s_cnt / s_base are rewritten next trip
     }
 }
 
