@@ -93,6 +93,17 @@ int main(int argc, char **argv) {
     void *tmp;
     CK(hipMalloc(&tmp, cap));
     const uint32_t V21 = (1u << 20) + 1, V20 = 1u << 20;
+    if (argc > 2) {   // tile sweep of the product's 11-bit digits (21 bits)
+        run<OS<11, 1024, 16>>("11-bit 1024x16 (product)", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 1024, 12>>("11-bit 1024x12", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 1024, 20>>("11-bit 1024x20", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 1024, 24>>("11-bit 1024x24", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 512, 32>>("11-bit 512x32", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 768, 16>>("11-bit 768x16", k0, k1, v0, v1, n, V21, 21, tmp, cap);
+        run<OS<11, 1024, 16>>("11-bit 1024x16 (product, again)", k0, k1, v0, v1, n, V21, 21,
+                              tmp, cap);
+        return 0;
+    }
     run<OS<11, 1024, 16>>("11-bit 1024x16 (product)", k0, k1, v0, v1, n, V21, 21, tmp, cap);
     run<OS<11, 1024, 16>>("11-bit 1024x16", k0, k1, v0, v1, n, V20, 20, tmp, cap);
     run<OS<10, 1024, 16>>("10-bit 1024x16", k0, k1, v0, v1, n, V20, 20, tmp, cap);

@@ -260,10 +260,11 @@ def test_owner_tables_two_ranks_equal_single_process(hip_device):
 
 
 # ---- the touched-row in-table exchange: lazy exact Adam (dw_adam_rows, OwnerLazyTables) -------
-@pytest.mark.parametrize('d', [64, 96])
-def test_rows_adam_replay_is_bit_exact(hip_device, d):
+@pytest.mark.parametrize('d,wd', [(64, 0.0), (96, 0.0), (128, 0.01)])
+def test_rows_adam_replay_is_bit_exact(hip_device, d, wd):
     """dw_adam_rows replaying a row's missed steps (g = 0, per-step lr) gives exactly what one
-    dense dw_adam_dense per step would have given; the gradient step on top matches too."""
+    dense dw_adam_dense per step would have given; the gradient step on top matches too.
+    wd = 0 replays through adam_elem_g0 (the zero-gradient form), wd > 0 through adam_elem."""
     from shallow_encoders.word2vec.sharding import adam_scalars, hip_adam, hip_rows_adam
     g = torch.Generator().manual_seed(d)
     V, S = 300, 7
@@ -271,7 +272,7 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d):
     lrs = [0.1, 0.1, 0.05, 0.05, 0.02, 0.01, 0.01, 0.01]       # step s uses lrs[s - 1]
     hist = torch.zeros((S + 2, 8))
     for s in range(1, S + 2):
-        hist[s, :7] = torch.tensor(adam_scalars(s, lrs[s - 1], betas, eps, 0.0))
+        hist[s, :7] = torch.tensor(adam_scalars(s, lrs[s - 1], betas, eps, wd))
     hist = hist.cuda()
     p0 = torch.randn((V, d), generator=g)
     m0 = torch.randn((V, d), generator=g) * 1e-2
@@ -283,7 +284,7 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d):
         rows = torch.nonzero(last0 < s).flatten().cuda()
         pp, mm, vv = (t[rows].contiguous() for t in ref)
         hip_adam(pp.view(-1), torch.zeros_like(pp).view(-1), mm.view(-1), vv.view(-1), s,
-                 lrs[s - 1], betas, eps, 0.0, False)
+                 lrs[s - 1], betas, eps, wd, False)
         for t, u in zip(ref, (pp, mm, vv)):
             t[rows] = u
     p, m, v = (t.cuda().clone() for t in (p0, m0, v0))
@@ -301,7 +302,7 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d):
     ri = rows.long()
     pp, mm, vv = (t[ri].contiguous() for t in ref)
     hip_adam(pp.view(-1), gr.clone().view(-1), mm.view(-1), vv.view(-1), S + 1, lrs[S], betas,
-             eps, 0.0, False)
+             eps, wd, False)
     torch.cuda.synchronize()
     assert torch.equal(p[ri], pp) and torch.equal(m[ri], mm) and torch.equal(v[ri], vv)
     assert (last[ri] == S + 1).all() and int((last == S + 1).sum()) == 5
