@@ -321,11 +321,18 @@ def main():
         return OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=0, emulate_world=emulate or None,
                                lazy_out=lazy_out)
 
+    # small batches on one GPU are replayed as a HIP graph (below); with the atomic scatter there
+    # is no output-table phase for the in-table Adam to hide behind, so both tables' Adam is one
+    # in-place launch after pass 1 (fewer graph nodes: no side stream, no double buffer)
+    graph_small = (world == 1 and not owner and args.graph != 'off'
+                   and args.method in ('deepwalk', 'node2vec') and not args.walk_prefetch
+                   and (args.graph == 'on' or B * (L - 2 * R) <= 100_000))
     if owner:
         tables = owner_tables(lazy)
     else:
         tables = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
-                               overlap_in=not args.no_overlap_in,
+                               overlap_in=not args.no_overlap_in and not (
+                                   graph_small and args.scatter == 'atomic'),
                                out_pieces=None if args.no_out_pieces else args.out_pieces)
     if args.scaling == 'strong':
         # SURVEY §8e parity mode: the global batch is --batch-walks, each rank trains 1/W of it
@@ -551,10 +558,7 @@ def main():
     _native.check_status(status, 'bench warmup')
     # small batches on one GPU: the step replayed as a HIP graph (word2vec/graphed.py)
     graphed = None
-    use_graph = (world == 1 and not owner and (fuse or args.scatter == 'atomic')
-                 and tables.overlap_in
-                 and args.method in ('deepwalk', 'node2vec') and not args.walk_prefetch
-                 and (args.graph == 'on' or (args.graph == 'auto' and centres <= 100_000)))
+    use_graph = graph_small and (fuse or args.scatter == 'atomic')
     if use_graph:
         from shallow_encoders.word2vec.graphed import GraphedStep
         graphed = GraphedStep(tables, walker, epoch_starts,
@@ -612,6 +616,7 @@ def main():
     op_ms = sgns_ms + (kern_ms['adam'] if overlap_in else 0.0)
     if graphed is not None:     # one replay: walk + SGNS + both tables' Adam
         op_ms = kern_ms['sgns']
+        out_adam_bytes = in_adam_bytes = V * d * 4 * 7
     if owner:
         # this rank's share of the job's algorithmic bytes: 1/W of the pairs' SGNS bytes and of
         # both tables' dense Adam (out slice fused in pass 2, own in-table rows on the side

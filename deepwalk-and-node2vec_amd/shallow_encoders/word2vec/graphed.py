@@ -37,9 +37,10 @@ def adam_history(n_steps: int, lr: float, betas, eps: float, weight_decay: float
 
 
 class GraphedStep:
-    """``replicated_step`` on one GPU (ShardedTables with the overlapped in-table Adam; the out
-    table's Adam fused into the records gather, or after the atomic scatter with
-    ``scatter='atomic'``), captured with the walker in front of it.
+    """``replicated_step`` on one GPU (ShardedTables; the out table's Adam fused into the records
+    gather, or after the atomic scatter with ``scatter='atomic'``; the in table's Adam
+    overlapped on the side stream, or with ``overlap_in=False`` both tables' Adam in one launch),
+    captured with the walker in front of it.
 
     ``walker``: a Philox walker (rng='philox'); ``epoch_starts``: device int32 — walk w of the
     epoch starts at epoch_starts[w mod len]; the step trains walks ``first_walk_id + k*B ..``.
@@ -49,8 +50,8 @@ class GraphedStep:
                  context_radius: int, neg_samples: int, *, seed: int, grad_scale: float,
                  loss_acc: torch.Tensor, status: torch.Tensor, first_walk_id: int,
                  n_steps: int, noise_offset: Optional[int] = None, scatter: str = 'sorted'):
-        if tables.world != 1 or not tables.overlap_in or not tables.can_fuse_out_adam():
-            raise ValueError('GraphedStep: one GPU, HIP Adam with the overlapped in-table update')
+        if tables.world != 1 or not tables.can_fuse_out_adam():
+            raise ValueError('GraphedStep: one GPU, HIP Adam')
         if epoch_starts.dtype != torch.int32 or epoch_starts.device != tables.device:
             raise ValueError('GraphedStep: epoch_starts must be int32 on the tables\' device')
         self.t, self.walker = tables, walker
@@ -83,7 +84,10 @@ class GraphedStep:
                          self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
                          _native.stream(dev))
         torch.cuda.synchronize(dev)
-        for _ in range(2):                  # one graph per parity of the in-table buffers
+        # one graph per parity of the in-table double buffer (overlap_in); without it (both
+        # tables' Adam in one in-place launch after pass 1: the tiny-batch form) one graph
+        n_graphs = 2 if tables.overlap_in else 1
+        for _ in range(n_graphs):
             parity = tables._cur_in
             g = torch.cuda.CUDAGraph()
             _native.call('dw_step_scalars_bind', _native.ptr(self.block))
@@ -93,7 +97,7 @@ class GraphedStep:
             finally:
                 _native.call('dw_step_scalars_bind', None)
             self.graphs[parity] = g
-        tables.step_count -= 2              # the captures ran no step (host bookkeeping only)
+        tables.step_count -= n_graphs       # the captures ran no step (host bookkeeping only)
         torch.cuda.synchronize(dev)
 
     def _body(self) -> None:
@@ -115,8 +119,9 @@ class GraphedStep:
         t = self.t
         self.graphs[t._cur_in].replay()
         t.step_count += 1
-        t._next_in = 2 - t._cur_in
-        t._cur_in = t._next_in
+        if t.overlap_in:
+            t._next_in = 2 - t._cur_in
+            t._cur_in = t._next_in
 
     def scalars(self) -> dict:
         """The device block (synchronises): walk_id0, noise_offset, step."""

@@ -26,8 +26,11 @@ def _setup(dev):
     return csr, walker, starts
 
 
-@pytest.mark.parametrize('scatter', ['sorted', 'atomic'])
-def test_graphed_step_equals_eager(hip_device, scatter):
+@pytest.mark.parametrize('scatter,overlap_in', [('sorted', True), ('atomic', True),
+                                                ('atomic', False)])
+def test_graphed_step_equals_eager(hip_device, scatter, overlap_in):
+    """overlap_in=False: both tables' Adam in one in-place launch after pass 1 (bench.py's tiny
+    atomic-scatter graphs), one captured graph instead of one per in-table buffer."""
     from shallow_encoders.word2vec.graphed import GraphedStep
     from shallow_encoders.word2vec.sharding import ShardedTables, replicated_step
     dev = hip_device
@@ -37,7 +40,7 @@ def test_graphed_step_equals_eager(hip_device, scatter):
     warm, steps = 2, 7
     runs = []
     for mode in ('eager', 'graph'):
-        t = ShardedTables(V, D, dev, lr=LR, init_seed=0)
+        t = ShardedTables(V, D, dev, lr=LR, init_seed=0, overlap_in=overlap_in)
         acc = torch.zeros(4, dtype=torch.float64, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
 
