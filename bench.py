@@ -561,10 +561,13 @@ def main():
     use_graph = graph_small and (fuse or args.scatter == 'atomic')
     if use_graph:
         from shallow_encoders.word2vec.graphed import GraphedStep
+        # several steps per graph: between replays the launch gap (~19 us) is as long as a
+        # tiny step; the unroll divides --steps so exactly --steps steps are timed
+        unroll = next(u for u in (8, 4, 2, 1) if args.steps % u == 0)
         graphed = GraphedStep(tables, walker, epoch_starts,
                               B, R, K, seed=99, grad_scale=grad_scale, loss_acc=loss_acc,
                               status=status, first_walk_id=step_idx[0] * B,
-                              n_steps=args.steps + 1, scatter=args.scatter)
+                              n_steps=args.steps + 1, scatter=args.scatter, unroll=unroll)
     loss_acc.zero_()
     if world > 1:
         dist.barrier()
@@ -575,7 +578,7 @@ def main():
         for _ in range(args.steps):
             one_step(True)
     else:
-        for _ in range(args.steps):
+        for _ in range(args.steps // graphed.unroll):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             e[0].record()
             graphed.replay()
@@ -595,6 +598,8 @@ def main():
         elapsed = float(t)
     _native.check_status(status, 'bench')
     kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    if graphed is not None:   # one replay = `unroll` steps
+        kern_ms = {k: v / graphed.unroll for k, v in kern_ms.items()}
     if owner and world > 1:             # each rank summed the loss terms of its own slots
         dist.all_reduce(loss_acc)
     terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
@@ -791,10 +796,12 @@ def main():
             'in_table_adam_blocks': (overlap_adam_blocks(V * d * 4 * 7, p2_bytes)
                                      if overlap_in else None),
             'ms_per_launch': op_ms,
-            'launches_timed': phases['calls'] if graphed is None else args.steps,
+            'launches_timed': (phases['calls'] if graphed is None
+                               else args.steps // graphed.unroll),
             'graph': (None if graphed is None else
-                      'HIP graph replay of walk + SGNS + both Adams (word2vec/graphed.py); '
-                      'the window is the whole replay, phases are not split'),
+                      f'HIP graph replay of walk + SGNS + both Adams (word2vec/graphed.py), '
+                      f'{graphed.unroll} steps per graph; ms_per_launch is per step, the '
+                      f'window is the whole replay, phases are not split'),
             'phases': phase_info,
         },
         'cpu_baseline': None,

@@ -49,11 +49,15 @@ class GraphedStep:
     def __init__(self, tables: ShardedTables, walker, epoch_starts: torch.Tensor, B: int,
                  context_radius: int, neg_samples: int, *, seed: int, grad_scale: float,
                  loss_acc: torch.Tensor, status: torch.Tensor, first_walk_id: int,
-                 n_steps: int, noise_offset: Optional[int] = None, scatter: str = 'sorted'):
+                 n_steps: int, noise_offset: Optional[int] = None, scatter: str = 'sorted',
+                 unroll: int = 1):
         if tables.world != 1 or not tables.can_fuse_out_adam():
             raise ValueError('GraphedStep: one GPU, HIP Adam')
         if epoch_starts.dtype != torch.int32 or epoch_starts.device != tables.device:
             raise ValueError('GraphedStep: epoch_starts must be int32 on the tables\' device')
+        if unroll < 1:
+            raise ValueError('GraphedStep: unroll must be >= 1')
+        self.unroll = int(unroll)
         self.t, self.walker = tables, walker
         dev = tables.device
         L = walker.length
@@ -84,20 +88,25 @@ class GraphedStep:
                          self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
                          _native.stream(dev))
         torch.cuda.synchronize(dev)
-        # one graph per parity of the in-table double buffer (overlap_in); without it (both
-        # tables' Adam in one in-place launch after pass 1: the tiny-batch form) one graph
-        n_graphs = 2 if tables.overlap_in else 1
+        # `unroll` consecutive steps per graph (one launch per `unroll` steps: at tiny batches
+        # the gap between replays is as long as the step). One graph per parity of the in-table
+        # double buffer (overlap_in) when a graph flips it (odd unroll); without the double
+        # buffer (both tables' Adam in one in-place launch: the tiny-batch form) one graph.
+        self._flips = tables.overlap_in and self.unroll % 2 == 1
+        n_graphs = 2 if self._flips else 1
         for _ in range(n_graphs):
             parity = tables._cur_in
             g = torch.cuda.CUDAGraph()
             _native.call('dw_step_scalars_bind', _native.ptr(self.block))
             try:
                 with torch.cuda.graph(g, capture_error_mode='relaxed'):
-                    self._body()
+                    for _ in range(self.unroll):
+                        self._body()
             finally:
                 _native.call('dw_step_scalars_bind', None)
             self.graphs[parity] = g
-        tables.step_count -= n_graphs       # the captures ran no step (host bookkeeping only)
+        # the captures ran no step (host bookkeeping only; an even unroll ends on its parity)
+        tables.step_count -= n_graphs * self.unroll
         torch.cuda.synchronize(dev)
 
     def _body(self) -> None:
@@ -114,12 +123,13 @@ class GraphedStep:
                          _native.stream(dev))
 
     def replay(self) -> None:
-        """One training step (enqueued on the current stream); the tables' host bookkeeping
-        (Adam step count, current in-table buffer) follows as the eager step's would."""
+        """``unroll`` training steps (enqueued on the current stream); the tables' host
+        bookkeeping (Adam step count, current in-table buffer) follows as the eager steps'
+        would."""
         t = self.t
         self.graphs[t._cur_in].replay()
-        t.step_count += 1
-        if t.overlap_in:
+        t.step_count += self.unroll
+        if self._flips:
             t._next_in = 2 - t._cur_in
             t._cur_in = t._next_in
 

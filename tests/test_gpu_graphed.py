@@ -26,18 +26,20 @@ def _setup(dev):
     return csr, walker, starts
 
 
-@pytest.mark.parametrize('scatter,overlap_in', [('sorted', True), ('atomic', True),
-                                                ('atomic', False)])
-def test_graphed_step_equals_eager(hip_device, scatter, overlap_in):
+@pytest.mark.parametrize('scatter,overlap_in,unroll', [('sorted', True, 1), ('atomic', True, 1),
+                                                       ('atomic', False, 1), ('sorted', True, 3),
+                                                       ('atomic', False, 4)])
+def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
     """overlap_in=False: both tables' Adam in one in-place launch after pass 1 (bench.py's tiny
-    atomic-scatter graphs), one captured graph instead of one per in-table buffer."""
+    atomic-scatter graphs), one captured graph instead of one per in-table buffer. unroll > 1:
+    several steps per graph (an odd unroll flips the in-table buffer, so two graphs)."""
     from shallow_encoders.word2vec.graphed import GraphedStep
     from shallow_encoders.word2vec.sharding import ShardedTables, replicated_step
     dev = hip_device
     csr, walker, epoch = _setup(dev)
     V = csr.vocab_size
     grad_scale = 1.0 / (B * (L - 2 * R) * 2 * R)
-    warm, steps = 2, 7
+    warm, steps = 2, 12
     runs = []
     for mode in ('eager', 'graph'):
         t = ShardedTables(V, D, dev, lr=LR, init_seed=0, overlap_in=overlap_in)
@@ -60,8 +62,8 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in):
         else:
             gs = GraphedStep(t, walker, epoch, B, R, K, seed=SEED, grad_scale=grad_scale,
                              loss_acc=acc, status=status, first_walk_id=warm * B,
-                             n_steps=steps, scatter=scatter)
-            for _ in range(steps):
+                             n_steps=steps, scatter=scatter, unroll=unroll)
+            for _ in range(steps // unroll):
                 gs.replay()
             last = gs.walks
             sc = gs.scalars()
