@@ -1,7 +1,8 @@
 #!/bin/bash
 # Bench lines at other batch shapes (one GPU): the reference's 64-walk batch and 1,024 walks on
 # C3, the W=8 global batch (65,536 walks) on one GPU, the C2 shape (default: the atomic
-# scatter at this size) and with the records (sorted) scatter. Each run has its own time limit; a failure stops the script.
+# scatter at this size) and with the records (sorted) scatter. Each run has its own time
+# limit; a failure stops the script.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
