@@ -145,6 +145,7 @@ struct SgnsArgs {
     int32_t owner, n_owners;
     int32_t own_shift;        //   log2(n_owners) when a power of two (mask / shift), else -1
     uint32_t *rec_counts;
+    uint32_t *count_out;      //   n_owners == 1: the records are dense; their count goes here
     int64_t region;
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
@@ -475,7 +476,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 // owner o % W, local row o / W (shift and mask for the usual W = 2, 4, 8)
                 const int32_t lrow = a.own_shift >= 0 ? (id >> a.own_shift) : id / a.n_owners;
                 const int32_t orow = id - lrow * a.n_owners;
-                const bool own = id >= 0 && orow == a.owner;
+                // one owner keeps every slot of an active centre, a bad id as a zero record:
+                // the per-wave regions then tile [0, batch * T) densely (no compaction)
+                const bool own = (id >= 0 && orow == a.owner) ||
+                                 (a.n_owners == 1 && active && t < T);
                 const uint32_t grp =
                     static_cast<uint32_t>(__ballot(own) >> (16 * q)) & 0xFFFFu;
                 if (own) {
@@ -601,8 +605,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int k = 0; k < G16_TMAX / 16; ++k) {
                 const int tt = gl + 16 * k;
                 if (tt < n_own) {
-                    a.rec_key[at + tt] = static_cast<uint32_t>(s_id[wv][q][tt]);
-                    a.rec_val[at + tt] = pack_record(s_coef[wv][q][tt], cid);
+                    const int32_t id = s_id[wv][q][tt];   // < 0: a bad id (one owner only)
+                    a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                    a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
+                                                     ok_c ? cid : 0);
                 }
             }
             filled += c0 + c1 + c2 + c3;
@@ -661,6 +667,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int f = 0; f < F4; ++f) atomicAdd(dst + 64 * f, pend[f]);
         }
         if (lane == 0) a.rec_counts[gw] = static_cast<uint32_t>(filled);
+        if (a.count_out && blockIdx.x == 0 && threadIdx.x == 0)
+            *a.count_out = static_cast<uint32_t>(a.batch * T);
     }
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
@@ -1588,8 +1596,12 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
                              "dw_sgns_owner_pass1", a.V, &occ);
     if (rc != DW_OK) return rc;
     g_timer.mark(0, st);
-    a.rec_key = ws.k0;
-    a.rec_val = ws.v0;
+    // n_owners > 1: per-wave regions in (k0, v0), compacted into (k1, v1); one owner keeps
+    // every slot, so the regions tile (k1, v1) densely and pass 1 writes there directly
+    const bool dense = a.n_owners == 1;
+    a.rec_key = dense ? ws.k1 : ws.k0;
+    a.rec_val = dense ? ws.v1 : ws.v0;
+    a.count_out = dense ? ws.count : nullptr;
     a.rec_counts = ws.wave_counts;
     a.region = lay.region;
     a.occ_per_wave = lay.region / T;
@@ -1601,13 +1613,16 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
         a.occ = occ.v0;
         rc = launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
-        hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts, lay.n_waves,
-                           ws.wave_offsets, ws.count);
-        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/scan");
-        int64_t cb = lay.n_waves < 65536 ? lay.n_waves : 65536;
-        hipLaunchKernelGGL(k_rec_compact, dim3((unsigned)cb), dim3(256), 0, st, ws.wave_counts,
-                           ws.wave_offsets, lay.n_waves, lay.region, ws.k0, ws.v0, ws.k1, ws.v1);
-        DW_LAUNCH_CHECK("dw_sgns_owner_pass1/compact");
+        if (!dense) {
+            hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts,
+                               lay.n_waves, ws.wave_offsets, ws.count);
+            DW_LAUNCH_CHECK("dw_sgns_owner_pass1/scan");
+            int64_t cb = lay.n_waves < 65536 ? lay.n_waves : 65536;
+            hipLaunchKernelGGL(k_rec_compact, dim3((unsigned)cb), dim3(256), 0, st,
+                               ws.wave_counts, ws.wave_offsets, lay.n_waves, lay.region, ws.k0,
+                               ws.v0, ws.k1, ws.v1);
+            DW_LAUNCH_CHECK("dw_sgns_owner_pass1/compact");
+        }
     } else if (hipMemsetAsync(ws.count, 0, sizeof(uint32_t), st) != hipSuccess) {
         dw::set_error("dw_sgns_owner_pass1: counter reset failed");
         return DW_E_HIP;
