@@ -27,6 +27,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
 
@@ -1468,6 +1470,66 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// Small batches (<= OCC_SMALL_MAX centres, e.g. the reference's 64-walk batch: 4,480): the
+// occurrence keys, their stable sort by node and the distinct nodes in ONE block — where the
+// device-wide sort + unique took ~11 launches (merge sort, copies, lookback scans).
+constexpr int OCC_SMALL_THREADS = 1024, OCC_SMALL_IPT = 8;
+constexpr int64_t OCC_SMALL_MAX = (int64_t)OCC_SMALL_THREADS * OCC_SMALL_IPT;
+
+__global__ void __launch_bounds__(OCC_SMALL_THREADS)
+    k_occ_small(const int32_t *__restrict__ walks, int64_t n_centres, int32_t L, int32_t R,
+                int32_t end_bit, uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
+                uint32_t *__restrict__ touched, int64_t *__restrict__ n_touched) {
+    using Sort = rocprim::block_radix_sort<uint32_t, OCC_SMALL_THREADS, OCC_SMALL_IPT, uint32_t>;
+    using Scan = rocprim::block_scan<uint32_t, OCC_SMALL_THREADS>;
+    __shared__ typename Sort::storage_type s_sort;
+    __shared__ typename Scan::storage_type s_scan;
+    __shared__ uint32_t s_last[OCC_SMALL_THREADS];
+    const int t = threadIdx.x;
+    const int64_t per = L - 2 * R;
+    uint32_t k[OCC_SMALL_IPT], v[OCC_SMALL_IPT];
+#pragma unroll
+    for (int i = 0; i < OCC_SMALL_IPT; ++i) {   // blocked: thread t holds items t*IPT + i
+        const int64_t b = (int64_t)t * OCC_SMALL_IPT + i;
+        if (b < n_centres) {
+            const int64_t w = b / per;
+            k[i] = static_cast<uint32_t>(walks[w * L + R + (b - w * per)]);
+            v[i] = static_cast<uint32_t>(b);
+        } else {   // padding sorts last (stable: it follows every real item)
+            k[i] = 0xFFFFFFFFu;
+            v[i] = 0xFFFFFFFFu;
+        }
+    }
+    Sort().sort(k, v, s_sort, 0, end_bit);   // stable: walk order within a node
+#pragma unroll
+    for (int i = 0; i < OCC_SMALL_IPT; ++i) {
+        const int64_t b = (int64_t)t * OCC_SMALL_IPT + i;
+        if (b < n_centres) {
+            keys_out[b] = k[i];
+            vals_out[b] = v[i];
+        }
+    }
+    if (!touched) return;   // (block-uniform)
+    s_last[t] = k[OCC_SMALL_IPT - 1];
+    __syncthreads();
+    uint32_t prev = t > 0 ? s_last[t - 1] : 0u;
+    bool f[OCC_SMALL_IPT];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < OCC_SMALL_IPT; ++i) {
+        const int64_t b = (int64_t)t * OCC_SMALL_IPT + i;
+        f[i] = b < n_centres && (b == 0 || k[i] != prev);
+        prev = k[i];
+        cnt += f[i] ? 1u : 0u;
+    }
+    uint32_t off = 0, total = 0;
+    Scan().exclusive_scan(cnt, off, 0u, total, s_scan);
+#pragma unroll
+    for (int i = 0; i < OCC_SMALL_IPT; ++i)
+        if (f[i]) touched[off++] = k[i];
+    if (t == 0) *n_touched = static_cast<int64_t>(total);
+}
+
 // the owner form's tail of the workspace (after the records part): the occurrence sort
 struct OccSpace {
     uint32_t *k0, *k1, *v0, *v1;
@@ -1527,6 +1589,13 @@ int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *work
 // also the distinct nodes, sorted, and their count (device int64).
 int owner_order(const SgnsArgs &a, const OccSpace &occ, uint32_t *touched, int64_t *n_touched,
                 hipStream_t st) {
+    if (a.batch <= OCC_SMALL_MAX) {
+        hipLaunchKernelGGL(k_occ_small, dim3(1), dim3(OCC_SMALL_THREADS), 0, st, a.walks,
+                           a.batch, a.L, a.R, end_bit_for(a.V), occ.k0, occ.v0, touched,
+                           n_touched);
+        DW_LAUNCH_CHECK("dw_sgns_owner/occ_small");
+        return DW_OK;
+    }
     int64_t ob = (a.batch + 255) / 256;
     if (ob > grid_cap(8)) ob = grid_cap(8);
     hipLaunchKernelGGL(k_occ_keys, dim3((unsigned)ob), dim3(256), 0, st, a.walks, a.batch, a.L,

@@ -459,3 +459,39 @@ def test_owner_pass2_without_count_readback(hip_device, W, mode):
     torch.testing.assert_close(g2, g1, rtol=1e-5, atol=1e-6 * scale)
     torch.testing.assert_close(m2, m1, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(w2, w1, rtol=1e-5, atol=1e-5 * 0.02)
+
+
+@pytest.mark.parametrize('n_walks', [3, 150, 400])
+def test_owner_prepare_touched_rows(hip_device, n_walks):
+    """dw_sgns_owner_prepare's distinct centre nodes (sorted) and their count: the one-block path
+    (<= 8,192 centres: k_occ_small) and the device-wide sort + unique above it; pass 1 with
+    order_ready=True then equals pass 1 ordering its centres itself."""
+    from shallow_encoders.word2vec.sgns import sgns_owner_prepare
+    g = torch.Generator().manual_seed(n_walks)
+    V, d, R, K, L = 700, 64, 3, 2, 30
+    walks = torch.randint(1, V, (n_walks, L), generator=g, dtype=torch.int32)
+    walks[:, ::7] = 5                                   # a repeated hub centre
+    walks = walks.cuda()
+    n_c = n_walks * (L - 2 * R)
+    touched = torch.full((n_c,), -1, dtype=torch.int32, device='cuda')
+    n_t = torch.zeros(1, dtype=torch.int64, device='cuda')
+    sgns_owner_prepare(walks, R, K, V, V, touched=touched, n_touched=n_t)
+    exp = torch.unique(walks[:, R:L - R].reshape(-1).long())
+    k = int(n_t.item())
+    assert k == exp.numel()
+    assert torch.equal(touched[:k].long(), exp)
+    w_in = torch.randn((V, d), generator=g).cuda() * 0.1
+    w_out = torch.randn((V, d), generator=g).cuda() * 0.1
+    res = []
+    for ready in (True, False):
+        if ready:
+            sgns_owner_prepare(walks, R, K, V, V, touched=touched, n_touched=n_t)
+        g_in = torch.zeros_like(w_in)
+        acc = sgns_owner_pass1(w_in, w_out, g_in, K, walks=walks, context_radius=R, owner=0,
+                               n_owners=1, vocab_size=V, seed=4, noise_offset=0,
+                               order_ready=ready)
+        res.append((g_in, acc))
+    torch.cuda.synchronize()
+    # (a hub's run of centres spans several waves: its row's atomics may add in either order)
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
