@@ -49,6 +49,7 @@ on the CPU (there the overlapped form runs its collectives synchronously). The d
 HIP kernel, which refuses host tensors.
 """
 import math
+import os
 from typing import Callable, Optional
 
 import torch
@@ -116,6 +117,9 @@ def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> in
     (0 = full grid, when no estimate is given)."""
     if not overlap_bytes:
         return 0
+    forced = int(os.environ.get('DW_OVERLAP_BLOCKS', '0') or 0)   # (tuning sweeps only)
+    if forced > 0:
+        return forced
     t = overlap_bytes / OVERLAP_PHASE_BPS
     need = OVERLAP_MARGIN * adam_bytes / t / ADAM_BLOCK_BPS
     return int(min(8192, max(32, math.ceil(need))))
