@@ -1148,14 +1148,14 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     // chunk size: GCH for large batches (balanced, few boundary rows); halved down to 32 while
     // the chunks would not give every SIMD of the chip a few waves — a 9K-record batch (C2 shape)
     // in 512-record chunks ran as 18 waves, 240 us of latency-bound gathers
-    int32_t gch = GCH;
+    static const int32_t gch0 = [] {   // DW_GCH: records per chunk, for tuning sweeps only
+        const char *e = getenv("DW_GCH");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 32 && v <= 8192) ? v : GCH;
+    }();
+    int32_t gch = gch0;
     {
-        static const int per_cu = [] {
-            const char *e = getenv("DW_GATHER_WAVES_PER_CU");
-            const int v = e ? atoi(e) : 0;
-            return v > 0 ? v : 16;
-        }();
-        const int64_t want = grid_cap(per_cu);   // 4 waves per SIMD
+        const int64_t want = grid_cap(16);   // 4 waves per SIMD
         while (gch > 32 && (n_rec + gch - 1) / gch < want) gch >>= 1;
     }
     const int64_t n_chunks = (n_rec + gch - 1) / gch;
