@@ -254,7 +254,13 @@ def main():
     backend = os.environ.get('DW_BENCH_BACKEND', 'nccl')
     if os.environ.get('DW_BENCH_ONE_DEVICE') == '1':
         local_rank = 0
-    if world > 1:
+    # DW_BENCH_DIST=1: take the multi-rank path (process group, collectives, owner layout) even
+    # at world 1, so the RCCL flow of the N > 1 lines runs on a one-GPU box (a check, not a
+    # measurement of scaling)
+    dist_on = world > 1 or os.environ.get('DW_BENCH_DIST') == '1'
+    if dist_on and world == 1:
+        os.environ['DW_FORCE_COLLECTIVES'] = '1'   # the tables take their N > 1 protocols
+    if dist_on:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         torch.cuda.set_device(local_rank)
         if backend == 'nccl':
@@ -285,27 +291,27 @@ def main():
         walker = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
     else:
         walker = DeepWalk(csr, L, rng='philox', seed=1234, device=dev)
-    emulate = args.emulate_world if (world == 1 and args.emulate_world >= 1) else 0
+    emulate = args.emulate_world if (not dist_on and args.emulate_world >= 1) else 0
     # one GPU, sparse batches: the owner path on one rank with the lazy exact in-table Adam
     # (auto: sparse batches over a large table — at C2 the table is 15 MB and the lazy path's
     # extra launches cost more than its Adam saves: 0.35 vs 0.20 ms per step)
-    n1_lazy = (world == 1 and not emulate and args.dist_mode == 'owner'
+    n1_lazy = (not dist_on and not emulate and args.dist_mode == 'owner'
                and (args.n1_in_adam == 'lazy' or
                     (args.n1_in_adam == 'auto' and B * (L - 2 * R) < 0.1 * V
                      and V * args.dim * 4 * 7 >= 1e9)))
     if n1_lazy:
         emulate, args.in_exchange = 1, 'lazy'
-    owner = emulate > 0 or (world > 1 and args.dist_mode == 'owner')
+    owner = emulate > 0 or (dist_on and args.dist_mode == 'owner')
     if args.scatter == 'auto':
         records = B * (L - 2 * R) * 2 * R * (1 + K)
-        args.scatter = 'atomic' if (world == 1 and not owner and records <= 65_536) else 'sorted'
+        args.scatter = 'atomic' if (not dist_on and not owner and records <= 65_536) else 'sorted'
     if owner and not (args.scatter == 'sorted' and d % 64 == 0 and d <= 512
                       and 2 * R * (1 + K) <= 64):
         raise SystemExit('owner mode needs the sorted path, d a multiple of 64 (<= 512) and '
                          '2R(1+K) <= 64; use --dist-mode replicated')
     W_eff = emulate or world            # ranks of the (possibly emulated) job
     # auto (N > 1 only; one rank has no exchange to choose): both protocols are timed below
-    auto_in = owner and args.in_exchange == 'auto' and world > 1
+    auto_in = owner and args.in_exchange == 'auto' and dist_on
     if owner and args.in_exchange == 'auto' and not auto_in:
         args.in_exchange = 'sharded'
     lazy = owner and args.in_exchange == 'lazy'
@@ -324,7 +330,7 @@ def main():
     # small batches on one GPU are replayed as a HIP graph (below); with the atomic scatter there
     # is no output-table phase for the in-table Adam to hide behind, so both tables' Adam is one
     # in-place launch after pass 1 (fewer graph nodes: no side stream, no double buffer)
-    graph_small = (world == 1 and not owner and args.graph != 'off'
+    graph_small = (not dist_on and not owner and args.graph != 'off'
                    and args.method in ('deepwalk', 'node2vec') and not args.walk_prefetch
                    and (args.graph == 'on' or B * (L - 2 * R) <= 100_000))
     if owner:
@@ -419,7 +425,7 @@ def main():
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
     fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
-    pieces = world > 1 and not args.no_out_pieces and not owner
+    pieces = dist_on and not args.no_out_pieces and not owner
     ev = {k: [] for k in ('walk', 'sgns', 'adam')}
     pb = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     p2_bytes = pb['sort'] + pb['pass2']        # the phase the in-table Adam overlaps
@@ -569,7 +575,7 @@ def main():
                               status=status, first_walk_id=step_idx[0] * B,
                               n_steps=args.steps + 1, scatter=args.scatter, unroll=unroll)
     loss_acc.zero_()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     phase_timing(graphed is None)
@@ -589,10 +595,10 @@ def main():
     torch.cuda.synchronize(dev)
     phases = phase_ms()
     phase_timing(False)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
@@ -600,7 +606,7 @@ def main():
     kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
     if graphed is not None:   # one replay = `unroll` steps
         kern_ms = {k: v / graphed.unroll for k, v in kern_ms.items()}
-    if owner and world > 1:             # each rank summed the loss terms of its own slots
+    if owner and dist_on:               # each rank summed the loss terms of its own slots
         dist.all_reduce(loss_acc)
     terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
     mean_loss = None if emulate > 1 else float(terms['loss'])   # one rank owns every slot at W=1
@@ -616,7 +622,7 @@ def main():
     out_adam_bytes = V * d * 4 * 7 if fuse else 0
     # one GPU, overlap_in: the in-table Adam (the other V*d*4 B x 7) runs on a side stream
     # inside the output-table phase; the window then ends when both streams are done
-    overlap_in = world == 1 and not owner and tables.overlap_in
+    overlap_in = not dist_on and not owner and tables.overlap_in
     in_adam_bytes = V * d * 4 * 7 if overlap_in else 0
     op_ms = sgns_ms + (kern_ms['adam'] if overlap_in else 0.0)
     if graphed is not None:     # one replay: walk + SGNS + both tables' Adam
@@ -666,7 +672,7 @@ def main():
             st = torch.arange(1, n_walks + 1, dtype=torch.int32, device=dev)
             out = torch.empty((n_walks, L), dtype=torch.int32, device=dev)
             w.walk_batch(st[:1024], walk_id0=0, out=out[:1024], check=False)
-            if world > 1:
+            if dist_on:
                 dist.barrier()
             torch.cuda.synchronize(dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -677,7 +683,7 @@ def main():
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - a
             kern_s = e0.elapsed_time(e1) * 1e-3
-            if world > 1:
+            if dist_on:
                 t = torch.tensor([dt], dtype=torch.float64, device=dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 dt = float(t)
@@ -710,24 +716,39 @@ def main():
                                     'frac': gbs / HBM_PEAK_GBS, 'p': p, 'q': q}, **extra)
             del out
         # the reference-exact walker (rng='python', dw_walk_replay): CPython's uniforms drawn on
-        # the host and copied in (8 B per step), fp64 choices arithmetic, a bounded sample
-        if rank == 0 and world == 1:
+        # the host (8 B per step), fp64 choices arithmetic. Unweighted graphs take the exact
+        # margin-checked picks (no serial sums; the serial replay only where the margin fails).
+        # walks_per_s: from the host uniforms (their H2D copy included); kernel_walks_per_s:
+        # uniforms already in HBM (HIP events around the launch)
+        if rank == 0 and not dist_on:
             import random as _random
             from shallow_encoders.graph.rng import draw_uniforms
             for meth, p, q in walk_methods:
-                n_r = 65_536 if meth == 'deepwalk' else 4_096
+                n_r = N if meth == 'deepwalk' else 65_536
                 w = (Node2Vec(csr, L, p=p, q=q, device=dev) if meth == 'node2vec'
                      else DeepWalk(csr, L, device=dev))
                 gen = _random.Random(0)
                 st = torch.arange(1, n_r + 1, dtype=torch.int32)
                 w.walk_batch(st[:64], uniforms=draw_uniforms(64 * (L - 1), gen))
                 u = draw_uniforms(n_r * (L - 1), gen)
+                out = torch.empty((n_r, L), dtype=torch.int32, device=dev)
                 torch.cuda.synchronize(dev)
                 a = time.perf_counter()
-                w.walk_batch(st, uniforms=u)
+                w.walk_batch(st, uniforms=u, out=out)
                 torch.cuda.synchronize(dev)
-                replay_stats[meth] = {'walks': n_r, 'p': p, 'q': q,
-                                      'walks_per_s': n_r / (time.perf_counter() - a)}
+                dt = time.perf_counter() - a
+                u_dev = torch.from_numpy(u).to(dev)
+                st_dev = st.to(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                w.walk_batch(st_dev, uniforms=u_dev, out=out, check=False)
+                e1.record()
+                torch.cuda.synchronize(dev)
+                kern_s = e0.elapsed_time(e1) * 1e-3
+                replay_stats[meth] = {'walks': n_r, 'p': p, 'q': q, 'walks_per_s': n_r / dt,
+                                      'kernel_walks_per_s': n_r / kern_s,
+                                      'kernel_ms': kern_s * 1e3}
+                del out, u_dev
 
     result = {
         'metric': 'positive-pairs/s + random-walks/s, 1M-node d=128 k=5, 1/2/4/8 MI355X',
@@ -758,7 +779,7 @@ def main():
                 f'value is a projection assuming the in-table exchange stays hidden; walks: '
                 f'{args.owner_walks})' if emulate
                 else f'REHEARSAL dp{world} over {backend}, all ranks on one device'
-                if backend != 'nccl' and world > 1 else
+                if backend != 'nccl' and dist_on else
                 f'dp{world} owner-computes (out table sharded by row owner o % {world}, no '
                 f'out-table collective; in table replicated: '
                 + ('touched rows all-reduced over RCCL, lazy exact Adam' if lazy else
@@ -828,12 +849,12 @@ def main():
                     result['roofline']['phases'][k]['traffic'] = per_k.get('sgns_' + k)
         except (OSError, ValueError):
             pass
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ('c2', 'c3'):
+    if rank == 0 and not dist_on and not args.no_cpu_baseline and args.config in ('c2', 'c3'):
         cb = cpu_baseline(csr, args, args.cpu_budget, walk_methods)
         result['cpu_baseline'] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -125,6 +125,14 @@ def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> in
     return int(min(8192, max(32, math.ceil(need))))
 
 
+def force_collectives() -> bool:
+    """DW_FORCE_COLLECTIVES=1 with a process group of one rank: take the N > 1 protocol
+    (reduce-scatter / all-gather / all-reduce, side-stream overlap) anyway, so the RCCL flow of
+    the multi-GPU step can be checked on a one-GPU box. Off by default: one rank then takes the
+    one-device shortcuts (fused Adam, no collectives)."""
+    return dist.is_initialized() and os.environ.get('DW_FORCE_COLLECTIVES') == '1'
+
+
 class ShardedTables:
     """In/out embedding tables + dense gradients + node-range-sharded Adam state."""
 
@@ -136,9 +144,10 @@ class ShardedTables:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.multi = self.world > 1 or force_collectives()   # collectives run
         self.V, self.d = int(vocab_size), int(dim)
         # out-table pieces: one per exchange pipelined behind the output-table phase (N > 1)
-        self.P = int(out_pieces) if out_pieces else (DEFAULT_OUT_PIECES if self.world > 1 else 1)
+        self.P = int(out_pieces) if out_pieces else (DEFAULT_OUT_PIECES if self.multi else 1)
         if not 1 <= self.P <= 1024:
             raise ValueError('out_pieces must be in [1, 1024]')
         unit = self.world * self.P
@@ -154,21 +163,21 @@ class ShardedTables:
         if overlap_in is None:
             overlap_in = True
         # one GPU: the in-table Adam overlaps only with the HIP kernel (out of place)
-        self.overlap_in = bool(overlap_in and self.world == 1 and self._cuda
+        self.overlap_in = bool(overlap_in and not self.multi and self._cuda
                                and self.adam_impl is hip_adam)
-        n_slots = 3 if (self.world > 1 or self.overlap_in) else 2
+        n_slots = 3 if (self.multi or self.overlap_in) else 2
         self.params = torch.zeros((n_slots, self.V_pad, self.d), dtype=torch.float32,
                                   device=self.device)
         self.grads = torch.zeros((2, self.V_pad, self.d), dtype=torch.float32, device=self.device)
         self.m = torch.zeros((2, self.S, self.d), dtype=torch.float32, device=self.device)
         self.v = torch.zeros_like(self.m)
-        self.grad_shard = torch.empty_like(self.m) if self.world > 1 else None
+        self.grad_shard = torch.empty_like(self.m) if self.multi else None
         self._cur_in = 0
         self._next_in = 0
         self._ag = []          # pending all-gathers / side-stream events (overlapped form)
         self._out_done = set()  # out-table pieces already exchanged this step
         self._side = (torch.cuda.Stream(self.device)
-                      if (self._cuda and (self.world > 1 or self.overlap_in)) else None)
+                      if (self._cuda and (self.multi or self.overlap_in)) else None)
         self._row_flags = None   # fused output-table Adam scratch (one device)
         if init_seed is not None:
             self.xavier_(init_seed)
@@ -278,7 +287,7 @@ class ShardedTables:
         """Exchange gradients, update this rank's rows, gather parameters; grads end zeroed."""
         self.sync()
         self.step_count += 1
-        if self.world == 1:
+        if not self.multi:
             self._adam_both()
             return
         self._exchange_in(self._cur_in, self._cur_in, False)
@@ -307,10 +316,10 @@ class ShardedTables:
         grid (overlap_adam_blocks); None = full grid."""
         self.step_count += 1
         self._out_done = set()
-        if self.world == 1 and not self.overlap_in:
+        if not self.multi and not self.overlap_in:
             return                              # exchange_out does the Adam
         self._next_in = 2 - self._cur_in
-        if self.world == 1:
+        if not self.multi:
             def adam_to(_async):
                 blocks = overlap_adam_blocks(self.V_pad * self.d * 4 * 7, overlap_bytes)
                 hip_adam_to(self.params[self._cur_in], self.params[self._next_in],
@@ -331,7 +340,7 @@ class ShardedTables:
         """Call right after the gather of out-table piece p is enqueued (its gradient rows
         final): its reduce-scatter / Adam / all-gather run on the side stream while the next
         pieces' gathers run. One GPU: nothing to exchange (exchange_out does the Adam)."""
-        if self.world == 1:
+        if not self.multi:
             return
         if p in self._out_done:
             raise RuntimeError(f'out-table piece {p} exchanged twice in one step')
@@ -340,7 +349,7 @@ class ShardedTables:
 
     def can_fuse_out_adam(self) -> bool:
         """The output table's Adam can run inside SGNS phase 2: one device, HIP Adam."""
-        return self.world == 1 and self._cuda and self.adam_impl is hip_adam
+        return not self.multi and self._cuda and self.adam_impl is hip_adam
 
     def out_adam_spec(self) -> Optional[dict]:
         """For SGNS phase 2 with the output table's Adam fused in (sgns_accumulate out_adam=):
@@ -360,7 +369,7 @@ class ShardedTables:
         """Call right after SGNS phase 2 is enqueued (g_out final): exchanges the out-table
         pieces exchange_out_piece has not. ``fused_out``: phase 2 already applied the output
         table's Adam (out_adam_spec, one GPU)."""
-        if self.world == 1:
+        if not self.multi:
             if self.overlap_in:
                 if not fused_out:       # the in table is done on the side stream (exchange_in)
                     self._adam(self.params[1].view(-1), self.grads[1].view(-1), 1, True)
@@ -472,6 +481,8 @@ class OwnerTables:
         self.emulated = bool(emulate_world) and self.world == 1
         if self.emulated:
             self.world, self.rank = int(emulate_world), 0
+        # collectives run (N > 1, or one rank with DW_FORCE_COLLECTIVES=1); never emulated
+        self.multi = (self.world > 1 or force_collectives()) and not self.emulated
         self.V, self.d = int(vocab_size), int(dim)
         self.V_pad = int(math.ceil(self.V / self.world)) * self.world
         self.S = self.V_pad // self.world
@@ -501,7 +512,7 @@ class OwnerTables:
         self.grads_in = torch.zeros((self.V_pad, self.d), **f32)
         self.m_in = torch.zeros((self.S, self.d), **f32)
         self.v_in = torch.zeros_like(self.m_in)
-        self.grad_shard = (torch.empty_like(self.m_in) if self.world > 1 and not self.emulated
+        self.grad_shard = (torch.empty_like(self.m_in) if self.multi
                            else None)
 
     # ---- views -------------------------------------------------------------------------------
@@ -547,7 +558,7 @@ class OwnerTables:
         """The whole (V, d) out table, gathered from every rank's slice (collective when N > 1)."""
         if self.emulated:
             raise RuntimeError('an emulated rank holds only its own slice')
-        if self.world == 1:
+        if not self.multi:
             return self.w_out[:self.V].clone()
         parts = torch.empty((self.world, self.S, self.d), dtype=torch.float32, device=self.device)
         if dist.get_backend(self.group) == 'nccl':
@@ -590,7 +601,7 @@ class OwnerTables:
         """reduce-scatter g_in -> Adam on own rows of the idle buffer -> all-gather into it;
         g_in ends zeroed. One rank: Adam over the whole in table into the idle buffer."""
         src, dst = self.params_in[self._cur_in], self.params_in[self._next_in]
-        if self.world == 1:
+        if self.world == 1 and not self.multi:
             dst.copy_(src)
             self._adam(dst.view(-1), self.grads_in.view(-1), self.m_in.view(-1),
                        self.v_in.view(-1), True)
@@ -843,7 +854,7 @@ class OwnerLazyTables(OwnerTables):
         sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
                            touched=self._touched, n_touched=self._n_touched)
         self._n_max = n
-        if self.world > 1 and not self.emulated:   # |U| sizes the all-reduce (exchange_touched)
+        if self.multi:   # |U| sizes the all-reduce (exchange_touched)
             self._n_host.copy_(self._n_touched, non_blocking=True)
             self._n_event = torch.cuda.Event()
             self._n_event.record(torch.cuda.current_stream(self.device))
@@ -894,7 +905,7 @@ class OwnerLazyTables(OwnerTables):
         """After pass 1: G = g_in[U] (those rows cleared); N > 1: all-reduce(SUM) of G, on a side
         stream behind the output-table phase."""
         n_max = self._n_max
-        multi = self.world > 1 and not self.emulated
+        multi = self.multi
         if self._hip():
             if self._G is None or self._G.shape[0] < max(n_max, 1):
                 self._G = torch.empty((max(n_max, 1), self.d), dtype=torch.float32,

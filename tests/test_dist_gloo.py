@@ -91,12 +91,15 @@ def train(t, rank, world, mode):
         assert float(t.grads.abs().max()) == 0.0
 
 
-def _worker(rank, world, port, mode, pieces, q):
+def _worker(rank, world, port, mode, pieces, q, force=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    if force:   # one rank that still runs the N > 1 protocol with its collectives
+        os.environ['DW_FORCE_COLLECTIVES'] = '1'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from shallow_encoders.word2vec.sharding import ShardedTables
     t = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam, out_pieces=pieces)
+    assert t.multi == (world > 1 or force)
     train(t, rank, world, mode)
     q.put((rank, t.w_in.numpy().copy(), t.w_out.numpy().copy(),
            (t.shard_range(), t.P, t.S, t.V_pad),
@@ -146,3 +149,24 @@ def test_sharded_adam_world2_equals_single_process(mode, pieces):
         keep = rows < V
         np.testing.assert_allclose(m[keep][np.argsort(rows[keep])], ref.m[k].numpy(),
                                    rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('mode,pieces', [('serial', None), ('pieces', 3)])
+def test_sharded_forced_collectives_one_rank_equals_single_process(mode, pieces):
+    """DW_FORCE_COLLECTIVES=1 at world 1 (how tests/test_gpu_rccl.py and bench.py's
+    DW_BENCH_DIST=1 run the RCCL flow on one GPU): the N > 1 protocol, reduce-scatter /
+    all-gather included, over a one-rank group equals the one-device step."""
+    from shallow_encoders.word2vec.sharding import ShardedTables
+    ref = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    train(ref, 0, 1, 'serial')
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), mode, pieces, q, True))
+    p.start()
+    _, i0, o0, (r0, P, S, V_pad), _ = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert P == (pieces or 8) and r0 == (0, V_pad) and S == V_pad
+    np.testing.assert_allclose(i0, ref.w_in.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(o0, ref.w_out.numpy(), rtol=1e-5, atol=1e-6)

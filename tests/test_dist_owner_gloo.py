@@ -41,12 +41,15 @@ def owner_train(t, rank, world):
         assert float(t.grads_in.abs().max()) == 0.0 and float(t.g_out.abs().max()) == 0.0
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, force=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    if force:   # one rank that still runs the N > 1 protocol with its collectives
+        os.environ['DW_FORCE_COLLECTIVES'] = '1'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from shallow_encoders.word2vec.sharding import OwnerTables
     t = OwnerTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    assert t.multi == (world > 1 or force)
     owner_train(t, rank, world)
     m_out, v_out = t.out_state_full()
     q.put((rank, t.w_in.numpy().copy(), t.full_w_out().numpy(), t.shard_range(),
@@ -79,8 +82,8 @@ def test_owner_split_sums_to_full_gradient():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('world', [2, 3])
-def test_owner_tables_equal_single_process(world):
+@pytest.mark.parametrize('world,force', [(2, False), (3, False), (1, True)])
+def test_owner_tables_equal_single_process(world, force):
     from shallow_encoders.word2vec.sharding import ShardedTables
     from test_dist_gloo import train
     ref = ShardedTables(V, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
@@ -88,7 +91,7 @@ def test_owner_tables_equal_single_process(world):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, force)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
@@ -149,12 +152,15 @@ def lazy_train(t, rank, world):
         assert int(t.last_in[torch.as_tensor(untouched)].min()) < t.step_count or t.step_count == 1
 
 
-def _lazy_worker(rank, world, port, q):
+def _lazy_worker(rank, world, port, q, force=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    if force:
+        os.environ['DW_FORCE_COLLECTIVES'] = '1'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from shallow_encoders.word2vec.sharding import OwnerLazyTables
     t = OwnerLazyTables(VL, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
+    assert t.multi == (world > 1 or force)
     lazy_train(t, rank, world)
     w_in = t.w_in.numpy().copy()             # flushes every deferred update
     assert int(t.last_in.min()) == t.step_count
@@ -164,8 +170,8 @@ def _lazy_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('world', [1, 2, 3])
-def test_owner_lazy_tables_equal_dense_single_process(world):
+@pytest.mark.parametrize('world,force', [(1, False), (2, False), (3, False), (1, True)])
+def test_owner_lazy_tables_equal_dense_single_process(world, force):
     from shallow_encoders.word2vec.sharding import ShardedTables
     ref = ShardedTables(VL, D, 'cpu', lr=0.05, init_seed=3, adam_impl=cpu_adam)
     for ins, tgt, noise in lazy_batches():
@@ -177,7 +183,8 @@ def test_owner_lazy_tables_equal_dense_single_process(world):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_lazy_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_lazy_worker, args=(r, world, port, q, force))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
