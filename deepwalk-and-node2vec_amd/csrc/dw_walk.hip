@@ -100,10 +100,166 @@ __device__ __forceinline__ int64_t bisect_right_lds(const double *cum, double x,
     return lo;
 }
 
+// ---- exact picks without the serial sum (unweighted graphs) ---------------------------------
+// On an unweighted graph a step's weights take at most three values (1, 1/p, 1/q), so the exact
+// real prefix W_i = a_i/p + b_i + c_i/q (a, b, c: integer counts of each class up to neighbour i)
+// and total T are known without CPython's left-to-right sums. CPython's cum[i] (accumulate of
+// fl(w / fl-sum(w))) and x = fl(U * cum[n-1]) differ from W_i / T and U by at most
+// (4n + 3) * 1.02 * 2^-53 (n roundings in the sum, n in the accumulate, one per division and
+// product; every partial sum is <= 1 + n 2^-53). The fp64 evaluation of D_i = W_i - U*T adds
+// under 10 * 2^-53 * T. So where |D_i| > M = (4.5 n + 20) 2^-53 T at the two neighbours that
+// bracket the crossing, sign(D_i) = sign(cum[i] - x) for every i (W is strictly increasing),
+// and bisect_right(cum, x, 0, n-1) = #{i <= n-2 : D_i <= 0} exactly. Where the margin fails
+// (probability ~1e-6 per step at a 45K-neighbour hub) the serial replay decides.
+__device__ __forceinline__ double exact_margin(int64_t n, double T) {
+    return (4.5 * static_cast<double>(n) + 20.0) * 0x1p-53 * T;
+}
+
+// All weights equal (DeepWalk unweighted, node2vec's first step): W_i = i + 1, T = n.
+// Returns the pick, or -1 where the margin leaves it to the serial replay.
+__device__ __forceinline__ int64_t uniform_pick_exact(double U, int64_t n) {
+    const double T = static_cast<double>(n);
+    const double f = U * T;
+    const double M = exact_margin(n, T);
+    double k = floor(f);  // #{i : i + 1 <= f}, i + 1 in [1, n-1]
+    if (k > T - 1.0) k = T - 1.0;
+    if (k >= 1.0 && fabs(k - f) <= M) return -1;                 // D_{k-1} = k - f
+    if (k + 1.0 <= T - 1.0 && fabs(k + 1.0 - f) <= M) return -1;  // D_k = k + 1 - f
+    return static_cast<int64_t>(k);
+}
+
+// The serial replay of one unweighted first-order step in one lane (the margin failed):
+// sum = n, nw = 1/n, cum = accumulate(nw), bisect_right(cum, U * cum[n-1], 0, n-1).
+__device__ int64_t uniform_pick_serial(double U, int64_t n) {
+    const double nw = 1.0 / static_cast<double>(n);
+    double total = nw;
+    for (int64_t i = 1; i < n; ++i) total = total + nw;
+    total = total + 0.0;
+    const double x = U * total;
+    double cum = nw;
+    for (int64_t i = 0; i < n - 1; ++i) {
+        if (i > 0) cum = cum + nw;
+        if (x < cum) return i;
+    }
+    return n - 1;
+}
+
+// DeepWalk on an unweighted graph: one lane per walker, O(1) per step.
+__global__ void __launch_bounds__(256)
+    k_walk_replay_uniform(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                          int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
+                          int32_t L, const double *__restrict__ uniforms,
+                          int32_t *__restrict__ out, int32_t *status, int serial_only) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t wk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wk < n_walks;
+         wk += stride) {
+        int32_t v = starts[wk];
+        int32_t *o = out + wk * (int64_t)L;
+        o[0] = v;
+        const double *u = uniforms + wk * (int64_t)(L - 1);
+        int32_t s = 1;
+        for (; s < L; ++s) {
+            if (v < 0 || (int64_t)v >= n_rows) {
+                dw::status_or(status, DW_S_BAD_CSR);
+                break;
+            }
+            const int64_t a = row_ptr[v];
+            const int64_t n = row_ptr[v + 1] - a;
+            if (n <= 0) {
+                dw::status_or(status, DW_S_ISOLATED_NODE);
+                break;
+            }
+            const double U = u[s - 1];
+            int64_t pick = serial_only ? -1 : uniform_pick_exact(U, n);
+            if (pick < 0) pick = uniform_pick_serial(U, n);
+            v = col[a + pick];
+            o[s] = v;
+        }
+        for (; s < L; ++s) o[s] = -1;
+    }
+}
+
+// node2vec, unweighted, one wave per walker: the class of every neighbour (x == prev, x in
+// N(prev), other) in rounds of 64 as two ballots, the class counts give T, and the round and
+// lane where W crosses U*T give the pick. Returns -1 (serial replay) where the margin fails.
+// `masks`: this wave's LDS (2 * cap u64); rows past cap rounds re-classify in the second pass.
+__device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n, int32_t prev,
+                                       const int32_t *np_lds, int np_lds_n,
+                                       const int32_t *np_g, int64_t np_g_n, double U,
+                                       uint64_t *masks, int64_t cap, int lane) {
+    const int64_t rounds = (n + WAVE - 1) / WAVE;
+    auto classify = [&](int64_t r, uint64_t &mp, uint64_t &mq) {
+        const int64_t i = r * WAVE + lane;
+        bool is_p = false, is_q = false;
+        if (i < n) {
+            const int32_t x = c.col[a + i];
+            if (x == prev)
+                is_p = true;
+            else
+                is_q = np_lds ? contains_lds(np_lds, np_lds_n, x)
+                              : contains_global(np_g, np_g_n, x);
+        }
+        mp = __ballot(is_p);
+        mq = __ballot(is_q);
+    };
+    int64_t A = 0, C = 0;
+    for (int64_t r = 0; r < rounds; ++r) {
+        uint64_t mp, mq;
+        classify(r, mp, mq);
+        if (r < cap && lane == 0) {
+            masks[2 * r] = mp;
+            masks[2 * r + 1] = mq;
+        }
+        A += __popcll(mp);
+        C += __popcll(mq);
+    }
+    dw::wave_lds_sync();
+    const double ip = c.inv_p, iq = c.inv_q;
+    auto W = [&](int64_t na, int64_t nb, int64_t nc) {
+        return static_cast<double>(na) * ip + static_cast<double>(nb) +
+               static_cast<double>(nc) * iq;
+    };
+    const double T = W(A, n - A - C, C);
+    const double UT = U * T;
+    const double M = exact_margin(n, T);
+    int64_t na = 0, nc = 0;  // counts before round r
+    double d_prev = -UT;     // D of the neighbour before the round (W = 0 before neighbour 0)
+    for (int64_t r = 0; r < rounds; ++r) {
+        uint64_t mp, mq;
+        if (r < cap) {
+            mp = masks[2 * r];
+            mq = masks[2 * r + 1];
+        } else {
+            classify(r, mp, mq);
+        }
+        const int64_t base = r * WAVE;
+        const int64_t in_round = n - base < WAVE ? n - base : WAVE;
+        const uint64_t le = (lane == WAVE - 1) ? ~0ull : ((2ull << lane) - 1);  // lanes <= lane
+        const int64_t pa = na + __popcll(mp & le), pc = nc + __popcll(mq & le);
+        const int64_t i = base + lane;
+        const double d = W(pa, (i + 1) - pa - pc, pc) - UT;  // D_i (lanes past n: unused)
+        const uint64_t over = __ballot(lane < in_round && d > 0.0);
+        if (over) {
+            const int first = __ffsll((unsigned long long)over) - 1;
+            int64_t k = base + first;  // first i with D_i > 0
+            const double d_k = __shfl(d, first);
+            const double d_km1 = first > 0 ? __shfl(d, first - 1) : d_prev;
+            if (k > n - 1) k = n - 1;
+            if (k >= 1 && fabs(d_km1) <= M) return -1;
+            if (k <= n - 2 && fabs(d_k) <= M) return -1;
+            return k;
+        }
+        d_prev = __shfl(d, static_cast<int>(in_round - 1));
+        na += __popcll(mp);
+        nc += __popcll(mq);
+    }
+    return -1;  // no D_i > 0: rounding at the top end; the serial replay decides
+}
+
 __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
-                  int32_t *__restrict__ out, int32_t *status) {
+                  int32_t *__restrict__ out, int32_t *status, int fast) {
     __shared__ double s_buf[REPLAY_WAVES][REPLAY_CH];
     __shared__ int32_t s_nprev[REPLAY_WAVES][REPLAY_NCAP];
     __shared__ int64_t s_pick[REPLAY_WAVES];
@@ -150,6 +306,23 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 }
             }
             const double uu = u[s - 1];
+            if (fast) {  // unweighted: the exact pick without the serial sums (above)
+                const int64_t fp =
+                    (!c.node2vec || prev < 0)
+                        ? uniform_pick_exact(uu, n)
+                        : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, uu,
+                                              reinterpret_cast<uint64_t *>(buf),
+                                              REPLAY_CH / 2, lane);
+                if (fp >= 0) {
+                    const int32_t child = c.col[a + fp];
+                    if (lane == 0) o[s] = child;
+                    prev = v;
+                    v = child;
+                    dw::wave_lds_sync();  // N(prev) / masks are rewritten next step
+                    continue;
+                }
+                dw::wave_lds_sync();
+            }
             if (n <= REPLAY_CH) {
                 for (int64_t i = lane; i < n; i += WAVE)
                     buf[i] = step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n);
@@ -716,9 +889,25 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
     c.inv_q = c.node2vec ? 1.0 / q : 1.0;
     int64_t blocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
     if (blocks > 16384) blocks = 16384;
+    // unweighted graphs take the exact picks without the serial sums (k_walk_replay_uniform,
+    // node2vec_pick_exact); DW_REPLAY_SERIAL=1 keeps the serial replay everywhere (tests compare
+    // the two bit for bit)
+    const char *ser = getenv("DW_REPLAY_SERIAL");
+    const bool serial_only = ser && ser[0] == '1';
+    const bool fast = !weights && !serial_only && c.inv_p > 0.0 && c.inv_q > 0.0 &&
+                      c.inv_p < 1e300 && c.inv_q < 1e300;
+    if (!c.node2vec && !weights) {
+        int64_t ublocks = (n_walks + 255) / 256;
+        if (ublocks > 65536) ublocks = 65536;
+        hipLaunchKernelGGL(k_walk_replay_uniform, dim3((unsigned)ublocks), dim3(256), 0,
+                           dw::as_stream(stream), row_ptr, col, n_rows, starts, n_walks,
+                           walk_length, uniforms, out, status, serial_only ? 1 : 0);
+        DW_LAUNCH_CHECK("dw_walk_replay");
+        return DW_OK;
+    }
     hipLaunchKernelGGL(k_walk_replay, dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
                        dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length, uniforms,
-                       out, status);
+                       out, status, fast ? 1 : 0);
     DW_LAUNCH_CHECK("dw_walk_replay");
     return DW_OK;
 }

@@ -159,7 +159,11 @@ class RandomWalk(ABC):
             if self._rng == 'python':
                 if uniforms is None:
                     uniforms = draw_uniforms(n * (L - 1))
-                u = torch.from_numpy(np.ascontiguousarray(uniforms, dtype=np.float64).reshape(-1))
+                if isinstance(uniforms, torch.Tensor):   # e.g. already resident on the device
+                    u = uniforms.reshape(-1).to(device=dev, dtype=torch.float64).contiguous()
+                else:
+                    u = torch.from_numpy(np.ascontiguousarray(uniforms,
+                                                              dtype=np.float64).reshape(-1))
                 if u.numel() != n * (L - 1):
                     raise ValueError('uniforms must have n_walks * (length - 1) values')
                 u = u.to(dev)

@@ -334,3 +334,29 @@ def test_counted_node2vec_walks_equal_and_count(hip_device):
         assert c['steps'] == n * 19
         assert c['blocks'] >= c['steps'] - n        # >= one proposal block per biased step
         assert c['bytes'] >= c['steps'] * 36 + c['blocks'] * 16
+
+
+@pytest.mark.parametrize('method,p,q,n_walks,L', [('deepwalk', 1.0, 1.0, 65_536, 40),
+                                                  ('node2vec', 0.25, 4.0, 1024, 16),
+                                                  ('node2vec', 1.0, 1.0, 1024, 16),
+                                                  ('node2vec', 0.3, 3.0, 1024, 16)])
+def test_replay_exact_picks_equal_serial_replay(method, p, q, n_walks, L, hip_device,
+                                                monkeypatch):
+    """The replay walker's margin-checked picks (uniform_pick_exact / node2vec_pick_exact, no
+    serial sums; their rule is checked against CPython's arithmetic in test_replay_exact.py)
+    give bit for bit the walks of the serial replay (DW_REPLAY_SERIAL=1, the path the reference
+    fixtures pin) on R-MAT 16 hubs, with uniforms at random and on the step boundaries k/n."""
+    csr = rmat_graph(16, 600_000, 0)
+    deg = csr.degree()
+    starts = torch.as_tensor(np.resize(np.argsort(-deg[1:])[:64] + 1, n_walks).astype(np.int32))
+    rng = np.random.default_rng(7)
+    u = rng.random((n_walks, L - 1))
+    # a quarter of the uniforms exactly on a boundary k/deg of a hub's row (the rule declines)
+    u[::4, 0] = (np.arange(len(u[::4])) % (deg[starts.numpy()[::4]] - 1) + 1) / deg[
+        starts.numpy()[::4]]
+    mk = (lambda: Node2Vec(csr, L, p=p, q=q)) if method == 'node2vec' else (lambda: DeepWalk(csr, L))
+    fast = mk().walk_batch(starts, uniforms=u).cpu().numpy()
+    monkeypatch.setenv('DW_REPLAY_SERIAL', '1')
+    serial = mk().walk_batch(starts, uniforms=u).cpu().numpy()
+    np.testing.assert_array_equal(fast, serial)
+    assert (fast > 0).all() and int(deg[starts.numpy()].max()) > 2048   # hub rows past LDS
