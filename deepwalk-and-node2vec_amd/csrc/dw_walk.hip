@@ -57,6 +57,10 @@ __device__ __forceinline__ bool contains_lds(const int32_t *s, int n, int32_t ke
 constexpr int REPLAY_WAVES = 2;      // waves per block
 constexpr int REPLAY_CH = 2048;      // cached step weights per wave (float64): 16 KiB
 constexpr int REPLAY_NCAP = 2048;    // staged N(prev) entries per wave (int32): 8 KiB
+// with the exact picks (unweighted): the step-weight cache only serves the rare serial
+// fallback, so it shrinks to 4 KiB (= the class masks of 256 rounds) and twice as many waves
+// fit a CU (12 KiB per wave instead of 24)
+constexpr int REPLAY_CH_EXACT = 512;
 
 struct ReplayCtx {
     const int64_t *row_ptr;
@@ -203,15 +207,47 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
         mq = __ballot(is_q);
     };
     int64_t A = 0, C = 0;
-    for (int64_t r = 0; r < rounds; ++r) {
-        uint64_t mp, mq;
-        classify(r, mp, mq);
-        if (r < cap && lane == 0) {
-            masks[2 * r] = mp;
-            masks[2 * r + 1] = mq;
+    // first pass, 4 rounds per trip: the four membership searches are independent, so their
+    // dependent load chains overlap (branchless lower_bound over the same sorted N(prev))
+    constexpr int RB = 4;
+    const int32_t *ns = np_lds ? np_lds : np_g;
+    const int64_t nn = np_lds ? static_cast<int64_t>(np_lds_n) : np_g_n;
+    for (int64_t r0 = 0; r0 < rounds; r0 += RB) {
+        int32_t x[RB];
+        int64_t base[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            const int64_t i = (r0 + j) * WAVE + lane;
+            x[j] = i < n ? c.col[a + i] : prev;  // past the row: counted as neither class
+            base[j] = 0;
         }
-        A += __popcll(mp);
-        C += __popcll(mq);
+        int64_t len = nn;
+        while (len > 1) {
+            const int64_t half = len >> 1;
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+                base[j] = (ns[base[j] + half] < x[j]) ? base[j] + half : base[j];
+            len -= half;
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            const int64_t r = r0 + j;
+            const int64_t i = r * WAVE + lane;
+            const bool in_row = i < n;
+            const bool is_p = in_row && x[j] == prev;
+            int64_t lb = base[j];
+            if (nn > 0 && ns[lb] < x[j]) ++lb;
+            const bool is_q = in_row && !is_p && lb < nn && ns[lb] == x[j];
+            const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
+            if (r < rounds) {
+                if (r < cap && lane == 0) {
+                    masks[2 * r] = mp;
+                    masks[2 * r + 1] = mq;
+                }
+                A += __popcll(mp);
+                C += __popcll(mq);
+            }
+        }
     }
     dw::wave_lds_sync();
     const double ip = c.inv_p, iq = c.inv_q;
@@ -256,11 +292,12 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
     return -1;  // no D_i > 0: rounding at the top end; the serial replay decides
 }
 
+template <int CH>
 __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
                   int32_t *__restrict__ out, int32_t *status, int fast) {
-    __shared__ double s_buf[REPLAY_WAVES][REPLAY_CH];
+    __shared__ double s_buf[REPLAY_WAVES][CH];
     __shared__ int32_t s_nprev[REPLAY_WAVES][REPLAY_NCAP];
     __shared__ int64_t s_pick[REPLAY_WAVES];
     const int lane = threadIdx.x & (WAVE - 1);
@@ -312,7 +349,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                         ? uniform_pick_exact(uu, n)
                         : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, uu,
                                               reinterpret_cast<uint64_t *>(buf),
-                                              REPLAY_CH / 2, lane);
+                                              CH / 2, lane);
                 if (fp >= 0) {
                     const int32_t child = c.col[a + fp];
                     if (lane == 0) o[s] = child;
@@ -323,7 +360,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 }
                 dw::wave_lds_sync();
             }
-            if (n <= REPLAY_CH) {
+            if (n <= CH) {
                 for (int64_t i = lane; i < n; i += WAVE)
                     buf[i] = step_weight(c, a + i, prev, np_lds, np_lds_n, np_g, np_g_n);
                 dw::wave_lds_sync();
@@ -905,9 +942,14 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
         DW_LAUNCH_CHECK("dw_walk_replay");
         return DW_OK;
     }
-    hipLaunchKernelGGL(k_walk_replay, dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
-                       dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length, uniforms,
-                       out, status, fast ? 1 : 0);
+    if (fast)
+        hipLaunchKernelGGL(k_walk_replay<REPLAY_CH_EXACT>, dim3((unsigned)blocks),
+                           dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
+                           n_walks, walk_length, uniforms, out, status, 1);
+    else
+        hipLaunchKernelGGL(k_walk_replay<REPLAY_CH>, dim3((unsigned)blocks),
+                           dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
+                           n_walks, walk_length, uniforms, out, status, 0);
     DW_LAUNCH_CHECK("dw_walk_replay");
     return DW_OK;
 }
