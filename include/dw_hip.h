@@ -136,7 +136,11 @@ int dw_csr_from_edges(const uint64_t *edges, int64_t n_edges, int64_t n_nodes,
  * uniforms: float64[n_walks, L-1], consumed in the reference's order (one per step).
  * out: int32[n_walks, L]. Weighted graphs: weights != NULL (float64, networkx 'weight').
  * Arithmetic follows CPython 3.10 exactly: left-to-right fp64 sum, w *= (1/p), w/sum,
- * itertools.accumulate, total = cum[-1] + 0.0, bisect_right(cum, u*total, 0, deg-1). */
+ * itertools.accumulate, total = cum[-1] + 0.0, bisect_right(cum, u*total, 0, deg-1).
+ * Unweighted graphs (weights == NULL) reach the same picks without the serial sums: exact
+ * class counts give W_i - u*T, decided against a proven rounding bound, with the serial
+ * arithmetic only where the bound cannot decide; environment
+ * DW_REPLAY_SERIAL=1 forces the serial arithmetic everywhere (a testing aid). */
 int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                    const double *weights, int64_t n_rows, const int32_t *starts, int64_t n_walks,
                    int32_t walk_length, int32_t method, double p, double q,
