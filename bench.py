@@ -236,7 +236,8 @@ def main():
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
-                         'saves, 6.89 vs 6.89 ms/step at C3)')
+                         'saves, 6.89 vs 6.89 ms/step at C3; on by default on the one-GPU lazy '
+                         'path of small batches)')
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
@@ -493,8 +494,10 @@ def main():
 
     n_rec = [0]
     # walks: one batch per step; prefetched on a side stream unless owner 'gather' (a collective)
-    prefetch = args.walk_prefetch and not (owner and args.owner_walks == 'gather'
-                                           and not emulate)
+    # (on by default for the one-GPU lazy path, i.e. small batches: there the walker's dependent
+    # chain is ~9% of a step and hides behind the previous step, 0.625 -> 0.603 ms at 64 walks)
+    prefetch = (args.walk_prefetch or n1_lazy) and not (owner and args.owner_walks == 'gather'
+                                                        and not emulate)
     feed = WalkFeed(BG if owner else B,
                     (lambda s: s * BG) if owner else (lambda s: (s * world + rank) * B),
                     prefetch)

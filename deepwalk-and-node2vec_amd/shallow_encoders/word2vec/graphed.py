@@ -65,8 +65,11 @@ class GraphedStep:
         self.B, self.centres = int(B), int(B) * (L - 2 * R)
         self.status, self.loss_acc = status, loss_acc
         self.epoch_starts = epoch_starts
-        self.walks = torch.empty((self.B, L), dtype=torch.int32, device=dev)
-        self.starts = torch.empty(self.B, dtype=torch.int32, device=dev)
+        # the walks of all `unroll` steps of a graph come from ONE walker launch at its head:
+        # walks are a pure function of the global walk id, and a latency-bound walker takes as
+        # long for unroll*B walks as for B (the steps then read slices of the buffer)
+        self.walks = torch.empty((self.unroll * self.B, L), dtype=torch.int32, device=dev)
+        self.starts = torch.empty(self.unroll * self.B, dtype=torch.int32, device=dev)
         s1 = tables.step_count + 1                      # the Adam step the first replay applies
         hist = adam_history(s1 + n_steps + 2, tables.lr, tables.betas, tables.eps,
                             tables.weight_decay)
@@ -82,10 +85,10 @@ class GraphedStep:
                           fuse_out_adam=scatter == 'sorted')
         self.R, self.K = R, K
         self.graphs = {}
-        # the first step's start nodes; every replay then ends by writing the next step's
+        # the first graph's start nodes; every replay then ends by writing the next graph's
         with torch.cuda.device(dev):
             _native.call('dw_step_starts', _native.ptr(self.block), _native.ptr(self.epoch_starts),
-                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
                          _native.stream(dev))
         torch.cuda.synchronize(dev)
         # `unroll` consecutive steps per graph (one launch per `unroll` steps: at tiny batches
@@ -100,8 +103,7 @@ class GraphedStep:
             _native.call('dw_step_scalars_bind', _native.ptr(self.block))
             try:
                 with torch.cuda.graph(g, capture_error_mode='relaxed'):
-                    for _ in range(self.unroll):
-                        self._body()
+                    self._body()
             finally:
                 _native.call('dw_step_scalars_bind', None)
             self.graphs[parity] = g
@@ -110,17 +112,23 @@ class GraphedStep:
         torch.cuda.synchronize(dev)
 
     def _body(self) -> None:
-        t, dev = self.t, self.t.device
+        """One graph: the walks of its `unroll` steps, then the steps (the last advance writes
+        the next graph's start nodes)."""
+        t, dev, B = self.t, self.t.device, self.B
         self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
                                status=self.status)
-        replicated_step(t, self.walks, self.R, self.K, noise_offset=0, loss_acc=self.loss_acc,
-                        status=self.status, **self._args)
-        with torch.cuda.device(dev):
-            _native.call('dw_step_scalars_advance', _native.ptr(self.block),
-                         _native.ptr(self.hist), self.hist.shape[0], self.B, self.centres,
-                         _native.ptr(self.status), _native.ptr(self.epoch_starts),
-                         self.epoch_starts.numel(), _native.ptr(self.starts), self.B,
-                         _native.stream(dev))
+        for k in range(self.unroll):
+            replicated_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, noise_offset=0,
+                            loss_acc=self.loss_acc, status=self.status, **self._args)
+            last = k == self.unroll - 1
+            with torch.cuda.device(dev):
+                _native.call('dw_step_scalars_advance', _native.ptr(self.block),
+                             _native.ptr(self.hist), self.hist.shape[0], B, self.centres,
+                             _native.ptr(self.status),
+                             _native.ptr(self.epoch_starts) if last else None,
+                             self.epoch_starts.numel() if last else 0,
+                             _native.ptr(self.starts) if last else None,
+                             self.starts.numel() if last else 0, _native.stream(dev))
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host
