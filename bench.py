@@ -233,6 +233,8 @@ def main():
                          '(C3 at 64-walk batches)')
     ap.add_argument('--calib-steps', type=int, default=8,
                     help='--in-exchange auto: timed steps per protocol')
+    ap.add_argument('--graph-unroll', type=int, default=0,
+                    help='steps per captured graph (0: the largest of 16, 8, 4, 2, 1 dividing --steps)')
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
@@ -572,7 +574,10 @@ def main():
         from shallow_encoders.word2vec.graphed import GraphedStep
         # several steps per graph: between replays the launch gap (~19 us) is as long as a
         # tiny step; the unroll divides --steps so exactly --steps steps are timed
-        unroll = next(u for u in (8, 4, 2, 1) if args.steps % u == 0)
+        unroll = (args.graph_unroll if args.graph_unroll > 0 else
+                  next(u for u in (16, 8, 4, 2, 1) if args.steps % u == 0))
+        if args.steps % unroll:
+            raise SystemExit(f'--graph-unroll {unroll} must divide --steps {args.steps}')
         graphed = GraphedStep(tables, walker, epoch_starts,
                               B, R, K, seed=99, grad_scale=grad_scale, loss_acc=loss_acc,
                               status=status, first_walk_id=step_idx[0] * B,

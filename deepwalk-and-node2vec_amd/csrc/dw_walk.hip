@@ -582,6 +582,39 @@ __global__ void __launch_bounds__(256)
         starts_out[k] = epoch[(base + static_cast<uint64_t>(k)) % static_cast<uint64_t>(n_epoch)];
 }
 
+// dw_step_scalars_expand: one block; thread 0 writes the blocks of the next n_steps steps and
+// moves `base` past them, then the block's threads write the first one's start nodes (for all
+// the steps' walks: n = n_steps * walks per step).
+__global__ void __launch_bounds__(256)
+    k_step_expand(dw_step_scalars *base, dw_step_scalars *steps, int64_t n_steps,
+                  const float *__restrict__ hist, int64_t hist_rows, uint64_t walks_per_step,
+                  uint64_t centres_per_step, int32_t *status, const int32_t *__restrict__ epoch,
+                  int64_t n_epoch, int32_t *__restrict__ starts_out, int64_t n) {
+    __shared__ uint64_t first_wid;
+    if (threadIdx.x == 0) {
+        dw_step_scalars b = *base;
+        first_wid = b.walk_id0;
+        for (int64_t j = 0; j <= n_steps; ++j) {
+            if (j > 0) {  // the advance of dw_step_scalars_advance
+                b.walk_id0 += walks_per_step;
+                b.noise_offset += centres_per_step;
+                const int64_t s = ++b.step;
+                if (s >= hist_rows)
+                    dw::status_or(status, DW_S_BAD_INDEX);
+                else
+                    for (int k = 0; k < 8; ++k) b.adam[k] = hist[8 * s + k];
+            }
+            if (j < n_steps) steps[j] = b;
+        }
+        *base = b;
+    }
+    if (!epoch) return;
+    __syncthreads();
+    const uint64_t w0 = first_wid;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x)
+        starts_out[k] = epoch[(w0 + static_cast<uint64_t>(k)) % static_cast<uint64_t>(n_epoch)];
+}
+
 constexpr int N2V_WAVES = 4;     // waves per block
 // (Occupancy: the hashed variant compiles to 73 VGPRs, 6 waves/SIMD. Forcing 8 waves/SIMD
 // (amdgpu_waves_per_eu) spills to scratch and measured 16% slower at C3.)
@@ -1064,6 +1097,23 @@ int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t his
                        hist_rows, walks_per_step, centres_per_step, status, epoch_starts, n_epoch,
                        starts_out, n);
     DW_LAUNCH_CHECK("dw_step_scalars_advance");
+    return DW_OK;
+}
+
+int dw_step_scalars_expand(dw_step_scalars *base, dw_step_scalars *steps, int64_t n_steps,
+                           const float *hist, int64_t hist_rows, uint64_t walks_per_step,
+                           uint64_t centres_per_step, int32_t *status,
+                           const int32_t *epoch_starts, int64_t n_epoch, int32_t *starts_out,
+                           int64_t n, void *stream) {
+    DW_REQUIRE(base && steps && hist && status && hist_rows >= 1 && n_steps >= 1 &&
+                   n_steps <= 4096,
+               "dw_step_scalars_expand: bad arguments");
+    DW_REQUIRE(!epoch_starts || (starts_out && n_epoch >= 1 && n >= 0),
+               "dw_step_scalars_expand: bad start-node arguments");
+    hipLaunchKernelGGL(k_step_expand, dim3(1), dim3(256), 0, dw::as_stream(stream), base, steps,
+                       n_steps, hist, hist_rows, walks_per_step, centres_per_step, status,
+                       epoch_starts, n_epoch, starts_out, n);
+    DW_LAUNCH_CHECK("dw_step_scalars_expand");
     return DW_OK;
 }
 

@@ -126,6 +126,8 @@ SIGNATURES = {
     'dw_step_scalars_advance': (ctypes.c_int, [_p, _p, _i64, _u64, _u64, _p, _p, _i64, _p,
                                                _i64, _p]),
     'dw_step_starts': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),
+    'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,
+                                              _p, _i64, _p]),
 }
 
 

@@ -8,13 +8,14 @@ of the input table's double buffer (two hipGraphs) and replays it.
 
 What changes from step to step is kept in device memory (include/dw_hip.h, dw_step_scalars):
 the walk id of the step's first walk (the Philox walker), the centre counter of its negatives
-(SGNS pass 1) and the Adam scalars (both tables' updates). While the block is bound during
-capture, those kernels read it instead of their by-value arguments; the captured step ends with
-``dw_step_scalars_advance``, which moves the block to the next step from a precomputed history of
-Adam scalars (float64 on the host, rounded to float32 exactly as the eager launches pass them).
-The start nodes come from the epoch's start list by walk id (``dw_step_starts`` for the first
-step; the advance writes the next step's). The kernels and
-their results are those of the eager step (tests/test_gpu_graphed.py).
+(SGNS pass 1) and the Adam scalars (both tables' updates). While a block is bound during
+capture, those kernels read it instead of their by-value arguments. A graph replays `unroll`
+steps: its first node, ``dw_step_scalars_expand``, writes the blocks of those steps from the
+running block (and moves it past them) using a precomputed history of Adam scalars (float64 on
+the host, rounded to float32 exactly as the eager launches pass them), plus the start nodes of
+all their walks from the epoch's start list; one walker launch then generates those walks, and
+step k's kernels are captured with block k bound. The kernels and their results are those of
+the eager step (tests/test_gpu_graphed.py).
 """
 from typing import Optional
 
@@ -81,15 +82,14 @@ class GraphedStep:
         blk['step'] = s1
         blk['adam'][0] = hist[s1]
         self.block = torch.from_numpy(np.frombuffer(blk.tobytes(), dtype=np.uint8).copy()).to(dev)
+        # the graph's steps' own blocks, written at its head by one dw_step_scalars_expand
+        # (instead of one advance launch per step); step k's launches bind self._step_blk(k)
+        self.step_blocks = torch.zeros(self.unroll * _STEP_DTYPE.itemsize, dtype=torch.uint8,
+                                       device=dev)
         self._args = dict(seed=seed, grad_scale=grad_scale, scatter=scatter,
                           fuse_out_adam=scatter == 'sorted')
         self.R, self.K = R, K
         self.graphs = {}
-        # the first graph's start nodes; every replay then ends by writing the next graph's
-        with torch.cuda.device(dev):
-            _native.call('dw_step_starts', _native.ptr(self.block), _native.ptr(self.epoch_starts),
-                         self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
-                         _native.stream(dev))
         torch.cuda.synchronize(dev)
         # `unroll` consecutive steps per graph (one launch per `unroll` steps: at tiny batches
         # the gap between replays is as long as the step). One graph per parity of the in-table
@@ -100,7 +100,6 @@ class GraphedStep:
         for _ in range(n_graphs):
             parity = tables._cur_in
             g = torch.cuda.CUDAGraph()
-            _native.call('dw_step_scalars_bind', _native.ptr(self.block))
             try:
                 with torch.cuda.graph(g, capture_error_mode='relaxed'):
                     self._body()
@@ -111,24 +110,26 @@ class GraphedStep:
         tables.step_count -= n_graphs * self.unroll
         torch.cuda.synchronize(dev)
 
+    def _step_blk(self, k: int) -> int:
+        return self.step_blocks.data_ptr() + k * _STEP_DTYPE.itemsize
+
     def _body(self) -> None:
-        """One graph: the walks of its `unroll` steps, then the steps (the last advance writes
-        the next graph's start nodes)."""
+        """One graph: its steps' scalar blocks and start nodes (one launch; self.block moves
+        past the graph), the walks of all its steps (one walker launch), then the steps."""
         t, dev, B = self.t, self.t.device, self.B
+        with torch.cuda.device(dev):
+            _native.call('dw_step_scalars_expand', _native.ptr(self.block), self._step_blk(0),
+                         self.unroll, _native.ptr(self.hist), self.hist.shape[0], B,
+                         self.centres, _native.ptr(self.status), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
+                         _native.stream(dev))
+        _native.call('dw_step_scalars_bind', self._step_blk(0))
         self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
                                status=self.status)
         for k in range(self.unroll):
+            _native.call('dw_step_scalars_bind', self._step_blk(k))
             replicated_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, noise_offset=0,
                             loss_acc=self.loss_acc, status=self.status, **self._args)
-            last = k == self.unroll - 1
-            with torch.cuda.device(dev):
-                _native.call('dw_step_scalars_advance', _native.ptr(self.block),
-                             _native.ptr(self.hist), self.hist.shape[0], B, self.centres,
-                             _native.ptr(self.status),
-                             _native.ptr(self.epoch_starts) if last else None,
-                             self.epoch_starts.numel() if last else 0,
-                             _native.ptr(self.starts) if last else None,
-                             self.starts.numel() if last else 0, _native.stream(dev))
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host

@@ -514,6 +514,17 @@ int dw_step_scalars_advance(dw_step_scalars *dev, const float *hist, int64_t his
                             const int32_t *epoch_starts, int64_t n_epoch, int32_t *starts_out,
                             int64_t n, void *stream);
 
+/* Several steps in one launch (a graph that replays n_steps steps): steps[j] = *base advanced j
+ * times as dw_step_scalars_advance would (j = 0 .. n_steps-1), then *base advanced n_steps
+ * times; with epoch_starts != NULL, starts_out[k] = epoch_starts[(steps[0].walk_id0 + k) mod
+ * n_epoch] for k < n (the start nodes of all n_steps steps' walks). Binding &steps[j] for step
+ * j's launches replaces the n_steps advance launches of a captured multi-step graph. */
+int dw_step_scalars_expand(dw_step_scalars *base, dw_step_scalars *steps, int64_t n_steps,
+                           const float *hist, int64_t hist_rows, uint64_t walks_per_step,
+                           uint64_t centres_per_step, int32_t *status,
+                           const int32_t *epoch_starts, int64_t n_epoch, int32_t *starts_out,
+                           int64_t n, void *stream);
+
 /* starts_out[k] = epoch_starts[(dev->walk_id0 + k) mod n_epoch] for k < n: the start nodes of
  * a step's walks when walk w of the epoch starts at epoch_starts[w] (RandomWalkDataset's
  * `_get_current_node`, datasets.py:69-76, with the walk ids of the epoch). */
