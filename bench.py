@@ -234,7 +234,8 @@ def main():
     ap.add_argument('--calib-steps', type=int, default=8,
                     help='--in-exchange auto: timed steps per protocol')
     ap.add_argument('--graph-unroll', type=int, default=0,
-                    help='steps per captured graph (0: the largest of 16, 8, 4, 2, 1 dividing --steps)')
+                    help='steps per captured graph (0: the largest of 16, 8, 4, 2, 1 that '
+                         'divides --steps)')
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '

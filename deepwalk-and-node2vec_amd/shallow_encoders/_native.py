@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
