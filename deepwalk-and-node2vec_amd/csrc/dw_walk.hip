@@ -183,6 +183,59 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// The same walks over the edge-inline CSR (dw_edges_inline_build: {x, deg(x), row_ptr[x]} per
+// entry): the picked entry carries the next row, so a step is one dependent 16-B load (plus the
+// step's uniform, which does not depend on the walk).
+__global__ void __launch_bounds__(256)
+    k_walk_replay_uniform_inline(const int64_t *__restrict__ row_ptr,
+                                 const int4 *__restrict__ edges, int64_t n_rows,
+                                 const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
+                                 const double *__restrict__ uniforms, int32_t *__restrict__ out,
+                                 int32_t *status, int serial_only) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t wk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wk < n_walks;
+         wk += stride) {
+        const int32_t v0 = starts[wk];
+        int32_t *o = out + wk * (int64_t)L;
+        const double *u = uniforms + wk * (int64_t)(L - 1);
+        bool ok = v0 >= 0 && (int64_t)v0 < n_rows;
+        if (!ok) dw::status_or(status, DW_S_BAD_CSR);
+        int64_t a = ok ? row_ptr[v0] : 0;
+        int64_t n = ok ? row_ptr[v0 + 1] - a : 0;
+        double U = L > 1 ? u[0] : 0.0;  // the coming step's uniform, loaded a step ahead
+        auto step = [&](int32_t s) -> int32_t {  // node at step s >= 1 (-1 once aborted)
+            if (!ok) return -1;
+            if (n <= 0) {
+                dw::status_or(status, DW_S_ISOLATED_NODE);
+                ok = false;
+                return -1;
+            }
+            int64_t pick = serial_only ? -1 : uniform_pick_exact(U, n);
+            if (pick < 0) pick = uniform_pick_serial(U, n);
+            const int4 e = edges[a + pick];
+            if (s + 1 < L) U = u[s];  // independent of e: overlaps the load's latency
+            a = static_cast<int64_t>(static_cast<uint32_t>(e.z)) |
+                (static_cast<int64_t>(e.w) << 32);
+            n = e.y;
+            return e.x;
+        };
+        if ((L & 3) == 0) {  // the walk leaves in 16-B stores of 4 steps
+            int4 *o4 = reinterpret_cast<int4 *>(o);
+            for (int32_t s0 = 0; s0 < L; s0 += 4) {
+                int4 pk;
+                pk.x = s0 == 0 ? v0 : step(s0);
+                pk.y = step(s0 + 1);
+                pk.z = step(s0 + 2);
+                pk.w = step(s0 + 3);
+                o4[s0 >> 2] = pk;
+            }
+        } else {
+            o[0] = v0;
+            for (int32_t s = 1; s < L; ++s) o[s] = step(s);
+        }
+    }
+}
+
 // node2vec, unweighted, one wave per walker: the class of every neighbour (x == prev, x in
 // N(prev), other) in rounds of 64 as two ballots, the class counts give T, and the round and
 // lane where W crosses U*T give the pick. Returns -1 (serial replay) where the margin fails.
@@ -984,6 +1037,27 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
                            dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
                            n_walks, walk_length, uniforms, out, status, 0);
     DW_LAUNCH_CHECK("dw_walk_replay");
+    return DW_OK;
+}
+
+int dw_walk_replay_inline(const int64_t *row_ptr, const int32_t *edges, int64_t n_rows,
+                          const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                          const double *uniforms, int32_t *out, int32_t *status, void *stream) {
+    DW_REQUIRE(walk_length >= 1, "dw_walk_replay_inline: walk_length must be >= 1");
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_replay_inline: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && edges && starts && out && status,
+               "dw_walk_replay_inline: null pointer");
+    DW_REQUIRE(walk_length == 1 || uniforms, "dw_walk_replay_inline: uniforms is null");
+    const char *ser = getenv("DW_REPLAY_SERIAL");
+    const bool serial_only = ser && ser[0] == '1';
+    int64_t blocks = (n_walks + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_walk_replay_uniform_inline, dim3((unsigned)blocks), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, reinterpret_cast<const int4 *>(edges),
+                       n_rows, starts, n_walks, walk_length, uniforms, out, status,
+                       serial_only ? 1 : 0);
+    DW_LAUNCH_CHECK("dw_walk_replay_inline");
     return DW_OK;
 }
 

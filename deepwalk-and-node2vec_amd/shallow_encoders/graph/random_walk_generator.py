@@ -67,7 +67,9 @@ class RandomWalk(ABC):
             layout: rng='philox' — 'indexed' (default, dw_walk_fast_indexed: DeepWalk over the
                 edge-inline CSR, one dependent load per step; node2vec adjacency tests in the
                 per-row hash) or 'csr' (dw_walk_fast: row_ptr / col, node2vec tests by search of
-                the sorted lists). Both give the same walks bit for bit.
+                the sorted lists). Both give the same walks bit for bit. rng='python':
+                'indexed' runs DeepWalk on unweighted graphs over the edge-inline CSR
+                (dw_walk_replay_inline), 'csr' keeps dw_walk_replay; the same walks.
         """
         assert length >= 1, 'Minimum walk length is 1!'
         if rng not in ('python', 'philox'):
@@ -146,9 +148,14 @@ class RandomWalk(ABC):
         # edge-inline CSR, node2vec with the per-row adjacency hash (the same walks as
         # dw_walk_fast, bit for bit; layout='csr' selects that one)
         indexed = self._rng == 'philox' and self._layout == 'indexed'
+        # replay, DeepWalk on an unweighted graph: the same walks over the edge-inline CSR
+        # (dw_walk_replay_inline; layout='csr' keeps dw_walk_replay)
+        replay_inline = (self._rng == 'python' and not n2v and self._layout == 'indexed'
+                         and self._csr.weights is None)
         d = self._csr.device_tensors(dev, need_sorted=n2v and not indexed,
                                      need_alias=self._rng == 'philox',
-                                     need_edges=indexed and not n2v, need_adj=indexed and n2v)
+                                     need_edges=(indexed and not n2v) or replay_inline,
+                                     need_adj=indexed and n2v)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         if status is None:
@@ -167,11 +174,19 @@ class RandomWalk(ABC):
                 if u.numel() != n * (L - 1):
                     raise ValueError('uniforms must have n_walks * (length - 1) values')
                 u = u.to(dev)
-                _native.call('dw_walk_replay', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
-                             _native.ptr(d.get('col_sorted')), _native.ptr(d['weights']),
-                             self._csr.vocab_size, _native.ptr(starts), n, L, self.METHOD,
-                             float(p), float(q), _native.ptr(u) if u.numel() else None,
-                             _native.ptr(out), _native.ptr(status), s)
+                if replay_inline:
+                    _native.call('dw_walk_replay_inline', _native.ptr(d['row_ptr']),
+                                 _native.ptr(d['edges']), self._csr.vocab_size,
+                                 _native.ptr(starts), n, L,
+                                 _native.ptr(u) if u.numel() else None, _native.ptr(out),
+                                 _native.ptr(status), s)
+                else:
+                    _native.call('dw_walk_replay', _native.ptr(d['row_ptr']),
+                                 _native.ptr(d['col']), _native.ptr(d.get('col_sorted')),
+                                 _native.ptr(d['weights']), self._csr.vocab_size,
+                                 _native.ptr(starts), n, L, self.METHOD, float(p), float(q),
+                                 _native.ptr(u) if u.numel() else None, _native.ptr(out),
+                                 _native.ptr(status), s)
             else:
                 wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
                 if indexed:

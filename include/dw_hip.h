@@ -146,6 +146,14 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
                    int32_t walk_length, int32_t method, double p, double q,
                    const double *uniforms, int32_t *out, int32_t *status, void *stream);
 
+/* dw_walk_replay for DeepWalk on an unweighted graph over the edge-inline CSR `edges`
+ * (dw_edges_inline_build): the same walks bit for bit (the exact picks of dw_walk_replay, with
+ * the serial arithmetic where their bound cannot decide, DW_REPLAY_SERIAL honoured), one
+ * dependent 16-B load per step. Replaces random_walk_generator.py:61-72 on unweighted graphs. */
+int dw_walk_replay_inline(const int64_t *row_ptr, const int32_t *edges, int64_t n_rows,
+                          const int32_t *starts, int64_t n_walks, int32_t walk_length,
+                          const double *uniforms, int32_t *out, int32_t *status, void *stream);
+
 /* Fast walker (Philox4x32-10 keyed by (seed, walk_id0 + w, step, round/lane)); walks are a pure
  * function of (seed, global walk id), identical for any grid and any number of GPUs.
  *   DeepWalk: one lane per walker; uniform neighbour (unweighted) or alias table (weighted).
