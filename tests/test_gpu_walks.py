@@ -356,9 +356,11 @@ def test_replay_exact_picks_equal_serial_replay(method, p, q, n_walks, L, hip_de
         starts.numpy()[::4]]
     mk = (lambda: Node2Vec(csr, L, p=p, q=q)) if method == 'node2vec' else (lambda: DeepWalk(csr, L))
     fast = mk().walk_batch(starts, uniforms=u).cpu().numpy()
-    if method == 'deepwalk':   # edge-inline replay (default) == plain-CSR replay (layout='csr')
-        plain = DeepWalk(csr, L, layout='csr').walk_batch(starts, uniforms=u).cpu().numpy()
-        np.testing.assert_array_equal(fast, plain)
+    # default layout (DeepWalk over the edge-inline CSR, node2vec with hashed adjacency tests)
+    # == the plain-CSR replay (layout='csr')
+    plain = (Node2Vec(csr, L, p=p, q=q, layout='csr') if method == 'node2vec'
+             else DeepWalk(csr, L, layout='csr')).walk_batch(starts, uniforms=u).cpu().numpy()
+    np.testing.assert_array_equal(fast, plain)
     monkeypatch.setenv('DW_REPLAY_SERIAL', '1')
     serial = mk().walk_batch(starts, uniforms=u).cpu().numpy()
     np.testing.assert_array_equal(fast, serial)
