@@ -61,6 +61,10 @@ constexpr int REPLAY_NCAP = 2048;    // staged N(prev) entries per wave (int32):
 // fallback, so it shrinks to 4 KiB (= the class masks of 256 rounds) and twice as many waves
 // fit a CU (12 KiB per wave instead of 24)
 constexpr int REPLAY_CH_EXACT = 512;
+#ifndef DW_REPLAY_NCAP_EXACT
+#define DW_REPLAY_NCAP_EXACT 2048
+#endif
+constexpr int REPLAY_NCAP_EXACT = DW_REPLAY_NCAP_EXACT;
 
 struct ReplayCtx {
     const int64_t *row_ptr;
@@ -345,13 +349,13 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
     return -1;  // no D_i > 0: rounding at the top end; the serial replay decides
 }
 
-template <int CH>
+template <int CH, int NCAP>
 __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
                   int32_t *__restrict__ out, int32_t *status, int fast) {
     __shared__ double s_buf[REPLAY_WAVES][CH];
-    __shared__ int32_t s_nprev[REPLAY_WAVES][REPLAY_NCAP];
+    __shared__ int32_t s_nprev[REPLAY_WAVES][NCAP];
     __shared__ int64_t s_pick[REPLAY_WAVES];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
@@ -385,7 +389,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             if (c.node2vec && prev >= 0) {
                 const int64_t pa = c.row_ptr[prev];
                 const int64_t pn = c.row_ptr[prev + 1] - pa;
-                if (pn <= REPLAY_NCAP) {
+                if (pn <= NCAP) {
                     for (int64_t e = lane; e < pn; e += WAVE) nprev_lds[e] = c.col_sorted[pa + e];
                     dw::wave_lds_sync();
                     np_lds = nprev_lds;
@@ -1029,11 +1033,11 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
         return DW_OK;
     }
     if (fast)
-        hipLaunchKernelGGL(k_walk_replay<REPLAY_CH_EXACT>, dim3((unsigned)blocks),
+        hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
                            dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
                            n_walks, walk_length, uniforms, out, status, 1);
     else
-        hipLaunchKernelGGL(k_walk_replay<REPLAY_CH>, dim3((unsigned)blocks),
+        hipLaunchKernelGGL((k_walk_replay<REPLAY_CH, REPLAY_NCAP>), dim3((unsigned)blocks),
                            dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
                            n_walks, walk_length, uniforms, out, status, 0);
     DW_LAUNCH_CHECK("dw_walk_replay");
