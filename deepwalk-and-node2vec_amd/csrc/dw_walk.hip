@@ -58,11 +58,16 @@ constexpr int REPLAY_WAVES = 2;      // waves per block
 constexpr int REPLAY_CH = 2048;      // cached step weights per wave (float64): 16 KiB
 constexpr int REPLAY_NCAP = 2048;    // staged N(prev) entries per wave (int32): 8 KiB
 // with the exact picks (unweighted): the step-weight cache only serves the rare serial
-// fallback, so it shrinks to 4 KiB (= the class masks of 256 rounds) and twice as many waves
-// fit a CU (12 KiB per wave instead of 24)
-constexpr int REPLAY_CH_EXACT = 512;
+// fallback, so it shrinks to 4 KiB (= the class masks of 256 rounds), and N(prev) is staged up
+// to 1024 entries (longer lists: binary search in HBM): 8 KiB per wave instead of 24, three
+// times the walkers per CU (measured at C3, 65,536 walks: 38.5 ms at 12 KiB, 31.0 at 8 KiB;
+// 768 or 512 staged entries, or a 2-KiB mask cache, were slower)
+#ifndef DW_REPLAY_CH_EXACT
+#define DW_REPLAY_CH_EXACT 512
+#endif
+constexpr int REPLAY_CH_EXACT = DW_REPLAY_CH_EXACT;
 #ifndef DW_REPLAY_NCAP_EXACT
-#define DW_REPLAY_NCAP_EXACT 2048
+#define DW_REPLAY_NCAP_EXACT 1024
 #endif
 constexpr int REPLAY_NCAP_EXACT = DW_REPLAY_NCAP_EXACT;
 
