@@ -737,7 +737,7 @@ def main():
                 w = (Node2Vec(csr, L, p=p, q=q, device=dev) if meth == 'node2vec'
                      else DeepWalk(csr, L, device=dev))
                 gen = _random.Random(0)
-                st = torch.arange(1, n_r + 1, dtype=torch.int32)
+                st = (torch.arange(n_r, dtype=torch.int32) % N) + 1   # node ids 1..N, cycled
                 w.walk_batch(st[:64], uniforms=draw_uniforms(64 * (L - 1), gen))
                 u = draw_uniforms(n_r * (L - 1), gen)
                 out = torch.empty((n_r, L), dtype=torch.int32, device=dev)
