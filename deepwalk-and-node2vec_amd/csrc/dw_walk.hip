@@ -193,54 +193,77 @@ __global__ void __launch_bounds__(256)
 }
 
 // The same walks over the edge-inline CSR (dw_edges_inline_build: {x, deg(x), row_ptr[x]} per
-// entry): the picked entry carries the next row, so a step is one dependent 16-B load (plus the
-// step's uniform, which does not depend on the walk).
+// entry): the picked entry carries the next row, so a step is one dependent 16-B load. The
+// uniforms arrive walk-major (the reference's stream order: walk w's L-1 draws together), so a
+// lane reading its own walk's draw touches a separate line per lane and step; a block instead
+// stages RU_T steps of its 256 walks in LDS with coalesced loads (16 lanes read one walk's
+// 128-B slice) and each lane then reads its draws from there.
+constexpr int RU_T = 16;  // staged steps per tile
 __global__ void __launch_bounds__(256)
     k_walk_replay_uniform_inline(const int64_t *__restrict__ row_ptr,
                                  const int4 *__restrict__ edges, int64_t n_rows,
                                  const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
                                  const double *__restrict__ uniforms, int32_t *__restrict__ out,
                                  int32_t *status, int serial_only) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t wk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wk < n_walks;
-         wk += stride) {
-        const int32_t v0 = starts[wk];
+    __shared__ double tile[256][RU_T + 1];  // +1: lanes of one wave read different banks
+    const int tid = threadIdx.x;
+    const int64_t n_chunks = (n_walks + 255) / 256;
+    const int64_t UL = L - 1;  // draws per walk
+    for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+        const int64_t w0 = ch * 256;
+        const int n_here = (n_walks - w0 < 256) ? static_cast<int>(n_walks - w0) : 256;
+        const int64_t wk = w0 + tid;
+        const bool live = tid < n_here;
+        int32_t v0 = live ? starts[wk] : 0;
         int32_t *o = out + wk * (int64_t)L;
-        const double *u = uniforms + wk * (int64_t)(L - 1);
-        bool ok = v0 >= 0 && (int64_t)v0 < n_rows;
-        if (!ok) dw::status_or(status, DW_S_BAD_CSR);
+        bool ok = live && v0 >= 0 && (int64_t)v0 < n_rows;
+        if (live && !ok) dw::status_or(status, DW_S_BAD_CSR);
         int64_t a = ok ? row_ptr[v0] : 0;
         int64_t n = ok ? row_ptr[v0 + 1] - a : 0;
-        double U = L > 1 ? u[0] : 0.0;  // the coming step's uniform, loaded a step ahead
-        auto step = [&](int32_t s) -> int32_t {  // node at step s >= 1 (-1 once aborted)
-            if (!ok) return -1;
-            if (n <= 0) {
-                dw::status_or(status, DW_S_ISOLATED_NODE);
-                ok = false;
-                return -1;
+        const bool pack = (L & 3) == 0;
+        int32_t q0 = v0, q1 = -1, q2 = -1;  // the current 4-step group (pack)
+        if (live && !pack) o[0] = v0;
+        for (int64_t t0 = 0; t0 < UL; t0 += RU_T) {
+            const int tn = (UL - t0 < RU_T) ? static_cast<int>(UL - t0) : RU_T;
+            __syncthreads();  // the previous tile is consumed
+#pragma unroll 4
+            for (int it = 0; it < RU_T; ++it) {
+                const int e = it * 256 + tid;
+                const int wl = e / RU_T, sl = e % RU_T;
+                if (wl < n_here && sl < tn) tile[wl][sl] = uniforms[(w0 + wl) * UL + t0 + sl];
             }
-            int64_t pick = serial_only ? -1 : uniform_pick_exact(U, n);
-            if (pick < 0) pick = uniform_pick_serial(U, n);
-            const int4 e = edges[a + pick];
-            if (s + 1 < L) U = u[s];  // independent of e: overlaps the load's latency
-            a = static_cast<int64_t>(static_cast<uint32_t>(e.z)) |
-                (static_cast<int64_t>(e.w) << 32);
-            n = e.y;
-            return e.x;
-        };
-        if ((L & 3) == 0) {  // the walk leaves in 16-B stores of 4 steps
-            int4 *o4 = reinterpret_cast<int4 *>(o);
-            for (int32_t s0 = 0; s0 < L; s0 += 4) {
-                int4 pk;
-                pk.x = s0 == 0 ? v0 : step(s0);
-                pk.y = step(s0 + 1);
-                pk.z = step(s0 + 2);
-                pk.w = step(s0 + 3);
-                o4[s0 >> 2] = pk;
+            __syncthreads();
+            if (!live) continue;
+            for (int j = 0; j < tn; ++j) {
+                const int32_t st = static_cast<int32_t>(t0) + 1 + j;  // the step this draw makes
+                int32_t node = -1;
+                if (ok) {
+                    if (n <= 0) {
+                        dw::status_or(status, DW_S_ISOLATED_NODE);
+                        ok = false;
+                    } else {
+                        const double U = tile[tid][j];
+                        int64_t pick = serial_only ? -1 : uniform_pick_exact(U, n);
+                        if (pick < 0) pick = uniform_pick_serial(U, n);
+                        const int4 e = edges[a + pick];
+                        a = static_cast<int64_t>(static_cast<uint32_t>(e.z)) |
+                            (static_cast<int64_t>(e.w) << 32);
+                        n = e.y;
+                        node = e.x;
+                    }
+                }
+                if (!pack) {
+                    o[st] = node;
+                } else {
+                    switch (st & 3) {  // the walk leaves in 16-B stores of 4 steps
+                        case 0: q0 = node; break;
+                        case 1: q1 = node; break;
+                        case 2: q2 = node; break;
+                        default:
+                            reinterpret_cast<int4 *>(o)[st >> 2] = int4{q0, q1, q2, node};
+                    }
+                }
             }
-        } else {
-            o[0] = v0;
-            for (int32_t s = 1; s < L; ++s) o[s] = step(s);
         }
     }
 }
