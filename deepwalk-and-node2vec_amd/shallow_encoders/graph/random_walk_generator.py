@@ -51,6 +51,47 @@ def _csr_of(graph) -> CSRGraph:
     return csr
 
 
+def _dyadic_scale(x: np.ndarray) -> int:
+    """Smallest k >= 0 such that every finite double in ``x`` is a multiple of 2**-k."""
+    x = np.abs(np.asarray(x, dtype=np.float64).reshape(-1))
+    x = x[x > 0]
+    if x.size == 0:
+        return 0
+    m, e = np.frexp(x)                                   # x = m * 2**e, m in [0.5, 1)
+    mant = (m * 2.0 ** 53).astype(np.uint64)             # x = mant * 2**(e - 53), exactly
+    low = mant & (~mant + np.uint64(1))                  # lowest set bit of the mantissa
+    tz = np.log2(low.astype(np.float64)).astype(np.int64)
+    return int(max(0, int(np.max(53 - e.astype(np.int64) - tz))))
+
+
+def sum_is_exact(csr: CSRGraph, inv_p: float, inv_q: float, node2vec: bool) -> bool:
+    """True when every left-to-right partial sum of every step's (modified) weights is exactly
+    representable, so naive and compensated summation give the same double (random_walk_generator
+    .py:50-53,110 ``sum(neighbor_weights)``): all terms are multiples of 2**-k and the largest
+    row's total stays below 2**53 at that scale."""
+    factors = [1.0, float(inv_p), float(inv_q)] if node2vec else [1.0]
+    if not all(np.isfinite(factors)):
+        return False
+    row_ptr = np.asarray(csr.row_ptr, dtype=np.int64)
+    deg = np.diff(row_ptr)
+    if csr.weights is None:
+        terms = np.asarray(factors, dtype=np.float64)
+        k = _dyadic_scale(terms)
+        bound = float(deg.max(initial=0)) * float(terms.max()) * 2.0 ** k
+        return bound < 2.0 ** 53
+    w = np.asarray(csr.weights, dtype=np.float64)
+    if not np.all(np.isfinite(w)):
+        return False
+    terms = [w * f for f in factors]                     # fl(w * (1/p)): the reference's product
+    k = max(_dyadic_scale(t) for t in terms)
+    big = np.max(np.stack([np.abs(t) for t in terms]), axis=0) if w.size else w
+    nz = deg > 0
+    if not nz.any():
+        return True
+    row_tot = np.add.reduceat(big, row_ptr[:-1][nz]) if big.size else np.zeros(0)
+    return float(row_tot.max(initial=0.0)) * 2.0 ** k < 2.0 ** 53
+
+
 class RandomWalk(ABC):
     """RandomWalk method interface (random_walk_generator.py:11-53)."""
     METHOD = _native.DW_METHOD_DEEPWALK
@@ -76,12 +117,6 @@ class RandomWalk(ABC):
             raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
         if layout not in ('indexed', 'csr'):
             raise ValueError(f'unknown layout "{layout}" (expected "indexed" or "csr")')
-        if rng == 'python' and sys.version_info >= (3, 12):
-            # the replay kernel sums the normalising weights left to right as CPython <= 3.11's
-            # sum() does; 3.12+ sums floats with compensation, so the walks would not be the
-            # reference's bit for bit
-            raise NotImplementedError("rng='python' (bit-exact replay) needs CPython < 3.12; "
-                                      "use rng='philox'")
         self._layout = layout
         self._graph = graph
         self._length = length
@@ -90,6 +125,24 @@ class RandomWalk(ABC):
         self._device = device
         self._csr = _csr_of(graph)
         self._next_walk_id = 0
+        self._check_sum_semantics()
+
+    def _check_sum_semantics(self) -> None:
+        """rng='python' on CPython >= 3.12: ``sum()`` of floats is compensated there (Neumaier),
+        while the replay's serial fallback sums left to right as <= 3.11 does. The two agree
+        whenever every partial sum of a step's weights is exact (``sum_is_exact``), which covers
+        unweighted DeepWalk (int 1s), integer weights, and p, q whose reciprocals are short
+        binary fractions (the BASELINE configs' 1, 2, 4, 0.25, 0.5); anything else raises."""
+        if self._rng != 'python' or sys.version_info < (3, 12):
+            return
+        p, q = self._params()
+        if not sum_is_exact(self._csr, 1.0 / p, 1.0 / q,
+                            node2vec=self.METHOD == _native.DW_METHOD_NODE2VEC):
+            raise NotImplementedError(
+                "rng='python' (bit-exact replay) on CPython >= 3.12 needs step weights whose "
+                "sums are exact (integer weights, reciprocals of p and q with short binary "
+                "expansions): 3.12's compensated float sum() would round differently; use "
+                "rng='philox' or CPython < 3.12")
 
     # ---- reference host helpers (random_walk_generator.py:41-53) -----------------------
     @property
@@ -255,9 +308,9 @@ class Node2Vec(RandomWalk):
     METHOD = _native.DW_METHOD_NODE2VEC
 
     def __init__(self, graph, length: int, p: float = 1.0, q: float = 1.0, **kwargs):
-        super().__init__(graph=graph, length=length, **kwargs)
-        self._p = p
+        self._p = p      # set first: the base constructor's sum check reads them
         self._q = q
+        super().__init__(graph=graph, length=length, **kwargs)
 
     def _params(self):
         return self._p, self._q

@@ -43,9 +43,15 @@ class GraphedStep:
     overlapped on the side stream, or with ``overlap_in=False`` both tables' Adam in one launch),
     captured with the walker in front of it.
 
-    ``walker``: a Philox walker (rng='philox'); ``epoch_starts``: device int32 — walk w of the
-    epoch starts at epoch_starts[w mod len]; the step trains walks ``first_walk_id + k*B ..``.
-    ``n_steps``: how many replays the Adam-scalar history covers."""
+    ``walker``: a Philox walker (rng='philox'; the replay walker's host-drawn uniforms cannot be
+    captured); ``epoch_starts``: device int32 — walk w of the epoch starts at
+    epoch_starts[w mod len]; the step trains walks ``first_walk_id + k*B ..``.
+    ``n_steps``: how many training STEPS the Adam-scalar history covers (a replay runs
+    ``unroll`` steps); ``replay`` raises before it would run past them.
+
+    The walker's device tensors and the SGNS workspace are built before the capture (one
+    eager walker launch into a scratch buffer — walks are a pure function of the walk id, so
+    nothing is trained), and the walker's own walk-id counter is left where it was."""
 
     def __init__(self, tables: ShardedTables, walker, epoch_starts: torch.Tensor, B: int,
                  context_radius: int, neg_samples: int, *, seed: int, grad_scale: float,
@@ -58,6 +64,9 @@ class GraphedStep:
             raise ValueError('GraphedStep: epoch_starts must be int32 on the tables\' device')
         if unroll < 1:
             raise ValueError('GraphedStep: unroll must be >= 1')
+        if getattr(walker, '_rng', None) != 'philox':
+            raise ValueError("GraphedStep: the walker must be a Philox walker (rng='philox'); "
+                             "rng='python' draws its uniforms on the host")
         self.unroll = int(unroll)
         self.t, self.walker = tables, walker
         dev = tables.device
@@ -90,6 +99,21 @@ class GraphedStep:
                           fuse_out_adam=scatter == 'sorted')
         self.R, self.K = R, K
         self.graphs = {}
+        # Steps the scalar history covers: a graph whose first step is s needs rows s .. s+unroll
+        # (the block it leaves for the next graph included), k_step_expand flags the rest
+        self._hist_rows = int(hist.shape[0])
+        # One-time builds happen here, not inside the capture: the walker's device tensors
+        # (CSR, edges, adjacency hash, alias tables) via one eager launch into a scratch buffer,
+        # and the records workspace of this step shape
+        next_wid = walker._next_walk_id
+        n_warm = min(self.B, int(epoch_starts.numel()))
+        walker.walk_batch(epoch_starts[:n_warm], walk_id0=int(first_walk_id),
+                          out=torch.empty((n_warm, L), dtype=torch.int32, device=dev),
+                          check=False, status=torch.zeros(1, dtype=torch.int32, device=dev))
+        walker._next_walk_id = next_wid
+        from shallow_encoders.word2vec.sgns import _use_records, workspace_for
+        if scatter == 'sorted' and _use_records(scatter, 2 * R, K, tables.V):
+            workspace_for(self.centres, 2 * R, K, tables.V, dev)
         torch.cuda.synchronize(dev)
         # `unroll` consecutive steps per graph (one launch per `unroll` steps: at tiny batches
         # the gap between replays is as long as the step). One graph per parity of the in-table
@@ -108,6 +132,7 @@ class GraphedStep:
             self.graphs[parity] = g
         # the captures ran no step (host bookkeeping only; an even unroll ends on its parity)
         tables.step_count -= n_graphs * self.unroll
+        walker._next_walk_id = next_wid   # the captured walker launch moved it (walk_id0=0)
         torch.cuda.synchronize(dev)
 
     def _step_blk(self, k: int) -> int:
@@ -136,6 +161,9 @@ class GraphedStep:
         bookkeeping (Adam step count, current in-table buffer) follows as the eager steps'
         would."""
         t = self.t
+        if t.step_count + 1 + self.unroll >= self._hist_rows:
+            raise RuntimeError(f'GraphedStep: the Adam-scalar history covers steps up to '
+                               f'{self._hist_rows - 2}; build a new GraphedStep (n_steps) to go on')
         self.graphs[t._cur_in].replay()
         t.step_count += self.unroll
         if self._flips:

@@ -127,6 +127,52 @@ def test_factory_contract():
     assert w.get_node_normalized_edge_weights('b') == [0.5, 0.5]
 
 
+def _neumaier_sum(xs):
+    """CPython 3.12's float sum() (bltinmodule.c builtin_sum_impl, Neumaier compensation)."""
+    s, c = 0.0, 0.0
+    for x in xs:
+        x = float(x)
+        t = s + x
+        c += (s - t) + x if abs(s) >= abs(x) else (x - t) + s
+        s = t
+    return s + c if c else s
+
+
+def test_replay_on_312_raises_only_where_sums_can_differ(monkeypatch):
+    """rng='python' must not refuse the default walkers on CPython >= 3.12. The
+    walker raises there only when a step's weight sum could round (3.12 compensates float sums);
+    the accepted cases' sums are exact, so naive and compensated summation agree."""
+    import networkx as nx
+    from shallow_encoders.graph import random_walk_generator as rwg
+    g = nx.relabel_nodes(nx.karate_club_graph(), {i: f'n{i + 1:02d}' for i in range(34)})
+    gu = nx.Graph(list(g.edges()))                         # the same graph, unweighted
+    monkeypatch.setattr(rwg.sys, 'version_info', (3, 12, 0, 'final', 0))
+    DeepWalk(gu, 5)                                        # int 1s: always exact
+    DeepWalk(g, 5)                                         # integer weights 1-7
+    Node2Vec(gu, 5, p=0.25, q=4)                           # 1/p = 4, 1/q = 0.25
+    Node2Vec(g, 5, p=1, q=0.5)                             # the karate config
+    random_walk_factory('node2vec', gu, 5, {'p': 1, 'q': 1})
+    for bad in ({'p': 0.3, 'q': 3}, {'p': 1, 'q': 3}):
+        with pytest.raises(NotImplementedError):
+            random_walk_factory('node2vec', gu, 5, bad)
+    Node2Vec(gu, 5, p=0.3, q=3, rng='philox')              # Philox walkers never sum
+    gw = nx.Graph()
+    gw.add_edge('a', 'b', weight=0.1)
+    gw.add_edge('b', 'c', weight=0.2)
+    with pytest.raises(NotImplementedError):
+        DeepWalk(gw, 3)
+    monkeypatch.setattr(rwg.sys, 'version_info', (3, 10, 12, 'final', 0))
+    DeepWalk(gw, 3)                                        # <= 3.11: the serial replay is exact
+    # the rule's premise, checked against 3.12's summation: accepted weight sets sum alike
+    rng = np.random.default_rng(0)
+    for vals in ([1, 4.0, 0.25], [1, 2.0, 1.0], [1.0, 7.0, 3.5, 0.5]):
+        for _ in range(200):
+            xs = list(rng.choice(vals, size=int(rng.integers(1, 300))))
+            assert sum(xs) == _neumaier_sum(xs)
+    xs = [1.0, 1.0 / 0.3] * 50 + [1.0 / 3] * 7
+    assert sum(xs) != _neumaier_sum(xs)                    # a rejected set: they can differ
+
+
 # ------------------------------------------------------------------------------ collate
 @pytest.mark.parametrize('R', [1, 2, 5])
 def test_collate_matches_reference_rule(R):

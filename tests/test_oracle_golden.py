@@ -192,6 +192,36 @@ def test_closed_form_torch_and_windows_torch_equal_numpy_forms():
                                                                 rel=1e-5)
 
 
+def test_column_chunked_closed_form_equals_numpy_form():
+    """sgns_coefs_torch + sgns_grad_columns_torch (the C5 full-scale test's reference: tables
+    too large for a float64 copy) equal the numpy closed form, column slab by column slab,
+    with the in-table gradient compacted to the touched rows."""
+    import torch
+    f = golden('sgns_d256_k5_r5.npz')
+    R = int(f['R'])
+    ins_t, tgt_t = sgns_ref.sg_windows_torch(torch.as_tensor(f['walks']), R)
+    ins, tgt = sgns_ref.sg_windows(f['walks'], R)
+    l64, gi64, go64 = sgns_ref.sgns_grads_closed_form(f['w_in0'], f['w_out0'], ins, tgt,
+                                                      f['noise'][0])
+    w_in, w_out = torch.as_tensor(f['w_in0']), torch.as_tensor(f['w_out0'])
+    noise = torch.as_tensor(f['noise'][0])
+    sums, ds, dt, _ = sgns_ref.sgns_coefs_torch(w_in, w_out, ins_t, tgt_t, noise, chunk=5)
+    assert float(sums[0] + sums[1]) / tgt.size == pytest.approx(l64, rel=1e-12)
+    rows = torch.unique(ins_t)
+    index = torch.full((w_in.shape[0],), -1, dtype=torch.int64)
+    index[rows] = torch.arange(rows.numel())
+    d = w_in.shape[1]
+    for c0 in range(0, d, 96):
+        c1 = min(d, c0 + 96)
+        gi, go = sgns_ref.sgns_grad_columns_torch(w_in, w_out, ins_t, tgt_t, noise, ds, dt, c0,
+                                                  c1, index, rows.numel(), chunk=9)
+        np.testing.assert_allclose(gi.numpy(), gi64[rows.numpy(), c0:c1], rtol=1e-12,
+                                   atol=1e-18)
+        np.testing.assert_allclose(go.numpy(), go64[:, c0:c1], rtol=1e-12, atol=1e-18)
+    untouched = np.setdiff1d(np.arange(w_in.shape[0]), rows.numpy())
+    assert not gi64[untouched].any()
+
+
 def test_oracle_d128_trajectory_matches_reference():
     """24 reference Adam steps at d=128, K=5, R=5, lr 0.01 (traj_d128_k5_r5.npz): the oracle
     replays the losses and final tables, and the fixture's negatives are torch's global stream
