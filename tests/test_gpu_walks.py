@@ -46,6 +46,34 @@ def test_replay_kernel_bit_exact_vs_reference(name, hip_device):
     np.testing.assert_array_equal(out.cpu().numpy(), f['walks'])
 
 
+HUB_FIXTURES = [f'walks_{g}_hubs_{m}.npz' for g in ('rmat16', 'rmat20')
+                for m in ('deepwalk', 'node2vec_p0.25_q4', 'node2vec_p1_q1')]
+
+
+@pytest.mark.parametrize('name', HUB_FIXTURES)
+def test_replay_bit_exact_at_hubs_vs_reference(name, hip_device):
+    """walks the reference itself took from the top-degree nodes of R-MAT 16 and
+    R-MAT 20 (C3's graph: hubs of 44,848 and ~18,500 neighbours), replayed through the default
+    path (layout='indexed': DeepWalk over the edge-inline CSR, node2vec's exact picks; no
+    DW_REPLAY_SERIAL) — bit-exact. The graph is rebuilt on the device and pinned to the one the
+    reference walked by the SHA-256 of its CSR."""
+    import hashlib
+    import os
+    assert os.environ.get('DW_REPLAY_SERIAL', '0') != '1'
+    f = golden(name)
+    csr = rmat_graph(int(f['scale']), int(f['n_edges']), int(f['graph_seed']), device=hip_device)
+    assert hashlib.sha256(np.asarray(csr.row_ptr, dtype='<i8').tobytes()).hexdigest() == \
+        str(f['row_ptr_sha256'])
+    assert hashlib.sha256(np.asarray(csr.host_col(), dtype='<i4').tobytes()).hexdigest() == \
+        str(f['col_sha256'])
+    walker = _walker(f, csr, device=hip_device)
+    out = walker.walk_batch(torch.as_tensor(f['starts']), uniforms=f['uniforms'])
+    np.testing.assert_array_equal(out.cpu().numpy(), f['walks'])
+    deg = np.diff(np.asarray(csr.row_ptr))[f['walks'][:, :-1]]
+    if int(f['scale']) == 20:   # picks made in rows of >= 10K neighbours, bit-exact
+        assert int((deg >= 10_000).sum()) >= 25 and int(deg.max()) == 44_848
+
+
 @pytest.mark.parametrize('name,cls,kw', [
     ('walks_karate_node2vec_p1_q0.5.npz', KarateClubDataset,
      dict(method='node2vec', method_params={'p': 1, 'q': 0.5})),

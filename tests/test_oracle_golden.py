@@ -11,7 +11,9 @@ import pytest
 from conftest import GOLDEN, golden
 from oracle import sgns_ref, walk_ref
 
-WALK_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'walks_*.npz')))
+# (the hub fixtures store the graph's spec and digest instead of its CSR: tested below)
+WALK_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'walks_*.npz'))
+                       if '_hubs_' not in p)
 SGNS_FIXTURES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'sgns_*.npz')))
 
 
@@ -190,6 +192,24 @@ def test_closed_form_torch_and_windows_torch_equal_numpy_forms():
     np.testing.assert_allclose(go.numpy(), go64, rtol=1e-12, atol=1e-18)
     assert float(sums[0] + sums[1]) / tgt.size == pytest.approx(float(f['losses'][0][0]),
                                                                 rel=1e-5)
+
+
+@pytest.mark.parametrize('m', ['deepwalk', 'node2vec_p0.25_q4', 'node2vec_p1_q1'])
+def test_oracle_replays_reference_hub_walks_rmat16(m):
+    """The oracle walker against the reference's walks from R-MAT 16's top hubs (the graph
+    rebuilt on the host and pinned by its CSR digest; tests/golden/make_golden.py hubs)."""
+    import hashlib
+    from shallow_encoders.graph.rmat import rmat_graph
+    f = golden(f'walks_rmat16_hubs_{m}.npz')
+    csr = rmat_graph(int(f['scale']), int(f['n_edges']), int(f['graph_seed']))
+    assert hashlib.sha256(np.asarray(csr.row_ptr, dtype='<i8').tobytes()).hexdigest() == \
+        str(f['row_ptr_sha256'])
+    assert hashlib.sha256(np.asarray(csr.col, dtype='<i4').tobytes()).hexdigest() == \
+        str(f['col_sha256'])
+    g = walk_ref.CSR(csr.row_ptr, csr.col, None)
+    out = walk_ref.walks_replay(g, f['starts'], int(f['walk_length']), str(f['method']),
+                                float(f['p']), float(f['q']), f['uniforms'])
+    np.testing.assert_array_equal(out, f['walks'])
 
 
 def test_column_chunked_closed_form_equals_numpy_form():
