@@ -724,40 +724,56 @@ def main():
                                     'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                     'frac': gbs / HBM_PEAK_GBS, 'p': p, 'q': q}, **extra)
             del out
-        # the reference-exact walker (rng='python', dw_walk_replay): CPython's uniforms drawn on
-        # the host (8 B per step), fp64 choices arithmetic. Unweighted graphs take the exact
+        # the reference-exact walker (rng='python', dw_walk_replay): CPython's random.random()
+        # stream, generated in HBM from the global generator's state (dw_mt_uniforms; the state
+        # is handed back), fp64 choices arithmetic. Unweighted graphs take the exact
         # margin-checked picks (no serial sums; the serial replay only where the margin fails).
-        # walks_per_s: from the host uniforms (their H2D copy included); kernel_walks_per_s:
-        # uniforms already in HBM (HIP events around the launch)
+        # walks_per_s: end to end from the generator's state (stream generation, the walk, the
+        # state copied back, the status check); kernel_walks_per_s: the walk alone (uniforms
+        # already in HBM, HIP events); uniforms_ms: dw_mt_uniforms alone; walks_per_s_host_uniforms:
+        # the previous path (numpy draws on the host + their 8 B per step copied in)
         if rank == 0 and not dist_on:
             import random as _random
-            from shallow_encoders.graph.rng import draw_uniforms
+            from shallow_encoders.graph.rng import draw_uniforms, draw_uniforms_device
             for meth, p, q in walk_methods:
                 n_r = N if meth == 'deepwalk' else 65_536
                 w = (Node2Vec(csr, L, p=p, q=q, device=dev) if meth == 'node2vec'
                      else DeepWalk(csr, L, device=dev))
-                gen = _random.Random(0)
                 st = (torch.arange(n_r, dtype=torch.int32) % N) + 1   # node ids 1..N, cycled
-                w.walk_batch(st[:64], uniforms=draw_uniforms(64 * (L - 1), gen))
-                u = draw_uniforms(n_r * (L - 1), gen)
+                st_dev = st.to(dev)
                 out = torch.empty((n_r, L), dtype=torch.int32, device=dev)
+                _random.seed(0)
+                w.walk_batch(st_dev[:64])                              # warm-up (jump tables)
+                w.walk_batch(st_dev, out=out)
+                torch.cuda.synchronize(dev)
+                a = time.perf_counter()
+                w.walk_batch(st_dev, out=out)
+                torch.cuda.synchronize(dev)
+                dt = time.perf_counter() - a
+                u_dev = torch.empty(n_r * (L - 1), dtype=torch.float64, device=dev)
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                e[0].record()
+                draw_uniforms_device(u_dev.numel(), dev, out=u_dev, defer=True)[1]()
+                e[1].record()
+                e[2].record()
+                w.walk_batch(st_dev, uniforms=u_dev, out=out, check=False)
+                e[3].record()
+                torch.cuda.synchronize(dev)
+                gen_s = e[0].elapsed_time(e[1]) * 1e-3
+                kern_s = e[2].elapsed_time(e[3]) * 1e-3
+                gen = _random.Random(0)
+                u = draw_uniforms(n_r * (L - 1), gen)
                 torch.cuda.synchronize(dev)
                 a = time.perf_counter()
                 w.walk_batch(st, uniforms=u, out=out)
                 torch.cuda.synchronize(dev)
-                dt = time.perf_counter() - a
-                u_dev = torch.from_numpy(u).to(dev)
-                st_dev = st.to(dev)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                w.walk_batch(st_dev, uniforms=u_dev, out=out, check=False)
-                e1.record()
-                torch.cuda.synchronize(dev)
-                kern_s = e0.elapsed_time(e1) * 1e-3
+                dt_host = time.perf_counter() - a
                 replay_stats[meth] = {'walks': n_r, 'p': p, 'q': q, 'walks_per_s': n_r / dt,
                                       'kernel_walks_per_s': n_r / kern_s,
-                                      'kernel_ms': kern_s * 1e3}
-                del out, u_dev
+                                      'kernel_ms': kern_s * 1e3, 'uniforms_ms': gen_s * 1e3,
+                                      'uniforms_GBps': u_dev.numel() * 8 / gen_s / 1e9,
+                                      'walks_per_s_host_uniforms': n_r / dt_host}
+                del out, u_dev, u
 
     result = {
         'metric': 'positive-pairs/s + random-walks/s, 1M-node d=128 k=5, 1/2/4/8 MI355X',

@@ -22,8 +22,10 @@ BUILD = os.path.join(HERE, 'build')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('DW_OFFLOAD_ARCH', 'gfx950')
 
-SOURCES = ['dw_abi.cpp', 'dw_host.cpp', 'dw_graph.hip', 'dw_walk.hip', 'dw_sgns.hip', 'dw_adam.hip', 'dw_rmat.hip']
-EXTRA = {'dw_walk.hip': ['-ffp-contract=off']}
+SOURCES = ['dw_abi.cpp', 'dw_host.cpp', 'dw_mt_host.cpp', 'dw_graph.hip', 'dw_walk.hip',
+           'dw_sgns.hip', 'dw_adam.hip', 'dw_rmat.hip', 'dw_mt.hip']
+# dw_mt_host.cpp is host-only C++ (jump-ahead polynomials over GF(2), carry-less multiplies)
+EXTRA = {'dw_walk.hip': ['-ffp-contract=off'], 'dw_mt_host.cpp': ['-x', 'c++']}
 HEADERS = [os.path.join(HERE, 'dw_common.h'), os.path.join(REPO, 'include', 'dw_hip.h')]
 BASE_FLAGS = ['-x', 'hip', f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17',
               '-Wall', '-Wno-unused-function', '-I', os.path.join(REPO, 'include')]

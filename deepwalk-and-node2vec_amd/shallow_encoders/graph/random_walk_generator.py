@@ -4,9 +4,11 @@ Two sampling modes, one kernel family each (include/dw_hip.h):
 
 * ``rng='python'`` (default, reference-exact): every step consumes ONE double of CPython's
   global ``random`` stream, exactly as ``random.choices(..., k=1)`` does in the reference
-  (random_walk_generator.py:68,113). The doubles are drawn on the host (rng.draw_uniforms) and
-  the replay kernel ``dw_walk_replay`` reproduces CPython's fp64 arithmetic, so
-  ``random.seed(s)`` yields the reference's walks bit for bit.
+  (random_walk_generator.py:68,113). The doubles are generated in HBM from the generator's
+  state (rng.draw_uniforms_device: CPython's MT19937 on the device, dw_mt_uniforms; the state is
+  handed back so ``random`` continues exactly) and the replay kernel ``dw_walk_replay``
+  reproduces CPython's fp64 arithmetic, so ``random.seed(s)`` yields the reference's walks bit
+  for bit.
 * ``rng='philox'``: ``dw_walk_fast_indexed`` (DeepWalk over the edge-inline CSR, node2vec
   adjacency tests in a per-row hash; the default) or ``dw_walk_fast`` (plain CSR,
   ``layout='csr'``), Philox4x32-10
@@ -25,7 +27,7 @@ import torch
 
 from shallow_encoders import _native
 from shallow_encoders.graph.csr import CSRGraph
-from shallow_encoders.graph.rng import draw_uniforms
+from shallow_encoders.graph.rng import draw_uniforms_device
 
 _CSR_CACHE_ATTR = '_dw_csr_cache'
 
@@ -185,8 +187,9 @@ class RandomWalk(ABC):
                    status: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Walks from every start id (vocabulary ids) — int32 [n, length] on the device.
 
-        rng='python': the next n*(length-1) doubles of the global ``random`` stream are used
-        (or ``uniforms`` when given, shape [n, length-1]). rng='philox': walk ``k`` of this
+        rng='python': the next n*(length-1) doubles of the global ``random`` stream are used,
+        generated on the device (or ``uniforms`` when given, shape [n, length-1]; host or
+        device). rng='philox': walk ``k`` of this
         call has global walk id ``walk_id0 + k`` (default: continues the previous call).
         ``check=False`` skips the synchronising status check (stream stays asynchronous);
         ``status``: the caller's int32 status word to OR conditions into (default: a new one).
@@ -216,9 +219,10 @@ class RandomWalk(ABC):
         p, q = self._params()
         with torch.cuda.device(dev):
             s = _native.stream(dev)
+            commit = None
             if self._rng == 'python':
-                if uniforms is None:
-                    uniforms = draw_uniforms(n * (L - 1))
+                if uniforms is None:   # the global stream, made in HBM; committed after launch
+                    uniforms, commit = draw_uniforms_device(n * (L - 1), dev, defer=True)
                 if isinstance(uniforms, torch.Tensor):   # e.g. already resident on the device
                     u = uniforms.reshape(-1).to(device=dev, dtype=torch.float64).contiguous()
                 else:
@@ -240,6 +244,8 @@ class RandomWalk(ABC):
                                  _native.ptr(starts), n, L, self.METHOD, float(p), float(q),
                                  _native.ptr(u) if u.numel() else None, _native.ptr(out),
                                  _native.ptr(status), s)
+                if commit is not None:
+                    commit()
             else:
                 wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
                 if indexed:

@@ -66,6 +66,31 @@ int dw_device_sync(void *stream);       /* hipStreamSynchronize(stream); used by
  * Python's shuffle would; perm: int64[n] out. */
 int dw_host_shuffle(uint32_t *mt_state, int64_t *perm, int64_t n);
 
+/* ---- the reference's uniform stream on the device ------------------------------------------
+ * CPython's random.random() (Modules/_randommodule.c: MT19937 + genrand_res53), the one draw per
+ * walk step of random_walk_generator.py:68,113 (random.choices(..., k=1)); replaces the host
+ * draw + H2D copy in front of dw_walk_replay(_inline). Replaces, in the reference,
+ * `random.random()` called n times on the global generator (datasets.py:87-91 -> walk()).
+ *
+ * dw_mt_jump_table (HOST, no device work): jump-ahead polynomials for dw_mt_uniforms. Chain c
+ * (c >= 1) of a call starts at raw word 624*window_stride*c of the generator's sequence; its
+ * entry lists the exponents l (ascending) of t^(624*window_stride*c - 2) mod phi(t), phi =
+ * MT19937's characteristic polynomial (degree 19937, 135 terms). offsets: int64[n_chains+1]
+ * (chain c's exponents are positions[offsets[c] .. offsets[c+1])); positions: uint16[capacity]
+ * (n_chains * 19937 always suffices; DW_E_INVALID_ARG when too small). Host buffers.
+ *
+ * dw_mt_uniforms: out[k] = the (k+1)-th random.random() of the generator whose state is
+ * (mt[0..623], index) — random.getstate()[1] — for k < n; state_out (625 words: array + index)
+ * receives the state after the n draws, for random.setstate. mt, out, state_out, jump_pos,
+ * jump_off: DEVICE buffers (jump_*: a dw_mt_jump_table of the same window_stride with at least
+ * ceil(windows / window_stride) chains, windows = (index + 2n - 1) / 624 + 1; may be NULL when
+ * that is one chain). One workgroup per chain; stream-ordered. */
+int dw_mt_jump_table(int64_t window_stride, int64_t n_chains, int64_t *offsets,
+                     uint16_t *positions, int64_t capacity);
+int dw_mt_uniforms(const uint32_t *mt, int32_t index, int64_t n, double *out,
+                   uint32_t *state_out, int64_t window_stride, const uint16_t *jump_pos,
+                   const int64_t *jump_off, int64_t n_chains_table, void *stream);
+
 /* ---- graph ------------------------------------------------------------------------------- */
 
 /* Validate a CSR on the device: row_ptr[0]==0, monotone, row_ptr[n_rows]==nnz, 0<=col<n_rows.

@@ -402,3 +402,84 @@ def test_step_scalars_layout_and_history():
     for s in range(1, 6):
         exp = [ctypes.c_float(x).value for x in adam_scalars(s, 0.01, (0.9, 0.999), 1e-8, 0.0)]
         assert h[s, :7].tolist() == exp and h[s, 7] == 0.0
+
+
+# ------------------------------------------------------------------------------ MT19937 stream
+def _py_state(seed, skip):
+    r = random.Random(seed)
+    for _ in range(skip):
+        r.random()
+    st = r.getstate()[1]
+    return r, list(st[:624]), st[624]
+
+
+@pytest.mark.parametrize('seed,skip', [(0, 0), (7, 1), (11, 311), (13, 312), (5, 1000)])
+def test_mt_oracle_stream_is_cpython_random(seed, skip):
+    """oracle/mt_ref.py's raw-sequence restatement gives random.random() and the state after."""
+    from oracle import mt_ref
+    r, mt, idx = _py_state(seed, skip)
+    n = 2000
+    out, arr, index = mt_ref.stream(mt, idx, n)
+    exp = np.array([r.random() for _ in range(n)])
+    np.testing.assert_array_equal(out, exp)
+    st = r.getstate()[1]
+    assert list(arr) == list(st[:624]) and index == st[624]
+
+
+def test_mt_characteristic_polynomial_annihilates_the_stream():
+    """phi (135 terms, degree 19937) kills every bit plane of the raw sequence, so t^J mod phi
+    gives the jump (Cayley-Hamilton on the 19937-bit state)."""
+    from oracle import mt_ref
+    _, mt, _ = _py_state(3, 17)
+    x = mt_ref.raw_sequence(mt, 60_000)
+    assert len(mt_ref.PHI_TERMS) == 134
+    assert mt_ref.annihilates(x, range(0, 60_000 - 19_938, 997))
+    assert not mt_ref.annihilates(x ^ np.uint32(1) * (np.arange(x.size) == 20_000), [20_000])
+
+
+def test_mt_jump_table_matches_restatement_and_jumps():
+    """dw_mt_jump_table (host C ABI) = the exponents of t^(624 S c - 2) mod phi computed in
+    Python; applied to the raw sequence they give x[J + 1 .. J + 625]."""
+    from oracle import mt_ref
+    from shallow_encoders import _native
+    _native.load()
+    _, mt, _ = _py_state(21, 5)
+    for stride, chains in ((1, 5), (3, 3), (256, 3)):
+        off = np.zeros(chains + 1, dtype=np.int64)
+        pos = np.zeros(chains * 19937, dtype=np.uint16)
+        _native.call('dw_mt_jump_table', stride, chains, off.ctypes.data, pos.ctypes.data,
+                     pos.size)
+        assert off[0] == off[1] == 0
+        x = mt_ref.raw_sequence(mt, 624 * stride * chains + 20_600)
+        base = x[:19937 + 626]
+        for c in range(1, chains):
+            J = 624 * stride * c - 2
+            ls = pos[off[c]:off[c + 1]].astype(np.int64)
+            if stride == 256 and c == 1:
+                np.testing.assert_array_equal(ls, mt_ref.exponents(mt_ref.t_pow_mod(J)))
+            got = mt_ref.jump(base, ls, np.arange(1, 626))
+            np.testing.assert_array_equal(got, x[J + 1:J + 626])
+    with pytest.raises(_native.DWError):
+        _native.call('dw_mt_jump_table', 256, 3, off.ctypes.data, pos.ctypes.data, 100)
+
+
+@pytest.mark.parametrize('stride,seed,skip,n', [(1, 1, 0, 1500), (1, 2, 1, 1500),
+                                                (2, 3, 311, 4001), (3, 4, 312, 2),
+                                                (1, 5, 623, 937)])
+def test_mt_chained_generation_is_cpython_random(stride, seed, skip, n):
+    """dw_mt_uniforms' decomposition (chains of `stride` windows seeded by the product's jump
+    table; doubles whose words straddle windows and chains; the final state) restated in numpy,
+    against CPython — odd and even start indices, a draw from the state's last word."""
+    from oracle import mt_ref
+    from shallow_encoders import _native
+    _native.load()
+    r, mt, idx = _py_state(seed, skip)
+    windows = (idx + 2 * n - 1) // 624 + 1
+    chains = -(-windows // stride)
+    off = np.zeros(chains + 1, dtype=np.int64)
+    pos = np.zeros(chains * 19937, dtype=np.uint16)
+    _native.call('dw_mt_jump_table', stride, chains, off.ctypes.data, pos.ctypes.data, pos.size)
+    out, arr, index = mt_ref.uniforms_chained(mt, idx, n, stride, pos, off)
+    np.testing.assert_array_equal(out, np.array([r.random() for _ in range(n)]))
+    st = r.getstate()[1]
+    assert list(arr) == list(st[:624]) and index == st[624]
