@@ -28,8 +28,9 @@ constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_D = MT_N - MT_M;   // 227: words per dependent phase
 constexpr uint32_t MATRIX_A = 0x9908b0dfu, UPPER = 0x80000000u, LOWER = 0x7fffffffu;
-constexpr int MT_THREADS = 640;
+constexpr int MT_THREADS = 320;   // the chain loop: 227-word phases, 312 doubles; the jump: 2 words
 constexpr int BASE_WORDS = 19937 + 625;   // x[0 .. 20562): every x[l + j] a jump reads
+constexpr int MAX_POS = 19937 + 7;        // a jump's exponents (< 19937), padded to 8
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b, uint32_t m) {
     const uint32_t y = (a & UPPER) | (b & LOWER);
@@ -57,6 +58,7 @@ __global__ void __launch_bounds__(MT_THREADS)
                 const int64_t *__restrict__ joff) {
     __shared__ uint32_t base[BASE_WORDS];
     __shared__ uint32_t win[2][MT_N];
+    __shared__ __attribute__((aligned(16))) uint16_t pos[MAX_POS + 1];   // this chain's exponents
     __shared__ uint32_t carry;   // x[624 w0 - 1]: the first word of a double straddling chains
     const int t = threadIdx.x;
     const int64_t c = blockIdx.x;
@@ -73,7 +75,12 @@ __global__ void __launch_bounds__(MT_THREADS)
         for (int k = t; k < MT_N; k += MT_THREADS) win[0][k] = mt_in[k];
         if (t == 0) carry = 0;
     } else {
+        // the jump's exponents into LDS (read back as broadcasts, 8 per 16-B read), then
         // x[0 .. BASE_WORDS) from the state, window by window in three dependent phases
+        const int64_t e0 = joff[c];
+        const int cnt = static_cast<int>(joff[c + 1] - e0);
+        for (int k = t; k < cnt; k += MT_THREADS) pos[k] = jpos[e0 + k];
+        for (int k = cnt + t; k < ((cnt + 7) & ~7); k += MT_THREADS) pos[k] = 0;
         for (int k = t; k < MT_N; k += MT_THREADS) base[k] = mt_in[k];
         __syncthreads();
         for (int w = 1; MT_N * w < BASE_WORDS; ++w) {
@@ -85,22 +92,51 @@ __global__ void __launch_bounds__(MT_THREADS)
                 __syncthreads();
             }
         }
-        // the jump: thread t computes x[J + t + 1], J = 624 S c - 2
-        uint32_t acc = 0;
-        if (t <= MT_N) {
-            const int64_t e0 = joff[c], e1 = joff[c + 1];
-            int64_t e = e0;
-            for (; e + 8 <= e1; e += 8) {   // eight independent LDS reads in flight
-                uint32_t r[8];
+        // the jump: thread t computes x[J + j] for j = t + 1 and t + 321 (<= 625),
+        // J = 624 S c - 2. 32 exponents per trip (four 16-B broadcast reads, the next trip's
+        // fetched before this trip's 64 word reads are consumed), so the LDS pipe stays busy at
+        // 1.25 waves per SIMD
+        const uint32_t *b0 = base + t + 1;
+        const uint32_t *b1 = base + (t + MT_THREADS < MT_N + 1 ? t + MT_THREADS + 1 : t + 1);
+        uint32_t acc0 = 0, acc1 = 0;
+        int e = 0;
+        constexpr int TRIP = 32;
+        uint4 pk[TRIP / 8];
+        if (cnt >= TRIP) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) r[u] = base[jpos[e + u] + t + 1];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc ^= r[u];
-            }
-            for (; e < e1; ++e) acc ^= base[jpos[e] + t + 1];
+            for (int q = 0; q < TRIP / 8; ++q) pk[q] = *reinterpret_cast<const uint4 *>(pos + 8 * q);
         }
-        if (t == 0) carry = acc;
-        else if (t <= MT_N) win[0][t - 1] = acc;
+        for (; e + TRIP <= cnt; e += TRIP) {
+            uint32_t r0[TRIP], r1[TRIP];
+#pragma unroll
+            for (int q = 0; q < TRIP / 8; ++q) {
+                const uint32_t l[8] = {pk[q].x & 0xFFFFu, pk[q].x >> 16, pk[q].y & 0xFFFFu,
+                                       pk[q].y >> 16,     pk[q].z & 0xFFFFu, pk[q].z >> 16,
+                                       pk[q].w & 0xFFFFu, pk[q].w >> 16};
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    r0[8 * q + u] = b0[l[u]];
+                    r1[8 * q + u] = b1[l[u]];
+                }
+            }
+            if (e + 2 * TRIP <= cnt) {
+#pragma unroll
+                for (int q = 0; q < TRIP / 8; ++q)
+                    pk[q] = *reinterpret_cast<const uint4 *>(pos + e + TRIP + 8 * q);
+            }
+#pragma unroll
+            for (int u = 0; u < TRIP; ++u) {
+                acc0 ^= r0[u];
+                acc1 ^= r1[u];
+            }
+        }
+        for (; e < cnt; ++e) {
+            acc0 ^= b0[pos[e]];
+            acc1 ^= b1[pos[e]];
+        }
+        if (t == 0) carry = acc0;
+        else win[0][t - 1] = acc0;
+        if (t + MT_THREADS < MT_N + 1) win[0][t + MT_THREADS - 1] = acc1;
     }
     __syncthreads();
     const int64_t first = index, last = index + 2 * n - 1;   // the stream's absolute words
