@@ -144,6 +144,41 @@ __global__ void k_adj_insert(const int64_t *__restrict__ row_ptr, const int32_t 
     }
 }
 
+// adj_hpos[slot] = the index of the slot's key in its row's insertion order (networkx
+// neighbour order): the bit-exact node2vec replay maps a neighbour of prev to its position in
+// N(v) with one probe (dw_walk_replay's "probe the shorter list" step).
+__global__ void k_adj_positions(const int64_t *__restrict__ row_ptr,
+                                const int32_t *__restrict__ col, int64_t n_rows,
+                                const int64_t *__restrict__ adj_off,
+                                const int32_t *__restrict__ tab, int32_t *__restrict__ hpos,
+                                int32_t *status) {
+    const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + threadIdx.x / 64; r < n_rows;
+         r += stride) {
+        const int64_t off = adj_off[r];
+        const uint32_t nb = static_cast<uint32_t>((adj_off[r + 1] - off) / 16);
+        if (nb == 0) continue;
+        const int64_t a = row_ptr[r], b = row_ptr[r + 1];
+        for (int64_t e = a + lane; e < b; e += 64) {
+            const int32_t x = col[e];
+            uint32_t bk = dw::adj_bucket(x, nb);
+            bool done = false;
+            for (uint32_t t = 0; t < nb && !done; ++t) {
+                const int64_t s0 = off + (int64_t)bk * 16;
+                for (int j = 0; j < 16; ++j)
+                    if (tab[s0 + j] == x) {
+                        hpos[s0 + j] = static_cast<int32_t>(e - a);
+                        done = true;
+                        break;
+                    }
+                if (++bk == nb) bk = 0;
+            }
+            if (!done) dw::status_or(status, DW_S_BAD_CSR);
+        }
+    }
+}
+
 inline int grid_for(int64_t work, int block, int cap = 8192) {
     int64_t g = (work + block - 1) / block;
     if (g < 1) g = 1;
@@ -243,6 +278,26 @@ int dw_adj_hash_offsets(const int64_t *row_ptr, int64_t n_rows, int64_t *adj_off
         dw::set_error("dw_adj_hash_offsets: hipcub scan: %s", hipGetErrorString(e));
         return DW_E_HIP;
     }
+    return DW_OK;
+}
+
+int dw_adj_hash_positions(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                          const int64_t *adj_off, const int32_t *adj_hash, int64_t n_slots,
+                          int32_t *adj_hpos, int32_t *status, void *stream) {
+    DW_REQUIRE(n_rows >= 0 && n_slots >= 0, "dw_adj_hash_positions: negative size");
+    DW_REQUIRE(row_ptr && adj_off && status, "dw_adj_hash_positions: null pointer");
+    if (n_slots == 0) return DW_OK;
+    DW_REQUIRE(col && adj_hash && adj_hpos, "dw_adj_hash_positions: null pointer");
+    hipError_t e = hipMemsetAsync(adj_hpos, 0xFF, (size_t)n_slots * sizeof(int32_t),
+                                  dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_adj_hash_positions: memset: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    hipLaunchKernelGGL(k_adj_positions, dim3(grid_for(n_rows * 64, 256)), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, col, n_rows, adj_off, adj_hash, adj_hpos,
+                       status);
+    DW_LAUNCH_CHECK("dw_adj_hash_positions");
     return DW_OK;
 }
 

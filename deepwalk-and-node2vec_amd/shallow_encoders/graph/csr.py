@@ -189,9 +189,10 @@ class CSRGraph:
     # ------------------------------------------------------------------ device side
     def device_tensors(self, device=None, need_sorted: bool = False,
                        need_alias: bool = False, need_edges: bool = False,
-                       need_adj: bool = False) -> Dict[str, torch.Tensor]:
+                       need_adj: bool = False,
+                       need_adj_pos: bool = False) -> Dict[str, torch.Tensor]:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
-        the per-row adjacency hash on the device)."""
+        the per-row adjacency hash / its slots' neighbour positions on the device)."""
         dev = _native.require_device(device)
         if self._dev_device != dev:
             if self.col is None and 'col' in self._dev:   # device-built: keep a host copy
@@ -216,8 +217,19 @@ class CSRGraph:
             self._build_alias(dev)
         if need_edges and 'edges' not in d:
             self._build_edges(dev)
-        if need_adj and 'adj_off' not in d:
+        if (need_adj or need_adj_pos) and 'adj_off' not in d:
             self._build_adj_hash(dev)
+        if need_adj_pos and 'adj_hpos' not in d:
+            n_slots = d['adj_hash'].numel()
+            hp = torch.empty(n_slots, dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                _native.call('dw_adj_hash_positions', _native.ptr(d['row_ptr']),
+                             _native.ptr(d['col']) if self.nnz else None, self.vocab_size,
+                             _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                             int(d['adj_off'][self.vocab_size]), _native.ptr(hp),
+                             _native.ptr(d['status']), _native.stream(dev))
+            _native.check_status(d['status'], 'adjacency positions build')
+            d['adj_hpos'] = hp
         return d
 
     def _build_edges(self, dev) -> None:

@@ -208,10 +208,14 @@ class RandomWalk(ABC):
         # (dw_walk_replay_inline; layout='csr' keeps dw_walk_replay)
         replay_inline = (self._rng == 'python' and not n2v and self._layout == 'indexed'
                          and self._csr.weights is None)
+        # replay, node2vec on an unweighted graph: the adjacency-hash replay (dw_walk_replay_
+        # indexed: the shorter list of each step probed; the same walks as dw_walk_replay)
+        replay_n2v_idx = (self._rng == 'python' and n2v and self._layout == 'indexed'
+                          and self._csr.weights is None)
         d = self._csr.device_tensors(dev, need_sorted=n2v and not indexed,
                                      need_alias=self._rng == 'philox',
                                      need_edges=(indexed and not n2v) or replay_inline,
-                                     need_adj=indexed and n2v)
+                                     need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         if status is None:
@@ -237,6 +241,14 @@ class RandomWalk(ABC):
                                  _native.ptr(starts), n, L,
                                  _native.ptr(u) if u.numel() else None, _native.ptr(out),
                                  _native.ptr(status), s)
+                elif replay_n2v_idx:
+                    _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
+                                 _native.ptr(d['col']), _native.ptr(d['col_sorted']),
+                                 _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                                 _native.ptr(d['adj_hpos']), self._csr.vocab_size,
+                                 _native.ptr(starts), n, L, float(p), float(q),
+                                 _native.ptr(u) if u.numel() else None, _native.ptr(out),
+                                 _native.ptr(status), None, s)
                 else:
                     _native.call('dw_walk_replay', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d.get('col_sorted')),
@@ -268,6 +280,38 @@ class RandomWalk(ABC):
         if check:
             _native.check_status(status, f'{type(self).__name__}.walk')
         return out
+
+    def count_replay_traffic(self, start_ids: torch.Tensor, uniforms: torch.Tensor,
+                             out: Optional[torch.Tensor] = None) -> dict:
+        """node2vec, rng='python', unweighted: the same walks as ``walk_batch(start_ids,
+        uniforms)`` with the replay walker's realised traffic counted (dw_walk_replay_indexed
+        with counters; a diagnostic launch): {'bytes', 'probes', 'entries', 'steps'}."""
+        if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'python' \
+                or self._csr.weights is not None:
+            raise ValueError('count_replay_traffic: node2vec with rng="python", unweighted')
+        dev = _native.require_device(self._device)
+        starts = torch.as_tensor(start_ids, dtype=torch.int32).to(dev).contiguous()
+        n, L = int(starts.numel()), self._length
+        u = torch.as_tensor(uniforms).reshape(-1).to(device=dev, dtype=torch.float64).contiguous()
+        if u.numel() != n * (L - 1):
+            raise ValueError('uniforms must have n_walks * (length - 1) values')
+        d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True)
+        if out is None:
+            out = torch.empty((n, L), dtype=torch.int32, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        p, q = self._params()
+        with torch.cuda.device(dev):
+            _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
+                         _native.ptr(d['col']), _native.ptr(d['col_sorted']),
+                         _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                         _native.ptr(d['adj_hpos']), self._csr.vocab_size, _native.ptr(starts),
+                         n, L, float(p), float(q), _native.ptr(u) if u.numel() else None,
+                         _native.ptr(out), _native.ptr(status), _native.ptr(counters),
+                         _native.stream(dev))
+        _native.check_status(status, f'{type(self).__name__}.count_replay_traffic')
+        c = counters.cpu().tolist()
+        return {'bytes': c[0], 'probes': c[1], 'entries': c[2], 'steps': c[3]}
 
     def count_traffic(self, start_ids: torch.Tensor, walk_id0: int,
                       out: Optional[torch.Tensor] = None) -> dict:

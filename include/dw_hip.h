@@ -117,6 +117,12 @@ int dw_adj_hash_offsets(const int64_t *row_ptr, int64_t n_rows, int64_t *adj_off
 int dw_adj_hash_build(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
                       const int64_t *adj_off, int64_t n_slots, int32_t *adj_hash, int32_t *status,
                       void *stream);
+/* adj_hpos int32[n_slots]: for every filled slot of adj_hash, the index of its key in the row's
+ * neighbour order (-1 for free slots) — the bit-exact node2vec replay's position lookups
+ * (dw_walk_replay_indexed). After dw_adj_hash_build. */
+int dw_adj_hash_positions(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                          const int64_t *adj_off, const int32_t *adj_hash, int64_t n_slots,
+                          int32_t *adj_hpos, int32_t *status, void *stream);
 
 /* Per-row Vose alias tables for first-order weighted sampling (the fast-mode replacement of
  * get_node_normalized_edge_weights + random.choices, random_walk_generator.py:50-53,68).
@@ -178,6 +184,20 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
 int dw_walk_replay_inline(const int64_t *row_ptr, const int32_t *edges, int64_t n_rows,
                           const int32_t *starts, int64_t n_walks, int32_t walk_length,
                           const double *uniforms, int32_t *out, int32_t *status, void *stream);
+
+/* dw_walk_replay for node2vec on an unweighted graph, over the per-row adjacency hash: the same
+ * walks bit for bit. At a step t -> v it probes the shorter of the two lists — N(v)'s classes
+ * from t's hash (adj_off / adj_hash), or N(t)'s members' positions in N(v) from v's hash and
+ * adj_hpos (dw_adj_hash_positions) — then the exact picks' margin rule, with the serial
+ * arithmetic (over col_sorted) where it cannot decide. counters: NULL, or uint64[4]
+ * (caller-zeroed) += {bytes, hash probes, list entries read, steps} — the realised traffic for
+ * the walk roofline (bench.py). Replaces random_walk_generator.py:94-119 on unweighted graphs. */
+int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
+                           const int64_t *adj_off, const int32_t *adj_hash,
+                           const int32_t *adj_hpos, int64_t n_rows, const int32_t *starts,
+                           int64_t n_walks, int32_t walk_length, double p, double q,
+                           const double *uniforms, int32_t *out, int32_t *status,
+                           uint64_t *counters, void *stream);
 
 /* Fast walker (Philox4x32-10 keyed by (seed, walk_id0 + w, step, round/lane)); walks are a pure
  * function of (seed, global walk id), identical for any grid and any number of GPUs.

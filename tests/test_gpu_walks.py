@@ -393,3 +393,29 @@ def test_replay_exact_picks_equal_serial_replay(method, p, q, n_walks, L, hip_de
     serial = mk().walk_batch(starts, uniforms=u).cpu().numpy()
     np.testing.assert_array_equal(fast, serial)
     assert (fast > 0).all() and int(deg[starts.numpy()].max()) > 2048   # hub rows past LDS
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0), (0.3, 3.0), (2.0, 0.5)])
+def test_indexed_node2vec_replay_equals_csr_replay_c3(p, q, hip_device):
+    """dw_walk_replay_indexed (default for node2vec, rng='python': the shorter list of each step
+    probed through the adjacency hash and its position table) gives bit for bit the walks of
+    dw_walk_replay (layout='csr': every neighbour of v classified against sorted N(prev)) on C3's
+    graph, from its top hubs and from random nodes; the counted launch gives the same walks."""
+    csr = rmat_graph(20, 10_000_000, 0, device=hip_device)
+    deg = csr.degree()
+    rng = np.random.default_rng(11)
+    hubs = np.argsort(-deg[1:])[:256] + 1
+    starts = np.concatenate([np.resize(hubs, 2048), rng.integers(1, csr.vocab_size, 2048)])
+    starts = torch.as_tensor(starts.astype(np.int32))
+    L = 24
+    u = torch.from_numpy(rng.random((starts.numel(), L - 1))).to(hip_device)
+    idx = Node2Vec(csr, L, p=p, q=q, device=hip_device)
+    got = idx.walk_batch(starts, uniforms=u).cpu().numpy()
+    ref = Node2Vec(csr, L, p=p, q=q, layout='csr', device=hip_device).walk_batch(
+        starts, uniforms=u).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+    out = torch.empty((starts.numel(), L), dtype=torch.int32, device=hip_device)
+    c = idx.count_replay_traffic(starts, u, out=out)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    assert c['steps'] == starts.numel() * (L - 1)
+    assert c['bytes'] >= c['steps'] * 48 + c['probes'] * 64
