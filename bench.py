@@ -47,6 +47,28 @@ CONFIGS = {
 }
 
 
+def measured_copy_gbs(dev, nbytes: int = 2 << 30, reps: int = 5) -> float:
+    """STREAM copy on this GPU (dw_stream_copy, float4 lanes): bytes read + written per second,
+    best of `reps` — the measured HBM roofline reported beside the 8 TB/s spec figure."""
+    from shallow_encoders import _native
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    best = None
+    with torch.cuda.device(dev):
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _native.call('dw_stream_copy', _native.ptr(src), _native.ptr(dst), nbytes,
+                         _native.stream(dev))
+            e1.record()
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (best * 1e-3) / 1e9
+
+
 def sgns_bytes_per_pair(d: int, K: int, R: int) -> float:
     """Algorithmic HBM bytes per positive pair: every gathered fp32 row read
     once and its gradient written once; int64 ids. 6,295 B at d=128, K=5, R=5."""
@@ -283,6 +305,7 @@ def main():
                                                     overlap_adam_blocks, replicated_step)
     _native.require_device(dev)
 
+    copy_gbs = measured_copy_gbs(dev)   # before the tables take the memory
     t0 = time.time()
     csr = rmat_graph(args.scale, args.edges, 0, device=dev)   # built in HBM (dw_rmat_edges)
     V = csr.vocab_size
@@ -837,6 +860,7 @@ def main():
                        if args.scatter == 'sorted' else 'dw_sgns_walks (k_sgns, atomic scatter)'),
             'bound': 'hbm', 'achieved': sgns_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': sgns_gbs / HBM_PEAK_GBS, 'traffic': None,
+            'measured_copy_GBps': copy_gbs, 'frac_of_measured': sgns_gbs / copy_gbs,
             'bytes_per_pair': bpp, 'pairs_per_launch': pairs_per_step,
             'out_table_adam_bytes': out_adam_bytes, 'in_table_adam_bytes': in_adam_bytes,
             'in_table_adam_blocks': (overlap_adam_blocks(V * d * 4 * 7, p2_bytes)

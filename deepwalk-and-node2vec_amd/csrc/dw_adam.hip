@@ -178,7 +178,44 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
+// STREAM copy (the "measured HBM roofline" of SURVEY.md §8d / BASELINE.md): dst = src in 16-B
+// lanes, four loads in flight per lane before the stores; bench.py times it once per run and
+// reports the SGNS step against it beside the 8 TB/s spec figure.
+__global__ void __launch_bounds__(256)
+    k_stream_copy(const float4 *__restrict__ src, float4 *__restrict__ dst, int64_t n4) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
+                     d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n4; i += stride) dst[i] = src[i];
+}
+
 extern "C" {
+
+int dw_stream_copy(const void *src, void *dst, int64_t bytes, void *stream) {
+    DW_REQUIRE(bytes >= 0 && bytes % 16 == 0, "dw_stream_copy: bytes must be a multiple of 16");
+    if (bytes == 0) return DW_OK;
+    DW_REQUIRE(src && dst, "dw_stream_copy: null pointer");
+    DW_REQUIRE((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16 == 0,
+               "dw_stream_copy: buffers must be 16-B aligned");
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n_cu = 256;
+    const int64_t n4 = bytes / 16;
+    int64_t blocks = (int64_t)n_cu * 8;
+    if (blocks * 256 > n4) blocks = (n4 + 255) / 256;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       reinterpret_cast<const float4 *>(src), reinterpret_cast<float4 *>(dst), n4);
+    DW_LAUNCH_CHECK("dw_stream_copy");
+    return DW_OK;
+}
 
 int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, float *exp_avg,
                      float *exp_avg_sq, int64_t n_elem, float one_minus_beta1, float beta2,

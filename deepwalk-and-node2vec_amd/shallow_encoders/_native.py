@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -49,6 +49,7 @@ SIGNATURES = {
     'dw_last_error_string': (ctypes.c_char_p, []),
     'dw_abi_version': (ctypes.c_int, []),
     'dw_device_sync': (ctypes.c_int, [_p]),
+    'dw_stream_copy': (ctypes.c_int, [_p, _p, _i64, _p]),
     'dw_host_shuffle': (ctypes.c_int, [_p, _p, _i64]),
     'dw_mt_jump_table': (ctypes.c_int, [_i64, _i64, _p, _p, _i64]),
     'dw_mt_uniforms': (ctypes.c_int, [_p, _i32, _i64, _p, _p, _i64, _p, _p, _i64, _p]),

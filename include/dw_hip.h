@@ -59,6 +59,9 @@ extern "C" {
 const char *dw_last_error_string(void);
 int dw_abi_version(void);               /* bumps on any signature change */
 int dw_device_sync(void *stream);       /* hipStreamSynchronize(stream); used by the host mirror */
+/* dst = src, bytes a multiple of 16 (16-B aligned device buffers): a STREAM-copy kernel, the
+ * measured HBM roofline bench.py reports beside the spec peak. */
+int dw_stream_copy(const void *src, void *dst, int64_t bytes, void *stream);
 
 /* Host-side (no device work): CPython 3.10 random.shuffle over range(n), bit for bit — the
  * reference's start-node shuffle (datasets.py:45,86-88) in native code. mt_state: the 625 words
