@@ -528,6 +528,8 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // one 64-B bucket load instead of a binary search.
 constexpr int RN_WAVES = 2;
 constexpr int RN_CAP = 2048;   // LDS words per wave: 512 rounds of class ballots (A) / positions (B)
+constexpr int RN_STAGE = 1024; // (A) with N(t) this short: staged sorted in LDS, LDS searches
+constexpr int RN_MASKW = 64;   // (A) staged: words of ballots ahead of the staged list (16 rounds)
 
 struct AdjRow {       // a row's CSR range and adjacency-hash buckets
     int64_t a, n, h;
@@ -592,12 +594,13 @@ __device__ __forceinline__ double n2v_w(int64_t na, int64_t nb, int64_t nc, doub
     return static_cast<double>(na) * ip + static_cast<double>(nb) + static_cast<double>(nc) * iq;
 }
 
-// (A): classify N(v) against t's hash. masks: 2 u64 per round, cap rounds in LDS.
+// (A): classify N(v) against N(t): t's sorted list staged in LDS (nt_lds, m <= RN_STAGE) or
+// t's hash. masks: 2 u64 per round, cap rounds in LDS.
 __device__ int64_t n2v_pick_classify(const int32_t *__restrict__ col,
                                      const int32_t *__restrict__ tab, const AdjRow &rv,
-                                     const AdjRow &rt, int32_t t, double U, double ip, double iq,
-                                     uint64_t *masks, int64_t cap, int lane, uint32_t &probes,
-                                     uint32_t &loads) {
+                                     const AdjRow &rt, int32_t t, const int32_t *nt_lds,
+                                     double U, double ip, double iq, uint64_t *masks, int64_t cap,
+                                     int lane, uint32_t &probes, uint32_t &loads) {
     const int64_t n = rv.n;
     const int64_t rounds = (n + WAVE - 1) / WAVE;
     auto classify = [&](int64_t r, uint64_t &mp, uint64_t &mq) {
@@ -607,7 +610,9 @@ __device__ int64_t n2v_pick_classify(const int32_t *__restrict__ col,
             const int32_t x = col[rv.a + i];
             ++loads;
             is_p = x == t;
-            if (!is_p) is_q = lane_member(col, tab, rt, x, probes);
+            if (!is_p)
+                is_q = nt_lds ? contains_lds(nt_lds, static_cast<int>(rt.n), x)
+                              : lane_member(col, tab, rt, x, probes);
         }
         mp = __ballot(is_p);
         mq = __ballot(is_q);
@@ -782,10 +787,19 @@ __global__ void __launch_bounds__(RN_WAVES *WAVE)
                                               c.inv_q, reinterpret_cast<int32_t *>(buf), lane,
                                               probes, loads);
                     if (STATS) ++c_b;
-                } else {
-                    pick = n2v_pick_classify(c.col, adj_hash, rv, rt, t, U, c.inv_p, c.inv_q,
-                                             reinterpret_cast<uint64_t *>(buf), RN_CAP / 4,
+                } else if (rt.n <= RN_STAGE) {   // N(t) sorted into LDS: n <= m <= 1024
+                    int32_t *nt = reinterpret_cast<int32_t *>(buf + RN_MASKW);
+                    const int64_t ta = c.row_ptr[t];
+                    for (int64_t e = lane; e < rt.n; e += WAVE) nt[e] = c.col_sorted[ta + e];
+                    if (STATS) loads += static_cast<uint32_t>((rt.n - lane + WAVE - 1) / WAVE);
+                    dw::wave_lds_sync();
+                    pick = n2v_pick_classify(c.col, adj_hash, rv, rt, t, nt, U, c.inv_p, c.inv_q,
+                                             reinterpret_cast<uint64_t *>(buf), RN_MASKW / 4,
                                              lane, probes, loads);
+                } else {
+                    pick = n2v_pick_classify(c.col, adj_hash, rv, rt, t, nullptr, U, c.inv_p,
+                                             c.inv_q, reinterpret_cast<uint64_t *>(buf),
+                                             RN_CAP / 4, lane, probes, loads);
                 }
                 dw::wave_lds_sync();   // buf is rewritten at the next step
                 if (pick < 0) {        // the margin rule could not decide: CPython's arithmetic

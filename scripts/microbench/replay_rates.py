@@ -48,9 +48,20 @@ def main():
     csr.device_tensors(dev)
     res = {'lib': os.environ.get('DW_LIB_PATH', 'default'),
            'node2vec_p0.25_q4': rate(Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev),
-                                     args.n2v_walks, args.L, dev)}
+                                     args.n2v_walks, args.L, dev),
+           'node2vec_p0.25_q4_csr': rate(Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev,
+                                                  layout='csr'), args.n2v_walks, args.L, dev),
+           'node2vec_p1_q1': rate(Node2Vec(csr, args.L, p=1.0, q=1.0, device=dev),
+                                  args.n2v_walks, args.L, dev)}
+    w = Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev)
+    gen = random.Random(0)
+    st = torch.arange(1, args.n2v_walks + 1, dtype=torch.int32, device=dev)
+    u = torch.from_numpy(draw_uniforms(args.n2v_walks * (args.L - 1), gen)).to(dev)
+    res['node2vec_counted'] = w.count_replay_traffic(st, u)
     if args.dw_walks:
         res['deepwalk'] = rate(DeepWalk(csr, args.L, device=dev), args.dw_walks, args.L, dev)
+        res['deepwalk_csr'] = rate(DeepWalk(csr, args.L, device=dev, layout='csr'), args.dw_walks,
+                                   args.L, dev)
     print(json.dumps(res), flush=True)
 
 
