@@ -225,10 +225,11 @@ def main():
                     help='one GPU, measurement only: run rank 0\'s share of an owner-mode job of '
                          'this many ranks (its walks, slots, Adam rows) without the collectives; '
                          'value is then a projection (comm assumed hidden)')
-    ap.add_argument('--owner-walks', default=None, choices=['all', 'gather'],
-                    help='owner mode: every rank generates the whole global batch of walks '
-                         '(all; default for DeepWalk, whose walker is cheap) or its own B walks '
-                         'and all-gathers them (gather; default for node2vec)')
+    ap.add_argument('--owner-walks', default='gather', choices=['all', 'gather'],
+                    help='owner mode: every rank generates its own node range\'s B walks (walk '
+                         'ids rank*B.., start nodes in node order) and all-gathers them over RCCL '
+                         '(gather; default, north_star\'s walk sharding by node-id range), or '
+                         'generates the whole global batch itself (all; a measured option)')
     ap.add_argument('--in-exchange', default=None, choices=['sharded', 'lazy', 'auto'],
                     help='owner mode, in table: sharded = dense reduce-scatter / own-rows Adam / '
                          'all-gather (OwnerTables); lazy = only the rows the batch touched are '
@@ -267,8 +268,6 @@ def main():
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
             setattr(args, k, v)
-    if args.owner_walks is None:
-        args.owner_walks = 'gather' if args.method == 'node2vec' else 'all'
     if args.in_exchange is None:
         args.in_exchange = 'lazy' if args.config == 'c5' else 'auto'
 
