@@ -528,7 +528,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // one 64-B bucket load instead of a binary search.
 constexpr int RN_WAVES = 2;
 constexpr int RN_CAP = 2048;   // LDS words per wave: 512 rounds of class ballots (A) / positions (B)
-constexpr int RN_STAGE = 1024; // (A) with N(t) this short: staged sorted in LDS, LDS searches
+constexpr int RN_STAGE = RN_CAP - 64;   // (A) with N(t) this short: staged sorted in LDS
 constexpr int RN_MASKW = 64;   // (A) staged: words of ballots ahead of the staged list (16 rounds)
 
 struct AdjRow {       // a row's CSR range and adjacency-hash buckets
@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(RN_WAVES *WAVE)
                       const int32_t *__restrict__ adj_hash, const int32_t *__restrict__ adj_hpos,
                       int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
                       int32_t L, const double *__restrict__ uniforms, int32_t *__restrict__ out,
-                      int32_t *status, unsigned long long *counters) {
+                      int32_t *status, unsigned long long *counters, int32_t b_factor) {
     __shared__ uint32_t s_buf[RN_WAVES][RN_CAP];
     __shared__ int64_t s_pick[RN_WAVES];
     const int lane = threadIdx.x & (WAVE - 1);
@@ -782,7 +782,9 @@ __global__ void __launch_bounds__(RN_WAVES *WAVE)
                 pick = uniform_pick_exact(U, rv.n);
                 if (pick < 0) pick = uniform_pick_serial(U, rv.n);
             } else {
-                if (rt.n < rv.n && rt.n <= RN_CAP) {
+                // (B) when N(t) is much the shorter list (a probe of v's hash is a random
+                // 64-B line, an LDS search of staged N(t) a few LDS reads: b_factor of them)
+                if (rt.n <= RN_CAP && rt.n * (int64_t)b_factor < rv.n) {
                     pick = n2v_pick_positions(c.col, adj_hash, adj_hpos, rv, rt, t, U, c.inv_p,
                                               c.inv_q, reinterpret_cast<int32_t *>(buf), lane,
                                               probes, loads);
@@ -1428,16 +1430,22 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
                               stream);
     int64_t blocks = (n_walks + RN_WAVES - 1) / RN_WAVES;
     if (blocks > 16384) blocks = 16384;
+    // (B) needs deg(v) > b_factor * deg(t); DW_N2V_BFACTOR overrides (tuning sweeps)
+    static const int32_t b_factor = [] {
+        const char *e = getenv("DW_N2V_BFACTOR");
+        const int f = e ? atoi(e) : 0;
+        return f > 0 ? f : 4;
+    }();
     if (counters)
         hipLaunchKernelGGL((k_walk_replay_n2v<true>), dim3((unsigned)blocks),
                            dim3(RN_WAVES * WAVE), 0, dw::as_stream(stream), c, adj_off, adj_hash,
                            adj_hpos, n_rows, starts, n_walks, walk_length, uniforms, out, status,
-                           reinterpret_cast<unsigned long long *>(counters));
+                           reinterpret_cast<unsigned long long *>(counters), b_factor);
     else
         hipLaunchKernelGGL((k_walk_replay_n2v<false>), dim3((unsigned)blocks),
                            dim3(RN_WAVES * WAVE), 0, dw::as_stream(stream), c, adj_off, adj_hash,
                            adj_hpos, n_rows, starts, n_walks, walk_length, uniforms, out, status,
-                           nullptr);
+                           nullptr, b_factor);
     DW_LAUNCH_CHECK("dw_walk_replay_indexed");
     return DW_OK;
 }
