@@ -377,11 +377,161 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
     return -1;  // no D_i > 0: rounding at the top end; the serial replay decides
 }
 
+// ---- node2vec replay over the adjacency hash: probe the shorter list --------------------------
+// The exact picks need, at a step (t -> v), the class of every neighbour of v: t itself, a
+// common neighbour (x in N(t)), or other. node2vec_pick_exact classifies all n = deg(v) of them
+// against N(t) (staged sorted in LDS, or searched in HBM). When N(t) is much the shorter list
+// (m = deg(t), m * b_factor < n), k_walk_replay maps N(t) into N(v) instead: m + 1 probes of v's
+// adjacency hash, each hit read back as the key's position in v's neighbour order (adj_hpos);
+// the positions P of the common neighbours and t's own position give every prefix count
+// c_i = #{P <= i}, T = A/p + B + C/q from the counts, and a binary search over i of
+// D_i = W(a_i, b_i, c_i) - U T (c_i summed over the wave) finds the crossing; the same margin
+// rule decides, the serial replay where it cannot. A walk visits hubs in proportion to their
+// degree (mean visited degree 1,425 at C3) while the mean of min(deg v, deg t) over its edges is
+// 276: a hub reached from a small node costs m probes instead of n classifications. A probe is
+// a random 64-B line where a staged search is a few LDS reads, hence the factor (a sweep on one
+// MI355X: scripts/experiments/n2v_bfactor_sweep.sh).
+
+struct AdjRow {       // a row's CSR range and adjacency-hash buckets
+    int64_t a, n, h;
+    uint32_t nb;
+};
+
+__device__ __forceinline__ AdjRow adj_row(const int64_t *__restrict__ row_ptr,
+                                          const int64_t *__restrict__ adj_off, int32_t v) {
+    const int64_t a = row_ptr[v], b = row_ptr[v + 1];
+    const int64_t h = adj_off[v], hb = adj_off[v + 1];
+    return AdjRow{a, b - a, h, static_cast<uint32_t>((hb - h) >> 4)};
+}
+
+// Slot of key x in a row's hash (relative to adj_hash), or -1; one lane, one key.
+__device__ __forceinline__ int64_t lane_hash_find(const int32_t *__restrict__ tab,
+                                                  const AdjRow &r, int32_t x, uint32_t &probes) {
+    uint32_t b = dw::adj_bucket(x, r.nb);
+    for (uint32_t k = 0; k < r.nb; ++k) {
+        const int64_t s0 = r.h + (int64_t)b * 16;
+        const int4 *q = reinterpret_cast<const int4 *>(tab + s0);
+        const int4 e0 = q[0], e1 = q[1], e2 = q[2], e3 = q[3];
+        ++probes;
+        const int32_t sl[16] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w,
+                                e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
+        bool free_slot = false;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (sl[j] == x) return s0 + j;
+            free_slot = free_slot || sl[j] < 0;
+        }
+        if (free_slot) return -1;
+        if (++b == r.nb) b = 0;
+    }
+    return -1;
+}
+
+// x in N(row)? (hash, or a scan of a short row's list)
+__device__ __forceinline__ bool lane_member(const int32_t *__restrict__ col,
+                                            const int32_t *__restrict__ tab, const AdjRow &r,
+                                            int32_t x, uint32_t &probes) {
+    if (r.nb > 0) return lane_hash_find(tab, r, x, probes) >= 0;
+    for (int64_t k = 0; k < r.n; ++k)
+        if (col[r.a + k] == x) return true;
+    return false;
+}
+
+// position of x in N(row) (neighbour order), or -1
+__device__ __forceinline__ int64_t lane_position(const int32_t *__restrict__ col,
+                                                 const int32_t *__restrict__ tab,
+                                                 const int32_t *__restrict__ hpos, const AdjRow &r,
+                                                 int32_t x, uint32_t &probes) {
+    if (r.nb > 0) {
+        const int64_t s = lane_hash_find(tab, r, x, probes);
+        return s >= 0 ? static_cast<int64_t>(hpos[s]) : -1;
+    }
+    for (int64_t k = 0; k < r.n; ++k)
+        if (col[r.a + k] == x) return k;
+    return -1;
+}
+
+__device__ __forceinline__ double n2v_w(int64_t na, int64_t nb, int64_t nc, double ip, double iq) {
+    return static_cast<double>(na) * ip + static_cast<double>(nb) + static_cast<double>(nc) * iq;
+}
+
+// positions of N(t)'s members in N(v) (m <= the per-wave buffer), then a binary search for
+// the crossing.
+__device__ int64_t n2v_pick_positions(const int32_t *__restrict__ col,
+                                      const int32_t *__restrict__ tab,
+                                      const int32_t *__restrict__ hpos, const AdjRow &rv,
+                                      const AdjRow &rt, int32_t t, double U, double ip,
+                                      double iq, int32_t *pos, int lane, uint32_t &probes,
+                                      uint32_t &loads) {
+    const int64_t n = rv.n, m = rt.n;
+    int64_t C = 0;
+    for (int64_t j0 = 0; j0 < m; j0 += WAVE) {
+        const int64_t j = j0 + lane;
+        int32_t ps = -1;
+        if (j < m) {
+            const int32_t y = col[rt.a + j];
+            ++loads;
+            ps = static_cast<int32_t>(lane_position(col, tab, hpos, rv, y, probes));
+            pos[j] = ps;
+        }
+        C += __popcll(__ballot(ps >= 0));
+    }
+    int64_t pos_t = -1;                          // t's own position in N(v)
+    if (lane == 0) pos_t = lane_position(col, tab, hpos, rv, t, probes);
+    pos_t = __shfl(pos_t, 0);
+    dw::wave_lds_sync();
+    const int64_t A = pos_t >= 0 ? 1 : 0;
+    const double T = n2v_w(A, n - A - C, C, ip, iq);
+    const double UT = U * T;
+    const double M = exact_margin(n, T);
+    auto D = [&](int64_t i) {                    // D_i = W_i - U T, exact counts
+        int64_t c = 0;
+        for (int64_t j = lane; j < m; j += WAVE) {
+            const int32_t ps = pos[j];
+            c += (ps >= 0 && ps <= i) ? 1 : 0;
+        }
+#pragma unroll
+        for (int off = WAVE / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, WAVE);
+        const int64_t a = (pos_t >= 0 && pos_t <= i) ? 1 : 0;
+        return n2v_w(a, (i + 1) - a - c, c, ip, iq) - UT;
+    };
+    int64_t lo = 0, hi = n - 1;                  // first i in [0, n-1] with D_i > 0
+    if (!(D(n - 1) > 0.0)) return -1;            // rounding at the top end: serial replay
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (D(mid) > 0.0)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    const int64_t k = lo;
+    if (k >= 1 && fabs(D(k - 1)) <= M) return -1;
+    if (k <= n - 2 && fabs(D(k)) <= M) return -1;
+    return k;
+}
+
+// The adjacency index of the probe-the-shorter-list steps (dw_walk_replay_indexed; adj_off ==
+// NULL: every step classifies N(v)) and the optional traffic counters (uint64[4] += {bytes,
+// hash probes, list entries read, steps}).
+struct N2VIndex {
+    const int64_t *adj_off;
+    const int32_t *adj_hash;
+    const int32_t *adj_hpos;
+    int32_t b_factor;
+    unsigned long long *counters;
+};
+
+__device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
+    uint32_t k = 0;
+    while ((int64_t(1) << k) < x) ++k;
+    return k;
+}
+
 template <int CH, int NCAP>
 __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
-                  int32_t *__restrict__ out, int32_t *status, int fast) {
+                  int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
     __shared__ double s_buf[REPLAY_WAVES][CH];
     __shared__ int32_t s_nprev[REPLAY_WAVES][NCAP];
     __shared__ int64_t s_pick[REPLAY_WAVES];
@@ -390,6 +540,8 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     double *buf = s_buf[wv];
     int32_t *nprev_lds = s_nprev[wv];
     const int64_t n_waves = (int64_t)gridDim.x * REPLAY_WAVES;
+    const bool counted = ix.counters != nullptr;
+    uint32_t probes = 0, loads = 0, steps = 0;   // counted launches only
 
     for (int64_t wk = (int64_t)blockIdx.x * REPLAY_WAVES + wv; wk < n_walks; wk += n_waves) {
         int32_t v = starts[wk];
@@ -409,14 +561,40 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 if (lane == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
                 break;
             }
+            const double uu = u[s - 1];
+            int64_t pa = 0, pn = 0;
+            if (c.node2vec && prev >= 0) {
+                pa = c.row_ptr[prev];
+                pn = c.row_ptr[prev + 1] - pa;
+            }
+            if (counted && lane == 0) ++steps;
+            // N(prev) much the shorter list: its members' positions in N(v) (v's hash)
+            if (fast && ix.adj_off && c.node2vec && prev >= 0 && pn <= 2 * CH &&
+                pn * (int64_t)ix.b_factor < n) {
+                const int64_t h = ix.adj_off[v];
+                const AdjRow rv{a, n, h, static_cast<uint32_t>((ix.adj_off[v + 1] - h) >> 4)};
+                const AdjRow rt{pa, pn, 0, 0};
+                const int64_t fp = n2v_pick_positions(
+                    c.col, ix.adj_hash, ix.adj_hpos, rv, rt, prev, uu, c.inv_p, c.inv_q,
+                    reinterpret_cast<int32_t *>(buf), lane, probes, loads);
+                dw::wave_lds_sync();
+                if (fp >= 0) {
+                    const int32_t child = c.col[a + fp];
+                    if (lane == 0) o[s] = child;
+                    prev = v;
+                    v = child;
+                    continue;
+                }
+            }
             // N(prev), sorted, for the adjacency test
             const int32_t *np_lds = nullptr;
             int np_lds_n = 0;
             const int32_t *np_g = nullptr;
             int64_t np_g_n = 0;
             if (c.node2vec && prev >= 0) {
-                const int64_t pa = c.row_ptr[prev];
-                const int64_t pn = c.row_ptr[prev + 1] - pa;
+                if (counted && lane == 0)   // N(v) read, N(prev) staged or searched in HBM
+                    loads += static_cast<uint32_t>(
+                        n + (pn <= NCAP ? pn : n * static_cast<int64_t>(ceil_log2(pn + 1))));
                 if (pn <= NCAP) {
                     for (int64_t e = lane; e < pn; e += WAVE) nprev_lds[e] = c.col_sorted[pa + e];
                     dw::wave_lds_sync();
@@ -427,7 +605,6 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                     np_g_n = pn;
                 }
             }
-            const double uu = u[s - 1];
             if (fast) {  // unweighted: the exact pick without the serial sums (above)
                 const int64_t fp =
                     (!c.node2vec || prev < 0)
@@ -510,333 +687,18 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
         if (lane == 0)
             for (; s < L; ++s) o[s] = -1;  // marks an aborted walk
     }
-}
-
-// ---- node2vec replay over the adjacency hash: probe the shorter list --------------------------
-// The exact picks need, at a step (t -> v), the class of every neighbour of v: t itself, a
-// common neighbour (x in N(t)), or other. With v's and t's degrees n and m, either
-//   (A) n <= m: classify N(v) — n probes of t's adjacency hash (or a scan of t's list when it has
-//       none), the classes kept as per-round ballots in LDS; or
-//   (B) m < n: map N(t) into N(v) — m + 1 probes of v's hash, each hit read back as the key's
-//       position in v's neighbour order (adj_hpos); the positions P of the common neighbours
-//       and t's own position pos_t then give every prefix count c_i = #{P <= i} directly.
-// Either way T = A/p + B + C/q from the counts; (A) finds the crossing by scanning the ballots,
-// (B) by a binary search over i of D_i = W(a_i, b_i, c_i) - U T with c_i summed over the wave.
-// The margin rule of node2vec_pick_exact decides; where it cannot, the serial replay does. A
-// random walk visits hubs in proportion to their degree (mean visited degree 1,425 at C3) while
-// the mean of min(deg v, deg t) over its edges is 276, so (B) removes most of the tests; each is
-// one 64-B bucket load instead of a binary search.
-constexpr int RN_WAVES = 2;
-constexpr int RN_CAP = 2048;   // LDS words per wave: 512 rounds of class ballots (A) / positions (B)
-constexpr int RN_STAGE = RN_CAP - 64;   // (A) with N(t) this short: staged sorted in LDS
-constexpr int RN_MASKW = 64;   // (A) staged: words of ballots ahead of the staged list (16 rounds)
-
-struct AdjRow {       // a row's CSR range and adjacency-hash buckets
-    int64_t a, n, h;
-    uint32_t nb;
-};
-
-__device__ __forceinline__ AdjRow adj_row(const int64_t *__restrict__ row_ptr,
-                                          const int64_t *__restrict__ adj_off, int32_t v) {
-    const int64_t a = row_ptr[v], b = row_ptr[v + 1];
-    const int64_t h = adj_off[v], hb = adj_off[v + 1];
-    return AdjRow{a, b - a, h, static_cast<uint32_t>((hb - h) >> 4)};
-}
-
-// Slot of key x in a row's hash (relative to adj_hash), or -1; one lane, one key.
-__device__ __forceinline__ int64_t lane_hash_find(const int32_t *__restrict__ tab,
-                                                  const AdjRow &r, int32_t x, uint32_t &probes) {
-    uint32_t b = dw::adj_bucket(x, r.nb);
-    for (uint32_t k = 0; k < r.nb; ++k) {
-        const int64_t s0 = r.h + (int64_t)b * 16;
-        const int4 *q = reinterpret_cast<const int4 *>(tab + s0);
-        const int4 e0 = q[0], e1 = q[1], e2 = q[2], e3 = q[3];
-        ++probes;
-        const int32_t sl[16] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w,
-                                e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
-        bool free_slot = false;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (sl[j] == x) return s0 + j;
-            free_slot = free_slot || sl[j] < 0;
-        }
-        if (free_slot) return -1;
-        if (++b == r.nb) b = 0;
-    }
-    return -1;
-}
-
-// x in N(row)? (hash, or a scan of a short row's list)
-__device__ __forceinline__ bool lane_member(const int32_t *__restrict__ col,
-                                            const int32_t *__restrict__ tab, const AdjRow &r,
-                                            int32_t x, uint32_t &probes) {
-    if (r.nb > 0) return lane_hash_find(tab, r, x, probes) >= 0;
-    for (int64_t k = 0; k < r.n; ++k)
-        if (col[r.a + k] == x) return true;
-    return false;
-}
-
-// position of x in N(row) (neighbour order), or -1
-__device__ __forceinline__ int64_t lane_position(const int32_t *__restrict__ col,
-                                                 const int32_t *__restrict__ tab,
-                                                 const int32_t *__restrict__ hpos, const AdjRow &r,
-                                                 int32_t x, uint32_t &probes) {
-    if (r.nb > 0) {
-        const int64_t s = lane_hash_find(tab, r, x, probes);
-        return s >= 0 ? static_cast<int64_t>(hpos[s]) : -1;
-    }
-    for (int64_t k = 0; k < r.n; ++k)
-        if (col[r.a + k] == x) return k;
-    return -1;
-}
-
-__device__ __forceinline__ double n2v_w(int64_t na, int64_t nb, int64_t nc, double ip, double iq) {
-    return static_cast<double>(na) * ip + static_cast<double>(nb) + static_cast<double>(nc) * iq;
-}
-
-// (A): classify N(v) against N(t): t's sorted list staged in LDS (nt_lds, m <= RN_STAGE) or
-// t's hash. masks: 2 u64 per round, cap rounds in LDS.
-__device__ int64_t n2v_pick_classify(const int32_t *__restrict__ col,
-                                     const int32_t *__restrict__ tab, const AdjRow &rv,
-                                     const AdjRow &rt, int32_t t, const int32_t *nt_lds,
-                                     double U, double ip, double iq, uint64_t *masks, int64_t cap,
-                                     int lane, uint32_t &probes, uint32_t &loads) {
-    const int64_t n = rv.n;
-    const int64_t rounds = (n + WAVE - 1) / WAVE;
-    auto classify = [&](int64_t r, uint64_t &mp, uint64_t &mq) {
-        const int64_t i = r * WAVE + lane;
-        bool is_p = false, is_q = false;
-        if (i < n) {
-            const int32_t x = col[rv.a + i];
-            ++loads;
-            is_p = x == t;
-            if (!is_p)
-                is_q = nt_lds ? contains_lds(nt_lds, static_cast<int>(rt.n), x)
-                              : lane_member(col, tab, rt, x, probes);
-        }
-        mp = __ballot(is_p);
-        mq = __ballot(is_q);
-    };
-    int64_t A = 0, C = 0;
-    for (int64_t r = 0; r < rounds; ++r) {
-        uint64_t mp, mq;
-        classify(r, mp, mq);
-        if (r < cap && lane == 0) {
-            masks[2 * r] = mp;
-            masks[2 * r + 1] = mq;
-        }
-        A += __popcll(mp);
-        C += __popcll(mq);
-    }
-    dw::wave_lds_sync();
-    const double T = n2v_w(A, n - A - C, C, ip, iq);
-    const double UT = U * T;
-    const double M = exact_margin(n, T);
-    int64_t na = 0, nc = 0;
-    double d_prev = -UT;
-    for (int64_t r = 0; r < rounds; ++r) {
-        uint64_t mp, mq;
-        if (r < cap) {
-            mp = masks[2 * r];
-            mq = masks[2 * r + 1];
-        } else {
-            classify(r, mp, mq);
-        }
-        const int64_t base = r * WAVE;
-        const int64_t in_round = n - base < WAVE ? n - base : WAVE;
-        const uint64_t le = (lane == WAVE - 1) ? ~0ull : ((2ull << lane) - 1);
-        const int64_t pa = na + __popcll(mp & le), pc = nc + __popcll(mq & le);
-        const int64_t i = base + lane;
-        const double d = n2v_w(pa, (i + 1) - pa - pc, pc, ip, iq) - UT;
-        const uint64_t over = __ballot(lane < in_round && d > 0.0);
-        if (over) {
-            const int first = __ffsll((unsigned long long)over) - 1;
-            int64_t k = base + first;
-            const double d_k = __shfl(d, first);
-            const double d_km1 = first > 0 ? __shfl(d, first - 1) : d_prev;
-            if (k > n - 1) k = n - 1;
-            if (k >= 1 && fabs(d_km1) <= M) return -1;
-            if (k <= n - 2 && fabs(d_k) <= M) return -1;
-            return k;
-        }
-        d_prev = __shfl(d, static_cast<int>(in_round - 1));
-        na += __popcll(mp);
-        nc += __popcll(mq);
-    }
-    return -1;
-}
-
-// (B): positions of N(t)'s members in N(v) (m <= RN_CAP), then a binary search for the crossing.
-__device__ int64_t n2v_pick_positions(const int32_t *__restrict__ col,
-                                      const int32_t *__restrict__ tab,
-                                      const int32_t *__restrict__ hpos, const AdjRow &rv,
-                                      const AdjRow &rt, int32_t t, double U, double ip,
-                                      double iq, int32_t *pos, int lane, uint32_t &probes,
-                                      uint32_t &loads) {
-    const int64_t n = rv.n, m = rt.n;
-    int64_t C = 0;
-    for (int64_t j0 = 0; j0 < m; j0 += WAVE) {
-        const int64_t j = j0 + lane;
-        int32_t ps = -1;
-        if (j < m) {
-            const int32_t y = col[rt.a + j];
-            ++loads;
-            ps = static_cast<int32_t>(lane_position(col, tab, hpos, rv, y, probes));
-            pos[j] = ps;
-        }
-        C += __popcll(__ballot(ps >= 0));
-    }
-    int64_t pos_t = -1;                          // t's own position in N(v)
-    if (lane == 0) pos_t = lane_position(col, tab, hpos, rv, t, probes);
-    pos_t = __shfl(pos_t, 0);
-    dw::wave_lds_sync();
-    const int64_t A = pos_t >= 0 ? 1 : 0;
-    const double T = n2v_w(A, n - A - C, C, ip, iq);
-    const double UT = U * T;
-    const double M = exact_margin(n, T);
-    auto D = [&](int64_t i) {                    // D_i = W_i - U T, exact counts
-        int64_t c = 0;
-        for (int64_t j = lane; j < m; j += WAVE) {
-            const int32_t ps = pos[j];
-            c += (ps >= 0 && ps <= i) ? 1 : 0;
-        }
-#pragma unroll
-        for (int off = WAVE / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, WAVE);
-        const int64_t a = (pos_t >= 0 && pos_t <= i) ? 1 : 0;
-        return n2v_w(a, (i + 1) - a - c, c, ip, iq) - UT;
-    };
-    int64_t lo = 0, hi = n - 1;                  // first i in [0, n-1] with D_i > 0
-    if (!(D(n - 1) > 0.0)) return -1;            // rounding at the top end: serial replay
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (D(mid) > 0.0)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    const int64_t k = lo;
-    if (k >= 1 && fabs(D(k - 1)) <= M) return -1;
-    if (k <= n - 2 && fabs(D(k)) <= M) return -1;
-    return k;
-}
-
-// the serial replay of one unweighted node2vec step in lane 0 (the margin rule failed)
-__device__ int64_t n2v_pick_serial(const ReplayCtx &c, const AdjRow &rv, int32_t prev,
-                                   int64_t pa, int64_t pn, double U) {
-    const int64_t n = rv.n;
-    const int32_t *np = c.col_sorted + pa;
-    double sum = 0.0;
-    for (int64_t i = 0; i < n; ++i)
-        sum = sum + step_weight(c, rv.a + i, prev, nullptr, 0, np, pn);
-    double total = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        const double nw = step_weight(c, rv.a + i, prev, nullptr, 0, np, pn) / sum;
-        total = (i == 0) ? nw : total + nw;
-    }
-    total = total + 0.0;
-    const double x = U * total;
-    double cum = 0.0;
-    for (int64_t i = 0; i < n - 1; ++i) {
-        const double nw = step_weight(c, rv.a + i, prev, nullptr, 0, np, pn) / sum;
-        cum = (i == 0) ? nw : cum + nw;
-        if (x < cum) return i;
-    }
-    return n - 1;
-}
-
-template <bool STATS>
-__global__ void __launch_bounds__(RN_WAVES *WAVE)
-    k_walk_replay_n2v(ReplayCtx c, const int64_t *__restrict__ adj_off,
-                      const int32_t *__restrict__ adj_hash, const int32_t *__restrict__ adj_hpos,
-                      int64_t n_rows, const int32_t *__restrict__ starts, int64_t n_walks,
-                      int32_t L, const double *__restrict__ uniforms, int32_t *__restrict__ out,
-                      int32_t *status, unsigned long long *counters, int32_t b_factor) {
-    __shared__ uint32_t s_buf[RN_WAVES][RN_CAP];
-    __shared__ int64_t s_pick[RN_WAVES];
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wv = threadIdx.x / WAVE;
-    uint32_t *buf = s_buf[wv];
-    const int64_t n_waves = (int64_t)gridDim.x * RN_WAVES;
-    uint32_t probes = 0, loads = 0, c_steps = 0, c_b = 0;   // STATS
-    for (int64_t wk = (int64_t)blockIdx.x * RN_WAVES + wv; wk < n_walks; wk += n_waves) {
-        int32_t v = starts[wk];
-        int32_t t = -1;
-        AdjRow rt{0, 0, 0, 0};
-        int32_t *o = out + wk * (int64_t)L;
-        if (lane == 0) o[0] = v;
-        const double *u = uniforms + wk * (int64_t)(L - 1);
-        int32_t s = 1;
-        for (; s < L; ++s) {
-            if (v < 0 || (int64_t)v >= n_rows) {
-                if (lane == 0) dw::status_or(status, DW_S_BAD_CSR);
-                break;
-            }
-            const AdjRow rv = adj_row(c.row_ptr, adj_off, v);
-            if (rv.n <= 0) {
-                if (lane == 0) dw::status_or(status, DW_S_ISOLATED_NODE);
-                break;
-            }
-            const double U = u[s - 1];
-            int64_t pick;
-            if (t < 0) {
-                pick = uniform_pick_exact(U, rv.n);
-                if (pick < 0) pick = uniform_pick_serial(U, rv.n);
-            } else {
-                // (B) when N(t) is much the shorter list (a probe of v's hash is a random
-                // 64-B line, an LDS search of staged N(t) a few LDS reads: b_factor of them)
-                if (rt.n <= RN_CAP && rt.n * (int64_t)b_factor < rv.n) {
-                    pick = n2v_pick_positions(c.col, adj_hash, adj_hpos, rv, rt, t, U, c.inv_p,
-                                              c.inv_q, reinterpret_cast<int32_t *>(buf), lane,
-                                              probes, loads);
-                    if (STATS) ++c_b;
-                } else if (rt.n <= RN_STAGE) {   // N(t) sorted into LDS: n <= m <= 1024
-                    int32_t *nt = reinterpret_cast<int32_t *>(buf + RN_MASKW);
-                    const int64_t ta = c.row_ptr[t];
-                    for (int64_t e = lane; e < rt.n; e += WAVE) nt[e] = c.col_sorted[ta + e];
-                    if (STATS) loads += static_cast<uint32_t>((rt.n - lane + WAVE - 1) / WAVE);
-                    dw::wave_lds_sync();
-                    pick = n2v_pick_classify(c.col, adj_hash, rv, rt, t, nt, U, c.inv_p, c.inv_q,
-                                             reinterpret_cast<uint64_t *>(buf), RN_MASKW / 4,
-                                             lane, probes, loads);
-                } else {
-                    pick = n2v_pick_classify(c.col, adj_hash, rv, rt, t, nullptr, U, c.inv_p,
-                                             c.inv_q, reinterpret_cast<uint64_t *>(buf),
-                                             RN_CAP / 4, lane, probes, loads);
-                }
-                dw::wave_lds_sync();   // buf is rewritten at the next step
-                if (pick < 0) {        // the margin rule could not decide: CPython's arithmetic
-                    if (lane == 0)
-                        s_pick[wv] = n2v_pick_serial(c, rv, t, c.row_ptr[t], rt.n, U);
-                    dw::wave_lds_sync();
-                    pick = s_pick[wv];
-                    dw::wave_lds_sync();
-                }
-            }
-            const int32_t child = c.col[rv.a + pick];
-            if (lane == 0) o[s] = child;
-            if (STATS) ++c_steps;
-            t = v;
-            rt = rv;
-            v = child;
-        }
-        if (lane == 0)
-            for (; s < L; ++s) o[s] = -1;
-    }
-    if constexpr (STATS) {
-        // per step: row_ptr + adj_off pairs (32 B), the uniform (8), the pick (4), the output
-        // (4); per probe one 64-B bucket; per list entry read 4 B (hits' positions included)
-        unsigned long long b = (unsigned long long)probes * 64ull + (unsigned long long)loads * 4ull;
-        unsigned long long v4[4] = {b, probes, loads, 0};
-        for (int k = 0; k < 3; ++k) {
-            unsigned long long x = v4[k];
-            for (int off = WAVE / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, WAVE);
-            if (lane == 0) atomicAdd(counters + k, x);
-        }
+    if (counted) {   // per step: row_ptr pairs of v and prev (32 B), the uniform, the pick and
+                     // the output (16); per probe a 64-B bucket; per list entry 4 B
+        unsigned long long v4[3] = {(unsigned long long)probes, (unsigned long long)loads,
+                                    (unsigned long long)steps};
+        for (int k = 0; k < 3; ++k)
+            for (int off = WAVE / 2; off > 0; off >>= 1) v4[k] += __shfl_xor(v4[k], off, WAVE);
         if (lane == 0) {
-            atomicAdd(counters + 0, (unsigned long long)c_steps * 48ull);
-            atomicAdd(counters + 3, (unsigned long long)c_steps);
+            atomicAdd(ix.counters + 0, v4[0] * 64ull + v4[1] * 4ull + v4[2] * 48ull);
+            atomicAdd(ix.counters + 1, v4[0]);
+            atomicAdd(ix.counters + 2, v4[1]);
+            atomicAdd(ix.counters + 3, v4[2]);
         }
-        (void)c_b;
     }
 }
 
@@ -1391,11 +1253,11 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
     if (fast)
         hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
                            dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
-                           n_walks, walk_length, uniforms, out, status, 1);
+                           n_walks, walk_length, uniforms, out, status, 1, N2VIndex{});
     else
         hipLaunchKernelGGL((k_walk_replay<REPLAY_CH, REPLAY_NCAP>), dim3((unsigned)blocks),
                            dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
-                           n_walks, walk_length, uniforms, out, status, 0);
+                           n_walks, walk_length, uniforms, out, status, 0, N2VIndex{});
     DW_LAUNCH_CHECK("dw_walk_replay");
     return DW_OK;
 }
@@ -1428,24 +1290,19 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
         return dw_walk_replay(row_ptr, col, col_sorted, nullptr, n_rows, starts, n_walks,
                               walk_length, DW_METHOD_NODE2VEC, p, q, uniforms, out, status,
                               stream);
-    int64_t blocks = (n_walks + RN_WAVES - 1) / RN_WAVES;
+    int64_t blocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
     if (blocks > 16384) blocks = 16384;
-    // (B) needs deg(v) > b_factor * deg(t); DW_N2V_BFACTOR overrides (tuning sweeps)
+    // N(prev) mapped into N(v) when deg(v) > b_factor deg(prev); DW_N2V_BFACTOR overrides
     static const int32_t b_factor = [] {
         const char *e = getenv("DW_N2V_BFACTOR");
         const int f = e ? atoi(e) : 0;
         return f > 0 ? f : 4;
     }();
-    if (counters)
-        hipLaunchKernelGGL((k_walk_replay_n2v<true>), dim3((unsigned)blocks),
-                           dim3(RN_WAVES * WAVE), 0, dw::as_stream(stream), c, adj_off, adj_hash,
-                           adj_hpos, n_rows, starts, n_walks, walk_length, uniforms, out, status,
-                           reinterpret_cast<unsigned long long *>(counters), b_factor);
-    else
-        hipLaunchKernelGGL((k_walk_replay_n2v<false>), dim3((unsigned)blocks),
-                           dim3(RN_WAVES * WAVE), 0, dw::as_stream(stream), c, adj_off, adj_hash,
-                           adj_hpos, n_rows, starts, n_walks, walk_length, uniforms, out, status,
-                           nullptr, b_factor);
+    const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
+                      reinterpret_cast<unsigned long long *>(counters)};
+    hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
+                       dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
+                       n_walks, walk_length, uniforms, out, status, 1, ix);
     DW_LAUNCH_CHECK("dw_walk_replay_indexed");
     return DW_OK;
 }
