@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -52,7 +52,9 @@ SIGNATURES = {
     'dw_stream_copy': (ctypes.c_int, [_p, _p, _i64, _p]),
     'dw_host_shuffle': (ctypes.c_int, [_p, _p, _i64]),
     'dw_mt_jump_table': (ctypes.c_int, [_i64, _i64, _p, _p, _i64]),
-    'dw_mt_uniforms': (ctypes.c_int, [_p, _i32, _i64, _p, _p, _i64, _p, _p, _i64, _p]),
+    'dw_mt_uniforms': (ctypes.c_int, [_p, _i32, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64,
+                                      _p]),
+    'dw_mt_workspace_words': (ctypes.c_int64, [_i64]),
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
     'dw_adj_hash_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),

@@ -67,17 +67,32 @@ def shuffled_range(n: int, rng: random.Random = None) -> np.ndarray:
 
 # ---- the same stream generated on the device (dw_mt_uniforms) ---------------------------------
 _MT_TABLES = {}          # (device, window_stride) -> (positions int16, offsets int64, n_chains)
+_MT_WS = {}              # device -> int32 workspace of the chains' jump windows
 _MT_LOCK = threading.Lock()
 MIN_CHAIN_WINDOWS = 256  # below this many 624-word windows per chain, one chain (no jump) wins
+CHAINS_PER_CU = 2        # chains the generation spreads over, per compute unit
 
 
 def mt_window_stride(n: int, index: int, n_cu: int) -> int:
     """Windows per chain for a call of n draws: at least MIN_CHAIN_WINDOWS, else a multiple of
-    64 just large enough that the chains fit the device's compute units once (one 127-KiB-LDS
-    workgroup each); a batch size that repeats reuses its jump table."""
+    64 just large enough for CHAINS_PER_CU chains per compute unit (a chain costs one jump, ~10^4
+    x 625 LDS reads, then its windows one after another); a batch size that repeats reuses its
+    jump table."""
     windows = (index + 2 * n - 1) // 624 + 1 if n > 0 else 1
-    per = -(-windows // max(1, n_cu))
+    per = -(-windows // max(1, CHAINS_PER_CU * n_cu))
     return max(MIN_CHAIN_WINDOWS, -(-per // 64) * 64)
+
+
+def mt_workspace(device: torch.device, n_chains: int) -> torch.Tensor:
+    """Device scratch of dw_mt_uniforms (the chains' jump windows), cached and grown."""
+    from shallow_encoders import _native
+    words = int(_native.load().dw_mt_workspace_words(int(n_chains)))
+    with _MT_LOCK:
+        ws = _MT_WS.get(device)
+        if ws is None or ws.numel() < words:
+            ws = torch.empty(max(words, 1), dtype=torch.int32, device=device)
+            _MT_WS[device] = ws
+        return ws
 
 
 def mt_jump_table(device: torch.device, window_stride: int, n_chains: int):
@@ -127,16 +142,17 @@ def draw_uniforms_device(n: int, device=None, rng: random.Random = None,
     stride = mt_window_stride(n, index, n_cu)
     windows = (index + 2 * n - 1) // 624 + 1
     chains = -(-windows // stride)
-    pos = off = None
+    pos = off = ws = None
     n_tab = 1
     if chains > 1:
         pos, off, n_tab = mt_jump_table(dev, stride, chains)
+        ws = mt_workspace(dev, chains)
     with torch.cuda.device(dev):
         mt = torch.from_numpy(state[:624].view(np.int32).copy()).to(dev, non_blocking=True)
         st_out = torch.empty(625, dtype=torch.int32, device=dev)
         _native.call('dw_mt_uniforms', _native.ptr(mt), index, n, _native.ptr(out),
                      _native.ptr(st_out), stride, _native.ptr(pos), _native.ptr(off), n_tab,
-                     _native.stream(dev))
+                     _native.ptr(ws), 0 if ws is None else ws.numel(), _native.stream(dev))
         host = torch.empty(625, dtype=torch.int32, pin_memory=True)
         host.copy_(st_out, non_blocking=True)
         done = torch.cuda.Event()

@@ -85,14 +85,17 @@ int dw_host_shuffle(uint32_t *mt_state, int64_t *perm, int64_t n);
  * dw_mt_uniforms: out[k] = the (k+1)-th random.random() of the generator whose state is
  * (mt[0..623], index) — random.getstate()[1] — for k < n; state_out (625 words: array + index)
  * receives the state after the n draws, for random.setstate. mt, out, state_out, jump_pos,
- * jump_off: DEVICE buffers (jump_*: a dw_mt_jump_table of the same window_stride with at least
- * ceil(windows / window_stride) chains, windows = (index + 2n - 1) / 624 + 1; may be NULL when
- * that is one chain). One workgroup per chain; stream-ordered. */
+ * jump_off, workspace: DEVICE buffers (jump_*: a dw_mt_jump_table of the same window_stride
+ * with at least chains = ceil(windows / window_stride) entries, windows = (index + 2n - 1) / 624
+ * + 1; workspace: dw_mt_workspace_words(chains) uint32 words; all may be NULL when that is one
+ * chain). Two stream-ordered launches: the chains' jumps, then one workgroup per chain. */
 int dw_mt_jump_table(int64_t window_stride, int64_t n_chains, int64_t *offsets,
                      uint16_t *positions, int64_t capacity);
 int dw_mt_uniforms(const uint32_t *mt, int32_t index, int64_t n, double *out,
                    uint32_t *state_out, int64_t window_stride, const uint16_t *jump_pos,
-                   const int64_t *jump_off, int64_t n_chains_table, void *stream);
+                   const int64_t *jump_off, int64_t n_chains_table, uint32_t *workspace,
+                   int64_t workspace_words, void *stream);
+int64_t dw_mt_workspace_words(int64_t n_chains);
 
 /* ---- graph ------------------------------------------------------------------------------- */
 

@@ -13,7 +13,8 @@ import pytest
 import torch
 
 from shallow_encoders import _native
-from shallow_encoders.graph.rng import draw_uniforms, draw_uniforms_device, mt_jump_table
+from shallow_encoders.graph.rng import (draw_uniforms, draw_uniforms_device, mt_jump_table,
+                                        mt_workspace)
 
 pytestmark = pytest.mark.gpu
 
@@ -78,8 +79,10 @@ def test_multi_chain_boundaries(stride, seed, skip, n, hip_device):
     mt = torch.from_numpy(internal[:624].view(np.int32).copy()).to(hip_device)
     out = torch.full((n,), float('nan'), dtype=torch.float64, device=hip_device)
     st = torch.zeros(625, dtype=torch.int32, device=hip_device)
+    ws = mt_workspace(hip_device, chains)
     _native.call('dw_mt_uniforms', _native.ptr(mt), index, n, _native.ptr(out), _native.ptr(st),
-                 stride, _native.ptr(pos), _native.ptr(off), n_tab, _native.stream(hip_device))
+                 stride, _native.ptr(pos), _native.ptr(off), n_tab, _native.ptr(ws), ws.numel(),
+                 _native.stream(hip_device))
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
     new = st.cpu().numpy().view(np.uint32)
     ref = exp_r.getstate()[1]
@@ -92,10 +95,10 @@ def test_abi_rejects_short_jump_table(hip_device):
     st = torch.empty(625, dtype=torch.int32, device=hip_device)
     with pytest.raises(_native.DWError):
         _native.call('dw_mt_uniforms', _native.ptr(mt), 0, 10_000, _native.ptr(out),
-                     _native.ptr(st), 1, None, None, 0, _native.stream(hip_device))
+                     _native.ptr(st), 1, None, None, 0, None, 0, _native.stream(hip_device))
     with pytest.raises(_native.DWError):
         _native.call('dw_mt_uniforms', _native.ptr(mt), 625, 1, _native.ptr(out),
-                     _native.ptr(st), 256, None, None, 0, _native.stream(hip_device))
+                     _native.ptr(st), 256, None, None, 0, None, 0, _native.stream(hip_device))
 
 
 @pytest.mark.parametrize('method', ['deepwalk', 'node2vec'])
