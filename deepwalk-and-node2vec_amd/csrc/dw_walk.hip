@@ -275,7 +275,8 @@ __global__ void __launch_bounds__(256)
 __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n, int32_t prev,
                                        const int32_t *np_lds, int np_lds_n,
                                        const int32_t *np_g, int64_t np_g_n, double U,
-                                       uint64_t *masks, int64_t cap, int lane) {
+                                       uint64_t *masks, int64_t cap, int lane,
+                                       const uint32_t *np_bits = nullptr) {
     const int64_t rounds = (n + WAVE - 1) / WAVE;
     auto classify = [&](int64_t r, uint64_t &mp, uint64_t &mq) {
         const int64_t i = r * WAVE + lane;
@@ -285,13 +286,44 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
             if (x == prev)
                 is_p = true;
             else
-                is_q = np_lds ? contains_lds(np_lds, np_lds_n, x)
-                              : contains_global(np_g, np_g_n, x);
+                is_q = np_bits ? ((np_bits[x >> 5] >> (x & 31)) & 1u) != 0u
+                       : np_lds ? contains_lds(np_lds, np_lds_n, x)
+                                : contains_global(np_g, np_g_n, x);
         }
         mp = __ballot(is_p);
         mq = __ballot(is_q);
     };
     int64_t A = 0, C = 0;
+    if (np_bits) {   // prev's neighbour bitmap (a hub): one 4-B load per test, no search
+        constexpr int RBB = 4;   // rounds per trip: their loads in flight together
+        for (int64_t r0 = 0; r0 < rounds; r0 += RBB) {
+            int32_t x[RBB];
+            uint32_t w[RBB];
+#pragma unroll
+            for (int j = 0; j < RBB; ++j) {
+                const int64_t i = (r0 + j) * WAVE + lane;
+                x[j] = i < n ? c.col[a + i] : prev;
+            }
+#pragma unroll
+            for (int j = 0; j < RBB; ++j) w[j] = x[j] != prev ? np_bits[x[j] >> 5] : 0u;
+#pragma unroll
+            for (int j = 0; j < RBB; ++j) {
+                const int64_t r = r0 + j;
+                const bool in_row = r * WAVE + lane < n;
+                const bool is_p = in_row && x[j] == prev;
+                const bool is_q = in_row && !is_p && ((w[j] >> (x[j] & 31)) & 1u) != 0u;
+                const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
+                if (r < rounds) {
+                    if (r < cap && lane == 0) {
+                        masks[2 * r] = mp;
+                        masks[2 * r + 1] = mq;
+                    }
+                    A += __popcll(mp);
+                    C += __popcll(mq);
+                }
+            }
+        }
+    } else {
     // first pass, 4 rounds per trip: the four membership searches are independent, so their
     // dependent load chains overlap (branchless lower_bound over the same sorted N(prev))
     constexpr int RB = 4;
@@ -333,6 +365,7 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
                 C += __popcll(mq);
             }
         }
+    }
     }
     dw::wave_lds_sync();
     const double ip = c.inv_p, iq = c.inv_q;
@@ -519,6 +552,9 @@ struct N2VIndex {
     const int32_t *adj_hpos;
     int32_t b_factor;
     unsigned long long *counters;
+    const int32_t *hub_idx;    // row -> its neighbour bitmap (dw_hub_bitmaps), or -1
+    const uint32_t *hub_bits;  // [n_hubs][hub_words]
+    int64_t hub_words;
 };
 
 __device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
@@ -591,10 +627,17 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             int np_lds_n = 0;
             const int32_t *np_g = nullptr;
             int64_t np_g_n = 0;
+            const uint32_t *np_bits = nullptr;
+            if (c.node2vec && prev >= 0 && pn > NCAP && ix.hub_idx) {
+                const int32_t hb = ix.hub_idx[prev];
+                if (hb >= 0) np_bits = ix.hub_bits + hb * ix.hub_words;
+            }
             if (c.node2vec && prev >= 0) {
-                if (counted && lane == 0)   // N(v) read, N(prev) staged or searched in HBM
+                if (counted && lane == 0)   // N(v) read; N(prev) staged, bit-tested or searched
                     loads += static_cast<uint32_t>(
-                        n + (pn <= NCAP ? pn : n * static_cast<int64_t>(ceil_log2(pn + 1))));
+                        n + (pn <= NCAP ? pn
+                                        : np_bits ? n
+                                                  : n * static_cast<int64_t>(ceil_log2(pn + 1))));
                 if (pn <= NCAP) {
                     for (int64_t e = lane; e < pn; e += WAVE) nprev_lds[e] = c.col_sorted[pa + e];
                     dw::wave_lds_sync();
@@ -611,7 +654,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                         ? uniform_pick_exact(uu, n)
                         : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, uu,
                                               reinterpret_cast<uint64_t *>(buf),
-                                              CH / 2, lane);
+                                              CH / 2, lane, np_bits);
                 if (fp >= 0) {
                     const int32_t child = c.col[a + fp];
                     if (lane == 0) o[s] = child;
@@ -806,6 +849,20 @@ __global__ void __launch_bounds__(256)
     } else {
         o[0] = v;
         for (int32_t s = 1; s < L; ++s) o[s] = step(s);
+    }
+}
+
+// One block per hub row: its neighbours as bits of a V-bit map (the bit-exact node2vec replay's
+// membership test against a hub prev: one 4-B load instead of a search of its sorted list).
+__global__ void __launch_bounds__(256)
+    k_hub_bitmaps(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                  const int32_t *__restrict__ hub_rows, int64_t hub_words,
+                  uint32_t *__restrict__ bits) {
+    const int32_t r = hub_rows[blockIdx.x];
+    uint32_t *b = bits + blockIdx.x * hub_words;
+    for (int64_t e = row_ptr[r] + threadIdx.x; e < row_ptr[r + 1]; e += blockDim.x) {
+        const int32_t x = col[e];
+        atomicOr(b + (x >> 5), 1u << (x & 31));
     }
 }
 
@@ -1264,9 +1321,10 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
 
 int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                            const int64_t *adj_off, const int32_t *adj_hash,
-                           const int32_t *adj_hpos, int64_t n_rows, const int32_t *starts,
-                           int64_t n_walks, int32_t walk_length, double p, double q,
-                           const double *uniforms, int32_t *out, int32_t *status,
+                           const int32_t *adj_hpos, const int32_t *hub_idx,
+                           const uint32_t *hub_bits, int64_t hub_words, int64_t n_rows,
+                           const int32_t *starts, int64_t n_walks, int32_t walk_length, double p,
+                           double q, const double *uniforms, int32_t *out, int32_t *status,
                            uint64_t *counters, void *stream) {
     DW_REQUIRE(walk_length >= 1, "dw_walk_replay_indexed: Minimum walk length is 1!");
     DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_replay_indexed: negative size");
@@ -1298,12 +1356,35 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
         const int f = e ? atoi(e) : 0;
         return f > 0 ? f : 4;
     }();
+    DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
+               "dw_walk_replay_indexed: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
-                      reinterpret_cast<unsigned long long *>(counters)};
+                      reinterpret_cast<unsigned long long *>(counters), hub_idx, hub_bits,
+                      hub_words};
     hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
                        dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
                        n_walks, walk_length, uniforms, out, status, 1, ix);
     DW_LAUNCH_CHECK("dw_walk_replay_indexed");
+    return DW_OK;
+}
+
+int dw_hub_bitmaps(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                   const int32_t *hub_rows, int64_t n_hubs, int64_t hub_words, uint32_t *bits,
+                   void *stream) {
+    DW_REQUIRE(n_hubs >= 0 && n_rows >= 0, "dw_hub_bitmaps: negative size");
+    if (n_hubs == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && hub_rows && bits, "dw_hub_bitmaps: null pointer");
+    DW_REQUIRE(hub_words >= (n_rows + 31) / 32, "dw_hub_bitmaps: hub_words too small");
+    DW_REQUIRE(n_hubs < (int64_t(1) << 31), "dw_hub_bitmaps: too many hubs");
+    hipError_t e = hipMemsetAsync(bits, 0, (size_t)n_hubs * hub_words * sizeof(uint32_t),
+                                  dw::as_stream(stream));
+    if (e != hipSuccess) {
+        dw::set_error("dw_hub_bitmaps: memset: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    hipLaunchKernelGGL(k_hub_bitmaps, dim3((unsigned)n_hubs), dim3(256), 0, dw::as_stream(stream),
+                       row_ptr, col, hub_rows, hub_words, bits);
+    DW_LAUNCH_CHECK("dw_hub_bitmaps");
     return DW_OK;
 }
 

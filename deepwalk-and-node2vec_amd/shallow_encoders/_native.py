@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -132,8 +132,9 @@ SIGNATURES = {
                                                _i64, _p]),
     'dw_step_starts': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),
     'dw_walk_replay_inline': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
-    'dw_walk_replay_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _f64,
-                                              _f64, _p, _p, _p, _p, _p]),
+    'dw_walk_replay_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p,
+                                              _i64, _i32, _f64, _f64, _p, _p, _p, _p, _p]),
+    'dw_hub_bitmaps': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i64, _p, _p]),
     'dw_adj_hash_positions': (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,
                                               _p, _i64, _p]),

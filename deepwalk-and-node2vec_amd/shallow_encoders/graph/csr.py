@@ -189,8 +189,8 @@ class CSRGraph:
     # ------------------------------------------------------------------ device side
     def device_tensors(self, device=None, need_sorted: bool = False,
                        need_alias: bool = False, need_edges: bool = False,
-                       need_adj: bool = False,
-                       need_adj_pos: bool = False) -> Dict[str, torch.Tensor]:
+                       need_adj: bool = False, need_adj_pos: bool = False,
+                       need_hub_bits: bool = False) -> Dict[str, torch.Tensor]:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
         the per-row adjacency hash / its slots' neighbour positions on the device)."""
         dev = _native.require_device(device)
@@ -230,7 +230,37 @@ class CSRGraph:
                              _native.ptr(d['status']), _native.stream(dev))
             _native.check_status(d['status'], 'adjacency positions build')
             d['adj_hpos'] = hp
+        if need_hub_bits and 'hub_idx' not in d:
+            self._build_hub_bits(dev)
         return d
+
+    # rows longer than the replay walker's LDS stage (1,024) get a V-bit neighbour map, the
+    # longest first, within this many bytes (DW_HUB_BITS_BYTES overrides)
+    HUB_MIN_DEGREE = 1024
+    HUB_BITS_BYTES = 2 << 30
+
+    def _build_hub_bits(self, dev) -> None:
+        """hub_idx int32[V] (-1 or the row's bitmap) / hub_bits int32[n_hubs, ceil(V/32)]
+        (dw_hub_bitmaps): the bit-exact node2vec replay's membership tests against a hub."""
+        import os
+        d = self._dev
+        V = self.vocab_size
+        words = (V + 31) // 32
+        budget = int(os.environ.get('DW_HUB_BITS_BYTES', self.HUB_BITS_BYTES))
+        deg = d['row_ptr'][1:] - d['row_ptr'][:-1]
+        order = torch.argsort(deg, descending=True)
+        n_big = int((deg > self.HUB_MIN_DEGREE).sum())
+        n_hubs = max(0, min(n_big, budget // max(1, words * 4)))
+        hubs = order[:n_hubs].to(torch.int32).contiguous()
+        idx = torch.full((V,), -1, dtype=torch.int32, device=dev)
+        bits = torch.empty((max(n_hubs, 1), words), dtype=torch.int32, device=dev)
+        if n_hubs:
+            idx[hubs.long()] = torch.arange(n_hubs, dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                _native.call('dw_hub_bitmaps', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
+                             V, _native.ptr(hubs), n_hubs, words, _native.ptr(bits),
+                             _native.stream(dev))
+        d['hub_idx'], d['hub_bits'], d['hub_words'] = idx, bits, words
 
     def _build_edges(self, dev) -> None:
         """edges int32[nnz, 4] (dw_edges_inline_build): {x, deg(x), row_ptr[x] lo, hi}."""

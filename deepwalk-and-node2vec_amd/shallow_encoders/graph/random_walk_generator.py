@@ -215,7 +215,8 @@ class RandomWalk(ABC):
         d = self._csr.device_tensors(dev, need_sorted=n2v and not indexed,
                                      need_alias=self._rng == 'philox',
                                      need_edges=(indexed and not n2v) or replay_inline,
-                                     need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx)
+                                     need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx,
+                                     need_hub_bits=replay_n2v_idx)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         if status is None:
@@ -245,8 +246,10 @@ class RandomWalk(ABC):
                     _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d['col_sorted']),
                                  _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                                 _native.ptr(d['adj_hpos']), self._csr.vocab_size,
-                                 _native.ptr(starts), n, L, float(p), float(q),
+                                 _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
+                                 _native.ptr(d['hub_bits']), d['hub_words'],
+                                 self._csr.vocab_size, _native.ptr(starts), n, L, float(p),
+                                 float(q),
                                  _native.ptr(u) if u.numel() else None, _native.ptr(out),
                                  _native.ptr(status), None, s)
                 else:
@@ -295,7 +298,8 @@ class RandomWalk(ABC):
         u = torch.as_tensor(uniforms).reshape(-1).to(device=dev, dtype=torch.float64).contiguous()
         if u.numel() != n * (L - 1):
             raise ValueError('uniforms must have n_walks * (length - 1) values')
-        d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True)
+        d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True,
+                                     need_hub_bits=True)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -305,8 +309,10 @@ class RandomWalk(ABC):
             _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
                          _native.ptr(d['col']), _native.ptr(d['col_sorted']),
                          _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                         _native.ptr(d['adj_hpos']), self._csr.vocab_size, _native.ptr(starts),
-                         n, L, float(p), float(q), _native.ptr(u) if u.numel() else None,
+                         _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
+                         _native.ptr(d['hub_bits']), d['hub_words'], self._csr.vocab_size,
+                         _native.ptr(starts), n, L, float(p), float(q),
+                         _native.ptr(u) if u.numel() else None,
                          _native.ptr(out), _native.ptr(status), _native.ptr(counters),
                          _native.stream(dev))
         _native.check_status(status, f'{type(self).__name__}.count_replay_traffic')

@@ -200,10 +200,19 @@ int dw_walk_replay_inline(const int64_t *row_ptr, const int32_t *edges, int64_t 
  * the walk roofline (bench.py). Replaces random_walk_generator.py:94-119 on unweighted graphs. */
 int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                            const int64_t *adj_off, const int32_t *adj_hash,
-                           const int32_t *adj_hpos, int64_t n_rows, const int32_t *starts,
-                           int64_t n_walks, int32_t walk_length, double p, double q,
-                           const double *uniforms, int32_t *out, int32_t *status,
+                           const int32_t *adj_hpos, const int32_t *hub_idx,
+                           const uint32_t *hub_bits, int64_t hub_words, int64_t n_rows,
+                           const int32_t *starts, int64_t n_walks, int32_t walk_length, double p,
+                           double q, const double *uniforms, int32_t *out, int32_t *status,
                            uint64_t *counters, void *stream);
+
+/* Neighbour bitmaps of hub rows for dw_walk_replay_indexed (hub_idx / hub_bits; NULL = none):
+ * bits[k * hub_words + (x >> 5)] bit (x & 31) = x in N(hub_rows[k]); hub_words >=
+ * ceil(n_rows / 32). A test of a neighbour of v against a hub prev too long for LDS is then one
+ * 4-B load instead of a binary search of its sorted list. */
+int dw_hub_bitmaps(const int64_t *row_ptr, const int32_t *col, int64_t n_rows,
+                   const int32_t *hub_rows, int64_t n_hubs, int64_t hub_words, uint32_t *bits,
+                   void *stream);
 
 /* Fast walker (Philox4x32-10 keyed by (seed, walk_id0 + w, step, round/lane)); walks are a pure
  * function of (seed, global walk id), identical for any grid and any number of GPUs.
