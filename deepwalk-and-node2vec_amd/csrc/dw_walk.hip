@@ -628,17 +628,20 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             const int32_t *np_g = nullptr;
             int64_t np_g_n = 0;
             const uint32_t *np_bits = nullptr;
-            if (c.node2vec && prev >= 0 && pn > NCAP && ix.hub_idx) {
+            if (c.node2vec && prev >= 0 && ix.hub_idx) {
                 const int32_t hb = ix.hub_idx[prev];
                 if (hb >= 0) np_bits = ix.hub_bits + hb * ix.hub_words;
             }
             if (c.node2vec && prev >= 0) {
                 if (counted && lane == 0)   // N(v) read; N(prev) staged, bit-tested or searched
                     loads += static_cast<uint32_t>(
-                        n + (pn <= NCAP ? pn
-                                        : np_bits ? n
+                        n + (np_bits ? n
+                                     : pn <= NCAP ? pn
                                                   : n * static_cast<int64_t>(ceil_log2(pn + 1))));
-                if (pn <= NCAP) {
+                if (np_bits) {
+                    np_g = c.col_sorted + pa;   // (the serial fallback's search)
+                    np_g_n = pn;
+                } else if (pn <= NCAP) {
                     for (int64_t e = lane; e < pn; e += WAVE) nprev_lds[e] = c.col_sorted[pa + e];
                     dw::wave_lds_sync();
                     np_lds = nprev_lds;

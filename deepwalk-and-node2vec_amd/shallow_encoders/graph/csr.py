@@ -247,9 +247,10 @@ class CSRGraph:
         V = self.vocab_size
         words = (V + 31) // 32
         budget = int(os.environ.get('DW_HUB_BITS_BYTES', self.HUB_BITS_BYTES))
+        min_deg = int(os.environ.get('DW_HUB_MIN_DEGREE', self.HUB_MIN_DEGREE))
         deg = d['row_ptr'][1:] - d['row_ptr'][:-1]
         order = torch.argsort(deg, descending=True)
-        n_big = int((deg > self.HUB_MIN_DEGREE).sum())
+        n_big = int((deg > min_deg).sum())
         n_hubs = max(0, min(n_big, budget // max(1, words * 4)))
         hubs = order[:n_hubs].to(torch.int32).contiguous()
         idx = torch.full((V,), -1, dtype=torch.int32, device=dev)
