@@ -795,6 +795,19 @@ def main():
                                       'kernel_ms': kern_s * 1e3, 'uniforms_ms': gen_s * 1e3,
                                       'uniforms_GBps': u_dev.numel() * 8 / gen_s / 1e9,
                                       'walks_per_s_host_uniforms': n_r / dt_host}
+                if meth == 'node2vec':
+                    # the bit-exact walker's realised traffic (dw_walk_replay_indexed counted:
+                    # row pairs, uniform, pick, output per step; every list entry read; every
+                    # 64-B hash bucket probed), same walks, untimed launch
+                    c = w.count_replay_traffic(st_dev, u_dev, out=out)
+                    gbs = c['bytes'] / kern_s / 1e9
+                    walk_roof['node2vec_replay'] = {
+                        'kernel_ms': kern_s * 1e3, 'walks': n_r, 'bytes': c['bytes'],
+                        'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': gbs / HBM_PEAK_GBS, 'p': p, 'q': q,
+                        'bytes_per_step': c['bytes'] / max(c['steps'], 1),
+                        'hash_probes_per_step': c['probes'] / max(c['steps'], 1),
+                        'list_entries_per_step': c['entries'] / max(c['steps'], 1)}
                 del out, u_dev, u
 
     result = {
