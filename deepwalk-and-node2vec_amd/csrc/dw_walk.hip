@@ -325,10 +325,52 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
         }
     } else {
     // first pass, 4 rounds per trip: the four membership searches are independent, so their
-    // dependent load chains overlap (branchless lower_bound over the same sorted N(prev))
+    // dependent load chains overlap (branchless lower_bound over the same sorted N(prev));
+    // 32-bit index arithmetic when N(prev) is staged in LDS
     constexpr int RB = 4;
-    const int32_t *ns = np_lds ? np_lds : np_g;
-    const int64_t nn = np_lds ? static_cast<int64_t>(np_lds_n) : np_g_n;
+    auto tally = [&](int64_t r, bool is_p, bool is_q) {
+        const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
+        if (r < rounds) {
+            if (r < cap && lane == 0) {
+                masks[2 * r] = mp;
+                masks[2 * r + 1] = mq;
+            }
+            A += __popcll(mp);
+            C += __popcll(mq);
+        }
+    };
+    if (np_lds) {
+        const int nn = np_lds_n;
+        for (int64_t r0 = 0; r0 < rounds; r0 += RB) {
+            int32_t x[RB];
+            int base[RB];
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+                const int64_t i = (r0 + j) * WAVE + lane;
+                x[j] = i < n ? c.col[a + i] : prev;  // past the row: counted as neither class
+                base[j] = 0;
+            }
+            int len = nn;
+            while (len > 1) {
+                const int half = len >> 1;
+#pragma unroll
+                for (int j = 0; j < RB; ++j)
+                    base[j] = (np_lds[base[j] + half] < x[j]) ? base[j] + half : base[j];
+                len -= half;
+            }
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+                const int64_t r = r0 + j;
+                const bool in_row = r * WAVE + lane < n;
+                const bool is_p = in_row && x[j] == prev;
+                int lb = base[j];
+                if (nn > 0 && np_lds[lb] < x[j]) ++lb;
+                tally(r, is_p, in_row && !is_p && lb < nn && np_lds[lb] == x[j]);
+            }
+        }
+    } else {
+    const int32_t *ns = np_g;
+    const int64_t nn = np_g_n;
     for (int64_t r0 = 0; r0 < rounds; r0 += RB) {
         int32_t x[RB];
         int64_t base[RB];
@@ -349,22 +391,13 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
             const int64_t r = r0 + j;
-            const int64_t i = r * WAVE + lane;
-            const bool in_row = i < n;
+            const bool in_row = r * WAVE + lane < n;
             const bool is_p = in_row && x[j] == prev;
             int64_t lb = base[j];
             if (nn > 0 && ns[lb] < x[j]) ++lb;
-            const bool is_q = in_row && !is_p && lb < nn && ns[lb] == x[j];
-            const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
-            if (r < rounds) {
-                if (r < cap && lane == 0) {
-                    masks[2 * r] = mp;
-                    masks[2 * r + 1] = mq;
-                }
-                A += __popcll(mp);
-                C += __popcll(mq);
-            }
+            tally(r, is_p, in_row && !is_p && lb < nn && ns[lb] == x[j]);
         }
+    }
     }
     }
     dw::wave_lds_sync();
@@ -388,6 +421,16 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
         }
         const int64_t base = r * WAVE;
         const int64_t in_round = n - base < WAVE ? n - base : WAVE;
+        {   // the round's last D from its counts (wave-uniform): no crossing in it -> next round
+            const int64_t ea = na + __popcll(mp), ec = nc + __popcll(mq);
+            const double d_end = W(ea, (base + in_round) - ea - ec, ec) - UT;
+            if (!(d_end > 0.0)) {
+                d_prev = d_end;
+                na = ea;
+                nc = ec;
+                continue;
+            }
+        }
         const uint64_t le = (lane == WAVE - 1) ? ~0ull : ((2ull << lane) - 1);  // lanes <= lane
         const int64_t pa = na + __popcll(mp & le), pc = nc + __popcll(mq & le);
         const int64_t i = base + lane;
@@ -1357,7 +1400,7 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
     static const int32_t b_factor = [] {
         const char *e = getenv("DW_N2V_BFACTOR");
         const int f = e ? atoi(e) : 0;
-        return f > 0 ? f : 4;
+        return f > 0 ? f : 16;
     }();
     DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
                "dw_walk_replay_indexed: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
