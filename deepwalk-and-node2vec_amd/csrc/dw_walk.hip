@@ -327,7 +327,10 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
     // first pass, 4 rounds per trip: the four membership searches are independent, so their
     // dependent load chains overlap (branchless lower_bound over the same sorted N(prev));
     // 32-bit index arithmetic when N(prev) is staged in LDS
-    constexpr int RB = 4;
+#ifndef DW_N2V_RB
+#define DW_N2V_RB 4
+#endif
+    constexpr int RB = DW_N2V_RB;
     auto tally = [&](int64_t r, bool is_p, bool is_q) {
         const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
         if (r < rounds) {
