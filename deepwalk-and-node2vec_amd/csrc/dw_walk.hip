@@ -271,7 +271,9 @@ __global__ void __launch_bounds__(256)
 // node2vec, unweighted, one wave per walker: the class of every neighbour (x == prev, x in
 // N(prev), other) in rounds of 64 as two ballots, the class counts give T, and the round and
 // lane where W crosses U*T give the pick. Returns -1 (serial replay) where the margin fails.
-// `masks`: this wave's LDS (2 * cap u64); rows past cap rounds re-classify in the second pass.
+// `masks`: this wave's LDS, one u64 per round (the common-neighbour ballot; x == prev happens at
+// most once in a simple graph, so its position is kept instead), cap rounds; rounds past cap
+// re-classify in the second pass.
 __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n, int32_t prev,
                                        const int32_t *np_lds, int np_lds_n,
                                        const int32_t *np_g, int64_t np_g_n, double U,
@@ -294,8 +296,20 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
         mq = __ballot(is_q);
     };
     int64_t A = 0, C = 0;
+    int64_t pos_p = -1;   // the position of prev in N(v) (bisected rounds: from the ballots)
+    auto tally = [&](int64_t r, bool is_p, bool is_q) {
+        const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
+        if (r < rounds) {
+            if (r < cap && lane == 0) masks[r] = mq;
+            if (mp) pos_p = r * WAVE + (__ffsll((unsigned long long)mp) - 1);
+            A += __popcll(mp);
+            C += __popcll(mq);
+        }
+    };
     if (np_bits) {   // prev's neighbour bitmap (a hub): one 4-B load per test, no search
-        constexpr int RBB = 4;   // rounds per trip: their loads in flight together
+        // rounds per trip: their col and bitmap loads in flight together (a hub-to-hub step
+        // classifies up to ~700 rounds: the walk's critical path)
+        constexpr int RBB = 16;
         for (int64_t r0 = 0; r0 < rounds; r0 += RBB) {
             int32_t x[RBB];
             uint32_t w[RBB];
@@ -311,16 +325,7 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
                 const int64_t r = r0 + j;
                 const bool in_row = r * WAVE + lane < n;
                 const bool is_p = in_row && x[j] == prev;
-                const bool is_q = in_row && !is_p && ((w[j] >> (x[j] & 31)) & 1u) != 0u;
-                const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
-                if (r < rounds) {
-                    if (r < cap && lane == 0) {
-                        masks[2 * r] = mp;
-                        masks[2 * r + 1] = mq;
-                    }
-                    A += __popcll(mp);
-                    C += __popcll(mq);
-                }
+                tally(r, is_p, in_row && !is_p && ((w[j] >> (x[j] & 31)) & 1u) != 0u);
             }
         }
     } else {
@@ -331,17 +336,6 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
 #define DW_N2V_RB 4
 #endif
     constexpr int RB = DW_N2V_RB;
-    auto tally = [&](int64_t r, bool is_p, bool is_q) {
-        const uint64_t mp = __ballot(is_p), mq = __ballot(is_q);
-        if (r < rounds) {
-            if (r < cap && lane == 0) {
-                masks[2 * r] = mp;
-                masks[2 * r + 1] = mq;
-            }
-            A += __popcll(mp);
-            C += __popcll(mq);
-        }
-    };
     if (np_lds) {
         const int nn = np_lds_n;
         for (int64_t r0 = 0; r0 < rounds; r0 += RB) {
@@ -417,8 +411,8 @@ __device__ int64_t node2vec_pick_exact(const ReplayCtx &c, int64_t a, int64_t n,
     for (int64_t r = 0; r < rounds; ++r) {
         uint64_t mp, mq;
         if (r < cap) {
-            mp = masks[2 * r];
-            mq = masks[2 * r + 1];
+            mq = masks[r];
+            mp = (pos_p >= r * WAVE && pos_p < (r + 1) * WAVE) ? (1ull << (pos_p - r * WAVE)) : 0ull;
         } else {
             classify(r, mp, mq);
         }
@@ -614,13 +608,18 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
                   int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
-    __shared__ double s_buf[REPLAY_WAVES][CH];
-    __shared__ int32_t s_nprev[REPLAY_WAVES][NCAP];
+    // per wave: CH doubles (the serial replay's weights / the exact picks' ballots) followed by
+    // the NCAP-entry N(prev) stage; the ballots take both halves when nothing is staged
+    __shared__ uint64_t s_lds[REPLAY_WAVES][CH + NCAP / 2];
     __shared__ int64_t s_pick[REPLAY_WAVES];
+#ifdef DW_REPLAY_PAD_LDS   // occupancy experiments only
+    __shared__ int32_t s_pad[DW_REPLAY_PAD_LDS];
+    if (threadIdx.x == 0) s_pad[0] = 0;
+#endif
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
-    double *buf = s_buf[wv];
-    int32_t *nprev_lds = s_nprev[wv];
+    double *buf = reinterpret_cast<double *>(s_lds[wv]);
+    int32_t *nprev_lds = reinterpret_cast<int32_t *>(s_lds[wv] + CH);
     const int64_t n_waves = (int64_t)gridDim.x * REPLAY_WAVES;
     const bool counted = ix.counters != nullptr;
     uint32_t probes = 0, loads = 0, steps = 0;   // counted launches only
@@ -703,7 +702,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                         ? uniform_pick_exact(uu, n)
                         : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, uu,
                                               reinterpret_cast<uint64_t *>(buf),
-                                              CH / 2, lane, np_bits);
+                                              np_lds ? CH : CH + NCAP / 2, lane, np_bits);
                 if (fp >= 0) {
                     const int32_t child = c.col[a + fp];
                     if (lane == 0) o[s] = child;
