@@ -178,22 +178,38 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
-// STREAM copy (the "measured HBM roofline" of SURVEY.md §8d / BASELINE.md): dst = src in 16-B
-// lanes, four loads in flight per lane before the stores; bench.py times it once per run and
-// reports the SGNS step against it beside the 8 TB/s spec figure.
+// STREAM copy (the "measured HBM roofline" of SURVEY.md §8d / BASELINE.md): dst = src. Each
+// block copies one tile of 256 x 4 float4 (all four loads in flight before the stores) with
+// non-temporal loads and stores, and the grid covers the array. Of the shapes measured on MI355X
+// (scripts/microbench/copy_rates.hip, profiles/r03_copy_rates.jsonl) this one is the fastest:
+// 6.17 TB/s for 2 GiB, against 4.62 for a grid-stride loop of 8 blocks per CU (the round-3
+// first version) and 4.96 for hipMemcpyAsync. bench.py times it once per run and reports the
+// SGNS step against it beside the 8 TB/s spec figure.
 __global__ void __launch_bounds__(256)
     k_stream_copy(const float4 *__restrict__ src, float4 *__restrict__ dst, int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
-                     d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+    constexpr int U = 4;
+    const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+    float4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + u * 256;
+        if (i < n4) {
+            r[u].x = __builtin_nontemporal_load(&src[i].x);
+            r[u].y = __builtin_nontemporal_load(&src[i].y);
+            r[u].z = __builtin_nontemporal_load(&src[i].z);
+            r[u].w = __builtin_nontemporal_load(&src[i].w);
+        }
     }
-    for (; i < n4; i += stride) dst[i] = src[i];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + u * 256;
+        if (i < n4) {
+            __builtin_nontemporal_store(r[u].x, &dst[i].x);
+            __builtin_nontemporal_store(r[u].y, &dst[i].y);
+            __builtin_nontemporal_store(r[u].z, &dst[i].z);
+            __builtin_nontemporal_store(r[u].w, &dst[i].w);
+        }
+    }
 }
 
 extern "C" {
@@ -204,13 +220,9 @@ int dw_stream_copy(const void *src, void *dst, int64_t bytes, void *stream) {
     DW_REQUIRE(src && dst, "dw_stream_copy: null pointer");
     DW_REQUIRE((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16 == 0,
                "dw_stream_copy: buffers must be 16-B aligned");
-    int dev = 0, n_cu = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        n_cu = 256;
     const int64_t n4 = bytes / 16;
-    int64_t blocks = (int64_t)n_cu * 8;
-    if (blocks * 256 > n4) blocks = (n4 + 255) / 256;
+    const int64_t blocks = (n4 + 1023) / 1024;
+    DW_REQUIRE(blocks <= 0x7FFFFFFF, "dw_stream_copy: %lld bytes is too large", (long long)bytes);
     hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
                        reinterpret_cast<const float4 *>(src), reinterpret_cast<float4 *>(dst), n4);
     DW_LAUNCH_CHECK("dw_stream_copy");

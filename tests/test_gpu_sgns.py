@@ -228,6 +228,20 @@ def test_adam_dense_to_equals_in_place(hip_device, max_blocks):
     assert float(b[1].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize('n16', [1, 1023, 1024, 1025, 300_001])
+def test_stream_copy_copies_exactly(hip_device, n16):
+    """dw_stream_copy (bench.py's measured copy roofline) copies every 16-B lane of ragged sizes
+    (a partial last tile) and nothing beyond them."""
+    n = n16 * 4
+    src = torch.randn(n + 8, device=hip_device)
+    dst = torch.full((n + 8,), -7.0, device=hip_device)
+    _native.call('dw_stream_copy', _native.ptr(src), _native.ptr(dst), n * 4,
+                 _native.stream(hip_device))
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:n], src[:n])
+    assert bool((dst[n:] == -7.0).all())
+
+
 @pytest.mark.parametrize('fuse', [True, False])
 def test_overlapped_in_table_adam_equals_serial(hip_device, fuse):
     """One GPU: the in-table Adam on the side stream into the second buffer (overlap_in) gives
