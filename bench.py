@@ -247,9 +247,10 @@ def main():
                          'under 10%% of the rows of a table of >= 1 GB of Adam bytes (C5: 3.4%% '
                          'of 16.8M rows; C3: 55%%, where dense measured faster)')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
-                    help='one GPU, replicated step: replay it as a HIP graph with the per-step '
-                         'scalars in device memory (word2vec/graphed.py); auto = for batches of '
-                         '<= 100K centres, where the step is launch-bound (C2 shape)')
+                    help='one GPU: replay the step (replicated, or the lazy owner step) as a HIP '
+                         'graph with the per-step scalars in device memory (word2vec/graphed.py); '
+                         'auto = for batches of <= 100K centres, where the step is launch-bound '
+                         '(the C2 shape; C3 at the reference\'s 64-walk batch)')
     ap.add_argument('--lazy-out', default='auto', choices=['auto', 'on', 'off'],
                     help='lazy in-table exchange: keep the out slice\'s Adam lazy (exact) too; '
                          'auto = when a step\'s records touch under ~half of the slice\'s rows '
@@ -593,7 +594,20 @@ def main():
     # small batches on one GPU: the step replayed as a HIP graph (word2vec/graphed.py)
     graphed = None
     use_graph = graph_small and (fuse or args.scatter == 'atomic')
-    if use_graph:
+    # the one-GPU lazy owner step (the reference's 64-walk batch on a large graph) likewise
+    graph_owner = (n1_lazy and args.graph != 'off'
+                   and (args.graph == 'on' or B * (L - 2 * R) <= 100_000))
+    if graph_owner:
+        from shallow_encoders.word2vec.graphed import GraphedOwnerStep
+        unroll = (args.graph_unroll if args.graph_unroll > 0 else
+                  next(u for u in (16, 8, 4, 2, 1) if args.steps % u == 0))
+        if args.steps % unroll:
+            raise SystemExit(f'--graph-unroll {unroll} must divide --steps {args.steps}')
+        graphed = GraphedOwnerStep(tables, walker, epoch_starts, B, R, K, seed=99,
+                                   grad_scale=grad_scale, loss_acc=loss_acc, status=status,
+                                   first_walk_id=step_idx[0] * BG, n_steps=args.steps + 1,
+                                   unroll=unroll)
+    elif use_graph:
         from shallow_encoders.word2vec.graphed import GraphedStep
         # several steps per graph: between replays the launch gap (~19 us) is as long as a
         # tiny step; the unroll divides --steps so exactly --steps steps are timed

@@ -108,7 +108,8 @@ __global__ void __launch_bounds__(512)
                 int32_t *__restrict__ last, int64_t n_table, int32_t d,
                 const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
                 int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
-                int32_t step) {
+                int32_t step_arg, const dw_step_scalars *__restrict__ dyn, int32_t delta) {
+    const int32_t step = dw::eff_step(dyn, delta, step_arg);   // graph replay: from the block
     const int e = threadIdx.x;
     const bool live = e < d;
     int64_t n = n_max;
@@ -280,17 +281,23 @@ int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_
     DW_REQUIRE(rows || !n_rows_dev, "dw_adam_rows: a device row count needs a row list");
     DW_REQUIRE(!grad_rows || step >= 1, "dw_adam_rows: a gradient step needs step >= 1");
     DW_REQUIRE(dim <= 512, "dw_adam_rows: dim > 512 is not supported");
+    const dw_step_scalars *dyn = nullptr;
+    int32_t delta = 0;
+    const int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_adam_rows");
+    if (rc != DW_OK) return rc;
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
     const int threads = 64 * ((dim + 63) / 64);
     if (grad_rows)
         hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0,
                            dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
-                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
+                           dyn, delta);
     else
         hipLaunchKernelGGL((k_rows_adam<false>), dim3((unsigned)blocks), dim3(threads), 0,
                            dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
-                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step);
+                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
+                           dyn, delta);
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
 }

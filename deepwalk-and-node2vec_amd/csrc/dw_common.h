@@ -15,6 +15,20 @@ void set_error(const char *fmt, ...);
 // The dw_step_scalars block bound on this host thread (dw_step_scalars_bind), or NULL.
 const dw_step_scalars *bound_step_scalars();
 
+// Lazy-Adam launches (dw_adam_rows, dw_sgns_owner_out_catch_up, dw_sgns_owner_pass2_lazy) take an
+// Adam step number. With a block bound by dw_step_scalars_bind_at(dev, host_step) their `step`
+// argument is relative to it: the kernels use dyn->step + (step - host_step), read on the
+// device. Returns DW_OK and sets *dyn / *delta (dyn NULL: nothing bound, use `step`), or
+// DW_E_INVALID_ARG when a block is bound without a host step (dw_step_scalars_bind): a captured
+// lazy step would otherwise replay a frozen step number.
+int bound_step_rel(int64_t step, const dw_step_scalars **dyn, int32_t *delta, const char *what);
+
+// The step a lazy kernel applies: the bound block's (plus the launch's delta) or the launch's.
+__device__ __forceinline__ int32_t eff_step(const dw_step_scalars *dyn, int32_t delta,
+                                            int32_t step) {
+    return dyn ? static_cast<int32_t>(dyn->step) + delta : step;
+}
+
 #define DW_REQUIRE(cond, ...)                 \
     do {                                      \
         if (!(cond)) {                        \

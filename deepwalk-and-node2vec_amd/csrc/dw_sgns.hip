@@ -697,13 +697,14 @@ struct OutAdam {
     const float *hist = nullptr;
     int32_t step = 0;
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
+    int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
-// `oa.step` with g (registers), record the step.
+// `step` (oa.step, or the bound block's) with g (registers), record the step.
 template <int VPL, bool MASKED>
-__device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, int32_t d,
-                                              int lane, const float (&g)[VPL]) {
+__device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, uint32_t row,
+                                              int32_t d, int lane, const float (&g)[VPL]) {
     // (row is wave-uniform; lanes past d carry zeros through a uniform replay loop)
     const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
     const int64_t o = static_cast<int64_t>(row) * d + lane;
@@ -717,7 +718,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, i
         vv[m] = live ? oa.v[i] : 0.f;
         gg[m] = g[m];
     }
-    for (int32_t t = from + 1; t < oa.step; ++t) {
+    for (int32_t t = from + 1; t < step; ++t) {
         const dw::AdamScalars h = dw::hist_at(oa.hist, t);
         if (h.wd == 0.f) {
 #pragma unroll
@@ -730,7 +731,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, i
             }
         }
     }
-    const dw::AdamScalars h = dw::hist_at(oa.hist, oa.step);
+    const dw::AdamScalars h = dw::hist_at(oa.hist, step);
 #pragma unroll
     for (int m = 0; m < VPL; ++m) {
         if (MASKED && lane + WAVE * m >= d) continue;
@@ -740,7 +741,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, uint32_t row, i
         oa.m[i] = mm[m];
         oa.v[i] = vv[m];
     }
-    if (lane == 0) oa.last[row] = oa.step;
+    if (lane == 0) oa.last[row] = step;
 }
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
@@ -756,6 +757,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     const int64_t hi = range ? range[1] : n_rec;
     const int64_t n_chunks = (hi - lo + gch - 1) / gch;
     const dw::AdamScalars sc = ADAM ? dw::step_adam(oa.dyn, oa.s) : oa.s;
+    const int32_t lstep = dw::eff_step(oa.dyn, oa.step_delta, oa.step);   // lazy form's step
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     bool live[VPL];
 #pragma unroll
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             float *dst = g_out + static_cast<int64_t>(row) * d + lane;
             if (row != before && row != after) {
                 if (ADAM && oa.last) {
-                    lazy_row_step<VPL, MASKED>(oa, row, d, lane, g);
+                    lazy_row_step<VPL, MASKED>(oa, lstep, row, d, lane, g);
                 } else if (ADAM) {
                     const int64_t o = static_cast<int64_t>(row) * d + lane;
 #pragma unroll
@@ -1083,7 +1085,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             g[m] = g_out[o + WAVE * m];
             g_out[o + WAVE * m] = 0.f;
         }
-        lazy_row_step<VPL, MASKED>(oa, row, d, lane, g);
+        lazy_row_step<VPL, MASKED>(oa, dw::eff_step(oa.dyn, oa.step_delta, oa.step), row, d,
+                                   lane, g);
     }
 }
 
@@ -1906,8 +1909,9 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // the wave appends its claimed rows to `list` with one counter atomic. dw_adam_rows then
 // replays the listed rows, all in parallel.
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step,
+    k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
+    const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
     // one centre per wave; the block's claimed rows are appended with ONE counter atomic (a
     // same-address atomic per wave serialised: 4,480 of them were ~40 us at the 64-walk batch)
     __shared__ uint32_t s_cnt[WAVES_PER_BLOCK];
@@ -1972,6 +1976,10 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                    n_rows && hist && status,
                "dw_sgns_owner_out_catch_up: null pointer");
     hipStream_t st = dw::as_stream(stream);
+    const dw_step_scalars *dyn = nullptr;
+    int32_t delta = 0;
+    int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_sgns_owner_out_catch_up");
+    if (rc != DW_OK) return rc;
     SgnsArgs a = base_args(vocab_size, dim, neg_samples, nullptr, w_out_local, nullptr, nullptr,
                            noise, seed, noise_offset, 0.f, nullptr, status);
     a.walks = walks;
@@ -1989,7 +1997,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, claim, step, rows_buf, reinterpret_cast<unsigned long long *>(n_rows));
+                       a, claim, step, delta, rows_buf,
+                       reinterpret_cast<unsigned long long *>(n_rows));
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
@@ -2241,6 +2250,8 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
+    const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
+    if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,

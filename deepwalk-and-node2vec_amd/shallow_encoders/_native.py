@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -128,6 +128,7 @@ SIGNATURES = {
                                          _f32, _f32, _i32, _i64, _p]),
     'dw_scale': (ctypes.c_int, [_p, _i64, _f32, _p, _p]),
     'dw_step_scalars_bind': (ctypes.c_int, [_p]),
+    'dw_step_scalars_bind_at': (ctypes.c_int, [_p, _i64]),
     'dw_step_scalars_advance': (ctypes.c_int, [_p, _p, _i64, _u64, _u64, _p, _p, _i64, _p,
                                                _i64, _p]),
     'dw_step_starts': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),

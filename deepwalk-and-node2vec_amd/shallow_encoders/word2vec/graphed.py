@@ -23,7 +23,8 @@ import numpy as np
 import torch
 
 from shallow_encoders import _native
-from shallow_encoders.word2vec.sharding import ShardedTables, adam_scalars, replicated_step
+from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables, adam_scalars,
+                                                owner_lazy_step, replicated_step)
 
 _STEP_DTYPE = np.dtype([('walk_id0', '<u8'), ('noise_offset', '<u8'), ('step', '<i8'),
                         ('adam', '<f4', (8,))])   # == dw_step_scalars (56 bytes)
@@ -169,6 +170,131 @@ class GraphedStep:
         if self._flips:
             t._next_in = 2 - t._cur_in
             t._cur_in = t._next_in
+
+    def scalars(self) -> dict:
+        """The device block (synchronises): walk_id0, noise_offset, step."""
+        b = np.frombuffer(self.block.cpu().numpy().tobytes(), dtype=_STEP_DTYPE)[0]
+        return {'walk_id0': int(b['walk_id0']), 'noise_offset': int(b['noise_offset']),
+                'step': int(b['step'])}
+
+
+class GraphedOwnerStep:
+    """``owner_lazy_step`` on one GPU (OwnerLazyTables: the lazy exact Adam of the in table, and
+    of the out table with ``lazy_out``) replayed as a HIP graph, with the walker in front of it:
+    the reference's own batch shape on a large graph (C3 at 64 walks per step), where a step is
+    ~40 kernel launches of a few microseconds each.
+
+    As GraphedStep, what changes from step to step lives in the bound dw_step_scalars blocks
+    (walk ids, the negatives' centre counter, the Adam scalars); the lazy kernels' step numbers
+    (catch-ups, the out rows' claims, the lazy gather, the touched rows' update) are bound
+    relative to each block (dw_step_scalars_bind_at), so the replays advance them on the device.
+    The tables' Adam-scalar history is written ahead for ``n_steps`` steps before the capture,
+    so begin_step copies nothing inside it.
+
+    The tables must have run one eager step at this batch shape first (it allocates the
+    touched-row, gather and workspace buffers the capture then reuses); the walker's device
+    tensors are built here by one eager launch into a scratch buffer, and its walk-id counter
+    is left where it was."""
+
+    def __init__(self, tables: OwnerLazyTables, walker, epoch_starts: torch.Tensor, B: int,
+                 context_radius: int, neg_samples: int, *, seed: int, grad_scale: float,
+                 loss_acc: torch.Tensor, status: torch.Tensor, first_walk_id: int,
+                 n_steps: int, unroll: int = 1):
+        if not isinstance(tables, OwnerLazyTables) or tables.multi or tables.world != 1 \
+                or not tables._hip():
+            raise ValueError('GraphedOwnerStep: one GPU, OwnerLazyTables with the HIP Adam')
+        if tables._touched is None or tables._G is None or tables.step_count < 1:
+            raise ValueError('GraphedOwnerStep: run one eager owner_lazy_step at this batch shape '
+                             'first (it allocates the buffers the capture reuses)')
+        if epoch_starts.dtype != torch.int32 or epoch_starts.device != tables.device:
+            raise ValueError('GraphedOwnerStep: epoch_starts must be int32 on the tables\' device')
+        if unroll < 1:
+            raise ValueError('GraphedOwnerStep: unroll must be >= 1')
+        if getattr(walker, '_rng', None) != 'philox':
+            raise ValueError("GraphedOwnerStep: the walker must be a Philox walker (rng='philox')")
+        self.unroll = int(unroll)
+        self.t, self.walker = tables, walker
+        dev = tables.device
+        L = walker.length
+        R, K = int(context_radius), int(neg_samples)
+        self.R, self.K = R, K
+        self.B, self.centres = int(B), int(B) * (L - 2 * R)
+        self.status, self.loss_acc, self.epoch_starts = status, loss_acc, epoch_starts
+        self.seed, self.grad_scale = int(seed), float(grad_scale)
+        self.walks = torch.empty((self.unroll * self.B, L), dtype=torch.int32, device=dev)
+        self.starts = torch.empty(self.unroll * self.B, dtype=torch.int32, device=dev)
+        s1 = tables.step_count + 1
+        self._last = s1 + int(n_steps) + self.unroll   # history rows the replays may read
+        tables.reserve_history(self._last)
+        self._key = tables._hist_key
+        hist = tables._hist
+        self._hist_ptr = hist.data_ptr()   # captured by the graph's kernels
+        blk = np.zeros(1, dtype=_STEP_DTYPE)
+        blk['walk_id0'] = first_walk_id
+        blk['noise_offset'] = first_walk_id * (L - 2 * R)
+        blk['step'] = s1
+        blk['adam'][0] = hist[s1].cpu().numpy()
+        self.block = torch.from_numpy(np.frombuffer(blk.tobytes(), dtype=np.uint8).copy()).to(dev)
+        self.step_blocks = torch.zeros(self.unroll * _STEP_DTYPE.itemsize, dtype=torch.uint8,
+                                       device=dev)
+        next_wid = walker._next_walk_id
+        n_warm = min(self.B, int(epoch_starts.numel()))
+        walker.walk_batch(epoch_starts[:n_warm], walk_id0=int(first_walk_id),
+                          out=torch.empty((n_warm, L), dtype=torch.int32, device=dev),
+                          check=False, status=torch.zeros(1, dtype=torch.int32, device=dev))
+        walker._next_walk_id = next_wid
+        torch.cuda.synchronize(dev)
+        steps0, lr0 = tables.step_count, len(tables._lr_hist)
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode='relaxed'):
+                self._body()
+        finally:
+            _native.call('dw_step_scalars_bind', None)
+            tables.step_count = steps0          # the capture ran no step
+            del tables._lr_hist[lr0:]
+            walker._next_walk_id = next_wid
+        torch.cuda.synchronize(dev)
+
+    def _step_blk(self, k: int) -> int:
+        return self.step_blocks.data_ptr() + k * _STEP_DTYPE.itemsize
+
+    def _body(self) -> None:
+        t, dev, B = self.t, self.t.device, self.B
+        with torch.cuda.device(dev):
+            _native.call('dw_step_scalars_expand', _native.ptr(self.block), self._step_blk(0),
+                         self.unroll, _native.ptr(t._hist), self._last + 1, B, self.centres,
+                         _native.ptr(self.status), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
+                         _native.stream(dev))
+        _native.call('dw_step_scalars_bind', self._step_blk(0))
+        self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
+                               status=self.status)
+        for k in range(self.unroll):
+            # the step numbers the lazy kernels get are relative to block k's (begin_step, inside
+            # owner_lazy_step, makes the host's count step_count + 1)
+            _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count + 1)
+            owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
+                            noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
+                            status=self.status)
+
+    def replay(self) -> None:
+        """``unroll`` training steps (enqueued on the current stream); the tables' host
+        bookkeeping (Adam step count) follows as the eager steps' would."""
+        t = self.t
+        if (t.lr, tuple(t.betas), t.eps, t.weight_decay) != self._key:
+            raise RuntimeError('GraphedOwnerStep: the Adam hyper-parameters changed since the '
+                               'capture; build a new GraphedOwnerStep')
+        if t._hist.data_ptr() != self._hist_ptr:
+            raise RuntimeError('GraphedOwnerStep: the tables\' Adam-scalar history was '
+                               'reallocated since the capture; build a new GraphedOwnerStep')
+        if t.step_count + self.unroll > self._last - self.unroll:
+            raise RuntimeError(f'GraphedOwnerStep: the Adam-scalar history covers steps up to '
+                               f'{self._last - self.unroll}; build a new GraphedOwnerStep '
+                               f'(n_steps) to go on')
+        self.graph.replay()
+        t.step_count += self.unroll
+        t._lr_hist.extend([t.lr] * self.unroll)
 
     def scalars(self) -> dict:
         """The device block (synchronises): walk_id0, noise_offset, step."""

@@ -830,20 +830,34 @@ class OwnerLazyTables(OwnerTables):
         s = self.step_count
         key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
         if s > self._hist_ready or key != self._hist_key:
-            hi = s + HIST_AHEAD - 1
-            if hi >= self._hist.shape[0]:
-                cap = max(2 * self._hist.shape[0], hi + 1)
-                h = torch.zeros((cap, 8), dtype=torch.float32, device=self.device)
-                h[:self._hist.shape[0]] = self._hist
-                hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
-                hh[:self._hist_host.shape[0]] = self._hist_host
-                self._hist, self._hist_host = h, hh
-            rows = [adam_scalars(t, self.lr, self.betas, self.eps, self.weight_decay)
-                    for t in range(s, hi + 1)]
-            self._hist_host[s:hi + 1, :7] = torch.tensor(rows, dtype=torch.float32)
-            self._hist[s:hi + 1].copy_(self._hist_host[s:hi + 1], non_blocking=True)
-            self._hist_ready, self._hist_key = hi, key
+            self._write_hist(s, s + HIST_AHEAD - 1)
         self._lr_hist.append(self.lr)
+
+    def _write_hist(self, lo: int, hi: int) -> None:
+        """History rows lo..hi (Adam steps) for the current hyper-parameters."""
+        if hi >= self._hist.shape[0]:
+            cap = max(2 * self._hist.shape[0], hi + 1)
+            h = torch.zeros((cap, 8), dtype=torch.float32, device=self.device)
+            h[:self._hist.shape[0]] = self._hist
+            hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
+            hh[:self._hist_host.shape[0]] = self._hist_host
+            self._hist, self._hist_host = h, hh
+        rows = [adam_scalars(t, self.lr, self.betas, self.eps, self.weight_decay)
+                for t in range(lo, hi + 1)]
+        self._hist_host[lo:hi + 1, :7] = torch.tensor(rows, dtype=torch.float32)
+        self._hist[lo:hi + 1].copy_(self._hist_host[lo:hi + 1], non_blocking=True)
+        self._hist_ready = hi
+        self._hist_key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
+
+    def reserve_history(self, last_step: int) -> None:
+        """The Adam-scalar history written up to ``last_step`` ahead of time (a captured step
+        replays begin_step without its host-to-device copies: word2vec/graphed.py)."""
+        key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
+        lo = self.step_count + 1
+        if key != self._hist_key:
+            self._write_hist(lo, max(last_step, lo))
+        elif last_step > self._hist_ready:
+            self._write_hist(self._hist_ready + 1, last_step)
 
     def prepare(self, walks: torch.Tensor, context_radius: int, neg_samples: int) -> None:
         """The batch's centre order (for pass 1 with order_ready) and its touched rows U."""

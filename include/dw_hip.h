@@ -573,6 +573,13 @@ typedef struct dw_step_scalars {
  * thread makes next. */
 int dw_step_scalars_bind(const dw_step_scalars *dev);
 
+/* As dw_step_scalars_bind, and the launches' Adam step numbers become relative to the block:
+ * dw_adam_rows, dw_sgns_owner_out_catch_up and dw_sgns_owner_pass2_lazy then apply
+ * dev->step + (step - host_step), read on the device, where `step` is their argument (the lazy
+ * exact Adam of a captured one-GPU owner step: word2vec/graphed.py GraphedOwnerStep). Those
+ * three refuse (DW_E_INVALID_ARG) a block bound without its host step. */
+int dw_step_scalars_bind_at(const dw_step_scalars *dev, int64_t host_step);
+
 /* walk_id0 += walks_per_step, noise_offset += centres_per_step, step += 1, adam = hist[step]
  * (hist: float32[hist_rows][8]; a step beyond hist_rows sets DW_S_BAD_INDEX in status and
  * leaves adam unchanged); then, with epoch_starts != NULL, the new step's start nodes into

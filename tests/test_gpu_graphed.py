@@ -81,3 +81,78 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
     for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
         assert_params_close(got, exp, LR)
         assert_no_row_drift(got, exp)
+
+
+@pytest.mark.parametrize('lazy_out,unroll', [(True, 1), (True, 4), (False, 3)])
+def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
+    """The one-GPU lazy owner step (bench.py's path for the reference's 64-walk batch on a large
+    graph) replayed as a HIP graph (GraphedOwnerStep: the lazy kernels' step numbers bound
+    relative to the step blocks) equals the eager steps: the same walks, losses to float64-atomic
+    order, and both tables, flushed, to fp32 atomic-order noise."""
+    from shallow_encoders.word2vec.graphed import GraphedOwnerStep
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    dev = hip_device
+    csr, walker, epoch = _setup(dev)
+    V = csr.vocab_size
+    grad_scale = 1.0 / (B * (L - 2 * R) * 2 * R)
+    warm, steps = 2, 12
+    runs = []
+    for mode in ('eager', 'graph'):
+        t = OwnerLazyTables(V, D, dev, lr=LR, init_seed=0, emulate_world=1, lazy_out=lazy_out)
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def eager(s):
+            g0 = s * B
+            st = epoch[torch.arange(g0, g0 + B, device=dev) % epoch.numel()]
+            walks = walker.walk_batch(st, walk_id0=g0, check=False)
+            owner_lazy_step(t, walks, R, K, seed=SEED, noise_offset=g0 * (L - 2 * R),
+                            grad_scale=grad_scale, loss_acc=acc, status=status)
+            return walks
+        for s in range(warm):
+            eager(s)
+        if mode == 'eager':
+            for s in range(warm, warm + steps):
+                last = eager(s)
+        else:
+            gs = GraphedOwnerStep(t, walker, epoch, B, R, K, seed=SEED, grad_scale=grad_scale,
+                                  loss_acc=acc, status=status, first_walk_id=warm * B,
+                                  n_steps=steps, unroll=unroll)
+            for _ in range(steps // unroll):
+                gs.replay()
+            last = gs.walks[-B:]
+            sc = gs.scalars()
+            assert sc == {'walk_id0': (warm + steps) * B,
+                          'noise_offset': (warm + steps) * B * (L - 2 * R),
+                          'step': warm + steps + 1}
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0
+        assert t.step_count == warm + steps
+        runs.append((t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(), acc.cpu().numpy(),
+                     last.cpu().numpy()))
+    (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
+    np.testing.assert_array_equal(walks_g, walks_e)
+    np.testing.assert_allclose(acc_g, acc_e, rtol=1e-9)
+    for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
+        assert_params_close(got, exp, LR)
+        assert_no_row_drift(got, exp)
+
+
+def test_lazy_kernels_refuse_a_block_bound_without_its_step(hip_device):
+    """dw_adam_rows (and the other lazy launches) take step numbers relative to a block bound by
+    dw_step_scalars_bind_at; under a plain dw_step_scalars_bind they refuse instead of capturing
+    a frozen step."""
+    from shallow_encoders import _native
+    from shallow_encoders.word2vec.sharding import hip_rows_adam
+    dev = hip_device
+    p = torch.zeros((4, 64), device=dev)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    last = torch.zeros(4, dtype=torch.int32, device=dev)
+    hist = torch.zeros((8, 8), device=dev)
+    blk = torch.zeros(64, dtype=torch.uint8, device=dev)
+    _native.call('dw_step_scalars_bind', _native.ptr(blk))
+    try:
+        with pytest.raises(Exception, match='bind_at'):
+            hip_rows_adam(p, m, v, last, None, None, 4, None, hist, 1)
+    finally:
+        _native.call('dw_step_scalars_bind', None)
