@@ -489,7 +489,7 @@ def main():
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
                          grad_scale=grad_scale, loss_acc=loss_acc, status=status,
-                         order_ready=lazy, lazy_out=tables.pass1_lazy_spec() if lazy else None)
+                         order_ready=lazy)
         if not gather:
             feed.next(s)
         if lazy:

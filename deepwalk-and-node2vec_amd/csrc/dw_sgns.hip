@@ -152,13 +152,6 @@ struct SgnsArgs {
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
-    // lazy out slice (dw_sgns_owner_pass1_lazy): the out rows are brought current to step - 1
-    // in registers as pass 1 loads them (their deferred g = 0 steps, hist's scalars); the lazy
-    // gather of pass 2 replays the same steps when it updates them, so nothing is written here
-    const float *lz_m, *lz_v;
-    const int32_t *lz_last;
-    const float *lz_hist;
-    int32_t lz_step, lz_delta;    //   step = dyn ? dyn->step + lz_delta : lz_step
 };
 
 #ifndef DW_NOISE_ROUNDS
@@ -389,14 +382,10 @@ __device__ __forceinline__ float row_sum16(float x) {
 // grow W-fold (2.35 GB per pass at W = 8, C3). The owner form therefore takes the centres in
 // node order (a sorted occurrence list, contiguous per wave): consecutive occurrences of one
 // node are summed in registers (pend) and leave as ONE atomic row per run.
-// (LZ: the register budget of 2 waves per SIMD; the lazy form runs at small batches, whose
-// few waves hold m and v of the rows in flight too)
-template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool LZ = false>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, LZ ? 2 : (CHR >= 8 ? 3 : G16_MIN_WAVES))
+template <int F4, bool FROM_WALKS, int CHR, bool OWNER>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
-    static_assert(!LZ || OWNER, "the lazy out slice is an owner-form pass");
     constexpr int D = 64 * F4;
-    const int32_t lz_step = LZ ? dw::eff_step(a.dyn, a.lz_delta, a.lz_step) : 0;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ uint8_t s_t[WAVES_PER_BLOCK][4][OWNER ? G16_TMAX : 1];
@@ -550,45 +539,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, LZ ? 2 : (CHR >= 8 ? 3 
                 for (int f = 0; f < F4; ++f)
                     o4[u][f] = rid[u] >= 0 ? *reinterpret_cast<const float4 *>(row + 64 * f)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            if constexpr (LZ) {   // stale rows: replay their deferred steps in registers
-                int32_t from[CHR];
-#pragma unroll
-                for (int u = 0; u < CHR; ++u) from[u] = rid[u] >= 0 ? a.lz_last[rid[u]] : lz_step;
-                float4 m4[CHR][F4], v4[CHR][F4];
-#pragma unroll
-                for (int u = 0; u < CHR; ++u) {
-                    const bool stale = from[u] + 1 < lz_step;
-                    const int64_t o = static_cast<int64_t>(rid[u] < 0 ? 0 : rid[u]) * D + 4 * gl;
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) {
-                        m4[u][f] = stale ? *reinterpret_cast<const float4 *>(a.lz_m + o + 64 * f)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                        v4[u][f] = stale ? *reinterpret_cast<const float4 *>(a.lz_v + o + 64 * f)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < CHR; ++u) {
-                    for (int32_t t = from[u] + 1; t < lz_step; ++t) {   // (k_rows_adam's rule)
-                        const dw::AdamScalars h = dw::hist_at(a.lz_hist, t);
-#pragma unroll
-                        for (int f = 0; f < F4; ++f) {
-                            float *pp = reinterpret_cast<float *>(&o4[u][f]);
-                            float *mm = reinterpret_cast<float *>(&m4[u][f]);
-                            float *vv = reinterpret_cast<float *>(&v4[u][f]);
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) {
-                                if (h.wd == 0.f) {
-                                    dw::adam_elem_g0(pp[c], mm[c], vv[c], h);
-                                } else {
-                                    float z = 0.f;
-                                    dw::adam_elem(pp[c], z, mm[c], vv[c], h);
-                                }
-                            }
-                        }
-                    }
-                }
             }
         };
         auto compute_chunk = [&](const float4(&o4)[CHR][F4], const int32_t(&rid)[CHR],
@@ -1028,7 +978,7 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
 
 // 16-lane-group pass 1 when d is a multiple of 64 (<= 512) and 2R(1+K) <= 64; otherwise
 // DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns). DW_SGNS_G16=0 disables it.
-template <bool FROM_WALKS, bool OWNER = false, bool LZ = false>
+template <bool FROM_WALKS, bool OWNER = false>
 int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     static const bool enabled = [] {
         const char *e = getenv("DW_SGNS_G16");
@@ -1040,14 +990,11 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    // rows per chunk: CHR * F4 float4 registers per lane (the lazy form holds m and v too:
-    // half the rows per chunk)
-    constexpr int H = LZ ? 2 : 1;
-    switch (a.d / 64) {
-        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8 / H, OWNER, LZ>), g, bl, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4 / H, OWNER, LZ>), g, bl, 0, st, a); break;
-        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2 / H, OWNER, LZ>), g, bl, 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER, LZ>), g, bl, 0, st, a); break;
+    switch (a.d / 64) {  // rows per chunk: CHR * F4 float4 registers per lane
+        case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, OWNER>), g, bl, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER>), g, bl, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, OWNER>), g, bl, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER>), g, bl, 0, st, a); break;
         default: return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns/g16");
@@ -1736,8 +1683,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
             if (rc != DW_OK) return rc;
         }
         a.occ = occ.v0;
-        rc = a.lz_last ? launch_pass1_g16<true, true, true>(a, st)
-                       : launch_pass1_g16<true, true>(a, st);
+        rc = launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
         if (!dense) {
             hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts,
@@ -2263,45 +2209,6 @@ int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_leng
     a.own_shift = -1;
     for (int sh = 0; sh < 31; ++sh)
         if ((1 << sh) == n_owners) a.own_shift = sh;
-    return launch_owner_pass1(a, local_rows, order_ready, workspace, workspace_bytes,
-                              dw::as_stream(stream));
-}
-
-int dw_sgns_owner_pass1_lazy(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                             int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                             int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
-                             int32_t order_ready, const float *w_in, const float *w_out_local,
-                             float *g_in, const int64_t *noise, uint64_t seed,
-                             uint64_t noise_offset, float grad_scale, double *loss_acc,
-                             const float *m_out, const float *v_out, const int32_t *last_step,
-                             const float *hist, int32_t step, int32_t *status, void *workspace,
-                             size_t workspace_bytes, void *stream) {
-    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
-                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && step >= 1,
-               "dw_sgns_owner_pass1_lazy: bad sizes");
-    DW_REQUIRE((walks || n_walks == 0) && w_in && w_out_local && g_in && status && m_out &&
-                   v_out && last_step && hist,
-               "dw_sgns_owner_pass1_lazy: null pointer");
-    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out_local, g_in, nullptr, noise,
-                           seed, noise_offset, grad_scale, loss_acc, status);
-    a.walks = walks;
-    a.L = walk_length;
-    a.R = context_radius;
-    a.batch = n_walks * (walk_length - 2 * context_radius);
-    a.C = 2 * context_radius;
-    a.owner = owner;
-    a.n_owners = n_owners;
-    a.own_shift = -1;
-    for (int sh = 0; sh < 31; ++sh)
-        if ((1 << sh) == n_owners) a.own_shift = sh;
-    a.lz_m = m_out;
-    a.lz_v = v_out;
-    a.lz_last = last_step;
-    a.lz_hist = hist;
-    a.lz_step = step;
-    const dw_step_scalars *dyn = nullptr;
-    const int rc = dw::bound_step_rel(step, &dyn, &a.lz_delta, "dw_sgns_owner_pass1_lazy");
-    if (rc != DW_OK) return rc;
     return launch_owner_pass1(a, local_rows, order_ready, workspace, workspace_bytes,
                               dw::as_stream(stream));
 }

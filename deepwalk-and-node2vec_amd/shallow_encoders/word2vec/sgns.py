@@ -322,17 +322,13 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
-                     order_ready: bool = False,
-                     lazy_out: Optional[dict] = None) -> torch.Tensor:
+                     order_ready: bool = False) -> torch.Tensor:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
     partial centre-table gradient of the owned slots; returns the float64[4] loss accumulator
     (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
-    ``order_ready``: sgns_owner_prepare already built the centre order for these walks.
-    ``lazy_out`` ({'m', 'v', 'last', 'hist', 'step'}, OwnerLazyTables.pass1_lazy_spec()): the
-    out slice's Adam is lazy and the rows pass 1 loads are brought current to step - 1 in
-    registers (dw_sgns_owner_pass1_lazy; no separate catch-up)."""
+    ``order_ready``: sgns_owner_prepare already built the centre order for these walks."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -357,18 +353,6 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
     ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
-    if lazy_out is not None:
-        with torch.cuda.device(dev):
-            _native.call('dw_sgns_owner_pass1_lazy', _native.ptr(walks), n, L, R, K,
-                         int(vocab_size), d, int(owner), int(n_owners), local_rows,
-                         1 if order_ready else 0, _native.ptr(w_in), _native.ptr(w_out_local),
-                         _native.ptr(g_in), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
-                         int(noise_offset), float(scale), _native.ptr(loss_acc),
-                         _native.ptr(lazy_out['m']), _native.ptr(lazy_out['v']),
-                         _native.ptr(lazy_out['last']), _native.ptr(lazy_out['hist']),
-                         int(lazy_out['step']), _native.ptr(status), _native.ptr(ws), ws.numel(),
-                         _native.stream(dev))
-        return loss_acc
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows, 1 if order_ready else 0,

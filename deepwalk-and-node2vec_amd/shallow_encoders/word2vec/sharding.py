@@ -758,10 +758,6 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = bool(lazy_out)
         super().__init__(*args, **kwargs)
         self.lazy_out = self.lazy_out and self._hip()
-        # lazy_out: pass 1 brings the rows it loads current in registers (pass1_lazy_spec,
-        # dw_sgns_owner_pass1_lazy) instead of a separate catch-up launch that rewrites them;
-        # DW_OUT_CATCH_UP=1 keeps the separate catch-up (measurements)
-        self.fused_out_catch_up = os.environ.get('DW_OUT_CATCH_UP') != '1'
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -773,7 +769,7 @@ class OwnerLazyTables(OwnerTables):
                      noise: Optional[torch.Tensor] = None) -> None:
         """lazy_out, before pass 1 of the batch ``walks``: the owned out rows its slots
         reference replay their deferred steps up to step - 1 (dw_sgns_owner_out_catch_up)."""
-        if not self.lazy_out or self.fused_out_catch_up:
+        if not self.lazy_out:
             return
         n, L = walks.shape
         slots = n * (L - 2 * int(context_radius)) * 2 * int(context_radius) * (1 + int(neg_samples))
@@ -789,14 +785,6 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist),
                          self.step_count, _native.ptr(status), _native.stream(self.device))
-
-    def pass1_lazy_spec(self) -> Optional[dict]:
-        """lazy_out with the fused catch-up: sgns_owner_pass1's ``lazy_out`` argument (after
-        begin_step); None otherwise."""
-        if not (self.lazy_out and self.fused_out_catch_up):
-            return None
-        return {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                'step': self.step_count}
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -1012,8 +1000,7 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
-                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
-                     lazy_out=tables.pass1_lazy_spec())
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True)
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,

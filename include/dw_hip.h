@@ -403,24 +403,6 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                int64_t *n_rows, const float *hist, int32_t step,
                                int32_t *status, void *stream);
 
-/* dw_sgns_owner_pass1 for a LAZY out slice (with dw_sgns_owner_pass2_lazy, instead of
- * dw_sgns_owner_out_catch_up before a plain pass 1): each output row pass 1 loads whose
- * last_step[row] < step - 1 is brought current to step - 1 in registers (its deferred g = 0
- * steps replayed through the same adam_elem, scalars hist[t]) before its logit; nothing is
- * written back — the lazy gather of pass 2 replays the same steps when it updates the row. One
- * pass over the rows instead of a claim launch, a replay that writes p / m / v, and pass 1's
- * read of the rows. Replaces no reference interface (the out table's torch Adam step,
- * trainer.py:131-152, kept exact for sparse batches). */
-int dw_sgns_owner_pass1_lazy(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                             int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                             int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
-                             int32_t order_ready, const float *w_in, const float *w_out_local,
-                             float *g_in, const int64_t *noise, uint64_t seed,
-                             uint64_t noise_offset, float grad_scale, double *loss_acc,
-                             const float *m_out, const float *v_out, const int32_t *last_step,
-                             const float *hist, int32_t step, int32_t *status, void *workspace,
-                             size_t workspace_bytes, void *stream);
-
 /* dw_sgns_owner_pass2 with the out slice's Adam kept LAZY and exact (OwnerLazyTables, small
  * batches): a row no record touched is not read or written; its deferred g = 0 steps are
  * replayed (scalars hist[t], fp32 [steps][8] as for dw_adam_rows) right before its next update,
@@ -592,11 +574,10 @@ typedef struct dw_step_scalars {
 int dw_step_scalars_bind(const dw_step_scalars *dev);
 
 /* As dw_step_scalars_bind, and the launches' Adam step numbers become relative to the block:
- * dw_adam_rows, dw_sgns_owner_out_catch_up, dw_sgns_owner_pass1_lazy and
- * dw_sgns_owner_pass2_lazy then apply dev->step + (step - host_step), read on the device, where
- * `step` is their argument (the lazy exact Adam of a captured one-GPU owner step:
- * word2vec/graphed.py GraphedOwnerStep). Those four refuse (DW_E_INVALID_ARG) a block bound
- * without its host step. */
+ * dw_adam_rows, dw_sgns_owner_out_catch_up and dw_sgns_owner_pass2_lazy then apply
+ * dev->step + (step - host_step), read on the device, where `step` is their argument (the lazy
+ * exact Adam of a captured one-GPU owner step: word2vec/graphed.py GraphedOwnerStep). Those
+ * three refuse (DW_E_INVALID_ARG) a block bound without its host step. */
 int dw_step_scalars_bind_at(const dw_step_scalars *dev, int64_t host_step);
 
 /* walk_id0 += walks_per_step, noise_offset += centres_per_step, step += 1, adam = hist[step]

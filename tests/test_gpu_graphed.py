@@ -128,8 +128,7 @@ def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
         torch.cuda.synchronize()
         assert int(status.item()) == 0
         assert t.step_count == warm + steps
-        t._flush_out()          # (an emulated one-rank slice is the whole out table)
-        runs.append((t.w_in.cpu().numpy(), t.w_out[:V].cpu().numpy(), acc.cpu().numpy(),
+        runs.append((t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(), acc.cpu().numpy(),
                      last.cpu().numpy()))
     (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
     np.testing.assert_array_equal(walks_g, walks_e)

@@ -308,14 +308,10 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d, wd):
     assert (last[ri] == S + 1).all() and int((last == S + 1).sum()) == 5
 
 
-def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False,
-                   fused=True):
-    """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L].
-    fused=False: the out rows' catch-up as its own launch (dw_sgns_owner_out_catch_up) instead
-    of in pass 1's registers (dw_sgns_owner_pass1_lazy)."""
+def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False):
+    """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L]."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
     t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
-    t.fused_out_catch_up = fused
     n, L = walks_all.shape[1:]
     per = L - 2 * R
     acc = torch.zeros(4, dtype=torch.float64, device=device)
@@ -360,26 +356,6 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
                                                       ref.w_out.cpu().numpy())):
         assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
                             max_abs=2.05 * lr * steps)
-        assert_no_row_drift(got, exp)
-
-
-def test_owner_lazy_out_fused_catch_up_equals_separate(hip_device):
-    """The out rows brought current in pass 1's registers (dw_sgns_owner_pass1_lazy, the
-    default) train the same tables as the separate catch-up launch that rewrites them
-    (dw_sgns_owner_out_catch_up + dw_adam_rows): the same adam_elem replays, so the losses agree
-    to float64-atomic order and the flushed tables to fp32 atomic-order noise."""
-    V, d, R, K, L, n, steps, lr = 3000, 128, 2, 5, 12, 24, 8, 0.01
-    walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(5),
-                          dtype=torch.int32)
-    runs = []
-    for fused in (True, False):
-        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, fused=fused)
-        assert int((t.last_out[:V] < steps).sum()) > V // 4   # rows really deferred
-        runs.append((t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(), acc.cpu().numpy()))
-    (wi_f, wo_f, acc_f), (wi_s, wo_s, acc_s) = runs
-    np.testing.assert_allclose(acc_f, acc_s, rtol=1e-9)
-    for got, exp in ((wi_f, wi_s), (wo_f, wo_s)):
-        assert_params_close(got, exp, lr)
         assert_no_row_drift(got, exp)
 
 
