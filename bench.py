@@ -482,9 +482,7 @@ def main():
             e[1].record()
         if lazy:
             tables.begin_step()
-            tables.prepare(walks, R, K)
-            tables.catch_up()
-            tables.catch_up_out(walks, R, K, 99, g0 * (L - 2 * R), status)
+            tables.before_pass1(walks, R, K, 99, g0 * (L - 2 * R), status)
         sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks,
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),

@@ -915,6 +915,29 @@ class OwnerLazyTables(OwnerTables):
         """Before pass 1: the touched rows replay their missed steps, up to step - 1."""
         self._rows(None, self.step_count - 1)
 
+    def before_pass1(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
+                     seed: int, noise_offset: int, status: torch.Tensor) -> None:
+        """prepare + catch_up + catch_up_out (after begin_step). With lazy_out on one rank the
+        centre order and in-table catch-up (a one-block sort, then ALU-bound replays) run on
+        the side stream beside the out rows' claim and catch-up (bandwidth-bound); the current
+        stream waits for both."""
+        if self.lazy_out and not self.multi:
+            main = torch.cuda.current_stream(self.device)
+            fork = torch.cuda.Event()
+            fork.record(main)
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(fork)
+                self.prepare(walks, context_radius, neg_samples)
+                self.catch_up()
+                join = torch.cuda.Event()
+                join.record(self._side)
+            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+            main.wait_event(join)
+            return
+        self.prepare(walks, context_radius, neg_samples)
+        self.catch_up()
+        self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+
     def exchange_touched(self) -> None:
         """After pass 1: G = g_in[U] (those rows cleared); N > 1: all-reduce(SUM) of G, on a side
         stream behind the output-table phase."""
@@ -994,9 +1017,7 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     same global batch). Returns this rank's record count."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
-    tables.prepare(walks, context_radius, neg_samples)
-    tables.catch_up()
-    tables.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+    tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
