@@ -94,10 +94,33 @@ class CSVMetricLogger:
         self._rows = []
 
 
+def _graph_source(trainer: Word2VecTrainer, dataloader, step_sched: bool):
+    """The RandomWalkDataset behind a walk-batch loader whose steps can be replayed as HIP graphs
+    (word2vec/graphed.py GraphedTrainerStep), or None. DW_TRAIN_GRAPH=0 keeps every step eager."""
+    from shallow_encoders.config_parser.core import WalkBatchLoader
+    from shallow_encoders.word2vec.graphed import GraphedTrainerStep
+    if os.environ.get('DW_TRAIN_GRAPH', '1') == '0' or step_sched:
+        return None
+    if not isinstance(dataloader, WalkBatchLoader) or not torch.cuda.is_available():
+        return None
+    rwd = dataloader.dataset.dataset
+    R = trainer._context_radius
+    if R is None or rwd.walk_length < 2 * R + 1:
+        return None
+    return rwd if GraphedTrainerStep.eligible(trainer, rwd) else None
+
+
 def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
         checkpoint_dir: Optional[str] = None, log_dir: Optional[str] = None,
-        log_every_n_steps: int = 50, verbose: bool = True) -> Dict[str, float]:
-    """Train for ``max_epochs``; returns the last epoch's metric means."""
+        log_every_n_steps: int = 50, verbose: bool = True,
+        graph_unroll: int = 16) -> Dict[str, float]:
+    """Train for ``max_epochs``; returns the last epoch's metric means.
+
+    Device walk batches with a Philox walker and device negatives (``noise: device``) are
+    replayed ``graph_unroll`` steps per HIP graph after each epoch's first (eager) batch
+    (GraphedTrainerStep): the same steps, kernels and results, without a Python launch per
+    kernel. The trailing batches that do not fill a graph, and everything else, run eagerly."""
+    from shallow_encoders.word2vec.graphed import GraphedTrainerStep
     trainer.manual_grads = True
     opt = trainer.optimizer
     sched = trainer.scheduler
@@ -113,7 +136,9 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
     for epoch in range(max_epochs):
         t0 = time.perf_counter()
         n_batches = 0
-        for batch in dataloader:
+
+        def run(batch):
+            nonlocal global_step, n_batches
             loss = trainer.training_step(batch)
             opt.step()
             opt.zero_grad()
@@ -123,6 +148,34 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
                 logger.log(global_step, epoch, {f'train/{k}': v for k, v in loss.items()})
             global_step += 1
             n_batches += 1
+
+        rwd = _graph_source(trainer, dataloader, step_sched)
+        if rwd is None:
+            for batch in dataloader:
+                run(batch)
+        else:
+            B = dataloader.batch_size
+            batch = rwd.next_walk_batch(B, check=False)   # eager: creates state / workspaces
+            if batch is not None:
+                run(batch)
+                n_rep = (len(rwd) - rwd._index) // B // graph_unroll
+                if n_rep > 0:
+                    gs = GraphedTrainerStep(trainer, rwd, B, n_rep * graph_unroll, graph_unroll)
+                    for _ in range(n_rep):
+                        loss = trainer.push_replayed(gs.replay(), graph_unroll)
+                        if log_dir and (-global_step) % log_every_n_steps < graph_unroll:
+                            logger.log(global_step + (-global_step) % log_every_n_steps, epoch,
+                                       {f'train/{k}': v for k, v in loss.items()})
+                        global_step += graph_unroll
+                        n_batches += graph_unroll
+                    torch.cuda.current_stream().synchronize()
+                    from shallow_encoders import _native
+                    _native.check_status(gs.status, 'graphed training steps')
+                while True:
+                    batch = rwd.next_walk_batch(B, check=False)
+                    if batch is None:
+                        break
+                    run(batch)
         last = trainer.on_train_epoch_end()         # synchronises with the device
         t_loop = time.perf_counter() - t0
         if not step_sched and sched_obj is not None:

@@ -303,6 +303,151 @@ class GraphedOwnerStep:
                 'step': int(b['step'])}
 
 
+class GraphedTrainerStep:
+    """The user-facing training step (tools/train.py -> word2vec/fit.py: ``training_step`` on a
+    device walk batch, then ``optimizer.step()``, trainer.py:131-152) replayed as a HIP graph of
+    ``unroll`` steps, with the walker launch for all of them at its head: the reference configs'
+    64-walk batches are launch-bound when stepped from Python one kernel at a time.
+
+    Eligible (``eligible``): a RandomWalkDataset with a Philox walker, ``noise='device'``,
+    ``manual_grads``, the HIP Adam holding exactly the two tables, no ``max_norm``. The step is
+    the trainer's own: the fused records step (the out table's Adam in the gather, the in
+    table's on the side stream) or, for batches of <= 65,536 records, the atomic output-table
+    scatter followed by ``optimizer.step()`` (bench.py's ``--scatter auto`` rule). What changes
+    per step lives in the bound dw_step_scalars blocks (walk ids from the epoch's start list,
+    the negatives' centre counter, the Adam scalars of the optimizer's history); the host
+    bookkeeping (the optimizer's step counts, the trainer's centre counter, the dataset's
+    position) follows each replay. ``unroll`` must be even: the fused step swaps the in table's
+    buffers every step, so an even graph ends where it began.
+
+    The tables, optimizer state and workspaces must exist (one eager step first: fit runs the
+    epoch's first batch eagerly). ``replay`` returns the replayed steps' mean loss terms (device
+    tensors), which fit pushes to the trainer's meter once per step they stand for."""
+
+    @staticmethod
+    def eligible(trainer, dataset) -> bool:
+        from shallow_encoders.word2vec.optim import Adam
+        walker = dataset.walk_generator
+        opt = trainer.optimizer
+        w_in, w_out = trainer.model.input_weight, trainer.model.output_weight
+        if not (isinstance(opt, Adam) and opt.fuse_into_sgns and opt.zero_grad_in_step
+                and len(opt.param_groups) == 1):
+            return False
+        mine = {id(p) for p in opt.param_groups[0]['params']}
+        return (getattr(walker, '_rng', None) == 'philox' and trainer._noise_mode == 'device'
+                and trainer.manual_grads and trainer.model.max_norm is None
+                and mine == {id(w_in), id(w_out)} and w_in.device.type == 'cuda'
+                and trainer._context_radius is not None)
+
+    def __init__(self, trainer, dataset, B: int, n_steps: int, unroll: int = 16):
+        if unroll < 2 or unroll % 2:
+            raise ValueError('GraphedTrainerStep: unroll must be even and >= 2')
+        if not self.eligible(trainer, dataset):
+            raise ValueError('GraphedTrainerStep: needs a Philox walker, noise=device, '
+                             'manual_grads and the fusable HIP Adam (see eligible)')
+        if not trainer.optimizer.can_fuse([trainer.model.input_weight,
+                                           trainer.model.output_weight]):
+            raise ValueError('GraphedTrainerStep: run one eager step first (gradient buffers, '
+                             'Adam state)')
+        from shallow_encoders.word2vec.sgns import _use_records
+        self.trainer, self.dataset, self.walker = trainer, dataset, dataset.walk_generator
+        self.unroll, self.B = int(unroll), int(B)
+        w_in, w_out = trainer.model.input_weight, trainer.model.output_weight
+        dev = w_in.device
+        L = dataset.walk_length
+        R, K = int(trainer._context_radius), int(trainer._neg_samples)
+        self.R, self.K = R, K
+        self.centres = self.B * (L - 2 * R)
+        records = self.centres * 2 * R * (1 + K)
+        self.scatter = 'atomic' if records <= 65_536 else None   # (None: the fused step)
+        if self.scatter is None and not _use_records('sorted', 2 * R, K, w_in.shape[0]):
+            raise ValueError('GraphedTrainerStep: shape outside the records path')
+        opt = trainer.optimizer
+        group = opt.param_groups[0]
+        self._params = (w_in, w_out)
+        steps = {int(opt.state[p]['step'].item()) for p in self._params}
+        if len(steps) != 1:
+            raise ValueError('GraphedTrainerStep: the two tables are at different Adam steps')
+        s1 = steps.pop() + 1
+        self._key = (group['lr'], tuple(group['betas']), group['eps'], group['weight_decay'])
+        self._last = s1 + int(n_steps)
+        hist = adam_history(self._last + self.unroll + 1, group['lr'], group['betas'],
+                            group['eps'], group['weight_decay'])
+        self.hist = torch.from_numpy(hist).to(dev)
+        self.epoch_starts = dataset._device_starts()
+        first = dataset._index
+        blk = np.zeros(1, dtype=_STEP_DTYPE)
+        blk['walk_id0'] = dataset._epoch * len(dataset) + first
+        blk['noise_offset'] = trainer._noise_offset
+        blk['step'] = s1
+        blk['adam'][0] = hist[s1]
+        self.block = torch.from_numpy(np.frombuffer(blk.tobytes(), dtype=np.uint8).copy()).to(dev)
+        self.step_blocks = torch.zeros(self.unroll * _STEP_DTYPE.itemsize, dtype=torch.uint8,
+                                       device=dev)
+        self.walks = torch.empty((self.unroll * self.B, L), dtype=torch.int32, device=dev)
+        self.starts = torch.empty(self.unroll * self.B, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        torch.cuda.synchronize(dev)
+        snap = ([opt.state[p]['step'].clone() for p in self._params], trainer._noise_offset,
+                w_in.data_ptr())
+        trainer._capture_acc, trainer._capture_scatter = self.acc, self.scatter
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode='relaxed'):
+                self._body()
+        finally:
+            _native.call('dw_step_scalars_bind', None)
+            trainer._capture_acc = trainer._capture_scatter = None
+            for p, st in zip(self._params, snap[0]):   # the capture ran no step
+                opt.state[p]['step'] = st
+            trainer._noise_offset = snap[1]
+        if w_in.data_ptr() != snap[2]:
+            raise RuntimeError('GraphedTrainerStep: the in table did not end in its buffer')
+        torch.cuda.synchronize(dev)
+
+    def _step_blk(self, k: int) -> int:
+        return self.step_blocks.data_ptr() + k * _STEP_DTYPE.itemsize
+
+    def _body(self) -> None:
+        dev, B = self.acc.device, self.B
+        self.acc.zero_()
+        with torch.cuda.device(dev):
+            _native.call('dw_step_scalars_expand', _native.ptr(self.block), self._step_blk(0),
+                         self.unroll, _native.ptr(self.hist), self.hist.shape[0], B,
+                         self.centres, _native.ptr(self.status), _native.ptr(self.epoch_starts),
+                         self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
+                         _native.stream(dev))
+        _native.call('dw_step_scalars_bind', self._step_blk(0))
+        self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
+                               status=self.status)
+        opt = self.trainer.optimizer
+        for k in range(self.unroll):
+            _native.call('dw_step_scalars_bind', self._step_blk(k))
+            self.trainer.training_step(self.walks[k * B:(k + 1) * B])
+            opt.step()
+            opt.zero_grad()
+
+    def replay(self) -> dict:
+        """``unroll`` training steps; returns their mean loss terms (device tensors)."""
+        from shallow_encoders.word2vec.sgns import loss_terms
+        t, opt = self.trainer, self.trainer.optimizer
+        group = opt.param_groups[0]
+        if (group['lr'], tuple(group['betas']), group['eps'], group['weight_decay']) != self._key:
+            raise RuntimeError('GraphedTrainerStep: the optimizer hyper-parameters changed since '
+                               'the capture; build a new one')
+        step = int(opt.state[self._params[0]]['step'].item())
+        if step + self.unroll > self._last:
+            raise RuntimeError('GraphedTrainerStep: the Adam-scalar history is used up; build a '
+                               'new one (n_steps)')
+        self.graph.replay()
+        for p in self._params:
+            opt.state[p]['step'] += self.unroll
+        t._noise_offset += self.unroll * self.centres
+        self.dataset._index += self.unroll * self.B
+        return loss_terms(self.acc, self.unroll * self.centres * 2 * self.R, self.K)
+
+
 def epoch_starts_node_order(n_nodes: int, walks_per_node: int, device) -> torch.Tensor:
     """bench.py's start order: walk w starts at node w // walks_per_node + 1 (vocabulary id)."""
     ids = torch.arange(1, n_nodes + 1, dtype=torch.int32, device=device)

@@ -81,6 +81,11 @@ class Word2VecTrainer(_Base):
         self.logged: Dict[str, object] = {}
         self._side = None          # side stream of the fused step (input-table Adam)
         self._row_flags = None     # fused output-table Adam scratch
+        # set while word2vec/graphed.py GraphedTrainerStep captures the step: the steps add
+        # their loss sums here and skip the per-step metrics (read once per replay), and
+        # _capture_scatter = 'atomic' takes the atomic output-table scatter (tiny batches)
+        self._capture_acc = None
+        self._capture_scatter = None
 
     # ---- reference properties -------------------------------------------------------------
     @property
@@ -187,18 +192,23 @@ class Word2VecTrainer(_Base):
                 p.grad = torch.zeros_like(p)
             if isinstance(self._optimizer, Adam):
                 self._optimizer.mark_grads(fresh, True)
-            if targets is None and self._can_fuse_step(w_in, w_out, C):
+            if targets is None and self._capture_scatter != 'atomic' and \
+                    self._can_fuse_step(w_in, w_out, C):
                 acc = self._fused_walk_step(w_in, w_out, src, R, noise, offset)
             elif targets is None:
                 acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
                                       self._neg_samples, walks=src, context_radius=R, noise=noise,
-                                      seed=self._seed, noise_offset=offset)
+                                      seed=self._seed, noise_offset=offset,
+                                      loss_acc=self._capture_acc,
+                                      scatter=self._capture_scatter or 'sorted')
             else:
                 acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad,
                                       self._neg_samples, inputs=src, targets=targets, noise=noise,
                                       seed=self._seed, noise_offset=offset)
             if isinstance(self._optimizer, Adam) and not self._optimizer._fused_done:
                 self._optimizer.mark_grads([w_in, w_out], False)   # accumulated, not consumed
+            if self._capture_acc is not None:   # a captured step: metrics once per replay
+                return None
             t = loss_terms(acc, n_centres * C, self._neg_samples)
             loss = {k: t[k] for k in ('loss', 'positive-loss', 'negative-loss')}
             recall, precision = t['recall'], t['precision']
@@ -234,7 +244,7 @@ class Word2VecTrainer(_Base):
         kw = dict(walks=walks, context_radius=R, noise=noise, seed=self._seed,
                   noise_offset=offset)
         acc = sgns_accumulate(w_in.detach(), w_out.detach(), w_in.grad, w_out.grad, K,
-                              phase=1, **kw)
+                              phase=1, loss_acc=self._capture_acc, **kw)
         if self._side is None or self._side.device != dev:
             self._side = torch.cuda.Stream(dev)
         if self._row_flags is None or self._row_flags.numel() != V or \
@@ -259,6 +269,20 @@ class Word2VecTrainer(_Base):
         main.wait_event(done)
         opt.swap_alt(w_in)
         return acc
+
+    def push_replayed(self, terms: Dict[str, torch.Tensor], n_steps: int) -> Dict[str, torch.Tensor]:
+        """The metrics of ``n_steps`` graph-replayed steps (word2vec/graphed.py
+        GraphedTrainerStep): their mean loss terms stand for each of the steps in the epoch
+        means, as training_step's per-step pushes would; returns the loss dict."""
+        loss = {k: terms[k] for k in ('loss', 'positive-loss', 'negative-loss')}
+        for _ in range(n_steps):
+            self._log_loss(loss, prefix='train', log_step=False)
+            self._meter.push('train-metrics/recall', terms['recall'])
+            self._meter.push('train-metrics/precision', terms['precision'])
+        for name, value in loss.items():
+            self.log(f'train/{name}', value)
+        self.log('epoch/lr', torch_helper.get_optim_lr(self.optimizer))
+        return loss
 
     def on_train_epoch_end(self) -> Dict[str, float]:
         """Log the epoch means; one host synchronisation per epoch (NaN check included)."""

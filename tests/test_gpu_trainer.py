@@ -248,3 +248,51 @@ def test_d128_trajectory_matches_reference(hip_device):
               f'outside, max |diff| {np.abs(ex - exp).max():.3e}')
         assert bad.mean() <= 1e-4, f'{name}: {bad.sum()} entries outside tolerance'
         assert np.abs(got - exp).max() <= lr / 10
+
+
+def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypatch):
+    """tools/train.py on the C2 shape (Cora-sized R-MAT, node2vec, L = 10, R = 2, 64-walk
+    batches, d = 128) with Philox walks and device negatives: word2vec/fit.py replays the steps
+    as HIP graphs of 16 (GraphedTrainerStep) after each epoch's first batch, and trains what the
+    eager loop (DW_TRAIN_GRAPH=0) trains — the same number of steps, Adam step counts, walks
+    (the dataset's epoch position) and, up to float summation order (the graphs take the atomic
+    output-table scatter at this size, the eager loop the records path), the same epoch losses
+    and tables."""
+    from tools import train as train_tool
+    from shallow_encoders.word2vec import graphed
+    from test_gpu_sgns import assert_no_row_drift, assert_params_close
+    replays = []
+    orig = graphed.GraphedTrainerStep.replay
+
+    def counting(self):
+        replays.append(self.unroll)
+        return orig(self)
+    monkeypatch.setattr(graphed.GraphedTrainerStep, 'replay', counting)
+    lr = 0.01
+    base = ['datamodule.dataset_name=graph_rmat', 'datamodule.additional_parameters.scale=12',
+            'datamodule.additional_parameters.n_edges=5429',
+            'datamodule.additional_parameters.graph_seed=0',
+            'datamodule.additional_parameters.walks_per_node=1',
+            'datamodule.additional_parameters.method_params.q=1',
+            'datamodule.additional_parameters.rng=philox', 'train.noise=device',
+            'model.embedding_size=128', f'train.optimizer.lr={lr}', 'train.max_epochs=2']
+    runs = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
+        out = str(tmp_path / f'runs{mode}')
+        torch.manual_seed(0)
+        last = train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
+                                f'output_dir={out}', f'train.experiment=g{mode}'] + base)
+        ck = os.path.join(out, 'graph_rmat', f'g{mode}', 'checkpoints', 'last.ckpt')
+        state = torch.load(ck, weights_only=True)
+        runs.append((last, state))
+    # 4,096 walks / 64 = 64 batches per epoch: 1 eager + 3 graphs of 16 + 15 eager, two epochs
+    assert replays == [16] * 6
+    (l0, s0), (l1, s1) = runs
+    assert s0['global_step'] == s1['global_step'] == 128
+    for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
+        np.testing.assert_allclose(l1[k], l0[k], rtol=1e-4)
+    for name in s0['state_dict']:
+        a, b = s1['state_dict'][name].numpy(), s0['state_dict'][name].numpy()
+        assert_params_close(a, b, lr, max_frac=1e-3, max_abs=lr)
+        assert_no_row_drift(a, b)
