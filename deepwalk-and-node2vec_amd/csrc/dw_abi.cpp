@@ -45,7 +45,7 @@ extern "C" {
 
 const char *dw_last_error_string(void) { return dw::g_err; }
 
-int dw_abi_version(void) { return 13; }
+int dw_abi_version(void) { return 14; }
 
 int dw_step_scalars_bind(const dw_step_scalars *dev) {
     dw::g_step = dev;

@@ -698,6 +698,9 @@ struct OutAdam {
     int32_t step = 0;
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
     int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
+    // lazy form: p already current to step - 1 (the catch-up's p-only replay, k_rows_adam
+    // P_ONLY), m and v still at last[row]: only their g = 0 recurrences are replayed here
+    bool p_current = false;
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -720,7 +723,13 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
     }
     for (int32_t t = from + 1; t < step; ++t) {
         const dw::AdamScalars h = dw::hist_at(oa.hist, t);
-        if (h.wd == 0.f) {
+        if (oa.p_current) {   // (every step here has wd == 0: the catch-up kept the row's last)
+#pragma unroll
+            for (int m = 0; m < VPL; ++m) {
+                mm[m] = fmaf(h.w1, -mm[m], mm[m]);   // adam_elem_g0's m, v operations
+                vv[m] = vv[m] * h.b2;
+            }
+        } else if (h.wd == 0.f) {
 #pragma unroll
             for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
         } else {
@@ -1962,7 +1971,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                float *w_out_local, float *m_out, float *v_out,
                                int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
                                int64_t *n_rows, const float *hist, int32_t step,
-                               int32_t *status, void *stream) {
+                               int32_t p_only, int32_t *status, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
                    owner >= 0 && owner < n_owners && step >= 1,
@@ -2002,8 +2011,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
-                        n_max, nullptr, hist, step - 1, stream);
+    return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
+                                n_rows, n_max, nullptr, hist, step - 1, p_only != 0, stream);
 }
 
 int dw_sgns_timing(int32_t enable) {
@@ -2241,7 +2250,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t *status, void *workspace,
+                             int32_t step, int32_t p_current, int32_t *status, void *workspace,
                              size_t workspace_bytes, int64_t *n_records, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
@@ -2250,6 +2259,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
+    oa.p_current = p_current != 0;
     const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
     if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);

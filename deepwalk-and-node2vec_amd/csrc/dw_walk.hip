@@ -583,6 +583,251 @@ __device__ int64_t n2v_pick_positions(const int32_t *__restrict__ col,
     return k;
 }
 
+// ---- node2vec picks with the step's class counts known (dw_edge_common_counts) ----------------
+// At a step t -> v over edge e, A = #{x in N(v) : x == t} and C = #{x in N(v) : x != t, x in
+// N(t)} are the edge's precomputed counts, so T = W(A, n - A - C, C) is known before any
+// neighbour is classified. D_i = W_i - U T is increasing in i, so the crossing round is found by
+// classifying rounds from the nearer end only — from the front while a round's last D is <= 0,
+// or from the back (prefix counts = totals - suffix counts) while the D before a round is > 0 —
+// and stops there: about a quarter of N(v) on average instead of all of it. The D values, T, M
+// and the bracketing test are the same expressions on the same integers as node2vec_pick_exact,
+// so the pick (or the serial fallback) is the same.
+
+// The classes of RB rounds (r0, r0 + dir, ...; rounds outside [0, rounds) are empty): the
+// membership searches of the RB rounds are interleaved so their dependent loads overlap.
+template <int RB>
+__device__ __forceinline__ void n2v_classify_trip(const int32_t *__restrict__ col, int64_t a,
+                                                  int64_t n, int64_t rounds, int32_t prev,
+                                                  const int32_t *np_lds, int np_lds_n,
+                                                  const int32_t *np_g, int64_t np_g_n,
+                                                  const uint32_t *np_bits, int64_t r0, int dir,
+                                                  int lane, uint64_t (&mp)[RB],
+                                                  uint64_t (&mq)[RB]) {
+    int32_t x[RB];
+    bool in_row[RB], memb[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int64_t r = r0 + dir * j;
+        const int64_t i = r * WAVE + lane;
+        in_row[j] = r >= 0 && r < rounds && i < n;
+        x[j] = in_row[j] ? col[a + i] : prev;   // outside the row: counted as neither class
+    }
+    if (np_bits) {
+        uint32_t w[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) w[j] = x[j] != prev ? np_bits[x[j] >> 5] : 0u;
+#pragma unroll
+        for (int j = 0; j < RB; ++j) memb[j] = ((w[j] >> (x[j] & 31)) & 1u) != 0u;
+    } else if (np_lds) {
+        const int nn = np_lds_n;
+        int base[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) base[j] = 0;
+        int len = nn;
+        while (len > 1) {
+            const int half = len >> 1;
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+                base[j] = (np_lds[base[j] + half] < x[j]) ? base[j] + half : base[j];
+            len -= half;
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            int lb = base[j];
+            if (nn > 0 && np_lds[lb] < x[j]) ++lb;
+            memb[j] = lb < nn && np_lds[lb] == x[j];
+        }
+    } else {
+        const int64_t nn = np_g_n;
+        int64_t base[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) base[j] = 0;
+        int64_t len = nn;
+        while (len > 1) {
+            const int64_t half = len >> 1;
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+                base[j] = (np_g[base[j] + half] < x[j]) ? base[j] + half : base[j];
+            len -= half;
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            int64_t lb = base[j];
+            if (nn > 0 && np_g[lb] < x[j]) ++lb;
+            memb[j] = lb < nn && np_g[lb] == x[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const bool is_p = in_row[j] && x[j] == prev;
+        mp[j] = __ballot(is_p);
+        mq[j] = __ballot(in_row[j] && !is_p && memb[j]);
+    }
+}
+
+#ifndef DW_N2V_CN_RB
+#define DW_N2V_CN_RB 4
+#endif
+#ifndef DW_N2V_CN_RBB
+#define DW_N2V_CN_RBB 8
+#endif
+
+// Returns the pick, or -1 (serial replay); `scanned` += the rounds classified.
+template <int RB>
+__device__ int64_t n2v_pick_counted_rb(const ReplayCtx &c, int64_t a, int64_t n, int32_t prev,
+                                       const int32_t *np_lds, int np_lds_n, const int32_t *np_g,
+                                       int64_t np_g_n, const uint32_t *np_bits, double U,
+                                       int64_t A, int64_t C, int lane, uint32_t &scanned) {
+    const int64_t rounds = (n + WAVE - 1) / WAVE;
+    const double ip = c.inv_p, iq = c.inv_q;
+    const double T = n2v_w(A, n - A - C, C, ip, iq);
+    const double UT = U * T;
+    const double M = exact_margin(n, T);
+    if (!(T - UT > 0.0)) return -1;   // D_{n-1} <= 0: rounding at the top end
+    // the crossing is in round r: D before it <= 0 < D at its end
+    auto resolve = [&](int64_t r, uint64_t mp, uint64_t mq, int64_t na, int64_t nc,
+                       double d_before) -> int64_t {
+        const int64_t base = r * WAVE;
+        const int64_t in_round = n - base < WAVE ? n - base : WAVE;
+        const uint64_t le = (lane == WAVE - 1) ? ~0ull : ((2ull << lane) - 1);  // lanes <= lane
+        const int64_t pa = na + __popcll(mp & le), pc = nc + __popcll(mq & le);
+        const int64_t i = base + lane;
+        const double d = n2v_w(pa, (i + 1) - pa - pc, pc, ip, iq) - UT;
+        const uint64_t over = __ballot(lane < in_round && d > 0.0);
+        if (!over) return -1;
+        const int first = __ffsll((unsigned long long)over) - 1;
+        const int64_t k = base + first;   // first i with D_i > 0
+        const double d_k = __shfl(d, first);
+        const double d_km1 = first > 0 ? __shfl(d, first - 1) : d_before;
+        if (k >= 1 && fabs(d_km1) <= M) return -1;
+        if (k <= n - 2 && fabs(d_k) <= M) return -1;
+        return k;
+    };
+    uint64_t mp[RB], mq[RB];
+    if (U < 0.5) {   // from the front
+        int64_t na = 0, nc = 0;
+        double d_prev = -UT;
+        for (int64_t r0 = 0; r0 < rounds; r0 += RB) {
+            n2v_classify_trip<RB>(c.col, a, n, rounds, prev, np_lds, np_lds_n, np_g, np_g_n,
+                                  np_bits, r0, 1, lane, mp, mq);
+            scanned += RB;
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+                const int64_t r = r0 + j;
+                if (r >= rounds) break;
+                const int64_t end = (r + 1) * WAVE < n ? (r + 1) * WAVE : n;
+                const int64_t ea = na + __popcll(mp[j]), ec = nc + __popcll(mq[j]);
+                const double d_end = n2v_w(ea, end - ea - ec, ec, ip, iq) - UT;
+                if (d_end > 0.0) return resolve(r, mp[j], mq[j], na, nc, d_prev);
+                d_prev = d_end;
+                na = ea;
+                nc = ec;
+            }
+        }
+        return -1;
+    }
+    int64_t sa = 0, sc = 0;   // from the back: the counts in the rounds after r
+    for (int64_t r0 = rounds - 1; r0 >= 0; r0 -= RB) {
+        n2v_classify_trip<RB>(c.col, a, n, rounds, prev, np_lds, np_lds_n, np_g, np_g_n, np_bits,
+                              r0, -1, lane, mp, mq);
+        scanned += RB;
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            const int64_t r = r0 - j;
+            if (r < 0) break;
+            const int64_t ba = A - sa - __popcll(mp[j]), bc = C - sc - __popcll(mq[j]);
+            const int64_t base = r * WAVE;
+            const double d_before = n2v_w(ba, base - ba - bc, bc, ip, iq) - UT;
+            if (!(d_before > 0.0)) return resolve(r, mp[j], mq[j], ba, bc, d_before);
+            sa += __popcll(mp[j]);
+            sc += __popcll(mq[j]);
+        }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int64_t n2v_pick_counted(const ReplayCtx &c, int64_t a, int64_t n,
+                                                    int32_t prev, const int32_t *np_lds,
+                                                    int np_lds_n, const int32_t *np_g,
+                                                    int64_t np_g_n, const uint32_t *np_bits,
+                                                    double U, int64_t A, int64_t C, int lane,
+                                                    uint32_t &scanned) {
+    // a bitmap test is one independent load: more rounds per trip; a search is a chain
+    return np_bits ? n2v_pick_counted_rb<DW_N2V_CN_RBB>(c, a, n, prev, np_lds, np_lds_n, np_g,
+                                                        np_g_n, np_bits, U, A, C, lane, scanned)
+                   : n2v_pick_counted_rb<DW_N2V_CN_RB>(c, a, n, prev, np_lds, np_lds_n, np_g,
+                                                       np_g_n, np_bits, U, A, C, lane, scanned);
+}
+
+// cn[e] for every directed edge e = (t -> v = col[e]) of row t: bit 31 = [t in N(v)], bits 0-30
+// = #{x in N(v) : x != t, x in N(t)} — the classes a node2vec step t -> v counts (above). Counted
+// over the shorter of N(t), N(v) against the other's adjacency hash (or list scan when it has
+// none), which is the same number on a simple graph (no repeated neighbours: networkx graphs and
+// the deduplicated R-MAT lists; the positions path above assumes the same). One lane per edge
+// when the shorter list has <= 16 entries, else the wave over that edge.
+__device__ __forceinline__ int64_t row_of_edge(const int64_t *__restrict__ row_ptr,
+                                               int64_t n_rows, int64_t e) {
+    int64_t lo = 0, hi = n_rows;   // last row with row_ptr[row] <= e
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (row_ptr[mid] <= e)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256)
+    k_edge_common(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                  const int64_t *__restrict__ adj_off, const int32_t *__restrict__ adj_hash,
+                  int64_t n_rows, int64_t n_edges, uint32_t *__restrict__ cn) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / WAVE;
+    uint32_t probes = 0;
+    for (int64_t e0 = wave * WAVE; e0 < n_edges; e0 += n_waves * WAVE) {
+        const int64_t e = e0 + lane;
+        const bool valid = e < n_edges;
+        int32_t t = 0, v = 0;
+        AdjRow rt{0, 0, 0, 0}, rv{0, 0, 0, 0};
+        if (valid) {
+            t = static_cast<int32_t>(row_of_edge(row_ptr, n_rows, e));
+            v = col[e];
+            rt = adj_row(row_ptr, adj_off, t);
+            rv = adj_row(row_ptr, adj_off, v);
+        }
+        const bool t_short = rt.n <= rv.n;
+        const AdjRow rs = t_short ? rt : rv, rl = t_short ? rv : rt;
+        uint32_t A = 0, C = 0;
+        const bool small = rs.n <= 16;
+        if (valid) A = lane_member(col, adj_hash, rv, t, probes) ? 1u : 0u;
+        if (valid && small)
+            for (int64_t k = 0; k < rs.n; ++k) {
+                const int32_t y = col[rs.a + k];
+                if (y != t && lane_member(col, adj_hash, rl, y, probes)) ++C;
+            }
+        uint64_t heavy = __ballot(valid && !small);
+        while (heavy) {   // one edge at a time, the wave over its shorter list
+            const int src = __ffsll((unsigned long long)heavy) - 1;
+            heavy &= heavy - 1;
+            const int32_t tt = __shfl(t, src);
+            const int64_t sa_ = __shfl(rs.a, src), sn = __shfl(rs.n, src);
+            const AdjRow l{__shfl(rl.a, src), __shfl(rl.n, src), __shfl(rl.h, src),
+                           static_cast<uint32_t>(__shfl(static_cast<int32_t>(rl.nb), src))};
+            uint32_t cnt = 0;
+            for (int64_t k = lane; k < sn; k += WAVE) {
+                const int32_t y = col[sa_ + k];
+                if (y != tt && lane_member(col, adj_hash, l, y, probes)) ++cnt;
+            }
+#pragma unroll
+            for (int off = WAVE / 2; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, WAVE);
+            if (lane == src) C = cnt;
+        }
+        if (valid) cn[e] = (A << 31) | (C & 0x7FFFFFFFu);
+    }
+}
+
 // The adjacency index of the probe-the-shorter-list steps (dw_walk_replay_indexed; adj_off ==
 // NULL: every step classifies N(v)) and the optional traffic counters (uint64[4] += {bytes,
 // hash probes, list entries read, steps}).
@@ -595,6 +840,7 @@ struct N2VIndex {
     const int32_t *hub_idx;    // row -> its neighbour bitmap (dw_hub_bitmaps), or -1
     const uint32_t *hub_bits;  // [n_hubs][hub_words]
     int64_t hub_words;
+    const uint32_t *edge_cn;   // per-edge class counts (dw_edge_common_counts), or NULL
 };
 
 __device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
@@ -627,6 +873,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     for (int64_t wk = (int64_t)blockIdx.x * REPLAY_WAVES + wv; wk < n_walks; wk += n_waves) {
         int32_t v = starts[wk];
         int32_t prev = -1;
+        int64_t e_in = -1;   // the edge prev -> v (its class counts: ix.edge_cn)
         int32_t *o = out + wk * (int64_t)L;
         if (lane == 0) o[0] = v;
         const double *u = uniforms + wk * (int64_t)(L - 1);
@@ -664,6 +911,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                     if (lane == 0) o[s] = child;
                     prev = v;
                     v = child;
+                    e_in = a + fp;
                     continue;
                 }
             }
@@ -677,9 +925,11 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 const int32_t hb = ix.hub_idx[prev];
                 if (hb >= 0) np_bits = ix.hub_bits + hb * ix.hub_words;
             }
+            // the class counts of prev -> v known: only the rounds up to the crossing classified
+            const bool known = fast && c.node2vec && prev >= 0 && ix.edge_cn && e_in >= 0;
             if (c.node2vec && prev >= 0) {
-                if (counted && lane == 0)   // N(v) read; N(prev) staged, bit-tested or searched
-                    loads += static_cast<uint32_t>(
+                if (counted && lane == 0 && !known)   // N(v) read; N(prev) staged, bit-tested
+                    loads += static_cast<uint32_t>(   // or searched
                         n + (np_bits ? n
                                      : pn <= NCAP ? pn
                                                   : n * static_cast<int64_t>(ceil_log2(pn + 1))));
@@ -697,17 +947,34 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 }
             }
             if (fast) {  // unweighted: the exact pick without the serial sums (above)
-                const int64_t fp =
-                    (!c.node2vec || prev < 0)
-                        ? uniform_pick_exact(uu, n)
-                        : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, uu,
-                                              reinterpret_cast<uint64_t *>(buf),
-                                              np_lds ? CH : CH + NCAP / 2, lane, np_bits);
+                int64_t fp;
+                if (known) {
+                    const uint32_t w = ix.edge_cn[e_in];
+                    uint32_t scanned = 0;
+                    fp = n2v_pick_counted(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n, np_bits,
+                                          uu, static_cast<int64_t>(w >> 31),
+                                          static_cast<int64_t>(w & 0x7FFFFFFFu), lane, scanned);
+                    if (counted && lane == 0) {   // the counts word; N(v) up to the crossing
+                        const int64_t ne = (int64_t)scanned * WAVE < n ? (int64_t)scanned * WAVE : n;
+                        loads += static_cast<uint32_t>(
+                            1 + ne + (np_bits ? ne
+                                              : pn <= NCAP ? pn
+                                                           : ne * static_cast<int64_t>(
+                                                                      ceil_log2(pn + 1))));
+                    }
+                } else {
+                    fp = (!c.node2vec || prev < 0)
+                             ? uniform_pick_exact(uu, n)
+                             : node2vec_pick_exact(c, a, n, prev, np_lds, np_lds_n, np_g, np_g_n,
+                                                   uu, reinterpret_cast<uint64_t *>(buf),
+                                                   np_lds ? CH : CH + NCAP / 2, lane, np_bits);
+                }
                 if (fp >= 0) {
                     const int32_t child = c.col[a + fp];
                     if (lane == 0) o[s] = child;
                     prev = v;
                     v = child;
+                    e_in = a + fp;
                     dw::wave_lds_sync();  // N(prev) / masks are rewritten next step
                     continue;
                 }
@@ -774,6 +1041,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             if (lane == 0) o[s] = child;
             prev = v;
             v = child;
+            e_in = a + pick;
         }
         if (lane == 0)
             for (; s < L; ++s) o[s] = -1;  // marks an aborted walk
@@ -1370,7 +1638,8 @@ int dw_walk_replay(const int64_t *row_ptr, const int32_t *col, const int32_t *co
 int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int32_t *col_sorted,
                            const int64_t *adj_off, const int32_t *adj_hash,
                            const int32_t *adj_hpos, const int32_t *hub_idx,
-                           const uint32_t *hub_bits, int64_t hub_words, int64_t n_rows,
+                           const uint32_t *hub_bits, int64_t hub_words,
+                           const uint32_t *edge_cn, int64_t n_rows,
                            const int32_t *starts, int64_t n_walks, int32_t walk_length, double p,
                            double q, const double *uniforms, int32_t *out, int32_t *status,
                            uint64_t *counters, void *stream) {
@@ -1408,11 +1677,26 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
                "dw_walk_replay_indexed: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
                       reinterpret_cast<unsigned long long *>(counters), hub_idx, hub_bits,
-                      hub_words};
+                      hub_words, edge_cn};
     hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
                        dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
                        n_walks, walk_length, uniforms, out, status, 1, ix);
     DW_LAUNCH_CHECK("dw_walk_replay_indexed");
+    return DW_OK;
+}
+
+int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                          const int32_t *adj_hash, int64_t n_rows, int64_t n_edges,
+                          uint32_t *edge_cn, void *stream) {
+    DW_REQUIRE(n_rows >= 0 && n_edges >= 0, "dw_edge_common_counts: negative size");
+    if (n_edges == 0 || n_rows == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && edge_cn,
+               "dw_edge_common_counts: null pointer");
+    int64_t blocks = (n_edges + 255) / 256;   // a wave per 64 edges
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_edge_common, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       row_ptr, col, adj_off, adj_hash, n_rows, n_edges, edge_cn);
+    DW_LAUNCH_CHECK("dw_edge_common_counts");
     return DW_OK;
 }
 

@@ -34,7 +34,7 @@ DW_S_RECORDS_FULL = 32
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -95,10 +95,10 @@ SIGNATURES = {
                                            ctypes.c_size_t, _p, _p]),
     'dw_sgns_owner_out_catch_up': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32,
                                                   _i32, _i64, _p, _u64, _u64, _p, _p, _p, _p, _p,
-                                                  _p, _p, _p, _i32, _p, _p]),
+                                                  _p, _p, _p, _i32, _i32, _p, _p]),
     'dw_sgns_owner_pass2_lazy': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p,
-                                                _p, _p, _p, _p, _i32, _p, _p, ctypes.c_size_t,
-                                                _p, _p]),
+                                                _p, _p, _p, _p, _i32, _i32, _p, _p,
+                                                ctypes.c_size_t, _p, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                                  _f32, _f32, _p, _p, ctypes.c_size_t, _p]),
@@ -133,8 +133,9 @@ SIGNATURES = {
                                                _i64, _p]),
     'dw_step_starts': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),
     'dw_walk_replay_inline': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
-    'dw_walk_replay_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p,
-                                              _i64, _i32, _f64, _f64, _p, _p, _p, _p, _p]),
+    'dw_walk_replay_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64,
+                                              _p, _i64, _i32, _f64, _f64, _p, _p, _p, _p, _p]),
+    'dw_edge_common_counts': (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _p, _p]),
     'dw_hub_bitmaps': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i64, _p, _p]),
     'dw_adj_hash_positions': (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,

@@ -190,7 +190,8 @@ class CSRGraph:
     def device_tensors(self, device=None, need_sorted: bool = False,
                        need_alias: bool = False, need_edges: bool = False,
                        need_adj: bool = False, need_adj_pos: bool = False,
-                       need_hub_bits: bool = False) -> Dict[str, torch.Tensor]:
+                       need_hub_bits: bool = False,
+                       need_edge_cn: bool = False) -> Dict[str, torch.Tensor]:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
         the per-row adjacency hash / its slots' neighbour positions on the device)."""
         dev = _native.require_device(device)
@@ -217,7 +218,7 @@ class CSRGraph:
             self._build_alias(dev)
         if need_edges and 'edges' not in d:
             self._build_edges(dev)
-        if (need_adj or need_adj_pos) and 'adj_off' not in d:
+        if (need_adj or need_adj_pos or need_edge_cn) and 'adj_off' not in d:
             self._build_adj_hash(dev)
         if need_adj_pos and 'adj_hpos' not in d:
             n_slots = d['adj_hash'].numel()
@@ -232,6 +233,14 @@ class CSRGraph:
             d['adj_hpos'] = hp
         if need_hub_bits and 'hub_idx' not in d:
             self._build_hub_bits(dev)
+        if need_edge_cn and 'edge_cn' not in d:
+            cn = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                _native.call('dw_edge_common_counts', _native.ptr(d['row_ptr']),
+                             _native.ptr(d['col']) if self.nnz else None,
+                             _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                             self.vocab_size, self.nnz, _native.ptr(cn), _native.stream(dev))
+            d['edge_cn'] = cn
         return d
 
     # rows longer than the replay walker's LDS stage (1,024) get a V-bit neighbour map, the

@@ -18,6 +18,7 @@ Two sampling modes, one kernel family each (include/dw_hip.h):
 ``walk(node) -> str`` keeps the reference signature; ``walk_batch`` is the batched device API
 (int32 vocabulary ids, shape [n_walks, length]) that feeds the fused SGNS kernel.
 """
+import os
 import sys
 from abc import ABC
 from typing import List, Optional, Sequence, Union
@@ -30,6 +31,12 @@ from shallow_encoders.graph.csr import CSRGraph
 from shallow_encoders.graph.rng import draw_uniforms_device
 
 _CSR_CACHE_ATTR = '_dw_csr_cache'
+
+
+def _edge_cn_enabled() -> bool:
+    """The node2vec replay's per-edge class counts (dw_edge_common_counts, built once per graph):
+    on by default; DW_N2V_EDGE_CN=0 classifies every step's whole N(v) (the same walks)."""
+    return os.environ.get('DW_N2V_EDGE_CN', '1') != '0'
 
 
 def _graph_fingerprint(graph) -> int:
@@ -216,7 +223,8 @@ class RandomWalk(ABC):
                                      need_alias=self._rng == 'philox',
                                      need_edges=(indexed and not n2v) or replay_inline,
                                      need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx,
-                                     need_hub_bits=replay_n2v_idx)
+                                     need_hub_bits=replay_n2v_idx,
+                                     need_edge_cn=replay_n2v_idx and _edge_cn_enabled())
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         if status is None:
@@ -248,6 +256,7 @@ class RandomWalk(ABC):
                                  _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
                                  _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
                                  _native.ptr(d['hub_bits']), d['hub_words'],
+                                 _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None),
                                  self._csr.vocab_size, _native.ptr(starts), n, L, float(p),
                                  float(q),
                                  _native.ptr(u) if u.numel() else None, _native.ptr(out),
@@ -299,7 +308,7 @@ class RandomWalk(ABC):
         if u.numel() != n * (L - 1):
             raise ValueError('uniforms must have n_walks * (length - 1) values')
         d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True,
-                                     need_hub_bits=True)
+                                     need_hub_bits=True, need_edge_cn=_edge_cn_enabled())
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -310,7 +319,9 @@ class RandomWalk(ABC):
                          _native.ptr(d['col']), _native.ptr(d['col_sorted']),
                          _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
                          _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
-                         _native.ptr(d['hub_bits']), d['hub_words'], self._csr.vocab_size,
+                         _native.ptr(d['hub_bits']), d['hub_words'],
+                         _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None),
+                         self._csr.vocab_size,
                          _native.ptr(starts), n, L, float(p), float(q),
                          _native.ptr(u) if u.numel() else None,
                          _native.ptr(out), _native.ptr(status), _native.ptr(counters),

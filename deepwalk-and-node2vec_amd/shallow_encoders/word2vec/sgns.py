@@ -419,8 +419,9 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(w_out_local), _native.ptr(g_out_local),
                          _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
-                         int(out_adam['step']), _native.ptr(status), _native.ptr(ws), ws.numel(),
-                         n_rec_p, _native.stream(dev))
+                         int(out_adam['step']), int(bool(out_adam.get('p_current', False))),
+                         _native.ptr(status), _native.ptr(ws), ws.numel(), n_rec_p,
+                         _native.stream(dev))
         return int(n_rec.value) if read_count else None
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),

@@ -758,6 +758,9 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = bool(lazy_out)
         super().__init__(*args, **kwargs)
         self.lazy_out = self.lazy_out and self._hip()
+        # the out catch-up writes p only where it can and pass 2 replays m, v itself (a third of
+        # the catch-up's writes); DW_LAZY_OUT_P_ONLY=0 writes whole rows there (the same tables)
+        self.p_only_out = os.environ.get('DW_LAZY_OUT_P_ONLY', '1') != '0'
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -784,7 +787,8 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist),
-                         self.step_count, _native.ptr(status), _native.stream(self.device))
+                         self.step_count, int(self.p_only_out), _native.ptr(status),
+                         _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -991,8 +995,9 @@ class OwnerLazyTables(OwnerTables):
     def out_adam_spec(self) -> Optional[dict]:
         spec = super().out_adam_spec()
         if spec is not None and self.lazy_out:
+            # (owner_lazy_step: catch_up_out of this batch ran before pass 1)
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                    'step': self.step_count}
+                    'step': self.step_count, 'p_current': self.p_only_out}
         return spec
 
     def full_w_out(self) -> torch.Tensor:

@@ -45,14 +45,25 @@ def main():
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     csr = rmat_graph(20, 10_000_000, 0, device=dev)
-    csr.device_tensors(dev)
-    res = {'lib': os.environ.get('DW_LIB_PATH', 'default'),
+    csr.device_tensors(dev, need_adj_pos=True, need_hub_bits=True, need_sorted=True)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    csr.device_tensors(dev, need_edge_cn=True)   # the per-edge class counts, built once
+    e1.record()
+    torch.cuda.synchronize(dev)
+    res = {'lib': os.environ.get('DW_LIB_PATH', 'default'), 'edge_cn_build_ms': e0.elapsed_time(e1)}
+    os.environ['DW_N2V_EDGE_CN'] = '0'
+    res['node2vec_p0.25_q4_nocn'] = rate(Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev),
+                                         args.n2v_walks, args.L, dev)
+    os.environ['DW_N2V_EDGE_CN'] = '1'
+    res.update({
            'node2vec_p0.25_q4': rate(Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev),
                                      args.n2v_walks, args.L, dev),
            'node2vec_p0.25_q4_csr': rate(Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev,
                                                   layout='csr'), args.n2v_walks, args.L, dev),
            'node2vec_p1_q1': rate(Node2Vec(csr, args.L, p=1.0, q=1.0, device=dev),
-                                  args.n2v_walks, args.L, dev)}
+                                  args.n2v_walks, args.L, dev)})
     w = Node2Vec(csr, args.L, p=0.25, q=4.0, device=dev)
     gen = random.Random(0)
     st = torch.arange(1, args.n2v_walks + 1, dtype=torch.int32, device=dev)

@@ -419,3 +419,73 @@ def test_indexed_node2vec_replay_equals_csr_replay_c3(p, q, hip_device):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     assert c['steps'] == starts.numel() * (L - 1)
     assert c['bytes'] >= c['steps'] * 48 + c['probes'] * 64
+
+
+def _edge_counts_host(row_ptr, col):
+    """edge_cn restated on the host: bit 31 = [t in N(v)], low bits = #{x in N(v): x != t,
+    x in N(t)} for every directed edge t -> v (the classes random_walk_generator.py:100-108
+    counts at a step t -> v)."""
+    n = len(row_ptr) - 1
+    sets = [set(col[row_ptr[i]:row_ptr[i + 1]].tolist()) for i in range(n)]
+    out = np.empty(len(col), dtype=np.uint32)
+    for t in range(n):
+        for e in range(row_ptr[t], row_ptr[t + 1]):
+            v = int(col[e])
+            nv = col[row_ptr[v]:row_ptr[v + 1]]
+            a = int((nv == t).sum())
+            c = len((sets[v] & sets[t]) - {t})
+            out[e] = (a << 31) | c
+    return out
+
+
+def _self_loop_graph():
+    # rows with self-loops (t in N(t), v in N(v)), a hub past the hash threshold and short rows
+    import networkx as nx
+    g = nx.Graph()
+    g.add_edges_from([(0, i) for i in range(1, 40)])
+    g.add_edges_from([(i, i + 1) for i in range(1, 39)])
+    g.add_edges_from([(0, 0), (5, 5), (7, 7), (3, 20), (20, 31)])
+    return CSRGraph.from_networkx(nx.relabel_nodes(g, {i: f'n{i}' for i in g.nodes}))
+
+
+@pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops'])
+def test_edge_common_counts_vs_host(which, hip_device):
+    """dw_edge_common_counts (the node2vec replay's per-edge class counts, counted over the
+    shorter list against the other's hash) equals the host restatement on every directed edge,
+    including self-loops and hub-to-hub edges."""
+    if which == 'karate':
+        csr = _csr(golden('walks_karate_node2vec_p1_q0.5.npz'))
+    elif which == 'rmat12':
+        csr = _csr(golden('walks_rmat12_node2vec_p0.25_q4.npz'))
+    else:
+        csr = _self_loop_graph()
+    d = csr.device_tensors(hip_device, need_edge_cn=True)
+    got = d['edge_cn'][:csr.nnz].cpu().numpy().view(np.uint32)
+    ref = _edge_counts_host(np.asarray(csr.row_ptr), np.asarray(csr.host_col()))
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0), (2.0, 0.5)])
+def test_node2vec_replay_edge_counts_same_walks(p, q, hip_device, monkeypatch):
+    """The replay with the per-edge class counts (a step classifies N(v) from its nearer end up
+    to the crossing) gives bit for bit the walks of the whole-row classification, from R-MAT 16's
+    hubs and random nodes; the counted launch reads fewer list entries."""
+    csr = rmat_graph(16, 600_000, 0, device=hip_device)
+    deg = csr.degree()
+    rng = np.random.default_rng(5)
+    hubs = np.argsort(-deg[1:])[:128] + 1
+    starts = torch.as_tensor(np.concatenate([np.resize(hubs, 1024),
+                                             rng.integers(1, csr.vocab_size, 1024)]).astype(np.int32))
+    L = 40
+    u = torch.from_numpy(rng.random((starts.numel(), L - 1))).to(hip_device)
+    w = Node2Vec(csr, L, p=p, q=q, device=hip_device)
+    monkeypatch.setenv('DW_N2V_EDGE_CN', '0')
+    ref = w.walk_batch(starts, uniforms=u).cpu().numpy()
+    c0 = w.count_replay_traffic(starts, u)
+    monkeypatch.setenv('DW_N2V_EDGE_CN', '1')
+    got = w.walk_batch(starts, uniforms=u).cpu().numpy()
+    out = torch.empty((starts.numel(), L), dtype=torch.int32, device=hip_device)
+    c1 = w.count_replay_traffic(starts, u, out=out)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    assert c1['steps'] == c0['steps'] and c1['entries'] < c0['entries']
