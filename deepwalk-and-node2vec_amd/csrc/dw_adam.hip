@@ -102,12 +102,7 @@ using dw::hist_at;
 // the barrier; thread 0 writes it after. STEP: replay the missed steps up to step - 1, then
 // apply `step` with the row's gradient g_rows[i]; else replay up to `step`. The step loop is
 // uniform: lanes past d carry zeros and are not stored.
-// P_ONLY (the lazy out slice's catch-up before pass 1, !STEP): where every replayed step has
-// weight_decay 0, only p is written and last[r] is left where it was — m and v do not depend on
-// p then, so the pass-2 update (lazy_row_step with p_current) replays them itself from last[r]
-// with the same operations; a row with a weight-decay step among its replays is written whole
-// and marked current, as without P_ONLY.
-template <bool STEP, bool P_ONLY = false>
+template <bool STEP>
 __global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
                 int32_t *__restrict__ last, int64_t n_table, int32_t d,
@@ -132,7 +127,6 @@ __global__ void __launch_bounds__(512)
         const int64_t o = r * d + e;
         float pp = live ? p[o] : 0.f, mm = live ? m[o] : 0.f, vv = live ? v[o] : 0.f;
         float gg = (STEP && live) ? g_rows[i * d + e] : 0.f;
-        bool any_wd = false;
         for (int32_t s = from + 1; s <= upto; ++s) {
             const dw::AdamScalars h = hist_at(hist, s);
             if (h.wd == 0.f) {
@@ -140,19 +134,15 @@ __global__ void __launch_bounds__(512)
             } else {
                 float z = 0.f;
                 dw::adam_elem(pp, z, mm, vv, h);
-                any_wd = true;
             }
         }
         if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
-        const bool whole = !P_ONLY || any_wd;   // (block-uniform: the scalars are per step)
         if (live) {
             p[o] = pp;
-            if (whole) {
-                m[o] = mm;
-                v[o] = vv;
-            }
+            m[o] = mm;
+            v[o] = vv;
         }
-        if (e == 0 && whole) last[r] = STEP ? step : upto;
+        if (e == 0) last[r] = STEP ? step : upto;
     }
 }
 
@@ -284,16 +274,6 @@ int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_
                  int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                  const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                  const float *hist, int32_t step, void *stream) {
-    return dw::adam_rows_launch(param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
-                                n_rows_dev, n_rows_max, grad_rows, hist, step, false, stream);
-}
-
-}  // extern "C"
-
-int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                         int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                         const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                         const float *hist, int32_t step, bool p_only, void *stream) {
     DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0 && step >= 0,
                "dw_adam_rows: bad sizes");
     if (n_rows_max == 0) return DW_OK;
@@ -308,14 +288,8 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
     const int threads = 64 * ((dim + 63) / 64);
-    DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays have no gradient");
     if (grad_rows)
         hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0,
-                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
-                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
-                           dyn, delta);
-    else if (p_only)
-        hipLaunchKernelGGL((k_rows_adam<false, true>), dim3((unsigned)blocks), dim3(threads), 0,
                            dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
                            n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
                            dyn, delta);
@@ -327,8 +301,6 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
 }
-
-extern "C" {
 
 int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                    const int64_t *n_rows_dev, int64_t n_rows_max, float *out,

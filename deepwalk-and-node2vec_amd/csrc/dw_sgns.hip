@@ -149,6 +149,7 @@ struct SgnsArgs {
     uint32_t *rec_counts;
     uint32_t *count_out;      //   n_owners == 1: the records are dense; their count goes here
     int64_t region;
+    bool walk_order = false;  //   one owner, presorted: values at b * T + t, keys not written
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
@@ -601,14 +602,16 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             const int c1 = __builtin_amdgcn_readlane(n_own, 16);
             const int c2 = __builtin_amdgcn_readlane(n_own, 32);
             const int c3 = __builtin_amdgcn_readlane(n_own, 48);
-            const int64_t at = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * a.region + filled +
-                               (q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2);
+            const int64_t at =
+                a.walk_order ? b * T   // (one owner: every slot kept, n_own = T)
+                             : ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * a.region + filled +
+                                   (q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2);
 #pragma unroll
             for (int k = 0; k < G16_TMAX / 16; ++k) {
                 const int tt = gl + 16 * k;
                 if (tt < n_own) {
                     const int32_t id = s_id[wv][q][tt];   // < 0: a bad id (one owner only)
-                    a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                    if (!a.walk_order) a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
                     a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
                                                      ok_c ? cid : 0);
                 }
@@ -698,9 +701,9 @@ struct OutAdam {
     int32_t step = 0;
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
     int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
-    // lazy form: p already current to step - 1 (the catch-up's p-only replay, k_rows_adam
-    // P_ONLY), m and v still at last[row]: only their g = 0 recurrences are replayed here
-    bool p_current = false;
+    // presorted records (dw_sgns_owner_presort): the sorted keys carry the index of their value
+    // in pass 1's walk-slot-ordered array; the gather reads vals[idx[e]]
+    const uint32_t *idx = nullptr;
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -723,13 +726,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
     }
     for (int32_t t = from + 1; t < step; ++t) {
         const dw::AdamScalars h = dw::hist_at(oa.hist, t);
-        if (oa.p_current) {   // (every step here has wd == 0: the catch-up kept the row's last)
-#pragma unroll
-            for (int m = 0; m < VPL; ++m) {
-                mm[m] = fmaf(h.w1, -mm[m], mm[m]);   // adam_elem_g0's m, v operations
-                vv[m] = vv[m] * h.b2;
-            }
-        } else if (h.wd == 0.f) {
+        if (h.wd == 0.f) {
 #pragma unroll
             for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
         } else {
@@ -823,7 +820,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 #pragma unroll
             for (int u = 0; u < GU; ++u) {
                 const bool in = e + u < e1;
-                const uint64_t v = in ? vals[e + u] : 0ull;
+                const uint64_t v = in ? vals[(ADAM && oa.idx) ? static_cast<int64_t>(oa.idx[e + u])
+                                                              : e + u]
+                                      : 0ull;
                 k[u] = in ? keys[e + u] : last;
                 coef[u] = in ? __uint_as_float(static_cast<uint32_t>(v >> 32)) : 0.f;
                 const float *src = w_in + static_cast<int64_t>(static_cast<uint32_t>(v)) * d + lane;
@@ -1680,6 +1679,9 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     // n_owners > 1: per-wave regions in (k0, v0), compacted into (k1, v1); one owner keeps
     // every slot, so the regions tile (k1, v1) densely and pass 1 writes there directly
     const bool dense = a.n_owners == 1;
+    const bool presorted = (order_ready & 2) != 0;   // dw_sgns_owner_presort ran: values only
+    DW_REQUIRE(!presorted || dense, "dw_sgns_owner_pass1: presorted records need one owner");
+    a.walk_order = presorted;
     a.rec_key = dense ? ws.k1 : ws.k0;
     a.rec_val = dense ? ws.v1 : ws.v0;
     a.count_out = dense ? ws.count : nullptr;
@@ -1687,7 +1689,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     a.region = lay.region;
     a.occ_per_wave = lay.region / T;
     if (a.batch > 0) {
-        if (!order_ready) {  // the centres in node order (stable: walk order within a node)
+        if (!(order_ready & 1)) {  // the centres in node order (stable: walk order within a node)
             rc = owner_order(a, occ, nullptr, nullptr, st);
             if (rc != DW_OK) return rc;
         }
@@ -1714,13 +1716,23 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
 
 int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
                        const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
-                       size_t workspace_bytes, int64_t *n_records, hipStream_t st) {
+                       size_t workspace_bytes, int64_t *n_records, hipStream_t st,
+                       bool presorted = false) {
     Workspace ws;
     OwnerLayout lay;
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
                              "dw_sgns_owner_pass2");
     if (rc != DW_OK) return rc;
     const int64_t bound = n_centres * T;
+    if (presorted) {   // dw_sgns_owner_presort's order + pass 1's walk-order values: no sort here
+        DW_REQUIRE(oa && !n_records, "dw_sgns_owner_pass2_lazy: presorted needs n_records NULL");
+        OutAdam o = *oa;
+        o.idx = reinterpret_cast<const uint32_t *>(ws.v0);
+        g_timer.mark(2, st);
+        if (bound > 0) rc = launch_pass2(ws.k0, ws.v1, bound, w_in, g_out, d, &o, local_rows, st);
+        g_timer.mark(3, st);
+        return rc;
+    }
     const int64_t *range = nullptr;
     int64_t n_rec = bound;
     if (n_records) {
@@ -1960,6 +1972,31 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     }
 }
 
+// dw_sgns_owner_presort (one owner): every slot's row keyed at its walk-order position b * T + t
+// (the rows k_out_claim and pass 1 compute: contexts from the walk, negatives from Philox), with
+// that position as the value. Sorted before pass 1, on a side stream beside the out rows'
+// catch-up, the records' order is ready when pass 1 has written their coefficients.
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
+    k_presort_keys(SgnsArgs a, uint32_t *__restrict__ keys, uint32_t *__restrict__ pos) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int T = a.C * (1 + a.K);
+    const int64_t per = a.L - 2 * a.R;
+    for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; b < a.batch;
+         b += n_waves) {
+        if (lane >= T) continue;
+        const int64_t w = b / per, i = a.R + b % per;
+        const int32_t c = a.walks[w * a.L + i];
+        int64_t o = 0;   // a bad centre or row: a zero record on row 0, as pass 1 writes it
+        if (c >= 0 && c < a.V) {
+            o = row_id<true>(a, b, a.walks + w * a.L, i, lane);
+            if (o < 0 || o >= a.V) o = 0;
+        }
+        keys[b * T + lane] = static_cast<uint32_t>(o);
+        pos[b * T + lane] = static_cast<uint32_t>(b * T + lane);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1971,7 +2008,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                float *w_out_local, float *m_out, float *v_out,
                                int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
                                int64_t *n_rows, const float *hist, int32_t step,
-                               int32_t p_only, int32_t *status, void *stream) {
+                               int32_t *status, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
                    owner >= 0 && owner < n_owners && step >= 1,
@@ -2011,8 +2048,68 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
-                                n_rows, n_max, nullptr, hist, step - 1, p_only != 0, stream);
+    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
+                        n_max, nullptr, hist, step - 1, stream);
+}
+
+int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                          int32_t *status, void *workspace, size_t workspace_bytes,
+                          void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   vocab_size >= 1 && neg_samples >= 0,
+               "dw_sgns_owner_presort: bad sizes");
+    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= WAVE,
+               "dw_sgns_owner_presort: 2R(1+K) must be <= 64");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(walks && status && workspace, "dw_sgns_owner_presort: null pointer");
+    hipStream_t st = dw::as_stream(stream);
+    SgnsArgs a = base_args(vocab_size, 64, neg_samples, nullptr, nullptr, nullptr, nullptr, noise,
+                           seed, noise_offset, 0.f, nullptr, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    const int64_t T = (int64_t)a.C * (1 + neg_samples);
+    Workspace ws;
+    OwnerLayout lay;
+    int rc = owner_workspace(a.batch, T, vocab_size, workspace, workspace_bytes, &ws, &lay, st,
+                             "dw_sgns_owner_presort");
+    if (rc != DW_OK) return rc;
+    const int64_t n = a.batch * T;
+    DW_REQUIRE(n < (int64_t(1) << 32), "dw_sgns_owner_presort: too many records");
+    uint32_t *p0 = reinterpret_cast<uint32_t *>(ws.v0), *p1 = p0 + n;   // v0 holds 2n u32
+    int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_presort_keys, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
+                       a, ws.k0, p0);
+    DW_LAUNCH_CHECK("dw_sgns_owner_presort/keys");
+    rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1), pb(p0, p1);
+    size_t need = 0;
+    if (sort_pairs(nullptr, need, kb, pb, static_cast<uint32_t>(n), end_bit_for(vocab_size),
+                   st) != hipSuccess ||
+        need > ws.cub_bytes) {
+        dw::set_error("dw_sgns_owner_presort: sort workspace too small");
+        return DW_E_HIP;
+    }
+    size_t cb = ws.cub_bytes;
+    hipError_t e = sort_pairs(ws.cub, cb, kb, pb, static_cast<uint32_t>(n),
+                              end_bit_for(vocab_size), st);
+    if (e != hipSuccess) {
+        dw::set_error("dw_sgns_owner_presort: sort failed: %s", hipGetErrorString(e));
+        return DW_E_HIP;
+    }
+    // the order where pass 2 reads it (k0, and the first half of v0); pass 1 writes only v1
+    if (kb.current() != ws.k0 &&
+        (hipMemcpyAsync(ws.k0, kb.current(), n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+         hipMemcpyAsync(p0, pb.current(), n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)) {
+        dw::set_error("dw_sgns_owner_presort: copy failed");
+        return DW_E_HIP;
+    }
+    return DW_OK;
 }
 
 int dw_sgns_timing(int32_t enable) {
@@ -2250,8 +2347,9 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t p_current, int32_t *status, void *workspace,
-                             size_t workspace_bytes, int64_t *n_records, void *stream) {
+                             int32_t step, int32_t presorted, int32_t *status,
+                             void *workspace, size_t workspace_bytes, int64_t *n_records,
+                             void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
                "dw_sgns_owner_pass2_lazy: bad sizes");
@@ -2259,13 +2357,12 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
-    oa.p_current = p_current != 0;
     const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
     if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
-                              dw::as_stream(stream));
+                              dw::as_stream(stream), presorted != 0);
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

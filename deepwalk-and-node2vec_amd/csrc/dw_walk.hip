@@ -760,11 +760,17 @@ __device__ __forceinline__ int64_t n2v_pick_counted(const ReplayCtx &c, int64_t 
 }
 
 // cn[e] for every directed edge e = (t -> v = col[e]) of row t: bit 31 = [t in N(v)], bits 0-30
-// = #{x in N(v) : x != t, x in N(t)} — the classes a node2vec step t -> v counts (above). Counted
-// over the shorter of N(t), N(v) against the other's adjacency hash (or list scan when it has
-// none), which is the same number on a simple graph (no repeated neighbours: networkx graphs and
-// the deduplicated R-MAT lists; the positions path above assumes the same). One lane per edge
-// when the shorter list has <= 16 entries, else the wave over that edge.
+// = #{x in N(v) : x != t, x in N(t)} — the classes a node2vec step t -> v counts (above). With
+// I = |N(t) ∩ N(v)|, counted over the shorter list against the other row (the same number from
+// either side on a simple graph: no repeated neighbours, as networkx graphs and the deduplicated
+// R-MAT lists; the positions path above assumes the same), C(t -> v) = I - [t in N(v) and t in
+// N(t)] and C(v -> t) = I - [v in N(v)]: one count serves both directions of an undirected edge,
+// so it is computed once, from the side t < v, and the reverse entry found through v's position
+// table (adj_hpos). Membership in a row with a neighbour bitmap (dw_hub_bitmaps) is one 4-B test
+// inside that row's V-bit map (L2-resident for the many edges that probe one hub), else a probe
+// of the row's adjacency hash or a scan of its short list. One lane per edge when the shorter
+// list has <= 16 entries, else the wave over that edge. The build is bound by random lines: at
+// C3, sum over edges of min(deg) = 5.5e9 tests, 79% of edges with both degrees > 16.
 __device__ __forceinline__ int64_t row_of_edge(const int64_t *__restrict__ row_ptr,
                                                int64_t n_rows, int64_t e) {
     int64_t lo = 0, hi = n_rows;   // last row with row_ptr[row] <= e
@@ -778,10 +784,32 @@ __device__ __forceinline__ int64_t row_of_edge(const int64_t *__restrict__ row_p
     return lo;
 }
 
+struct EdgeIndex {   // the membership tests' index (dw_edge_common_counts)
+    const int32_t *col;
+    const int64_t *adj_off;
+    const int32_t *adj_hash;
+    const int32_t *adj_hpos;
+    const int32_t *hub_idx;    // row -> its bitmap, -1 (or NULL: no bitmaps)
+    const uint32_t *hub_bits;
+    int64_t hub_words;
+};
+
+__device__ __forceinline__ const uint32_t *row_bits(const EdgeIndex &x, int32_t row) {
+    if (!x.hub_idx) return nullptr;
+    const int32_t h = x.hub_idx[row];
+    return h >= 0 ? x.hub_bits + h * x.hub_words : nullptr;
+}
+
+// y in N(row)? (bitmap, hash or list scan)
+__device__ __forceinline__ bool edge_member(const EdgeIndex &x, const uint32_t *bits,
+                                            const AdjRow &r, int32_t y, uint32_t &probes) {
+    if (bits) return ((bits[y >> 5] >> (y & 31)) & 1u) != 0u;
+    return lane_member(x.col, x.adj_hash, r, y, probes);
+}
+
 __global__ void __launch_bounds__(256)
-    k_edge_common(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-                  const int64_t *__restrict__ adj_off, const int32_t *__restrict__ adj_hash,
-                  int64_t n_rows, int64_t n_edges, uint32_t *__restrict__ cn) {
+    k_edge_common(EdgeIndex x, const int64_t *__restrict__ row_ptr, int64_t n_rows,
+                  int64_t n_edges, uint32_t *__restrict__ cn) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / WAVE;
@@ -791,40 +819,51 @@ __global__ void __launch_bounds__(256)
         const bool valid = e < n_edges;
         int32_t t = 0, v = 0;
         AdjRow rt{0, 0, 0, 0}, rv{0, 0, 0, 0};
+        const uint32_t *bt = nullptr, *bv = nullptr;
         if (valid) {
             t = static_cast<int32_t>(row_of_edge(row_ptr, n_rows, e));
-            v = col[e];
-            rt = adj_row(row_ptr, adj_off, t);
-            rv = adj_row(row_ptr, adj_off, v);
+            v = x.col[e];
+            rt = adj_row(row_ptr, x.adj_off, t);
+            rv = adj_row(row_ptr, x.adj_off, v);
+            bt = row_bits(x, t);
+            bv = row_bits(x, v);
         }
+        // A = [t in N(v)]; an undirected edge's pair is counted from its t < v side
+        const bool A = valid && edge_member(x, bv, rv, t, probes);
+        const bool mine = valid && (t <= v || !A);
+        int64_t rev = -1;   // the entry of v -> t, written here too
+        if (mine && A && t < v) {
+            const int64_t pos = lane_position(x.col, x.adj_hash, x.adj_hpos, rv, t, probes);
+            rev = pos >= 0 ? rv.a + pos : -1;
+        }
+        const bool self_t = mine && A && edge_member(x, bt, rt, t, probes);
+        const bool self_v = rev >= 0 && edge_member(x, bv, rv, v, probes);
         const bool t_short = rt.n <= rv.n;
         const AdjRow rs = t_short ? rt : rv, rl = t_short ? rv : rt;
-        uint32_t A = 0, C = 0;
+        const uint32_t *bl = t_short ? bv : bt;
+        uint32_t I = 0;
         const bool small = rs.n <= 16;
-        if (valid) A = lane_member(col, adj_hash, rv, t, probes) ? 1u : 0u;
-        if (valid && small)
-            for (int64_t k = 0; k < rs.n; ++k) {
-                const int32_t y = col[rs.a + k];
-                if (y != t && lane_member(col, adj_hash, rl, y, probes)) ++C;
-            }
-        uint64_t heavy = __ballot(valid && !small);
+        if (mine && small)
+            for (int64_t k = 0; k < rs.n; ++k)
+                if (edge_member(x, bl, rl, x.col[rs.a + k], probes)) ++I;
+        uint64_t heavy = __ballot(mine && !small);
         while (heavy) {   // one edge at a time, the wave over its shorter list
             const int src = __ffsll((unsigned long long)heavy) - 1;
             heavy &= heavy - 1;
-            const int32_t tt = __shfl(t, src);
             const int64_t sa_ = __shfl(rs.a, src), sn = __shfl(rs.n, src);
             const AdjRow l{__shfl(rl.a, src), __shfl(rl.n, src), __shfl(rl.h, src),
                            static_cast<uint32_t>(__shfl(static_cast<int32_t>(rl.nb), src))};
+            const uint32_t *b = reinterpret_cast<const uint32_t *>(
+                __shfl(reinterpret_cast<unsigned long long>(bl), src));
             uint32_t cnt = 0;
-            for (int64_t k = lane; k < sn; k += WAVE) {
-                const int32_t y = col[sa_ + k];
-                if (y != tt && lane_member(col, adj_hash, l, y, probes)) ++cnt;
-            }
+            for (int64_t k = lane; k < sn; k += WAVE)
+                if (edge_member(x, b, l, x.col[sa_ + k], probes)) ++cnt;
 #pragma unroll
             for (int off = WAVE / 2; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, WAVE);
-            if (lane == src) C = cnt;
+            if (lane == src) I = cnt;
         }
-        if (valid) cn[e] = (A << 31) | (C & 0x7FFFFFFFu);
+        if (mine) cn[e] = (A ? 0x80000000u : 0u) | ((I - (self_t ? 1u : 0u)) & 0x7FFFFFFFu);
+        if (rev >= 0) cn[rev] = 0x80000000u | ((I - (self_v ? 1u : 0u)) & 0x7FFFFFFFu);
     }
 }
 
@@ -1667,11 +1706,14 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
                               stream);
     int64_t blocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
     if (blocks > 16384) blocks = 16384;
-    // N(prev) mapped into N(v) when deg(v) > b_factor deg(prev); DW_N2V_BFACTOR overrides
-    static const int32_t b_factor = [] {
+    // N(prev) mapped into N(v) when deg(v) > b_factor deg(prev); DW_N2V_BFACTOR overrides.
+    // With the per-edge class counts a classification scans ~deg(v)/4 entries, so the mapping
+    // pays only for a much shorter N(prev): 64 (C3, 65,536 walks: 14.5 ms at 16, 13.5 at 64,
+    // 13.6 at 256, 17.8 at 4); without the counts 16 (scripts/gpu_n2v_cn.sh)
+    const int32_t b_factor = [edge_cn] {
         const char *e = getenv("DW_N2V_BFACTOR");
         const int f = e ? atoi(e) : 0;
-        return f > 0 ? f : 16;
+        return f > 0 ? f : (edge_cn ? 64 : 16);
     }();
     DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
                "dw_walk_replay_indexed: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
@@ -1686,16 +1728,20 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
 }
 
 int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
-                          const int32_t *adj_hash, int64_t n_rows, int64_t n_edges,
-                          uint32_t *edge_cn, void *stream) {
+                          const int32_t *adj_hash, const int32_t *adj_hpos,
+                          const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                          int64_t n_rows, int64_t n_edges, uint32_t *edge_cn, void *stream) {
     DW_REQUIRE(n_rows >= 0 && n_edges >= 0, "dw_edge_common_counts: negative size");
     if (n_edges == 0 || n_rows == 0) return DW_OK;
-    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && edge_cn,
+    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && adj_hpos && edge_cn,
                "dw_edge_common_counts: null pointer");
+    DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
+               "dw_edge_common_counts: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
     int64_t blocks = (n_edges + 255) / 256;   // a wave per 64 edges
     if (blocks > 65536) blocks = 65536;
+    const EdgeIndex x{col, adj_off, adj_hash, adj_hpos, hub_idx, hub_bits, hub_words};
     hipLaunchKernelGGL(k_edge_common, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
-                       row_ptr, col, adj_off, adj_hash, n_rows, n_edges, edge_cn);
+                       x, row_ptr, n_rows, n_edges, edge_cn);
     DW_LAUNCH_CHECK("dw_edge_common_counts");
     return DW_OK;
 }

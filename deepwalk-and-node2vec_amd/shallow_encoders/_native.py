@@ -95,10 +95,12 @@ SIGNATURES = {
                                            ctypes.c_size_t, _p, _p]),
     'dw_sgns_owner_out_catch_up': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32,
                                                   _i32, _i64, _p, _u64, _u64, _p, _p, _p, _p, _p,
-                                                  _p, _p, _p, _i32, _i32, _p, _p]),
+                                                  _p, _p, _p, _i32, _p, _p]),
     'dw_sgns_owner_pass2_lazy': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p,
                                                 _p, _p, _p, _p, _i32, _i32, _p, _p,
                                                 ctypes.c_size_t, _p, _p]),
+    'dw_sgns_owner_presort': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _p, _u64, _u64, _p,
+                                             _p, ctypes.c_size_t, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                                  _f32, _f32, _p, _p, ctypes.c_size_t, _p]),
@@ -135,7 +137,8 @@ SIGNATURES = {
     'dw_walk_replay_inline': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
     'dw_walk_replay_indexed': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64,
                                               _p, _i64, _i32, _f64, _f64, _p, _p, _p, _p, _p]),
-    'dw_edge_common_counts': (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _p, _p]),
+    'dw_edge_common_counts': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
+                                             _p]),
     'dw_hub_bitmaps': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i64, _p, _p]),
     'dw_adj_hash_positions': (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,

@@ -234,12 +234,16 @@ class CSRGraph:
         if need_hub_bits and 'hub_idx' not in d:
             self._build_hub_bits(dev)
         if need_edge_cn and 'edge_cn' not in d:
+            if 'adj_hpos' not in d or 'hub_idx' not in d:
+                self.device_tensors(dev, need_adj_pos=True, need_hub_bits=True)
             cn = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
             with torch.cuda.device(dev):
                 _native.call('dw_edge_common_counts', _native.ptr(d['row_ptr']),
                              _native.ptr(d['col']) if self.nnz else None,
                              _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                             self.vocab_size, self.nnz, _native.ptr(cn), _native.stream(dev))
+                             _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
+                             _native.ptr(d['hub_bits']), d['hub_words'], self.vocab_size,
+                             self.nnz, _native.ptr(cn), _native.stream(dev))
             d['edge_cn'] = cn
         return d
 

@@ -96,7 +96,9 @@ class CSVMetricLogger:
 
 def _graph_source(trainer: Word2VecTrainer, dataloader, step_sched: bool):
     """The RandomWalkDataset behind a walk-batch loader whose steps can be replayed as HIP graphs
-    (word2vec/graphed.py GraphedTrainerStep), or None. DW_TRAIN_GRAPH=0 keeps every step eager."""
+    (word2vec/graphed.py GraphedTrainerStep), or None. DW_TRAIN_GRAPH=0 keeps every step eager;
+    DW_TRAIN_GRAPH_SCATTER=records makes the graphs take the eager loop's records step even
+    where the atomic scatter is faster (GraphedTrainerStep's ``scatter``)."""
     from shallow_encoders.config_parser.core import WalkBatchLoader
     from shallow_encoders.word2vec.graphed import GraphedTrainerStep
     if os.environ.get('DW_TRAIN_GRAPH', '1') == '0' or step_sched:
@@ -160,7 +162,8 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
                 run(batch)
                 n_rep = (len(rwd) - rwd._index) // B // graph_unroll
                 if n_rep > 0:
-                    gs = GraphedTrainerStep(trainer, rwd, B, n_rep * graph_unroll, graph_unroll)
+                    gs = GraphedTrainerStep(trainer, rwd, B, n_rep * graph_unroll, graph_unroll,
+                                            os.environ.get('DW_TRAIN_GRAPH_SCATTER', 'auto'))
                     for _ in range(n_rep):
                         loss = trainer.push_replayed(gs.replay(), graph_unroll)
                         if log_dir and (-global_step) % log_every_n_steps < graph_unroll:

@@ -339,7 +339,14 @@ class GraphedTrainerStep:
                 and mine == {id(w_in), id(w_out)} and w_in.device.type == 'cuda'
                 and trainer._context_radius is not None)
 
-    def __init__(self, trainer, dataset, B: int, n_steps: int, unroll: int = 16):
+    def __init__(self, trainer, dataset, B: int, n_steps: int, unroll: int = 16,
+                 scatter: str = 'auto'):
+        """``scatter``: 'auto' (the atomic output-table scatter for <= 65,536 records, else the
+        fused records step), 'records' (always the fused records step: the eager loop's kernels,
+        so a graph trains what the eager steps train up to float-atomic order at chunk
+        boundaries) or 'atomic'."""
+        if scatter not in ('auto', 'records', 'atomic'):
+            raise ValueError(f'GraphedTrainerStep: unknown scatter {scatter!r}')
         if unroll < 2 or unroll % 2:
             raise ValueError('GraphedTrainerStep: unroll must be even and >= 2')
         if not self.eligible(trainer, dataset):
@@ -359,7 +366,8 @@ class GraphedTrainerStep:
         self.R, self.K = R, K
         self.centres = self.B * (L - 2 * R)
         records = self.centres * 2 * R * (1 + K)
-        self.scatter = 'atomic' if records <= 65_536 else None   # (None: the fused step)
+        self.scatter = ('atomic' if scatter == 'atomic' or (scatter == 'auto' and records <= 65_536)
+                        else None)   # (None: the fused step)
         if self.scatter is None and not _use_records('sorted', 2 * R, K, w_in.shape[0]):
             raise ValueError('GraphedTrainerStep: shape outside the records path')
         opt = trainer.optimizer

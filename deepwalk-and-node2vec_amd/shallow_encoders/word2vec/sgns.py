@@ -322,13 +322,15 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
-                     order_ready: bool = False) -> torch.Tensor:
+                     order_ready: bool = False, presorted: bool = False) -> torch.Tensor:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
     partial centre-table gradient of the owned slots; returns the float64[4] loss accumulator
     (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
-    ``order_ready``: sgns_owner_prepare already built the centre order for these walks."""
+    ``order_ready``: sgns_owner_prepare already built the centre order for these walks;
+    ``presorted``: sgns_owner_presort already sorted these walks' records (one owner): pass 1
+    writes only their values, in walk-slot order."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -355,13 +357,37 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
-                     int(owner), int(n_owners), local_rows, 1 if order_ready else 0,
+                     int(owner), int(n_owners), local_rows,
+                     (1 if order_ready else 0) | (2 if presorted else 0),
                      _native.ptr(w_in),
                      _native.ptr(w_out_local), _native.ptr(g_in), _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),
                      _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws), ws.numel(),
                      _native.stream(dev))
     return loss_acc
+
+
+def sgns_owner_presort(walks: torch.Tensor, context_radius: int, neg_samples: int,
+                       vocab_size: int, local_rows: int, *, seed: int = 0, noise_offset: int = 0,
+                       noise: Optional[torch.Tensor] = None,
+                       status: Optional[torch.Tensor] = None) -> None:
+    """dw_sgns_owner_presort (one owner): the records' order for ``walks`` (every slot's row —
+    contexts, and the negatives pass 1 will draw — sorted with its walk-slot position), before
+    pass 1, so that pass 1 (presorted=True) writes only the values and pass 2 (out_adam
+    'presorted') gathers without sorting. The same workspace as the passes."""
+    dev = walks.device
+    if walks.dtype != torch.int32 or walks.dim() != 2:
+        raise TypeError('walks must be int32 [n_walks, L]')
+    n, L = walks.shape
+    R, K = int(context_radius), int(neg_samples)
+    n_centres = n * (L - 2 * R)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
+    with torch.cuda.device(dev):
+        _native.call('dw_sgns_owner_presort', _native.ptr(walks), n, L, R, K, int(vocab_size),
+                     _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
+                     _native.ptr(status), _native.ptr(ws), ws.numel(), _native.stream(dev))
 
 
 def sgns_owner_prepare(walks: torch.Tensor, context_radius: int, neg_samples: int,
@@ -419,7 +445,7 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(w_out_local), _native.ptr(g_out_local),
                          _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
-                         int(out_adam['step']), int(bool(out_adam.get('p_current', False))),
+                         int(out_adam['step']), int(bool(out_adam.get('presorted', False))),
                          _native.ptr(status), _native.ptr(ws), ws.numel(), n_rec_p,
                          _native.stream(dev))
         return int(n_rec.value) if read_count else None

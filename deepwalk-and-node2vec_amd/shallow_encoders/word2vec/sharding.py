@@ -758,9 +758,11 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = bool(lazy_out)
         super().__init__(*args, **kwargs)
         self.lazy_out = self.lazy_out and self._hip()
-        # the out catch-up writes p only where it can and pass 2 replays m, v itself (a third of
-        # the catch-up's writes); DW_LAZY_OUT_P_ONLY=0 writes whole rows there (the same tables)
-        self.p_only_out = os.environ.get('DW_LAZY_OUT_P_ONLY', '1') != '0'
+        # one rank, lazy out slice: the records sorted before pass 1 on the side stream, beside
+        # the out rows' catch-up (dw_sgns_owner_presort); DW_PRESORT=0 sorts them in pass 2
+        self.presort = (self.lazy_out and not self.multi
+                        and os.environ.get('DW_PRESORT', '1') != '0')
+        self._presorted = False
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -787,8 +789,7 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist),
-                         self.step_count, int(self.p_only_out), _native.ptr(status),
-                         _native.stream(self.device))
+                         self.step_count, _native.ptr(status), _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -925,12 +926,18 @@ class OwnerLazyTables(OwnerTables):
         centre order and in-table catch-up (a one-block sort, then ALU-bound replays) run on
         the side stream beside the out rows' claim and catch-up (bandwidth-bound); the current
         stream waits for both."""
+        self._presorted = False
         if self.lazy_out and not self.multi:
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
+                if self.presort:
+                    from shallow_encoders.word2vec.sgns import sgns_owner_presort
+                    sgns_owner_presort(walks, context_radius, neg_samples, self.V, self.S,
+                                       seed=seed, noise_offset=noise_offset, status=status)
+                    self._presorted = True
                 self.prepare(walks, context_radius, neg_samples)
                 self.catch_up()
                 join = torch.cuda.Event()
@@ -995,9 +1002,8 @@ class OwnerLazyTables(OwnerTables):
     def out_adam_spec(self) -> Optional[dict]:
         spec = super().out_adam_spec()
         if spec is not None and self.lazy_out:
-            # (owner_lazy_step: catch_up_out of this batch ran before pass 1)
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                    'step': self.step_count, 'p_current': self.p_only_out}
+                    'step': self.step_count, 'presorted': self._presorted}
         return spec
 
     def full_w_out(self) -> torch.Tensor:
@@ -1026,7 +1032,8 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
-                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True)
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
+                     presorted=tables._presorted)
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,

@@ -212,11 +212,14 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
 /* edge_cn uint32[n_edges] for every directed edge e = (t -> v = col[e]) of row t: bit 31 =
  * [t in N(v)], bits 0-30 = #{x in N(v) : x != t, x in N(t)} — the class counts (x == prev, x a
  * neighbour of prev) of a node2vec step t -> v (random_walk_generator.py:100-108), computed once
- * per graph over the shorter list against the other's adjacency hash (dw_adj_hash_build). The
- * graph must be simple (no repeated neighbour in a row). */
+ * per graph over the shorter list against the other row: its neighbour bitmap (hub_idx /
+ * hub_bits of dw_hub_bitmaps; NULL = none), else its adjacency hash (dw_adj_hash_build); both
+ * directions of an undirected edge from one count (the reverse entry through adj_hpos,
+ * dw_adj_hash_positions). The graph must be simple (no repeated neighbour in a row). */
 int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
-                          const int32_t *adj_hash, int64_t n_rows, int64_t n_edges,
-                          uint32_t *edge_cn, void *stream);
+                          const int32_t *adj_hash, const int32_t *adj_hpos,
+                          const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                          int64_t n_rows, int64_t n_edges, uint32_t *edge_cn, void *stream);
 
 /* Neighbour bitmaps of hub rows for dw_walk_replay_indexed (hub_idx / hub_bits; NULL = none):
  * bits[k * hub_words + (x >> 5)] bit (x & 31) = x in N(hub_rows[k]); hub_words >=
@@ -378,7 +381,9 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
  * it instead of building its own): the centres sorted by node (stable). touched (optional,
  * uint32[n_walks*(L-2R)]) receives the batch's distinct centre nodes in increasing order and
  * *n_touched (device int64) their count — the rows a step reads and updates in the in table
- * (OwnerLazyTables). Same workspace as the pass-1 / pass-2 calls that follow. */
+ * (OwnerLazyTables). Same workspace as the pass-1 / pass-2 calls that follow.
+ * dw_sgns_owner_pass1's order_ready is a bit set: 1 = this order is ready; 2 = the records
+ * were presorted (dw_sgns_owner_presort, one owner). */
 int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           int64_t local_rows, uint32_t *touched, int64_t *n_touched,
@@ -405,17 +410,14 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
  * the rows the dense update holds. claim int32 [local_rows] (zero-initialised, never reset): a
  * row is listed once per step, claimed via atomicMax(claim[row], step); rows_buf uint32
  * [min(local_rows, B' * 2R(1+K))] and n_rows (int64, device) receive the list, which
- * dw_adam_rows then replays. 2R(1+K) <= 64, dim <= 512. p_only != 0: where a row's replayed
- * steps all have weight_decay 0, only its p is written (m, v and last_step stay behind; the
- * same batch's dw_sgns_owner_pass2_lazy with p_current != 0 replays them) — a third of the
- * catch-up's writes. */
+ * dw_adam_rows then replays. 2R(1+K) <= 64, dim <= 512. */
 int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                                int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
                                int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
-                               int64_t *n_rows, const float *hist, int32_t step, int32_t p_only,
+                               int64_t *n_rows, const float *hist, int32_t step,
                                int32_t *status, void *stream);
 
 /* dw_sgns_owner_pass2 with the out slice's Adam kept LAZY and exact (OwnerLazyTables, small
@@ -423,15 +425,26 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * replayed (scalars hist[t], fp32 [steps][8] as for dw_adam_rows) right before its next update,
  * through the same adam_elem, so the slice equals the dense update bit for bit once flushed
  * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
- * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
- * p_current != 0: the batch's rows went through dw_sgns_owner_out_catch_up with p_only (their
- * p current to step - 1, m and v still at last_step), so only m, v are replayed here. */
+ * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t p_current, int32_t *status, void *workspace,
+                             int32_t step, int32_t presorted, int32_t *status, void *workspace,
                              size_t workspace_bytes, int64_t *n_records, void *stream);
+
+/* One owner, before dw_sgns_owner_pass1 of the same batch (pass 1's order_ready | 2, pass 2's
+ * presorted = 1, n_records NULL): the records' order — every slot's row (contexts from the
+ * walks, negatives as pass 1 draws them) sorted with its walk-slot position b * 2R(1+K) + t —
+ * so pass 1 writes only the values, in that position, and pass 2 gathers without a sort. It
+ * depends only on the walks and the negatives' stream, so it can run on a side stream beside
+ * dw_sgns_owner_out_catch_up (the reference's 64-walk batch: the ~10 launches of a small sort
+ * off the step's critical path). The same workspace as the passes. 2R(1+K) <= 64. */
+int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                          int32_t *status, void *workspace, size_t workspace_bytes,
+                          void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */

@@ -245,11 +245,11 @@ def _owner_run(rank, world, port, q):
             snaps.append(_owner_snapshot(t, V2))
         _native.check_status(status, 'owner_step')
         q.put((rank, t.w_in.cpu().numpy().copy(), t.full_w_out().cpu().numpy(),
-               acc.cpu().numpy(), snaps))
+               acc.cpu().numpy(), None, snaps))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # report, the parent asserts
-        q.put((rank, None, None, None, repr(e)))
+        q.put((rank, None, None, None, repr(e), None))
 
 
 def _free_port():
@@ -284,7 +284,7 @@ def test_owner_tables_two_ranks_equal_single_process(hip_device):
         p.join(timeout=60)
     errs = [r[4] for r in res if r[4]]
     assert not errs, errs
-    (_, i0, o0, a0, s0), (_, i1, o1, a1, s1) = res
+    (_, i0, o0, a0, _, s0), (_, i1, o1, a1, _, s1) = res
     np.testing.assert_array_equal(i0, i1)
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_allclose(a0 + a1, acc_ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
@@ -411,11 +411,11 @@ def _lazy_run(rank, world, port, q):
         snaps = []
         t, acc = _lazy_vs_dense('cuda:0', _walks_all(), V2, D2, R2, K2, LR2, snaps=snaps)
         q.put((rank, t.w_in.cpu().numpy().copy(), t.full_w_out().cpu().numpy(),
-               acc.cpu().numpy(), snaps))
+               acc.cpu().numpy(), None, snaps))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # report, the parent asserts
-        q.put((rank, None, None, None, repr(e)))
+        q.put((rank, None, None, None, repr(e), None))
 
 
 @pytest.mark.timeout(600)
@@ -441,7 +441,7 @@ def test_owner_lazy_two_ranks_equal_single_process(hip_device):
         p.join(timeout=60)
     errs = [r[4] for r in res if r[4]]
     assert not errs, errs
-    (_, i0, o0, a0, s0), (_, i1, o1, a1, s1) = res
+    (_, i0, o0, a0, _, s0), (_, i1, o1, a1, _, s1) = res
     np.testing.assert_array_equal(i0, i1)
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_allclose(a0 + a1, acc_ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
@@ -543,3 +543,26 @@ def test_owner_prepare_touched_rows(hip_device, n_walks):
     # (a hub's run of centres spans several waves: its row's atomics may add in either order)
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
+
+
+def test_presorted_records_equal_pass2_sort(hip_device, monkeypatch):
+    """One rank, lazy out slice: the records sorted before pass 1 (dw_sgns_owner_presort on the
+    side stream; pass 1 writes values in walk-slot order, pass 2 gathers without a sort) train
+    what pass 2's own sort trains — up to the order of a row's records in its sum (walk order vs
+    the centres' node order) — and the same Adam steps (every row's last step equal)."""
+    V, d, R, K, L, n, steps, lr = 5000, 128, 2, 3, 12, 16, 4, 0.01
+    walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(9),
+                          dtype=torch.int32)
+    runs = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('DW_PRESORT', flag)
+        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True)
+        assert t.presort == (flag == '1')
+        runs.append((t.last_out.clone(), t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(),
+                     acc.cpu().numpy()))
+    (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
+    assert torch.equal(l0, l1)                 # the same rows stepped, at the same steps
+    np.testing.assert_allclose(a1, a0, rtol=1e-6)
+    for got, exp in ((i1, i0), (o1, o0)):
+        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
+        assert_no_row_drift(got, exp)

@@ -198,10 +198,13 @@ def test_phase2_pieces_equal_phase2(hip_device, n_pieces, extra):
                        piece_rows=rows, on_piece=on_piece)
     torch.cuda.synchronize()
     assert seen == list(range(n_pieces))
+    # (float-atomic order at the hub row's chunk boundaries: thousands of terms summed in a
+    # run-dependent order, so the bar scales with the largest entry; 1e-7 of it failed 1 entry
+    # in 384,000 at 1.4x the bar on one run)
     np.testing.assert_allclose(g_in.cpu().numpy(), ref_in.cpu().numpy(), rtol=1e-5,
-                               atol=1e-7 * float(ref_in.abs().max()))
+                               atol=1e-6 * float(ref_in.abs().max()))
     np.testing.assert_allclose(g_out.cpu().numpy(), ref_out.cpu().numpy(), rtol=1e-5,
-                               atol=1e-7 * float(ref_out.abs().max()))
+                               atol=1e-6 * float(ref_out.abs().max()))
 
 
 @pytest.mark.parametrize('max_blocks', [0, 32, 47])

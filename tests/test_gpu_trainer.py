@@ -277,9 +277,10 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
             'datamodule.additional_parameters.rng=philox', 'train.noise=device',
             'model.embedding_size=128', f'train.optimizer.lr={lr}', 'train.max_epochs=2']
     runs = []
-    for mode in ('0', '1'):
+    for mode, scatter in (('0', 'auto'), ('1', 'records'), ('1', 'auto')):
         monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
-        out = str(tmp_path / f'runs{mode}')
+        monkeypatch.setenv('DW_TRAIN_GRAPH_SCATTER', scatter)
+        out = str(tmp_path / f'runs{mode}{scatter}')
         torch.manual_seed(0)
         last = train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
                                 f'output_dir={out}', f'train.experiment=g{mode}'] + base)
@@ -287,12 +288,19 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
         state = torch.load(ck, weights_only=True)
         runs.append((last, state))
     # 4,096 walks / 64 = 64 batches per epoch: 1 eager + 3 graphs of 16 + 15 eager, two epochs
-    assert replays == [16] * 6
-    (l0, s0), (l1, s1) = runs
-    assert s0['global_step'] == s1['global_step'] == 128
+    assert replays == [16] * 12
+    (l0, s0), (l1, s1), (l2, s2) = runs
+    assert s0['global_step'] == s1['global_step'] == s2['global_step'] == 128
+    # graphs of the eager loop's own records step: the same training
     for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
-        np.testing.assert_allclose(l1[k], l0[k], rtol=1e-4)
+        np.testing.assert_allclose(l1[k], l0[k], rtol=1e-5)
     for name in s0['state_dict']:
         a, b = s1['state_dict'][name].numpy(), s0['state_dict'][name].numpy()
         assert_params_close(a, b, lr, max_frac=1e-3, max_abs=lr)
         assert_no_row_drift(a, b)
+    # the default graphs (atomic output-table scatter at this size; that kernel is checked
+    # against the records path in test_gpu_graphed.py): the same steps, walks and negatives, the
+    # tables apart by summation order amplified through Adam (g ~ 0 entries), so the epoch losses
+    # agree to the order of that noise only
+    for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
+        np.testing.assert_allclose(l2[k], l0[k], rtol=1e-2)
