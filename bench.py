@@ -776,6 +776,15 @@ def main():
                 st = (torch.arange(n_r, dtype=torch.int32) % N) + 1   # node ids 1..N, cycled
                 st_dev = st.to(dev)
                 out = torch.empty((n_r, L), dtype=torch.int32, device=dev)
+                build_ms = None
+                if meth == 'node2vec':   # the per-edge class counts, built once per graph (timed)
+                    csr.device_tensors(dev, need_sorted=True, need_adj_pos=True,
+                                       need_hub_bits=True)
+                    torch.cuda.synchronize(dev)
+                    a = time.perf_counter()
+                    csr.device_tensors(dev, need_edge_cn=True)
+                    torch.cuda.synchronize(dev)
+                    build_ms = (time.perf_counter() - a) * 1e3
                 _random.seed(0)
                 w.walk_batch(st_dev[:64])                              # warm-up (jump tables)
                 w.walk_batch(st_dev, out=out)
@@ -807,6 +816,8 @@ def main():
                                       'kernel_ms': kern_s * 1e3, 'uniforms_ms': gen_s * 1e3,
                                       'uniforms_GBps': u_dev.numel() * 8 / gen_s / 1e9,
                                       'walks_per_s_host_uniforms': n_r / dt_host}
+                if build_ms is not None:
+                    replay_stats[meth]['edge_counts_build_ms'] = build_ms
                 if meth == 'node2vec':
                     # the bit-exact walker's realised traffic (dw_walk_replay_indexed counted:
                     # row pairs, uniform, pick, output per step; every list entry read; every

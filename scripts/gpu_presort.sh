@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_owner.py tests/test_gpu_graphed.py tests/test_gpu_c3_step.py tests/test_gpu_trainer.py tests/test_gpu_sgns.py -q -p no:cacheprovider -rf --timeout 600 > gpurun_out/presort_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_walks.py tests/test_gpu_owner.py tests/test_gpu_graphed.py tests/test_gpu_c3_step.py tests/test_gpu_trainer.py tests/test_gpu_sgns.py -q -p no:cacheprovider -rf --timeout 600 > gpurun_out/presort_tests.log 2>&1; rc=$?
 tail -6 gpurun_out/presort_tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 for ps in 1 0; do
