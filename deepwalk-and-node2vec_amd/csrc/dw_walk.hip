@@ -70,6 +70,12 @@ constexpr int REPLAY_CH_EXACT = DW_REPLAY_CH_EXACT;
 #define DW_REPLAY_NCAP_EXACT 1024
 #endif
 constexpr int REPLAY_NCAP_EXACT = DW_REPLAY_NCAP_EXACT;
+// with the per-edge class counts no class masks are kept (k_walk_replay COUNTS): the weight
+// cache of the serial fallback shrinks to 64 doubles, 4.6 KiB of LDS per wave
+#ifndef DW_REPLAY_CH_CN
+#define DW_REPLAY_CH_CN 64
+#endif
+constexpr int REPLAY_CH_CN = DW_REPLAY_CH_CN;
 
 struct ReplayCtx {
     const int64_t *row_ptr;
@@ -888,11 +894,17 @@ __device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
     return k;
 }
 
-template <int CH, int NCAP>
-__global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
-    k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
-                  int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
-                  int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
+// COUNTS: the launch has the per-edge class counts (ix.edge_cn): every step after the first
+// takes n2v_pick_counted, so the full classification (node2vec_pick_exact) and its class-mask
+// cache are not compiled in; CH then only sizes the serial fallback's weight cache (hub rows
+// past it recompute their weights in lane 0) and, with the N(prev) stage, the positions buffer.
+template <int CH, int NCAP, bool COUNTS>
+__device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
+                                                 const int32_t *__restrict__ starts,
+                                                 int64_t n_walks, int32_t L,
+                                                 const double *__restrict__ uniforms,
+                                                 int32_t *__restrict__ out, int32_t *status,
+                                                 int fast, N2VIndex ix) {
     // per wave: CH doubles (the serial replay's weights / the exact picks' ballots) followed by
     // the NCAP-entry N(prev) stage; the ballots take both halves when nothing is staged
     __shared__ uint64_t s_lds[REPLAY_WAVES][CH + NCAP / 2];
@@ -936,7 +948,8 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             }
             if (counted && lane == 0) ++steps;
             // N(prev) much the shorter list: its members' positions in N(v) (v's hash)
-            if (fast && ix.adj_off && c.node2vec && prev >= 0 && pn <= 2 * CH &&
+            // (positions: the wave's buffer and N(prev) stage, contiguous: 2 CH + NCAP entries)
+            if (fast && ix.adj_off && c.node2vec && prev >= 0 && pn <= 2 * CH + NCAP &&
                 pn * (int64_t)ix.b_factor < n) {
                 const int64_t h = ix.adj_off[v];
                 const AdjRow rv{a, n, h, static_cast<uint32_t>((ix.adj_off[v + 1] - h) >> 4)};
@@ -965,7 +978,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                 if (hb >= 0) np_bits = ix.hub_bits + hb * ix.hub_words;
             }
             // the class counts of prev -> v known: only the rounds up to the crossing classified
-            const bool known = fast && c.node2vec && prev >= 0 && ix.edge_cn && e_in >= 0;
+            const bool known = COUNTS && fast && c.node2vec && prev >= 0 && e_in >= 0;
             if (c.node2vec && prev >= 0) {
                 if (counted && lane == 0 && !known)   // N(v) read; N(prev) staged, bit-tested
                     loads += static_cast<uint32_t>(   // or searched
@@ -1001,6 +1014,8 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                                                            : ne * static_cast<int64_t>(
                                                                       ceil_log2(pn + 1))));
                     }
+                } else if constexpr (COUNTS) {
+                    fp = (!c.node2vec || prev < 0) ? uniform_pick_exact(uu, n) : -1;
                 } else {
                     fp = (!c.node2vec || prev < 0)
                              ? uniform_pick_exact(uu, n)
@@ -1098,6 +1113,30 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
             atomicAdd(ix.counters + 3, v4[2]);
         }
     }
+}
+
+template <int CH, int NCAP>
+__global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
+    k_walk_replay(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
+                  int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
+                  int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
+    walk_replay_body<CH, NCAP, false>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
+                                      ix);
+}
+
+// The COUNTS form is latency-bound on each walker's dependent chain and its LDS (4.6 KiB per
+// wave) allows 34 walkers per CU, so its registers are bounded for more waves per SIMD
+#ifndef DW_N2V_CN_WAVES
+#define DW_N2V_CN_WAVES 5
+#endif
+template <int CH, int NCAP>
+__global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
+    __attribute__((amdgpu_waves_per_eu(DW_N2V_CN_WAVES, 8)))
+    k_walk_replay_cn(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
+                     int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
+                     int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
+    walk_replay_body<CH, NCAP, true>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
+                                     ix);
 }
 
 // =============================================================================================
@@ -1720,9 +1759,16 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
                       reinterpret_cast<unsigned long long *>(counters), hub_idx, hub_bits,
                       hub_words, edge_cn};
-    hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>), dim3((unsigned)blocks),
-                       dim3(REPLAY_WAVES * WAVE), 0, dw::as_stream(stream), c, n_rows, starts,
-                       n_walks, walk_length, uniforms, out, status, 1, ix);
+    if (edge_cn)
+        hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>),
+                           dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
+                           dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,
+                           uniforms, out, status, 1, ix);
+    else
+        hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>),
+                           dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
+                           dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,
+                           uniforms, out, status, 1, ix);
     DW_LAUNCH_CHECK("dw_walk_replay_indexed");
     return DW_OK;
 }
