@@ -752,7 +752,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
 // records of whole rows, so a piece's rows never continue in another piece's chunks.
-template <int VPL, bool MASKED, bool ADAM>
+template <int VPL, bool MASKED, bool ADAM, bool IDX = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
@@ -820,9 +820,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 #pragma unroll
             for (int u = 0; u < GU; ++u) {
                 const bool in = e + u < e1;
-                const uint64_t v = in ? vals[(ADAM && oa.idx) ? static_cast<int64_t>(oa.idx[e + u])
-                                                              : e + u]
-                                      : 0ull;
+                const uint64_t v =
+                    in ? vals[IDX ? static_cast<int64_t>(oa.idx[e + u]) : e + u] : 0ull;
                 k[u] = in ? keys[e + u] : last;
                 coef[u] = in ? __uint_as_float(static_cast<uint32_t>(v >> 32)) : 0.f;
                 const float *src = w_in + static_cast<int64_t>(static_cast<uint32_t>(v)) * d + lane;
@@ -1119,7 +1118,14 @@ void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const 
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
                    const OutAdam *oa, const int64_t *range, int32_t gch) {
     const bool exact = d == 64 * VPL;
-    if (oa) {
+    if (oa && oa->idx) {   // presorted records (the lazy one-owner step)
+        if (exact)
+            hipLaunchKernelGGL((k_rec_gather<VPL, false, true, true>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, *oa, range, gch);
+        else
+            hipLaunchKernelGGL((k_rec_gather<VPL, true, true, true>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, *oa, range, gch);
+    } else if (oa) {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
                                w_in, g_out, d, *oa, range, gch);
