@@ -421,23 +421,6 @@ def test_indexed_node2vec_replay_equals_csr_replay_c3(p, q, hip_device):
     assert c['bytes'] >= c['steps'] * 48 + c['probes'] * 64
 
 
-def _edge_counts_host(row_ptr, col):
-    """edge_cn restated on the host: bit 31 = [t in N(v)], low bits = #{x in N(v): x != t,
-    x in N(t)} for every directed edge t -> v (the classes random_walk_generator.py:100-108
-    counts at a step t -> v)."""
-    n = len(row_ptr) - 1
-    sets = [set(col[row_ptr[i]:row_ptr[i + 1]].tolist()) for i in range(n)]
-    out = np.empty(len(col), dtype=np.uint32)
-    for t in range(n):
-        for e in range(row_ptr[t], row_ptr[t + 1]):
-            v = int(col[e])
-            nv = col[row_ptr[v]:row_ptr[v + 1]]
-            a = int((nv == t).sum())
-            c = len((sets[v] & sets[t]) - {t})
-            out[e] = (a << 31) | c
-    return out
-
-
 def _self_loop_graph():
     # rows with self-loops (t in N(t), v in N(v)), a hub past the hash threshold and short rows
     import networkx as nx
@@ -450,8 +433,9 @@ def _self_loop_graph():
 
 @pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops'])
 def test_edge_common_counts_vs_host(which, hip_device):
-    """dw_edge_common_counts (the node2vec replay's per-edge class counts, counted over the
-    shorter list against the other's hash) equals the host restatement on every directed edge,
+    """dw_edge_common_counts (the node2vec replay's per-edge class counts: one intersection per
+    undirected edge over the shorter list, hub bitmaps or hashes) equals the oracle's
+    restatement of the reference rule (walk_ref.edge_class_counts) on every directed edge,
     including self-loops and hub-to-hub edges."""
     if which == 'karate':
         csr = _csr(golden('walks_karate_node2vec_p1_q0.5.npz'))
@@ -461,7 +445,7 @@ def test_edge_common_counts_vs_host(which, hip_device):
         csr = _self_loop_graph()
     d = csr.device_tensors(hip_device, need_edge_cn=True)
     got = d['edge_cn'][:csr.nnz].cpu().numpy().view(np.uint32)
-    ref = _edge_counts_host(np.asarray(csr.row_ptr), np.asarray(csr.host_col()))
+    ref = walk_ref.edge_class_counts(walk_ref.CSR(csr.row_ptr, csr.host_col(), None))
     np.testing.assert_array_equal(got, ref)
 
 

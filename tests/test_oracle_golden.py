@@ -273,3 +273,22 @@ def test_listscan_node2vec_equals_reference_walks():
         w = walk_ref.node2vec_walk(g, int(f['starts'][k]), L, float(f['p']), float(f['q']),
                                    f['uniforms'][k].tolist(), listscan=True)
         np.testing.assert_array_equal(w, f['walks'][k])
+
+
+@pytest.mark.parametrize('name', ['walks_karate_node2vec_p1_q0.5.npz',
+                                  'walks_rmat12_node2vec_p0.25_q4.npz'])
+def test_edge_class_counts_follow_the_reference_weight_rule(name):
+    """oracle.walk_ref.edge_class_counts (what dw_edge_common_counts computes on the device)
+    equals, for every directed edge t -> v, the number of neighbours of v the reference's rule
+    (random_walk_generator.py:102-108, restated in walk_ref.node2vec_weights) weights 1/p and
+    1/q at a step with prev = t — read off the weights at p = 1/2, q = 1/4 (factors 2 and 4)."""
+    f = golden(name)
+    g = walk_ref.CSR(f['row_ptr'], f['col'], None)   # unweighted: the factors read off as is
+    cn = walk_ref.edge_class_counts(g)
+    n = len(g.row_ptr) - 1
+    for t in range(n):
+        for e in range(g.row_ptr[t], g.row_ptr[t + 1]):
+            _, w = walk_ref.node2vec_weights(g, t, g.col[e], 0.5, 0.25)
+            assert int(cn[e]) >> 31 == sum(1 for x in w if x == 2.0)
+            assert int(cn[e]) & 0x7FFFFFFF == sum(1 for x in w if x == 4.0)
+    assert (cn >> 31 == 1).all()          # undirected: t is always a neighbour of v
