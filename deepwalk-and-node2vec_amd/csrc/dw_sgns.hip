@@ -2054,8 +2054,15 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
-                        n_max, nullptr, hist, step - 1, stream);
+    static const bool per_row_blocks = [] {   // DW_CATCHUP_BLOCKS=1: k_rows_adam (A/B only)
+        const char *e = getenv("DW_CATCHUP_BLOCKS");
+        return e && e[0] == '1';
+    }();
+    if (per_row_blocks)
+        return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
+                            n_rows, n_max, nullptr, hist, step - 1, stream);
+    return dw::rows_replay_wave(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
+                                n_rows, n_max, hist, step - 1, stream);
 }
 
 int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
