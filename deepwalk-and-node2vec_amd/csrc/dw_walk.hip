@@ -978,7 +978,8 @@ __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
                 if (hb >= 0) np_bits = ix.hub_bits + hb * ix.hub_words;
             }
             // the class counts of prev -> v known: only the rounds up to the crossing classified
-            const bool known = COUNTS && fast && c.node2vec && prev >= 0 && e_in >= 0;
+            const bool known =
+                (COUNTS || ix.edge_cn != nullptr) && fast && c.node2vec && prev >= 0 && e_in >= 0;
             if (c.node2vec && prev >= 0) {
                 if (counted && lane == 0 && !known)   // N(v) read; N(prev) staged, bit-tested
                     loads += static_cast<uint32_t>(   // or searched
@@ -1759,7 +1760,12 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
                       reinterpret_cast<unsigned long long *>(counters), hub_idx, hub_bits,
                       hub_words, edge_cn};
-    if (edge_cn)
+    // DW_N2V_CN_KERNEL=0: the counts through the general kernel (round 3's first form; A/B)
+    static const bool cn_kernel = [] {
+        const char *e = getenv("DW_N2V_CN_KERNEL");
+        return !(e && e[0] == '0');
+    }();
+    if (edge_cn && cn_kernel)
         hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
                            dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,

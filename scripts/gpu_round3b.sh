@@ -6,8 +6,8 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash scripts/gpu_presort.sh || exit 1
-for v in default; do
-  if [ "$v" = default ]; then unset DW_LIB_PATH; else export DW_LIB_PATH=$PWD/$v; fi
+for v in default cn0; do
+  if [ "$v" = cn0 ]; then export DW_N2V_CN_KERNEL=0; else unset DW_N2V_CN_KERNEL; fi
   timeout -k 10 300 python -u scripts/microbench/replay_rates.py --dw-walks 0 > gpurun_out/rates_$(basename $v).log 2>&1 || { tail -5 gpurun_out/rates_$(basename $v).log; exit 1; }
   echo "$v"; python3 -c "import json; d=json.loads(open('gpurun_out/rates_$(basename $v).log').read().strip().splitlines()[-1]); print({k:(round(x['kernel_ms'],2) if isinstance(x,dict) and 'kernel_ms' in x else x) for k,x in d.items()})"
 done
