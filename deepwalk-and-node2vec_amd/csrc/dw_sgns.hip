@@ -149,7 +149,8 @@ struct SgnsArgs {
     uint32_t *rec_counts;
     uint32_t *count_out;      //   n_owners == 1: the records are dense; their count goes here
     int64_t region;
-    bool walk_order = false;  //   one owner, presorted: values at b * T + t, keys not written
+    bool walk_order = false;  //   one owner, presorted: values at rec_inv[b * T + t] (their
+    const uint32_t *rec_inv = nullptr;   //   sorted position), keys not written
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
@@ -611,9 +612,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 const int tt = gl + 16 * k;
                 if (tt < n_own) {
                     const int32_t id = s_id[wv][q][tt];   // < 0: a bad id (one owner only)
-                    if (!a.walk_order) a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
-                    a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
+                    const uint64_t val = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
                                                      ok_c ? cid : 0);
+                    if (a.walk_order) {   // presorted: straight to the record's sorted place
+                        a.rec_val[a.rec_inv[at + tt]] = val;
+                    } else {
+                        a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                        a.rec_val[at + tt] = val;
+                    }
                 }
             }
             filled += c0 + c1 + c2 + c3;
@@ -701,9 +707,6 @@ struct OutAdam {
     int32_t step = 0;
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
     int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
-    // presorted records (dw_sgns_owner_presort): the sorted keys carry the index of their value
-    // in pass 1's walk-slot-ordered array; the gather reads vals[idx[e]]
-    const uint32_t *idx = nullptr;
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -752,7 +755,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
 // records of whole rows, so a piece's rows never continue in another piece's chunks.
-template <int VPL, bool MASKED, bool ADAM, bool IDX = false>
+template <int VPL, bool MASKED, bool ADAM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
@@ -820,8 +823,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 #pragma unroll
             for (int u = 0; u < GU; ++u) {
                 const bool in = e + u < e1;
-                const uint64_t v =
-                    in ? vals[IDX ? static_cast<int64_t>(oa.idx[e + u]) : e + u] : 0ull;
+                const uint64_t v = in ? vals[e + u] : 0ull;
                 k[u] = in ? keys[e + u] : last;
                 coef[u] = in ? __uint_as_float(static_cast<uint32_t>(v >> 32)) : 0.f;
                 const float *src = w_in + static_cast<int64_t>(static_cast<uint32_t>(v)) * d + lane;
@@ -908,12 +910,40 @@ hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
     return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
 }
 
+// The same stable sort with separate output arrays (the result lands in k_out / v_out whatever
+// the pass count; the alternate buffers live in tmp). With tmp == nullptr: *bytes.
+hipError_t sort_pairs_to(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out,
+                         const uint32_t *v_in, uint32_t *v_out, uint32_t n, int end_bit,
+                         hipStream_t st) {
+    if (tmp == nullptr) {
+        size_t a = 0, b = 0;
+        hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, k_in, k_out, v_in,
+                                                                   v_out, n, 0, end_bit, st);
+        if (e == hipSuccess)
+            e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, k_in, k_out, v_in, v_out, n,
+                                                           0, end_bit, st);
+        bytes = a > b ? a : b;
+        return e;
+    }
+    if (n < SMALL_SORT_MAX)
+        return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n,
+                                                          0, end_bit, st);
+    return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n, 0,
+                                                       end_bit, st);
+}
+
 int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStream_t st) {
     size_t cub_bytes = 0;
     rocprim::double_buffer<uint32_t> kb(nullptr, nullptr);
     rocprim::double_buffer<uint64_t> vb(nullptr, nullptr);
     hipError_t e = sort_pairs(nullptr, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
                               end_bit_for(V), st);
+    if (e == hipSuccess) {   // dw_sgns_owner_presort's sort (separate outputs) shares the space
+        size_t pb = 0;
+        e = sort_pairs_to(nullptr, pb, nullptr, nullptr, nullptr, nullptr,
+                          static_cast<uint32_t>(n_rec), end_bit_for(V), st);
+        if (pb > cub_bytes) cub_bytes = pb;
+    }
     if (e != hipSuccess) {
         dw::set_error("dw_sgns: sort size query failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
@@ -1118,14 +1148,7 @@ void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const 
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
                    const OutAdam *oa, const int64_t *range, int32_t gch) {
     const bool exact = d == 64 * VPL;
-    if (oa && oa->idx) {   // presorted records (the lazy one-owner step)
-        if (exact)
-            hipLaunchKernelGGL((k_rec_gather<VPL, false, true, true>), g, bl, 0, st, keys, vals,
-                               n_rec, w_in, g_out, d, *oa, range, gch);
-        else
-            hipLaunchKernelGGL((k_rec_gather<VPL, true, true, true>), g, bl, 0, st, keys, vals,
-                               n_rec, w_in, g_out, d, *oa, range, gch);
-    } else if (oa) {
+    if (oa) {
         if (exact)
             hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
                                w_in, g_out, d, *oa, range, gch);
@@ -1688,6 +1711,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     const bool presorted = (order_ready & 2) != 0;   // dw_sgns_owner_presort ran: values only
     DW_REQUIRE(!presorted || dense, "dw_sgns_owner_pass1: presorted records need one owner");
     a.walk_order = presorted;
+    a.rec_inv = reinterpret_cast<const uint32_t *>(ws.v0) + a.batch * T;   // presort's inverse
     a.rec_key = dense ? ws.k1 : ws.k0;
     a.rec_val = dense ? ws.v1 : ws.v0;
     a.count_out = dense ? ws.count : nullptr;
@@ -1732,10 +1756,8 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     const int64_t bound = n_centres * T;
     if (presorted) {   // dw_sgns_owner_presort's order + pass 1's walk-order values: no sort here
         DW_REQUIRE(oa && !n_records, "dw_sgns_owner_pass2_lazy: presorted needs n_records NULL");
-        OutAdam o = *oa;
-        o.idx = reinterpret_cast<const uint32_t *>(ws.v0);
         g_timer.mark(2, st);
-        if (bound > 0) rc = launch_pass2(ws.k0, ws.v1, bound, w_in, g_out, d, &o, local_rows, st);
+        if (bound > 0) rc = launch_pass2(ws.k0, ws.v1, bound, w_in, g_out, d, oa, local_rows, st);
         g_timer.mark(3, st);
         return rc;
     }
@@ -2003,6 +2025,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     }
 }
 
+// inv[pos[i]] = i: each walk-slot position's place in the sorted order (pass 1 writes there)
+__global__ void __launch_bounds__(256)
+    k_presort_inverse(const uint32_t *__restrict__ pos, int64_t n, uint32_t *__restrict__ inv) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        inv[pos[i]] = static_cast<uint32_t>(i);
+}
+
 }  // namespace
 
 extern "C" {
@@ -2054,15 +2084,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    static const bool per_row_blocks = [] {   // DW_CATCHUP_BLOCKS=1: k_rows_adam (A/B only)
-        const char *e = getenv("DW_CATCHUP_BLOCKS");
-        return e && e[0] == '1';
-    }();
-    if (per_row_blocks)
-        return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
-                            n_rows, n_max, nullptr, hist, step - 1, stream);
-    return dw::rows_replay_wave(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
-                                n_rows, n_max, hist, step - 1, stream);
+    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
+                        n_max, nullptr, hist, step - 1, stream);
 }
 
 int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
@@ -2093,35 +2116,34 @@ int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_le
     if (rc != DW_OK) return rc;
     const int64_t n = a.batch * T;
     DW_REQUIRE(n < (int64_t(1) << 32), "dw_sgns_owner_presort: too many records");
-    uint32_t *p0 = reinterpret_cast<uint32_t *>(ws.v0), *p1 = p0 + n;   // v0 holds 2n u32
+    // keys (k1) and walk-slot positions (the second half of v0) in, the sorted keys to k0 and the
+    // sorted positions to the first half of v0 (fixed places: a sort with separate outputs), then
+    // the inverse over the input positions: pass 1 writes each value to v1 at its sorted place
+    uint32_t *p_sorted = reinterpret_cast<uint32_t *>(ws.v0), *p_in = p_sorted + n;
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_presort_keys, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, ws.k0, p0);
+                       a, ws.k1, p_in);
     DW_LAUNCH_CHECK("dw_sgns_owner_presort/keys");
-    rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1), pb(p0, p1);
     size_t need = 0;
-    if (sort_pairs(nullptr, need, kb, pb, static_cast<uint32_t>(n), end_bit_for(vocab_size),
-                   st) != hipSuccess ||
+    if (sort_pairs_to(nullptr, need, ws.k1, ws.k0, p_in, p_sorted, static_cast<uint32_t>(n),
+                      end_bit_for(vocab_size), st) != hipSuccess ||
         need > ws.cub_bytes) {
         dw::set_error("dw_sgns_owner_presort: sort workspace too small");
         return DW_E_HIP;
     }
     size_t cb = ws.cub_bytes;
-    hipError_t e = sort_pairs(ws.cub, cb, kb, pb, static_cast<uint32_t>(n),
-                              end_bit_for(vocab_size), st);
+    hipError_t e = sort_pairs_to(ws.cub, cb, ws.k1, ws.k0, p_in, p_sorted,
+                                 static_cast<uint32_t>(n), end_bit_for(vocab_size), st);
     if (e != hipSuccess) {
         dw::set_error("dw_sgns_owner_presort: sort failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
     }
-    // the order where pass 2 reads it (k0, and the first half of v0); pass 1 writes only v1
-    if (kb.current() != ws.k0 &&
-        (hipMemcpyAsync(ws.k0, kb.current(), n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-         hipMemcpyAsync(p0, pb.current(), n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)) {
-        dw::set_error("dw_sgns_owner_presort: copy failed");
-        return DW_E_HIP;
-    }
+    int64_t ib = (n + 255) / 256;
+    if (ib > grid_cap(4)) ib = grid_cap(4);
+    hipLaunchKernelGGL(k_presort_inverse, dim3((unsigned)ib), dim3(256), 0, st, p_sorted, n, p_in);
+    DW_LAUNCH_CHECK("dw_sgns_owner_presort/inverse");
     return DW_OK;
 }
 

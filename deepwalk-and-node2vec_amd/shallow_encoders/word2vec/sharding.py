@@ -933,13 +933,13 @@ class OwnerLazyTables(OwnerTables):
             fork.record(main)
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
-                if self.presort:
-                    from shallow_encoders.word2vec.sgns import sgns_owner_presort
+                self.prepare(walks, context_radius, neg_samples)
+                self.catch_up()
+                if self.presort:   # (after the short in-table work: the side chain stays the
+                    from shallow_encoders.word2vec.sgns import sgns_owner_presort   # shorter)
                     sgns_owner_presort(walks, context_radius, neg_samples, self.V, self.S,
                                        seed=seed, noise_offset=noise_offset, status=status)
                     self._presorted = True
-                self.prepare(walks, context_radius, neg_samples)
-                self.catch_up()
                 join = torch.cuda.Event()
                 join.record(self._side)
             self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)

@@ -12,6 +12,4 @@ for ps in 1 0; do
   DW_PRESORT=$ps timeout -k 10 300 python bench.py --batch-walks 64 --steps 400 --no-cpu-baseline --no-walk-bench > gpurun_out/c3_64_presort$ps.log 2>&1 || { tail -5 gpurun_out/c3_64_presort$ps.log; exit 1; }
   grep '^{' gpurun_out/c3_64_presort$ps.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('presort $ps', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done
-DW_CATCHUP_BLOCKS=1 timeout -k 10 300 python bench.py --batch-walks 64 --steps 400 --no-cpu-baseline --no-walk-bench > gpurun_out/c3_64_catchup_blocks.log 2>&1 || { tail -5 gpurun_out/c3_64_catchup_blocks.log; exit 1; }
-grep '^{' gpurun_out/c3_64_catchup_blocks.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('catch-up blocks', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 bash scripts/gpu_trace_c3_64.sh
