@@ -890,6 +890,15 @@ using SmallSortConfig = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     128 * 1024>;
 constexpr uint32_t SMALL_SORT_MAX = 4u << 20;
+// dw_sgns_owner_presort's sort (the reference's 64-walk batch: 269K records, 21-bit rows), which
+// runs beside the memory-bound catch-up: 11-bit digits on 2K-item tiles, two passes (and two
+// lookback resets) instead of three.
+using PresortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>,
+                                        rocprim::kernel_config<256, 8>, 11,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 
 // Stable LSD sort of (key, value) pairs on bits [0, end_bit), the config chosen by size. With
 // tmp == nullptr: *bytes = the larger of both configs' needs for n (so any n' <= n fits).
@@ -920,14 +929,14 @@ hipError_t sort_pairs_to(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_
         hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, k_in, k_out, v_in,
                                                                    v_out, n, 0, end_bit, st);
         if (e == hipSuccess)
-            e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, k_in, k_out, v_in, v_out, n,
-                                                           0, end_bit, st);
+            e = rocprim::radix_sort_pairs<PresortConfig>(nullptr, b, k_in, k_out, v_in, v_out, n,
+                                                         0, end_bit, st);
         bytes = a > b ? a : b;
         return e;
     }
     if (n < SMALL_SORT_MAX)
-        return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n,
-                                                          0, end_bit, st);
+        return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n,
+                                                        0, end_bit, st);
     return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n, 0,
                                                        end_bit, st);
 }

@@ -763,6 +763,7 @@ class OwnerLazyTables(OwnerTables):
         self.presort = (self.lazy_out and not self.multi
                         and os.environ.get('DW_PRESORT', '1') != '0')
         self._presorted = False
+        self._side2 = None
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -928,22 +929,33 @@ class OwnerLazyTables(OwnerTables):
         stream waits for both."""
         self._presorted = False
         if self.lazy_out and not self.multi:
+            # three branches from one fork: the out rows' claim + catch-up (the longest; enqueued
+            # first, so a captured graph launches it first), the centre order + in-table catch-up,
+            # and the records' presort
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
+            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+            joins = []
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
                 self.prepare(walks, context_radius, neg_samples)
                 self.catch_up()
-                if self.presort:   # (after the short in-table work: the side chain stays the
-                    from shallow_encoders.word2vec.sgns import sgns_owner_presort   # shorter)
+                joins.append(torch.cuda.Event())
+                joins[-1].record(self._side)
+            if self.presort:
+                from shallow_encoders.word2vec.sgns import sgns_owner_presort
+                if self._side2 is None:
+                    self._side2 = torch.cuda.Stream(self.device)
+                with torch.cuda.stream(self._side2):
+                    self._side2.wait_event(fork)
                     sgns_owner_presort(walks, context_radius, neg_samples, self.V, self.S,
                                        seed=seed, noise_offset=noise_offset, status=status)
-                    self._presorted = True
-                join = torch.cuda.Event()
-                join.record(self._side)
-            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
-            main.wait_event(join)
+                    joins.append(torch.cuda.Event())
+                    joins[-1].record(self._side2)
+                self._presorted = True
+            for j in joins:
+                main.wait_event(j)
             return
         self.prepare(walks, context_radius, neg_samples)
         self.catch_up()
