@@ -758,10 +758,12 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = bool(lazy_out)
         super().__init__(*args, **kwargs)
         self.lazy_out = self.lazy_out and self._hip()
-        # one rank, lazy out slice: the records sorted before pass 1 on the side stream, beside
-        # the out rows' catch-up (dw_sgns_owner_presort); DW_PRESORT=0 sorts them in pass 2
+        # one rank, lazy out slice, DW_PRESORT=1: the records sorted before pass 1 on a side
+        # stream beside the out rows' catch-up (dw_sgns_owner_presort). Off by default: beside
+        # the catch-up's HBM traffic the sort's passes stretch 3-5x and the presort branch
+        # becomes the longest (C3 at 64 walks: 0.540 vs 0.500 ms per step)
         self.presort = (self.lazy_out and not self.multi
-                        and os.environ.get('DW_PRESORT', '1') != '0')
+                        and os.environ.get('DW_PRESORT', '0') == '1')
         self._presorted = False
         self._side2 = None
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
