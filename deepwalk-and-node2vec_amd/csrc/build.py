@@ -31,6 +31,18 @@ BASE_FLAGS = ['-x', 'hip', f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17
               '-Wall', '-Wno-unused-function', '-I', os.path.join(REPO, 'include')]
 
 
+def source_id() -> str:
+    """SHA-256 (first 16 hex digits) over every source and header the library is built from:
+    compiled into libdw_hip.so as dw_build_id(), so a shipped binary can be checked against the
+    tree it travels with (tests/test_host.py, __graft_entry__.smoke())."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in [os.path.join(HERE, n) for n in SOURCES] + HEADERS:
+        with open(path, 'rb') as f:
+            h.update(os.path.basename(path).encode() + b'\0' + f.read())
+    return h.hexdigest()[:16]
+
+
 def _stale(src, obj):
     if not os.path.exists(obj):
         return True
@@ -41,9 +53,16 @@ def _stale(src, obj):
 def _compile(name, force):
     src = os.path.join(HERE, name)
     obj = os.path.join(BUILD, os.path.splitext(name)[0] + '.o')
-    if not force and not _stale(src, obj):
+    stale = _stale(src, obj)
+    if name == 'dw_abi.cpp':   # carries the build id: stale when any source is newer
+        stale = stale or not os.path.exists(obj) or any(
+            os.path.getmtime(os.path.join(HERE, n)) > os.path.getmtime(obj) for n in SOURCES)
+    if not force and not stale:
         return obj, None
-    cmd = [HIPCC] + BASE_FLAGS + EXTRA.get(name, []) + ['-c', src, '-o', obj]
+    extra = list(EXTRA.get(name, []))
+    if name == 'dw_abi.cpp':   # the build id (sources hash): rebuilt whenever any source changes
+        extra += [f'-DDW_BUILD_ID="{source_id()}"']
+    cmd = [HIPCC] + BASE_FLAGS + extra + ['-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f'{" ".join(cmd)}\n{r.stdout}\n{r.stderr}'

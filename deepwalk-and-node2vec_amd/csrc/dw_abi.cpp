@@ -47,6 +47,11 @@ const char *dw_last_error_string(void) { return dw::g_err; }
 
 int dw_abi_version(void) { return 14; }
 
+#ifndef DW_BUILD_ID
+#define DW_BUILD_ID "unknown"
+#endif
+const char *dw_build_id(void) { return DW_BUILD_ID; }
+
 int dw_step_scalars_bind(const dw_step_scalars *dev) {
     dw::g_step = dev;
     dw::g_step_has_host = false;

@@ -48,6 +48,7 @@ _szp = ctypes.POINTER(ctypes.c_size_t)
 SIGNATURES = {
     'dw_last_error_string': (ctypes.c_char_p, []),
     'dw_abi_version': (ctypes.c_int, []),
+    'dw_build_id': (ctypes.c_char_p, []),
     'dw_device_sync': (ctypes.c_int, [_p]),
     'dw_stream_copy': (ctypes.c_int, [_p, _p, _i64, _p]),
     'dw_host_shuffle': (ctypes.c_int, [_p, _p, _i64]),

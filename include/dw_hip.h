@@ -58,6 +58,9 @@ extern "C" {
 /* ---- library ---------------------------------------------------------------------------- */
 const char *dw_last_error_string(void);
 int dw_abi_version(void);               /* bumps on any signature change */
+/* SHA-256 prefix (16 hex digits) of the sources the library was built from (csrc/build.py
+ * source_id): a shipped binary can be checked against the tree it came with. */
+const char *dw_build_id(void);
 int dw_device_sync(void *stream);       /* hipStreamSynchronize(stream); used by the host mirror */
 /* dst = src, bytes a multiple of 16 (16-B aligned device buffers): a STREAM-copy kernel, the
  * measured HBM roofline bench.py reports beside the spec peak. */

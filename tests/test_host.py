@@ -483,3 +483,16 @@ def test_mt_chained_generation_is_cpython_random(stride, seed, skip, n):
     np.testing.assert_array_equal(out, np.array([r.random() for _ in range(n)]))
     st = r.getstate()[1]
     assert list(arr) == list(st[:624]) and index == st[624]
+
+
+def test_library_built_from_these_sources():
+    """The shipped libdw_hip.so carries the hash of the sources it was built from
+    (csrc/build.py source_id, dw_build_id()): equal to this tree's, so the binary that travels
+    to the GPU box is not stale."""
+    import importlib.util
+    from shallow_encoders import _native
+    spec = importlib.util.spec_from_file_location(
+        'dw_build', os.path.join(os.path.dirname(_native.__file__), '..', 'csrc', 'build.py'))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert _native.load().dw_build_id().decode() == b.source_id()
