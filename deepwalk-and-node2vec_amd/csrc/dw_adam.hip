@@ -146,77 +146,6 @@ __global__ void __launch_bounds__(512)
     }
 }
 
-// The memory-bound form of k_rows_adam's g = 0 replay (no gradient step), for rows that are a
-// few steps behind (the lazy out slice's catch-up before pass 1: at C3's 64-walk batch ~240K rows
-// a step, each ~4 steps stale): one wave per row, VPL = d / 64 contiguous elements per lane
-// (16-B / 8-B vector loads), two rows per trip with all six arrays' loads in flight before the
-// replays, grid-stride — instead of one 2-wave block per row. The same adam_elem(_g0) sequence
-// per element, so the same bits.
-template <int VPL>
-__global__ void __launch_bounds__(256)
-    k_rows_replay_wave(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
-                       int32_t *__restrict__ last, int64_t n_table,
-                       const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
-                       int64_t n_max, const float *__restrict__ hist, int32_t step_arg,
-                       const dw_step_scalars *__restrict__ dyn, int32_t delta) {
-    const int32_t upto = dw::eff_step(dyn, delta, step_arg);
-    const int lane = threadIdx.x & 63;
-    int64_t n = n_max;
-    if (n_dev) {
-        const int64_t c = *n_dev;
-        n = c < n_max ? c : n_max;
-    }
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
-    const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / 64;
-    constexpr int d = 64 * VPL;
-    for (int64_t i0 = 2 * wave; i0 < n; i0 += 2 * n_waves) {
-        int64_t r[2];
-        int32_t from[2];
-        float pp[2][VPL], mm[2][VPL], vv[2][VPL];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t i = i0 + j;
-            r[j] = i < n ? (rows ? static_cast<int64_t>(rows[i]) : i) : -1;
-            from[j] = (r[j] >= 0 && r[j] < n_table) ? __builtin_amdgcn_readfirstlane(last[r[j]])
-                                                     : upto;
-            if (from[j] < upto) {
-                const int64_t o = r[j] * d + lane * VPL;
-#pragma unroll
-                for (int e = 0; e < VPL; ++e) {
-                    pp[j][e] = p[o + e];
-                    mm[j][e] = m[o + e];
-                    vv[j][e] = v[o + e];
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            if (from[j] >= upto) continue;
-            for (int32_t s = from[j] + 1; s <= upto; ++s) {
-                const dw::AdamScalars h = hist_at(hist, s);
-                if (h.wd == 0.f) {
-#pragma unroll
-                    for (int e = 0; e < VPL; ++e) dw::adam_elem_g0(pp[j][e], mm[j][e], vv[j][e], h);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < VPL; ++e) {
-                        float z = 0.f;
-                        dw::adam_elem(pp[j][e], z, mm[j][e], vv[j][e], h);
-                    }
-                }
-            }
-            const int64_t o = r[j] * d + lane * VPL;
-#pragma unroll
-            for (int e = 0; e < VPL; ++e) {
-                p[o + e] = pp[j][e];
-                m[o + e] = mm[j][e];
-                v[o + e] = vv[j][e];
-            }
-            if (lane == 0) last[r[j]] = upto;
-        }
-    }
-}
-
 // out[i] = table[rows[i]] (one wave per row); zero: the source rows are cleared in the same pass
 __global__ void __launch_bounds__(256)
     k_rows_gather(float *__restrict__ table, int64_t n_table, int32_t d,
@@ -372,50 +301,6 @@ int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
 }
-
-}  // extern "C"
-
-int dw::rows_replay_wave(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                         int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                         const int64_t *n_rows_dev, int64_t n_rows_max, const float *hist,
-                         int32_t step, void *stream) {
-    if (dim % 64 != 0 || dim > 512 || dim == 192 || (dim > 256 && dim != 512))
-        return dw_adam_rows(param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
-                            n_rows_dev, n_rows_max, nullptr, hist, step, stream);
-    DW_REQUIRE(n_table_rows >= 0 && n_rows_max >= 0 && step >= 0, "dw_adam_rows: bad sizes");
-    if (n_rows_max == 0) return DW_OK;
-    DW_REQUIRE(param && exp_avg && exp_avg_sq && last_step && hist, "dw_adam_rows: null pointer");
-    DW_REQUIRE(rows || !n_rows_dev, "dw_adam_rows: a device row count needs a row list");
-    const dw_step_scalars *dyn = nullptr;
-    int32_t delta = 0;
-    const int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_adam_rows");
-    if (rc != DW_OK) return rc;
-    int64_t blocks = (n_rows_max + 7) / 8;   // 4 waves per block, 2 rows per wave and trip
-    static const int cus = [] {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess)
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return n > 0 ? n : 256;
-    }();
-    if (blocks > 16LL * cus) blocks = 16LL * cus;
-    if (blocks < 1) blocks = 1;
-    hipStream_t st = dw::as_stream(stream);
-#define DW_RRW(VPL)                                                                              \
-    hipLaunchKernelGGL((k_rows_replay_wave<VPL>), dim3((unsigned)blocks), dim3(256), 0, st, param, \
-                       exp_avg, exp_avg_sq, last_step, n_table_rows, rows, n_rows_dev,           \
-                       n_rows_max, hist, step, dyn, delta)
-    switch (dim / 64) {
-        case 1: DW_RRW(1); break;
-        case 2: DW_RRW(2); break;
-        case 4: DW_RRW(4); break;
-        default: DW_RRW(8); break;
-    }
-#undef DW_RRW
-    DW_LAUNCH_CHECK("dw_adam_rows/replay_wave");
-    return DW_OK;
-}
-
-extern "C" {
 
 int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                    const int64_t *n_rows_dev, int64_t n_rows_max, float *out,

@@ -22,12 +22,6 @@ const dw_step_scalars *bound_step_scalars();
 // DW_E_INVALID_ARG when a block is bound without a host step (dw_step_scalars_bind): a captured
 // lazy step would otherwise replay a frozen step number.
 int bound_step_rel(int64_t step, const dw_step_scalars **dyn, int32_t *delta, const char *what);
-// dw_adam_rows' g = 0 replay up to `step` in its memory-bound form (one wave per row; the lazy
-// out slice's catch-up), k_rows_adam's per-row blocks for other shapes (dw_adam.hip)
-int rows_replay_wave(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                     int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                     const int64_t *n_rows_dev, int64_t n_rows_max, const float *hist,
-                     int32_t step, void *stream);
 
 // The step a lazy kernel applies: the bound block's (plus the launch's delta) or the launch's.
 __device__ __forceinline__ int32_t eff_step(const dw_step_scalars *dyn, int32_t delta,

@@ -891,12 +891,13 @@ using SmallSortConfig = rocprim::radix_sort_config<
     128 * 1024>;
 constexpr uint32_t SMALL_SORT_MAX = 4u << 20;
 // dw_sgns_owner_presort's sort (the reference's 64-walk batch: 269K records, 21-bit rows), which
-// runs beside the memory-bound catch-up: 11-bit digits on 2K-item tiles, two passes (and two
-// lookback resets) instead of three.
+// runs beside the memory-bound catch-up: 11-bit digits on 4K-item tiles, two passes (and two
+// lookback resets) instead of three; alone on the chip 62 us against 65 for SmallSortConfig
+// and 126 for 11-bit digits on 2K-item tiles (scripts/microbench/small_sort_bench.hip).
 using PresortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>,
-                                        rocprim::kernel_config<256, 8>, 11,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 4>,
+                                        rocprim::kernel_config<1024, 4>, 11,
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
@@ -906,23 +907,14 @@ template <class K, class Vt>
 hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
                       rocprim::double_buffer<Vt> &vb, uint32_t n, int end_bit, hipStream_t st) {
     if (tmp == nullptr) {
-        size_t a = 0, b = 0, c = 0;
+        size_t a = 0, b = 0;
         hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, kb, vb, n, 0,
                                                                    end_bit, st);
         if (e == hipSuccess)
             e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, kb, vb, n, 0, end_bit, st);
-        if (e == hipSuccess)
-            e = rocprim::radix_sort_pairs<PresortConfig>(nullptr, c, kb, vb, n, 0, end_bit, st);
         bytes = a > b ? a : b;
-        bytes = bytes > c ? bytes : c;
         return e;
     }
-    static const bool sort11 = [] {   // DW_SORT11=1: two 11-bit passes for small sorts (A/B)
-        const char *e = getenv("DW_SORT11");
-        return e && e[0] == '1';
-    }();
-    if (sort11 && n < (1u << 20))
-        return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     if (n < SMALL_SORT_MAX)
         return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
@@ -2102,17 +2094,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    // DW_CATCHUP_WAVE=1: one wave per row (k_rows_replay_wave); default: a block per row
-    // (k_rows_adam) — beside the presort's traffic the wave form measured slower (216 vs 165 us)
-    static const bool per_row_blocks = [] {
-        const char *e = getenv("DW_CATCHUP_WAVE");
-        return !(e && e[0] == '1');
-    }();
-    if (per_row_blocks)
-        return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
-                            n_rows, n_max, nullptr, hist, step - 1, stream);
-    return dw::rows_replay_wave(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
-                                n_rows, n_max, hist, step - 1, stream);
+    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
+                        n_max, nullptr, hist, step - 1, stream);
 }
 
 int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,

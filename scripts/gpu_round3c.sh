@@ -8,10 +8,6 @@ export TMPDIR=/tmp
 timeout -k 10 120 ./scripts/microbench/small_sort_bench > gpurun_out/small_sort_bench.log 2>&1 || { tail -3 gpurun_out/small_sort_bench.log; exit 1; }
 cat gpurun_out/small_sort_bench.log
 BATCH_SPECS="c3_64:--batch-walks 64 --steps 400;c3_1024:--batch-walks 1024 --steps 100;c2:--config c2 --steps 400" bash scripts/gpu_batches.sh || exit 1
-for ab in "DW_CATCHUP_WAVE=1" "DW_SORT11=1" "DW_CATCHUP_WAVE=1 DW_SORT11=1"; do
-  env $ab timeout -k 10 300 python bench.py --batch-walks 64 --steps 400 --no-cpu-baseline --no-walk-bench > gpurun_out/c3_64_ab.log 2>&1 || { tail -5 gpurun_out/c3_64_ab.log; exit 1; }
-  grep '^{' gpurun_out/c3_64_ab.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3_64 $ab', d['value'], d['ms_per_step'])"
-done
 timeout -k 10 400 python bench.py --config c5 --steps 30 --warmup 3 --no-cpu-baseline --no-walk-bench > gpurun_out/bench_c5.log 2>&1 || { tail -5 gpurun_out/bench_c5.log; exit 1; }
 grep '^{' gpurun_out/bench_c5.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v['ms'],2) for k, v in d['roofline'].get('phases', {}).items()})"
 cd deepwalk-and-node2vec_amd
