@@ -629,8 +629,13 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 const int tt = gl + 16 * k;
                 if (tt < T) {
                     const int32_t id = s_id[wv][q][tt];
-                    a.rec_key[b * T + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
-                    a.rec_val[b * T + tt] = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
+                    const uint64_t val = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
+                    if (a.walk_order) {   // presorted: the value straight to its sorted place
+                        a.rec_val[a.rec_inv[b * T + tt]] = val;
+                    } else {
+                        a.rec_key[b * T + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                        a.rec_val[b * T + tt] = val;
+                    }
                 }
             }
         }
@@ -1270,13 +1275,18 @@ PhaseTimer g_timer;
 // the output-table phase runs (ShardedTables.exchange_in).
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st, const OutAdam *oa);
+                     hipStream_t st, const OutAdam *oa, bool presorted);
 
+// phase: 0 = both passes, 1 = pass 1, 2 = the output-table phase; | 4 = the records were
+// presorted (dw_sgns_walks_presort): pass 1 writes values only, phase 2 does not sort
 template <bool FROM_WALKS>
 int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, hipStream_t st,
                 const OutAdam *oa = nullptr) {
+    const bool presorted = (phase & 4) != 0;
+    phase &= 3;
     if (phase != 2) g_timer.mark(0, st);
-    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st, oa);
+    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st, oa,
+                                                presorted);
     if (rc != DW_OK) {
         if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
         return rc;
@@ -1287,8 +1297,10 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, 
 
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st, const OutAdam *oa) {
+                     hipStream_t st, const OutAdam *oa, bool presorted) {
     const bool do1 = phase != 2, do2 = phase != 1;
+    DW_REQUIRE(!presorted || (FROM_WALKS && phase != 0 && workspace),
+               "dw_sgns: presorted records need the walks, a phase split and the workspace");
     if (a.batch == 0 && do2 && oa) {  // no records: every out row gets Adam with g = g_out
         if (do1) g_timer.mark(1, st);
         g_timer.mark(2, st);
@@ -1317,12 +1329,21 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     if (do1) {
         a.rec_key = ws.k0;
         a.rec_val = ws.v0;
+        if (presorted) {   // dw_sgns_walks_presort's layout: values to v1 through the inverse
+            a.walk_order = true;
+            a.rec_val = ws.v1;
+            a.rec_inv = reinterpret_cast<const uint32_t *>(ws.v0) + n_rec;
+        }
         rc = launch_pass1_g16<FROM_WALKS>(a, st);
-        if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
+        if (rc == DW_E_UNSUPPORTED && !presorted) rc = launch_pass1<FROM_WALKS, true>(a, st);
         if (rc != DW_OK) return rc;
         g_timer.mark(1, st);
     }
     if (!do2) return DW_OK;
+    if (presorted) {
+        g_timer.mark(2, st);
+        return launch_pass2(ws.k0, ws.v1, n_rec, a.w_in, a.g_out, a.d, oa, a.V, st);
+    }
     rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
     rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
@@ -2043,6 +2064,8 @@ __global__ void __launch_bounds__(256)
         inv[pos[i]] = static_cast<uint32_t>(i);
 }
 
+int presort_impl(const SgnsArgs &a, const Workspace &ws, int64_t vocab_size, hipStream_t st);
+
 }  // namespace
 
 extern "C" {
@@ -2124,6 +2147,44 @@ int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_le
     int rc = owner_workspace(a.batch, T, vocab_size, workspace, workspace_bytes, &ws, &lay, st,
                              "dw_sgns_owner_presort");
     if (rc != DW_OK) return rc;
+    return presort_impl(a, ws, vocab_size, st);
+}
+
+int dw_sgns_walks_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                          int32_t *status, void *workspace, size_t workspace_bytes,
+                          void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   vocab_size >= 1 && neg_samples >= 0,
+               "dw_sgns_walks_presort: bad sizes");
+    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= WAVE,
+               "dw_sgns_walks_presort: 2R(1+K) must be <= 64");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(walks && status && workspace, "dw_sgns_walks_presort: null pointer");
+    hipStream_t st = dw::as_stream(stream);
+    SgnsArgs a = base_args(vocab_size, 64, neg_samples, nullptr, nullptr, nullptr, nullptr, noise,
+                           seed, noise_offset, 0.f, nullptr, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_walks * (walk_length - 2 * context_radius);
+    a.C = 2 * context_radius;
+    const int64_t n_rec = a.batch * (int64_t)a.C * (1 + neg_samples);
+    DW_REQUIRE(n_rec < 0x7FFFFFFF, "dw_sgns_walks_presort: too many records");
+    Workspace ws;   // dw_sgns_walks_phase's layout
+    int rc = plan_workspace(n_rec, vocab_size, workspace, &ws, st);
+    if (rc != DW_OK) return rc;
+    DW_REQUIRE(workspace_bytes >= ws.total, "dw_sgns_walks_presort: workspace too small");
+    return presort_impl(a, ws, vocab_size, st);
+}
+
+}  // extern "C"
+
+namespace {
+// The records' order for a batch ahead of pass 1 (dw_sgns_owner_presort / dw_sgns_walks_presort)
+int presort_impl(const SgnsArgs &a, const Workspace &ws, int64_t vocab_size, hipStream_t st) {
+    const int64_t T = (int64_t)a.C * (1 + a.K);
     const int64_t n = a.batch * T;
     DW_REQUIRE(n < (int64_t(1) << 32), "dw_sgns_owner_presort: too many records");
     // keys (k1) and walk-slot positions (the second half of v0) in, the sorted keys to k0 and the
@@ -2156,6 +2217,9 @@ int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_le
     DW_LAUNCH_CHECK("dw_sgns_owner_presort/inverse");
     return DW_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int dw_sgns_timing(int32_t enable) {
     g_timer.on = enable != 0;
@@ -2206,7 +2270,8 @@ int sgns_walks(int phase, const int32_t *walks, int64_t n_walks, int32_t walk_le
                const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
                double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
                void *stream) {
-    DW_REQUIRE(phase >= 0 && phase <= 2, "dw_sgns_walks_phase: phase must be 0, 1 or 2");
+    DW_REQUIRE((phase & 3) <= 2 && (phase & ~7) == 0 && phase != 4,
+               "dw_sgns_walks_phase: phase must be 0, 1 or 2 (| 4: presorted)");
     DW_REQUIRE(context_radius >= 1, "dw_sgns_walks: context_radius must be >= 1");
     DW_REQUIRE(walk_length >= 2 * context_radius + 1,
                "dw_sgns_walks: walk_length %d < 2R+1 (Text is too short!)", walk_length);
@@ -2241,8 +2306,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                               float *m_out, float *v_out, uint8_t *row_flags,
                               float one_minus_beta1, float beta2, float one_minus_beta2,
                               float bias_correction2_sqrt, float neg_step_size, float eps,
-                              float weight_decay, int32_t *status, void *workspace,
-                              size_t workspace_bytes, void *stream) {
+                              float weight_decay, int32_t presorted, int32_t *status,
+                              void *workspace, size_t workspace_bytes, void *stream) {
     DW_REQUIRE(workspace && m_out && v_out && row_flags && w_out && g_out,
                "dw_sgns_walks_phase2_adam: needs the records workspace and the Adam state");
     DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_sgns_walks_phase2_adam: bad Adam scalars");
@@ -2261,7 +2326,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
                                neg_step_size, eps, weight_decay}};
     oa.dyn = dw::bound_step_scalars();
-    return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
+    return launch_sgns<true>(a, workspace, workspace_bytes, presorted ? (2 | 4) : 2,
+                             dw::as_stream(stream), &oa);
 }
 
 int dw_sgns_walks_phase2_piece(int32_t piece, int32_t n_pieces, int64_t piece_rows,

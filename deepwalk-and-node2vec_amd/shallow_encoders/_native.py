@@ -104,7 +104,9 @@ SIGNATURES = {
                                              _p, ctypes.c_size_t, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
-                                                 _f32, _f32, _p, _p, ctypes.c_size_t, _p]),
+                                                 _f32, _f32, _i32, _p, _p, ctypes.c_size_t, _p]),
+    'dw_sgns_walks_presort': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _p, _u64, _u64, _p,
+                                             _p, ctypes.c_size_t, _p]),
     'dw_sgns_pairs': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),

@@ -420,6 +420,16 @@ def replicated_step(tables: ShardedTables, walks: torch.Tensor, context_radius: 
               grad_scale=grad_scale, loss_acc=loss_acc, status=status, scatter=scatter)
     fuse = fuse_out_adam and scatter == 'sorted' and tables.can_fuse_out_adam()
     pb = sgns_phase_bytes(n, L, R, K, tables.d, tables.V, scatter, fuse)
+    # DW_PRESORT_STEP=1 (one GPU, records path; an A/B knob, off by default): the records'
+    # order sorted ahead of pass 1 (sgns_walks_presort), which then writes each value at its
+    # sorted place, so the output-table phase starts without a sort. Pass 1 needs the inverse
+    # map, so the sort cannot hide beside it; nothing else of this step runs before pass 1.
+    if (scatter == 'sorted' and not pieces and not tables.multi
+            and os.environ.get('DW_PRESORT_STEP', '0') == '1'):
+        from shallow_encoders.word2vec.sgns import sgns_walks_presort
+        sgns_walks_presort(walks, R, K, tables.V, seed=seed, noise_offset=noise_offset,
+                           status=status)
+        kw['presorted'] = True
     sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
     if after_pass1 is not None:
         after_pass1()

@@ -351,8 +351,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                               float *m_out, float *v_out, uint8_t *row_flags,
                               float one_minus_beta1, float beta2, float one_minus_beta2,
                               float bias_correction2_sqrt, float neg_step_size, float eps,
-                              float weight_decay, int32_t *status, void *workspace,
-                              size_t workspace_bytes, void *stream);
+                              float weight_decay, int32_t presorted, int32_t *status,
+                              void *workspace, size_t workspace_bytes, void *stream);
 
 /* Owner-computes form of the walks SGNS step for N > 1 (ShardedTables(mode='owner'), bench.py).
  * The output ("context") table is sharded by row owner: rank `owner` of `n_owners` holds only
@@ -443,6 +443,15 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
  * depends only on the walks and the negatives' stream, so it can run on a side stream beside
  * dw_sgns_owner_out_catch_up (the reference's 64-walk batch: the ~10 launches of a small sort
  * off the step's critical path). The same workspace as the passes. 2R(1+K) <= 64. */
+/* dw_sgns_owner_presort for the one-device walks path (dw_sgns_walks_phase's workspace): then
+ * dw_sgns_walks_phase(1 | 4, ...) writes only the values, each at its sorted place, and
+ * dw_sgns_walks_phase(2 | 4, ...) / dw_sgns_walks_phase2_adam(presorted = 1) gather without a
+ * sort. Meant to run on a side stream beside pass 1 (which it does not depend on). */
+int dw_sgns_walks_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                          int32_t *status, void *workspace, size_t workspace_bytes,
+                          void *stream);
 int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           const int64_t *noise, uint64_t seed, uint64_t noise_offset,
