@@ -1987,7 +1987,10 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64); a row is
 // claimed by exactly one lane in the launch — atomicMax(claim[row], step) returning < step — and
 // the wave appends its claimed rows to `list` with one counter atomic. dw_adam_rows then
-// replays the listed rows, all in parallel.
+// replays the listed rows, all in parallel. A row the previous step claimed (old == step - 1) is
+// not listed: that step's lazy gather brings it to step - 1 itself. So the listed rows are
+// disjoint from the previous step's, and this claim and catch-up may run beside that step's
+// output-table phase (OwnerLazyTables.catch_up_out_ahead).
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
@@ -2012,7 +2015,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                 dw::status_or(a.status, DW_S_BAD_INDEX);
             } else if (o % a.n_owners == a.owner) {
                 lo = static_cast<uint32_t>(o / a.n_owners);
-                mine = atomicMax(claim + lo, step) < step;
+                mine = atomicMax(claim + lo, step) < step - 1;
             }
         }
         const unsigned long long mask = __ballot(mine);

@@ -776,6 +776,12 @@ class OwnerLazyTables(OwnerTables):
                         and os.environ.get('DW_PRESORT', '0') == '1')
         self._presorted = False
         self._side2 = None
+        # one rank, lazy out slice: the next batch's out rows claimed and caught up beside this
+        # step's output-table phase (catch_up_out_ahead; DW_OUT_AHEAD=0 turns it off)
+        self.out_ahead = (self.lazy_out and not self.multi
+                          and os.environ.get('DW_OUT_AHEAD', '1') != '0')
+        self._ahead = None
+        self._side3 = None
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -784,11 +790,13 @@ class OwnerLazyTables(OwnerTables):
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
-                     noise: Optional[torch.Tensor] = None) -> None:
+                     noise: Optional[torch.Tensor] = None, step: Optional[int] = None) -> None:
         """lazy_out, before pass 1 of the batch ``walks``: the owned out rows its slots
-        reference replay their deferred steps up to step - 1 (dw_sgns_owner_out_catch_up)."""
+        reference replay their deferred steps up to step - 1 (dw_sgns_owner_out_catch_up).
+        ``step``: the Adam step of that batch (default: the current one)."""
         if not self.lazy_out:
             return
+        step = self.step_count if step is None else int(step)
         n, L = walks.shape
         slots = n * (L - 2 * int(context_radius)) * 2 * int(context_radius) * (1 + int(neg_samples))
         cap = max(1, min(self.S, slots))
@@ -802,7 +810,31 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist),
-                         self.step_count, _native.ptr(status), _native.stream(self.device))
+                         step, _native.ptr(status), _native.stream(self.device))
+
+    def catch_up_out_ahead(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
+                           seed: int, noise_offset: int, status: torch.Tensor) -> bool:
+        """One rank, lazy_out, after pass 1 of step t: the out-row claim and catch-up of the
+        NEXT batch ``walks`` (step t + 1), on a side stream beside this step's output-table
+        phase. The claim leaves out the rows step t claimed (its lazy gather brings them to t),
+        so the replayed rows are disjoint from the ones step t's pass 2 writes. Step t + 1 must
+        then train exactly ``walks`` (before_pass1 checks it). Returns False where it does not
+        apply (several ranks, dense out slice, DW_OUT_AHEAD=0)."""
+        if not self.out_ahead or self._ahead is not None:
+            return False
+        main = torch.cuda.current_stream(self.device)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        if self._side3 is None:
+            self._side3 = torch.cuda.Stream(self.device)
+        with torch.cuda.stream(self._side3):
+            self._side3.wait_event(fork)
+            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status,
+                              step=self.step_count + 1)
+            done = torch.cuda.Event()
+            done.record(self._side3)
+        self._ahead = ((walks.data_ptr(), tuple(walks.shape), self.step_count + 1), done)
+        return True
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -947,8 +979,16 @@ class OwnerLazyTables(OwnerTables):
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
-            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
             joins = []
+            if self._ahead is not None:   # claimed and caught up during the previous step
+                key, done = self._ahead
+                self._ahead = None
+                if key != (walks.data_ptr(), tuple(walks.shape), self.step_count):
+                    raise RuntimeError('OwnerLazyTables: the out rows were caught up ahead for '
+                                       'another batch (catch_up_out_ahead) than this step trains')
+                joins.append(done)
+            else:
+                self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
                 self.prepare(walks, context_radius, neg_samples)
@@ -969,6 +1009,8 @@ class OwnerLazyTables(OwnerTables):
             for j in joins:
                 main.wait_event(j)
             return
+        if self._ahead is not None:
+            raise RuntimeError('OwnerLazyTables: catch_up_out_ahead is one-rank only')
         self.prepare(walks, context_radius, neg_samples)
         self.catch_up()
         self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1019,6 +1061,9 @@ class OwnerLazyTables(OwnerTables):
 
     def _flush_out(self) -> None:
         """lazy_out: every out-slice row up to the current step."""
+        if self._ahead is not None:
+            raise RuntimeError('OwnerLazyTables: a catch-up for the next batch is pending; run '
+                               'that step before reading the out table')
         if self.lazy_out and self.step_count > 0:
             hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
                           self.S, None, self._hist, self.step_count)
@@ -1047,9 +1092,11 @@ class OwnerLazyTables(OwnerTables):
 
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
                     neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
-                    loss_acc: torch.Tensor, status: torch.Tensor) -> int:
+                    loss_acc: torch.Tensor, status: torch.Tensor,
+                    after_pass1: Optional[Callable[[], None]] = None) -> int:
     """One owner-computes step with the touched-row in-table exchange (every rank passes the
-    same global batch). Returns this rank's record count."""
+    same global batch). Returns this rank's record count. ``after_pass1``: a host callback at
+    that point of the enqueue order (the next batch's catch_up_out_ahead goes there)."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1058,6 +1105,8 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
                      grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
                      presorted=tables._presorted)
+    if after_pass1 is not None:
+        after_pass1()
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,

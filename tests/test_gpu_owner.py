@@ -348,18 +348,26 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d, wd):
 
 
 def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False,
-                   snaps=None):
+                   snaps=None, ahead=False):
     """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L];
-    ``snaps``: a list receiving _owner_snapshot after every step."""
+    ``snaps``: a list receiving _owner_snapshot after every step; ``ahead``: every step but
+    the last claims and catches up the next batch's out rows after its pass 1
+    (catch_up_out_ahead)."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
     t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
     n, L = walks_all.shape[1:]
     per = L - 2 * R
     acc = torch.zeros(4, dtype=torch.float64, device=device)
     status = torch.zeros(1, dtype=torch.int32, device=device)
+    dev_walks = [walks_all[s].to(device) for s in range(walks_all.shape[0])]
     for s in range(walks_all.shape[0]):
-        owner_lazy_step(t, walks_all[s].to(device), R, K, seed=11, noise_offset=s * n * per,
-                        grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status)
+        hook = None
+        if ahead and s + 1 < len(dev_walks):
+            def hook(s=s):
+                assert t.catch_up_out_ahead(dev_walks[s + 1], R, K, 11, (s + 1) * n * per, status)
+        owner_lazy_step(t, dev_walks[s], R, K, seed=11, noise_offset=s * n * per,
+                        grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status,
+                        after_pass1=hook)
         if snaps is not None:
             torch.cuda.synchronize()
             snaps.append(_owner_snapshot(t, V))
@@ -368,11 +376,13 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
     return t, acc
 
 
-@pytest.mark.parametrize('lazy_out', [False, True])
-def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
+@pytest.mark.parametrize('lazy_out,ahead', [(False, False), (True, False), (True, True)])
+def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead):
     """One rank: sparse batches (most rows untouched for several steps) through the lazy
     protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush;
-    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary)."""
+    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary);
+    ahead: each next batch's out rows claimed and caught up beside the step before's output-table
+    phase (catch_up_out_ahead)."""
     from shallow_encoders.word2vec.sharding import ShardedTables
     V, d, R, K, L, n, steps, lr = 5000, 64, 2, 3, 12, 16, 6, 0.01
     walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(3),
@@ -384,7 +394,7 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
         sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
                         context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
         ref.step()
-    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out)
+    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out, ahead=ahead)
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
     if lazy_out:
@@ -568,3 +578,24 @@ def test_presorted_records_equal_pass2_sort(hip_device, monkeypatch):
         # Adam's normalisation; 1 entry in 640,000 at 1.5x the bar on one run)
         assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-4, max_abs=lr * steps)
         assert_no_row_drift(got, exp)
+
+
+def test_out_ahead_checks_its_batch(hip_device):
+    """A catch-up ahead for one batch and a step on another is refused (the claims would skip
+    rows the other batch needs), as is reading the out table while one is pending."""
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    V, d, R, K, L, n = 2000, 64, 2, 3, 12, 8
+    t = OwnerLazyTables(V, d, hip_device, lr=0.01, init_seed=4, lazy_out=True)
+    assert t.out_ahead
+    g = torch.Generator().manual_seed(1)
+    w = [torch.randint(1, V, (n, L), generator=g, dtype=torch.int32).to(hip_device)
+         for _ in range(3)]
+    acc = torch.zeros(4, dtype=torch.float64, device=hip_device)
+    status = torch.zeros(1, dtype=torch.int32, device=hip_device)
+    kw = dict(seed=11, grad_scale=1.0, loss_acc=acc, status=status)
+    owner_lazy_step(t, w[0], R, K, noise_offset=0,
+                    after_pass1=lambda: t.catch_up_out_ahead(w[1], R, K, 11, 64, status), **kw)
+    with pytest.raises(RuntimeError, match='pending'):
+        t.full_w_out()
+    with pytest.raises(RuntimeError, match='another batch'):
+        owner_lazy_step(t, w[2], R, K, noise_offset=64, **kw)
