@@ -1778,7 +1778,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
 int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
                        const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
                        size_t workspace_bytes, int64_t *n_records, hipStream_t st,
-                       bool presorted = false) {
+                       bool presorted = false, hipEvent_t sorted_event = nullptr) {
     Workspace ws;
     OwnerLayout lay;
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
@@ -1788,6 +1788,10 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     if (presorted) {   // dw_sgns_owner_presort's order + pass 1's walk-order values: no sort here
         DW_REQUIRE(oa && !n_records, "dw_sgns_owner_pass2_lazy: presorted needs n_records NULL");
         g_timer.mark(2, st);
+        if (sorted_event && hipEventRecord(sorted_event, st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner_pass2: recording the sorted event failed");
+            return DW_E_HIP;
+        }
         if (bound > 0) rc = launch_pass2(ws.k0, ws.v1, bound, w_in, g_out, d, oa, local_rows, st);
         g_timer.mark(3, st);
         return rc;
@@ -1829,6 +1833,11 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
         vals = vb.current();
     }
     g_timer.mark(2, st);
+    // the records are sorted: work waiting on this event runs beside the gather
+    if (sorted_event && hipEventRecord(sorted_event, st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner_pass2: recording the sorted event failed");
+        return DW_E_HIP;
+    }
     if (n_rec > 0 || oa) {
         rc = launch_pass2(keys, vals, n_rec, w_in, g_out, d, oa, local_rows, st, range);
         if (rc != DW_OK) return rc;
@@ -2463,7 +2472,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
                              int32_t step, int32_t presorted, int32_t *status,
                              void *workspace, size_t workspace_bytes, int64_t *n_records,
-                             void *stream) {
+                             void *sorted_event, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
                "dw_sgns_owner_pass2_lazy: bad sizes");
@@ -2476,7 +2485,8 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
-                              dw::as_stream(stream), presorted != 0);
+                              dw::as_stream(stream), presorted != 0,
+                              static_cast<hipEvent_t>(sorted_event));
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

@@ -279,11 +279,11 @@ class GraphedOwnerStep:
                 ahead = self._ahead_fn(k)
             owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
                             noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
-                            status=self.status, after_pass1=ahead)
+                            status=self.status, ahead=ahead)
 
     def _ahead_fn(self, k: int):
-        """After pass 1 of step k: step k + 1's out-row claim and catch-up, bound to block
-        k + 1 (its step number and negatives), beside step k's output-table phase."""
+        """Once step k's pass 2 is enqueued: step k + 1's out-row claim and catch-up, bound to
+        block k + 1 (its step number and negatives), beside step k's lazy gather."""
         t, B = self.t, self.B
 
         def ahead() -> None:

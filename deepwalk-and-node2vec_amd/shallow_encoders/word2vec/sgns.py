@@ -475,7 +475,7 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
                          int(out_adam['step']), int(bool(out_adam.get('presorted', False))),
                          _native.ptr(status), _native.ptr(ws), ws.numel(), n_rec_p,
-                         _native.stream(dev))
+                         out_adam.get('sorted_event') or None, _native.stream(dev))
         return int(n_rec.value) if read_count else None
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),

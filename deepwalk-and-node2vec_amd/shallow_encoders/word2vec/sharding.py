@@ -782,6 +782,8 @@ class OwnerLazyTables(OwnerTables):
                           and os.environ.get('DW_OUT_AHEAD', '1') != '0')
         self._ahead = None
         self._side3 = None
+        self._sorted_ev = None      # recorded by pass 2 once its records are sorted
+        self._sorted_armed = False
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -812,19 +814,37 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._n_out), _native.ptr(self._hist),
                          step, _native.ptr(status), _native.stream(self.device))
 
+    def sorted_event(self) -> Optional[int]:
+        """The hipEvent_t pass 2 records once its records are sorted (dw_sgns_owner_pass2_lazy's
+        sorted_event), for the next catch_up_out_ahead to start from; None where that does not
+        apply."""
+        if not self.out_ahead:
+            return None
+        if self._sorted_ev is None:
+            self._sorted_ev = torch.cuda.Event()
+        if not self._sorted_ev.cuda_event:   # torch creates the event at its first record
+            self._sorted_ev.record(torch.cuda.current_stream(self.device))
+        self._sorted_armed = True
+        return self._sorted_ev.cuda_event
+
     def catch_up_out_ahead(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                            seed: int, noise_offset: int, status: torch.Tensor) -> bool:
-        """One rank, lazy_out, after pass 1 of step t: the out-row claim and catch-up of the
-        NEXT batch ``walks`` (step t + 1), on a side stream beside this step's output-table
-        phase. The claim leaves out the rows step t claimed (its lazy gather brings them to t),
-        so the replayed rows are disjoint from the ones step t's pass 2 writes. Step t + 1 must
-        then train exactly ``walks`` (before_pass1 checks it). Returns False where it does not
-        apply (several ranks, dense out slice, DW_OUT_AHEAD=0)."""
+        """One rank, lazy_out, during step t (after its pass 2 was enqueued): the out-row claim
+        and catch-up of the NEXT batch ``walks`` (step t + 1), on a side stream that starts once
+        step t's records are sorted (sorted_event), beside its lazy gather. The claim leaves out
+        the rows step t claimed (that gather brings them to t), so the replayed rows are disjoint
+        from the ones step t's pass 2 writes. Step t + 1 must then train exactly ``walks``
+        (before_pass1 checks it). Returns False where it does not apply (several ranks, dense
+        out slice, DW_OUT_AHEAD=0)."""
         if not self.out_ahead or self._ahead is not None:
             return False
         main = torch.cuda.current_stream(self.device)
-        fork = torch.cuda.Event()
-        fork.record(main)
+        if self._sorted_armed:
+            fork = self._sorted_ev
+            self._sorted_armed = False
+        else:
+            fork = torch.cuda.Event()
+            fork.record(main)
         if self._side3 is None:
             self._side3 = torch.cuda.Stream(self.device)
         with torch.cuda.stream(self._side3):
@@ -1093,10 +1113,10 @@ class OwnerLazyTables(OwnerTables):
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
                     neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
                     loss_acc: torch.Tensor, status: torch.Tensor,
-                    after_pass1: Optional[Callable[[], None]] = None) -> int:
+                    ahead: Optional[Callable[[], None]] = None) -> int:
     """One owner-computes step with the touched-row in-table exchange (every rank passes the
-    same global batch). Returns this rank's record count. ``after_pass1``: a host callback at
-    that point of the enqueue order (the next batch's catch_up_out_ahead goes there)."""
+    same global batch). Returns this rank's record count. ``ahead``: a host callback run once
+    pass 2 is enqueued, with its sorted event armed (the next batch's catch_up_out_ahead)."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1105,13 +1125,15 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
                      grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
                      presorted=tables._presorted)
-    if after_pass1 is not None:
-        after_pass1()
     tables.exchange_touched()
     spec = tables.out_adam_spec()
+    if ahead is not None and spec is not None and getattr(tables, 'out_ahead', False):
+        spec['sorted_event'] = tables.sorted_event()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,
                          context_radius=context_radius, out_adam=spec, status=status,
                          read_count=tables.world > 1)
+    if ahead is not None:
+        ahead()
     if n is None:   # one owner keeps every slot (no count readback)
         n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
             1 + neg_samples)

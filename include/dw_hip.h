@@ -428,13 +428,16 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * replayed (scalars hist[t], fp32 [steps][8] as for dw_adam_rows) right before its next update,
  * through the same adam_elem, so the slice equals the dense update bit for bit once flushed
  * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
- * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53). */
+ * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
+ * sorted_event (a hipEvent_t, or NULL): recorded on the stream once the records are sorted,
+ * before the gather (the next batch's out-row catch-up waits on it and runs beside the gather). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
                              int32_t step, int32_t presorted, int32_t *status, void *workspace,
-                             size_t workspace_bytes, int64_t *n_records, void *stream);
+                             size_t workspace_bytes, int64_t *n_records, void *sorted_event,
+                             void *stream);
 
 /* One owner, before dw_sgns_owner_pass1 of the same batch (pass 1's order_ready | 2, pass 2's
  * presorted = 1, n_records NULL): the records' order — every slot's row (contexts from the

@@ -351,7 +351,7 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
                    snaps=None, ahead=False):
     """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L];
     ``snaps``: a list receiving _owner_snapshot after every step; ``ahead``: every step but
-    the last claims and catches up the next batch's out rows after its pass 1
+    the last claims and catches up the next batch's out rows beside its gather
     (catch_up_out_ahead)."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
     t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
@@ -367,7 +367,7 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
                 assert t.catch_up_out_ahead(dev_walks[s + 1], R, K, 11, (s + 1) * n * per, status)
         owner_lazy_step(t, dev_walks[s], R, K, seed=11, noise_offset=s * n * per,
                         grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status,
-                        after_pass1=hook)
+                        ahead=hook)
         if snaps is not None:
             torch.cuda.synchronize()
             snaps.append(_owner_snapshot(t, V))
@@ -594,7 +594,7 @@ def test_out_ahead_checks_its_batch(hip_device):
     status = torch.zeros(1, dtype=torch.int32, device=hip_device)
     kw = dict(seed=11, grad_scale=1.0, loss_acc=acc, status=status)
     owner_lazy_step(t, w[0], R, K, noise_offset=0,
-                    after_pass1=lambda: t.catch_up_out_ahead(w[1], R, K, 11, 64, status), **kw)
+                    ahead=lambda: t.catch_up_out_ahead(w[1], R, K, 11, 64, status), **kw)
     with pytest.raises(RuntimeError, match='pending'):
         t.full_w_out()
     with pytest.raises(RuntimeError, match='another batch'):
