@@ -776,10 +776,13 @@ class OwnerLazyTables(OwnerTables):
                         and os.environ.get('DW_PRESORT', '0') == '1')
         self._presorted = False
         self._side2 = None
-        # one rank, lazy out slice: the next batch's out rows claimed and caught up beside this
-        # step's output-table phase (catch_up_out_ahead; DW_OUT_AHEAD=0 turns it off)
+        # one rank, lazy out slice, DW_OUT_AHEAD=1: the next batch's out rows claimed and caught
+        # up beside this step's lazy gather (catch_up_out_ahead). Off by default: the two share
+        # the chip's throughput (C3 at 64 walks: 0.514 / 0.518 vs 0.507 ms per step, the gather
+        # stretched by the catch-up's length; forked after pass 1 instead, beside the sort too:
+        # 0.548 vs 0.512), and the in-table catch-up it used to hide is exposed
         self.out_ahead = (self.lazy_out and not self.multi
-                          and os.environ.get('DW_OUT_AHEAD', '1') != '0')
+                          and os.environ.get('DW_OUT_AHEAD', '0') == '1')
         self._ahead = None
         self._side3 = None
         self._sorted_ev = None      # recorded by pass 2 once its records are sorted

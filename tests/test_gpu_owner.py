@@ -377,7 +377,7 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
 
 
 @pytest.mark.parametrize('lazy_out,ahead', [(False, False), (True, False), (True, True)])
-def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead):
+def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead, monkeypatch):
     """One rank: sparse batches (most rows untouched for several steps) through the lazy
     protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush;
     lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary);
@@ -394,7 +394,9 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead):
         sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
                         context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
         ref.step()
+    monkeypatch.setenv('DW_OUT_AHEAD', '1' if ahead else '0')
     t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out, ahead=ahead)
+    assert t.out_ahead == ahead
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
     if lazy_out:
@@ -580,10 +582,11 @@ def test_presorted_records_equal_pass2_sort(hip_device, monkeypatch):
         assert_no_row_drift(got, exp)
 
 
-def test_out_ahead_checks_its_batch(hip_device):
+def test_out_ahead_checks_its_batch(hip_device, monkeypatch):
     """A catch-up ahead for one batch and a step on another is refused (the claims would skip
     rows the other batch needs), as is reading the out table while one is pending."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    monkeypatch.setenv('DW_OUT_AHEAD', '1')
     V, d, R, K, L, n = 2000, 64, 2, 3, 12, 8
     t = OwnerLazyTables(V, d, hip_device, lr=0.01, init_seed=4, lazy_out=True)
     assert t.out_ahead
