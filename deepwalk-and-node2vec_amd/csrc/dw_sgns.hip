@@ -906,20 +906,35 @@ using PresortConfig = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
+// DW_SORT_SMALL11=1 (an A/B knob): small sorts of more than 16 key bits on PresortConfig (two
+// 11-bit passes) instead of SmallSortConfig (three 8-bit passes).
+bool small_sort_11() {
+    static const bool on = [] {
+        const char *e = std::getenv("DW_SORT_SMALL11");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // Stable LSD sort of (key, value) pairs on bits [0, end_bit), the config chosen by size. With
-// tmp == nullptr: *bytes = the larger of both configs' needs for n (so any n' <= n fits).
+// tmp == nullptr: *bytes = the largest of the configs' needs for n (so any n' <= n fits).
 template <class K, class Vt>
 hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
                       rocprim::double_buffer<Vt> &vb, uint32_t n, int end_bit, hipStream_t st) {
     if (tmp == nullptr) {
-        size_t a = 0, b = 0;
+        size_t a = 0, b = 0, c = 0;
         hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, kb, vb, n, 0,
                                                                    end_bit, st);
         if (e == hipSuccess)
             e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, kb, vb, n, 0, end_bit, st);
+        if (e == hipSuccess)
+            e = rocprim::radix_sort_pairs<PresortConfig>(nullptr, c, kb, vb, n, 0, end_bit, st);
         bytes = a > b ? a : b;
+        bytes = bytes > c ? bytes : c;
         return e;
     }
+    if (n < SMALL_SORT_MAX && end_bit > 16 && small_sort_11())
+        return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     if (n < SMALL_SORT_MAX)
         return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
