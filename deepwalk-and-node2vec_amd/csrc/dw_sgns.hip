@@ -906,12 +906,14 @@ using PresortConfig = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
-// DW_SORT_SMALL11=1 (an A/B knob): small sorts of more than 16 key bits on PresortConfig (two
-// 11-bit passes) instead of SmallSortConfig (three 8-bit passes).
+// Small sorts of more than 16 key bits (C3's 64-walk batch: 269K records on 20-bit rows) run on
+// PresortConfig — two 11-bit passes and two lookback resets instead of SmallSortConfig's three
+// 8-bit passes: 0.499 vs 0.509 ms per step, twice each (profiles/r03_sort_small11_ab.txt).
+// DW_SORT_SMALL11=0 restores the 8-bit passes.
 bool small_sort_11() {
     static const bool on = [] {
         const char *e = std::getenv("DW_SORT_SMALL11");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return on;
 }
