@@ -910,6 +910,15 @@ using PresortConfig = rocprim::radix_sort_config<
 // PresortConfig — two 11-bit passes and two lookback resets instead of SmallSortConfig's three
 // 8-bit passes: 0.499 vs 0.509 ms per step, twice each (profiles/r03_sort_small11_ab.txt).
 // DW_SORT_SMALL11=0 restores the 8-bit passes.
+// DW_SORT_SMALL11_MAX (an A/B knob): the record count below which that holds (SMALL_SORT_MAX).
+uint32_t small11_max() {
+    static const uint32_t m = [] {
+        const char *e = std::getenv("DW_SORT_SMALL11_MAX");
+        return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : SMALL_SORT_MAX;
+    }();
+    return m;
+}
+
 bool small_sort_11() {
     static const bool on = [] {
         const char *e = std::getenv("DW_SORT_SMALL11");
@@ -935,7 +944,7 @@ hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
         bytes = bytes > c ? bytes : c;
         return e;
     }
-    if (n < SMALL_SORT_MAX && end_bit > 16 && small_sort_11())
+    if (n < small11_max() && end_bit > 16 && small_sort_11())
         return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     if (n < SMALL_SORT_MAX)
         return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
