@@ -149,8 +149,6 @@ struct SgnsArgs {
     uint32_t *rec_counts;
     uint32_t *count_out;      //   n_owners == 1: the records are dense; their count goes here
     int64_t region;
-    bool walk_order = false;  //   one owner, presorted: values at rec_inv[b * T + t] (their
-    const uint32_t *rec_inv = nullptr;   //   sorted position), keys not written
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
@@ -603,23 +601,16 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             const int c1 = __builtin_amdgcn_readlane(n_own, 16);
             const int c2 = __builtin_amdgcn_readlane(n_own, 32);
             const int c3 = __builtin_amdgcn_readlane(n_own, 48);
-            const int64_t at =
-                a.walk_order ? b * T   // (one owner: every slot kept, n_own = T)
-                             : ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * a.region + filled +
-                                   (q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2);
+            const int64_t at = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + wv) * a.region + filled +
+                               (q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2);
 #pragma unroll
             for (int k = 0; k < G16_TMAX / 16; ++k) {
                 const int tt = gl + 16 * k;
                 if (tt < n_own) {
                     const int32_t id = s_id[wv][q][tt];   // < 0: a bad id (one owner only)
-                    const uint64_t val = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
+                    a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                    a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
                                                      ok_c ? cid : 0);
-                    if (a.walk_order) {   // presorted: straight to the record's sorted place
-                        a.rec_val[a.rec_inv[at + tt]] = val;
-                    } else {
-                        a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
-                        a.rec_val[at + tt] = val;
-                    }
                 }
             }
             filled += c0 + c1 + c2 + c3;
@@ -629,13 +620,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 const int tt = gl + 16 * k;
                 if (tt < T) {
                     const int32_t id = s_id[wv][q][tt];
-                    const uint64_t val = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
-                    if (a.walk_order) {   // presorted: the value straight to its sorted place
-                        a.rec_val[a.rec_inv[b * T + tt]] = val;
-                    } else {
-                        a.rec_key[b * T + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
-                        a.rec_val[b * T + tt] = val;
-                    }
+                    a.rec_key[b * T + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                    a.rec_val[b * T + tt] = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
                 }
             }
         }
@@ -895,37 +881,18 @@ using SmallSortConfig = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     128 * 1024>;
 constexpr uint32_t SMALL_SORT_MAX = 4u << 20;
-// dw_sgns_owner_presort's sort (the reference's 64-walk batch: 269K records, 21-bit rows), which
-// runs beside the memory-bound catch-up: 11-bit digits on 4K-item tiles, two passes (and two
-// lookback resets) instead of three; alone on the chip 62 us against 65 for SmallSortConfig
-// and 126 for 11-bit digits on 2K-item tiles (scripts/microbench/small_sort_bench.hip).
-using PresortConfig = rocprim::radix_sort_config<
+// Small sorts of more than 16 key bits (C3's 64-walk batch: 269K records on 20-bit rows): 11-bit
+// digits on 4K-item tiles — two passes and two lookback resets instead of SmallSortConfig's
+// three 8-bit passes: 0.499 vs 0.509 ms per step, twice each (profiles/r03_sort_small11_ab.txt);
+// 62 us alone on the chip against 65 for SmallSortConfig and 126 for 11-bit digits on 2K-item
+// tiles (scripts/microbench/small_sort_bench.hip). At 1,024 walks (4.3M records) the 4K tiles
+// measured slower than RecordSortConfig (1.82 vs 1.73 ms per step), hence SMALL_SORT_MAX.
+using Small11SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 4>,
                                         rocprim::kernel_config<1024, 4>, 11,
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
-
-// Small sorts of more than 16 key bits (C3's 64-walk batch: 269K records on 20-bit rows) run on
-// PresortConfig — two 11-bit passes and two lookback resets instead of SmallSortConfig's three
-// 8-bit passes: 0.499 vs 0.509 ms per step, twice each (profiles/r03_sort_small11_ab.txt).
-// DW_SORT_SMALL11=0 restores the 8-bit passes.
-// DW_SORT_SMALL11_MAX (an A/B knob): the record count below which that holds (SMALL_SORT_MAX).
-uint32_t small11_max() {
-    static const uint32_t m = [] {
-        const char *e = std::getenv("DW_SORT_SMALL11_MAX");
-        return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : SMALL_SORT_MAX;
-    }();
-    return m;
-}
-
-bool small_sort_11() {
-    static const bool on = [] {
-        const char *e = std::getenv("DW_SORT_SMALL11");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 // Stable LSD sort of (key, value) pairs on bits [0, end_bit), the config chosen by size. With
 // tmp == nullptr: *bytes = the largest of the configs' needs for n (so any n' <= n fits).
@@ -939,38 +906,17 @@ hipError_t sort_pairs(void *tmp, size_t &bytes, rocprim::double_buffer<K> &kb,
         if (e == hipSuccess)
             e = rocprim::radix_sort_pairs<SmallSortConfig>(nullptr, b, kb, vb, n, 0, end_bit, st);
         if (e == hipSuccess)
-            e = rocprim::radix_sort_pairs<PresortConfig>(nullptr, c, kb, vb, n, 0, end_bit, st);
+            e = rocprim::radix_sort_pairs<Small11SortConfig>(nullptr, c, kb, vb, n, 0, end_bit,
+                                                             st);
         bytes = a > b ? a : b;
         bytes = bytes > c ? bytes : c;
         return e;
     }
-    if (n < small11_max() && end_bit > 16 && small_sort_11())
-        return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
+    if (n < SMALL_SORT_MAX && end_bit > 16)
+        return rocprim::radix_sort_pairs<Small11SortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     if (n < SMALL_SORT_MAX)
         return rocprim::radix_sort_pairs<SmallSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
     return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, kb, vb, n, 0, end_bit, st);
-}
-
-// The same stable sort with separate output arrays (the result lands in k_out / v_out whatever
-// the pass count; the alternate buffers live in tmp). With tmp == nullptr: *bytes.
-hipError_t sort_pairs_to(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out,
-                         const uint32_t *v_in, uint32_t *v_out, uint32_t n, int end_bit,
-                         hipStream_t st) {
-    if (tmp == nullptr) {
-        size_t a = 0, b = 0;
-        hipError_t e = rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, a, k_in, k_out, v_in,
-                                                                   v_out, n, 0, end_bit, st);
-        if (e == hipSuccess)
-            e = rocprim::radix_sort_pairs<PresortConfig>(nullptr, b, k_in, k_out, v_in, v_out, n,
-                                                         0, end_bit, st);
-        bytes = a > b ? a : b;
-        return e;
-    }
-    if (n < SMALL_SORT_MAX)
-        return rocprim::radix_sort_pairs<PresortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n,
-                                                        0, end_bit, st);
-    return rocprim::radix_sort_pairs<RecordSortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, n, 0,
-                                                       end_bit, st);
 }
 
 int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStream_t st) {
@@ -979,12 +925,6 @@ int plan_workspace(int64_t n_rec, int64_t V, void *base, Workspace *ws, hipStrea
     rocprim::double_buffer<uint64_t> vb(nullptr, nullptr);
     hipError_t e = sort_pairs(nullptr, cub_bytes, kb, vb, static_cast<uint32_t>(n_rec),
                               end_bit_for(V), st);
-    if (e == hipSuccess) {   // dw_sgns_owner_presort's sort (separate outputs) shares the space
-        size_t pb = 0;
-        e = sort_pairs_to(nullptr, pb, nullptr, nullptr, nullptr, nullptr,
-                          static_cast<uint32_t>(n_rec), end_bit_for(V), st);
-        if (pb > cub_bytes) cub_bytes = pb;
-    }
     if (e != hipSuccess) {
         dw::set_error("dw_sgns: sort size query failed: %s", hipGetErrorString(e));
         return DW_E_HIP;
@@ -1301,18 +1241,14 @@ PhaseTimer g_timer;
 // the output-table phase runs (ShardedTables.exchange_in).
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st, const OutAdam *oa, bool presorted);
+                     hipStream_t st, const OutAdam *oa);
 
-// phase: 0 = both passes, 1 = pass 1, 2 = the output-table phase; | 4 = the records were
-// presorted (dw_sgns_walks_presort): pass 1 writes values only, phase 2 does not sort
+// phase: 0 = both passes, 1 = pass 1, 2 = the output-table phase
 template <bool FROM_WALKS>
 int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, hipStream_t st,
                 const OutAdam *oa = nullptr) {
-    const bool presorted = (phase & 4) != 0;
-    phase &= 3;
     if (phase != 2) g_timer.mark(0, st);
-    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st, oa,
-                                                presorted);
+    const int rc = launch_sgns_impl<FROM_WALKS>(a, workspace, workspace_bytes, phase, st, oa);
     if (rc != DW_OK) {
         if (g_timer.active()) g_timer.on = false;  // a failed call leaves its slots unusable
         return rc;
@@ -1323,10 +1259,8 @@ int launch_sgns(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase, 
 
 template <bool FROM_WALKS>
 int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int phase,
-                     hipStream_t st, const OutAdam *oa, bool presorted) {
+                     hipStream_t st, const OutAdam *oa) {
     const bool do1 = phase != 2, do2 = phase != 1;
-    DW_REQUIRE(!presorted || (FROM_WALKS && phase != 0 && workspace),
-               "dw_sgns: presorted records need the walks, a phase split and the workspace");
     if (a.batch == 0 && do2 && oa) {  // no records: every out row gets Adam with g = g_out
         if (do1) g_timer.mark(1, st);
         g_timer.mark(2, st);
@@ -1355,21 +1289,12 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     if (do1) {
         a.rec_key = ws.k0;
         a.rec_val = ws.v0;
-        if (presorted) {   // dw_sgns_walks_presort's layout: values to v1 through the inverse
-            a.walk_order = true;
-            a.rec_val = ws.v1;
-            a.rec_inv = reinterpret_cast<const uint32_t *>(ws.v0) + n_rec;
-        }
         rc = launch_pass1_g16<FROM_WALKS>(a, st);
-        if (rc == DW_E_UNSUPPORTED && !presorted) rc = launch_pass1<FROM_WALKS, true>(a, st);
+        if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
         if (rc != DW_OK) return rc;
         g_timer.mark(1, st);
     }
     if (!do2) return DW_OK;
-    if (presorted) {
-        g_timer.mark(2, st);
-        return launch_pass2(ws.k0, ws.v1, n_rec, a.w_in, a.g_out, a.d, oa, a.V, st);
-    }
     rocprim::double_buffer<uint32_t> kb(ws.k0, ws.k1);
     rocprim::double_buffer<uint64_t> vb(ws.v0, ws.v1);
     size_t cub_bytes = ws.cub_bytes;
@@ -1765,10 +1690,6 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     // n_owners > 1: per-wave regions in (k0, v0), compacted into (k1, v1); one owner keeps
     // every slot, so the regions tile (k1, v1) densely and pass 1 writes there directly
     const bool dense = a.n_owners == 1;
-    const bool presorted = (order_ready & 2) != 0;   // dw_sgns_owner_presort ran: values only
-    DW_REQUIRE(!presorted || dense, "dw_sgns_owner_pass1: presorted records need one owner");
-    a.walk_order = presorted;
-    a.rec_inv = reinterpret_cast<const uint32_t *>(ws.v0) + a.batch * T;   // presort's inverse
     a.rec_key = dense ? ws.k1 : ws.k0;
     a.rec_val = dense ? ws.v1 : ws.v0;
     a.count_out = dense ? ws.count : nullptr;
@@ -1803,25 +1724,13 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
 
 int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
                        const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
-                       size_t workspace_bytes, int64_t *n_records, hipStream_t st,
-                       bool presorted = false, hipEvent_t sorted_event = nullptr) {
+                       size_t workspace_bytes, int64_t *n_records, hipStream_t st) {
     Workspace ws;
     OwnerLayout lay;
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
                              "dw_sgns_owner_pass2");
     if (rc != DW_OK) return rc;
     const int64_t bound = n_centres * T;
-    if (presorted) {   // dw_sgns_owner_presort's order + pass 1's walk-order values: no sort here
-        DW_REQUIRE(oa && !n_records, "dw_sgns_owner_pass2_lazy: presorted needs n_records NULL");
-        g_timer.mark(2, st);
-        if (sorted_event && hipEventRecord(sorted_event, st) != hipSuccess) {
-            dw::set_error("dw_sgns_owner_pass2: recording the sorted event failed");
-            return DW_E_HIP;
-        }
-        if (bound > 0) rc = launch_pass2(ws.k0, ws.v1, bound, w_in, g_out, d, oa, local_rows, st);
-        g_timer.mark(3, st);
-        return rc;
-    }
     const int64_t *range = nullptr;
     int64_t n_rec = bound;
     if (n_records) {
@@ -1859,11 +1768,6 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
         vals = vb.current();
     }
     g_timer.mark(2, st);
-    // the records are sorted: work waiting on this event runs beside the gather
-    if (sorted_event && hipEventRecord(sorted_event, st) != hipSuccess) {
-        dw::set_error("dw_sgns_owner_pass2: recording the sorted event failed");
-        return DW_E_HIP;
-    }
     if (n_rec > 0 || oa) {
         rc = launch_pass2(keys, vals, n_rec, w_in, g_out, d, oa, local_rows, st, range);
         if (rc != DW_OK) return rc;
@@ -2023,9 +1927,7 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // claimed by exactly one lane in the launch — atomicMax(claim[row], step) returning < step — and
 // the wave appends its claimed rows to `list` with one counter atomic. dw_adam_rows then
 // replays the listed rows, all in parallel. A row the previous step claimed (old == step - 1) is
-// not listed: that step's lazy gather brings it to step - 1 itself. So the listed rows are
-// disjoint from the previous step's, and this claim and catch-up may run beside that step's
-// output-table phase (OwnerLazyTables.catch_up_out_ahead).
+// not listed: that step's records held it, so its lazy gather already brought it to step - 1.
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
@@ -2068,41 +1970,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         __syncthreads();   // s_cnt / s_base are rewritten next trip
     }
 }
-
-// dw_sgns_owner_presort (one owner): every slot's row keyed at its walk-order position b * T + t
-// (the rows k_out_claim and pass 1 compute: contexts from the walk, negatives from Philox), with
-// that position as the value. Sorted before pass 1, on a side stream beside the out rows'
-// catch-up, the records' order is ready when pass 1 has written their coefficients.
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_presort_keys(SgnsArgs a, uint32_t *__restrict__ keys, uint32_t *__restrict__ pos) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
-    const int T = a.C * (1 + a.K);
-    const int64_t per = a.L - 2 * a.R;
-    for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; b < a.batch;
-         b += n_waves) {
-        if (lane >= T) continue;
-        const int64_t w = b / per, i = a.R + b % per;
-        const int32_t c = a.walks[w * a.L + i];
-        int64_t o = 0;   // a bad centre or row: a zero record on row 0, as pass 1 writes it
-        if (c >= 0 && c < a.V) {
-            o = row_id<true>(a, b, a.walks + w * a.L, i, lane);
-            if (o < 0 || o >= a.V) o = 0;
-        }
-        keys[b * T + lane] = static_cast<uint32_t>(o);
-        pos[b * T + lane] = static_cast<uint32_t>(b * T + lane);
-    }
-}
-
-// inv[pos[i]] = i: each walk-slot position's place in the sorted order (pass 1 writes there)
-__global__ void __launch_bounds__(256)
-    k_presort_inverse(const uint32_t *__restrict__ pos, int64_t n, uint32_t *__restrict__ inv) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        inv[pos[i]] = static_cast<uint32_t>(i);
-}
-
-int presort_impl(const SgnsArgs &a, const Workspace &ws, int64_t vocab_size, hipStream_t st);
 
 }  // namespace
 
@@ -2159,106 +2026,6 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                         n_max, nullptr, hist, step - 1, stream);
 }
 
-int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
-                          int32_t *status, void *workspace, size_t workspace_bytes,
-                          void *stream) {
-    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
-                   vocab_size >= 1 && neg_samples >= 0,
-               "dw_sgns_owner_presort: bad sizes");
-    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= WAVE,
-               "dw_sgns_owner_presort: 2R(1+K) must be <= 64");
-    if (n_walks == 0) return DW_OK;
-    DW_REQUIRE(walks && status && workspace, "dw_sgns_owner_presort: null pointer");
-    hipStream_t st = dw::as_stream(stream);
-    SgnsArgs a = base_args(vocab_size, 64, neg_samples, nullptr, nullptr, nullptr, nullptr, noise,
-                           seed, noise_offset, 0.f, nullptr, status);
-    a.walks = walks;
-    a.L = walk_length;
-    a.R = context_radius;
-    a.batch = n_walks * (walk_length - 2 * context_radius);
-    a.C = 2 * context_radius;
-    const int64_t T = (int64_t)a.C * (1 + neg_samples);
-    Workspace ws;
-    OwnerLayout lay;
-    int rc = owner_workspace(a.batch, T, vocab_size, workspace, workspace_bytes, &ws, &lay, st,
-                             "dw_sgns_owner_presort");
-    if (rc != DW_OK) return rc;
-    return presort_impl(a, ws, vocab_size, st);
-}
-
-int dw_sgns_walks_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
-                          int32_t *status, void *workspace, size_t workspace_bytes,
-                          void *stream) {
-    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
-                   vocab_size >= 1 && neg_samples >= 0,
-               "dw_sgns_walks_presort: bad sizes");
-    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= WAVE,
-               "dw_sgns_walks_presort: 2R(1+K) must be <= 64");
-    if (n_walks == 0) return DW_OK;
-    DW_REQUIRE(walks && status && workspace, "dw_sgns_walks_presort: null pointer");
-    hipStream_t st = dw::as_stream(stream);
-    SgnsArgs a = base_args(vocab_size, 64, neg_samples, nullptr, nullptr, nullptr, nullptr, noise,
-                           seed, noise_offset, 0.f, nullptr, status);
-    a.walks = walks;
-    a.L = walk_length;
-    a.R = context_radius;
-    a.batch = n_walks * (walk_length - 2 * context_radius);
-    a.C = 2 * context_radius;
-    const int64_t n_rec = a.batch * (int64_t)a.C * (1 + neg_samples);
-    DW_REQUIRE(n_rec < 0x7FFFFFFF, "dw_sgns_walks_presort: too many records");
-    Workspace ws;   // dw_sgns_walks_phase's layout
-    int rc = plan_workspace(n_rec, vocab_size, workspace, &ws, st);
-    if (rc != DW_OK) return rc;
-    DW_REQUIRE(workspace_bytes >= ws.total, "dw_sgns_walks_presort: workspace too small");
-    return presort_impl(a, ws, vocab_size, st);
-}
-
-}  // extern "C"
-
-namespace {
-// The records' order for a batch ahead of pass 1 (dw_sgns_owner_presort / dw_sgns_walks_presort)
-int presort_impl(const SgnsArgs &a, const Workspace &ws, int64_t vocab_size, hipStream_t st) {
-    const int64_t T = (int64_t)a.C * (1 + a.K);
-    const int64_t n = a.batch * T;
-    DW_REQUIRE(n < (int64_t(1) << 32), "dw_sgns_owner_presort: too many records");
-    // keys (k1) and walk-slot positions (the second half of v0) in, the sorted keys to k0 and the
-    // sorted positions to the first half of v0 (fixed places: a sort with separate outputs), then
-    // the inverse over the input positions: pass 1 writes each value to v1 at its sorted place
-    uint32_t *p_sorted = reinterpret_cast<uint32_t *>(ws.v0), *p_in = p_sorted + n;
-    int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    if (blocks > grid_cap(8)) blocks = grid_cap(8);
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_presort_keys, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, ws.k1, p_in);
-    DW_LAUNCH_CHECK("dw_sgns_owner_presort/keys");
-    size_t need = 0;
-    if (sort_pairs_to(nullptr, need, ws.k1, ws.k0, p_in, p_sorted, static_cast<uint32_t>(n),
-                      end_bit_for(vocab_size), st) != hipSuccess ||
-        need > ws.cub_bytes) {
-        dw::set_error("dw_sgns_owner_presort: sort workspace too small");
-        return DW_E_HIP;
-    }
-    size_t cb = ws.cub_bytes;
-    hipError_t e = sort_pairs_to(ws.cub, cb, ws.k1, ws.k0, p_in, p_sorted,
-                                 static_cast<uint32_t>(n), end_bit_for(vocab_size), st);
-    if (e != hipSuccess) {
-        dw::set_error("dw_sgns_owner_presort: sort failed: %s", hipGetErrorString(e));
-        return DW_E_HIP;
-    }
-    int64_t ib = (n + 255) / 256;
-    if (ib > grid_cap(4)) ib = grid_cap(4);
-    hipLaunchKernelGGL(k_presort_inverse, dim3((unsigned)ib), dim3(256), 0, st, p_sorted, n, p_in);
-    DW_LAUNCH_CHECK("dw_sgns_owner_presort/inverse");
-    return DW_OK;
-}
-}  // namespace
-
-extern "C" {
-
 int dw_sgns_timing(int32_t enable) {
     g_timer.on = enable != 0;
     if (enable) g_timer.calls = 0;
@@ -2308,8 +2075,7 @@ int sgns_walks(int phase, const int32_t *walks, int64_t n_walks, int32_t walk_le
                const int64_t *noise, uint64_t seed, uint64_t noise_offset, float grad_scale,
                double *loss_acc, int32_t *status, void *workspace, size_t workspace_bytes,
                void *stream) {
-    DW_REQUIRE((phase & 3) <= 2 && (phase & ~7) == 0 && phase != 4,
-               "dw_sgns_walks_phase: phase must be 0, 1 or 2 (| 4: presorted)");
+    DW_REQUIRE(phase >= 0 && phase <= 2, "dw_sgns_walks_phase: phase must be 0, 1 or 2");
     DW_REQUIRE(context_radius >= 1, "dw_sgns_walks: context_radius must be >= 1");
     DW_REQUIRE(walk_length >= 2 * context_radius + 1,
                "dw_sgns_walks: walk_length %d < 2R+1 (Text is too short!)", walk_length);
@@ -2344,8 +2110,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                               float *m_out, float *v_out, uint8_t *row_flags,
                               float one_minus_beta1, float beta2, float one_minus_beta2,
                               float bias_correction2_sqrt, float neg_step_size, float eps,
-                              float weight_decay, int32_t presorted, int32_t *status,
-                              void *workspace, size_t workspace_bytes, void *stream) {
+                              float weight_decay, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream) {
     DW_REQUIRE(workspace && m_out && v_out && row_flags && w_out && g_out,
                "dw_sgns_walks_phase2_adam: needs the records workspace and the Adam state");
     DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_sgns_walks_phase2_adam: bad Adam scalars");
@@ -2364,8 +2130,7 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
                                neg_step_size, eps, weight_decay}};
     oa.dyn = dw::bound_step_scalars();
-    return launch_sgns<true>(a, workspace, workspace_bytes, presorted ? (2 | 4) : 2,
-                             dw::as_stream(stream), &oa);
+    return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
 }
 
 int dw_sgns_walks_phase2_piece(int32_t piece, int32_t n_pieces, int64_t piece_rows,
@@ -2496,9 +2261,8 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t presorted, int32_t *status,
-                             void *workspace, size_t workspace_bytes, int64_t *n_records,
-                             void *sorted_event, void *stream) {
+                             int32_t step, int32_t *status, void *workspace,
+                             size_t workspace_bytes, int64_t *n_records, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
                "dw_sgns_owner_pass2_lazy: bad sizes");
@@ -2511,8 +2275,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
-                              dw::as_stream(stream), presorted != 0,
-                              static_cast<hipEvent_t>(sorted_event));
+                              dw::as_stream(stream));
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

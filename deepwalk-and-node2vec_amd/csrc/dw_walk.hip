@@ -550,7 +550,9 @@ __device__ int64_t n2v_pick_positions(const int32_t *__restrict__ col,
         if (j < m) {
             const int32_t y = col[rt.a + j];
             ++loads;
-            ps = static_cast<int32_t>(lane_position(col, tab, hpos, rv, y, probes));
+            // t in N(t) (a self-loop at t): x == t is the 1/p class (counted by pos_t below),
+            // never a common neighbour (random_walk_generator.py:102-104 tests x == prev first)
+            if (y != t) ps = static_cast<int32_t>(lane_position(col, tab, hpos, rv, y, probes));
             pos[j] = ps;
         }
         C += __popcll(__ballot(ps >= 0));
@@ -909,10 +911,6 @@ __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
     // the NCAP-entry N(prev) stage; the ballots take both halves when nothing is staged
     __shared__ uint64_t s_lds[REPLAY_WAVES][CH + NCAP / 2];
     __shared__ int64_t s_pick[REPLAY_WAVES];
-#ifdef DW_REPLAY_PAD_LDS   // occupancy experiments only
-    __shared__ int32_t s_pad[DW_REPLAY_PAD_LDS];
-    if (threadIdx.x == 0) s_pad[0] = 0;
-#endif
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     double *buf = reinterpret_cast<double *>(s_lds[wv]);
@@ -1760,12 +1758,9 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,
                       reinterpret_cast<unsigned long long *>(counters), hub_idx, hub_bits,
                       hub_words, edge_cn};
-    // DW_N2V_CN_KERNEL=0: the counts through the general kernel (round 3's first form; A/B)
-    static const bool cn_kernel = [] {
-        const char *e = getenv("DW_N2V_CN_KERNEL");
-        return !(e && e[0] == '0');
-    }();
-    if (edge_cn && cn_kernel)
+    // with the counts: their own kernel (no class-mask cache: 11.25 ms against 13.45 ms through
+    // the general kernel for 65,536 C3 walks; profiles/r03_replay_rates.jsonl)
+    if (edge_cn)
         hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
                            dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,

@@ -30,11 +30,12 @@ DW_S_REJECTION_CAP = 4
 DW_S_BAD_CSR = 8
 DW_S_BAD_INDEX = 16
 DW_S_RECORDS_FULL = 32
+DW_S_DUP_NEIGHBOR = 64
 
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -58,6 +59,7 @@ SIGNATURES = {
     'dw_mt_workspace_words': (ctypes.c_int64, [_i64]),
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
+    'dw_csr_check_simple': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_adj_hash_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),
     'dw_adj_hash_build': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _p, _p]),
     'dw_alias_build': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
@@ -98,15 +100,11 @@ SIGNATURES = {
                                                   _i32, _i64, _p, _u64, _u64, _p, _p, _p, _p, _p,
                                                   _p, _p, _p, _i32, _p, _p]),
     'dw_sgns_owner_pass2_lazy': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p,
-                                                _p, _p, _p, _p, _i32, _i32, _p, _p,
-                                                ctypes.c_size_t, _p, _p, _p]),
-    'dw_sgns_owner_presort': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _p, _u64, _u64, _p,
-                                             _p, ctypes.c_size_t, _p]),
+                                                _p, _p, _p, _p, _i32, _p, _p, ctypes.c_size_t,
+                                                _p, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
-                                                 _f32, _f32, _i32, _p, _p, ctypes.c_size_t, _p]),
-    'dw_sgns_walks_presort': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _p, _u64, _u64, _p,
-                                             _p, ctypes.c_size_t, _p]),
+                                                 _f32, _f32, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_pairs': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),
     'dw_sgns_workspace_bytes': (ctypes.c_int, [_i64, _i32, _i32, _i64, _szp]),
@@ -244,4 +242,7 @@ def check_status(status: torch.Tensor, what: str) -> None:
         raise IndexError(f'{what}: index out of range [0, vocab_size)')
     if s & DW_S_RECORDS_FULL:
         raise RuntimeError(f'{what}: SGNS records exceeded the workspace')
+    if s & DW_S_DUP_NEIGHBOR:
+        raise ValueError(f'{what}: a CSR row lists the same neighbour twice (the reference\'s '
+                         f'networkx.Graph cannot hold a repeated edge)')
     raise RuntimeError(f'{what}: device status {s:#x}')

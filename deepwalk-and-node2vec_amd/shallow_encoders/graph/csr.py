@@ -325,7 +325,23 @@ class CSRGraph:
                          self.vocab_size, self.nnz, _native.ptr(out), _native.ptr(tmp),
                          ctypes.byref(nbytes), s)
             del tmp
+            # a repeated neighbour in a row (checked once, read by require_simple)
+            d['simple_status'] = torch.zeros(1, dtype=torch.int32, device=dev)
+            _native.call('dw_csr_check_simple', _native.ptr(d['row_ptr']), _native.ptr(out),
+                         self.vocab_size, self.nnz, _native.ptr(d['simple_status']), s)
         return out[:self.nnz] if self.nnz else out
+
+    def require_simple(self, device=None) -> None:
+        """Raise ValueError when a row lists the same neighbour twice. The reference walks a
+        ``networkx.Graph``, which keeps one entry per neighbour (random_walk_generator.py:41-42);
+        the bit-exact node2vec replay relies on that (one position of prev in N(v), class counts
+        by intersection), so it refuses such a CSR instead of walking it differently
+        (dw_csr_check_simple over col_sorted; one synchronisation per graph and device)."""
+        d = self.device_tensors(device, need_sorted=True)
+        if d.get('simple_ok'):
+            return
+        _native.check_status(d['simple_status'], 'CSR check (node2vec replay)')
+        d['simple_ok'] = True
 
     def _build_alias(self, dev) -> None:
         d = self._dev

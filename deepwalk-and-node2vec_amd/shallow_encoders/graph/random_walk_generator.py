@@ -225,6 +225,8 @@ class RandomWalk(ABC):
                                      need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx,
                                      need_hub_bits=replay_n2v_idx,
                                      need_edge_cn=replay_n2v_idx and _edge_cn_enabled())
+        if self._rng == 'python' and n2v:
+            self._csr.require_simple(dev)   # no repeated neighbour (nx.Graph's invariant)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         if status is None:
@@ -309,6 +311,7 @@ class RandomWalk(ABC):
             raise ValueError('uniforms must have n_walks * (length - 1) values')
         d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True,
                                      need_hub_bits=True, need_edge_cn=_edge_cn_enabled())
+        self._csr.require_simple(dev)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)

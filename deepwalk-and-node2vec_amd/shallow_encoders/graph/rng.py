@@ -67,7 +67,7 @@ def shuffled_range(n: int, rng: random.Random = None) -> np.ndarray:
 
 # ---- the same stream generated on the device (dw_mt_uniforms) ---------------------------------
 _MT_TABLES = {}          # (device, window_stride) -> (positions int16, offsets int64, n_chains)
-_MT_WS = {}              # device -> int32 workspace of the chains' jump windows
+_MT_WS = {}              # (device, stream) -> int32 workspace of the chains' jump windows
 _MT_LOCK = threading.Lock()
 MIN_CHAIN_WINDOWS = 256  # below this many 624-word windows per chain, one chain (no jump) wins
 CHAINS_PER_CU = 2        # chains the generation spreads over, per compute unit
@@ -84,14 +84,18 @@ def mt_window_stride(n: int, index: int, n_cu: int) -> int:
 
 
 def mt_workspace(device: torch.device, n_chains: int) -> torch.Tensor:
-    """Device scratch of dw_mt_uniforms (the chains' jump windows), cached and grown."""
+    """Device scratch of dw_mt_uniforms (the chains' jump windows), cached and grown per
+    (device, stream): two generations enqueued on different streams (or from different host
+    threads on their own streams) never share one, so their jump windows cannot overwrite each
+    other. Within one stream the launches are ordered, so reuse is safe."""
     from shallow_encoders import _native
     words = int(_native.load().dw_mt_workspace_words(int(n_chains)))
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
     with _MT_LOCK:
-        ws = _MT_WS.get(device)
+        ws = _MT_WS.get(key)
         if ws is None or ws.numel() < words:
             ws = torch.empty(max(words, 1), dtype=torch.int32, device=device)
-            _MT_WS[device] = ws
+            _MT_WS[key] = ws
         return ws
 
 

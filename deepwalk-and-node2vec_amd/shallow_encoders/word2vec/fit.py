@@ -120,8 +120,14 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
 
     Device walk batches with a Philox walker and device negatives (``noise: device``) are
     replayed ``graph_unroll`` steps per HIP graph after each epoch's first (eager) batch
-    (GraphedTrainerStep): the same steps, kernels and results, without a Python launch per
-    kernel. The trailing batches that do not fill a graph, and everything else, run eagerly."""
+    (GraphedTrainerStep), without a Python launch per kernel. The trailing batches that do not
+    fill a graph, and everything else, run eagerly. The replayed steps train the same batches with
+    the same update, but with DW_TRAIN_GRAPH_SCATTER='auto' (the default) a batch of at most
+    65,536 output records (the reference configs' 64-walk batches) takes the atomic output-table
+    scatter and one Adam launch over both tables, where the eager step sorts the records and
+    fuses the out table's Adam into their gather: the same sums in another float order, so the
+    tables agree to float-atomic rounding, not bit for bit. 'records' replays the eager step's
+    own kernels."""
     from shallow_encoders.word2vec.graphed import GraphedTrainerStep
     trainer.manual_grads = True
     opt = trainer.optimizer

@@ -274,24 +274,9 @@ class GraphedOwnerStep:
             # the step numbers the lazy kernels get are relative to block k's (begin_step, inside
             # owner_lazy_step, makes the host's count step_count + 1)
             _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count + 1)
-            ahead = None
-            if k + 1 < self.unroll and t.out_ahead:
-                ahead = self._ahead_fn(k)
             owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
                             noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
-                            status=self.status, ahead=ahead)
-
-    def _ahead_fn(self, k: int):
-        """Once step k's pass 2 is enqueued: step k + 1's out-row claim and catch-up, bound to
-        block k + 1 (its step number and negatives), beside step k's lazy gather."""
-        t, B = self.t, self.B
-
-        def ahead() -> None:
-            _native.call('dw_step_scalars_bind_at', self._step_blk(k + 1), t.step_count + 1)
-            t.catch_up_out_ahead(self.walks[(k + 1) * B:(k + 2) * B], self.R, self.K, self.seed,
-                                 0, self.status)
-            _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count)
-        return ahead
+                            status=self.status)
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host

@@ -75,8 +75,7 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                     seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                     loss_acc: Optional[torch.Tensor] = None,
                     status: Optional[torch.Tensor] = None, scatter: str = 'sorted',
-                    phase: int = 0, out_adam: Optional[dict] = None,
-                    presorted: bool = False) -> torch.Tensor:
+                    phase: int = 0, out_adam: Optional[dict] = None) -> torch.Tensor:
     """Launch the fused SGNS kernel(s); returns the float64[4] loss accumulator.
 
     Either ``walks`` (int32 [n, L]) + ``context_radius``, or ``inputs`` (int64 [B] or [B, 1];
@@ -89,8 +88,6 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
     ``out_adam`` (phase 2, records path, one device): ``{'m', 'v', 'flags', 'scalars'}`` — the
     output table's Adam step is fused into the phase (w_out updated in place, g_out left zero;
     ShardedTables.out_adam_spec()).
-    ``presorted`` (walks, phases 1 and 2, records path): sgns_walks_presort ran for this batch —
-    pass 1 writes only the values, each at its sorted place, and phase 2 does not sort.
     """
     dev = w_in.device
     V, d = w_in.shape
@@ -128,13 +125,9 @@ def sgns_accumulate(w_in: torch.Tensor, w_out: torch.Tensor, g_in: torch.Tensor,
                              _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_out),
                              _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                              _native.ptr(out_adam['flags']), *out_adam['scalars'],
-                             1 if presorted else 0, _native.ptr(status), _native.ptr(ws),
-                             ws.numel(), s)
+                             _native.ptr(status), _native.ptr(ws), ws.numel(), s)
                 return loss_acc
-            if presorted and (phase == 0 or ws is None):
-                raise ValueError('presorted records need the records path and a phase split')
-            _native.call('dw_sgns_walks_phase', int(phase) | (4 if presorted else 0),
-                         _native.ptr(walks), n, L, R, K, V, d,
+            _native.call('dw_sgns_walks_phase', int(phase), _native.ptr(walks), n, L, R, K, V, d,
                          _native.ptr(w_in), _native.ptr(w_out), _native.ptr(g_in),
                          _native.ptr(g_out), _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), float(scale), _native.ptr(loss_acc),
@@ -329,15 +322,13 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
-                     order_ready: bool = False, presorted: bool = False) -> torch.Tensor:
+                     order_ready: bool = False) -> torch.Tensor:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
     partial centre-table gradient of the owned slots; returns the float64[4] loss accumulator
     (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
-    ``order_ready``: sgns_owner_prepare already built the centre order for these walks;
-    ``presorted``: sgns_owner_presort already sorted these walks' records (one owner): pass 1
-    writes only their values, in walk-slot order."""
+    ``order_ready``: sgns_owner_prepare already built the centre order for these walks."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -364,58 +355,13 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
-                     int(owner), int(n_owners), local_rows,
-                     (1 if order_ready else 0) | (2 if presorted else 0),
+                     int(owner), int(n_owners), local_rows, 1 if order_ready else 0,
                      _native.ptr(w_in),
                      _native.ptr(w_out_local), _native.ptr(g_in), _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),
                      _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws), ws.numel(),
                      _native.stream(dev))
     return loss_acc
-
-
-def sgns_walks_presort(walks: torch.Tensor, context_radius: int, neg_samples: int,
-                       vocab_size: int, *, seed: int = 0, noise_offset: int = 0,
-                       noise: Optional[torch.Tensor] = None,
-                       status: Optional[torch.Tensor] = None) -> None:
-    """dw_sgns_walks_presort: the records' order for ``walks`` ahead of sgns_accumulate's
-    phases with ``presorted=True`` (the same workspace); independent of pass 1, so it can run
-    on a side stream beside it."""
-    dev = walks.device
-    if walks.dtype != torch.int32 or walks.dim() != 2:
-        raise TypeError('walks must be int32 [n_walks, L]')
-    n, L = walks.shape
-    R, K = int(context_radius), int(neg_samples)
-    if status is None:
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = workspace_for(n * (L - 2 * R), 2 * R, K, vocab_size, dev)
-    with torch.cuda.device(dev):
-        _native.call('dw_sgns_walks_presort', _native.ptr(walks), n, L, R, K, int(vocab_size),
-                     _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
-                     _native.ptr(status), _native.ptr(ws), ws.numel(), _native.stream(dev))
-
-
-def sgns_owner_presort(walks: torch.Tensor, context_radius: int, neg_samples: int,
-                       vocab_size: int, local_rows: int, *, seed: int = 0, noise_offset: int = 0,
-                       noise: Optional[torch.Tensor] = None,
-                       status: Optional[torch.Tensor] = None) -> None:
-    """dw_sgns_owner_presort (one owner): the records' order for ``walks`` (every slot's row —
-    contexts, and the negatives pass 1 will draw — sorted with its walk-slot position), before
-    pass 1, so that pass 1 (presorted=True) writes only the values and pass 2 (out_adam
-    'presorted') gathers without sorting. The same workspace as the passes."""
-    dev = walks.device
-    if walks.dtype != torch.int32 or walks.dim() != 2:
-        raise TypeError('walks must be int32 [n_walks, L]')
-    n, L = walks.shape
-    R, K = int(context_radius), int(neg_samples)
-    n_centres = n * (L - 2 * R)
-    if status is None:
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
-    with torch.cuda.device(dev):
-        _native.call('dw_sgns_owner_presort', _native.ptr(walks), n, L, R, K, int(vocab_size),
-                     _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset),
-                     _native.ptr(status), _native.ptr(ws), ws.numel(), _native.stream(dev))
 
 
 def sgns_owner_prepare(walks: torch.Tensor, context_radius: int, neg_samples: int,
@@ -473,9 +419,8 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(w_out_local), _native.ptr(g_out_local),
                          _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
-                         int(out_adam['step']), int(bool(out_adam.get('presorted', False))),
-                         _native.ptr(status), _native.ptr(ws), ws.numel(), n_rec_p,
-                         out_adam.get('sorted_event') or None, _native.stream(dev))
+                         int(out_adam['step']), _native.ptr(status), _native.ptr(ws),
+                         ws.numel(), n_rec_p, _native.stream(dev))
         return int(n_rec.value) if read_count else None
     if out_adam is not None:
         m, v, flags, sc = (_native.ptr(out_adam['m']), _native.ptr(out_adam['v']),

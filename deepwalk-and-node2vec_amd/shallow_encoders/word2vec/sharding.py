@@ -420,16 +420,6 @@ def replicated_step(tables: ShardedTables, walks: torch.Tensor, context_radius: 
               grad_scale=grad_scale, loss_acc=loss_acc, status=status, scatter=scatter)
     fuse = fuse_out_adam and scatter == 'sorted' and tables.can_fuse_out_adam()
     pb = sgns_phase_bytes(n, L, R, K, tables.d, tables.V, scatter, fuse)
-    # DW_PRESORT_STEP=1 (one GPU, records path; an A/B knob, off by default): the records'
-    # order sorted ahead of pass 1 (sgns_walks_presort), which then writes each value at its
-    # sorted place, so the output-table phase starts without a sort. Pass 1 needs the inverse
-    # map, so the sort cannot hide beside it; nothing else of this step runs before pass 1.
-    if (scatter == 'sorted' and not pieces and not tables.multi
-            and os.environ.get('DW_PRESORT_STEP', '0') == '1'):
-        from shallow_encoders.word2vec.sgns import sgns_walks_presort
-        sgns_walks_presort(walks, R, K, tables.V, seed=seed, noise_offset=noise_offset,
-                           status=status)
-        kw['presorted'] = True
     sgns_accumulate(tables.w_in, tables.w_out, tables.g_in, tables.g_out, K, phase=1, **kw)
     if after_pass1 is not None:
         after_pass1()
@@ -768,25 +758,6 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = bool(lazy_out)
         super().__init__(*args, **kwargs)
         self.lazy_out = self.lazy_out and self._hip()
-        # one rank, lazy out slice, DW_PRESORT=1: the records sorted before pass 1 on a side
-        # stream beside the out rows' catch-up (dw_sgns_owner_presort). Off by default: beside
-        # the catch-up's HBM traffic the sort's passes stretch 3-5x and the presort branch
-        # becomes the longest (C3 at 64 walks: 0.540 vs 0.500 ms per step)
-        self.presort = (self.lazy_out and not self.multi
-                        and os.environ.get('DW_PRESORT', '0') == '1')
-        self._presorted = False
-        self._side2 = None
-        # one rank, lazy out slice, DW_OUT_AHEAD=1: the next batch's out rows claimed and caught
-        # up beside this step's lazy gather (catch_up_out_ahead). Off by default: the two share
-        # the chip's throughput (C3 at 64 walks: 0.514 / 0.518 vs 0.507 ms per step, the gather
-        # stretched by the catch-up's length; forked after pass 1 instead, beside the sort too:
-        # 0.548 vs 0.512), and the in-table catch-up it used to hide is exposed
-        self.out_ahead = (self.lazy_out and not self.multi
-                          and os.environ.get('DW_OUT_AHEAD', '0') == '1')
-        self._ahead = None
-        self._side3 = None
-        self._sorted_ev = None      # recorded by pass 2 once its records are sorted
-        self._sorted_armed = False
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
@@ -816,48 +787,6 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist),
                          step, _native.ptr(status), _native.stream(self.device))
-
-    def sorted_event(self) -> Optional[int]:
-        """The hipEvent_t pass 2 records once its records are sorted (dw_sgns_owner_pass2_lazy's
-        sorted_event), for the next catch_up_out_ahead to start from; None where that does not
-        apply."""
-        if not self.out_ahead:
-            return None
-        if self._sorted_ev is None:
-            self._sorted_ev = torch.cuda.Event()
-        if not self._sorted_ev.cuda_event:   # torch creates the event at its first record
-            self._sorted_ev.record(torch.cuda.current_stream(self.device))
-        self._sorted_armed = True
-        return self._sorted_ev.cuda_event
-
-    def catch_up_out_ahead(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
-                           seed: int, noise_offset: int, status: torch.Tensor) -> bool:
-        """One rank, lazy_out, during step t (after its pass 2 was enqueued): the out-row claim
-        and catch-up of the NEXT batch ``walks`` (step t + 1), on a side stream that starts once
-        step t's records are sorted (sorted_event), beside its lazy gather. The claim leaves out
-        the rows step t claimed (that gather brings them to t), so the replayed rows are disjoint
-        from the ones step t's pass 2 writes. Step t + 1 must then train exactly ``walks``
-        (before_pass1 checks it). Returns False where it does not apply (several ranks, dense
-        out slice, DW_OUT_AHEAD=0)."""
-        if not self.out_ahead or self._ahead is not None:
-            return False
-        main = torch.cuda.current_stream(self.device)
-        if self._sorted_armed:
-            fork = self._sorted_ev
-            self._sorted_armed = False
-        else:
-            fork = torch.cuda.Event()
-            fork.record(main)
-        if self._side3 is None:
-            self._side3 = torch.cuda.Stream(self.device)
-        with torch.cuda.stream(self._side3):
-            self._side3.wait_event(fork)
-            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status,
-                              step=self.step_count + 1)
-            done = torch.cuda.Event()
-            done.record(self._side3)
-        self._ahead = ((walks.data_ptr(), tuple(walks.shape), self.step_count + 1), done)
-        return True
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -994,46 +923,22 @@ class OwnerLazyTables(OwnerTables):
         centre order and in-table catch-up (a one-block sort, then ALU-bound replays) run on
         the side stream beside the out rows' claim and catch-up (bandwidth-bound); the current
         stream waits for both."""
-        self._presorted = False
         if self.lazy_out and not self.multi:
-            # three branches from one fork: the out rows' claim + catch-up (the longest; enqueued
-            # first, so a captured graph launches it first), the centre order + in-table catch-up,
-            # and the records' presort
+            # two branches from one fork: the out rows' claim + catch-up (the longer; enqueued
+            # first, so a captured graph launches it first) and the centre order + in-table
+            # catch-up
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
-            joins = []
-            if self._ahead is not None:   # claimed and caught up during the previous step
-                key, done = self._ahead
-                self._ahead = None
-                if key != (walks.data_ptr(), tuple(walks.shape), self.step_count):
-                    raise RuntimeError('OwnerLazyTables: the out rows were caught up ahead for '
-                                       'another batch (catch_up_out_ahead) than this step trains')
-                joins.append(done)
-            else:
-                self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
                 self.prepare(walks, context_radius, neg_samples)
                 self.catch_up()
-                joins.append(torch.cuda.Event())
-                joins[-1].record(self._side)
-            if self.presort:
-                from shallow_encoders.word2vec.sgns import sgns_owner_presort
-                if self._side2 is None:
-                    self._side2 = torch.cuda.Stream(self.device)
-                with torch.cuda.stream(self._side2):
-                    self._side2.wait_event(fork)
-                    sgns_owner_presort(walks, context_radius, neg_samples, self.V, self.S,
-                                       seed=seed, noise_offset=noise_offset, status=status)
-                    joins.append(torch.cuda.Event())
-                    joins[-1].record(self._side2)
-                self._presorted = True
-            for j in joins:
-                main.wait_event(j)
+                join = torch.cuda.Event()
+                join.record(self._side)
+            main.wait_event(join)
             return
-        if self._ahead is not None:
-            raise RuntimeError('OwnerLazyTables: catch_up_out_ahead is one-rank only')
         self.prepare(walks, context_radius, neg_samples)
         self.catch_up()
         self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1084,9 +989,6 @@ class OwnerLazyTables(OwnerTables):
 
     def _flush_out(self) -> None:
         """lazy_out: every out-slice row up to the current step."""
-        if self._ahead is not None:
-            raise RuntimeError('OwnerLazyTables: a catch-up for the next batch is pending; run '
-                               'that step before reading the out table')
         if self.lazy_out and self.step_count > 0:
             hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
                           self.S, None, self._hist, self.step_count)
@@ -1095,7 +997,7 @@ class OwnerLazyTables(OwnerTables):
         spec = super().out_adam_spec()
         if spec is not None and self.lazy_out:
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                    'step': self.step_count, 'presorted': self._presorted}
+                    'step': self.step_count}
         return spec
 
     def full_w_out(self) -> torch.Tensor:
@@ -1115,28 +1017,21 @@ class OwnerLazyTables(OwnerTables):
 
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
                     neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
-                    loss_acc: torch.Tensor, status: torch.Tensor,
-                    ahead: Optional[Callable[[], None]] = None) -> int:
+                    loss_acc: torch.Tensor, status: torch.Tensor) -> int:
     """One owner-computes step with the touched-row in-table exchange (every rank passes the
-    same global batch). Returns this rank's record count. ``ahead``: a host callback run once
-    pass 2 is enqueued, with its sorted event armed (the next batch's catch_up_out_ahead)."""
+    same global batch). Returns this rank's record count."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
-                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
-                     presorted=tables._presorted)
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True)
     tables.exchange_touched()
     spec = tables.out_adam_spec()
-    if ahead is not None and spec is not None and getattr(tables, 'out_ahead', False):
-        spec['sorted_event'] = tables.sorted_event()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,
                          context_radius=context_radius, out_adam=spec, status=status,
                          read_count=tables.world > 1)
-    if ahead is not None:
-        ahead()
     if n is None:   # one owner keeps every slot (no count readback)
         n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
             1 + neg_samples)

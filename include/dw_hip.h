@@ -48,6 +48,7 @@ extern "C" {
 #define DW_S_BAD_CSR         8   /* row_ptr not monotone / col out of range                          */
 #define DW_S_BAD_INDEX      16   /* an index outside [0, V) reached the SGNS kernel                  */
 #define DW_S_RECORDS_FULL   32   /* owner-form SGNS records exceeded the workspace (not expected)    */
+#define DW_S_DUP_NEIGHBOR   64   /* a CSR row lists a neighbour twice (dw_csr_check_simple)          */
 
 #define DW_METHOD_DEEPWALK   0   /* random_walk_generator.py:56-72 ('deepwalk' and 'dfs')          */
 #define DW_METHOD_NODE2VEC   1   /* random_walk_generator.py:75-119                                  */
@@ -112,6 +113,14 @@ int dw_csr_validate(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, 
  * Two-phase temp-storage protocol: call with temp==NULL to get *temp_bytes, then again. */
 int dw_csr_sort_copy(const int64_t *row_ptr, const int32_t *col, int64_t n_rows, int64_t nnz,
                      int32_t *col_sorted, void *temp, size_t *temp_bytes, void *stream);
+
+/* Sets DW_S_DUP_NEIGHBOR in status when a row of col_sorted (dw_csr_sort_copy) holds two equal
+ * entries. The reference's networkx.Graph keeps one entry per neighbour
+ * (random_walk_generator.py:41-42 lists graph.neighbors(node)), and the bit-exact node2vec replay
+ * relies on it (one position of prev in N(v), class counts by intersection), so the host refuses a
+ * non-simple CSR there. */
+int dw_csr_check_simple(const int64_t *row_ptr, const int32_t *col_sorted, int64_t n_rows,
+                        int64_t nnz, int32_t *status, void *stream);
 
 /* Per-row adjacency hash for the fast node2vec walker's test `prev_node in
  * candidate_neighbors` (random_walk_generator.py:106-107): one probe of a 64-B bucket instead of
@@ -351,8 +360,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
                               float *m_out, float *v_out, uint8_t *row_flags,
                               float one_minus_beta1, float beta2, float one_minus_beta2,
                               float bias_correction2_sqrt, float neg_step_size, float eps,
-                              float weight_decay, int32_t presorted, int32_t *status,
-                              void *workspace, size_t workspace_bytes, void *stream);
+                              float weight_decay, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream);
 
 /* Owner-computes form of the walks SGNS step for N > 1 (ShardedTables(mode='owner'), bench.py).
  * The output ("context") table is sharded by row owner: rank `owner` of `n_owners` holds only
@@ -385,8 +394,7 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
  * uint32[n_walks*(L-2R)]) receives the batch's distinct centre nodes in increasing order and
  * *n_touched (device int64) their count — the rows a step reads and updates in the in table
  * (OwnerLazyTables). Same workspace as the pass-1 / pass-2 calls that follow.
- * dw_sgns_owner_pass1's order_ready is a bit set: 1 = this order is ready; 2 = the records
- * were presorted (dw_sgns_owner_presort, one owner). */
+ * dw_sgns_owner_pass1's order_ready: 1 = this order is ready (else pass 1 builds it). */
 int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           int64_t local_rows, uint32_t *touched, int64_t *n_touched,
@@ -428,38 +436,13 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * replayed (scalars hist[t], fp32 [steps][8] as for dw_adam_rows) right before its next update,
  * through the same adam_elem, so the slice equals the dense update bit for bit once flushed
  * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
- * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
- * sorted_event (a hipEvent_t, or NULL): recorded on the stream once the records are sorted,
- * before the gather (the next batch's out-row catch-up waits on it and runs beside the gather). */
+ * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t presorted, int32_t *status, void *workspace,
-                             size_t workspace_bytes, int64_t *n_records, void *sorted_event,
-                             void *stream);
-
-/* One owner, before dw_sgns_owner_pass1 of the same batch (pass 1's order_ready | 2, pass 2's
- * presorted = 1, n_records NULL): the records' order — every slot's row (contexts from the
- * walks, negatives as pass 1 draws them) sorted with its walk-slot position b * 2R(1+K) + t —
- * so pass 1 writes only the values, in that position, and pass 2 gathers without a sort. It
- * depends only on the walks and the negatives' stream, so it can run on a side stream beside
- * dw_sgns_owner_out_catch_up (the reference's 64-walk batch: the ~10 launches of a small sort
- * off the step's critical path). The same workspace as the passes. 2R(1+K) <= 64. */
-/* dw_sgns_owner_presort for the one-device walks path (dw_sgns_walks_phase's workspace): then
- * dw_sgns_walks_phase(1 | 4, ...) writes only the values, each at its sorted place, and
- * dw_sgns_walks_phase(2 | 4, ...) / dw_sgns_walks_phase2_adam(presorted = 1) gather without a
- * sort. Meant to run on a side stream beside pass 1 (which it does not depend on). */
-int dw_sgns_walks_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
-                          int32_t *status, void *workspace, size_t workspace_bytes,
-                          void *stream);
-int dw_sgns_owner_presort(const int32_t *walks, int64_t n_walks, int32_t walk_length,
-                          int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
-                          const int64_t *noise, uint64_t seed, uint64_t noise_offset,
-                          int32_t *status, void *workspace, size_t workspace_bytes,
-                          void *stream);
+                             int32_t step, int32_t *status, void *workspace,
+                             size_t workspace_bytes, int64_t *n_records, void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */

@@ -87,16 +87,12 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
         assert_no_row_drift(got, exp)
 
 
-@pytest.mark.parametrize('lazy_out,unroll,ahead', [(True, 1, False), (True, 4, False),
-                                                    (False, 3, False), (True, 4, True)])
-def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll, ahead, monkeypatch):
+@pytest.mark.parametrize('lazy_out,unroll', [(True, 1), (True, 4), (False, 3)])
+def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
     """The one-GPU lazy owner step (bench.py's path for the reference's 64-walk batch on a large
     graph) replayed as a HIP graph (GraphedOwnerStep: the lazy kernels' step numbers bound
     relative to the step blocks) equals the eager steps: the same walks, losses to float64-atomic
-    order, and both tables, flushed, to fp32 atomic-order noise. ahead: inside each graph, the
-    next step's out rows claimed and caught up beside the gather (DW_OUT_AHEAD=1, bound to the
-    next step's block)."""
-    monkeypatch.setenv('DW_OUT_AHEAD', '1' if ahead else '0')
+    order, and both tables, flushed, to fp32 atomic-order noise."""
     from shallow_encoders.word2vec.graphed import GraphedOwnerStep
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
     dev = hip_device

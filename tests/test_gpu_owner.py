@@ -348,11 +348,9 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d, wd):
 
 
 def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False,
-                   snaps=None, ahead=False):
+                   snaps=None):
     """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L];
-    ``snaps``: a list receiving _owner_snapshot after every step; ``ahead``: every step but
-    the last claims and catches up the next batch's out rows beside its gather
-    (catch_up_out_ahead)."""
+    ``snaps``: a list receiving _owner_snapshot after every step."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
     t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
     n, L = walks_all.shape[1:]
@@ -361,13 +359,8 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
     status = torch.zeros(1, dtype=torch.int32, device=device)
     dev_walks = [walks_all[s].to(device) for s in range(walks_all.shape[0])]
     for s in range(walks_all.shape[0]):
-        hook = None
-        if ahead and s + 1 < len(dev_walks):
-            def hook(s=s):
-                assert t.catch_up_out_ahead(dev_walks[s + 1], R, K, 11, (s + 1) * n * per, status)
         owner_lazy_step(t, dev_walks[s], R, K, seed=11, noise_offset=s * n * per,
-                        grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status,
-                        ahead=hook)
+                        grad_scale=1.0 / (n * per * 2 * R), loss_acc=acc, status=status)
         if snaps is not None:
             torch.cuda.synchronize()
             snaps.append(_owner_snapshot(t, V))
@@ -376,13 +369,11 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
     return t, acc
 
 
-@pytest.mark.parametrize('lazy_out,ahead', [(False, False), (True, False), (True, True)])
-def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead, monkeypatch):
+@pytest.mark.parametrize('lazy_out', [False, True])
+def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
     """One rank: sparse batches (most rows untouched for several steps) through the lazy
     protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush;
-    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary);
-    ahead: each next batch's out rows claimed and caught up beside the step before's output-table
-    phase (catch_up_out_ahead)."""
+    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary)."""
     from shallow_encoders.word2vec.sharding import ShardedTables
     V, d, R, K, L, n, steps, lr = 5000, 64, 2, 3, 12, 16, 6, 0.01
     walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(3),
@@ -394,9 +385,7 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, ahead, monkey
         sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
                         context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
         ref.step()
-    monkeypatch.setenv('DW_OUT_AHEAD', '1' if ahead else '0')
-    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out, ahead=ahead)
-    assert t.out_ahead == ahead
+    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out)
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
     if lazy_out:
@@ -555,50 +544,3 @@ def test_owner_prepare_touched_rows(hip_device, n_walks):
     # (a hub's run of centres spans several waves: its row's atomics may add in either order)
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
-
-
-def test_presorted_records_equal_pass2_sort(hip_device, monkeypatch):
-    """One rank, lazy out slice: the records sorted before pass 1 (dw_sgns_owner_presort on the
-    side stream; pass 1 writes values in walk-slot order, pass 2 gathers without a sort) train
-    what pass 2's own sort trains — up to the order of a row's records in its sum (walk order vs
-    the centres' node order) — and the same Adam steps (every row's last step equal)."""
-    V, d, R, K, L, n, steps, lr = 5000, 128, 2, 3, 12, 16, 4, 0.01
-    walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(9),
-                          dtype=torch.int32)
-    runs = []
-    for flag in ('0', '1'):
-        monkeypatch.setenv('DW_PRESORT', flag)
-        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True)
-        assert t.presort == (flag == '1')
-        runs.append((t.last_out.clone(), t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(),
-                     acc.cpu().numpy()))
-    (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
-    assert torch.equal(l0, l1)                 # the same rows stepped, at the same steps
-    np.testing.assert_allclose(a1, a0, rtol=1e-6)
-    for got, exp in ((i1, i0), (o1, o0)):
-        # (a row's records summed in another order: isolated entries with g ~ 0 move through
-        # Adam's normalisation; 1 entry in 640,000 at 1.5x the bar on one run)
-        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-4, max_abs=lr * steps)
-        assert_no_row_drift(got, exp)
-
-
-def test_out_ahead_checks_its_batch(hip_device, monkeypatch):
-    """A catch-up ahead for one batch and a step on another is refused (the claims would skip
-    rows the other batch needs), as is reading the out table while one is pending."""
-    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
-    monkeypatch.setenv('DW_OUT_AHEAD', '1')
-    V, d, R, K, L, n = 2000, 64, 2, 3, 12, 8
-    t = OwnerLazyTables(V, d, hip_device, lr=0.01, init_seed=4, lazy_out=True)
-    assert t.out_ahead
-    g = torch.Generator().manual_seed(1)
-    w = [torch.randint(1, V, (n, L), generator=g, dtype=torch.int32).to(hip_device)
-         for _ in range(3)]
-    acc = torch.zeros(4, dtype=torch.float64, device=hip_device)
-    status = torch.zeros(1, dtype=torch.int32, device=hip_device)
-    kw = dict(seed=11, grad_scale=1.0, loss_acc=acc, status=status)
-    owner_lazy_step(t, w[0], R, K, noise_offset=0,
-                    ahead=lambda: t.catch_up_out_ahead(w[1], R, K, 11, 64, status), **kw)
-    with pytest.raises(RuntimeError, match='pending'):
-        t.full_w_out()
-    with pytest.raises(RuntimeError, match='another batch'):
-        owner_lazy_step(t, w[2], R, K, noise_offset=64, **kw)

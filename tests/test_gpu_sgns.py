@@ -543,37 +543,3 @@ def test_fused_out_table_adam_equals_unfused(hip_device, d, nw):
         assert_no_row_drift(a.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_allclose(fused.m.cpu().numpy(), plain.m.cpu().numpy(), rtol=1e-3,
                                atol=1e-6)
-
-
-@pytest.mark.parametrize('fuse', [True, False])
-def test_walks_presort_equals_phase2_sort(hip_device, fuse, monkeypatch):
-    """dw_sgns_walks_presort (the records' order sorted ahead of pass 1; pass 1 writes each
-    value at its sorted place and phase 2 does not sort — replicated_step's DW_PRESORT_STEP=1)
-    gives the tables of the default path (pass 1 in walk order, sort in phase 2), with the
-    output table's Adam fused or not. Equal keys keep walk order in both sorts, so the records
-    reach each row in the same order; only float atomics (g_in) differ, compared with the
-    Adam-aware tolerance."""
-    from shallow_encoders.graph.random_walk_generator import DeepWalk
-    from shallow_encoders.graph.rmat import rmat_graph
-    from shallow_encoders.word2vec.sharding import ShardedTables, replicated_step
-    csr = rmat_graph(12, 40_000, 0, device=hip_device)
-    walker = DeepWalk(csr, 40, rng='philox', seed=3, device=hip_device)
-    V, R, K, d, nw = csr.vocab_size, 3, 4, 64, 256
-    pre = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5)
-    ref = ShardedTables(V, d, hip_device, lr=0.02, init_seed=5)
-    status = torch.zeros(1, dtype=torch.int32, device=hip_device)
-    for step in range(3):
-        starts = torch.randint(1, V, (nw,), generator=torch.Generator().manual_seed(step),
-                               dtype=torch.int32).to(hip_device)
-        walks = walker.walk_batch(starts, walk_id0=step * nw)
-        for t, flag in ((pre, '1'), (ref, '0')):
-            monkeypatch.setenv('DW_PRESORT_STEP', flag)
-            loss = torch.zeros(4, dtype=torch.float64, device=hip_device)
-            replicated_step(t, walks, R, K, seed=7, noise_offset=step * nw * 34, grad_scale=1.0,
-                            loss_acc=loss, status=status, fuse_out_adam=fuse)
-    torch.cuda.synchronize()
-    assert int(status.item()) == 0
-    for a, b in ((pre.w_in, ref.w_in), (pre.w_out, ref.w_out)):
-        assert_params_close(a.cpu().numpy(), b.cpu().numpy(), 0.02, max_frac=5e-3,
-                            max_abs=2.05 * 0.02 * 3)
-        assert_no_row_drift(a.cpu().numpy(), b.cpu().numpy())

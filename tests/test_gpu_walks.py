@@ -431,6 +431,66 @@ def _self_loop_graph():
     return CSRGraph.from_networkx(nx.relabel_nodes(g, {i: f'n{i}' for i in g.nodes}))
 
 
+def _self_looped_leaves_graph(n_leaves=300):
+    # a hub whose leaves carry self-loops (N(leaf) = {hub, leaf}, some leaves also linked to a
+    # neighbour leaf), so a step leaf -> hub has deg(hub) > 64 * deg(leaf): the positions path
+    import networkx as nx
+    g = nx.Graph()
+    g.add_edges_from([('h', f'l{i:03d}') for i in range(n_leaves)])
+    g.add_edges_from([(f'l{i:03d}', f'l{i:03d}') for i in range(n_leaves)])
+    g.add_edges_from([(f'l{i:03d}', f'l{i + 1:03d}') for i in range(0, n_leaves - 1, 7)])
+    g.add_edge('h', 'h')
+    return CSRGraph.from_networkx(g)
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (2.0, 0.5), (1.0, 1.0)])
+def test_node2vec_replay_self_looped_prev_vs_oracle(p, q, hip_device):
+    """at a step t -> v where t has a self-loop and deg(v) > 64 * deg(t), the
+    positions path mapped t (a member of N(t)) into N(v) as a common neighbour as well as the
+    1/p class. The reference gives x == prev only 1/p (random_walk_generator.py:102-104). The
+    default walker, the plain-CSR walker and the oracle's restatement agree bit for bit."""
+    csr = _self_looped_leaves_graph()
+    rng = np.random.default_rng(3)
+    leaves = np.arange(2, csr.vocab_size)   # ids: <unk> 0, 'h' 1, leaves after
+    starts = torch.as_tensor(rng.choice(leaves, 2048).astype(np.int32))
+    L = 12
+    u = rng.random((starts.numel(), L - 1))
+    got = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(starts, uniforms=u)
+    got = got.cpu().numpy()
+    plain = Node2Vec(csr, L, p=p, q=q, layout='csr', device=hip_device).walk_batch(
+        starts, uniforms=u).cpu().numpy()
+    ref = walk_ref.walks_replay(walk_ref.CSR(csr.row_ptr, csr.host_col(), None),
+                                starts.numpy(), L, 'node2vec', p, q, u)
+    np.testing.assert_array_equal(plain, ref)
+    np.testing.assert_array_equal(got, ref)
+    # the path under test was taken: leaf -> hub steps
+    assert int((got[:, 1:-1] == 1).sum()) > 1000
+
+
+def test_node2vec_replay_refuses_repeated_neighbours(hip_device):
+    """a CSR row listing a neighbour twice cannot come from the reference's
+    nx.Graph, and the exact node2vec picks assume simple rows (one position of prev, class counts
+    by intersection): the replay refuses it (dw_csr_check_simple) instead of walking it
+    differently from the serial arithmetic; DeepWalk and the Philox walkers take it."""
+    # row 1 = {2, 3, 2, 4, ...}: node 2 twice; a hub past the hash threshold elsewhere
+    rows = [[], [2, 3, 2, 4], [1, 1, 3], [1, 2], [1] + list(range(5, 20))]
+    rows += [[4] for _ in range(5, 20)]
+    row_ptr = np.cumsum([0] + [len(r) for r in rows]).astype(np.int64)
+    col = np.concatenate([np.asarray(r, dtype=np.int32) for r in rows])
+    csr = CSRGraph.from_arrays(row_ptr, col)
+    starts = torch.tensor([1, 2, 4], dtype=torch.int32)
+    with pytest.raises(ValueError, match='same neighbour twice'):
+        Node2Vec(csr, 8, p=0.5, q=2.0, device=hip_device).walk_batch(starts)
+    with pytest.raises(ValueError, match='same neighbour twice'):
+        Node2Vec(csr, 8, p=0.5, q=2.0, layout='csr', device=hip_device).walk_batch(starts)
+    assert DeepWalk(csr, 8, device=hip_device).walk_batch(starts).shape == (3, 8)
+    assert Node2Vec(csr, 8, p=0.5, q=2.0, rng='philox',
+                    device=hip_device).walk_batch(starts).shape == (3, 8)
+    # a simple graph passes the check (karate)
+    ok = _csr(golden('walks_karate_node2vec_p1_q0.5.npz'))
+    Node2Vec(ok, 4, device=hip_device).walk_batch(torch.tensor([1], dtype=torch.int32))
+
+
 @pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops'])
 def test_edge_common_counts_vs_host(which, hip_device):
     """dw_edge_common_counts (the node2vec replay's per-edge class counts: one intersection per
