@@ -260,6 +260,15 @@ def main():
     ap.add_argument('--graph-unroll', type=int, default=0,
                     help='steps per captured graph (0: the largest of 16, 8, 4, 2, 1 that '
                          'divides --steps)')
+    ap.add_argument('--exact-steps', type=int, default=None,
+                    help='one GPU, replicated step: then time this many steps (default --steps) '
+                         'with the bit-exact replay walker instead of the Philox one (rng='
+                         '"python": CPython\'s random.random() stream generated in HBM from a '
+                         'resident MT19937 state, dw_mt_draw, walked by dw_walk_replay(_inline)) '
+                         'and report it as value_exact_walks; 0 = skip')
+    ap.add_argument('--exact-prefetch', default='on', choices=['on', 'off'],
+                    help='exact-walk steps: generate the next step\'s uniforms and walks on a '
+                         'side stream during this step\'s SGNS')
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
@@ -415,8 +424,7 @@ def main():
         def _gen(self, s):
             i = s % len(self.walks)
             g0 = self.first_id(s)
-            walker.walk_batch(step_starts(g0, self.n, self.starts[i]), walk_id0=g0,
-                              out=self.walks[i][:self.n], check=False)
+            gen_walks(step_starts(g0, self.n, self.starts[i]), g0, self.walks[i][:self.n])
 
         def _launch(self, s):
             i = s % 2
@@ -448,6 +456,10 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(dev))
                 self.free[s % 2] = ev
+    def philox_walks(starts, g0, out):
+        walker.walk_batch(starts, walk_id0=g0, out=out, check=False)
+    gen_walks = philox_walks
+
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     step_idx = [0]
@@ -649,6 +661,52 @@ def main():
     kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
     if graphed is not None:   # one replay = `unroll` steps
         kern_ms = {k: v / graphed.unroll for k, v in kern_ms.items()}
+
+    # ---- the same step with the bit-exact walker ----------------------------
+    # rng='python': the walks the reference's DeepWalk.walk / Node2Vec.walk take from CPython's
+    # random.random() stream (random_walk_generator.py:61-72,113), that stream generated in HBM
+    # from a resident MT19937 state (DeviceMT, dw_mt_draw; no host round trip per step) and
+    # walked by the exact replay kernels; everything else is the timed step above
+    exact = None
+    n_exact = args.steps if args.exact_steps is None else args.exact_steps
+    if n_exact > 0 and not dist_on and not owner and graphed is None:
+        import random as _random
+        from shallow_encoders.graph.rng import DeviceMT
+        ew = (Node2Vec(csr, L, p=args.p, q=args.q, device=dev) if args.method == 'node2vec'
+              else DeepWalk(csr, L, device=dev))
+        _random.seed(0)
+        gen = DeviceMT.from_random(dev)
+        ubufs = [torch.empty(B * (L - 1), dtype=torch.float64, device=dev) for _ in range(2)]
+        ucount = [0]
+
+        def exact_walks(starts, g0, out):
+            u = ubufs[ucount[0] % 2]
+            ucount[0] += 1
+            gen.uniforms(u.numel(), out=u)
+            ew.walk_batch(starts, uniforms=u, out=out, check=False)
+        gen_walks = exact_walks
+        feed = WalkFeed(B, lambda s: (s * world + rank) * B, args.exact_prefetch == 'on')
+        loss_keep = loss_acc.clone()   # the headline's loss terms
+        for _ in range(args.warmup):
+            one_step(False)
+        torch.cuda.synchronize(dev)
+        for k in ev:
+            ev[k].clear()
+        ta = time.perf_counter()
+        for _ in range(n_exact):
+            one_step(True)
+        torch.cuda.synchronize(dev)
+        et = time.perf_counter() - ta
+        _native.check_status(status, 'bench exact walks')
+        loss_acc.copy_(loss_keep)
+        ekern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+        exact = {'value': pairs_per_step * n_exact / et, 'steps': n_exact,
+                 'ms_per_step': et / n_exact * 1e3, 'vs_philox_step': (et / n_exact) /
+                 (elapsed / args.steps), 'prefetch': args.exact_prefetch == 'on',
+                 'walk_ms': ekern['walk'], 'method': args.method,
+                 'walker': ('dw_mt_draw (CPython random.random() from a resident MT19937 state) '
+                            '+ ' + ('dw_walk_replay_indexed' if args.method == 'node2vec'
+                                    else 'dw_walk_replay_inline'))}
     if owner and dist_on:               # each rank summed the loss terms of its own slots
         dist.all_reduce(loss_acc)
     terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
@@ -882,6 +940,8 @@ def main():
         'kernel_ms': kern_ms,
         'records_per_step_per_gpu': n_rec[0] if owner else pairs_per_step * (1 + K),
         'mean_loss': mean_loss,
+        'value_exact_walks': exact['value'] if exact else None,
+        'exact_walks': exact,
         'roofline': {
             'kernel': ('dw_sgns_owner_pass1 + dw_sgns_owner_pass2 = k_sgns_g16<owner> + rocprim '
                        'onesweep radix sort + k_rec_gather with the out-slice Adam fused + '

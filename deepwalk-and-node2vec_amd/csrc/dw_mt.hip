@@ -113,15 +113,28 @@ __global__ void __launch_bounds__(JUMP_THREADS)
     jwin[c * JWIN + t] = acc;   // [0] = x[624 S c - 1], [1 + k] = x[624 S c + k]
 }
 
+// MODE 0: random.random() doubles, two words each (genrand_res53); MODE 1: torch's CPU
+// randint over [0, range) for range < 2^28 (aten uniform_int_from_to_distribution takes ONE
+// 32-bit output, `random() % range`), one word each, int64 out; MODE 2: the same for
+// 2^28 <= range < 2^32, where it takes random64() = (first output << 32 | second) % range (the
+// threshold measured against torch 2.10's CPU generator, tests/test_host.py). index_dev != 0:
+// the index is
+// mt_in[624] (a state held in HBM, e.g. inside a captured graph) and the grid covers the worst
+// case; blocks past the last window return.
+template <int MODE>
 __global__ void __launch_bounds__(MT_THREADS)
-    k_mt_chains(const uint32_t *__restrict__ mt_in, int32_t index, int64_t n,
-                double *__restrict__ out, uint32_t *__restrict__ state_out, int64_t S,
-                int64_t n_windows, const uint32_t *__restrict__ jwin) {
+    k_mt_chains(const uint32_t *__restrict__ mt_in, int32_t index_arg, int32_t index_dev,
+                int64_t n, void *__restrict__ out_v, uint64_t range,
+                uint32_t *__restrict__ state_out, int64_t S, const uint32_t *__restrict__ jwin) {
     __shared__ uint32_t win[2][MT_N];
     __shared__ uint32_t carry;   // x[624 w0 - 1]: the first word of a double straddling chains
+    constexpr int WPD = MODE == 1 ? 1 : 2;   // words per draw
+    const int32_t index = index_dev ? static_cast<int32_t>(mt_in[MT_N]) : index_arg;
+    const int64_t n_windows = n > 0 ? (index + WPD * n - 1) / MT_N + 1 : 1;
     const int t = threadIdx.x;
     const int64_t c = blockIdx.x;
     const int64_t w0 = c * S;
+    if (w0 >= n_windows) return;   // (block-uniform: a device index sized the grid for 624)
     const int64_t w1 = (w0 + S < n_windows) ? w0 + S : n_windows;
     if (n == 0) {   // nothing drawn: the state is unchanged
         if (c == 0) {
@@ -139,7 +152,7 @@ __global__ void __launch_bounds__(MT_THREADS)
         if (t == 0) carry = jw[0];
     }
     __syncthreads();
-    const int64_t first = index, last = index + 2 * n - 1;   // the stream's absolute words
+    const int64_t first = index, last = index + WPD * n - 1;   // the stream's absolute words
     for (int64_t w = w0; w < w1; ++w) {
         const int cur = static_cast<int>((w - w0) & 1);
         if (w > w0) {   // window w = twist(window w - 1), the in-place loop's three phases
@@ -155,17 +168,32 @@ __global__ void __launch_bounds__(MT_THREADS)
             }
             __syncthreads();
         }
-        // doubles whose second word a2 lies in this window: (a2 - index) odd
         const int64_t p0 = static_cast<int64_t>(MT_N) * w;
-        const int par = static_cast<int>((p0 - first + 1) & 1);
-        if (t < MT_N / 2) {
-            const int64_t a2 = p0 + 2 * t + par;
-            if (a2 > first && a2 <= last) {
-                const int o2 = static_cast<int>(a2 - p0);
-                const uint32_t x2 = win[cur][o2];
-                const uint32_t x1 = o2 > 0 ? win[cur][o2 - 1]
-                                           : (w == w0 ? carry : win[cur ^ 1][MT_N - 1]);
-                out[(a2 - first) >> 1] = res53(x1, x2);
+        if constexpr (MODE != 1) {
+            // draws whose second word a2 lies in this window: (a2 - index) odd
+            const int par = static_cast<int>((p0 - first + 1) & 1);
+            if (t < MT_N / 2) {
+                const int64_t a2 = p0 + 2 * t + par;
+                if (a2 > first && a2 <= last) {
+                    const int o2 = static_cast<int>(a2 - p0);
+                    const uint32_t x2 = win[cur][o2];
+                    const uint32_t x1 = o2 > 0 ? win[cur][o2 - 1]
+                                               : (w == w0 ? carry : win[cur ^ 1][MT_N - 1]);
+                    if constexpr (MODE == 0) {
+                        static_cast<double *>(out_v)[(a2 - first) >> 1] = res53(x1, x2);
+                    } else {
+                        const uint64_t r = (static_cast<uint64_t>(temper(x1)) << 32) | temper(x2);
+                        static_cast<int64_t *>(out_v)[(a2 - first) >> 1] =
+                            static_cast<int64_t>(r % range);
+                    }
+                }
+            }
+        } else {   // one draw per word of the window
+            int64_t *out = static_cast<int64_t *>(out_v);
+            for (int o = t; o < MT_N; o += MT_THREADS) {
+                const int64_t a = p0 + o;
+                if (a >= first && a <= last)
+                    out[a - first] = static_cast<int64_t>(temper(win[cur][o]) % range);
             }
         }
         if (w == n_windows - 1) {   // the window holding the last word: the final state
@@ -179,37 +207,86 @@ __global__ void __launch_bounds__(MT_THREADS)
 
 extern "C" {
 
+}  // extern "C"
+
+namespace {
+// index >= 0: the index (the host knows it); < 0: mt[624] on the device.
+int mt_generate(int32_t mode, const uint32_t *mt, int32_t index, int64_t n, void *out,
+                uint64_t range, uint32_t *state_out, int64_t window_stride,
+                const uint16_t *jump_pos, const int64_t *jump_off, int64_t n_chains_table,
+                uint32_t *workspace, int64_t workspace_words, hipStream_t st, const char *what) {
+    DW_REQUIRE(mode >= 0 && mode <= 2, "%s: mode must be 0, 1 or 2", what);
+    DW_REQUIRE(index <= MT_N, "%s: index must be in [0, 624]", what);
+    DW_REQUIRE(n >= 0 && n <= (int64_t(1) << 40), "%s: n must be in [0, 2^40]", what);
+    DW_REQUIRE(window_stride >= 1, "%s: window_stride must be >= 1", what);
+    DW_REQUIRE(mode == 0 || (mode == 1 && range >= 1 && range < (uint64_t(1) << 28)) ||
+                   (mode == 2 && range >= (uint64_t(1) << 28) && range < (uint64_t(1) << 32)),
+               "%s: randint range must be in [1, 2^28) (mode 1) or [2^28, 2^32) (mode 2)", what);
+    DW_REQUIRE(mt && state_out && (out || n == 0), "%s: null pointer", what);
+    const int wpd = mode == 1 ? 1 : 2;
+    int64_t n_windows = 1, chains = 1;
+    if (n > 0) {   // (a device index: sized for the largest, 624)
+        n_windows = ((index >= 0 ? index : MT_N) + wpd * n - 1) / MT_N + 1;
+        chains = (n_windows + window_stride - 1) / window_stride;
+    }
+    DW_REQUIRE(chains == 1 || (jump_pos && jump_off && chains <= n_chains_table),
+               "%s: %lld chains of %lld windows need a jump table of that many chains "
+               "(dw_mt_jump_table), have %lld", what, static_cast<long long>(chains),
+               static_cast<long long>(window_stride), static_cast<long long>(n_chains_table));
+    DW_REQUIRE(chains == 1 || (workspace && workspace_words >= chains * JWIN),
+               "%s: the workspace needs %lld words (dw_mt_workspace_words)", what,
+               static_cast<long long>(chains * JWIN));
+    DW_REQUIRE(chains < (int64_t(1) << 31), "%s: too many chains", what);
+    if (chains > 1) {
+        hipLaunchKernelGGL(k_mt_jump, dim3(static_cast<unsigned>(chains - 1)), dim3(JUMP_THREADS),
+                           0, st, mt, jump_pos, jump_off, workspace);
+        DW_LAUNCH_CHECK("dw_mt/jump");
+    }
+    const int32_t idx_dev = index < 0 ? 1 : 0;
+    const dim3 g(static_cast<unsigned>(chains)), bl(MT_THREADS);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_mt_chains<0>, g, bl, 0, st, mt, index, idx_dev, n, out, range,
+                           state_out, window_stride, workspace);
+    else if (mode == 1)
+        hipLaunchKernelGGL(k_mt_chains<1>, g, bl, 0, st, mt, index, idx_dev, n, out, range,
+                           state_out, window_stride, workspace);
+    else
+        hipLaunchKernelGGL(k_mt_chains<2>, g, bl, 0, st, mt, index, idx_dev, n, out, range,
+                           state_out, window_stride, workspace);
+    DW_LAUNCH_CHECK("dw_mt/chains");
+    return DW_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int dw_mt_uniforms(const uint32_t *mt, int32_t index, int64_t n, double *out,
                    uint32_t *state_out, int64_t window_stride, const uint16_t *jump_pos,
                    const int64_t *jump_off, int64_t n_chains_table, uint32_t *workspace,
                    int64_t workspace_words, void *stream) {
-    DW_REQUIRE(index >= 0 && index <= MT_N, "dw_mt_uniforms: index must be in [0, 624]");
-    DW_REQUIRE(n >= 0 && n <= (int64_t(1) << 40), "dw_mt_uniforms: n must be in [0, 2^40]");
-    DW_REQUIRE(window_stride >= 1, "dw_mt_uniforms: window_stride must be >= 1");
-    DW_REQUIRE(mt && state_out && (out || n == 0), "dw_mt_uniforms: null pointer");
-    int64_t n_windows = 1, chains = 1;
-    if (n > 0) {
-        n_windows = (index + 2 * n - 1) / MT_N + 1;
-        chains = (n_windows + window_stride - 1) / window_stride;
+    DW_REQUIRE(index >= 0, "dw_mt_uniforms: index must be in [0, 624]");
+    return mt_generate(0, mt, index, n, out, 0, state_out, window_stride, jump_pos, jump_off,
+                       n_chains_table, workspace, workspace_words, dw::as_stream(stream),
+                       "dw_mt_uniforms");
+}
+
+int dw_mt_draw(int32_t mode, uint32_t *state, int32_t index, int64_t n, void *out,
+               uint64_t range, uint32_t *scratch, int64_t window_stride,
+               const uint16_t *jump_pos, const int64_t *jump_off, int64_t n_chains_table,
+               uint32_t *workspace, int64_t workspace_words, void *stream) {
+    DW_REQUIRE(state && scratch && state != scratch, "dw_mt_draw: state / scratch");
+    hipStream_t st = dw::as_stream(stream);
+    const int rc = mt_generate(mode, state, index < 0 ? -1 : index, n, out, range, scratch,
+                               window_stride, jump_pos, jump_off, n_chains_table, workspace,
+                               workspace_words, st, "dw_mt_draw");
+    if (rc != DW_OK) return rc;
+    // the state after the draws back into place (625 words; stream-ordered, capturable)
+    const hipError_t e = hipMemcpyAsync(state, scratch, (MT_N + 1) * sizeof(uint32_t),
+                                        hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) {
+        dw::set_error("dw_mt_draw: state copy: %s", hipGetErrorString(e));
+        return DW_E_HIP;
     }
-    DW_REQUIRE(chains == 1 || (jump_pos && jump_off && chains <= n_chains_table),
-               "dw_mt_uniforms: %lld chains of %lld windows need a jump table of that many "
-               "chains (dw_mt_jump_table), have %lld",
-               static_cast<long long>(chains), static_cast<long long>(window_stride),
-               static_cast<long long>(n_chains_table));
-    DW_REQUIRE(chains == 1 || (workspace && workspace_words >= chains * JWIN),
-               "dw_mt_uniforms: the workspace needs %lld words (dw_mt_workspace_words)",
-               static_cast<long long>(chains * JWIN));
-    DW_REQUIRE(chains < (int64_t(1) << 31), "dw_mt_uniforms: too many chains");
-    if (chains > 1) {
-        hipLaunchKernelGGL(k_mt_jump, dim3(static_cast<unsigned>(chains - 1)), dim3(JUMP_THREADS),
-                           0, dw::as_stream(stream), mt, jump_pos, jump_off, workspace);
-        DW_LAUNCH_CHECK("dw_mt_uniforms/jump");
-    }
-    hipLaunchKernelGGL(k_mt_chains, dim3(static_cast<unsigned>(chains)), dim3(MT_THREADS), 0,
-                       dw::as_stream(stream), mt, index, n, out, state_out, window_stride,
-                       n_windows, workspace);
-    DW_LAUNCH_CHECK("dw_mt_uniforms");
     return DW_OK;
 }
 

@@ -57,6 +57,8 @@ SIGNATURES = {
     'dw_mt_uniforms': (ctypes.c_int, [_p, _i32, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64,
                                       _p]),
     'dw_mt_workspace_words': (ctypes.c_int64, [_i64]),
+    'dw_mt_draw': (ctypes.c_int, [_i32, _p, _i32, _i64, _p, _u64, _p, _i64, _p, _p, _i64, _p,
+                                  _i64, _p]),
     'dw_csr_validate': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_csr_sort_copy': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _szp, _p]),
     'dw_csr_check_simple': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),

@@ -171,3 +171,115 @@ def draw_uniforms_device(n: int, device=None, rng: random.Random = None,
         return out, commit
     commit()
     return out
+
+
+# ---- a generator held in HBM across draws (dw_mt_draw) ------------------------------------------
+def _torch_state_words(state: torch.Tensor):
+    """torch's CPU generator state (torch.get_rng_state(): aten CPUGeneratorImplStateLegacy,
+    little-endian: the_initial_seed u64, left i32, seeded i32, next u64, state u64[624], then the
+    normal-sample cache) -> (624 uint32 words, index in CPython's convention: the position of the
+    next output in the array, 624 = twist first). aten's mt19937 decrements ``left`` per draw and
+    twists when it reaches 0, so index = 625 - left (seeding leaves left = 1: twist first)."""
+    b = state.numpy()
+    left = int(b[8:12].view(np.int32)[0])
+    words = b[24:24 + 624 * 8].view(np.uint64).astype(np.uint32)
+    return words, 625 - left
+
+
+def _torch_state_with(state: torch.Tensor, words: np.ndarray, index: int) -> torch.Tensor:
+    """``state`` with the twister's array and position replaced (left = 625 - index, next =
+    index); the seed and the normal-sample cache untouched."""
+    b = state.numpy().copy()
+    b[8:12] = np.array([625 - index], dtype=np.int32).view(np.uint8)
+    b[16:24] = np.array([index], dtype=np.uint64).view(np.uint8)
+    b[24:24 + 624 * 8] = np.asarray(words, dtype=np.uint64).view(np.uint8)
+    return torch.from_numpy(b)
+
+
+class DeviceMT:
+    """An MT19937 generator whose state stays in HBM between draws (dw_mt_draw): CPython's
+    ``random`` (``uniforms``: random.random(), the walkers' stream, random_walk_generator.py:
+    68,113) or torch's CPU generator (``randint``: torch.randint(0, high, ...), the reference's
+    negatives, utils/sampling.py:7-21). No host round trip per draw: the host only follows the
+    index (a pure function of the draw counts), and the state returns to Python / torch on
+    ``to_random`` / ``to_torch``. ``device_index=True`` reads the index on the device instead,
+    so launches can be captured once and replayed (word2vec/graphed.py)."""
+
+    def __init__(self, words: np.ndarray, index: int, device, device_index: bool = False):
+        from shallow_encoders import _native
+        self.device = _native.require_device(device)
+        st = np.empty(625, dtype=np.uint32)
+        st[:624] = np.asarray(words, dtype=np.uint32)
+        st[624] = int(index)
+        self.state = torch.from_numpy(st.view(np.int32).copy()).to(self.device)
+        self.scratch = torch.empty(625, dtype=torch.int32, device=self.device)
+        self.index = None if device_index else int(index)
+        self.n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+
+    @classmethod
+    def from_random(cls, device=None, rng: random.Random = None, **kw) -> 'DeviceMT':
+        rng = random._inst if rng is None else rng  # noqa: SLF001
+        st = np.asarray(rng.getstate()[1], dtype=np.uint32)
+        return cls(st[:624], int(st[624]), device, **kw)
+
+    @classmethod
+    def from_torch(cls, device=None, **kw) -> 'DeviceMT':
+        words, index = _torch_state_words(torch.get_rng_state())
+        return cls(words, index, device, **kw)
+
+    def _draw(self, mode: int, n: int, out: torch.Tensor, high: int = 0) -> torch.Tensor:
+        from shallow_encoders import _native
+        n = int(n)
+        wpd = 1 if mode == 1 else 2
+        idx = 624 if self.index is None else self.index
+        windows = (idx + wpd * n - 1) // 624 + 1 if n > 0 else 1
+        per = -(-windows // max(1, CHAINS_PER_CU * self.n_cu))
+        stride = max(MIN_CHAIN_WINDOWS, -(-per // 64) * 64)
+        chains = -(-windows // stride)
+        pos = off = ws = None
+        n_tab = 1
+        if chains > 1:
+            pos, off, n_tab = mt_jump_table(self.device, stride, chains)
+            ws = mt_workspace(self.device, chains)
+        with torch.cuda.device(self.device):
+            _native.call('dw_mt_draw', mode, _native.ptr(self.state),
+                         -1 if self.index is None else self.index, n, _native.ptr(out),
+                         int(high), _native.ptr(self.scratch), stride, _native.ptr(pos),
+                         _native.ptr(off), n_tab, _native.ptr(ws), 0 if ws is None else ws.numel(),
+                         _native.stream(self.device))
+        if self.index is not None and n > 0:
+            last = self.index + wpd * n - 1
+            self.index = last + 1 - 624 * (last // 624)
+        return out
+
+    def uniforms(self, n: int, out: torch.Tensor = None) -> torch.Tensor:
+        """float64 [n]: the next n random.random() of this generator."""
+        if out is None:
+            out = torch.empty(int(n), dtype=torch.float64, device=self.device)
+        return self._draw(0, n, out)
+
+    def randint(self, high: int, n: int, out: torch.Tensor = None) -> torch.Tensor:
+        """int64 [n]: the next n torch.randint(0, high) values of this generator (0 < high <
+        2^32: one output per value below 2^28, two from there, as torch takes them)."""
+        if not 0 < int(high) < (1 << 32):
+            raise ValueError('randint: high must be in (0, 2^32)')
+        if out is None:
+            out = torch.empty(int(n), dtype=torch.int64, device=self.device)
+        return self._draw(1 if int(high) < (1 << 28) else 2, n, out, high)
+
+    def host_state(self):
+        """(624 uint32 words, index): synchronises the current stream."""
+        st = self.state.cpu().numpy().view(np.uint32)
+        return st[:624].copy(), int(st[624])
+
+    def to_random(self, rng: random.Random = None) -> None:
+        """Hand the state back to CPython's generator (default: the global one)."""
+        rng = random._inst if rng is None else rng  # noqa: SLF001
+        version, _, gauss = rng.getstate()
+        words, index = self.host_state()
+        rng.setstate((version, tuple(int(w) for w in words) + (index,), gauss))
+
+    def to_torch(self) -> None:
+        """Hand the state back to torch's CPU generator."""
+        words, index = self.host_state()
+        torch.set_rng_state(_torch_state_with(torch.get_rng_state(), words, index))

@@ -101,6 +101,25 @@ int dw_mt_uniforms(const uint32_t *mt, int32_t index, int64_t n, double *out,
                    int64_t workspace_words, void *stream);
 int64_t dw_mt_workspace_words(int64_t n_chains);
 
+/* A generator whose state lives in HBM (state: 625 uint32 words, the 624-word array + the
+ * index, random.getstate()[1]'s layout; torch's CPU generator maps onto the same layout), advanced
+ * in place by n draws (through scratch, 625 words, then copied back; stream-ordered and
+ * capturable in a HIP graph):
+ *   mode 0: out float64[n] = the next n random.random() (as dw_mt_uniforms);
+ *   mode 1: out int64[n] = the next n torch.randint(0, range, ...) values of torch's CPU
+ *           generator for range < 2^28 (aten's mt19937, one 32-bit output per value,
+ *           `% range`) — generate_noise_batch (utils/sampling.py:7-21), noise='torch';
+ *   mode 2: the same for 2^28 <= range < 2^32, where torch takes two outputs per value
+ *           ((first << 32 | second) % range).
+ * index >= 0: the host knows the index (it must equal state[624]), the launch is sized to it;
+ * index < 0: read on the device (a replayed graph), the launch covers the largest index.
+ * jump_* / workspace as dw_mt_uniforms for chains = ceil(windows / window_stride), windows =
+ * (index + w n - 1) / 624 + 1, w = 1 (mode 1) or 2, index = 624 when read on device. */
+int dw_mt_draw(int32_t mode, uint32_t *state, int32_t index, int64_t n, void *out,
+               uint64_t range, uint32_t *scratch, int64_t window_stride,
+               const uint16_t *jump_pos, const int64_t *jump_off, int64_t n_chains_table,
+               uint32_t *workspace, int64_t workspace_words, void *stream);
+
 /* ---- graph ------------------------------------------------------------------------------- */
 
 /* Validate a CSR on the device: row_ptr[0]==0, monotone, row_ptr[n_rows]==nnz, 0<=col<n_rows.

@@ -159,3 +159,23 @@ def uniforms_chained(mt: Sequence[int], index: int, n: int, stride: int, positio
                 state = (win.copy(), last + 1 - p0)
             prev = win
     return out, state[0], state[1]
+
+
+def torch_randint(mt: Sequence[int], index: int, n: int, high: int) -> Tuple[np.ndarray, np.ndarray, int]:
+    """torch.randint(0, high, (n,)) on torch's CPU generator (aten/src/ATen/core/
+    DistributionsHelper.h uniform_int_from_to_distribution; the same MT19937 as CPython's), from
+    state (mt, index) in CPython's convention — the reference's generate_noise_batch
+    (utils/sampling.py:7-21): below a range of 2^28 ONE 32-bit output per value, ``random() %
+    range``; from 2^28 (the threshold of torch 2.10, measured in tests/test_host.py) random64() =
+    (first output << 32 | second) % range. Returns (int64 values, new array, new index)."""
+    if n == 0:
+        return np.zeros(0, dtype=np.int64), np.asarray(mt, dtype=np.uint32), index
+    w = 1 if high < (1 << 28) else 2
+    last = index + w * n - 1
+    x = raw_sequence(mt, (last // N + 1) * N)
+    t = temper(x[index:index + w * n]).astype(np.uint64)
+    if w == 2:
+        t = (t[0::2] << np.uint64(32)) | t[1::2]
+    vals = (t % np.uint64(high)).astype(np.int64)
+    blk = last // N
+    return vals, x[blk * N:(blk + 1) * N].copy(), last + 1 - blk * N

@@ -120,3 +120,78 @@ def test_walker_default_stream_is_device_generated_and_exact(method, hip_device)
     exp = w.walk_batch(starts, uniforms=u).cpu().numpy()
     np.testing.assert_array_equal(got, exp)
     assert random.getstate() == after
+
+
+# ---- a generator held in HBM (DeviceMT / dw_mt_draw): torch's negatives and CPython's walks ---
+def _torch_expected(seed, skip, high, sizes):
+    """torch.randint draws of the given sizes after torch.manual_seed(seed) and `skip` draws, and
+    torch's generator state after them (CPU; the reference's generate_noise_batch)."""
+    torch.manual_seed(seed)
+    if skip:
+        torch.randint(0, 7, (skip,))
+    st0 = torch.get_rng_state()
+    exp = [torch.randint(0, high, (n,), dtype=torch.long) for n in sizes]
+    return st0, exp, torch.get_rng_state()
+
+
+@pytest.mark.parametrize('seed,skip,high,sizes', [
+    (0, 0, 1_048_577, [4480 * 50] * 6),            # the reference's 64-walk C3 batches
+    (1, 311, 2708, [1, 623, 624, 625, 9_999]),      # Cora-sized vocabulary, window edges
+    (2, 5, 2 ** 28 + 11, [3, 1000, 77_777]),        # two outputs per value
+    (3, 0, 1_048_577, [10_000_001]),                # >= 10^7 draws in one call
+])
+def test_device_torch_randint_equals_torch(seed, skip, high, sizes, hip_device):
+    """DeviceMT.randint (dw_mt_draw mode 1 / 2) from torch's CPU generator state
+    gives torch.randint's values bit for bit, call after call, with the state kept in HBM between
+    calls; to_torch() leaves torch.get_rng_state() equal to what the host draws leave."""
+    from shallow_encoders.graph.rng import DeviceMT
+    st0, exp, st1 = _torch_expected(seed, skip, high, sizes)
+    torch.set_rng_state(st0)
+    g = DeviceMT.from_torch(hip_device)
+    for n, e in zip(sizes, exp):
+        got = g.randint(high, n)
+        assert torch.equal(got.cpu(), e), n
+    g.to_torch()
+    assert torch.equal(torch.get_rng_state(), st1)
+
+
+def test_device_torch_randint_device_index_and_graph(hip_device):
+    """The index read on the device (device_index=True) and the draws captured once in a HIP
+    graph and replayed: the same stream as torch.randint, replay after replay (the graphed
+    training loop's negatives)."""
+    from shallow_encoders.graph.rng import DeviceMT
+    high, n, reps = 1_048_577, 4480 * 50, 5
+    st0, exp, st1 = _torch_expected(4, 3, high, [n] * (reps + 1))
+    torch.set_rng_state(st0)
+    g = DeviceMT.from_torch(hip_device, device_index=True)
+    out = torch.empty(n, dtype=torch.int64, device=hip_device)
+    g.randint(high, n, out=out)                       # eager, device index
+    assert torch.equal(out.cpu(), exp[0])
+    s = torch.cuda.Stream(hip_device)
+    s.wait_stream(torch.cuda.current_stream(hip_device))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        g.randint(high, n, out=out)
+    for k in range(reps):
+        graph.replay()
+        torch.cuda.synchronize(hip_device)
+        assert torch.equal(out.cpu(), exp[k + 1]), k
+    g.to_torch()
+    assert torch.equal(torch.get_rng_state(), st1)
+
+
+@pytest.mark.parametrize('device_index', [False, True])
+def test_device_mt_uniforms_resident_equals_cpython(device_index, hip_device):
+    """DeviceMT.uniforms: CPython's random.random() stream call after call with the state in
+    HBM (no host round trip; the host follows the index, or the device reads it), then handed
+    back to `random` exactly."""
+    from shallow_encoders.graph.rng import DeviceMT
+    r = _gen(31, 7)
+    exp_r = _clone(r)
+    g = DeviceMT.from_random(hip_device, rng=r, device_index=device_index)
+    for n in (1, 311, 312, 647_168, 5):
+        got = g.uniforms(n)
+        exp = draw_uniforms(n, exp_r) if n >= 64 else np.array([exp_r.random() for _ in range(n)])
+        assert torch.equal(got.cpu(), torch.from_numpy(exp)), n
+    g.to_random(r)
+    assert r.getstate() == exp_r.getstate()

@@ -485,6 +485,34 @@ def test_mt_chained_generation_is_cpython_random(stride, seed, skip, n):
     assert list(arr) == list(st[:624]) and index == st[624]
 
 
+@pytest.mark.parametrize('seed,skip,high,n', [(0, 0, 2708, 3000), (1234, 5, 1_048_577, 700),
+                                              (7, 623, 34, 1), (99, 624, 2 ** 32 - 1, 2000),
+                                              (3, 400, 5, 0), (8, 1, 2 ** 28 - 1, 999),
+                                              (9, 2, 2 ** 28, 999), (10, 311, 2 ** 30 + 3, 313)])
+def test_torch_randint_oracle_and_state_mapping(seed, skip, high, n):
+    """The reference's negatives are torch.randint on torch's CPU generator
+    (utils/sampling.py:7-21). oracle.mt_ref.torch_randint restates it from the MT19937 state in
+    CPython's layout, and graph/rng.py maps torch.get_rng_state() onto that layout and back
+    (_torch_state_words / _torch_state_with): the values and the generator state after them equal
+    torch's own, for fresh seeds (index 624), odd positions and a window's last word."""
+    from oracle import mt_ref
+    from shallow_encoders.graph.rng import _torch_state_with, _torch_state_words
+    torch.manual_seed(seed)
+    if skip:
+        torch.randint(0, 3, (skip,))
+    st0 = torch.get_rng_state()
+    words, index = _torch_state_words(st0)
+    vals, arr, idx = mt_ref.torch_randint(words, index, n, high)
+    exp = torch.randint(0, high, (n,), dtype=torch.long).numpy()
+    np.testing.assert_array_equal(vals, exp)
+    assert torch.equal(_torch_state_with(st0, arr, idx), torch.get_rng_state())
+    # the mapping round-trips (a fresh seed's next = 0 is written as 624: the same position)
+    torch.set_rng_state(_torch_state_with(st0, words, index))
+    after = torch.randint(0, high, (n + 5,), dtype=torch.long)
+    torch.set_rng_state(st0)
+    assert torch.equal(after, torch.randint(0, high, (n + 5,), dtype=torch.long))
+
+
 def test_library_built_from_these_sources():
     """The shipped libdw_hip.so carries the hash of the sources it was built from
     (csrc/build.py source_id, dw_build_id()): equal to this tree's, so the binary that travels
