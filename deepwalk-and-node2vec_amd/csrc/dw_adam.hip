@@ -102,7 +102,7 @@ using dw::hist_at;
 // the barrier; thread 0 writes it after. STEP: replay the missed steps up to step - 1, then
 // apply `step` with the row's gradient g_rows[i]; else replay up to `step`. The step loop is
 // uniform: lanes past d carry zeros and are not stored.
-template <bool STEP>
+template <bool STEP, bool P_ONLY = false>
 __global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
                 int32_t *__restrict__ last, int64_t n_table, int32_t d,
@@ -139,10 +139,12 @@ __global__ void __launch_bounds__(512)
         if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
         if (live) {
             p[o] = pp;
-            m[o] = mm;
-            v[o] = vv;
+            if (!P_ONLY) {
+                m[o] = mm;
+                v[o] = vv;
+            }
         }
-        if (e == 0) last[r] = STEP ? step : upto;
+        if (e == 0 && !P_ONLY) last[r] = STEP ? step : upto;
     }
 }
 
@@ -270,10 +272,12 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
                             weight_decay, zero_grad, 0, stream);
 }
 
-int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                 const float *hist, int32_t step, void *stream) {
+}  // extern "C"
+
+int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
+                         int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                         const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
+                         const float *hist, int32_t step, bool p_only, hipStream_t st) {
     DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0 && step >= 0,
                "dw_adam_rows: bad sizes");
     if (n_rows_max == 0) return DW_OK;
@@ -287,19 +291,33 @@ int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_
     if (rc != DW_OK) return rc;
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
+    DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
     const int threads = 64 * ((dim + 63) / 64);
     if (grad_rows)
-        hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0,
-                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
-                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
-                           dyn, delta);
+        hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0, st,
+                           param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
+                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
+    else if (p_only)
+        hipLaunchKernelGGL((k_rows_adam<false, true>), dim3((unsigned)blocks), dim3(threads), 0,
+                           st, param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
+                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
     else
-        hipLaunchKernelGGL((k_rows_adam<false>), dim3((unsigned)blocks), dim3(threads), 0,
-                           dw::as_stream(stream), param, exp_avg, exp_avg_sq, last_step,
-                           n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step,
-                           dyn, delta);
+        hipLaunchKernelGGL((k_rows_adam<false>), dim3((unsigned)blocks), dim3(threads), 0, st,
+                           param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
+                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
+}
+
+extern "C" {
+
+int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
+                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
+                 const float *hist, int32_t step, void *stream) {
+    return dw::adam_rows_launch(param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
+                                n_rows_dev, n_rows_max, grad_rows, hist, step, false,
+                                dw::as_stream(stream));
 }
 
 int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,

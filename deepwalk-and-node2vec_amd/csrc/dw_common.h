@@ -157,6 +157,14 @@ __device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
     return AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6]};
 }
 
+// dw_adam_rows (dw_adam.hip) with p_only: the replayed g = 0 steps go back to memory as p alone
+// (m, v and last[] untouched) — the lazy out slice's catch-up before pass 1, whose lazy gather
+// then replays m and v itself (their g = 0 recurrences are a multiply each) before the step.
+int adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
+                     int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                     const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
+                     const float *hist, int32_t step, bool p_only, hipStream_t stream);
+
 // Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
 __device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
     const float *h = hist + 8 * s;

@@ -30,7 +30,10 @@
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/block/block_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "dw_common.h"
 
@@ -149,6 +152,9 @@ struct SgnsArgs {
     uint32_t *rec_counts;
     uint32_t *count_out;      //   n_owners == 1: the records are dense; their count goes here
     int64_t region;
+    // placed records (one owner or many, after k_out_claim): slot (b, t)'s record goes to
+    // place_off[row] + place_rank[b * T + t]; no regions, no compaction, no sort
+    const uint32_t *place_rank = nullptr, *place_off = nullptr;
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
@@ -608,9 +614,18 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 const int tt = gl + 16 * k;
                 if (tt < n_own) {
                     const int32_t id = s_id[wv][q][tt];   // < 0: a bad id (one owner only)
-                    a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
-                    a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
-                                                     ok_c ? cid : 0);
+                    if (a.place_off) {   // placed: k_out_claim counted only the valid rows
+                        if (id >= 0) {
+                            const uint32_t pos = a.place_off[id] +
+                                                 a.place_rank[b * T + s_t[wv][q][tt]];
+                            a.rec_key[pos] = static_cast<uint32_t>(id);
+                            a.rec_val[pos] = pack_record(s_coef[wv][q][tt], ok_c ? cid : 0);
+                        }
+                    } else {
+                        a.rec_key[at + tt] = static_cast<uint32_t>(id < 0 ? 0 : id);
+                        a.rec_val[at + tt] = pack_record(id < 0 ? 0.f : s_coef[wv][q][tt],
+                                                         ok_c ? cid : 0);
+                    }
                 }
             }
             filled += c0 + c1 + c2 + c3;
@@ -698,6 +713,7 @@ struct OutAdam {
     int32_t step = 0;
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
     int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
+    bool p_current = false;   // lazy form: the catch-up brought p (not m, v, last) to step - 1
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -718,16 +734,32 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
         vv[m] = live ? oa.v[i] : 0.f;
         gg[m] = g[m];
     }
-    for (int32_t t = from + 1; t < step; ++t) {
-        const dw::AdamScalars h = dw::hist_at(oa.hist, t);
-        if (h.wd == 0.f) {
-#pragma unroll
-            for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
-        } else {
+    if (oa.p_current) {
+        // p is at step - 1 already (the p-only catch-up): m and v replay their g = 0 steps — the
+        // same two IEEE operations adam_elem_g0 applies to them, one multiply-add each (the
+        // host enables this only while every step has weight_decay 0: then m, v never read p)
+        for (int32_t t = from + 1; t < step; ++t) {
+            const float *h = oa.hist + 8 * static_cast<int64_t>(t);
+            const float w1 = h[0], b2 = h[1];
 #pragma unroll
             for (int m = 0; m < VPL; ++m) {
-                float z = 0.f;
-                dw::adam_elem(pp[m], z, mm[m], vv[m], h);
+#pragma clang fp contract(off)
+                mm[m] = fmaf(w1, -mm[m], mm[m]);
+                vv[m] = vv[m] * b2;
+            }
+        }
+    } else {
+        for (int32_t t = from + 1; t < step; ++t) {
+            const dw::AdamScalars h = dw::hist_at(oa.hist, t);
+            if (h.wd == 0.f) {
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
+            } else {
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) {
+                    float z = 0.f;
+                    dw::adam_elem(pp[m], z, mm[m], vv[m], h);
+                }
             }
         }
     }
@@ -1584,9 +1616,56 @@ int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t 
     return DW_OK;
 }
 
+// A row's slot count this step (0 unless its claim word carries the step): the scan's input.
+struct StepCount {
+    const unsigned long long *claim;
+    int64_t n_rows;
+    const dw_step_scalars *dyn;
+    int32_t delta, step;
+    __device__ uint32_t operator()(uint32_t r) const {
+        if (r >= n_rows) return 0u;
+        const unsigned long long c = claim[r];
+        return (c >> 32) == static_cast<uint32_t>(dw::eff_step(dyn, delta, step))
+                   ? static_cast<uint32_t>(c) : 0u;
+    }
+};
+
+// the records' placement (k_out_claim's ranks, one owner or many): rank[slot], off[row] (the
+// exclusive scan of the step's per-row counts, off[local_rows] = their total) and the scan's
+// temporary storage; between the records part and OccSpace
+struct PlaceSpace {
+    uint32_t *rank, *off;
+    void *tmp;
+    size_t tmp_bytes, total;
+};
+
+using StepCountIter =
+    rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, StepCount, uint32_t>;
+
+int plan_place(int64_t n_slots, int64_t local_rows, void *base, PlaceSpace *pl, hipStream_t st) {
+    size_t tmp = 0;
+    StepCountIter it(rocprim::counting_iterator<uint32_t>(0), StepCount{});
+    if (rocprim::exclusive_scan(nullptr, tmp, it, static_cast<uint32_t *>(nullptr), 0u,
+                                static_cast<size_t>(local_rows + 1), rocprim::plus<uint32_t>(),
+                                st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner: placement scan size query failed");
+        return DW_E_HIP;
+    }
+    const size_t a = align256((size_t)(n_slots > 0 ? n_slots : 1) * 4);
+    const size_t b = align256((size_t)(local_rows + 1) * 4);
+    char *p = static_cast<char *>(base);
+    pl->rank = reinterpret_cast<uint32_t *>(p);
+    pl->off = reinterpret_cast<uint32_t *>(p + a);
+    pl->tmp = p + a + b;
+    pl->tmp_bytes = tmp;
+    pl->total = a + b + align256(tmp);
+    return DW_OK;
+}
+
 int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *workspace,
                     size_t workspace_bytes, Workspace *ws, OwnerLayout *lay, hipStream_t st,
-                    const char *what, int64_t V = 0, OccSpace *occ = nullptr) {
+                    const char *what, int64_t V = 0, OccSpace *occ = nullptr,
+                    PlaceSpace *place = nullptr) {
     *lay = owner_layout(n_centres, T);
     DW_REQUIRE(lay->total < 0x7FFFFFFF, "%s: too many records (%lld)", what,
                (long long)lay->total);
@@ -1595,10 +1674,14 @@ int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *work
     DW_REQUIRE(workspace != nullptr, "%s: needs the records workspace", what);
     int rc = plan_workspace(lay->total, local_rows, workspace, ws, st);
     if (rc != DW_OK) return rc;
-    size_t need = ws->total;
+    PlaceSpace pl;
+    rc = plan_place(n_centres * T, local_rows, static_cast<char *>(workspace) + ws->total, &pl, st);
+    if (rc != DW_OK) return rc;
+    if (place) *place = pl;
+    size_t need = ws->total + pl.total;
     if (occ) {
-        rc = plan_occ(n_centres > 0 ? n_centres : 1, V, static_cast<char *>(workspace) + ws->total,
-                      occ, st);
+        rc = plan_occ(n_centres > 0 ? n_centres : 1, V, static_cast<char *>(workspace) + need, occ,
+                      st);
         if (rc != DW_OK) return rc;
         need += occ->total;
     }
@@ -1683,13 +1766,21 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     Workspace ws;
     OwnerLayout lay;
     OccSpace occ;
+    PlaceSpace pl;
     int rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
-                             "dw_sgns_owner_pass1", a.V, &occ);
+                             "dw_sgns_owner_pass1", a.V, &occ, &pl);
     if (rc != DW_OK) return rc;
     g_timer.mark(0, st);
     // n_owners > 1: per-wave regions in (k0, v0), compacted into (k1, v1); one owner keeps
-    // every slot, so the regions tile (k1, v1) densely and pass 1 writes there directly
-    const bool dense = a.n_owners == 1;
+    // every slot, so the regions tile (k1, v1) densely and pass 1 writes there directly;
+    // placed (order_ready & 2, after dw_sgns_owner_out_catch_up with flags & 1): each record
+    // straight to its row's segment of (k1, v1)
+    const bool placed = (order_ready & 2) != 0;
+    const bool dense = a.n_owners == 1 || placed;
+    if (placed) {
+        a.place_rank = pl.rank;
+        a.place_off = pl.off;
+    }
     a.rec_key = dense ? ws.k1 : ws.k0;
     a.rec_val = dense ? ws.v1 : ws.v0;
     a.count_out = dense ? ws.count : nullptr;
@@ -1724,7 +1815,8 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
 
 int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
                        const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
-                       size_t workspace_bytes, int64_t *n_records, hipStream_t st) {
+                       size_t workspace_bytes, int64_t *n_records, hipStream_t st,
+                       bool placed = false) {
     Workspace ws;
     OwnerLayout lay;
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
@@ -1733,6 +1825,19 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     const int64_t bound = n_centres * T;
     const int64_t *range = nullptr;
     int64_t n_rec = bound;
+    if (placed) {
+        // pass 1 wrote every record into its row's segment of (k1, v1): no sort; the range
+        // [0, count) was written by the catch-up (k_place_range); the grid is sized for the bound
+        DW_REQUIRE(!n_records, "dw_sgns_owner_pass2: placed records need n_records NULL");
+        g_timer.mark(2, st);
+        if (bound > 0 || oa) {
+            rc = launch_pass2(ws.k1, ws.v1, bound, w_in, g_out, d, oa, local_rows, st,
+                              bound > 0 ? ws.bounds : nullptr);
+            if (rc != DW_OK) return rc;
+        }
+        g_timer.mark(3, st);
+        return DW_OK;
+    }
     if (n_records) {
         // the record count decides the sort's size on the host: one stream synchronisation
         uint32_t n = 0;
@@ -1923,14 +2028,24 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // Lazy out slice (dw_sgns_owner_out_catch_up), before pass 1: every owned output row a slot of
 // this batch references must be brought current to step - 1 (its deferred g = 0 steps replayed
 // through adam_elem with hist's scalars), so pass 1 reads the rows the dense update would hold.
-// This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64); a row is
-// claimed by exactly one lane in the launch — atomicMax(claim[row], step) returning < step — and
-// the wave appends its claimed rows to `list` with one counter atomic. dw_adam_rows then
-// replays the listed rows, all in parallel. A row the previous step claimed (old == step - 1) is
-// not listed: that step's records held it, so its lazy gather already brought it to step - 1.
+// This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64). Each owned
+// row has a 64-bit claim word {step of its last touch : 32, slots of that step : 32}, updated by
+// CAS: the first slot of a step to reach a row restarts the count at 1, the others add 1. The
+// first toucher lists the row when its last touch is older than step - 1 (a row the previous
+// step touched held a record there, so its lazy gather already brought it to step - 1); the
+// wave's listed rows are appended to `list` with one counter atomic per block. dw_adam_rows then
+// replays the listed rows, all in parallel.
+// Placement (rank != NULL): the count a slot's CAS returned is its rank among the step's slots
+// of that row, kept per slot (rank[b * T + t]); an exclusive scan of the step's counts then gives
+// every row a segment of the records array, and pass 1 writes each record at off[row] + rank:
+// the records come out grouped by row with no sort (the 64-walk batch: 269K records, whose
+// radix sort was ~10 launches and ~85 us of the step). The order of a row's records is the order
+// the CAS loops resolved — as nondeterministic as the float atomics of rows that straddle two
+// gather chunks.
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
-                uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list) {
+    k_out_claim(SgnsArgs a, unsigned long long *__restrict__ claim, int32_t step_arg,
+                int32_t delta, uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
+                uint32_t *__restrict__ rank) {
     const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
     // one centre per wave; the block's claimed rows are appended with ONE counter atomic (a
     // same-address atomic per wave serialised: 4,480 of them were ~40 us at the 64-walk batch)
@@ -1941,6 +2056,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int T = a.C * (1 + a.K);
     const int64_t per = a.L - 2 * a.R;
+    const unsigned long long tag = static_cast<unsigned long long>(step) << 32;
     for (int64_t b0 = (int64_t)blockIdx.x * WAVES_PER_BLOCK; b0 < a.batch; b0 += n_waves) {
         const int64_t b = b0 + wv;   // block-uniform trip count (barriers below)
         bool mine = false;
@@ -1952,7 +2068,18 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                 dw::status_or(a.status, DW_S_BAD_INDEX);
             } else if (o % a.n_owners == a.owner) {
                 lo = static_cast<uint32_t>(o / a.n_owners);
-                mine = atomicMax(claim + lo, step) < step - 1;
+                unsigned long long old = claim[lo];
+                while (true) {
+                    const unsigned long long nw = (old >> 32) == static_cast<uint32_t>(step)
+                                                      ? old + 1ull : (tag | 1ull);
+                    const unsigned long long prev = atomicCAS(claim + lo, old, nw);
+                    if (prev == old) break;
+                    old = prev;
+                }
+                const int32_t seen = static_cast<int32_t>(old >> 32);
+                const bool first = seen != step;
+                mine = first && seen < step - 1;
+                if (rank) rank[b * T + lane] = first ? 0u : static_cast<uint32_t>(old);
             }
         }
         const unsigned long long mask = __ballot(mine);
@@ -1971,6 +2098,15 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     }
 }
 
+// the placed records' range for the gather (off[n_rows] = their count)
+__global__ void k_place_range(const uint32_t *__restrict__ off, int64_t n_rows,
+                              int64_t *__restrict__ range) {
+    if (threadIdx.x == 0) {
+        range[0] = 0;
+        range[1] = static_cast<int64_t>(off[n_rows]);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1980,9 +2116,10 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
-                               int32_t *last_step, int32_t *claim, uint32_t *rows_buf,
-                               int64_t *n_rows, const float *hist, int32_t step,
-                               int32_t *status, void *stream) {
+                               int32_t *last_step, uint64_t *claim, uint32_t *rows_buf,
+                               int64_t *n_rows, const float *hist, int32_t step, int32_t flags,
+                               int32_t *status, void *workspace, size_t workspace_bytes,
+                               void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
                    owner >= 0 && owner < n_owners && step >= 1,
@@ -1995,6 +2132,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && rows_buf &&
                    n_rows && hist && status,
                "dw_sgns_owner_out_catch_up: null pointer");
+    DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2");
+    const bool place = (flags & 1) != 0, p_only = (flags & 2) != 0;
     hipStream_t st = dw::as_stream(stream);
     const dw_step_scalars *dyn = nullptr;
     int32_t delta = 0;
@@ -2013,17 +2152,40 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
         dw::set_error("dw_sgns_owner_out_catch_up: counter reset failed");
         return DW_E_HIP;
     }
+    const int64_t T = (int64_t)a.C * (1 + a.K);
+    Workspace ws;
+    OwnerLayout lay;
+    PlaceSpace pl{};
+    if (place) {
+        rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
+                             "dw_sgns_owner_out_catch_up", vocab_size, nullptr, &pl);
+        if (rc != DW_OK) return rc;
+    }
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
+    auto *claim64 = reinterpret_cast<unsigned long long *>(claim);
     hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, claim, step, delta, rows_buf,
-                       reinterpret_cast<unsigned long long *>(n_rows));
+                       a, claim64, step, delta, rows_buf,
+                       reinterpret_cast<unsigned long long *>(n_rows), place ? pl.rank : nullptr);
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
-    // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1
-    const int64_t n_max = std::min<int64_t>(local_rows, a.batch * a.C * (1 + (int64_t)a.K));
-    return dw_adam_rows(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf, n_rows,
-                        n_max, nullptr, hist, step - 1, stream);
+    if (place) {   // every row's segment of the records: the scan of the step's counts
+        StepCountIter it(rocprim::counting_iterator<uint32_t>(0),
+                         StepCount{claim64, local_rows, dyn, delta, step});
+        size_t tb = pl.tmp_bytes;
+        if (rocprim::exclusive_scan(pl.tmp, tb, it, pl.off, 0u, static_cast<size_t>(local_rows + 1),
+                                    rocprim::plus<uint32_t>(), st) != hipSuccess) {
+            dw::set_error("dw_sgns_owner_out_catch_up: placement scan failed");
+            return DW_E_HIP;
+        }
+        hipLaunchKernelGGL(k_place_range, dim3(1), dim3(64), 0, st, pl.off, local_rows, ws.bounds);
+        DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/range");
+    }
+    // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1 (p_only:
+    // only p is written back; the lazy gather replays m and v itself, cheaply, before the step)
+    const int64_t n_max = std::min<int64_t>(local_rows, a.batch * T);
+    return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
+                                n_rows, n_max, nullptr, hist, step - 1, p_only, st);
 }
 
 int dw_sgns_timing(int32_t enable) {
@@ -2175,12 +2337,16 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
     DW_REQUIRE(lay.total < 0x7FFFFFFF, "dw_sgns_owner_workspace_bytes: too many records");
     Workspace ws;
     OccSpace occ;
+    PlaceSpace pl;
     char dummy;
     int rc = plan_workspace(lay.total > 0 ? lay.total : 1, local_rows, &dummy, &ws, nullptr);
     if (rc != DW_OK) return rc;
+    rc = plan_place(n_centres * (int64_t)n_ctx * (1 + neg_samples), local_rows, &dummy, &pl,
+                    nullptr);
+    if (rc != DW_OK) return rc;
     rc = plan_occ(n_centres > 0 ? n_centres : 1, vocab_size, &dummy, &occ, nullptr);
     if (rc != DW_OK) return rc;
-    *bytes = ws.total + occ.total;
+    *bytes = ws.total + pl.total + occ.total;
     return DW_OK;
 }
 
@@ -2261,7 +2427,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t *status, void *workspace,
+                             int32_t step, int32_t flags, int32_t *status, void *workspace,
                              size_t workspace_bytes, int64_t *n_records, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
@@ -2269,13 +2435,15 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     DW_REQUIRE(w_in && w_out_local && g_out_local && m_out && v_out && last_step && hist &&
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
+    DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_pass2_lazy: flags must be a set of 1 | 2");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
+    oa.p_current = (flags & 2) != 0;
     const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
     if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
-                              dw::as_stream(stream));
+                              dw::as_stream(stream), (flags & 1) != 0);
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

@@ -35,7 +35,7 @@ DW_S_DUP_NEIGHBOR = 64
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -100,10 +100,11 @@ SIGNATURES = {
                                            ctypes.c_size_t, _p, _p]),
     'dw_sgns_owner_out_catch_up': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32,
                                                   _i32, _i64, _p, _u64, _u64, _p, _p, _p, _p, _p,
-                                                  _p, _p, _p, _i32, _p, _p]),
+                                                  _p, _p, _p, _i32, _i32, _p, _p,
+                                                  ctypes.c_size_t, _p]),
     'dw_sgns_owner_pass2_lazy': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p,
-                                                _p, _p, _p, _p, _i32, _p, _p, ctypes.c_size_t,
-                                                _p, _p]),
+                                                _p, _p, _p, _p, _i32, _i32, _p, _p,
+                                                ctypes.c_size_t, _p, _p]),
     'dw_sgns_walks_phase2_adam': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p,
                                                  _p, _p, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                                  _f32, _f32, _p, _p, ctypes.c_size_t, _p]),

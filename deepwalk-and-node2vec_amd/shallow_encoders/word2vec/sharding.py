@@ -760,9 +760,21 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = self.lazy_out and self._hip()
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
-        self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
+        # claim words {step of the last touch : 32 | slots : 32} (dw_sgns_owner_out_catch_up)
+        self._claim_out = (torch.zeros(self.S, dtype=torch.int64, device=self.device)
+                           if self.lazy_out else None)
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # one rank: the records placed by the claim (no sort before the lazy gather)
+        self.place = self.lazy_out and not self.multi
+        self._wd_seen = False   # any step with weight decay: the p-only catch-up no longer holds
+
+    def out_flags(self) -> int:
+        """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
+        records (one rank), 2 = the catch-up replays p only (no weight decay so far)."""
+        if not self.lazy_out:
+            return 0
+        return (1 if self.place else 0) | (0 if self._wd_seen else 2)
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
@@ -772,12 +784,15 @@ class OwnerLazyTables(OwnerTables):
         ``step``: the Adam step of that batch (default: the current one)."""
         if not self.lazy_out:
             return
+        from shallow_encoders.word2vec.sgns import workspace_for
         step = self.step_count if step is None else int(step)
         n, L = walks.shape
-        slots = n * (L - 2 * int(context_radius)) * 2 * int(context_radius) * (1 + int(neg_samples))
+        R, K = int(context_radius), int(neg_samples)
+        slots = n * (L - 2 * R) * 2 * R * (1 + K)
         cap = max(1, min(self.S, slots))
         if self._out_rows is None or self._out_rows.numel() < cap:
             self._out_rows = torch.empty(cap, dtype=torch.int32, device=self.device)
+        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_catch_up', _native.ptr(walks), n, L,
                          int(context_radius), int(neg_samples), self.V, self.d, self.rank,
@@ -785,8 +800,9 @@ class OwnerLazyTables(OwnerTables):
                          int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
                          _native.ptr(self._claim_out), _native.ptr(self._out_rows),
-                         _native.ptr(self._n_out), _native.ptr(self._hist),
-                         step, _native.ptr(status), _native.stream(self.device))
+                         _native.ptr(self._n_out), _native.ptr(self._hist), step,
+                         self.out_flags(), _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -830,6 +846,7 @@ class OwnerLazyTables(OwnerTables):
         current hyper-parameters; a change of lr (a scheduler) rewrites them from step t."""
         self.step_count += 1
         s = self.step_count
+        self._wd_seen = self._wd_seen or self.weight_decay != 0
         key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
         if s > self._hist_ready or key != self._hist_key:
             self._write_hist(s, s + HIST_AHEAD - 1)
@@ -997,7 +1014,7 @@ class OwnerLazyTables(OwnerTables):
         spec = super().out_adam_spec()
         if spec is not None and self.lazy_out:
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                    'step': self.step_count}
+                    'step': self.step_count, 'flags': self.out_flags()}
         return spec
 
     def full_w_out(self) -> torch.Tensor:
@@ -1026,7 +1043,8 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
-                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True)
+                     grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
+                     placed=bool(tables.out_flags() & 1))
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,
