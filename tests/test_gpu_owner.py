@@ -348,11 +348,14 @@ def test_rows_adam_replay_is_bit_exact(hip_device, d, wd):
 
 
 def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=False,
-                   snaps=None):
+                   snaps=None, wd=0.0, configure=None):
     """(lazy tables after the run, per-step record counts) over walks_all [steps, n, L];
-    ``snaps``: a list receiving _owner_snapshot after every step."""
+    ``snaps``: a list receiving _owner_snapshot after every step; ``configure``: called on the
+    fresh tables (e.g. to select the out slice's catch-up forms)."""
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
-    t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out)
+    t = OwnerLazyTables(V, d, device, lr=lr, init_seed=4, lazy_out=lazy_out, weight_decay=wd)
+    if configure is not None:
+        configure(t)
     n, L = walks_all.shape[1:]
     per = L - 2 * R
     acc = torch.zeros(4, dtype=torch.float64, device=device)
@@ -369,23 +372,27 @@ def _lazy_vs_dense(device, walks_all, V, d, R, K, lr, world=1, rank=0, lazy_out=
     return t, acc
 
 
-@pytest.mark.parametrize('lazy_out', [False, True])
-def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out):
+@pytest.mark.parametrize('lazy_out,wd', [(False, 0.0), (True, 0.0), (True, 0.01)])
+def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, wd):
     """One rank: sparse batches (most rows untouched for several steps) through the lazy
     protocol equal dense training (ShardedTables + dw_adam_dense every step) after a flush;
-    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary)."""
+    lazy_out: the out slice's Adam deferred too (dw_sgns_owner_pass2_lazy, k_lazy_boundary),
+    with the records placed by the claim and the p-only catch-up (m, v replayed in the gather);
+    with weight decay the catch-up replays p, m and v (m, v then read p)."""
     from shallow_encoders.word2vec.sharding import ShardedTables
     V, d, R, K, L, n, steps, lr = 5000, 64, 2, 3, 12, 16, 6, 0.01
     walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(3),
                           dtype=torch.int32)
-    ref = ShardedTables(V, d, hip_device, lr=lr, init_seed=4)
+    ref = ShardedTables(V, d, hip_device, lr=lr, init_seed=4, weight_decay=wd)
     per = L - 2 * R
     acc_ref = torch.zeros(4, dtype=torch.float64, device=hip_device)
     for s in range(steps):
         sgns_accumulate(ref.w_in, ref.w_out, ref.g_in, ref.g_out, K, walks=walks[s].cuda(),
                         context_radius=R, seed=11, noise_offset=s * n * per, loss_acc=acc_ref)
         ref.step()
-    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out)
+    t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out, wd=wd)
+    if lazy_out:
+        assert t.out_flags() == (1 if wd else 3)
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
     if lazy_out:
@@ -544,3 +551,31 @@ def test_owner_prepare_touched_rows(hip_device, n_walks):
     # (a hub's run of centres spans several waves: its row's atomics may add in either order)
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize('d', [64, 128])
+def test_placed_records_equal_sorted_records(hip_device, d):
+    """The one-rank lazy out slice with the records placed by the claim (no sort) and the p-only
+    catch-up equals the form with the records sorted and the full catch-up: every row stepped at
+    the same steps (last_out equal) and the tables equal up to the order a row's records are
+    summed in (the claim's CAS order vs the sort's node order)."""
+    V, R, K, L, n, steps, lr = 3000, 2, 4, 14, 24, 8, 0.02
+    walks = torch.randint(1, V, (steps, n, L), generator=torch.Generator().manual_seed(17),
+                          dtype=torch.int32)
+
+    def sorted_full(t):
+        t.place = False
+        t._wd_seen = True   # full catch-up (the form weight decay needs)
+    runs = []
+    for cfg in (None, sorted_full):
+        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, configure=cfg)
+        assert t.out_flags() == (3 if cfg is None else 0)
+        runs.append((t.last_out.clone(), t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(),
+                     acc.cpu().numpy()))
+    (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
+    assert torch.equal(l0, l1)
+    np.testing.assert_allclose(a0, a1, rtol=1e-6)
+    for got, exp in ((i0, i1), (o0, o1)):
+        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
+                            max_abs=2.05 * lr * steps)
+        assert_no_row_drift(got, exp)
