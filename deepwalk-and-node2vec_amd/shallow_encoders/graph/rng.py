@@ -215,6 +215,7 @@ class DeviceMT:
         self.scratch = torch.empty(625, dtype=torch.int32, device=self.device)
         self.index = None if device_index else int(index)
         self.n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        self._ws = None   # this generator's own jump workspace (no sharing across streams)
 
     @classmethod
     def from_random(cls, device=None, rng: random.Random = None, **kw) -> 'DeviceMT':
@@ -227,20 +228,34 @@ class DeviceMT:
         words, index = _torch_state_words(torch.get_rng_state())
         return cls(words, index, device, **kw)
 
-    def _draw(self, mode: int, n: int, out: torch.Tensor, high: int = 0) -> torch.Tensor:
+    def _plan(self, mode: int, n: int):
+        """(stride, jump positions, offsets, table chains, workspace) of a draw of n values
+        (a device index plans for the largest index, 624)."""
         from shallow_encoders import _native
-        n = int(n)
         wpd = 1 if mode == 1 else 2
         idx = 624 if self.index is None else self.index
         windows = (idx + wpd * n - 1) // 624 + 1 if n > 0 else 1
         per = -(-windows // max(1, CHAINS_PER_CU * self.n_cu))
         stride = max(MIN_CHAIN_WINDOWS, -(-per // 64) * 64)
         chains = -(-windows // stride)
-        pos = off = ws = None
-        n_tab = 1
-        if chains > 1:
-            pos, off, n_tab = mt_jump_table(self.device, stride, chains)
-            ws = mt_workspace(self.device, chains)
+        if chains <= 1:
+            return stride, None, None, 1, None
+        pos, off, n_tab = mt_jump_table(self.device, stride, chains)
+        words = int(_native.load().dw_mt_workspace_words(int(chains)))
+        if self._ws is None or self._ws.numel() < words:
+            self._ws = torch.empty(words, dtype=torch.int32, device=self.device)
+        return stride, pos, off, n_tab, self._ws
+
+    def reserve(self, n: int, high: int = 0) -> None:
+        """Build the jump table and workspace a draw of n values needs (uniforms: high = 0;
+        randint: its high) ahead of time, e.g. before the draw is captured into a graph."""
+        self._plan(0 if not high else (1 if int(high) < (1 << 28) else 2), int(n))
+
+    def _draw(self, mode: int, n: int, out: torch.Tensor, high: int = 0) -> torch.Tensor:
+        from shallow_encoders import _native
+        n = int(n)
+        wpd = 1 if mode == 1 else 2
+        stride, pos, off, n_tab, ws = self._plan(mode, n)
         with torch.cuda.device(self.device):
             _native.call('dw_mt_draw', mode, _native.ptr(self.state),
                          -1 if self.index is None else self.index, n, _native.ptr(out),

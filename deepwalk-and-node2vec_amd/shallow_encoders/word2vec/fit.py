@@ -118,8 +118,9 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
         graph_unroll: int = 16) -> Dict[str, float]:
     """Train for ``max_epochs``; returns the last epoch's metric means.
 
-    Device walk batches with a Philox walker and device negatives (``noise: device``) are
-    replayed ``graph_unroll`` steps per HIP graph after each epoch's first (eager) batch
+    Device walk batches (Philox walks or the reference's own, rng='python'; device or torch
+    negatives) are replayed ``graph_unroll`` steps per HIP graph after each epoch's first (eager)
+    batch
     (GraphedTrainerStep), without a Python launch per kernel. The trailing batches that do not
     fill a graph, and everything else, run eagerly. The replayed steps train the same batches with
     the same update, but with DW_TRAIN_GRAPH_SCATTER='auto' (the default) a batch of at most
@@ -178,6 +179,7 @@ def fit(trainer: Word2VecTrainer, dataloader: Iterable, max_epochs: int,
                         global_step += graph_unroll
                         n_batches += graph_unroll
                     torch.cuda.current_stream().synchronize()
+                    gs.release_rng()   # the reference's streams back to random / torch
                     from shallow_encoders import _native
                     _native.check_status(gs.status, 'graphed training steps')
                 while True:

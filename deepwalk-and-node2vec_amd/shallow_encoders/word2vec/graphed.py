@@ -309,8 +309,15 @@ class GraphedTrainerStep:
     ``unroll`` steps, with the walker launch for all of them at its head: the reference configs'
     64-walk batches are launch-bound when stepped from Python one kernel at a time.
 
-    Eligible (``eligible``): a RandomWalkDataset with a Philox walker, ``noise='device'``,
-    ``manual_grads``, the HIP Adam holding exactly the two tables, no ``max_norm``. The step is
+    Eligible (``eligible``): a RandomWalkDataset, ``manual_grads``, the HIP Adam holding exactly
+    the two tables, no ``max_norm``. The walks are the Philox walker's, or (``rng='python'``) the
+    reference's own: the walker's CPython random.random() stream generated in HBM by a generator
+    whose state stays there across replays (graph/rng.py DeviceMT, the index read on the device),
+    then the bit-exact replay walker. The negatives are the device Philox stream
+    (``noise='device'``) or the reference's own (``noise='torch'``): torch.randint on the CPU
+    generator's stream, likewise generated in HBM (DeviceMT.randint) for all the graph's steps at
+    its head. The Python and torch generators get their states back on ``release_rng`` (fit calls
+    it after the replays), exactly where the eager steps would have left them. The step is
     the trainer's own: the fused records step (the out table's Adam in the gather, the in
     table's on the side stream) or, for batches of <= 65,536 records, the atomic output-table
     scatter followed by ``optimizer.step()`` (bench.py's ``--scatter auto`` rule). What changes
@@ -334,7 +341,8 @@ class GraphedTrainerStep:
                 and len(opt.param_groups) == 1):
             return False
         mine = {id(p) for p in opt.param_groups[0]['params']}
-        return (getattr(walker, '_rng', None) == 'philox' and trainer._noise_mode == 'device'
+        return (getattr(walker, '_rng', None) in ('philox', 'python')
+                and trainer._noise_mode in ('device', 'torch')
                 and trainer.manual_grads and trainer.model.max_norm is None
                 and mine == {id(w_in), id(w_out)} and w_in.device.type == 'cuda'
                 and trainer._context_radius is not None)
@@ -350,8 +358,8 @@ class GraphedTrainerStep:
         if unroll < 2 or unroll % 2:
             raise ValueError('GraphedTrainerStep: unroll must be even and >= 2')
         if not self.eligible(trainer, dataset):
-            raise ValueError('GraphedTrainerStep: needs a Philox walker, noise=device, '
-                             'manual_grads and the fusable HIP Adam (see eligible)')
+            raise ValueError('GraphedTrainerStep: needs a walk-batch dataset, manual_grads and '
+                             'the fusable HIP Adam (see eligible)')
         if not trainer.optimizer.can_fuse([trainer.model.input_weight,
                                            trainer.model.output_weight]):
             raise ValueError('GraphedTrainerStep: run one eager step first (gradient buffers, '
@@ -396,6 +404,20 @@ class GraphedTrainerStep:
         self.starts = torch.empty(self.unroll * self.B, dtype=torch.int32, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        # the reference's own streams, generated in HBM from generators held there across replays
+        from shallow_encoders.graph.rng import DeviceMT
+        self.mt_walks = self.mt_noise = self.uniforms = self.noise = None
+        if self.walker._rng == 'python':
+            self.uniforms = torch.empty(self.unroll * self.B * (L - 1), dtype=torch.float64,
+                                        device=dev)
+            self.mt_walks = DeviceMT.from_random(dev, device_index=True)
+            self.mt_walks.reserve(self.uniforms.numel())
+        if trainer._noise_mode == 'torch':
+            self.V = int(w_in.shape[0])
+            self.noise = torch.empty((self.unroll, self.centres, 2 * R, K), dtype=torch.int64,
+                                     device=dev)
+            self.mt_noise = DeviceMT.from_torch(dev, device_index=True)
+            self.mt_noise.reserve(self.noise.numel(), self.V)
         torch.cuda.synchronize(dev)
         snap = ([opt.state[p]['step'].clone() for p in self._params], trainer._noise_offset,
                 w_in.data_ptr())
@@ -427,14 +449,26 @@ class GraphedTrainerStep:
                          self.epoch_starts.numel(), _native.ptr(self.starts), self.starts.numel(),
                          _native.stream(dev))
         _native.call('dw_step_scalars_bind', self._step_blk(0))
-        self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
-                               status=self.status)
+        if self.mt_walks is not None:   # the next unroll * B walks' uniforms, in walk order
+            self.mt_walks.uniforms(self.uniforms.numel(), out=self.uniforms)
+            self.walker.walk_batch(self.starts, uniforms=self.uniforms, out=self.walks,
+                                   check=False, status=self.status)
+        else:
+            self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
+                                   status=self.status)
+        if self.mt_noise is not None:   # every step's generate_noise_batch, in step order
+            self.mt_noise.randint(self.V, self.noise.numel(), out=self.noise.view(-1))
         opt = self.trainer.optimizer
-        for k in range(self.unroll):
-            _native.call('dw_step_scalars_bind', self._step_blk(k))
-            self.trainer.training_step(self.walks[k * B:(k + 1) * B])
-            opt.step()
-            opt.zero_grad()
+        try:
+            for k in range(self.unroll):
+                _native.call('dw_step_scalars_bind', self._step_blk(k))
+                if self.noise is not None:
+                    self.trainer._noise_override = self.noise[k]
+                self.trainer.training_step(self.walks[k * B:(k + 1) * B])
+                opt.step()
+                opt.zero_grad()
+        finally:
+            self.trainer._noise_override = None
 
     def replay(self) -> dict:
         """``unroll`` training steps; returns their mean loss terms (device tensors)."""
@@ -454,6 +488,15 @@ class GraphedTrainerStep:
         t._noise_offset += self.unroll * self.centres
         self.dataset._index += self.unroll * self.B
         return loss_terms(self.acc, self.unroll * self.centres * 2 * self.R, self.K)
+
+    def release_rng(self) -> None:
+        """Hand the walk and noise streams back to CPython's ``random`` and torch's CPU
+        generator (synchronises): after it they stand where the replayed steps, run eagerly, would
+        have left them. Call it before anything else draws from either."""
+        if self.mt_walks is not None:
+            self.mt_walks.to_random()
+        if self.mt_noise is not None:
+            self.mt_noise.to_torch()
 
 
 def epoch_starts_node_order(n_nodes: int, walks_per_node: int, device) -> torch.Tensor:

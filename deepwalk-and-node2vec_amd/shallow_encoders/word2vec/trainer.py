@@ -86,6 +86,9 @@ class Word2VecTrainer(_Base):
         # _capture_scatter = 'atomic' takes the atomic output-table scatter (tiny batches)
         self._capture_acc = None
         self._capture_scatter = None
+        # set by GraphedTrainerStep for noise='torch': the step's negatives, already drawn on the
+        # device from torch's generator stream (graph/rng.py DeviceMT.randint)
+        self._noise_override = None
 
     # ---- reference properties -------------------------------------------------------------
     @property
@@ -143,6 +146,8 @@ class Word2VecTrainer(_Base):
     def _noise(self, n_centres: int, n_ctx: int, device) -> Union[torch.Tensor, None]:
         if self._noise_mode == 'device':
             return None
+        if self._noise_override is not None:
+            return self._noise_override
         noise = generate_noise_batch(n_centres, n_ctx, self._neg_samples, self._vocab_size)
         return noise.to(device, non_blocking=True)
 

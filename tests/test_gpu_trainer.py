@@ -300,3 +300,126 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
     for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
         np.testing.assert_allclose(l1[k], l0[k], rtol=3e-2)
         np.testing.assert_allclose(l2[k], l0[k], rtol=3e-2)
+
+
+def _karate_fit(f, graph: str, monkeypatch):
+    """The reference's karate node2vec trajectory (traj_karate_node2vec.npz: random.seed and
+    torch.manual_seed(seed), the dataset, SkipGram, Adam + StepLR per epoch, 64-walk batches,
+    noise from torch's generator) through word2vec/fit.py with the reference's own streams
+    (rng='python' walks, noise='torch'); graph='1' replays the middle batches of every epoch as
+    HIP graphs of 2 (GraphedTrainerStep: both streams generated in HBM)."""
+    import random
+    from shallow_encoders.config_parser.core import WalkBatchLoader
+    from shallow_encoders.word2vec.dataloader.torch_dataset import GraphDataset
+    from shallow_encoders.word2vec.fit import fit
+    monkeypatch.setenv('DW_TRAIN_GRAPH', graph)
+    seed = int(f['seed'])
+    random.seed(seed)
+    torch.manual_seed(seed)
+    ds = GraphDataset('graph_karate_club', context_radius=int(f['R']),
+                      additional_parameters={'walks_per_node': 8, 'walk_length': 10,
+                                             'method': 'node2vec',
+                                             'method_params': {'p': 1, 'q': 0.5}})
+    V, d = int(f['V']), int(f['d'])
+    model = SkipGram(V, d)
+    np.testing.assert_array_equal(model.input_embedding.numpy(), f['w_in0'])
+    model = model.cuda()
+    opt = Adam(model.parameters(), lr=float(f['lr']))
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=int(f['step_size']),
+                                            gamma=float(f['gamma']))
+    tr = Word2VecTrainer(model, opt, sched, neg_samples=int(f['K']), vocab_size=V, noise='torch',
+                         context_radius=int(f['R']))
+    epochs = []
+    orig = tr.on_train_epoch_end
+
+    def epoch_end():
+        out = orig()
+        epochs.append(out)
+        return out
+    tr.on_train_epoch_end = epoch_end
+    fit(tr, WalkBatchLoader(ds, 64), max_epochs=int(f['epochs']), verbose=False, graph_unroll=2)
+    return model, epochs, random.getstate(), torch.get_rng_state()
+
+
+def test_karate_trajectory_through_graphed_loop(hip_device, monkeypatch):
+    """the reference's configs with their own streams on the graphed loop. The
+    karate trajectory fixture (the reference's dataset, model, noise and StepLR) replayed through
+    fit() with graphs of 2 steps: per-epoch mean losses at the fixture's bar (rtol 1e-4), final
+    tables inside the reference's own envelope, and `random` / torch's generator left bit-equal
+    to the eager loop's (so every walk and negative was the reference's)."""
+    from shallow_encoders.word2vec import graphed
+    replays = []
+    orig = graphed.GraphedTrainerStep.replay
+
+    def counting(self):
+        replays.append((self.mt_walks is not None, self.mt_noise is not None))
+        return orig(self)
+    monkeypatch.setattr(graphed.GraphedTrainerStep, 'replay', counting)
+    f = golden('traj_karate_node2vec.npz')
+    model, epochs, py_state, t_state = _karate_fit(f, '1', monkeypatch)
+    assert replays == [(True, True)] * int(f['epochs'])   # one graph of 2 per epoch
+    eo = f['epoch_of_step']
+    for e, got in enumerate(epochs):
+        np.testing.assert_allclose(got['train-epoch/loss'], f['losses'][eo == e].mean(),
+                                   rtol=1e-4)
+    from oracle import sgns_ref
+    from test_gpu_sgns import assert_within_envelope, reference_envelope
+    offs = np.concatenate([[0], np.cumsum(f['batch_sizes'])])
+    batches, noff = [], 0
+    for step in range(len(f['batch_sizes'])):
+        ins, tgt = sgns_ref.sg_windows(f['walks'][offs[step]:offs[step + 1]], int(f['R']))
+        batches.append((ins, tgt, f['noise'][noff:noff + len(ins)], float(f['lrs'][step])))
+        noff += len(ins)
+    ex_in, ex_out = reference_envelope(f['w_in0'], f['w_out0'], float(f['lr']), batches)
+    lr = float(f['lr'])
+    assert_within_envelope(model.input_embedding.numpy(), f['w_in'], ex_in, lr, rtol=1e-4,
+                           atol=1e-5)
+    assert_within_envelope(model.output_embedding.numpy(), f['w_out'], ex_out, lr, rtol=1e-4,
+                           atol=1e-5)
+    _, eager_epochs, py_eager, t_eager = _karate_fit(f, '0', monkeypatch)
+    assert py_state == py_eager
+    assert torch.equal(t_state, t_eager)
+    for a, b in zip(epochs, eager_epochs):
+        np.testing.assert_allclose(a['train-epoch/loss'], b['train-epoch/loss'], rtol=1e-4)
+
+
+def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
+    """tools/train.py --config-name=sge_sg_cora on the Cora-shaped R-MAT with the reference's
+    own streams (rng: python walks, noise: torch) replays its steps as graphs of 16 and leaves
+    `random` and torch's generator exactly where the eager loop leaves them (the same walks and
+    negatives, step for step), with the same step count and epoch losses within the loop's
+    run-to-run envelope."""
+    import random
+    from tools import train as train_tool
+    from shallow_encoders.word2vec import graphed
+    replays = []
+    orig = graphed.GraphedTrainerStep.replay
+
+    def counting(self):
+        replays.append(self.unroll)
+        return orig(self)
+    monkeypatch.setattr(graphed.GraphedTrainerStep, 'replay', counting)
+    base = ['datamodule.dataset_name=graph_rmat', 'datamodule.additional_parameters.scale=12',
+            'datamodule.additional_parameters.n_edges=5429',
+            'datamodule.additional_parameters.graph_seed=0',
+            'datamodule.additional_parameters.walks_per_node=1',
+            'datamodule.additional_parameters.method_params.q=1',
+            'datamodule.additional_parameters.rng=python', 'train.noise=torch',
+            'model.embedding_size=128', 'train.optimizer.lr=0.01', 'train.max_epochs=2']
+    runs = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
+        out = str(tmp_path / f'runs{mode}')
+        random.seed(5)
+        torch.manual_seed(0)
+        last = train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
+                                f'output_dir={out}', f'train.experiment=g{mode}'] + base)
+        ck = os.path.join(out, 'graph_rmat', f'g{mode}', 'checkpoints', 'last.ckpt')
+        state = torch.load(ck, weights_only=True)
+        runs.append((last, state, random.getstate(), torch.get_rng_state()))
+    assert replays == [16] * 6
+    (l0, s0, r0, t0), (l1, s1, r1, t1) = runs
+    assert s0['global_step'] == s1['global_step'] == 128
+    assert r0 == r1 and torch.equal(t0, t1)
+    for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
+        np.testing.assert_allclose(l1[k], l0[k], rtol=3e-2)
