@@ -766,8 +766,10 @@ class OwnerLazyTables(OwnerTables):
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
         # one rank: the records placed by the claim (no sort before the lazy gather)
-        self.place = self.lazy_out and not self.multi
-        self._wd_seen = False   # any step with weight decay: the p-only catch-up no longer holds
+        self.place = (self.lazy_out and not self.multi
+                      and os.environ.get('DW_OUT_PLACE', '1') != '0')   # (A/B, round 4)
+        # any step with weight decay: the p-only catch-up no longer holds
+        self._wd_seen = os.environ.get('DW_OUT_P_ONLY', '1') == '0'   # (A/B, round 4)
 
     def out_flags(self) -> int:
         """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
