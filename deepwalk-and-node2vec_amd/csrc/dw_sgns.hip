@@ -32,8 +32,6 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "dw_common.h"
 
@@ -714,6 +712,8 @@ struct OutAdam {
     const dw_step_scalars *dyn = nullptr;   // bound step block: the scalars come from it
     int32_t step_delta = 0;                 //   lazy form: step = dyn->step + step_delta
     bool p_current = false;   // lazy form: the catch-up brought p (not m, v, last) to step - 1
+    bool betas_const = false; //   and every step had the same betas: m, v replay with step's
+    uint32_t *counts = nullptr;   // placed records: the rows' counts, cleared as they step
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -737,15 +737,29 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
     if (oa.p_current) {
         // p is at step - 1 already (the p-only catch-up): m and v replay their g = 0 steps — the
         // same two IEEE operations adam_elem_g0 applies to them, one multiply-add each (the
-        // host enables this only while every step has weight_decay 0: then m, v never read p)
-        for (int32_t t = from + 1; t < step; ++t) {
-            const float *h = oa.hist + 8 * static_cast<int64_t>(t);
+        // host enables this only while every step has weight_decay 0: then m, v never read p);
+        // with constant betas the scalars are this step's (no history load per step)
+        if (oa.betas_const) {
+            const float *h = oa.hist + 8 * static_cast<int64_t>(step);
             const float w1 = h[0], b2 = h[1];
+            for (int32_t t = from + 1; t < step; ++t) {
 #pragma unroll
-            for (int m = 0; m < VPL; ++m) {
+                for (int m = 0; m < VPL; ++m) {
 #pragma clang fp contract(off)
-                mm[m] = fmaf(w1, -mm[m], mm[m]);
-                vv[m] = vv[m] * b2;
+                    mm[m] = fmaf(w1, -mm[m], mm[m]);
+                    vv[m] = vv[m] * b2;
+                }
+            }
+        } else {
+            for (int32_t t = from + 1; t < step; ++t) {
+                const float *h = oa.hist + 8 * static_cast<int64_t>(t);
+                const float w1 = h[0], b2 = h[1];
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) {
+#pragma clang fp contract(off)
+                    mm[m] = fmaf(w1, -mm[m], mm[m]);
+                    vv[m] = vv[m] * b2;
+                }
             }
         }
     } else {
@@ -773,7 +787,10 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
         oa.m[i] = mm[m];
         oa.v[i] = vv[m];
     }
-    if (lane == 0) oa.last[row] = step;
+    if (lane == 0) {
+        oa.last[row] = step;
+        if (oa.counts) oa.counts[row] = 0u;   // placed records: the count back to zero
+    }
 }
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
@@ -1616,36 +1633,19 @@ int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t 
     return DW_OK;
 }
 
-// A row's slot count this step (0 unless its claim word carries the step): the scan's input.
-struct StepCount {
-    const unsigned long long *claim;
-    int64_t n_rows;
-    const dw_step_scalars *dyn;
-    int32_t delta, step;
-    __device__ uint32_t operator()(uint32_t r) const {
-        if (r >= n_rows) return 0u;
-        const unsigned long long c = claim[r];
-        return (c >> 32) == static_cast<uint32_t>(dw::eff_step(dyn, delta, step))
-                   ? static_cast<uint32_t>(c) : 0u;
-    }
-};
-
 // the records' placement (k_out_claim's ranks, one owner or many): rank[slot], off[row] (the
-// exclusive scan of the step's per-row counts, off[local_rows] = their total) and the scan's
-// temporary storage; between the records part and OccSpace
+// exclusive scan of the per-row counts, with one zero past the rows: off[local_rows] = their
+// total) and the scan's temporary storage; between the records part and OccSpace
 struct PlaceSpace {
     uint32_t *rank, *off;
     void *tmp;
     size_t tmp_bytes, total;
 };
 
-using StepCountIter =
-    rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, StepCount, uint32_t>;
-
 int plan_place(int64_t n_slots, int64_t local_rows, void *base, PlaceSpace *pl, hipStream_t st) {
     size_t tmp = 0;
-    StepCountIter it(rocprim::counting_iterator<uint32_t>(0), StepCount{});
-    if (rocprim::exclusive_scan(nullptr, tmp, it, static_cast<uint32_t *>(nullptr), 0u,
+    if (rocprim::exclusive_scan(nullptr, tmp, static_cast<const uint32_t *>(nullptr),
+                                static_cast<uint32_t *>(nullptr), 0u,
                                 static_cast<size_t>(local_rows + 1), rocprim::plus<uint32_t>(),
                                 st) != hipSuccess) {
         dw::set_error("dw_sgns_owner: placement scan size query failed");
@@ -2028,24 +2028,24 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // Lazy out slice (dw_sgns_owner_out_catch_up), before pass 1: every owned output row a slot of
 // this batch references must be brought current to step - 1 (its deferred g = 0 steps replayed
 // through adam_elem with hist's scalars), so pass 1 reads the rows the dense update would hold.
-// This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64). Each owned
-// row has a 64-bit claim word {step of its last touch : 32, slots of that step : 32}, updated by
-// CAS: the first slot of a step to reach a row restarts the count at 1, the others add 1. The
-// first toucher lists the row when its last touch is older than step - 1 (a row the previous
-// step touched held a record there, so its lazy gather already brought it to step - 1); the
-// wave's listed rows are appended to `list` with one counter atomic per block. dw_adam_rows then
-// replays the listed rows, all in parallel.
-// Placement (rank != NULL): the count a slot's CAS returned is its rank among the step's slots
-// of that row, kept per slot (rank[b * T + t]); an exclusive scan of the step's counts then gives
-// every row a segment of the records array, and pass 1 writes each record at off[row] + rank:
-// the records come out grouped by row with no sort (the 64-walk batch: 269K records, whose
-// radix sort was ~10 launches and ~85 us of the step). The order of a row's records is the order
-// the CAS loops resolved — as nondeterministic as the float atomics of rows that straddle two
-// gather chunks.
+// This kernel lists them once each: one wave per centre, lane t = slot t (T <= 64); a row is
+// claimed by exactly one lane in the launch — atomicMax(claim[row], step) returning < step — and
+// listed when its last claim is older than step - 1 (a row the previous step claimed held a
+// record there, so its lazy gather already brought it to step - 1); the wave's listed rows are
+// appended to `list` with one counter atomic per block. dw_adam_rows then replays the listed
+// rows, all in parallel.
+// Placement (count != NULL): every slot also adds 1 to its row's count (zero between steps: the
+// lazy gather clears the counts of the rows it steps); the value it got back is its rank among
+// the step's slots of that row, kept per slot (rank[b * T + t]). An exclusive scan of the counts
+// then gives every row a segment of the records array, and pass 1 writes each record at
+// off[row] + rank: the records come out grouped by row with no sort (the 64-walk batch: 269K
+// records, whose radix sort was ~10 launches and ~85 us of the step). The order of a row's
+// records is the order the atomics resolved — as nondeterministic as the float atomics of rows
+// that straddle two gather chunks. (The two atomics of a slot are independent: one round trip.)
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_out_claim(SgnsArgs a, unsigned long long *__restrict__ claim, int32_t step_arg,
-                int32_t delta, uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
-                uint32_t *__restrict__ rank) {
+    k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
+                uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
+                uint32_t *__restrict__ count, uint32_t *__restrict__ rank) {
     const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
     // one centre per wave; the block's claimed rows are appended with ONE counter atomic (a
     // same-address atomic per wave serialised: 4,480 of them were ~40 us at the 64-walk batch)
@@ -2056,7 +2056,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int T = a.C * (1 + a.K);
     const int64_t per = a.L - 2 * a.R;
-    const unsigned long long tag = static_cast<unsigned long long>(step) << 32;
     for (int64_t b0 = (int64_t)blockIdx.x * WAVES_PER_BLOCK; b0 < a.batch; b0 += n_waves) {
         const int64_t b = b0 + wv;   // block-uniform trip count (barriers below)
         bool mine = false;
@@ -2068,18 +2067,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                 dw::status_or(a.status, DW_S_BAD_INDEX);
             } else if (o % a.n_owners == a.owner) {
                 lo = static_cast<uint32_t>(o / a.n_owners);
-                unsigned long long old = claim[lo];
-                while (true) {
-                    const unsigned long long nw = (old >> 32) == static_cast<uint32_t>(step)
-                                                      ? old + 1ull : (tag | 1ull);
-                    const unsigned long long prev = atomicCAS(claim + lo, old, nw);
-                    if (prev == old) break;
-                    old = prev;
-                }
-                const int32_t seen = static_cast<int32_t>(old >> 32);
-                const bool first = seen != step;
-                mine = first && seen < step - 1;
-                if (rank) rank[b * T + lane] = first ? 0u : static_cast<uint32_t>(old);
+                mine = atomicMax(claim + lo, step) < step - 1;
+                if (count) rank[b * T + lane] = atomicAdd(count + lo, 1u);
             }
         }
         const unsigned long long mask = __ballot(mine);
@@ -2116,10 +2105,10 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
-                               int32_t *last_step, uint64_t *claim, uint32_t *rows_buf,
-                               int64_t *n_rows, const float *hist, int32_t step, int32_t flags,
-                               int32_t *status, void *workspace, size_t workspace_bytes,
-                               void *stream) {
+                               int32_t *last_step, int32_t *claim, uint32_t *counts,
+                               uint32_t *rows_buf, int64_t *n_rows, const float *hist,
+                               int32_t step, int32_t flags, int32_t *status, void *workspace,
+                               size_t workspace_bytes, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
                    owner >= 0 && owner < n_owners && step >= 1,
@@ -2134,6 +2123,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                "dw_sgns_owner_out_catch_up: null pointer");
     DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2");
     const bool place = (flags & 1) != 0, p_only = (flags & 2) != 0;
+    DW_REQUIRE(!place || counts, "dw_sgns_owner_out_catch_up: placing needs the row counts");
     hipStream_t st = dw::as_stream(stream);
     const dw_step_scalars *dyn = nullptr;
     int32_t delta = 0;
@@ -2164,16 +2154,15 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
-    auto *claim64 = reinterpret_cast<unsigned long long *>(claim);
     hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, claim64, step, delta, rows_buf,
-                       reinterpret_cast<unsigned long long *>(n_rows), place ? pl.rank : nullptr);
+                       a, claim, step, delta, rows_buf,
+                       reinterpret_cast<unsigned long long *>(n_rows), place ? counts : nullptr,
+                       place ? pl.rank : nullptr);
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
-    if (place) {   // every row's segment of the records: the scan of the step's counts
-        StepCountIter it(rocprim::counting_iterator<uint32_t>(0),
-                         StepCount{claim64, local_rows, dyn, delta, step});
+    if (place) {   // every row's segment of the records: the scan of the counts (+ one zero)
         size_t tb = pl.tmp_bytes;
-        if (rocprim::exclusive_scan(pl.tmp, tb, it, pl.off, 0u, static_cast<size_t>(local_rows + 1),
+        if (rocprim::exclusive_scan(pl.tmp, tb, static_cast<const uint32_t *>(counts), pl.off, 0u,
+                                    static_cast<size_t>(local_rows + 1),
                                     rocprim::plus<uint32_t>(), st) != hipSuccess) {
             dw::set_error("dw_sgns_owner_out_catch_up: placement scan failed");
             return DW_E_HIP;
@@ -2427,17 +2416,21 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t flags, int32_t *status, void *workspace,
-                             size_t workspace_bytes, int64_t *n_records, void *stream) {
+                             int32_t step, int32_t flags, uint32_t *counts, int32_t *status,
+                             void *workspace, size_t workspace_bytes, int64_t *n_records,
+                             void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && local_rows >= 1 && neg_samples >= 0 && step >= 1,
                "dw_sgns_owner_pass2_lazy: bad sizes");
     DW_REQUIRE(w_in && w_out_local && g_out_local && m_out && v_out && last_step && hist &&
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
-    DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_pass2_lazy: flags must be a set of 1 | 2");
+    DW_REQUIRE((flags & ~7) == 0, "dw_sgns_owner_pass2_lazy: flags must be a set of 1 | 2 | 4");
+    DW_REQUIRE(!(flags & 1) || counts, "dw_sgns_owner_pass2_lazy: placed records need counts");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
     oa.p_current = (flags & 2) != 0;
+    oa.betas_const = (flags & 4) != 0;
+    oa.counts = (flags & 1) ? counts : nullptr;
     const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
     if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);

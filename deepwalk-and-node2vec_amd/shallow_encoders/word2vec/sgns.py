@@ -423,7 +423,8 @@ def sgns_owner_pass2(w_in: torch.Tensor, w_out_local: torch.Tensor, g_out_local:
                          _native.ptr(out_adam['m']), _native.ptr(out_adam['v']),
                          _native.ptr(out_adam['last']), _native.ptr(out_adam['hist']),
                          int(out_adam['step']), int(out_adam.get('flags', 0)),
-                         _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         _native.ptr(out_adam.get('counts')), _native.ptr(status),
+                         _native.ptr(ws), ws.numel(),
                          None if out_adam.get('flags', 0) & 1 else n_rec_p,
                          _native.stream(dev))
         return int(n_rec.value) if read_count else None

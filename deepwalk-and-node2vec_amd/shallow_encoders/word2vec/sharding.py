@@ -760,9 +760,12 @@ class OwnerLazyTables(OwnerTables):
         self.lazy_out = self.lazy_out and self._hip()
         self.last_out = (torch.zeros(self.S, dtype=torch.int32, device=self.device)
                          if self.lazy_out else None)
-        # claim words {step of the last touch : 32 | slots : 32} (dw_sgns_owner_out_catch_up)
-        self._claim_out = (torch.zeros(self.S, dtype=torch.int64, device=self.device)
+        self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
+        # placed records: every row's slot count of the step (+ one zero past the rows), cleared
+        # by the lazy gather (dw_sgns_owner_out_catch_up / _pass2_lazy)
+        self._count_out = (torch.zeros(self.S + 1, dtype=torch.int32, device=self.device)
                            if self.lazy_out else None)
+        self._betas0 = tuple(self.betas)
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
         # one rank: the records placed by the claim (no sort before the lazy gather)
@@ -773,10 +776,13 @@ class OwnerLazyTables(OwnerTables):
 
     def out_flags(self) -> int:
         """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
-        records (one rank), 2 = the catch-up replays p only (no weight decay so far)."""
+        records (one rank), 2 = the catch-up replays p only (no weight decay so far), 4 = the
+        betas never changed (the gather's m, v replays need no history loads)."""
         if not self.lazy_out:
             return 0
-        return (1 if self.place else 0) | (0 if self._wd_seen else 2)
+        p_only = not self._wd_seen
+        return ((1 if self.place else 0) | (2 if p_only else 0)
+                | (4 if p_only and self._betas0 is not None else 0))
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
@@ -801,7 +807,8 @@ class OwnerLazyTables(OwnerTables):
                          self.world, self.S, _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._claim_out), _native.ptr(self._out_rows),
+                         _native.ptr(self._claim_out), _native.ptr(self._count_out),
+                         _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
                          self.out_flags(), _native.ptr(status), _native.ptr(ws), ws.numel(),
                          _native.stream(self.device))
@@ -849,6 +856,8 @@ class OwnerLazyTables(OwnerTables):
         self.step_count += 1
         s = self.step_count
         self._wd_seen = self._wd_seen or self.weight_decay != 0
+        if self.lazy_out and tuple(self.betas) != self._betas0:
+            self._betas0 = None   # the history's betas differ from step to step from now on
         key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)
         if s > self._hist_ready or key != self._hist_key:
             self._write_hist(s, s + HIST_AHEAD - 1)
@@ -1016,7 +1025,8 @@ class OwnerLazyTables(OwnerTables):
         spec = super().out_adam_spec()
         if spec is not None and self.lazy_out:
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
-                    'step': self.step_count, 'flags': self.out_flags()}
+                    'step': self.step_count, 'flags': self.out_flags(),
+                    'counts': self._count_out}
         return spec
 
     def full_w_out(self) -> torch.Tensor:

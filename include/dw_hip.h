@@ -440,14 +440,16 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
 /* The lazy out slice's catch-up, before dw_sgns_owner_pass1 of the same batch: every owned
  * output row a slot references (contexts from the walks, negatives as pass 1 draws them) is
  * brought current to step - 1 (its deferred g = 0 steps replayed, hist as above), so pass 1 reads
- * the rows the dense update holds. claim uint64 [local_rows] (zero-initialised, never reset):
- * {step of the row's last touch : 32 | slots of that step : 32}, advanced by CAS; a row last
- * touched before step - 1 is listed once, rows_buf uint32 [min(local_rows, B' * 2R(1+K))] and
- * n_rows (int64, device) receive the list, which is then replayed. flags (a bit set):
- *   1 = place the records: each slot's rank among its row's slots and the exclusive scan of the
- *       rows' counts go to `workspace` (the owner form's, dw_sgns_owner_workspace_bytes), for
- *       dw_sgns_owner_pass1 (order_ready | 2) and dw_sgns_owner_pass2_lazy (flags | 1): the
- *       records land grouped by row, no sort (the order of one row's records is the CAS order);
+ * the rows the dense update holds. claim int32 [local_rows] (zero-initialised, never reset): a
+ * row is listed once per step, claimed via atomicMax(claim[row], step), when its last claim is
+ * older than step - 1; rows_buf uint32 [min(local_rows, B' * 2R(1+K))] and n_rows (int64,
+ * device) receive the list, which is then replayed. flags (a bit set):
+ *   1 = place the records: counts uint32 [local_rows + 1] (zero-initialised; the lazy gather
+ *       clears the rows it steps, so it is zero between steps) counts every row's slots, each
+ *       slot's rank among them and the exclusive scan of the counts go to `workspace` (the owner
+ *       form's, dw_sgns_owner_workspace_bytes), for dw_sgns_owner_pass1 (order_ready | 2) and
+ *       dw_sgns_owner_pass2_lazy (flags | 1, the same counts): the records land grouped by row,
+ *       no sort (the order of one row's records is the order the atomics resolved);
  *   2 = replay p only: m, v and last_step stay behind, and dw_sgns_owner_pass2_lazy (flags | 2)
  *       replays m and v (a multiply each per step) before the step — valid while every step has
  *       weight_decay 0.
@@ -457,10 +459,10 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                                int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                                const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                                float *w_out_local, float *m_out, float *v_out,
-                               int32_t *last_step, uint64_t *claim, uint32_t *rows_buf,
-                               int64_t *n_rows, const float *hist, int32_t step, int32_t flags,
-                               int32_t *status, void *workspace, size_t workspace_bytes,
-                               void *stream);
+                               int32_t *last_step, int32_t *claim, uint32_t *counts,
+                               uint32_t *rows_buf, int64_t *n_rows, const float *hist,
+                               int32_t step, int32_t flags, int32_t *status, void *workspace,
+                               size_t workspace_bytes, void *stream);
 
 /* dw_sgns_owner_pass2 with the out slice's Adam kept LAZY and exact (OwnerLazyTables, small
  * batches): a row no record touched is not read or written; its deferred g = 0 steps are
@@ -468,14 +470,16 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * through the same adam_elem, so the slice equals the dense update bit for bit once flushed
  * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
  * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
- * flags: 1 = the records were placed (see dw_sgns_owner_out_catch_up; n_records NULL), 2 = the
- * catch-up replayed p only (m, v are replayed here). */
+ * flags: 1 = the records were placed (see dw_sgns_owner_out_catch_up; n_records NULL; counts:
+ * its row counts, cleared here as the rows step), 2 = the catch-up replayed p only (m, v are
+ * replayed here), 4 = every step so far had the same betas (those replays use this step's). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,
                              float *m_out, float *v_out, int32_t *last_step, const float *hist,
-                             int32_t step, int32_t flags, int32_t *status, void *workspace,
-                             size_t workspace_bytes, int64_t *n_records, void *stream);
+                             int32_t step, int32_t flags, uint32_t *counts, int32_t *status,
+                             void *workspace, size_t workspace_bytes, int64_t *n_records,
+                             void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */
