@@ -269,6 +269,11 @@ def main():
     ap.add_argument('--exact-prefetch', default='on', choices=['on', 'off'],
                     help='exact-walk steps: generate the next step\'s uniforms and walks on a '
                          'side stream during this step\'s SGNS')
+    ap.add_argument('--verify-step', default='auto', choices=['auto', 'on', 'off'],
+                    help='after the timed steps, check one more step on a sample of rows against '
+                         'a float64 restatement of the reference step from the full tables '
+                         '(word2vec/verify.py; every rank gathers them); exit non-zero on a miss. '
+                         'auto = on for the owner layout with collectives (the N > 1 lines)')
     ap.add_argument('--walk-prefetch', action='store_true',
                     help='generate the next batch\'s walks on a side stream during this step\'s '
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
@@ -465,7 +470,7 @@ def main():
     step_idx = [0]
     fuse = not args.no_fuse_adam and args.scatter == 'sorted' and tables.can_fuse_out_adam()
     pieces = dist_on and not args.no_out_pieces and not owner
-    ev = {k: [] for k in ('walk', 'sgns', 'adam')}
+    ev = {k: [] for k in ('walk', 'sgns', 'adam', 'gather')}
     pb = sgns_phase_bytes(B, L, R, K, d, V, args.scatter, fuse)
     p2_bytes = pb['sort'] + pb['pass2']        # the phase the in-table Adam overlaps
 
@@ -485,6 +490,10 @@ def main():
             a0 = g0 + tables.rank * B
             own = walks_buf[tables.rank * B:(tables.rank + 1) * B]
             walker.walk_batch(step_starts(a0, B, starts_buf), walk_id0=a0, out=own, check=False)
+            if record:
+                eg = torch.cuda.Event(enable_timing=True)
+                eg.record()
+                ev['gather'].append((eg, e[1]))
             send = own if backend == 'nccl' else own.clone()
             dist.all_gather_into_tensor(walks_buf.view(-1), send.reshape(-1))
             walks = walks_buf
@@ -658,7 +667,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     _native.check_status(status, 'bench')
-    kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items() if v}
     if graphed is not None:   # one replay = `unroll` steps
         kern_ms = {k: v / graphed.unroll for k, v in kern_ms.items()}
 
@@ -699,7 +708,8 @@ def main():
         et = time.perf_counter() - ta
         _native.check_status(status, 'bench exact walks')
         loss_acc.copy_(loss_keep)
-        ekern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+        ekern = {k: float(np.mean([a.elapsed_time(b) for a, b in v]))
+                 for k, v in ev.items() if v}
         exact = {'value': pairs_per_step * n_exact / et, 'steps': n_exact,
                  'ms_per_step': et / n_exact * 1e3, 'vs_philox_step': (et / n_exact) /
                  (elapsed / args.steps), 'prefetch': args.exact_prefetch == 'on',
@@ -707,6 +717,43 @@ def main():
                  'walker': ('dw_mt_draw (CPython random.random() from a resident MT19937 state) '
                             '+ ' + ('dw_walk_replay_indexed' if args.method == 'node2vec'
                                     else 'dw_walk_replay_inline'))}
+
+    # ---- one more step, checked on a sample of rows ---------------------------
+    # every rank gathers the full tables before and after it; rank 0 restates the step in float64
+    # for ~256 in rows and ~256 out rows and holds them to the single-step bars. DW_BENCH_CORRUPT=1
+    # perturbs one sampled out row in the last rank's shard after the step: the check must fail.
+    step_check = None
+    want_check = (args.verify_step == 'on' or
+                  (args.verify_step == 'auto' and owner and dist_on))
+    if want_check and owner and not emulate and graphed is None and \
+            args.owner_walks == 'gather' and V * d * 4 * 6 <= (16 << 30):
+        from shallow_encoders.word2vec import verify
+        loss_keep = loss_acc.clone()
+        g0 = step_idx[0] * BG
+        pre = tables.full_state()
+        one_step(False)
+        torch.cuda.synchronize(dev)
+        _native.check_status(status, 'bench step check')
+        walks_chk = walks_buf.clone()
+        rows_in, rows_out = verify.sample_rows(walks_chk, R, K, V, 99, g0 * (L - 2 * R), 256)
+        if os.environ.get('DW_BENCH_CORRUPT') == '1' and tables.rank == tables.world - 1:
+            bad = rows_out[rows_out % tables.world == tables.rank][0]
+            tables.m_out[int(bad) // tables.world] += 1e-3   # a corrupted shard row (test aid)
+        post = tables.full_state()
+        loss_acc.copy_(loss_keep)
+        if rank == 0:
+            gi, go = verify.sampled_grads(pre[0], pre[3], walks_chk, R, K, 99, g0 * (L - 2 * R),
+                                          rows_in, rows_out)
+            kw = dict(step=tables.step_count, lr=args.lr, betas=tables.betas, eps=tables.eps,
+                      weight_decay=tables.weight_decay)
+            res = {'in': verify.check_rows(gi, tuple(x[rows_in] for x in pre[:3]),
+                                           tuple(x[rows_in] for x in post[:3]), **kw),
+                   'out': verify.check_rows(go, tuple(x[rows_out] for x in pre[3:]),
+                                            tuple(x[rows_out] for x in post[3:]), **kw)}
+            step_check = dict(verify.summarize(res), rows_in=int(rows_in.numel()),
+                              rows_out=int(rows_out.numel()), step=tables.step_count)
+        del pre, post
+        torch.cuda.empty_cache()
     if owner and dist_on:               # each rank summed the loss terms of its own slots
         dist.all_reduce(loss_acc)
     terms = loss_terms(loss_acc, pairs_per_step * args.steps * (W_eff if owner else 1), K)
@@ -940,6 +987,15 @@ def main():
         'kernel_ms': kern_ms,
         'records_per_step_per_gpu': n_rec[0] if owner else pairs_per_step * (1 + K),
         'mean_loss': mean_loss,
+        'rccl_world': dist.get_world_size() if dist_on else None,
+        'exposed_collective_ms_per_step': ({
+            'walks_allgather': kern_ms.get('gather'),
+            'after_output_phase': kern_ms.get('adam'),
+            'note': ('walks_allgather: the all-gather of the node-range walks (main stream); '
+                     'after_output_phase: from the end of the output-table phase to the in '
+                     'table being current (the exchange not hidden behind sort + pass 2, plus the '
+                     'touched-row update in the lazy exchange)')} if owner and dist_on else None),
+        'step_check': step_check,
         'value_exact_walks': exact['value'] if exact else None,
         'exact_walks': exact,
         'roofline': {
@@ -998,9 +1054,16 @@ def main():
         result['cpu_baseline'] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)
+    failed = bool(step_check) and not step_check['ok']
     if dist_on:
+        flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)   # every rank exits with rank 0's verdict
+        failed = bool(flag.item())
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        log(rank, f'[bench] step check FAILED: {step_check}')
+        sys.exit(3)
 
 
 if __name__ == '__main__':

@@ -579,6 +579,34 @@ class OwnerTables:
                 self.w_out = w
         return tuple(res)
 
+    def in_state_full(self):
+        """(m, v) of the in table as full (V, d) tensors: the node-range shards all-gathered
+        (collective when N > 1)."""
+        if self.emulated:
+            raise RuntimeError('an emulated rank holds only its own shard')
+        if not self.multi:
+            return self.m_in[:self.V].clone(), self.v_in[:self.V].clone()
+        res = []
+        for t in (self.m_in, self.v_in):
+            full = torch.empty((self.world * self.S, self.d), dtype=torch.float32,
+                               device=self.device)
+            if dist.get_backend(self.group) == 'nccl':
+                dist.all_gather_into_tensor(full.view(-1), t.reshape(-1), group=self.group)
+            else:
+                dist.all_gather(list(full.view(self.world, self.S, self.d).unbind(0)), t.clone(),
+                                group=self.group)
+            res.append(full[:self.V].clone())
+        return tuple(res)
+
+    def full_state(self):
+        """(w_in, m_in, v_in, w_out, m_out, v_out), each the whole (V, d) table as the dense
+        update holds it, on every rank (collectives when N > 1; lazy rows flushed first):
+        bench.py's step self-check."""
+        w_in = self.w_in.clone()
+        m_in, v_in = self.in_state_full()
+        m_out, v_out = self.out_state_full()
+        return w_in, m_in, v_in, self.full_w_out(), m_out, v_out
+
     # ---- the step ------------------------------------------------------------------------------
     def _adam(self, p, g, m, v, zero_grad: bool) -> None:
         self.adam_impl(p, g, m, v, self.step_count, self.lr, self.betas, self.eps,
@@ -1032,6 +1060,11 @@ class OwnerLazyTables(OwnerTables):
     def full_w_out(self) -> torch.Tensor:
         self._flush_out()
         return super().full_w_out()
+
+    def in_state_full(self):
+        """(m, v) of the in table (replicated here), every row brought current."""
+        self.flush()
+        return self.m_in[:self.V].clone(), self.v_in[:self.V].clone()
 
     def out_state_full(self):
         self._flush_out()

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 4: the N > 1 bench flow over RCCL on one GPU (DW_BENCH_DIST=1, one 'nccl' rank) with its
+# new self-check fields (rccl_world, exposed collective ms, step_check), the same with a
+# corrupted shard (must exit non-zero), then the graphed-loop tests with the reference's streams.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # run <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 4 "gpurun_out/$name.log" | cut -c1-600
+  return $rc
+}
+TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1"
+DW_BENCH_DIST=1 run r04_rccl_check 300 $TR --master-port 29621 bench.py --steps 20 --warmup 3 --no-walk-bench --no-cpu-baseline || exit 1
+DW_BENCH_DIST=1 DW_BENCH_CORRUPT=1 run r04_rccl_corrupt 300 $TR --master-port 29622 bench.py --steps 10 --warmup 2 --no-walk-bench --no-cpu-baseline
+rc=$?
+if [ $rc -eq 0 ]; then echo "corrupted shard was NOT detected"; exit 1; fi
+if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then echo "corrupt run timed out"; exit 1; fi
+echo "corrupted shard detected (rc=$rc)"
+run r04_tests_trainer 900 python -u -m pytest tests/test_gpu_trainer.py tests/test_gpu_mt.py tests/test_gpu_graphed.py -x -q -p no:cacheprovider -rf --timeout 600 --timeout-method thread
