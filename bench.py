@@ -875,7 +875,7 @@ def main():
             import random as _random
             from shallow_encoders.graph.rng import draw_uniforms, draw_uniforms_device
             for meth, p, q in walk_methods:
-                n_r = N if meth == 'deepwalk' else 65_536
+                n_r = N   # one walk per node (the reference's epoch: a walk from every node)
                 w = (Node2Vec(csr, L, p=p, q=q, device=dev) if meth == 'node2vec'
                      else DeepWalk(csr, L, device=dev))
                 st = (torch.arange(n_r, dtype=torch.int32) % N) + 1   # node ids 1..N, cycled
@@ -890,6 +890,9 @@ def main():
                     csr.device_tensors(dev, need_edge_cn=True)
                     torch.cuda.synchronize(dev)
                     build_ms = (time.perf_counter() - a) * 1e3
+                    # the position index (dw_n2v_edge_index_build), built once per graph (timed
+                    # inside the build; entries and bytes reported)
+                    csr.device_tensors(dev, need_n2v_index=True)
                 _random.seed(0)
                 w.walk_batch(st_dev[:64])                              # warm-up (jump tables)
                 w.walk_batch(st_dev, out=out)
@@ -923,10 +926,17 @@ def main():
                                       'walks_per_s_host_uniforms': n_r / dt_host}
                 if build_ms is not None:
                     replay_stats[meth]['edge_counts_build_ms'] = build_ms
+                    info = csr.device_tensors(dev).get('n2v_index_info', {})
+                    replay_stats[meth]['position_index'] = dict(info)
+                    replay_stats[meth]['walker'] = (
+                        'dw_walk_replay_positions (lane per walker over the position index)'
+                        if csr.device_tensors(dev).get('n2v_rec') is not None
+                        else 'dw_walk_replay_indexed (wave per walker, per-edge counts)')
                 if meth == 'node2vec':
-                    # the bit-exact walker's realised traffic (dw_walk_replay_indexed counted:
-                    # row pairs, uniform, pick, output per step; every list entry read; every
-                    # 64-B hash bucket probed), same walks, untimed launch
+                    # the bit-exact walker's realised traffic (counted launch, same walks,
+                    # untimed: the position walker's 32-B edge record, uniform and output per
+                    # step and 4 B per position read; the wave walker's row pairs, list entries
+                    # and 64-B hash buckets for the steps handed to it)
                     c = w.count_replay_traffic(st_dev, u_dev, out=out)
                     gbs = c['bytes'] / kern_s / 1e9
                     walk_roof['node2vec_replay'] = {

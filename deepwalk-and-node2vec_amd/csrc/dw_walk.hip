@@ -17,6 +17,10 @@
 //     proposal wins (ballot); adjacency tests only where the uniform leaves the outcome open.
 #include <stdlib.h>
 
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
 #include "dw_common.h"
 
 namespace {
@@ -875,6 +879,151 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ---- the per-edge position index (dw_n2v_edge_index_build) ----------------------------------
+// A step t -> v over edge e needs, of N(v)'s classes, only WHERE the 1/p neighbour (t itself)
+// and the C(e) 1/q neighbours sit: every other neighbour weighs 1. So per directed edge the
+// index keeps t's position in N(v) (or -1) and the sorted positions in N(v) of the common
+// neighbours; the pick is then a binary search over those C positions (log2 C dependent loads)
+// and an ALU-only search inside the gap between two of them. Positions are found over the
+// shorter list, as the counts were: N(t) shorter — each y in N(t) \ {t} probed into v's hash,
+// read back through adj_hpos (unsorted; the segmented sort orders them); N(v) shorter — each
+// of its entries tested against N(t) in order. One lane per edge when the shorter list has
+// <= 16 entries, else the wave over that edge (ballot compaction keeps the list order). An
+// edge whose positions do not add up to its counted C sets DW_S_BAD_CSR.
+__global__ void __launch_bounds__(256)
+    k_edge_cn_positions(EdgeIndex x, const int64_t *__restrict__ row_ptr, int64_t n_rows,
+                        int64_t n_edges, const uint32_t *__restrict__ cn,
+                        const int64_t *__restrict__ off, int32_t *__restrict__ pos,
+                        int32_t *__restrict__ pos_t, int32_t *status) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / WAVE;
+    const uint64_t lt = (1ull << lane) - 1;   // lanes below this one
+    uint32_t probes = 0;
+    for (int64_t e0 = wave * WAVE; e0 < n_edges; e0 += n_waves * WAVE) {
+        const int64_t e = e0 + lane;
+        const bool valid = e < n_edges;
+        int32_t t = 0;
+        AdjRow rt{0, 0, 0, 0}, rv{0, 0, 0, 0};
+        const uint32_t *bt = nullptr;
+        uint32_t w = 0;
+        int64_t o = 0;
+        if (valid) {
+            t = static_cast<int32_t>(row_of_edge(row_ptr, n_rows, e));
+            const int32_t v = x.col[e];
+            rt = adj_row(row_ptr, x.adj_off, t);
+            rv = adj_row(row_ptr, x.adj_off, v);
+            bt = row_bits(x, t);
+            w = cn[e];
+            o = off[e];
+            int32_t pt = -1;
+            if (w >> 31) {
+                const int64_t p = lane_position(x.col, x.adj_hash, x.adj_hpos, rv, t, probes);
+                if (p < 0) dw::status_or(status, DW_S_BAD_CSR);
+                pt = static_cast<int32_t>(p);
+            }
+            pos_t[e] = pt;
+        }
+        const int64_t C = w & 0x7FFFFFFFu;
+        const bool t_short = rt.n <= rv.n;
+        const bool small = (t_short ? rt.n : rv.n) <= 16;
+        if (valid && C > 0 && small) {
+            int64_t k = 0;
+            if (t_short) {
+                for (int64_t j = 0; j < rt.n; ++j) {
+                    const int32_t y = x.col[rt.a + j];
+                    if (y == t) continue;   // x == prev: the 1/p class, never a common neighbour
+                    const int64_t p = lane_position(x.col, x.adj_hash, x.adj_hpos, rv, y, probes);
+                    if (p >= 0) {
+                        if (k < C) pos[o + k] = static_cast<int32_t>(p);
+                        ++k;
+                    }
+                }
+            } else {
+                for (int64_t i = 0; i < rv.n; ++i) {
+                    const int32_t y = x.col[rv.a + i];
+                    if (y != t && edge_member(x, bt, rt, y, probes)) {
+                        if (k < C) pos[o + k] = static_cast<int32_t>(i);
+                        ++k;
+                    }
+                }
+            }
+            if (k != C) dw::status_or(status, DW_S_BAD_CSR);
+        }
+        uint64_t heavy = __ballot(valid && C > 0 && !small);
+        while (heavy) {   // one edge at a time, the wave over its shorter list
+            const int src = __ffsll((unsigned long long)heavy) - 1;
+            heavy &= heavy - 1;
+            const bool ts = __shfl(t_short ? 1 : 0, src) != 0;
+            const int32_t tt = __shfl(t, src);
+            const AdjRow l_t{__shfl(rt.a, src), __shfl(rt.n, src), __shfl(rt.h, src),
+                             static_cast<uint32_t>(__shfl(static_cast<int32_t>(rt.nb), src))};
+            const AdjRow l_v{__shfl(rv.a, src), __shfl(rv.n, src), __shfl(rv.h, src),
+                             static_cast<uint32_t>(__shfl(static_cast<int32_t>(rv.nb), src))};
+            const uint32_t *b = reinterpret_cast<const uint32_t *>(
+                __shfl(reinterpret_cast<unsigned long long>(bt), src));
+            const int64_t oo = __shfl(o, src), cc = __shfl(C, src);
+            int64_t k = 0;
+            const int64_t len = ts ? l_t.n : l_v.n;
+            for (int64_t j0 = 0; j0 < len; j0 += WAVE) {
+                const int64_t j = j0 + lane;
+                int64_t p = -1;
+                if (j < len) {
+                    if (ts) {
+                        const int32_t y = x.col[l_t.a + j];
+                        if (y != tt)
+                            p = lane_position(x.col, x.adj_hash, x.adj_hpos, l_v, y, probes);
+                    } else {
+                        const int32_t y = x.col[l_v.a + j];
+                        if (y != tt && edge_member(x, b, l_t, y, probes)) p = j;
+                    }
+                }
+                const uint64_t hit = __ballot(p >= 0);
+                const int64_t slot = k + __popcll(hit & lt);
+                if (p >= 0 && slot < cc) pos[oo + slot] = static_cast<int32_t>(p);
+                k += __popcll(hit);
+            }
+            if (lane == src && k != cc) dw::status_or(status, DW_S_BAD_CSR);
+        }
+    }
+}
+
+// The walker's 32-B edge record: {x, deg(x), row_ptr[x] lo, hi} (the edge-inline CSR entry)
+// then {off lo, off hi, counts word, t's position in N(x)} — one line per step.
+__global__ void k_n2v_edge_records(const int64_t *__restrict__ row_ptr,
+                                   const int32_t *__restrict__ col, const uint32_t *__restrict__ cn,
+                                   const int64_t *__restrict__ off,
+                                   const int32_t *__restrict__ pos_t, int64_t n_edges,
+                                   int4 *__restrict__ rec) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n_edges; e += stride) {
+        const int32_t v = col[e];
+        const int64_t a = row_ptr[v];
+        const int64_t o = off[e];
+        rec[2 * e] = int4{v, static_cast<int32_t>(row_ptr[v + 1] - a),
+                          static_cast<int32_t>(static_cast<uint32_t>(a)),
+                          static_cast<int32_t>(a >> 32)};
+        rec[2 * e + 1] = int4{static_cast<int32_t>(static_cast<uint32_t>(o)),
+                              static_cast<int32_t>(o >> 32), static_cast<int32_t>(cn[e]),
+                              pos_t[e]};
+    }
+}
+
+struct CnCount64 {   // C(e) of a counts word, widened for the offsets' scan
+    __host__ __device__ __forceinline__ int64_t operator()(uint32_t w) const {
+        return static_cast<int64_t>(w & 0x7FFFFFFFu);
+    }
+};
+
+#define DW_WALK_HIP_OK(expr, what)                                                  \
+    do {                                                                            \
+        hipError_t e_ = (expr);                                                     \
+        if (e_ != hipSuccess) {                                                     \
+            ::dw::set_error("%s: %s", what, hipGetErrorString(e_));                 \
+            return DW_E_HIP;                                                        \
+        }                                                                           \
+    } while (0)
+
 // The adjacency index of the probe-the-shorter-list steps (dw_walk_replay_indexed; adj_off ==
 // NULL: every step classifies N(v)) and the optional traffic counters (uint64[4] += {bytes,
 // hash probes, list entries read, steps}).
@@ -900,13 +1049,22 @@ __device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
 // takes n2v_pick_counted, so the full classification (node2vec_pick_exact) and its class-mask
 // cache are not compiled in; CH then only sizes the serial fallback's weight cache (hub rows
 // past it recompute their weights in lane 0) and, with the N(prev) stage, the positions buffer.
+// A walk the lane-per-walk position walker (k_walk_replay_n2v_pos) handed over at step s (a
+// pick its margin could not decide): the wave walker resumes it from (v, prev, e_in).
+struct N2VDefer {
+    int64_t wk, e_in;
+    int32_t s, v, prev, pad;
+};
+
 template <int CH, int NCAP, bool COUNTS>
 __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
                                                  const int32_t *__restrict__ starts,
                                                  int64_t n_walks, int32_t L,
                                                  const double *__restrict__ uniforms,
                                                  int32_t *__restrict__ out, int32_t *status,
-                                                 int fast, N2VIndex ix) {
+                                                 int fast, N2VIndex ix,
+                                                 const N2VDefer *__restrict__ resume,
+                                                 const uint32_t *__restrict__ n_resume) {
     // per wave: CH doubles (the serial replay's weights / the exact picks' ballots) followed by
     // the NCAP-entry N(prev) stage; the ballots take both halves when nothing is staged
     __shared__ uint64_t s_lds[REPLAY_WAVES][CH + NCAP / 2];
@@ -918,15 +1076,26 @@ __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
     const int64_t n_waves = (int64_t)gridDim.x * REPLAY_WAVES;
     const bool counted = ix.counters != nullptr;
     uint32_t probes = 0, loads = 0, steps = 0;   // counted launches only
+    const int64_t n_items = resume ? static_cast<int64_t>(*n_resume) : n_walks;
 
-    for (int64_t wk = (int64_t)blockIdx.x * REPLAY_WAVES + wv; wk < n_walks; wk += n_waves) {
-        int32_t v = starts[wk];
-        int32_t prev = -1;
+    for (int64_t it = (int64_t)blockIdx.x * REPLAY_WAVES + wv; it < n_items; it += n_waves) {
+        int64_t wk = it;
+        int32_t v, prev = -1;
         int64_t e_in = -1;   // the edge prev -> v (its class counts: ix.edge_cn)
-        int32_t *o = out + wk * (int64_t)L;
-        if (lane == 0) o[0] = v;
-        const double *u = uniforms + wk * (int64_t)(L - 1);
         int32_t s = 1;
+        if (resume) {        // a handed-over walk: steps < s are written
+            const N2VDefer r = resume[it];
+            wk = r.wk;
+            v = r.v;
+            prev = r.prev;
+            e_in = r.e_in;
+            s = r.s;
+        } else {
+            v = starts[wk];
+        }
+        int32_t *o = out + wk * (int64_t)L;
+        if (!resume && lane == 0) o[0] = v;
+        const double *u = uniforms + wk * (int64_t)(L - 1);
         for (; s < L; ++s) {
             if (v < 0 || (int64_t)v >= n_rows) {
                 if (lane == 0) dw::status_or(status, DW_S_BAD_CSR);
@@ -1120,7 +1289,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
                   int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
     walk_replay_body<CH, NCAP, false>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
-                                      ix);
+                                      ix, nullptr, nullptr);
 }
 
 // The COUNTS form is latency-bound on each walker's dependent chain and its LDS (4.6 KiB per
@@ -1133,9 +1302,169 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     __attribute__((amdgpu_waves_per_eu(DW_N2V_CN_WAVES, 8)))
     k_walk_replay_cn(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                      int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
-                     int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
+                     int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix,
+                     const N2VDefer *__restrict__ resume, const uint32_t *__restrict__ n_resume) {
     walk_replay_body<CH, NCAP, true>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
-                                     ix);
+                                     ix, resume, n_resume);
+}
+
+// ---- node2vec over the position index: one lane per walker ----------------------------------
+// With t's position pt and the sorted common-neighbour positions P[0..C) of the step's edge,
+// the prefix counts at neighbour i are a_i = [pt <= i] and c_i = #{P <= i}: the pick (the
+// first i with D_i = W(a_i, i + 1 - a_i - c_i, c_i) - U T > 0, T = W(A, n - A - C, C)) is
+// found by a binary search over j of D at P[j] (c = j + 1), then inside the gap
+// (P[j-1], P[j]] where c is j (j + 1 at P[j] itself) by a search with no loads. The D values,
+// T, M and the bracketing test are the expressions of node2vec_pick_exact on the same
+// integers, so the pick — or the hand-over where the margin fails — is the same.
+__device__ __forceinline__ int64_t n2v_pick_pos(const int32_t *__restrict__ P, int64_t C,
+                                                int64_t pt, int64_t n, double U, double ip,
+                                                double iq, uint32_t &loads) {
+    const int64_t A = pt >= 0 ? 1 : 0;
+    const double T = n2v_w(A, n - A - C, C, ip, iq);
+    const double UT = U * T;
+    const double M = exact_margin(n, T);
+    if (!(T - UT > 0.0)) return -1;   // D_{n-1} <= 0: rounding at the top end
+    auto D = [&](int64_t i, int64_t c) {
+        const int64_t a = (pt >= 0 && pt <= i) ? 1 : 0;
+        return n2v_w(a, (i + 1) - a - c, c, ip, iq) - UT;
+    };
+    int64_t lo = 0, hi = C;           // first j with D(P[j], j + 1) > 0, else C
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        ++loads;
+        if (D(P[mid], mid + 1) > 0.0)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    const int64_t j = lo;
+    const int64_t pj = j < C ? static_cast<int64_t>(P[j]) : n - 1;   // D(pj) > 0
+    int64_t a = j > 0 ? static_cast<int64_t>(P[j - 1]) + 1 : 0;       // D(P[j-1]) <= 0
+    if (j > 0) ++loads;
+    int64_t b = pj;
+    while (a < b) {                   // i < pj: c_i = j
+        const int64_t mid = (a + b) >> 1;
+        if (D(mid, j) > 0.0)
+            b = mid;
+        else
+            a = mid + 1;
+    }
+    const int64_t k = a;
+    const double d_k = D(k, (j < C && k == pj) ? j + 1 : j);
+    if (k >= 1 && fabs(D(k - 1, j)) <= M) return -1;
+    if (k <= n - 2 && fabs(d_k) <= M) return -1;
+    return k;
+}
+
+// The walks of dw_walk_replay_indexed, one lane per walker over the 32-B edge records
+// (k_n2v_edge_records): a step is the record of the edge it arrived by (its next row and its
+// index entry in one line), the search of its positions, and nothing else. The uniforms are
+// staged in LDS per tile of steps as in k_walk_replay_uniform_inline. A pick the margin leaves
+// open hands the walk to the wave walker (k_walk_replay_cn over `defer`), which finishes it.
+// 8 staged steps per tile (17 KiB of LDS per block): the walk is latency-bound, so blocks
+// per CU count for more than the uniforms' reload rate
+constexpr int RP_T = 8;
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+    k_walk_replay_n2v_pos(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ rec,
+                          const int32_t *__restrict__ pos, int64_t n_rows,
+                          const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
+                          const double *__restrict__ uniforms, double ip, double iq,
+                          int32_t *__restrict__ out, int32_t *status, N2VDefer *__restrict__ defer,
+                          uint32_t *__restrict__ n_defer, unsigned long long *counters) {
+    __shared__ double tile[256][RP_T + 1];
+    const int tid = threadIdx.x;
+    const int64_t n_chunks = (n_walks + 255) / 256;
+    const int64_t UL = L - 1;
+    uint32_t loads = 0, steps = 0;
+    for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+        const int64_t w0 = ch * 256;
+        const int n_here = (n_walks - w0 < 256) ? static_cast<int>(n_walks - w0) : 256;
+        const int64_t wk = w0 + tid;
+        const bool live = tid < n_here;
+        int32_t v = live ? starts[wk] : 0;
+        int32_t *o = out + wk * (int64_t)L;
+        bool ok = live && v >= 0 && (int64_t)v < n_rows;
+        if (live && !ok) dw::status_or(status, DW_S_BAD_CSR);
+        int64_t a = ok ? row_ptr[v] : 0;
+        int64_t n = ok ? row_ptr[v + 1] - a : 0;
+        int32_t prev = -1;
+        int64_t e_in = -1, p_off = 0;
+        uint32_t cw = 0;   // the counts word of e_in
+        int32_t pt = -1;
+        const bool pack = (L & 3) == 0;
+        int32_t q0 = v, q1 = -1, q2 = -1;
+        if (live && !pack) o[0] = v;
+        for (int64_t t0 = 0; t0 < UL; t0 += RP_T) {
+            const int tn = (UL - t0 < RP_T) ? static_cast<int>(UL - t0) : RP_T;
+            __syncthreads();
+#pragma unroll 4
+            for (int it = 0; it < RP_T; ++it) {
+                const int e = it * 256 + tid;
+                const int wl = e / RP_T, sl = e % RP_T;
+                if (wl < n_here && sl < tn) tile[wl][sl] = uniforms[(w0 + wl) * UL + t0 + sl];
+            }
+            __syncthreads();
+            if (!live) continue;
+            for (int j = 0; j < tn; ++j) {
+                const int32_t st = static_cast<int32_t>(t0) + 1 + j;
+                int32_t node = -1;
+                if (ok) {
+                    if (n <= 0) {
+                        dw::status_or(status, DW_S_ISOLATED_NODE);
+                        ok = false;
+                    } else {
+                        const double U = tile[tid][j];
+                        if (COUNT) ++steps;
+                        const int64_t k =
+                            prev < 0 ? uniform_pick_exact(U, n)
+                                     : n2v_pick_pos(pos + p_off, cw & 0x7FFFFFFFu,
+                                                    (cw >> 31) ? pt : -1, n, U, ip, iq, loads);
+                        if (k < 0) {   // the wave walker takes it from here
+                            const uint32_t slot = atomicAdd(n_defer, 1u);
+                            defer[slot] = N2VDefer{wk, e_in, st, v, prev, 0};
+                            ok = false;
+                        } else {
+                            const int64_t e = a + k;
+                            const int4 r0 = rec[2 * e], r1 = rec[2 * e + 1];
+                            prev = v;
+                            v = r0.x;
+                            n = r0.y;
+                            a = static_cast<int64_t>(static_cast<uint32_t>(r0.z)) |
+                                (static_cast<int64_t>(r0.w) << 32);
+                            p_off = static_cast<int64_t>(static_cast<uint32_t>(r1.x)) |
+                                    (static_cast<int64_t>(r1.y) << 32);
+                            cw = static_cast<uint32_t>(r1.z);
+                            pt = r1.w;
+                            e_in = e;
+                            node = v;
+                        }
+                    }
+                }
+                if (!pack) {
+                    o[st] = node;
+                } else {
+                    switch (st & 3) {
+                        case 0: q0 = node; break;
+                        case 1: q1 = node; break;
+                        case 2: q2 = node; break;
+                        default:
+                            reinterpret_cast<int4 *>(o)[st >> 2] = int4{q0, q1, q2, node};
+                    }
+                }
+            }
+        }
+    }
+    if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); 4 B per search load
+        unsigned long long v2[2] = {(unsigned long long)loads, (unsigned long long)steps};
+        for (int k = 0; k < 2; ++k)
+            for (int off = WAVE / 2; off > 0; off >>= 1) v2[k] += __shfl_xor(v2[k], off, WAVE);
+        if ((tid & (WAVE - 1)) == 0) {
+            atomicAdd(counters + 0, v2[0] * 4ull + v2[1] * 44ull);
+            atomicAdd(counters + 2, v2[0]);
+            atomicAdd(counters + 3, v2[1]);
+        }
+    }
 }
 
 // =============================================================================================
@@ -1764,7 +2093,7 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
         hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
                            dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,
-                           uniforms, out, status, 1, ix);
+                           uniforms, out, status, 1, ix, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
@@ -1790,6 +2119,153 @@ int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int6
     hipLaunchKernelGGL(k_edge_common, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
                        x, row_ptr, n_rows, n_edges, edge_cn);
     DW_LAUNCH_CHECK("dw_edge_common_counts");
+    return DW_OK;
+}
+
+int dw_n2v_edge_offsets(const uint32_t *edge_cn, int64_t n_edges, int64_t *off, void *tmp,
+                        size_t *tmp_bytes, void *stream) {
+    DW_REQUIRE(n_edges >= 0 && tmp_bytes, "dw_n2v_edge_offsets: bad arguments");
+    DW_REQUIRE(n_edges < (int64_t(1) << 32), "dw_n2v_edge_offsets: too many edges");
+    const auto in = rocprim::make_transform_iterator(edge_cn, CnCount64{});
+    const hipStream_t st = dw::as_stream(stream);
+    size_t need = 0;
+    if (n_edges > 0)
+        DW_WALK_HIP_OK(rocprim::inclusive_scan(nullptr, need, in, static_cast<int64_t *>(nullptr),
+                                               static_cast<size_t>(n_edges),
+                                               rocprim::plus<int64_t>(), st),
+                       "dw_n2v_edge_offsets: scan");
+    if (!tmp) {
+        *tmp_bytes = need > 0 ? need : 1;
+        return DW_OK;
+    }
+    DW_REQUIRE(*tmp_bytes >= need, "dw_n2v_edge_offsets: tmp too small");
+    DW_REQUIRE(off && (n_edges == 0 || edge_cn), "dw_n2v_edge_offsets: null pointer");
+    DW_WALK_HIP_OK(hipMemsetAsync(off, 0, sizeof(int64_t), st), "dw_n2v_edge_offsets: memset");
+    if (n_edges > 0)
+        DW_WALK_HIP_OK(rocprim::inclusive_scan(tmp, need, in, off + 1,
+                                               static_cast<size_t>(n_edges),
+                                               rocprim::plus<int64_t>(), st),
+                       "dw_n2v_edge_offsets: scan");
+    return DW_OK;
+}
+
+int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                            const int32_t *adj_hash, const int32_t *adj_hpos,
+                            const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                            const uint32_t *edge_cn, const int64_t *off, int64_t n_rows,
+                            int64_t n_edges, int64_t n_pos, int32_t *pos, int32_t *pos_unsorted,
+                            int32_t *rec, void *tmp, size_t *tmp_bytes, int32_t *status,
+                            void *stream) {
+    DW_REQUIRE(n_rows >= 0 && n_edges >= 0 && n_pos >= 0 && tmp_bytes,
+               "dw_n2v_edge_index_build: bad arguments");
+    DW_REQUIRE(n_edges < (int64_t(1) << 31) && n_pos < (int64_t(1) << 32),
+               "dw_n2v_edge_index_build: index too large for one segmented sort");
+    const hipStream_t st = dw::as_stream(stream);
+    uint32_t end_bit = 1;
+    while (end_bit < 31 && (int64_t(1) << end_bit) < n_rows) ++end_bit;   // positions < deg <= V
+    // tmp: t's positions (int32 per edge), then the segmented sort's storage
+    const size_t pt_bytes = ((static_cast<size_t>(n_edges) * 4 + 255) / 256) * 256;
+    size_t sort_bytes = 0;
+    if (n_pos > 0)
+        DW_WALK_HIP_OK(rocprim::segmented_radix_sort_keys(
+                           nullptr, sort_bytes, static_cast<const int32_t *>(nullptr),
+                           static_cast<int32_t *>(nullptr), static_cast<unsigned>(n_pos),
+                           static_cast<unsigned>(n_edges), static_cast<const int64_t *>(nullptr),
+                           static_cast<const int64_t *>(nullptr), 0, end_bit, st),
+                       "dw_n2v_edge_index_build: sort");
+    if (!tmp) {
+        *tmp_bytes = pt_bytes + sort_bytes + 256;
+        return DW_OK;
+    }
+    DW_REQUIRE(*tmp_bytes >= pt_bytes + sort_bytes, "dw_n2v_edge_index_build: tmp too small");
+    if (n_edges == 0 || n_rows == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && adj_hpos && edge_cn && off && rec &&
+                   status && (n_pos == 0 || (pos && pos_unsorted)),
+               "dw_n2v_edge_index_build: null pointer");
+    DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
+               "dw_n2v_edge_index_build: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
+    int32_t *pos_t = static_cast<int32_t *>(tmp);
+    int64_t blocks = (n_edges + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    const EdgeIndex x{col, adj_off, adj_hash, adj_hpos, hub_idx, hub_bits, hub_words};
+    hipLaunchKernelGGL(k_edge_cn_positions, dim3((unsigned)blocks), dim3(256), 0, st, x, row_ptr,
+                       n_rows, n_edges, edge_cn, off, pos_unsorted, pos_t, status);
+    DW_LAUNCH_CHECK("dw_n2v_edge_index_build/positions");
+    if (n_pos > 0)
+        DW_WALK_HIP_OK(rocprim::segmented_radix_sort_keys(
+                           static_cast<char *>(tmp) + pt_bytes, sort_bytes,
+                           static_cast<const int32_t *>(pos_unsorted), pos,
+                           static_cast<unsigned>(n_pos), static_cast<unsigned>(n_edges), off,
+                           off + 1, 0, end_bit, st),
+                       "dw_n2v_edge_index_build: sort");
+    hipLaunchKernelGGL(k_n2v_edge_records, dim3((unsigned)blocks), dim3(256), 0, st, row_ptr, col,
+                       edge_cn, off, pos_t, n_edges, reinterpret_cast<int4 *>(rec));
+    DW_LAUNCH_CHECK("dw_n2v_edge_index_build/records");
+    return DW_OK;
+}
+
+size_t dw_walk_replay_positions_workspace_bytes(int64_t n_walks) {
+    return 256 + static_cast<size_t>(n_walks > 0 ? n_walks : 0) * sizeof(N2VDefer);
+}
+
+int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
+                             const int32_t *col_sorted, const int64_t *adj_off,
+                             const int32_t *adj_hash, const int32_t *adj_hpos,
+                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                             const uint32_t *edge_cn, const int32_t *n2v_rec,
+                             const int32_t *n2v_pos, int64_t n_rows, const int32_t *starts,
+                             int64_t n_walks, int32_t walk_length, double p, double q,
+                             const double *uniforms, int32_t *out, int32_t *status,
+                             void *workspace, size_t workspace_bytes, uint64_t *counters,
+                             void *stream) {
+    DW_REQUIRE(walk_length >= 1, "dw_walk_replay_positions: Minimum walk length is 1!");
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_replay_positions: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && col_sorted && adj_off && adj_hash && adj_hpos && edge_cn &&
+                   n2v_rec && starts && out && status && workspace,
+               "dw_walk_replay_positions: null pointer");
+    DW_REQUIRE(workspace_bytes >= dw_walk_replay_positions_workspace_bytes(n_walks),
+               "dw_walk_replay_positions: workspace too small");
+    DW_REQUIRE(walk_length == 1 || uniforms, "dw_walk_replay_positions: uniforms is null");
+    DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_replay_positions: p and q must be positive");
+    DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
+               "dw_walk_replay_positions: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
+    ReplayCtx c;
+    c.row_ptr = row_ptr;
+    c.col = col;
+    c.col_sorted = col_sorted;
+    c.w = nullptr;
+    c.node2vec = true;
+    c.inv_p = 1.0 / p;   // `1 / self._p` (host IEEE division)
+    c.inv_q = 1.0 / q;
+    DW_REQUIRE(c.inv_p < 1e300 && c.inv_q < 1e300, "dw_walk_replay_positions: p, q too small");
+    const hipStream_t st = dw::as_stream(stream);
+    uint32_t *n_defer = static_cast<uint32_t *>(workspace);
+    N2VDefer *defer = reinterpret_cast<N2VDefer *>(static_cast<char *>(workspace) + 256);
+    DW_WALK_HIP_OK(hipMemsetAsync(n_defer, 0, sizeof(uint32_t), st),
+                   "dw_walk_replay_positions: memset");
+    int64_t blocks = (n_walks + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    auto *cnt = reinterpret_cast<unsigned long long *>(counters);
+    if (counters)
+        hipLaunchKernelGGL(k_walk_replay_n2v_pos<true>, dim3((unsigned)blocks), dim3(256), 0, st,
+                           row_ptr, reinterpret_cast<const int4 *>(n2v_rec), n2v_pos, n_rows,
+                           starts, n_walks, walk_length, uniforms, c.inv_p, c.inv_q, out, status,
+                           defer, n_defer, cnt);
+    else
+        hipLaunchKernelGGL(k_walk_replay_n2v_pos<false>, dim3((unsigned)blocks), dim3(256), 0, st,
+                           row_ptr, reinterpret_cast<const int4 *>(n2v_rec), n2v_pos, n_rows,
+                           starts, n_walks, walk_length, uniforms, c.inv_p, c.inv_q, out, status,
+                           defer, n_defer, cnt);
+    DW_LAUNCH_CHECK("dw_walk_replay_positions");
+    // the handed-over walks (the count stays on the device: a fixed grid, graph-capturable)
+    const N2VIndex ix{adj_off, adj_hash, adj_hpos, 64, cnt, hub_idx, hub_bits, hub_words, edge_cn};
+    int64_t rblocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
+    if (rblocks > 1024) rblocks = 1024;
+    hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>), dim3((unsigned)rblocks),
+                       dim3(REPLAY_WAVES * WAVE), 0, st, c, n_rows, starts, n_walks, walk_length,
+                       uniforms, out, status, 1, ix, defer, n_defer);
+    DW_LAUNCH_CHECK("dw_walk_replay_positions/handed over");
     return DW_OK;
 }
 

@@ -35,7 +35,7 @@ DW_S_DUP_NEIGHBOR = 64
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -144,6 +144,13 @@ SIGNATURES = {
     'dw_edge_common_counts': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
                                              _p]),
     'dw_hub_bitmaps': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i64, _p, _p]),
+    'dw_n2v_edge_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),
+    'dw_n2v_edge_index_build': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _i64,
+                                               _i64, _i64, _p, _p, _p, _p, _szp, _p, _p]),
+    'dw_walk_replay_positions_workspace_bytes': (ctypes.c_size_t, [_i64]),
+    'dw_walk_replay_positions': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p,
+                                                _i64, _p, _i64, _i32, _f64, _f64, _p, _p, _p, _p,
+                                                ctypes.c_size_t, _p, _p]),
     'dw_adj_hash_positions': (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,
                                               _p, _i64, _p]),

@@ -191,7 +191,8 @@ class CSRGraph:
                        need_alias: bool = False, need_edges: bool = False,
                        need_adj: bool = False, need_adj_pos: bool = False,
                        need_hub_bits: bool = False,
-                       need_edge_cn: bool = False) -> Dict[str, torch.Tensor]:
+                       need_edge_cn: bool = False,
+                       need_n2v_index: bool = False) -> Dict[str, torch.Tensor]:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
         the per-row adjacency hash / its slots' neighbour positions on the device)."""
         dev = _native.require_device(device)
@@ -245,7 +246,65 @@ class CSRGraph:
                              _native.ptr(d['hub_bits']), d['hub_words'], self.vocab_size,
                              self.nnz, _native.ptr(cn), _native.stream(dev))
             d['edge_cn'] = cn
+        if need_n2v_index and 'n2v_rec' not in d:
+            self._build_n2v_index(dev)
         return d
+
+    # the position index is built when its entries, scratch and records fit this many bytes
+    # (DW_N2V_INDEX_BYTES overrides); above it the walker keeps the counted classification
+    N2V_INDEX_BYTES = 48 << 30
+
+    def _build_n2v_index(self, dev) -> None:
+        """n2v_rec int32[nnz, 8] / n2v_pos int32[entries] (dw_n2v_edge_offsets +
+        dw_n2v_edge_index_build): per directed edge t -> v, t's position in N(v) and the sorted
+        positions of N(t) ∩ N(v) — the exact node2vec pick's binary search
+        (dw_walk_replay_positions). Both None when the index would exceed the byte budget;
+        n2v_index_info = {'entries', 'bytes', 'build_ms'} or {'entries', 'bytes', 'skipped'}."""
+        import ctypes
+        import os
+        import time
+        d = self.device_tensors(dev, need_edge_cn=True)
+        E = self.nnz
+        with torch.cuda.device(dev):
+            s = _native.stream(dev)
+            t0 = time.perf_counter()
+            off = torch.empty(E + 1, dtype=torch.int64, device=dev)
+            nb = ctypes.c_size_t(0)
+            _native.call('dw_n2v_edge_offsets', _native.ptr(d['edge_cn']), E, _native.ptr(off),
+                         None, ctypes.byref(nb), s)
+            tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            _native.call('dw_n2v_edge_offsets', _native.ptr(d['edge_cn']), E, _native.ptr(off),
+                         _native.ptr(tmp), ctypes.byref(nb), s)
+            del tmp
+            n_pos = int(off[E])            # synchronises: the index size
+            nb = ctypes.c_size_t(0)
+            args = [_native.ptr(d['row_ptr']), _native.ptr(d['col']) if E else None,
+                    _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                    _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
+                    _native.ptr(d['hub_bits']), d['hub_words'], _native.ptr(d['edge_cn']),
+                    _native.ptr(off), self.vocab_size, E, n_pos]
+            fits = n_pos < (1 << 32) and E < (1 << 31)
+            if fits:
+                _native.call('dw_n2v_edge_index_build', *args, None, None, None, None,
+                             ctypes.byref(nb), None, s)
+            need = 8 * n_pos + 32 * E + int(nb.value)
+            budget = int(os.environ.get('DW_N2V_INDEX_BYTES', self.N2V_INDEX_BYTES))
+            if not fits or need > budget:
+                d['n2v_rec'], d['n2v_pos'] = None, None
+                d['n2v_index_info'] = {'entries': n_pos, 'bytes': need, 'skipped': True}
+                return
+            pos = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
+            scratch = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
+            rec = torch.empty((max(E, 1), 8), dtype=torch.int32, device=dev)
+            tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            _native.call('dw_n2v_edge_index_build', *args, _native.ptr(pos), _native.ptr(scratch),
+                         _native.ptr(rec), _native.ptr(tmp), ctypes.byref(nb),
+                         _native.ptr(d['status']), s)
+            del tmp, scratch, off
+            _native.check_status(d['status'], 'node2vec position index build')
+            d['n2v_rec'], d['n2v_pos'] = rec, pos
+            d['n2v_index_info'] = {'entries': n_pos, 'bytes': 4 * n_pos + 32 * E,
+                                   'build_ms': (time.perf_counter() - t0) * 1e3}
 
     # rows longer than the replay walker's LDS stage (1,024) get a V-bit neighbour map, the
     # longest first, within this many bytes (DW_HUB_BITS_BYTES overrides)

@@ -39,6 +39,13 @@ def _edge_cn_enabled() -> bool:
     return os.environ.get('DW_N2V_EDGE_CN', '1') != '0'
 
 
+def _n2v_index_enabled() -> bool:
+    """The node2vec replay over the per-edge position index (dw_n2v_edge_index_build, built once
+    per graph within CSRGraph.N2V_INDEX_BYTES; one lane per walker, dw_walk_replay_positions):
+    on by default; DW_N2V_POS=0 keeps the wave walker with the counts (the same walks)."""
+    return _edge_cn_enabled() and os.environ.get('DW_N2V_POS', '1') != '0'
+
+
 def _graph_fingerprint(graph) -> int:
     """Hash of the adjacency in insertion order with edge weights: a rewired edge or a changed
     weight gives a new CSR (the reference reads the live graph on every step). O(E)."""
@@ -224,7 +231,8 @@ class RandomWalk(ABC):
                                      need_edges=(indexed and not n2v) or replay_inline,
                                      need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx,
                                      need_hub_bits=replay_n2v_idx,
-                                     need_edge_cn=replay_n2v_idx and _edge_cn_enabled())
+                                     need_edge_cn=replay_n2v_idx and _edge_cn_enabled(),
+                                     need_n2v_index=replay_n2v_idx and _n2v_index_enabled())
         if self._rng == 'python' and n2v:
             self._csr.require_simple(dev)   # no repeated neighbour (nx.Graph's invariant)
         if out is None:
@@ -253,16 +261,7 @@ class RandomWalk(ABC):
                                  _native.ptr(u) if u.numel() else None, _native.ptr(out),
                                  _native.ptr(status), s)
                 elif replay_n2v_idx:
-                    _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
-                                 _native.ptr(d['col']), _native.ptr(d['col_sorted']),
-                                 _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                                 _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
-                                 _native.ptr(d['hub_bits']), d['hub_words'],
-                                 _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None),
-                                 self._csr.vocab_size, _native.ptr(starts), n, L, float(p),
-                                 float(q),
-                                 _native.ptr(u) if u.numel() else None, _native.ptr(out),
-                                 _native.ptr(status), None, s)
+                    self._replay_n2v(d, starts, n, u, out, status, None, s)
                 else:
                     _native.call('dw_walk_replay', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d.get('col_sorted')),
@@ -310,28 +309,41 @@ class RandomWalk(ABC):
         if u.numel() != n * (L - 1):
             raise ValueError('uniforms must have n_walks * (length - 1) values')
         d = self._csr.device_tensors(dev, need_sorted=True, need_adj_pos=True,
-                                     need_hub_bits=True, need_edge_cn=_edge_cn_enabled())
+                                     need_hub_bits=True, need_edge_cn=_edge_cn_enabled(),
+                                     need_n2v_index=_n2v_index_enabled())
         self._csr.require_simple(dev)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
         counters = torch.zeros(4, dtype=torch.int64, device=dev)
-        p, q = self._params()
         with torch.cuda.device(dev):
-            _native.call('dw_walk_replay_indexed', _native.ptr(d['row_ptr']),
-                         _native.ptr(d['col']), _native.ptr(d['col_sorted']),
-                         _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                         _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
-                         _native.ptr(d['hub_bits']), d['hub_words'],
-                         _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None),
-                         self._csr.vocab_size,
-                         _native.ptr(starts), n, L, float(p), float(q),
-                         _native.ptr(u) if u.numel() else None,
-                         _native.ptr(out), _native.ptr(status), _native.ptr(counters),
-                         _native.stream(dev))
+            self._replay_n2v(d, starts, n, u, out, status, counters, _native.stream(dev))
         _native.check_status(status, f'{type(self).__name__}.count_replay_traffic')
         c = counters.cpu().tolist()
         return {'bytes': c[0], 'probes': c[1], 'entries': c[2], 'steps': c[3]}
+
+    def _replay_n2v(self, d, starts, n, u, out, status, counters, s) -> None:
+        """The exact node2vec walks on an unweighted graph: over the position index when it is
+        built (dw_walk_replay_positions), else the wave walker (dw_walk_replay_indexed)."""
+        L = self._length
+        p, q = self._params()
+        common = [_native.ptr(d['row_ptr']), _native.ptr(d['col']), _native.ptr(d['col_sorted']),
+                  _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
+                  _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
+                  _native.ptr(d['hub_bits']), d['hub_words'],
+                  _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None)]
+        uptr = _native.ptr(u) if u.numel() else None
+        if _n2v_index_enabled() and d.get('n2v_rec') is not None:
+            nb = int(_native.load().dw_walk_replay_positions_workspace_bytes(n))
+            ws = torch.empty(nb, dtype=torch.uint8, device=out.device)
+            _native.call('dw_walk_replay_positions', *common, _native.ptr(d['n2v_rec']),
+                         _native.ptr(d['n2v_pos']), self._csr.vocab_size, _native.ptr(starts),
+                         n, L, float(p), float(q), uptr, _native.ptr(out), _native.ptr(status),
+                         _native.ptr(ws), nb, _native.ptr(counters), s)
+            return
+        _native.call('dw_walk_replay_indexed', *common, self._csr.vocab_size,
+                     _native.ptr(starts), n, L, float(p), float(q), uptr, _native.ptr(out),
+                     _native.ptr(status), _native.ptr(counters), s)
 
     def count_traffic(self, start_ids: torch.Tensor, walk_id0: int,
                       out: Optional[torch.Tensor] = None) -> dict:

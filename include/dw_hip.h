@@ -252,6 +252,51 @@ int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int6
                           const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
                           int64_t n_rows, int64_t n_edges, uint32_t *edge_cn, void *stream);
 
+/* The node2vec position index, step 1: off int64[n_edges + 1] = exclusive prefix sums of the
+ * common-neighbour counts C(e) (edge_cn bits 0-30); off[n_edges] = the index's entry count.
+ * tmp == NULL: *tmp_bytes = the scan's scratch size, nothing launched. */
+int dw_n2v_edge_offsets(const uint32_t *edge_cn, int64_t n_edges, int64_t *off, void *tmp,
+                        size_t *tmp_bytes, void *stream);
+
+/* The node2vec position index, step 2 (random_walk_generator.py:100-108: at a step t -> v only
+ * the 1/p neighbour t and the 1/q neighbours N(t) ∩ N(v) weigh other than 1): pos int32[n_pos]
+ * (n_pos = off[n_edges]) holds, at off[e], the positions in N(v) of the C(e) common neighbours
+ * of edge e = (t -> v), ascending; rec int32[n_edges][8] the walker's 32-B edge records {v,
+ * deg(v), row_ptr[v] lo, hi, off[e] lo, hi, edge_cn[e], position of t in N(v) or -1}.
+ * pos_unsorted int32[n_pos] is scratch. Positions come from the shorter list as the counts do
+ * (same adjacency index arguments as dw_edge_common_counts); a row whose positions disagree
+ * with its count sets DW_S_BAD_CSR in *status. tmp == NULL: *tmp_bytes = the scratch size.
+ * n_pos < 2^32 and n_edges < 2^31. */
+int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
+                            const int32_t *adj_hash, const int32_t *adj_hpos,
+                            const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                            const uint32_t *edge_cn, const int64_t *off, int64_t n_rows,
+                            int64_t n_edges, int64_t n_pos, int32_t *pos, int32_t *pos_unsorted,
+                            int32_t *rec, void *tmp, size_t *tmp_bytes, int32_t *status,
+                            void *stream);
+
+/* Bytes of dw_walk_replay_positions' workspace for n_walks walks. */
+size_t dw_walk_replay_positions_workspace_bytes(int64_t n_walks);
+
+/* dw_walk_replay_indexed's walks, bit for bit, over the position index (n2v_rec / n2v_pos of
+ * dw_n2v_edge_index_build): one lane per walker, a step reads its edge's 32-B record and
+ * binary-searches that edge's positions (log2 C loads), the pick by the same margin rule. A walk
+ * whose pick the margin cannot decide is handed, from that step, to the wave walker of
+ * dw_walk_replay_indexed (the remaining arguments serve it) in a second launch whose grid does
+ * not depend on how many were handed over (graph-capturable). counters: NULL, or uint64[4]
+ * (caller-zeroed) += {bytes, hash probes, list / position entries read, steps}. Replaces
+ * random_walk_generator.py:94-119 on unweighted graphs. */
+int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
+                             const int32_t *col_sorted, const int64_t *adj_off,
+                             const int32_t *adj_hash, const int32_t *adj_hpos,
+                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
+                             const uint32_t *edge_cn, const int32_t *n2v_rec,
+                             const int32_t *n2v_pos, int64_t n_rows, const int32_t *starts,
+                             int64_t n_walks, int32_t walk_length, double p, double q,
+                             const double *uniforms, int32_t *out, int32_t *status,
+                             void *workspace, size_t workspace_bytes, uint64_t *counters,
+                             void *stream);
+
 /* Neighbour bitmaps of hub rows for dw_walk_replay_indexed (hub_idx / hub_bits; NULL = none):
  * bits[k * hub_words + (x >> 5)] bit (x & 31) = x in N(hub_rows[k]); hub_words >=
  * ceil(n_rows / 32). A test of a neighbour of v against a hub prev too long for LDS is then one

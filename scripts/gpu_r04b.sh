@@ -11,3 +11,8 @@ for cfg in "1 1" "0 0" "1 0" "0 1" "1 1"; do
   grep '^{' gpurun_out/c3_64_p$1_o$2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('place', '$1', 'p_only', '$2', d['ms_per_step'])"
 done
 bash scripts/gpu_trace_c3_64.sh || exit 1
+# the node2vec position index: parity tests, then the walk bench (replay stats)
+timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_walks.py -k "n2v_position or indexed_node2vec or edge_counts_same or hubs or self_looped" > gpurun_out/r04b_n2v_tests.log 2>&1 || { tail -40 gpurun_out/r04b_n2v_tests.log; exit 1; }
+tail -3 gpurun_out/r04b_n2v_tests.log
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --exact-steps 0 > gpurun_out/r04b_walkbench.log 2>&1 || { tail -20 gpurun_out/r04b_walkbench.log; exit 1; }
+grep '^{' gpurun_out/r04b_walkbench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({k: d.get(k) for k in ('walks_per_s_replay','roofline_walk')}, indent=1))"

@@ -533,3 +533,118 @@ def test_node2vec_replay_edge_counts_same_walks(p, q, hip_device, monkeypatch):
     np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     assert c1['steps'] == c0['steps'] and c1['entries'] < c0['entries']
+
+
+@pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops', 'self_looped_leaves'])
+def test_n2v_position_index_vs_oracle(which, hip_device):
+    """dw_n2v_edge_index_build (the node2vec position index: per directed edge t -> v, t's
+    position in N(v) and the ascending positions of N(t) ∩ N(v) \\ {t}) equals the oracle's
+    restatement of the reference rule (walk_ref.edge_class_positions) on every edge; the 32-B
+    records carry the edge-inline entry, the offset and the counts word."""
+    if which == 'karate':
+        csr = _csr(golden('walks_karate_node2vec_p1_q0.5.npz'))
+    elif which == 'rmat12':
+        csr = _csr(golden('walks_rmat12_node2vec_p0.25_q4.npz'))
+    elif which == 'self_loops':
+        csr = _self_loop_graph()
+    else:
+        csr = _self_looped_leaves_graph()
+    d = csr.device_tensors(hip_device, need_n2v_index=True)
+    assert d['n2v_rec'] is not None
+    E = csr.nnz
+    rec = d['n2v_rec'][:E].cpu().numpy()
+    off_ref, pos_ref, pt_ref = walk_ref.edge_class_positions(
+        walk_ref.CSR(csr.row_ptr, csr.host_col(), None))
+    col = csr.host_col()
+    rp = np.asarray(csr.row_ptr, dtype=np.int64)
+    np.testing.assert_array_equal(rec[:, 0], col)
+    np.testing.assert_array_equal(rec[:, 1], rp[col + 1] - rp[col])
+    np.testing.assert_array_equal(rec[:, 2].view(np.uint32).astype(np.int64)
+                                  | (rec[:, 3].astype(np.int64) << 32), rp[col])
+    off = rec[:, 4].view(np.uint32).astype(np.int64) | (rec[:, 5].astype(np.int64) << 32)
+    np.testing.assert_array_equal(off, off_ref[:-1])
+    cn = walk_ref.edge_class_counts(walk_ref.CSR(csr.row_ptr, col, None))
+    np.testing.assert_array_equal(rec[:, 6].view(np.uint32), cn)
+    np.testing.assert_array_equal(rec[:, 7], pt_ref)
+    assert d['n2v_index_info']['entries'] == len(pos_ref)
+    np.testing.assert_array_equal(d['n2v_pos'][:len(pos_ref)].cpu().numpy(), pos_ref)
+
+
+def _boundary_uniforms(csr, starts, L, p, q, rng):
+    """Uniforms with a quarter of the walks' first draws exactly on k / deg (the first step's
+    margin declines) and a quarter of the second draws on an exact node2vec prefix W_k / T of
+    the step the oracle takes there (the position walker's margin declines): those walks are
+    handed to the wave walker."""
+    g = walk_ref.CSR(csr.row_ptr, csr.host_col(), None)
+    deg = csr.degree()
+    n = len(starts)
+    u = rng.random((n, L - 1))
+    for w in range(0, n, 4):
+        s = int(starts[w])
+        u[w, 0] = float(rng.integers(1, deg[s])) / deg[s] if deg[s] > 1 else u[w, 0]
+    for w in range(1, n, 4):
+        s = int(starts[w])
+        v1 = walk_ref.walks_replay(g, np.asarray([s], dtype=np.int32), 2, 'node2vec', p, q,
+                                   u[w:w + 1, :1])[0, 1]
+        nbrs, wt = walk_ref.node2vec_weights(g, s, int(v1), p, q)
+        if len(nbrs) < 2:
+            continue
+        k = int(rng.integers(0, len(nbrs) - 1))
+        u[w, 1] = float(np.sum(wt[:k + 1])) / float(np.sum(wt))
+    return u
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (2.0, 0.5), (1.0, 1.0)])
+def test_n2v_positions_hand_over_vs_oracle(p, q, hip_device):
+    """dw_walk_replay_positions hands a walk whose pick its margin cannot decide (uniforms on
+    exact class boundaries, at the first step and at a second-order step) to the wave walker,
+    which finishes it from that step: the walks equal the oracle's serial replay bit for bit,
+    and equal the wave walker's (DW_N2V_POS=0)."""
+    import os
+    f = golden('walks_rmat12_node2vec_p0.25_q4.npz')
+    csr = _csr(f)
+    rng = np.random.default_rng(17)
+    deg = csr.degree()
+    nodes = np.nonzero(deg > 0)[0]
+    starts = rng.choice(nodes, 512).astype(np.int32)
+    L = 12
+    u = _boundary_uniforms(csr, starts, L, p, q, rng)
+    got = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(torch.as_tensor(starts),
+                                                                   uniforms=u).cpu().numpy()
+    assert csr.device_tensors(hip_device).get('n2v_rec') is not None
+    ref = walk_ref.walks_replay(walk_ref.CSR(csr.row_ptr, csr.host_col(), None), starts, L,
+                                'node2vec', p, q, u)
+    np.testing.assert_array_equal(got, ref)
+    os.environ['DW_N2V_POS'] = '0'
+    try:
+        wave = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(
+            torch.as_tensor(starts), uniforms=u).cpu().numpy()
+    finally:
+        del os.environ['DW_N2V_POS']
+    np.testing.assert_array_equal(wave, ref)
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0)])
+def test_n2v_positions_equal_wave_walker_c3(p, q, hip_device, monkeypatch):
+    """C3's graph (R-MAT 20, hubs of 44,848): the position walker gives the wave walker's walks
+    bit for bit from hubs and random nodes, reading a few position entries per step where the
+    wave walker reads hundreds of list entries."""
+    csr = rmat_graph(20, 10_000_000, 0, device=hip_device)
+    deg = csr.degree()
+    rng = np.random.default_rng(23)
+    hubs = np.argsort(-deg[1:])[:256] + 1
+    starts = torch.as_tensor(np.concatenate([np.resize(hubs, 4096),
+                                             rng.integers(1, csr.vocab_size, 12288)]
+                                            ).astype(np.int32))
+    L = 20
+    u = torch.from_numpy(rng.random((starts.numel(), L - 1))).to(hip_device)
+    w = Node2Vec(csr, L, p=p, q=q, device=hip_device)
+    out = torch.empty((starts.numel(), L), dtype=torch.int32, device=hip_device)
+    c_pos = w.count_replay_traffic(starts, u, out=out)
+    got = out.cpu().numpy()
+    assert csr.device_tensors(hip_device)['n2v_rec'] is not None
+    monkeypatch.setenv('DW_N2V_POS', '0')
+    c_wave = w.count_replay_traffic(starts, u, out=out)
+    np.testing.assert_array_equal(got, out.cpu().numpy())
+    assert c_pos['steps'] == c_wave['steps'] == starts.numel() * (L - 1)
+    assert c_pos['entries'] * 20 < c_wave['entries']
