@@ -165,6 +165,32 @@ int adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *l
                      const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                      const float *hist, int32_t step, bool p_only, hipStream_t stream);
 
+// ---- deterministic accumulation (dw_exact_register) -----------------------------------------
+// A gradient term t (fp32) enters an int64 accumulator as round(t * 2^frac): integer sums are
+// associative, so the accumulated value is independent of the order of the atomics and of how
+// the terms are split over waves, chunks or ranks. One f64 product (exact: a power of two) and
+// the 1.5 * 2^52 magic addition round to the nearest integer; valid while |t| 2^frac < 2^51
+// (`range` records a term past it: DW_S_FIXED_RANGE).
+struct Fixed {
+    int64_t *acc;       // the accumulator of the launch's gradient buffer (NULL: float path)
+    double fs, fi;      // 2^frac, 2^-frac
+};
+
+__device__ __forceinline__ int64_t to_fixed(float t, double fs, bool &range) {
+    const double y = static_cast<double>(t) * fs;
+    range = range || !(fabs(y) < 0x1p51);
+    const double r = y + 6755399441055744.0;
+    return __double_as_longlong(r) - 0x4338000000000000LL;
+}
+
+__device__ __forceinline__ float from_fixed(int64_t a, double fi) {
+    return static_cast<float>(static_cast<double>(a) * fi);
+}
+
+__device__ __forceinline__ void fixed_add(int64_t *dst, int64_t v) {
+    if (v) atomicAdd(reinterpret_cast<unsigned long long *>(dst), static_cast<unsigned long long>(v));
+}
+
 // Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
 __device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
     const float *h = hist + 8 * s;

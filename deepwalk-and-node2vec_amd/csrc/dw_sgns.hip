@@ -23,6 +23,7 @@
 //     gathered bytes move at read speed, not atomic speed.
 #include <stdlib.h>
 
+#include <cmath>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -156,6 +157,7 @@ struct SgnsArgs {
     const uint32_t *occ;      // centres in node order (k_occ_keys + sort): wave g takes
     int64_t occ_per_wave;     //   occ[g * occ_per_wave, (g+1) * occ_per_wave)
     const dw_step_scalars *dyn;   // bound step block (graph replay): noise_offset from it
+    dw::Fixed fx_in{};        // deterministic mode: g_in's int64 accumulator (dw_exact_register)
 };
 
 #ifndef DW_NOISE_ROUNDS
@@ -207,8 +209,12 @@ __device__ __forceinline__ int64_t row_id(const SgnsArgs &a, int64_t b, const in
 // butterfly every lane holds every logit; lane t evaluates sigmoid / log / the clamp mask for
 // its own row only and the coefficients are read back per row. Records are written by the
 // owning lane (coalesced), so no LDS staging is needed.
-template <int VPL, bool MASKED, bool FROM_WALKS, bool RECORDS, int CH>
+// EXACT (records only, no pooling): each centre-gradient term enters g_in's int64 accumulator
+// as a fixed-point integer (dw::to_fixed) — the sum independent of the atomics' order.
+template <int VPL, bool MASKED, bool FROM_WALKS, bool RECORDS, int CH, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
+    static_assert(!EXACT || RECORDS, "the exact form writes records");
+    bool range = false;   // EXACT: a term past the fixed-point range
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
@@ -248,6 +254,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
             continue;
         }
         float c[VPL], gc[VPL];
+        int64_t gx[VPL];
         const float *crow = a.w_in + cid * a.d + lane;
 #pragma unroll
         for (int m = 0; m < VPL; ++m) {
@@ -255,6 +262,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                    : pool   ? pooled(a.inputs, b, a.n_in, a.w_in, a.d, lane + WAVE * m)
                             : crow[WAVE * m];
             gc[m] = 0.f;
+            gx[m] = 0;
         }
         for (int g0 = 0; g0 < n_rows; g0 += WAVE) {
             const int g_rows = (n_rows - g0 < WAVE) ? n_rows - g0 : WAVE;
@@ -314,7 +322,12 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                     const float gs =
                         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(coef), r0 + u));
 #pragma unroll
-                    for (int m = 0; m < VPL; ++m) gc[m] += gs * o[u][m];
+                    for (int m = 0; m < VPL; ++m) {
+                        if constexpr (EXACT)
+                            gx[m] += dw::to_fixed(gs * o[u][m], a.fx_in.fs, range);
+                        else
+                            gc[m] += gs * o[u][m];
+                    }
                     if (!RECORDS && gs != 0.f) {
                         float *grow = a.g_out + static_cast<int64_t>(id[u]) * a.d + lane;
 #pragma unroll
@@ -335,6 +348,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                 for (int m = 0; m < VPL; ++m)
                     if (live[m]) atomicAdd(grow + WAVE * m, gc[m] / static_cast<float>(a.n_in));
             }
+        } else if constexpr (EXACT) {
+            int64_t *gxrow = a.fx_in.acc + cid * a.d + lane;
+#pragma unroll
+            for (int m = 0; m < VPL; ++m)
+                if (live[m]) dw::fixed_add(gxrow + WAVE * m, gx[m]);
         } else {
             float *gcrow = a.g_in + cid * a.d + lane;
 #pragma unroll
@@ -342,6 +360,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_sgns(SgnsArgs a) {
                 if (live[m]) atomicAdd(gcrow + WAVE * m, gc[m]);
         }
     }
+    if constexpr (EXACT)
+        if (__ballot(range) && lane == 0) dw::status_or(a.status, DW_S_FIXED_RANGE);
 
     // loss partials: wave-reduce the per-lane sums, one double atomic per wave and value
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
@@ -386,14 +406,18 @@ __device__ __forceinline__ float row_sum16(float x) {
 // grow W-fold (2.35 GB per pass at W = 8, C3). The owner form therefore takes the centres in
 // node order (a sorted occurrence list, contiguous per wave): consecutive occurrences of one
 // node are summed in registers (pend) and leave as ONE atomic row per run.
-template <int F4, bool FROM_WALKS, int CHR, bool OWNER>
+// EXACT: the centre-gradient terms enter g_in's int64 accumulator as fixed-point integers
+// (dw::to_fixed), each lane adding its 4 F4 elements of its group's centre straight from
+// registers (no LDS staging, no run summing: integer sums need no order).
+template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ uint8_t s_t[WAVES_PER_BLOCK][4][OWNER ? G16_TMAX : 1];
-    __shared__ float4 s_g[WAVES_PER_BLOCK][4][16 * F4];
+    __shared__ float4 s_g[WAVES_PER_BLOCK][4][EXACT ? 1 : 16 * F4];
+    bool range = false;   // EXACT: a term past the fixed-point range
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int q = lane >> 4, gl = lane & 15;
@@ -524,6 +548,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             n_loop = max(max(c0, c1), max(c2, c3));
         }
         float4 c4[F4], g4[F4];
+        int64_t gx[EXACT ? 4 * F4 : 1];
         const float *crow = a.w_in + (ok_c ? cid : 0) * D + 4 * gl;
 #pragma unroll
         for (int f = 0; f < F4; ++f) {
@@ -531,6 +556,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                          : make_float4(0.f, 0.f, 0.f, 0.f);
             g4[f] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#pragma unroll
+        for (int k = 0; k < (EXACT ? 4 * F4 : 1); ++k) gx[k] = 0;
         dw::wave_lds_sync();
         auto load_chunk = [&](float4(&o4)[CHR][F4], int32_t(&rid)[CHR], int t0) {
 #pragma unroll
@@ -580,6 +607,17 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 #pragma unroll
             for (int u = 0; u < CHR; ++u) {
                 const float cu = __shfl(coef, (q << 4) | u, WAVE);
+                if constexpr (EXACT) {
+                    const double fs = a.fx_in.fs;
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) {
+                        gx[4 * f + 0] += dw::to_fixed(cu * o4[u][f].x, fs, range);
+                        gx[4 * f + 1] += dw::to_fixed(cu * o4[u][f].y, fs, range);
+                        gx[4 * f + 2] += dw::to_fixed(cu * o4[u][f].z, fs, range);
+                        gx[4 * f + 3] += dw::to_fixed(cu * o4[u][f].w, fs, range);
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
                     g4[f].x = fmaf(cu, o4[u][f].x, g4[f].x);
@@ -597,8 +635,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             load_chunk(o4, rid, t0);
             compute_chunk(o4, rid, t0);
         }
+        if constexpr (!EXACT) {
 #pragma unroll
-        for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
+            for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
+        }
         dw::wave_lds_sync();
         if constexpr (OWNER) {  // the wave's owned records, appended to its region
             const int c0 = __builtin_amdgcn_readlane(n_own, 0);
@@ -638,6 +678,17 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 }
             }
         }
+        if constexpr (EXACT) {   // the group's centre, 4 F4 elements per lane
+            if (ok_c && n_own > 0) {
+                int64_t *dst = a.fx_in.acc + cid * D + 4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) dw::fixed_add(dst + 64 * f + k, gx[4 * f + k]);
+            }
+            dw::wave_lds_sync();
+            continue;
+        }
         // centre gradients: per centre, 64 lanes x dword = 256 contiguous bytes per atomic
         const float *sg_flat = reinterpret_cast<const float *>(&s_g[wv][0][0]);
 #pragma unroll
@@ -675,8 +726,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         }
         dw::wave_lds_sync();
     }
+    if constexpr (EXACT)
+        if (__ballot(range) && lane == 0) dw::status_or(a.status, DW_S_FIXED_RANGE);
     if constexpr (OWNER) {
-        if (pend_c >= 0) {
+        if (!EXACT && pend_c >= 0) {
             float *dst = a.g_in + static_cast<int64_t>(pend_c) * D + lane;
 #pragma unroll
             for (int f = 0; f < F4; ++f) atomicAdd(dst + 64 * f, pend[f]);
@@ -795,11 +848,16 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
 
 // range (row pieces, dw_sgns_walks_phase2_piece): only records [range[0], range[1]) — the
 // records of whole rows, so a piece's rows never continue in another piece's chunks.
-template <int VPL, bool MASKED, bool ADAM>
+// EXACT: each term coef * w_in enters the row's int64 sum as a fixed-point integer (fo); a row
+// inside the chunk converts its exact sum back to float for the update, a straddling row adds
+// its integer part into fo.acc (k_fixed_boundary converts it once every chunk has).
+template <int VPL, bool MASKED, bool ADAM, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_rec_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
-                 int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch) {
+                 int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch,
+                 dw::Fixed fo, int32_t *status) {
+    bool fx_range = false;
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t lo = range ? range[0] : 0;
@@ -823,11 +881,26 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         const uint32_t last = keys[e1 - 1];
         uint32_t cur = keys[e0];
         float g[VPL];
+        int64_t gx[VPL];
 #pragma unroll
-        for (int m = 0; m < VPL; ++m) g[m] = 0.f;
+        for (int m = 0; m < VPL; ++m) {
+            g[m] = 0.f;
+            gx[m] = 0;
+        }
 
         auto flush = [&](uint32_t row) {
             float *dst = g_out + static_cast<int64_t>(row) * d + lane;
+            if constexpr (EXACT) {
+                if (row == before || row == after) {   // the integer part of a straddling row
+                    int64_t *acc = fo.acc + static_cast<int64_t>(row) * d + lane;
+#pragma unroll
+                    for (int m = 0; m < VPL; ++m)
+                        if (live[m]) dw::fixed_add(acc + WAVE * m, gx[m]);
+                    return;
+                }
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) g[m] = dw::from_fixed(gx[m], fo.fi);
+            }
             if (row != before && row != after) {
                 if (ADAM && oa.last) {
                     lazy_row_step<VPL, MASKED>(oa, lstep, row, d, lane, g);
@@ -876,13 +949,97 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                     flush(cur);
                     cur = k[u];
 #pragma unroll
-                    for (int m = 0; m < VPL; ++m) g[m] = 0.f;
+                    for (int m = 0; m < VPL; ++m) {
+                        g[m] = 0.f;
+                        gx[m] = 0;
+                    }
                 }
 #pragma unroll
-                for (int m = 0; m < VPL; ++m) g[m] += coef[u] * x[u][m];
+                for (int m = 0; m < VPL; ++m) {
+                    if constexpr (EXACT)
+                        gx[m] += dw::to_fixed(coef[u] * x[u][m], fo.fs, fx_range);
+                    else
+                        g[m] += coef[u] * x[u][m];
+                }
             }
         }
         flush(cur);
+    }
+    if constexpr (EXACT)
+        if (__ballot(fx_range) && lane == 0) dw::status_or(status, DW_S_FIXED_RANGE);
+}
+
+// Deterministic mode, after k_rec_gather: the rows that straddle chunks hold their sums in the
+// int64 accumulator; each such row converts once (the first and last rows of every chunk are
+// visited, the per-element exchange hands each value to exactly one of the visitors, which
+// adds it to g_out; the others add nothing), before k_adam_rest / k_lazy_boundary read g_out.
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
+    k_fixed_boundary(const uint32_t *__restrict__ keys, int64_t n_rec, int32_t gch,
+                     const int64_t *__restrict__ range, dw::Fixed fo, float *__restrict__ g_out,
+                     int32_t d) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t lo = range ? range[0] : 0;
+    const int64_t hi = range ? range[1] : n_rec;
+    const int64_t n_chunks = (hi - lo + gch - 1) / gch;
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; ch < n_chunks;
+         ch += n_waves) {
+        const int64_t e0 = lo + ch * gch;
+        const int64_t e1 = (e0 + gch < hi) ? e0 + gch : hi;
+        const uint32_t first = keys[e0], last = keys[e1 - 1];
+        const bool a = e0 > lo && keys[e0 - 1] == first;
+        const bool b = e1 < hi && keys[e1] == last;
+        for (int k = 0; k < 2; ++k) {
+            if (!(k == 0 ? a : b)) continue;
+            const int64_t o = static_cast<int64_t>(k == 0 ? first : last) * d;
+            for (int e = lane; e < d; e += WAVE) {
+                const unsigned long long v =
+                    atomicExch(reinterpret_cast<unsigned long long *>(fo.acc + o + e), 0ull);
+                if (v) atomicAdd(g_out + o + e, dw::from_fixed(static_cast<int64_t>(v), fo.fi));
+            }
+        }
+    }
+}
+
+// Deterministic mode, after pass 1: every centre's row of the int64 accumulator converted into
+// g_in (the same exchange rule as k_fixed_boundary: one visitor per element adds the value).
+template <bool FROM_WALKS>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE) k_fixed_centres(SgnsArgs a) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    for (int64_t b = (int64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / WAVE; b < a.batch;
+         b += n_waves) {
+        int64_t cid;
+        if (FROM_WALKS) {
+            const int64_t per = a.L - 2 * a.R;
+            const int64_t w = b / per;
+            cid = a.walks[w * a.L + a.R + (b - w * per)];
+        } else {
+            cid = a.inputs[b];
+        }
+        if (cid < 0 || cid >= a.V) continue;
+        const int64_t o = cid * a.d;
+        for (int e = lane; e < a.d; e += WAVE) {
+            const unsigned long long v =
+                atomicExch(reinterpret_cast<unsigned long long *>(a.fx_in.acc + o + e), 0ull);
+            if (v) atomicAdd(a.g_in + o + e, dw::from_fixed(static_cast<int64_t>(v), a.fx_in.fi));
+        }
+    }
+}
+
+// Dense conversion (dw_fixed_to_float): g = (accumulate ? g : 0) + fl(acc), acc = 0.
+__global__ void k_fixed_dense(int64_t *__restrict__ acc, float *__restrict__ g, int64_t n,
+                              double fi, int32_t accumulate) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t v = acc[i];
+        if (v) acc[i] = 0;
+        const float f = dw::from_fixed(v, fi);
+        if (accumulate) {
+            if (v) g[i] += f;
+        } else {
+            g[i] = f;
+        }
     }
 }
 
@@ -1017,15 +1174,52 @@ int64_t grid_cap(int per_cu) {
     return (int64_t)n_cu[dev] * per_cu;
 }
 
+// ---- deterministic mode: gradient buffers with an int64 fixed-point accumulator -------------
+struct ExactEntry {
+    int64_t *acc;
+    int64_t n;
+    int32_t frac, flags;
+};
+std::mutex g_exact_mu;
+std::unordered_map<const float *, ExactEntry> g_exact;
+
+// The accumulator registered for gradient buffer g (dw_exact_register) as a launch's Fixed,
+// {NULL} when g has none; `need` elements must fit.
+int exact_of(const float *g, int64_t need, dw::Fixed *fx, int32_t *flags, const char *who) {
+    *fx = dw::Fixed{};
+    if (flags) *flags = 0;
+    if (!g) return DW_OK;
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    const auto it = g_exact.find(g);
+    if (it == g_exact.end()) return DW_OK;
+    DW_REQUIRE(it->second.n >= need, "%s: the registered accumulator holds %lld elements, the "
+               "launch needs %lld", who, (long long)it->second.n, (long long)need);
+    *fx = dw::Fixed{it->second.acc, ldexp(1.0, it->second.frac), ldexp(1.0, -it->second.frac)};
+    if (flags) *flags = it->second.flags;
+    return DW_OK;
+}
+
 template <bool FROM_WALKS, bool RECORDS>
 int launch_pass1(const SgnsArgs &a, hipStream_t st) {
     int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    const bool exact = a.fx_in.acc != nullptr;
+    DW_REQUIRE(!exact || RECORDS, "dw_sgns: the deterministic mode needs the records (sorted) "
+               "output-table path");
+    DW_REQUIRE(!exact || FROM_WALKS || a.n_in == 1,
+               "dw_sgns: the deterministic mode does not cover pooled (CBOW) inputs");
 #define DW_SGNS_CASE(VPL)                                                                    \
     if (a.d <= 64 * VPL) {                                                                    \
-        if (a.d == 64 * VPL)                                                                  \
+        const bool full = a.d == 64 * VPL;                                                    \
+        if (exact && RECORDS && full)                                                         \
+            hipLaunchKernelGGL((k_sgns<VPL, false, FROM_WALKS, RECORDS, CHUNK, RECORDS>), g,  \
+                               bl, 0, st, a);                                                 \
+        else if (exact && RECORDS)                                                            \
+            hipLaunchKernelGGL((k_sgns<VPL, true, FROM_WALKS, RECORDS, CHUNK, RECORDS>), g,   \
+                               bl, 0, st, a);                                                 \
+        else if (full)                                                                        \
             hipLaunchKernelGGL((k_sgns<VPL, false, FROM_WALKS, RECORDS, CHUNK>), g, bl, 0, st, \
                                a);                                                            \
         else                                                                                  \
@@ -1057,6 +1251,17 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    if (a.fx_in.acc) {   // deterministic mode
+        switch (a.d / 64) {
+            case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, OWNER, true>), g, bl, 0, st, a); break;
+            case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER, true>), g, bl, 0, st, a); break;
+            case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, OWNER, true>), g, bl, 0, st, a); break;
+            case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER, true>), g, bl, 0, st, a); break;
+            default: return DW_E_UNSUPPORTED;
+        }
+        DW_LAUNCH_CHECK("dw_sgns/g16");
+        return DW_OK;
+    }
     switch (a.d / 64) {  // rows per chunk: CHR * F4 float4 registers per lane
         case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, OWNER>), g, bl, 0, st, a); break;
         case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER>), g, bl, 0, st, a); break;
@@ -1173,26 +1378,40 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
                            range);
 }
 
+template <int VPL, bool EXACT>
+void launch_gather_fx(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys,
+                      const uint64_t *vals, int64_t n_rec, const float *w_in, float *g_out,
+                      int32_t d, const OutAdam *oa, const int64_t *range, int32_t gch,
+                      const dw::Fixed &fo, int32_t *status) {
+    const bool full = d == 64 * VPL;
+    if (oa) {
+        if (full)
+            hipLaunchKernelGGL((k_rec_gather<VPL, false, true, EXACT>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, *oa, range, gch, fo, status);
+        else
+            hipLaunchKernelGGL((k_rec_gather<VPL, true, true, EXACT>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, *oa, range, gch, fo, status);
+    } else {
+        if (full)
+            hipLaunchKernelGGL((k_rec_gather<VPL, false, false, EXACT>), g, bl, 0, st, keys,
+                               vals, n_rec, w_in, g_out, d, OutAdam{}, range, gch, fo, status);
+        else
+            hipLaunchKernelGGL((k_rec_gather<VPL, true, false, EXACT>), g, bl, 0, st, keys, vals,
+                               n_rec, w_in, g_out, d, OutAdam{}, range, gch, fo, status);
+    }
+}
+
 template <int VPL>
 void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const uint64_t *vals,
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
-                   const OutAdam *oa, const int64_t *range, int32_t gch) {
-    const bool exact = d == 64 * VPL;
-    if (oa) {
-        if (exact)
-            hipLaunchKernelGGL((k_rec_gather<VPL, false, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa, range, gch);
-        else
-            hipLaunchKernelGGL((k_rec_gather<VPL, true, true>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, *oa, range, gch);
-    } else {
-        if (exact)
-            hipLaunchKernelGGL((k_rec_gather<VPL, false, false>), g, bl, 0, st, keys, vals,
-                               n_rec, w_in, g_out, d, OutAdam{}, range, gch);
-        else
-            hipLaunchKernelGGL((k_rec_gather<VPL, true, false>), g, bl, 0, st, keys, vals, n_rec,
-                               w_in, g_out, d, OutAdam{}, range, gch);
-    }
+                   const OutAdam *oa, const int64_t *range, int32_t gch, const dw::Fixed &fo,
+                   int32_t *status) {
+    if (fo.acc)
+        launch_gather_fx<VPL, true>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch,
+                                    fo, status);
+    else
+        launch_gather_fx<VPL, false>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range,
+                                     gch, fo, status);
 }
 
 template <int VPL>
@@ -1214,7 +1433,12 @@ void launch_rest(hipStream_t st, int64_t V, int32_t d, float *g_out, const OutAd
 // sized for `share` of the records (grid-stride beyond).
 int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, const float *w_in,
                  float *g_out, int32_t d, const OutAdam *oa, int64_t V, hipStream_t st,
-                 const int64_t *range = nullptr, double share = 1.0) {
+                 const int64_t *range = nullptr, double share = 1.0, int32_t *status = nullptr) {
+    dw::Fixed fo;   // deterministic mode: g_out's accumulator
+    {
+        const int rc = exact_of(g_out, V * d, &fo, nullptr, "dw_sgns pass 2");
+        if (rc != DW_OK) return rc;
+    }
     // chunk size: GCH for large batches (balanced, few boundary rows); halved down to 32 while
     // the chunks would not give every SIMD of the chip a few waves — a 9K-record batch (C2 shape)
     // in 512-record chunks ran as 18 waves, 240 us of latency-bound gathers
@@ -1233,12 +1457,16 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
-    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
-    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
-    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch);
+    if (d <= 64) launch_gather<1>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch, fo, status);
+    else if (d <= 128) launch_gather<2>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch, fo, status);
+    else if (d <= 256) launch_gather<4>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch, fo, status);
+    else if (d <= 512) launch_gather<8>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch, fo, status);
     else return DW_E_UNSUPPORTED;
     DW_LAUNCH_CHECK("dw_sgns/gather");
+    if (fo.acc && n_rec > 0) {   // the straddling rows' exact sums into g_out
+        hipLaunchKernelGGL(k_fixed_boundary, g, bl, 0, st, keys, n_rec, gch, range, fo, g_out, d);
+        DW_LAUNCH_CHECK("dw_sgns/fixed_boundary");
+    }
     if (oa && oa->last) {   // lazy: only the straddling rows remain; untouched rows wait
         if (n_rec > 0) {
             if (d <= 64) launch_boundary<1>(st, keys, n_rec, gch, g_out, d, *oa, range);
@@ -1317,6 +1545,12 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     }
     if (a.batch == 0 || workspace == nullptr) {
         if (do1 && a.batch > 0) {
+            dw::Fixed f0;
+            int rc0 = exact_of(a.g_in, 0, &f0, nullptr, "dw_sgns");
+            if (rc0 == DW_OK) rc0 = exact_of(a.g_out, 0, &f0, nullptr, "dw_sgns");
+            if (rc0 != DW_OK) return rc0;
+            DW_REQUIRE(!f0.acc, "dw_sgns: the deterministic mode needs the records (sorted) "
+                       "output-table path (a workspace)");
             const int rc = launch_pass1<FROM_WALKS, false>(a, st);
             if (rc != DW_OK) return rc;
         }
@@ -1338,9 +1572,19 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
     if (do1) {
         a.rec_key = ws.k0;
         a.rec_val = ws.v0;
+        int32_t fl = 0;
+        rc = exact_of(a.g_in, a.V * a.d, &a.fx_in, &fl, "dw_sgns pass 1");
+        if (rc != DW_OK) return rc;
         rc = launch_pass1_g16<FROM_WALKS>(a, st);
         if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
         if (rc != DW_OK) return rc;
+        if (a.fx_in.acc && !(fl & DW_EXACT_DEFER)) {   // the centres' exact sums into g_in
+            int64_t cb = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+            if (cb > grid_cap(8)) cb = grid_cap(8);
+            hipLaunchKernelGGL(k_fixed_centres<FROM_WALKS>, dim3((unsigned)cb),
+                               dim3(WAVES_PER_BLOCK * WAVE), 0, st, a);
+            DW_LAUNCH_CHECK("dw_sgns/fixed_centres");
+        }
         g_timer.mark(1, st);
     }
     if (!do2) return DW_OK;
@@ -1354,7 +1598,8 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
         return DW_E_HIP;
     }
     g_timer.mark(2, st);
-    return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, oa, a.V, st);
+    return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, oa, a.V, st,
+                        nullptr, 1.0, a.status);
 }
 
 // ---- output-table phase in row pieces (N > 1: exchange a piece while the next one runs) -------
@@ -1793,8 +2038,18 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
             if (rc != DW_OK) return rc;
         }
         a.occ = occ.v0;
+        int32_t fl = 0;
+        rc = exact_of(a.g_in, a.V * a.d, &a.fx_in, &fl, "dw_sgns_owner_pass1");
+        if (rc != DW_OK) return rc;
         rc = launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
+        if (a.fx_in.acc && !(fl & DW_EXACT_DEFER)) {   // one rank: the centres' exact sums
+            int64_t cb = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+            if (cb > grid_cap(8)) cb = grid_cap(8);
+            hipLaunchKernelGGL(k_fixed_centres<true>, dim3((unsigned)cb),
+                               dim3(WAVES_PER_BLOCK * WAVE), 0, st, a);
+            DW_LAUNCH_CHECK("dw_sgns_owner_pass1/fixed_centres");
+        }
         if (!dense) {
             hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, st, ws.wave_counts,
                                lay.n_waves, ws.wave_offsets, ws.count);
@@ -2175,6 +2430,44 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * T);
     return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
                                 n_rows, n_max, nullptr, hist, step - 1, p_only, st);
+}
+
+int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t frac,
+                      int32_t flags) {
+    DW_REQUIRE(grad && acc && n_elems >= 0, "dw_exact_register: bad arguments");
+    DW_REQUIRE(frac >= 0 && frac <= 62, "dw_exact_register: frac %d outside [0, 62]", frac);
+    DW_REQUIRE((flags & ~DW_EXACT_DEFER) == 0, "dw_exact_register: unknown flags %d", flags);
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    g_exact[grad] = ExactEntry{acc, n_elems, frac, flags};
+    return DW_OK;
+}
+
+int dw_exact_unregister(const float *grad) {
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    g_exact.erase(grad);
+    return DW_OK;
+}
+
+int32_t dw_exact_frac_bits(double scale) {
+    // terms are |coef| <= scale times table entries: 2^32 of headroom above scale's magnitude
+    // for the entries (|w| < 2^19 keeps a term under 2^51) and 2^31 of sum range left in int64
+    const double a = fabs(scale);
+    if (!(a > 0.0) || !std::isfinite(a)) return 40;
+    int f = 32 + static_cast<int>(ceil(-log2(a)));
+    return f < 16 ? 16 : (f > 62 ? 62 : f);
+}
+
+int dw_fixed_to_float(int64_t *acc, float *grad, int64_t n, int32_t frac, int32_t accumulate,
+                      void *stream) {
+    DW_REQUIRE(n >= 0 && frac >= 0 && frac <= 62, "dw_fixed_to_float: bad arguments");
+    if (n == 0) return DW_OK;
+    DW_REQUIRE(acc && grad, "dw_fixed_to_float: null pointer");
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    hipLaunchKernelGGL(k_fixed_dense, dim3((unsigned)blocks), dim3(256), 0, dw::as_stream(stream),
+                       acc, grad, n, ldexp(1.0, -frac), accumulate);
+    DW_LAUNCH_CHECK("dw_fixed_to_float");
+    return DW_OK;
 }
 
 int dw_sgns_timing(int32_t enable) {

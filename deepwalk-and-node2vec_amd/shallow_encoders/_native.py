@@ -31,6 +31,8 @@ DW_S_BAD_CSR = 8
 DW_S_BAD_INDEX = 16
 DW_S_RECORDS_FULL = 32
 DW_S_DUP_NEIGHBOR = 64
+DW_S_FIXED_RANGE = 128
+DW_EXACT_DEFER = 1
 
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
@@ -148,6 +150,10 @@ SIGNATURES = {
     'dw_n2v_edge_index_build': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _i64,
                                                _i64, _i64, _p, _p, _p, _p, _szp, _p, _p]),
     'dw_walk_replay_positions_workspace_bytes': (ctypes.c_size_t, [_i64]),
+    'dw_exact_register': (ctypes.c_int, [_p, _p, _i64, _i32, _i32]),
+    'dw_exact_unregister': (ctypes.c_int, [_p]),
+    'dw_exact_frac_bits': (ctypes.c_int32, [_f64]),
+    'dw_fixed_to_float': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),
     'dw_walk_replay_positions': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p,
                                                 _i64, _p, _i64, _i32, _f64, _f64, _p, _p, _p, _p,
                                                 ctypes.c_size_t, _p, _p]),
@@ -255,4 +261,7 @@ def check_status(status: torch.Tensor, what: str) -> None:
     if s & DW_S_DUP_NEIGHBOR:
         raise ValueError(f'{what}: a CSR row lists the same neighbour twice (the reference\'s '
                          f'networkx.Graph cannot hold a repeated edge)')
+    if s & DW_S_FIXED_RANGE:
+        raise OverflowError(f'{what}: a gradient term exceeded the deterministic mode\'s '
+                            f'fixed-point range (|term| * 2^frac >= 2^51)')
     raise RuntimeError(f'{what}: device status {s:#x}')

@@ -374,7 +374,12 @@ class GraphedTrainerStep:
         self.R, self.K = R, K
         self.centres = self.B * (L - 2 * R)
         records = self.centres * 2 * R * (1 + K)
-        self.scatter = ('atomic' if scatter == 'atomic' or (scatter == 'auto' and records <= 65_536)
+        from shallow_encoders.word2vec import exact
+        if exact.enabled() and scatter == 'atomic':
+            raise ValueError('GraphedTrainerStep: the deterministic mode needs the records step')
+        # (the deterministic mode takes the records step: the atomic scatter sums in floats)
+        self.scatter = ('atomic' if scatter == 'atomic' or (scatter == 'auto' and records <= 65_536
+                                                            and not exact.enabled())
                         else None)   # (None: the fused step)
         if self.scatter is None and not _use_records('sorted', 2 * R, K, w_in.shape[0]):
             raise ValueError('GraphedTrainerStep: shape outside the records path')

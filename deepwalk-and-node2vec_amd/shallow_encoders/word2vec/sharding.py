@@ -227,6 +227,18 @@ class ShardedTables:
         self.params[self._cur_in, :self.V].copy_(w_in)
         self.params[1, :self.V].copy_(w_out)
 
+    def enable_exact(self, grad_scale: float) -> None:
+        """The deterministic mode (word2vec/exact.py) for steps of this grad_scale: both
+        gradient buffers get int64 fixed-point accumulators. One rank only: the replicated N > 1
+        layout reduces float partial sums (use OwnerTables there)."""
+        from shallow_encoders.word2vec import exact
+        if self.multi:
+            raise NotImplementedError('the deterministic mode covers the owner layout at N > 1 '
+                                      '(OwnerTables), not the replicated one')
+        self._exact = exact.Registry()
+        self._exact.ensure(0, self.grads[0], grad_scale)
+        self._exact.ensure(1, self.grads[1], grad_scale)
+
     # ---- one table's exchange -------------------------------------------------------------------
     def _adam(self, p, g, t: int, zero_grad: bool) -> None:
         self.adam_impl(p, g, self.m[t].view(-1), self.v[t].view(-1), self.step_count, self.lr,
@@ -554,6 +566,22 @@ class OwnerTables:
         self.w_out.zero_()
         self.w_out[keep] = w_out[rows[keep]].to(self.device)
 
+    def enable_exact(self, grad_scale: float) -> None:
+        """The deterministic mode (word2vec/exact.py) for steps of this grad_scale: g_out and
+        g_in get int64 fixed-point accumulators. N > 1: each rank's centre sums stay integers,
+        are reduce-scattered as int64 (exact) and converted on the owning rank — the tables are
+        bit-identical to one rank's."""
+        from shallow_encoders.word2vec import exact
+        if getattr(self, 'lazy', False) or type(self) is not OwnerTables:
+            raise NotImplementedError('the deterministic mode covers the dense OwnerTables')
+        if self.emulated:
+            raise NotImplementedError('the deterministic mode needs the real collectives')
+        self._exact = exact.Registry()
+        self._exact.ensure(0, self.grads_in, grad_scale, defer=self.multi)
+        self._exact.ensure(1, self.g_out, grad_scale)
+        self._shard64 = torch.empty((self.S, self.d), dtype=torch.int64, device=self.device) \
+            if self.multi else None
+
     def full_w_out(self) -> torch.Tensor:
         """The whole (V, d) out table, gathered from every rank's slice (collective when N > 1)."""
         if self.emulated:
@@ -639,10 +667,21 @@ class OwnerTables:
             self._adam_own(src[a:b], dst[a:b], self.grads_in[a:b])
             self.grads_in.zero_()
             return None
-        w = dist.reduce_scatter_tensor(self.grad_shard.view(-1), self.grads_in.view(-1),
-                                       op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-        if async_op:
-            w.wait()
+        fx = self._exact.get(0) if getattr(self, '_exact', None) is not None else None
+        if fx is not None:   # deterministic: the integer centre sums, reduced exactly
+            w = dist.reduce_scatter_tensor(self._shard64.view(-1), fx.acc.view(-1),
+                                           op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=async_op)
+            if async_op:
+                w.wait()
+            fx.acc.zero_()
+            fx.convert(acc=self._shard64, out=self.grad_shard)
+        else:
+            w = dist.reduce_scatter_tensor(self.grad_shard.view(-1), self.grads_in.view(-1),
+                                           op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=async_op)
+            if async_op:
+                w.wait()
         self.grads_in.zero_()
         own = dst[a:b]
         self._adam_own(src[a:b], own, self.grad_shard)

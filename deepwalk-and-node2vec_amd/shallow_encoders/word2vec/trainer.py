@@ -43,6 +43,7 @@ import torch
 from torch.optim import Optimizer
 
 from shallow_encoders import _native
+from shallow_encoders.word2vec import exact
 from shallow_encoders.word2vec.model import W2VBase
 from shallow_encoders.word2vec.sgns import (SGNSLoss, _use_records, device_noise, loss_terms,
                                             renorm_, sgns_accumulate, sgns_phase_bytes)
@@ -89,6 +90,8 @@ class Word2VecTrainer(_Base):
         # set by GraphedTrainerStep for noise='torch': the step's negatives, already drawn on the
         # device from torch's generator stream (graph/rng.py DeviceMT.randint)
         self._noise_override = None
+        # the deterministic mode's accumulators (word2vec/exact.py; DW_DETERMINISTIC=1)
+        self._exact = None
 
     # ---- reference properties -------------------------------------------------------------
     @property
@@ -197,6 +200,15 @@ class Word2VecTrainer(_Base):
                 p.grad = torch.zeros_like(p)
             if isinstance(self._optimizer, Adam):
                 self._optimizer.mark_grads(fresh, True)
+            if exact.enabled():   # int64 fixed-point accumulators for the two gradient buffers
+                if self._exact is None:
+                    self._exact = exact.Registry()
+                scale = 1.0 / max(n_centres * C, 1)
+                self._exact.ensure(0, w_in.grad, scale)
+                self._exact.ensure(1, w_out.grad, scale)
+            elif self._exact is not None:
+                self._exact.release()
+                self._exact = None
             if targets is None and self._capture_scatter != 'atomic' and \
                     self._can_fuse_step(w_in, w_out, C):
                 acc = self._fused_walk_step(w_in, w_out, src, R, noise, offset)

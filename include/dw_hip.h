@@ -49,6 +49,7 @@ extern "C" {
 #define DW_S_BAD_INDEX      16   /* an index outside [0, V) reached the SGNS kernel                  */
 #define DW_S_RECORDS_FULL   32   /* owner-form SGNS records exceeded the workspace (not expected)    */
 #define DW_S_DUP_NEIGHBOR   64   /* a CSR row lists a neighbour twice (dw_csr_check_simple)          */
+#define DW_S_FIXED_RANGE   128   /* a gradient term past the deterministic fixed-point range         */
 
 #define DW_METHOD_DEEPWALK   0   /* random_walk_generator.py:56-72 ('deepwalk' and 'dfs')          */
 #define DW_METHOD_NODE2VEC   1   /* random_walk_generator.py:75-119                                  */
@@ -274,6 +275,28 @@ int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const in
                             int64_t n_edges, int64_t n_pos, int32_t *pos, int32_t *pos_unsorted,
                             int32_t *rec, void *tmp, size_t *tmp_bytes, int32_t *status,
                             void *stream);
+
+/* ---- deterministic accumulation (SURVEY.md §5 "race detection": run-to-run, eager / graph
+ * and 1 / N-rank bit-identical tables) --------------------------------------------------------
+ * Registers acc (int64[n_elems], zeroed by the caller) as the accumulator of the float gradient
+ * buffer grad: every later SGNS launch whose g_in / g_out is grad adds each gradient term t as
+ * round(t * 2^frac) into acc with integer atomics — sums independent of order and of how the
+ * terms are split over waves, chunks or ranks — and converts the exact sums back into grad
+ * (centre rows after pass 1, output rows in the records gather) unless flags has
+ * DW_EXACT_DEFER: then acc keeps the centre sums for the caller to reduce across ranks and
+ * convert (dw_fixed_to_float). The records (sorted) output path only; pooled (CBOW) inputs are
+ * refused. frac: dw_exact_frac_bits(the launches' grad scale). Host-side registry, keyed by
+ * the grad pointer (graph-captured launches keep the accumulator they were captured with). */
+#define DW_EXACT_DEFER 1
+int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t frac,
+                      int32_t flags);
+int dw_exact_unregister(const float *grad);
+/* 32 + ceil(-log2 |scale|), clamped to [16, 62]: terms |coef| <= |scale| times entries below
+ * 2^19 stay under 2^51, sums under 2^31 fit int64. */
+int32_t dw_exact_frac_bits(double scale);
+/* grad[i] = (accumulate ? grad[i] : 0) + fl(acc[i] * 2^-frac); acc[i] = 0 (i < n). */
+int dw_fixed_to_float(int64_t *acc, float *grad, int64_t n, int32_t frac, int32_t accumulate,
+                      void *stream);
 
 /* Bytes of dw_walk_replay_positions' workspace for n_walks walks. */
 size_t dw_walk_replay_positions_workspace_bytes(int64_t n_walks);

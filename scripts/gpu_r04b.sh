@@ -16,3 +16,8 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method threa
 tail -3 gpurun_out/r04b_n2v_tests.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --exact-steps 0 > gpurun_out/r04b_walkbench.log 2>&1 || { tail -20 gpurun_out/r04b_walkbench.log; exit 1; }
 grep '^{' gpurun_out/r04b_walkbench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({k: d.get(k) for k in ('walks_per_s_replay','roofline_walk')}, indent=1))"
+# the deterministic mode (tests/test_gpu_exact.py); a plain test failure (rc 1) does not stop the script
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_exact.py > gpurun_out/r04b_exact_tests.log 2>&1
+rc=$?
+tail -25 gpurun_out/r04b_exact_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
