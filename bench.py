@@ -279,7 +279,13 @@ def main():
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
                          'saves, 6.89 vs 6.89 ms/step at C3; on by default on the one-GPU lazy '
                          'path of small batches)')
+    ap.add_argument('--deterministic', action='store_true',
+                    help='the deterministic accumulation mode (word2vec/exact.py: int64 '
+                         'fixed-point gradient sums, bit-identical tables run to run and across '
+                         'ranks); dense in-table Adam and the records path, as that mode needs')
     args = ap.parse_args()
+    if args.deterministic:
+        args.n1_in_adam, args.scatter = 'dense', 'sorted'
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -389,6 +395,11 @@ def main():
     centres = B * (L - 2 * R)
     pairs_per_step = centres * 2 * R
     grad_scale = 1.0 / (pairs_per_step * W_eff)   # mean over the GLOBAL batch
+    if args.deterministic:
+        if lazy or auto_in:
+            raise SystemExit('--deterministic needs the dense in-table exchange '
+                             '(--in-exchange sharded)')
+        tables.enable_exact(grad_scale)
     walks_total = N * args.walks_per_node
     BG = B * W_eff if owner else B      # walks each rank generates per step (owner: all ranks')
     walks_buf = torch.empty((BG, L), dtype=torch.int32, device=dev)
@@ -988,6 +999,7 @@ def main():
                 f'in-table exchange overlapped'
                 + (f', out table in {tables.P} pieces pipelined' if pieces else '') + ')'),
         },
+        'deterministic': bool(args.deterministic),
         'in_exchange': args.in_exchange if owner else None,
         'in_exchange_calibration_ms_per_step': calib_ms,
         'walks_per_s': walk_stats.get('deepwalk'),

@@ -21,3 +21,11 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method threa
 rc=$?
 tail -25 gpurun_out/r04b_exact_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+# the deterministic mode's cost: C3 (8192 walks) and C3/64 (dense in-table Adam, records), float vs exact
+for b in 8192 64; do
+  for det in "" "--deterministic"; do
+    tag=det_b${b}${det:+_exact}
+    timeout -k 10 300 python bench.py --batch-walks $b --steps 100 --warmup 5 --no-cpu-baseline --no-walk-bench --exact-steps 0 --n1-in-adam dense --scatter sorted $det > gpurun_out/$tag.log 2>&1 || { tail -5 gpurun_out/$tag.log; exit 1; }
+    grep '^{' gpurun_out/$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', d['ms_per_step'], d.get('deterministic'))"
+  done
+done
