@@ -29,3 +29,6 @@ for b in 8192 64; do
     grep '^{' gpurun_out/$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', d['ms_per_step'], d.get('deterministic'))"
   done
 done
+# the records sort's tile / digit configurations
+timeout -k 10 180 ./scripts/microbench/sort_bench > gpurun_out/r04b_sort_bench.txt 2>&1 || { tail -5 gpurun_out/r04b_sort_bench.txt; exit 1; }
+cat gpurun_out/r04b_sort_bench.txt

@@ -103,5 +103,16 @@ int main(int argc, char **argv) {
     run<OS<8, 1024, 12>>("8-bit 1024x12", k0, k1, v0, v1, n, bits, tmp, cap);
     refill();
     run<OS<11, 1024, 16>>("11-bit 1024x16", k0, k1, v0, v1, n, bits, tmp, cap);
+    // round 4: bigger tiles put more items per bucket run (fewer partial lines)
+    refill();
+    run<OS<11, 1024, 20>>("11-bit 1024x20", k0, k1, v0, v1, n, bits, tmp, cap);
+    refill();
+    run<OS<11, 1024, 24>>("11-bit 1024x24", k0, k1, v0, v1, n, bits, tmp, cap);
+    refill();
+    run<OS<11, 1024, 32>>("11-bit 1024x32", k0, k1, v0, v1, n, bits, tmp, cap);
+    refill();
+    run<OS<10, 1024, 24>>("10-bit 1024x24 (3 passes)", k0, k1, v0, v1, n, bits, tmp, cap);
+    refill();
+    run<OS<11, 1024, 16>>("11-bit 1024x16 (product, again)", k0, k1, v0, v1, n, bits, tmp, cap);
     return 0;
 }
