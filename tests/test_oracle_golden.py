@@ -292,3 +292,25 @@ def test_edge_class_counts_follow_the_reference_weight_rule(name):
             assert int(cn[e]) >> 31 == sum(1 for x in w if x == 2.0)
             assert int(cn[e]) & 0x7FFFFFFF == sum(1 for x in w if x == 4.0)
     assert (cn >> 31 == 1).all()          # undirected: t is always a neighbour of v
+
+
+@pytest.mark.parametrize('name', ['walks_karate_node2vec_p1_q0.5.npz',
+                                  'walks_rmat12_node2vec_p0.25_q4.npz'])
+def test_edge_class_positions_follow_the_reference_weight_rule(name):
+    """oracle.walk_ref.edge_class_positions (what dw_n2v_edge_index_build stores: t's position
+    in N(v) and the ascending positions of the 1/q neighbours) reads, for every directed edge
+    t -> v, exactly the positions the reference's rule weights 1/p and 1/q (factors 2 and 4 at
+    p = 1/2, q = 1/4), and agrees with the class counts."""
+    f = golden(name)
+    g = walk_ref.CSR(f['row_ptr'], f['col'], None)
+    off, pos, pos_t = walk_ref.edge_class_positions(g)
+    cn = walk_ref.edge_class_counts(g)
+    n = len(g.row_ptr) - 1
+    for t in range(n):
+        for e in range(g.row_ptr[t], g.row_ptr[t + 1]):
+            _, w = walk_ref.node2vec_weights(g, t, g.col[e], 0.5, 0.25)
+            q_pos = [i for i, x in enumerate(w) if x == 4.0]
+            p_pos = [i for i, x in enumerate(w) if x == 2.0]
+            assert pos[off[e]:off[e + 1]].tolist() == q_pos
+            assert (pos_t[e] == p_pos[0]) if p_pos else pos_t[e] == -1
+            assert off[e + 1] - off[e] == int(cn[e]) & 0x7FFFFFFF
