@@ -877,7 +877,7 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._claim_out), _native.ptr(self._count_out),
                          _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
-                         self.out_flags(), _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         self.out_flags() & 3, _native.ptr(status), _native.ptr(ws), ws.numel(),
                          _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
