@@ -1,6 +1,8 @@
 """Reproducibility of tools/train.py's C2-shape loop: eager twice, graph-records, graph-auto;
-epoch losses and table differences (is the eager loop itself run-to-run reproducible?)."""
+epoch losses and table differences (is the eager loop itself run-to-run reproducible?).
+DW_DETERMINISTIC=1 in the environment runs it in the deterministic accumulation mode."""
 import os
+import random
 import sys
 import tempfile
 
@@ -27,6 +29,7 @@ for tag, g, sc in (('eagerA', '0', 'auto'), ('eagerB', '0', 'auto'), ('graphR', 
     os.environ['DW_TRAIN_GRAPH_SCATTER'] = sc
     out = os.path.join(tmp, tag)
     torch.manual_seed(0)
+    random.seed(0)   # the start-node shuffle draws from the global generator (datasets.py:45)
     last = train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
                             f'output_dir={out}', f'train.experiment={tag}'] + base)
     st = torch.load(os.path.join(out, 'graph_rmat', tag, 'checkpoints', 'last.ckpt'),

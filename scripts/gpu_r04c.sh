@@ -15,6 +15,12 @@ run() {  # run <name> <timeout_s> <cmd...>
   tail -n 4 "gpurun_out/$name.log" | cut -c1-600
   return $rc
 }
+# C3 at 64 walks: records per lazy-gather chunk (more waves in flight for the latency-bound gather)
+for g in 64 32; do
+  DW_GCH=$g run r04_c3_64_gch$g 300 python bench.py --batch-walks 64 --steps 400 --no-cpu-baseline --no-walk-bench --exact-steps 0 || exit 1
+  grep '^{' gpurun_out/r04_c3_64_gch$g.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('gch $g', d['ms_per_step'])"
+done
+run r04_exact_loop 600 python -u -m pytest tests/test_gpu_exact.py -x -q -p no:cacheprovider -rf --timeout 500 --timeout-method thread -k train_loop
 TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1"
 DW_BENCH_DIST=1 run r04_rccl_check 300 $TR --master-port 29621 bench.py --steps 20 --warmup 3 --no-walk-bench --no-cpu-baseline || exit 1
 DW_BENCH_DIST=1 DW_BENCH_CORRUPT=1 run r04_rccl_corrupt 300 $TR --master-port 29622 bench.py --steps 10 --warmup 2 --no-walk-bench --no-cpu-baseline

@@ -12,6 +12,7 @@ chunking of the records, a graph replay or the number of ranks:
     bit-identical tables.
 """
 import os
+import random
 import socket
 
 import numpy as np
@@ -236,6 +237,7 @@ def test_exact_train_loop_eager_twice_and_graphs_bit_identical(tmp_path, hip_dev
         monkeypatch.setenv('DW_TRAIN_GRAPH_SCATTER', 'auto')
         out = str(tmp_path / tag)
         torch.manual_seed(0)
+        random.seed(0)   # the start-node shuffle (datasets.py:45,86-88: the global generator)
         train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
                          f'output_dir={out}', f'train.experiment={tag}'] + base)
         ck = os.path.join(out, 'graph_rmat', tag, 'checkpoints', 'last.ckpt')
