@@ -392,7 +392,8 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, wd):
         ref.step()
     t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=lazy_out, wd=wd)
     if lazy_out:
-        assert t.out_flags() == (1 if wd else 3)
+        # placed, p-only catch-up and constant betas without weight decay (step 6: slot 0)
+        assert t.out_flags() == (1 if wd else 7)
     lag = int((t.last_in[:V] < steps).sum())
     assert lag > V // 2                      # most rows were deferred before the flush
     if lazy_out:
