@@ -1881,6 +1881,8 @@ int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t 
 // the records' placement (k_out_claim's ranks, one owner or many): rank[slot], off[row] (the
 // exclusive scan of the per-row counts, with one zero past the rows: off[local_rows] = their
 // total) and the scan's temporary storage; between the records part and OccSpace
+constexpr int PLACE_TILE = 4096;   // placement-scan counts per block (16 per thread; k_place_scan)
+
 struct PlaceSpace {
     uint32_t *rank, *off;
     void *tmp;
@@ -1888,14 +1890,8 @@ struct PlaceSpace {
 };
 
 int plan_place(int64_t n_slots, int64_t local_rows, void *base, PlaceSpace *pl, hipStream_t st) {
-    size_t tmp = 0;
-    if (rocprim::exclusive_scan(nullptr, tmp, static_cast<const uint32_t *>(nullptr),
-                                static_cast<uint32_t *>(nullptr), 0u,
-                                static_cast<size_t>(local_rows + 1), rocprim::plus<uint32_t>(),
-                                st) != hipSuccess) {
-        dw::set_error("dw_sgns_owner: placement scan size query failed");
-        return DW_E_HIP;
-    }
+    (void)st;
+    const size_t tmp = static_cast<size_t>((local_rows + PLACE_TILE - 1) / PLACE_TILE) * 4;
     const size_t a = align256((size_t)(n_slots > 0 ? n_slots : 1) * 4);
     const size_t b = align256((size_t)(local_rows + 1) * 4);
     char *p = static_cast<char *>(base);
@@ -2365,6 +2361,73 @@ __global__ void k_place_range(const uint32_t *__restrict__ off, int64_t n_rows,
     }
 }
 
+// The placement offsets in two short launches instead of a lookback scan (a 1M-row slice's
+// counts are 4 MB: the scan's cost is its latency, ~25 us as rocprim's decoupled lookback at
+// C3's 64-walk batch). k_place_sums: each 256-thread block sums its PLACE_TILE counts;
+// k_place_scan: each block adds the sums of the blocks before it (at most a few hundred, read
+// from L2) and scans its tile; the last block also writes the gather's range {0, total}.
+
+__global__ void __launch_bounds__(256)
+    k_place_sums(const uint32_t *__restrict__ counts, int64_t n, uint32_t *__restrict__ sums) {
+    __shared__ uint32_t s_w[4];
+    const int64_t a = (int64_t)blockIdx.x * PLACE_TILE;
+    uint32_t t = 0;
+    for (int k = 0; k < PLACE_TILE / 256; ++k) {
+        const int64_t i = a + k * 256 + threadIdx.x;
+        t += i < n ? counts[i] : 0u;
+    }
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ void __launch_bounds__(256)
+    k_place_scan(const uint32_t *__restrict__ counts, int64_t n, const uint32_t *__restrict__ sums,
+                 uint32_t *__restrict__ off, int64_t *__restrict__ range) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // this block's base: the sums of the blocks before it
+    uint32_t b = 0;
+    for (int64_t j = threadIdx.x; j < blockIdx.x; j += 256) b += sums[j];
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (lane == 0) s_w[wv] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    // thread k holds counts [a + 16k, a + 16k + 16): its sum, the block's exclusive scan of them
+    const int64_t a = (int64_t)blockIdx.x * PLACE_TILE + 16 * threadIdx.x;
+    uint32_t c[16], t = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        c[k] = a + k < n ? counts[a + k] : 0u;
+        t += c[k];
+    }
+    uint32_t x = t;   // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint32_t pre = s_base;
+    for (int w = 0; w < wv; ++w) pre += s_w[w];
+    uint32_t run = pre + x - t;   // exclusive prefix of this thread's first count
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (a + k < n) off[a + k] = run;
+        run += c[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) {   // off[n]: the total
+        off[n] = run;
+        range[0] = 0;
+        range[1] = static_cast<int64_t>(run);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -2430,17 +2493,15 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                        reinterpret_cast<unsigned long long *>(n_rows), place ? counts : nullptr,
                        place ? pl.rank : nullptr);
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
-    if (place) {   // every row's segment of the records: the scan of the counts (+ one zero)
-        size_t tb = pl.tmp_bytes;
-        if (rocprim::exclusive_scan(pl.tmp, tb, static_cast<const uint32_t *>(counts), pl.off, 0u,
-                                    static_cast<size_t>(local_rows + 1),
-                                    rocprim::plus<uint32_t>(), st) != hipSuccess) {
-            dw::set_error("dw_sgns_owner_out_catch_up: placement scan failed");
-            return DW_E_HIP;
-        }
-        hipLaunchKernelGGL(k_place_range, dim3(1), dim3(64), 0, st, pl.off, local_rows,
-                           ws.bounds + 2 * slot);
-        DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/range");
+    if (place) {   // every row's segment of the records: the scan of the counts (+ the total)
+        const int64_t nb = (local_rows + PLACE_TILE - 1) / PLACE_TILE;
+        DW_REQUIRE(pl.tmp_bytes >= (size_t)nb * 4, "dw_sgns_owner_out_catch_up: scan scratch");
+        uint32_t *sums = static_cast<uint32_t *>(pl.tmp);
+        hipLaunchKernelGGL(k_place_sums, dim3((unsigned)nb), dim3(256), 0, st, counts, local_rows,
+                           sums);
+        hipLaunchKernelGGL(k_place_scan, dim3((unsigned)nb), dim3(256), 0, st, counts, local_rows,
+                           sums, pl.off, ws.bounds + 2 * slot);
+        DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place");
     }
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1 (p_only:
     // only p is written back; the lazy gather replays m and v itself, cheaply, before the step)
