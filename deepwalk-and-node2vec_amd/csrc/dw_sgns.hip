@@ -2307,37 +2307,57 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // records, whose radix sort was ~10 launches and ~85 us of the step). The order of a row's
 // records is the order the atomics resolved — as nondeterministic as the float atomics of rows
 // that straddle two gather chunks. (The two atomics of a slot are independent: one round trip.)
+// CLAIM_TRIPS centres per wave, their row ids and atomics issued together (independent chains
+// in flight), and ONE list atomic per block for all of them: a same-address atomic per block
+// serialises (1,120 blocks of one trip each were ~36 us at C3's 64-walk batch).
+constexpr int CLAIM_TRIPS = 4;
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
                 uint32_t *__restrict__ count, uint32_t *__restrict__ rank) {
     const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
-    // one centre per wave; the block's claimed rows are appended with ONE counter atomic (a
-    // same-address atomic per wave serialised: 4,480 of them were ~40 us at the 64-walk batch)
+    __shared__ uint32_t s_rows[WAVES_PER_BLOCK][CLAIM_TRIPS * WAVE];
     __shared__ uint32_t s_cnt[WAVES_PER_BLOCK];
     __shared__ unsigned long long s_base;
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
-    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int T = a.C * (1 + a.K);
     const int64_t per = a.L - 2 * a.R;
-    for (int64_t b0 = (int64_t)blockIdx.x * WAVES_PER_BLOCK; b0 < a.batch; b0 += n_waves) {
-        const int64_t b = b0 + wv;   // block-uniform trip count (barriers below)
-        bool mine = false;
-        uint32_t lo = 0;
-        if (b < a.batch && lane < T) {
-            const int64_t w = b / per, i = a.R + b % per;
-            const int64_t o = row_id<true>(a, b, a.walks + w * a.L, i, lane);
-            if (o < 0 || o >= a.V) {
-                dw::status_or(a.status, DW_S_BAD_INDEX);
-            } else if (o % a.n_owners == a.owner) {
-                lo = static_cast<uint32_t>(o / a.n_owners);
-                mine = atomicMax(claim + lo, step) < step - 1;
-                if (count) rank[b * T + lane] = atomicAdd(count + lo, 1u);
+    const int64_t tile = (int64_t)WAVES_PER_BLOCK * CLAIM_TRIPS;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int64_t b0 = (int64_t)blockIdx.x * tile; b0 < a.batch; b0 += (int64_t)gridDim.x * tile) {
+        int64_t o[CLAIM_TRIPS];   // each trip's row (-1: none)
+#pragma unroll
+        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+            const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
+            o[k] = -1;
+            if (b < a.batch && lane < T) {
+                const int64_t w = b / per, i = a.R + b % per;
+                const int64_t r = row_id<true>(a, b, a.walks + w * a.L, i, lane);
+                if (r < 0 || r >= a.V)
+                    dw::status_or(a.status, DW_S_BAD_INDEX);
+                else if (r % a.n_owners == a.owner)
+                    o[k] = r / a.n_owners;
             }
         }
-        const unsigned long long mask = __ballot(mine);
-        if (lane == 0) s_cnt[wv] = static_cast<uint32_t>(__popcll(mask));
+        bool mine[CLAIM_TRIPS];
+#pragma unroll
+        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+            mine[k] = false;
+            if (o[k] >= 0) {
+                const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
+                mine[k] = atomicMax(claim + o[k], step) < step - 1;
+                if (count) rank[b * T + lane] = atomicAdd(count + o[k], 1u);
+            }
+        }
+        uint32_t n_mine = 0;   // wave-uniform
+#pragma unroll
+        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+            const uint64_t mask = __ballot(mine[k]);
+            if (mine[k]) s_rows[wv][n_mine + __popcll(mask & lt)] = static_cast<uint32_t>(o[k]);
+            n_mine += __popcll(mask);
+        }
+        if (lane == 0) s_cnt[wv] = n_mine;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t tot = 0;
@@ -2347,8 +2367,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         __syncthreads();
         unsigned long long base = s_base;
         for (int k = 0; k < wv; ++k) base += s_cnt[k];
-        if (mine) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = lo;
-        __syncthreads();   // s_cnt / s_base are rewritten next trip
+        for (uint32_t e = lane; e < n_mine; e += WAVE) list[base + e] = s_rows[wv][e];
+        __syncthreads();   // s_rows / s_cnt / s_base are rewritten next tile
     }
 }
 
@@ -2485,7 +2505,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                              "dw_sgns_owner_out_catch_up", vocab_size, nullptr, &pl, slot);
         if (rc != DW_OK) return rc;
     }
-    int64_t blocks = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    const int64_t ctile = (int64_t)WAVES_PER_BLOCK * CLAIM_TRIPS;
+    int64_t blocks = (a.batch + ctile - 1) / ctile;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
