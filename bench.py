@@ -519,8 +519,7 @@ def main():
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
                          grad_scale=grad_scale, loss_acc=loss_acc, status=status,
-                         order_ready=lazy, placed=lazy and bool(tables.out_flags() & 1),
-                         slot=1 if lazy and tables.out_flags() & 8 else 0)
+                         order_ready=lazy, placed=lazy and bool(tables.out_flags() & 1))
         if not gather:
             feed.next(s)
         if lazy:

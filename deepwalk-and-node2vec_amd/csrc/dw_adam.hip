@@ -293,11 +293,6 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     if (rc != DW_OK) return rc;
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
-    static const int64_t grid_cap_env = [] {   // (A/B, round 4: the catch-up beside the gather)
-        const char *e = getenv("DW_ROWS_ADAM_GRID");
-        return e ? atoll(e) : 0;
-    }();
-    if (grid_cap_env > 0 && blocks > grid_cap_env) blocks = grid_cap_env;
     DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
     const int threads = 64 * ((dim + 63) / 64);
     if (grad_rows)

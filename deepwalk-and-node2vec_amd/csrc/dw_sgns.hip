@@ -1903,15 +1903,10 @@ int plan_place(int64_t n_slots, int64_t local_rows, void *base, PlaceSpace *pl, 
     return DW_OK;
 }
 
-// Two placement slots (rank / off / scan scratch, and the gather's range at bounds + 2 slot):
-// the out rows of step s + 1 are claimed, counted and placed (slot (s + 1) & 1) while step s's
-// pass 1 and gather still read slot s & 1 (OwnerLazyTables.catch_up_out_ahead).
-constexpr int32_t DW_SLOT1 = 8;   // flags / order_ready bit: placement slot 1
-
 int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *workspace,
                     size_t workspace_bytes, Workspace *ws, OwnerLayout *lay, hipStream_t st,
                     const char *what, int64_t V = 0, OccSpace *occ = nullptr,
-                    PlaceSpace *place = nullptr, int slot = 0) {
+                    PlaceSpace *place = nullptr) {
     *lay = owner_layout(n_centres, T);
     DW_REQUIRE(lay->total < 0x7FFFFFFF, "%s: too many records (%lld)", what,
                (long long)lay->total);
@@ -1921,18 +1916,10 @@ int owner_workspace(int64_t n_centres, int64_t T, int64_t local_rows, void *work
     int rc = plan_workspace(lay->total, local_rows, workspace, ws, st);
     if (rc != DW_OK) return rc;
     PlaceSpace pl;
-    rc = plan_place(n_centres * T, local_rows,
-                    static_cast<char *>(workspace) + ws->total, &pl, st);
+    rc = plan_place(n_centres * T, local_rows, static_cast<char *>(workspace) + ws->total, &pl, st);
     if (rc != DW_OK) return rc;
-    if (place) {
-        if (slot)
-            rc = plan_place(n_centres * T, local_rows,
-                            static_cast<char *>(workspace) + ws->total + pl.total, place, st);
-        else
-            *place = pl;
-        if (rc != DW_OK) return rc;
-    }
-    size_t need = ws->total + 2 * pl.total;
+    if (place) *place = pl;
+    size_t need = ws->total + pl.total;
     if (occ) {
         rc = plan_occ(n_centres > 0 ? n_centres : 1, V, static_cast<char *>(workspace) + need, occ,
                       st);
@@ -2022,8 +2009,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     OccSpace occ;
     PlaceSpace pl;
     int rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
-                             "dw_sgns_owner_pass1", a.V, &occ, &pl,
-                             (order_ready & DW_SLOT1) ? 1 : 0);
+                             "dw_sgns_owner_pass1", a.V, &occ, &pl);
     if (rc != DW_OK) return rc;
     g_timer.mark(0, st);
     // n_owners > 1: per-wave regions in (k0, v0), compacted into (k1, v1); one owner keeps
@@ -2081,7 +2067,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
 int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t d,
                        const float *w_in, float *g_out, const OutAdam *oa, void *workspace,
                        size_t workspace_bytes, int64_t *n_records, hipStream_t st,
-                       bool placed = false, int slot = 0) {
+                       bool placed = false) {
     Workspace ws;
     OwnerLayout lay;
     int rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
@@ -2092,12 +2078,12 @@ int launch_owner_pass2(int64_t n_centres, int64_t T, int64_t local_rows, int32_t
     int64_t n_rec = bound;
     if (placed) {
         // pass 1 wrote every record into its row's segment of (k1, v1): no sort; the range
-        // [0, count) was written by the catch-up (k_place_range); the grid is sized for the bound
+        // [0, count) was written by the catch-up (k_place_scan); the grid is sized for the bound
         DW_REQUIRE(!n_records, "dw_sgns_owner_pass2: placed records need n_records NULL");
         g_timer.mark(2, st);
         if (bound > 0 || oa) {
             rc = launch_pass2(ws.k1, ws.v1, bound, w_in, g_out, d, oa, local_rows, st,
-                              bound > 0 ? ws.bounds + 2 * slot : nullptr);
+                              bound > 0 ? ws.bounds : nullptr);
             if (rc != DW_OK) return rc;
         }
         g_timer.mark(3, st);
@@ -2372,15 +2358,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     }
 }
 
-// the placed records' range for the gather (off[n_rows] = their count)
-__global__ void k_place_range(const uint32_t *__restrict__ off, int64_t n_rows,
-                              int64_t *__restrict__ range) {
-    if (threadIdx.x == 0) {
-        range[0] = 0;
-        range[1] = static_cast<int64_t>(off[n_rows]);
-    }
-}
-
 // The placement offsets in two short launches instead of a lookback scan (a 1M-row slice's
 // counts are 4 MB: the scan's cost is its latency, ~25 us as rocprim's decoupled lookback at
 // C3's 64-walk batch). k_place_sums: each 256-thread block sums its PLACE_TILE counts;
@@ -2473,10 +2450,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && rows_buf &&
                    n_rows && hist && status,
                "dw_sgns_owner_out_catch_up: null pointer");
-    DW_REQUIRE((flags & ~(3 | DW_SLOT1)) == 0,
-               "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2 | 8");
+    DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2");
     const bool place = (flags & 1) != 0, p_only = (flags & 2) != 0;
-    const int slot = (flags & DW_SLOT1) ? 1 : 0;
     DW_REQUIRE(!place || counts, "dw_sgns_owner_out_catch_up: placing needs the row counts");
     hipStream_t st = dw::as_stream(stream);
     const dw_step_scalars *dyn = nullptr;
@@ -2502,7 +2477,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     PlaceSpace pl{};
     if (place) {
         rc = owner_workspace(a.batch, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
-                             "dw_sgns_owner_out_catch_up", vocab_size, nullptr, &pl, slot);
+                             "dw_sgns_owner_out_catch_up", vocab_size, nullptr, &pl);
         if (rc != DW_OK) return rc;
     }
     const int64_t ctile = (int64_t)WAVES_PER_BLOCK * CLAIM_TRIPS;
@@ -2521,7 +2496,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
         hipLaunchKernelGGL(k_place_sums, dim3((unsigned)nb), dim3(256), 0, st, counts, local_rows,
                            sums);
         hipLaunchKernelGGL(k_place_scan, dim3((unsigned)nb), dim3(256), 0, st, counts, local_rows,
-                           sums, pl.off, ws.bounds + 2 * slot);
+                           sums, pl.off, ws.bounds);
         DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place");
     }
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1 (p_only:
@@ -2727,7 +2702,7 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
     if (rc != DW_OK) return rc;
     rc = plan_occ(n_centres > 0 ? n_centres : 1, vocab_size, &dummy, &occ, nullptr);
     if (rc != DW_OK) return rc;
-    *bytes = ws.total + 2 * pl.total + occ.total;
+    *bytes = ws.total + pl.total + occ.total;
     return DW_OK;
 }
 
@@ -2817,8 +2792,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     DW_REQUIRE(w_in && w_out_local && g_out_local && m_out && v_out && last_step && hist &&
                    status,
                "dw_sgns_owner_pass2_lazy: null pointer");
-    DW_REQUIRE((flags & ~(7 | DW_SLOT1)) == 0,
-               "dw_sgns_owner_pass2_lazy: flags must be a set of 1 | 2 | 4 | 8");
+    DW_REQUIRE((flags & ~7) == 0, "dw_sgns_owner_pass2_lazy: flags must be a set of 1 | 2 | 4");
     DW_REQUIRE(!(flags & 1) || counts, "dw_sgns_owner_pass2_lazy: placed records need counts");
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
     oa.p_current = (flags & 2) != 0;
@@ -2829,8 +2803,7 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
-                              dw::as_stream(stream), (flags & 1) != 0,
-                              (flags & DW_SLOT1) ? 1 : 0);
+                              dw::as_stream(stream), (flags & 1) != 0);
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

@@ -17,7 +17,6 @@ all their walks from the epoch's start list; one walker launch then generates th
 step k's kernels are captured with block k bound. The kernels and their results are those of
 the eager step (tests/test_gpu_graphed.py).
 """
-import os
 from typing import Optional
 
 import numpy as np
@@ -277,20 +276,7 @@ class GraphedOwnerStep:
             _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count + 1)
             owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
                             noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
-                            status=self.status,
-                            ahead=(lambda k=k: self._ahead(k)) if k + 1 < self.unroll else None)
-
-    def _ahead(self, k: int) -> None:
-        """Inside step k: the out rows of step k + 1 claimed, placed and caught up beside step
-        k's pass 1 and gather (OwnerLazyTables.catch_up_out_ahead; its kernels read block k + 1:
-        the negatives' centre counter and the step number), then block k bound again."""
-        t, B = self.t, self.B
-        if not (t.lazy_out and t.place) or os.environ.get('DW_OUT_AHEAD', '1') == '0':
-            return
-        _native.call('dw_step_scalars_bind_at', self._step_blk(k + 1), t.step_count + 1)
-        t.catch_up_out_ahead(self.walks[(k + 1) * B:(k + 2) * B], self.R, self.K, self.seed, 0,
-                             self.status)
-        _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count)
+                            status=self.status)
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host

@@ -322,8 +322,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      seed: int = 0, noise_offset: int = 0, grad_scale: Optional[float] = None,
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
-                     order_ready: bool = False, placed: bool = False,
-                     slot: int = 0) -> torch.Tensor:
+                     order_ready: bool = False, placed: bool = False) -> torch.Tensor:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
@@ -331,7 +330,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
     ``order_ready``: sgns_owner_prepare already built the centre order for these walks;
     ``placed``: dw_sgns_owner_out_catch_up placed this batch's records (flags & 1): each goes
-    straight into its row's segment; ``slot``: the placement slot it used (its flags & 8)."""
+    straight into its row's segment."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -359,7 +358,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows,
-                     (1 if order_ready else 0) | (2 if placed else 0) | (8 if slot else 0),
+                     (1 if order_ready else 0) | (2 if placed else 0),
                      _native.ptr(w_in),
                      _native.ptr(w_out_local), _native.ptr(g_in), _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),

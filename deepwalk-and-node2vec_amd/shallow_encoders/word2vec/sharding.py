@@ -829,12 +829,9 @@ class OwnerLazyTables(OwnerTables):
                          if self.lazy_out else None)
         self._claim_out = torch.zeros_like(self.last_out) if self.lazy_out else None
         # placed records: every row's slot count of the step (+ one zero past the rows), cleared
-        # by the lazy gather (dw_sgns_owner_out_catch_up / _pass2_lazy); one per placement slot
-        # (step & 1), so the next step's rows can be counted while this step's gather clears
-        self._count_out = ([torch.zeros(self.S + 1, dtype=torch.int32, device=self.device)
-                            for _ in range(2)] if self.lazy_out else None)
-        self._ahead = None    # (step, walks key, done event) of catch_up_out_ahead
-        self._side3 = None
+        # by the lazy gather (dw_sgns_owner_out_catch_up / _pass2_lazy)
+        self._count_out = (torch.zeros(self.S + 1, dtype=torch.int32, device=self.device)
+                           if self.lazy_out else None)
         self._betas0 = tuple(self.betas)
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -844,18 +841,15 @@ class OwnerLazyTables(OwnerTables):
         # any step with weight decay: the p-only catch-up no longer holds
         self._wd_seen = os.environ.get('DW_OUT_P_ONLY', '1') == '0'   # (A/B, round 4)
 
-    def out_flags(self, step: Optional[int] = None) -> int:
-        """dw_sgns_owner_out_catch_up / _pass2_lazy flags of step ``step`` (default: the
-        current one): 1 = place the records (one rank), 2 = the catch-up replays p only (no
-        weight decay so far), 4 = the betas never changed (the gather's m, v replays need no
-        history loads), 8 = placement slot 1 (odd steps)."""
+    def out_flags(self) -> int:
+        """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
+        records (one rank), 2 = the catch-up replays p only (no weight decay so far), 4 = the
+        betas never changed (the gather's m, v replays need no history loads)."""
         if not self.lazy_out:
             return 0
-        step = self.step_count if step is None else int(step)
         p_only = not self._wd_seen
         return ((1 if self.place else 0) | (2 if p_only else 0)
-                | (4 if p_only and self._betas0 is not None else 0)
-                | (8 if self.place and step & 1 else 0))
+                | (4 if p_only and self._betas0 is not None else 0))
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
@@ -880,38 +874,11 @@ class OwnerLazyTables(OwnerTables):
                          self.world, self.S, _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._claim_out), _native.ptr(self._count_out[step & 1]),
+                         _native.ptr(self._claim_out), _native.ptr(self._count_out),
                          _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
-                         self.out_flags(step) & 11, _native.ptr(status), _native.ptr(ws),
-                         ws.numel(),
+                         self.out_flags() & 3, _native.ptr(status), _native.ptr(ws), ws.numel(),
                          _native.stream(self.device))
-
-    def catch_up_out_ahead(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
-                           seed: int, noise_offset: int, status: torch.Tensor) -> bool:
-        """One rank, lazy_out and placed records, during step t (after its own catch-up was
-        enqueued): the out-row claim, placement and catch-up of the NEXT batch ``walks`` (step
-        t + 1, placement slot (t + 1) & 1) on a third stream, beside step t's pass 1 and lazy
-        gather. The claim leaves out the rows step t references (its gather brings them to t),
-        so the replayed rows are disjoint from everything step t reads or writes; the catch-up
-        is ALU-bound (the deferred steps' sqrt and divisions) where the gather is bound by
-        memory. Step t + 1 must then train exactly ``walks`` (before_pass1 checks it). Returns
-        False where it does not apply."""
-        if not (self.lazy_out and self.place and not self.multi) or self._ahead is not None:
-            return False
-        main = torch.cuda.current_stream(self.device)
-        fork = torch.cuda.Event()
-        fork.record(main)
-        if self._side3 is None:
-            self._side3 = torch.cuda.Stream(self.device)
-        with torch.cuda.stream(self._side3):
-            self._side3.wait_event(fork)
-            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status,
-                              step=self.step_count + 1)
-            done = torch.cuda.Event()
-            done.record(self._side3)
-        self._ahead = (self.step_count + 1, (walks.data_ptr(), tuple(walks.shape)), done)
-        return True
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -1053,20 +1020,12 @@ class OwnerLazyTables(OwnerTables):
         stream waits for both."""
         if self.lazy_out and not self.multi:
             # two branches from one fork: the out rows' claim + catch-up (the longer; enqueued
-            # first, so a captured graph launches it first; or already done beside the previous
-            # step, catch_up_out_ahead) and the centre order + in-table catch-up
+            # first, so a captured graph launches it first) and the centre order + in-table
+            # catch-up
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
-            if self._ahead is not None:
-                step, key, done = self._ahead
-                self._ahead = None
-                if (step, key) != (self.step_count, (walks.data_ptr(), tuple(walks.shape))):
-                    raise RuntimeError('OwnerLazyTables: the out rows were caught up ahead for '
-                                       'another batch or step than this one trains')
-                main.wait_event(done)
-            else:
-                self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
+            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
             with torch.cuda.stream(self._side):
                 self._side.wait_event(fork)
                 self.prepare(walks, context_radius, neg_samples)
@@ -1075,8 +1034,6 @@ class OwnerLazyTables(OwnerTables):
                 join.record(self._side)
             main.wait_event(join)
             return
-        if self._ahead is not None:
-            raise RuntimeError('OwnerLazyTables: catch_up_out_ahead is one-rank only')
         self.prepare(walks, context_radius, neg_samples)
         self.catch_up()
         self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1136,7 +1093,7 @@ class OwnerLazyTables(OwnerTables):
         if spec is not None and self.lazy_out:
             spec = {'m': self.m_out, 'v': self.v_out, 'last': self.last_out, 'hist': self._hist,
                     'step': self.step_count, 'flags': self.out_flags(),
-                    'counts': self._count_out[self.step_count & 1]}
+                    'counts': self._count_out}
         return spec
 
     def full_w_out(self) -> torch.Tensor:
@@ -1161,23 +1118,17 @@ class OwnerLazyTables(OwnerTables):
 
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
                     neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
-                    loss_acc: torch.Tensor, status: torch.Tensor,
-                    ahead: Optional[Callable[[], None]] = None) -> int:
+                    loss_acc: torch.Tensor, status: torch.Tensor) -> int:
     """One owner-computes step with the touched-row in-table exchange (every rank passes the
-    same global batch). Returns this rank's record count. ``ahead``: a host callback run once
-    this step's out rows are caught up (word2vec/graphed.py starts the next batch's
-    catch_up_out_ahead there)."""
+    same global batch). Returns this rank's record count."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
-    if ahead is not None:
-        ahead()
-    flags = tables.out_flags()
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
                      grad_scale=grad_scale, loss_acc=loss_acc, status=status, order_ready=True,
-                     placed=bool(flags & 1), slot=1 if flags & 8 else 0)
+                     placed=bool(tables.out_flags() & 1))
     tables.exchange_touched()
     spec = tables.out_adam_spec()
     n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, neg_samples, walks=walks,

@@ -484,8 +484,7 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
  * dw_sgns_owner_pass1's order_ready is a bit set: 1 = this order is ready (else pass 1 builds
  * it); 2 = the records are placed (dw_sgns_owner_out_catch_up ran with flags & 1 on this batch
  * and workspace): pass 1 writes each record straight into its row's segment, and
- * dw_sgns_owner_pass2_lazy (flags & 1) gathers them without a sort; 8 = the placement is in
- * slot 1 of the workspace (see below). */
+ * dw_sgns_owner_pass2_lazy (flags & 1) gathers them without a sort. */
 int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           int64_t local_rows, uint32_t *touched, int64_t *n_touched,
@@ -521,12 +520,7 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
  *       no sort (the order of one row's records is the order the atomics resolved);
  *   2 = replay p only: m, v and last_step stay behind, and dw_sgns_owner_pass2_lazy (flags | 2)
  *       replays m and v (a multiply each per step) before the step — valid while every step has
- *       weight_decay 0;
- *   8 = use placement slot 1 of the workspace (slot 0 otherwise; pass 1 and pass 2 of the batch
- *       name the same slot): the next batch's rows can be claimed, placed and caught up (slot
- *       (step + 1) & 1) while this batch's pass 1 and lazy gather still read slot step & 1. The
- *       claim skips rows claimed the step before, which that step's gather brings current, so
- *       the replayed rows are disjoint from the rows the running gather writes.
+ *       weight_decay 0.
  * 2R(1+K) <= 64, dim <= 512. */
 int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                                int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
@@ -546,8 +540,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
  * flags: 1 = the records were placed (see dw_sgns_owner_out_catch_up; n_records NULL; counts:
  * its row counts, cleared here as the rows step), 2 = the catch-up replayed p only (m, v are
- * replayed here), 4 = every step so far had the same betas (those replays use this step's),
- * 8 = placement slot 1. */
+ * replayed here), 4 = every step so far had the same betas (those replays use this step's). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
                              const float *w_in, float *w_out_local, float *g_out_local,

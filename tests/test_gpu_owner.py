@@ -570,7 +570,7 @@ def test_placed_records_equal_sorted_records(hip_device, d):
     runs = []
     for cfg in (None, sorted_full):
         t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, configure=cfg)
-        assert t.out_flags() == (3 if cfg is None else 0)
+        assert t.out_flags() == (7 if cfg is None else 0)
         runs.append((t.last_out.clone(), t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(),
                      acc.cpu().numpy()))
     (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
