@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256)
 // those updates and replays them here, one step at a time through the same adam_elem, when the
 // row is next read or at a flush: every element goes through the same fp32 operations in the
 // same order as under the dense update, so the tables are bit-for-bit the dense ones.
-//   hist[8 s + k]: step s's scalars (AdamScalars order, one pad), s >= 1
+//   hist[8 s + k]: step s's scalars (AdamScalars order; [7] = RN(1 / bc2s), 0: divide), s >= 1
 //   last[r]:       the step up to which row r's (p, m, v) are current
 using dw::hist_at;
 
@@ -248,7 +248,7 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
                "dw_adam_dense: buffers must be 16-byte aligned");
     DW_REQUIRE(bias_correction2_sqrt > 0.f, "dw_adam_dense: bias_correction2_sqrt must be > 0");
     dw::AdamScalars s{one_minus_beta1, beta2,         one_minus_beta2, bias_correction2_sqrt,
-                      neg_step_size,   eps,           weight_decay};
+                      neg_step_size,   eps,           weight_decay,    1.0f / bias_correction2_sqrt};
     int64_t blocks = ((n_elem >> 2) + 255) / 256;
     if (blocks < 1) blocks = 1;
     if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond

@@ -2646,7 +2646,8 @@ int dw_sgns_walks_phase2_adam(const int32_t *walks, int64_t n_walks, int32_t wal
     a.C = 2 * context_radius;
     OutAdam oa{w_out, m_out, v_out, row_flags,
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
-                               neg_step_size, eps, weight_decay}};
+                               neg_step_size, eps, weight_decay,
+                               bias_correction2_sqrt > 0.f ? 1.0f / bias_correction2_sqrt : 0.f}};
     oa.dyn = dw::bound_step_scalars();
     return launch_sgns<true>(a, workspace, workspace_bytes, 2, dw::as_stream(stream), &oa);
 }
@@ -2771,7 +2772,8 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
                "dw_sgns_owner_pass2: the fused Adam needs w_out_local, m, v, flags, scalars");
     OutAdam oa{w_out_local, m_out, v_out, row_flags,
                dw::AdamScalars{one_minus_beta1, beta2, one_minus_beta2, bias_correction2_sqrt,
-                               neg_step_size, eps, weight_decay}};
+                               neg_step_size, eps, weight_decay,
+                               bias_correction2_sqrt > 0.f ? 1.0f / bias_correction2_sqrt : 0.f}};
     oa.dyn = dw::bound_step_scalars();
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,

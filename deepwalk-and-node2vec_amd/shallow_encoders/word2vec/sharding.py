@@ -52,6 +52,7 @@ import math
 import os
 from typing import Callable, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -67,6 +68,15 @@ def adam_scalars(step: int, lr: float, betas, eps: float, weight_decay: float):
     bias_correction2 = 1 - beta2 ** step
     return (1 - beta1, beta2, 1 - beta2, bias_correction2 ** 0.5, -(lr / bias_correction1), eps,
             weight_decay)
+
+
+def hist_row(step: int, lr: float, betas, eps: float, weight_decay: float) -> np.ndarray:
+    """float32[8]: adam_scalars as the kernels take them, then RN(1 / sqrt(bias_correction2))
+    (the replays divide by the step's uniform sqrt(bias_correction2) through it: dw::div_bc2s)."""
+    h = np.zeros(8, dtype=np.float32)
+    h[:7] = np.asarray(adam_scalars(step, lr, betas, eps, weight_decay), dtype=np.float32)
+    h[7] = np.float32(1.0) / h[3]
+    return h
 
 
 def hip_adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
@@ -939,9 +949,9 @@ class OwnerLazyTables(OwnerTables):
             hh = torch.zeros((cap, 8), dtype=torch.float32, pin_memory=self._cuda)
             hh[:self._hist_host.shape[0]] = self._hist_host
             self._hist, self._hist_host = h, hh
-        rows = [adam_scalars(t, self.lr, self.betas, self.eps, self.weight_decay)
-                for t in range(lo, hi + 1)]
-        self._hist_host[lo:hi + 1, :7] = torch.tensor(rows, dtype=torch.float32)
+        rows = np.stack([hist_row(t, self.lr, self.betas, self.eps, self.weight_decay)
+                         for t in range(lo, hi + 1)])
+        self._hist_host[lo:hi + 1] = torch.from_numpy(rows)
         self._hist[lo:hi + 1].copy_(self._hist_host[lo:hi + 1], non_blocking=True)
         self._hist_ready = hi
         self._hist_key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)

@@ -665,7 +665,8 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         current to; updated;
  *   hist: float32[(step+1) * 8]: row s = Adam step s's scalars in dw_adam_dense's order
  *         (1-beta1, beta2, 1-beta2, sqrt(bias_correction2), -lr/bias_correction1, eps,
- *         weight_decay, unused);
+ *         weight_decay), then fp32 1 / sqrt(bias_correction2) correctly rounded (0 = not given:
+ *         the kernels divide; given, they take three operations for the same quotient);
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
  *         gradient grad_rows[i]. */
@@ -699,7 +700,7 @@ typedef struct dw_step_scalars {
     uint64_t walk_id0;      /* global walk id of the step's first walk */
     uint64_t noise_offset;  /* centre counter of the step's device negatives */
     int64_t step;           /* the Adam step this step applies (1-based) */
-    float adam[8];          /* its scalars, dw_adam_dense order (as a dw_adam_rows hist row) */
+    float adam[8];          /* its scalars, dw_adam_dense order, then RN(1/bias_correction2_sqrt) or 0 (a dw_adam_rows hist row) */
 } dw_step_scalars;
 
 /* Bind (dev != NULL) or unbind (NULL) a device dw_step_scalars for the launches this host

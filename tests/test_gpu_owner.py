@@ -580,3 +580,33 @@ def test_placed_records_equal_sorted_records(hip_device, d):
         assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
                             max_abs=2.05 * lr * steps)
         assert_no_row_drift(got, exp)
+
+
+def test_adam_reciprocal_division_bit_identical(hip_device):
+    """dw::div_bc2s: sqrt(v) / sqrt(bias_correction2) through the host's correctly rounded
+    reciprocal (three operations) gives the IEEE quotient's bits — the same tables as the
+    division (a history without the reciprocal) over 40 replayed steps of rows lagging 0-39
+    steps, v spread over 80 binary orders of magnitude (some waves fall back to the division)."""
+    import numpy as np
+    from shallow_encoders.word2vec.sharding import hip_rows_adam, hist_row
+    g = torch.Generator().manual_seed(2)
+    n, d, steps = 8192, 128, 40
+    p0 = torch.randn((n, d), generator=g)
+    m0 = torch.randn((n, d), generator=g) * 1e-3
+    v0 = torch.rand((n, d), generator=g) * torch.pow(10.0, -40 * torch.rand((n, d), generator=g))
+    v0[::97] = 0.0
+    last0 = torch.randint(0, steps, (n,), generator=g, dtype=torch.int32)
+    hist = np.stack([hist_row(max(s, 1), 0.01, (0.9, 0.999), 1e-8, 0.0)
+                     for s in range(steps + 1)])
+    outs = []
+    for recip in (True, False):
+        h = hist.copy()
+        if not recip:
+            h[:, 7] = 0.0
+        p, m, v, last = (x.clone().to(hip_device) for x in (p0, m0, v0, last0))
+        hip_rows_adam(p, m, v, last, None, None, n, None, torch.from_numpy(h).to(hip_device),
+                      steps)
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), m.cpu(), v.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -381,7 +381,7 @@ def test_cora_ingest_matches_reference(tmp_path, monkeypatch):
 def test_step_scalars_layout_and_history():
     """word2vec/graphed.py's dw_step_scalars block matches include/dw_hip.h's struct (56 bytes,
     walk_id0 @0, noise_offset @8, step @16, adam[8] @24) and its Adam history rows equal the
-    scalars the eager launches pass (adam_scalars rounded to float32)."""
+    scalars the eager launches pass (adam_scalars rounded to float32, then the reciprocal)."""
     import ctypes
     from shallow_encoders.word2vec.graphed import _STEP_DTYPE, adam_history
     from shallow_encoders.word2vec.sharding import adam_scalars
@@ -401,7 +401,8 @@ def test_step_scalars_layout_and_history():
     h = adam_history(5, 0.01, (0.9, 0.999), 1e-8, 0.0)
     for s in range(1, 6):
         exp = [ctypes.c_float(x).value for x in adam_scalars(s, 0.01, (0.9, 0.999), 1e-8, 0.0)]
-        assert h[s, :7].tolist() == exp and h[s, 7] == 0.0
+        # [7]: the correctly rounded fp32 reciprocal of sqrt(bias_correction2) (dw::div_bc2s)
+        assert h[s, :7].tolist() == exp and h[s, 7] == np.float32(1.0) / np.float32(exp[3])
 
 
 # ------------------------------------------------------------------------------ MT19937 stream
