@@ -769,16 +769,15 @@ struct OutAdam {
     uint32_t *counts = nullptr;   // placed records: the rows' counts, cleared as they step
 };
 
-// One row's lazy Adam step (one wave, VPL elements per lane) in two halves: lazy_row_load reads
-// the row's state (p, m, v and the step it is current to) — issued early by k_lazy_gather, a
-// row ahead of its update — and lazy_row_finish replays the missed steps, applies `step` (oa.step,
-// or the bound block's) with g (registers) and records the step.
+// One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
+// `step` (oa.step, or the bound block's) with g (registers), record the step.
 template <int VPL, bool MASKED>
-__device__ __forceinline__ int32_t lazy_row_load(const OutAdam &oa, uint32_t row, int32_t d,
-                                                 int lane, float (&pp)[VPL], float (&mm)[VPL],
-                                                 float (&vv)[VPL]) {
+__device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, uint32_t row,
+                                              int32_t d, int lane, const float (&g)[VPL]) {
     // (row is wave-uniform; lanes past d carry zeros through a uniform replay loop)
+    const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
     const int64_t o = static_cast<int64_t>(row) * d + lane;
+    float pp[VPL], mm[VPL], vv[VPL], gg[VPL];
 #pragma unroll
     for (int m = 0; m < VPL; ++m) {
         const bool live = !MASKED || lane + WAVE * m < d;
@@ -786,16 +785,8 @@ __device__ __forceinline__ int32_t lazy_row_load(const OutAdam &oa, uint32_t row
         pp[m] = live ? oa.p[i] : 0.f;
         mm[m] = live ? oa.m[i] : 0.f;
         vv[m] = live ? oa.v[i] : 0.f;
+        gg[m] = g[m];
     }
-    return __builtin_amdgcn_readfirstlane(oa.last[row]);
-}
-
-template <int VPL, bool MASKED>
-__device__ __forceinline__ void lazy_row_finish(const OutAdam &oa, int32_t step, uint32_t row,
-                                                int32_t from, int32_t d, int lane,
-                                                float (&pp)[VPL], float (&mm)[VPL],
-                                                float (&vv)[VPL], const float (&g)[VPL]) {
-    const int64_t o = static_cast<int64_t>(row) * d + lane;
     if (oa.p_current) {
         // p is at step - 1 already (the p-only catch-up): m and v replay their g = 0 steps — the
         // same two IEEE operations adam_elem_g0 applies to them, one multiply-add each (the
@@ -843,8 +834,7 @@ __device__ __forceinline__ void lazy_row_finish(const OutAdam &oa, int32_t step,
 #pragma unroll
     for (int m = 0; m < VPL; ++m) {
         if (MASKED && lane + WAVE * m >= d) continue;
-        float gg = g[m];
-        dw::adam_elem(pp[m], gg, mm[m], vv[m], h);
+        dw::adam_elem(pp[m], gg[m], mm[m], vv[m], h);
         const int64_t i = o + WAVE * m;
         oa.p[i] = pp[m];
         oa.m[i] = mm[m];
@@ -853,107 +843,6 @@ __device__ __forceinline__ void lazy_row_finish(const OutAdam &oa, int32_t step,
     if (lane == 0) {
         oa.last[row] = step;
         if (oa.counts) oa.counts[row] = 0u;   // placed records: the count back to zero
-    }
-}
-
-template <int VPL, bool MASKED>
-__device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, uint32_t row,
-                                              int32_t d, int lane, const float (&g)[VPL]) {
-    float pp[VPL], mm[VPL], vv[VPL];
-    const int32_t from = lazy_row_load<VPL, MASKED>(oa, row, d, lane, pp, mm, vv);
-    lazy_row_finish<VPL, MASKED>(oa, step, row, from, d, lane, pp, mm, vv, g);
-}
-
-// The lazy gather (one device, small batches: the rows' state moves once each, ~1.3 records per
-// row at C3's 64-walk batch) with a row's state read a row AHEAD: a wave takes a chunk of at most
-// 64 records, reads all their keys and values in one load each, finds the rows' starts by ballot,
-// and while it gathers row j's centre rows it already has row j + 1's p, m, v and last step in
-// flight — the wave's chain per row is one memory round trip instead of two. The same sums in the
-// same record order and the same update as k_rec_gather's lazy flush (lazy_row_finish); rows
-// that straddle chunks add g into g_out (k_lazy_boundary updates them).
-template <int VPL, bool MASKED>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_lazy_gather(const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
-                  int64_t n_rec, const float *__restrict__ w_in, float *__restrict__ g_out,
-                  int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-    const int64_t lo = range ? range[0] : 0;
-    const int64_t hi = range ? range[1] : n_rec;
-    const int64_t n_chunks = (hi - lo + gch - 1) / gch;
-    const int32_t lstep = dw::eff_step(oa.dyn, oa.step_delta, oa.step);
-    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
-    bool live[VPL];
-#pragma unroll
-    for (int m = 0; m < VPL; ++m) live[m] = !MASKED || (lane + WAVE * m < d);
-
-    for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
-        const int64_t e0 = lo + ch * gch;
-        const int64_t e1 = (e0 + gch < hi) ? e0 + gch : hi;
-        const int n = static_cast<int>(e1 - e0);   // <= WAVE
-        const uint32_t before = e0 > lo ? keys[e0 - 1] : 0xFFFFFFFFu;
-        const uint32_t after = e1 < hi ? keys[e1] : 0xFFFFFFFFu;
-        const uint32_t key = lane < n ? keys[e0 + lane] : 0xFFFFFFFFu;
-        const uint64_t val = lane < n ? vals[e0 + lane] : 0ull;
-        const uint32_t vcoef = static_cast<uint32_t>(val >> 32), vcen = static_cast<uint32_t>(val);
-        const uint32_t kprev = __shfl_up(key, 1, WAVE);
-        uint64_t starts = __ballot(lane < n && (lane == 0 || key != kprev));
-        int r0 = __ffsll(static_cast<long long>(starts)) - 1;
-        starts &= starts - 1ull;
-        uint32_t row = __builtin_amdgcn_readlane(key, r0);
-        float pp[VPL], mm[VPL], vv[VPL];
-        int32_t from = 0;
-        bool interior = row != before && row != after;
-        if (interior) from = lazy_row_load<VPL, MASKED>(oa, row, d, lane, pp, mm, vv);
-        while (true) {
-            const int r1 = starts ? __ffsll(static_cast<long long>(starts)) - 1 : n;
-            if (starts) starts &= starts - 1ull;
-            // the next row's state in flight while this row's records are gathered
-            const uint32_t nrow = r1 < n ? __builtin_amdgcn_readlane(key, r1) : 0xFFFFFFFFu;
-            const bool n_interior = r1 < n && nrow != before && nrow != after;
-            float np_[VPL], nm[VPL], nv[VPL];
-            int32_t nfrom = 0;
-            if (n_interior) nfrom = lazy_row_load<VPL, MASKED>(oa, nrow, d, lane, np_, nm, nv);
-            float g[VPL];
-#pragma unroll
-            for (int m = 0; m < VPL; ++m) g[m] = 0.f;
-            for (int e = r0; e < r1; e += GU) {
-                float coef[GU], x[GU][VPL];
-#pragma unroll
-                for (int u = 0; u < GU; ++u) {
-                    const bool in = e + u < r1;
-                    const int src_lane = in ? e + u : r0;
-                    coef[u] = in ? __uint_as_float(__builtin_amdgcn_readlane(vcoef, src_lane)) : 0.f;
-                    const uint32_t c = __builtin_amdgcn_readlane(vcen, src_lane);
-                    const float *src = w_in + static_cast<int64_t>(c) * d + lane;
-#pragma unroll
-                    for (int m = 0; m < VPL; ++m) x[u][m] = (in && live[m]) ? src[WAVE * m] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < GU; ++u)
-#pragma unroll
-                    for (int m = 0; m < VPL; ++m) g[m] += coef[u] * x[u][m];
-            }
-            if (interior) {
-                lazy_row_finish<VPL, MASKED>(oa, lstep, row, from, d, lane, pp, mm, vv, g);
-            } else {   // a row that continues in a neighbouring chunk: its part into g_out
-                float *dst = g_out + static_cast<int64_t>(row) * d + lane;
-#pragma unroll
-                for (int m = 0; m < VPL; ++m)
-                    if (live[m]) atomicAdd(dst + WAVE * m, g[m]);
-            }
-            if (r1 >= n) break;
-            r0 = r1;
-            row = nrow;
-            interior = n_interior;
-            from = nfrom;
-#pragma unroll
-            for (int m = 0; m < VPL; ++m) {
-                pp[m] = np_[m];
-                mm[m] = nm[m];
-                vv[m] = nv[m];
-            }
-        }
     }
 }
 
@@ -1517,19 +1406,6 @@ void launch_gather(dim3 g, dim3 bl, hipStream_t st, const uint32_t *keys, const 
                    int64_t n_rec, const float *w_in, float *g_out, int32_t d,
                    const OutAdam *oa, const int64_t *range, int32_t gch, const dw::Fixed &fo,
                    int32_t *status) {
-    static const bool prefetch = [] {   // (A/B, round 4)
-        const char *e = getenv("DW_LAZY_PREFETCH");
-        return !(e && e[0] == '0');
-    }();
-    if (prefetch && !fo.acc && oa && oa->last && gch <= WAVE) {   // the lazy gather, rows ahead
-        if (d == 64 * VPL)
-            hipLaunchKernelGGL((k_lazy_gather<VPL, false>), g, bl, 0, st, keys, vals, n_rec, w_in,
-                               g_out, d, *oa, range, gch);
-        else
-            hipLaunchKernelGGL((k_lazy_gather<VPL, true>), g, bl, 0, st, keys, vals, n_rec, w_in,
-                               g_out, d, *oa, range, gch);
-        return;
-    }
     if (fo.acc)
         launch_gather_fx<VPL, true>(g, bl, st, keys, vals, n_rec, w_in, g_out, d, oa, range, gch,
                                     fo, status);
