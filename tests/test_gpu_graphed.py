@@ -77,7 +77,9 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
                      last.cpu().numpy()))
     (wi_e, wo_e, acc_e, walks_e), (wi_g, wo_g, acc_g, walks_g) = runs
     np.testing.assert_array_equal(walks_g, walks_e)        # same walk ids and starts
-    np.testing.assert_allclose(acc_g, acc_e, rtol=1e-9)
+    # the loss sums are float64 atomics over tables that already differ by fp32 atomic-order
+    # noise (below): a run measured 1.05e-9 relative on the 12-step positive-loss sum
+    np.testing.assert_allclose(acc_g, acc_e, rtol=1e-8 if scatter == 'atomic' else 1e-9)
     # the atomic scatter sums every out-row gradient in a run-dependent order, so each of the 12
     # Adam steps can amplify an ulp in any near-zero gradient entry (not only at chunk edges as
     # the sorted path): a run measured 1.06e-4 on one entry against lr/100; lr/10 there
