@@ -127,17 +127,11 @@ __global__ void __launch_bounds__(512)
         __syncthreads();   // every wave has read last[r] before thread 0 advances it
         if (from >= (STEP ? step : upto)) continue;   // already current (or stepped)
         const int64_t o = r * d + e;
-        float pp = live ? p[o] : 0.f, mm = live ? m[o] : 0.f, vv = live ? v[o] : 0.f;
+        float pr[1] = {live ? p[o] : 0.f}, mr[1] = {live ? m[o] : 0.f};
+        float vr[1] = {live ? v[o] : 0.f};
         float gg = (STEP && live) ? g_rows[i * d + e] : 0.f;
-        for (int32_t s = from + 1; s <= upto; ++s) {
-            const dw::AdamScalars h = hist_at(hist, s);
-            if (h.wd == 0.f) {
-                dw::adam_elem_g0(pp, mm, vv, h);
-            } else {
-                float z = 0.f;
-                dw::adam_elem(pp, z, mm, vv, h);
-            }
-        }
+        dw::replay_g0(pr, mr, vr, hist, from, upto);
+        float &pp = pr[0], &mm = mr[0], &vv = vr[0];
         if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
         if (live) {
             p[o] = pp;

@@ -167,6 +167,134 @@ __device__ __forceinline__ void adam_elem_g0(float &p, float &m, float &v, const
     p = p + s.nstep * (m / denom);
 }
 
+// Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
+__device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
+    const float *h = hist + 8 * s;
+    return AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+}
+
+// ---- the g = 0 replay inside a box where sqrt and division need no range scaling ----------------
+// sqrtf and the IEEE division compile to range-scaled sequences: sqrtf scales x < 2^-96 by 2^32
+// (and back) and selects x itself for +-0 / inf / NaN; the division runs v_div_scale on both
+// operands, v_div_fmas and v_div_fixup around the reciprocal's Newton / Markstein steps. Inside
+// the box below no operand is scaled (v_div_scale returns it unchanged, v_div_fmas is a plain fma,
+// v_div_fixup passes the quotient through), so the unscaled steps are the same operations on the
+// same values — the same bits — for ~30 VALU slots per element-step instead of ~45 (the lazy
+// replays run at the VALU's issue rate). Checked on MI355X for every x in the box's sqrt range
+// and 2^32 random quotients (scripts/microbench/box_check.hip), and by the lazy-vs-dense tests.
+__device__ __forceinline__ float sqrt_box(float x) {   // x = +0 or x in [2^-96, 2^20]
+#pragma clang fp contract(off)
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+    const float su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = fmaf(-sd, s, x), ru = fmaf(-su, s, x);
+    float t = rd <= 0.f ? sd : s;
+    return ru > 0.f ? su : t;
+}
+
+__device__ __forceinline__ float div_box(float n, float d) {   // |n| in [2^-100, 2^60] or n = +0,
+#pragma clang fp contract(off)                                  // d in [2^-27, 2^21]
+    float r = __builtin_amdgcn_rcpf(d);
+    float e = fmaf(-d, r, 1.0f);
+    r = fmaf(e, r, r);
+    float q = n * r;
+    e = fmaf(-d, q, n);
+    q = fmaf(e, r, q);
+    e = fmaf(-d, q, n);
+    return fmaf(e, r, q);
+}
+
+// A step whose scalars keep every replayed operand in the box (integer tests on the bits: the
+// step is wave-uniform, so they run on the scalar unit): weight_decay +0 (the g = 0 form), the
+// reciprocal present, eps in [2^-27, 1], bc2s in [2^-10, 1], w1 and b2 in [0, 1] — then |m| and v
+// only shrink, sqrt(v) <= 2^10 when v <= 2^20, and the denominator sqrt(v) / bc2s + eps lies in
+// [2^-27, 2^21).
+__device__ __forceinline__ bool in_bits(float x, float lo, float hi) {
+    return __float_as_uint(x) - __float_as_uint(lo) <= __float_as_uint(hi) - __float_as_uint(lo);
+}
+__device__ __forceinline__ bool box_step(const AdamScalars &h) {
+    return __float_as_uint(h.wd) == 0u && __float_as_uint(h.rbc2s) != 0u &&
+           in_bits(h.eps, 0x1p-27f, 1.f) && in_bits(h.bc2s, 0x1p-10f, 1.f) &&
+           in_bits(h.w1, 0.f, 1.f) && in_bits(h.b2, 0.f, 1.f);
+}
+
+__device__ __forceinline__ void adam_elem_g0_box(float &p, float &m, float &v, const AdamScalars &s) {
+#pragma clang fp contract(off)
+    m = fmaf(s.w1, -m, m);
+    v = v * s.b2;
+    const float x = sqrt_box(v);
+    const float q = x * s.rbc2s;
+    const float c = fmaf(-s.bc2s, q, x);
+    const float denom = fmaf(c, s.rbc2s, q) + s.eps;
+    p = p + s.nstep * div_box(m, denom);
+}
+
+// Replays steps from + 1 .. upto with g = 0 on N elements per lane, bit for bit adam_elem_g0 /
+// adam_elem. |m| and v are non-increasing over box steps, so the box holds for every step of a
+// run of them when it holds at both ends: at the start v <= 2^20 and |m| <= 2^60, at the end
+// v >= 2^-96 unless v started +0 (it stays +0) and |m| >= 2^-100 unless m started +0 (likewise).
+// A wave whose run ends outside restarts the run from its saved state on the scaled path; a step
+// outside the box ends the run and the rest replays on the scaled path.
+// The history read as constant memory: the scalar unit loads the step's scalars (uniform) and
+// tests them, where a generic pointer after the kernel's own stores gets vector loads.
+typedef __attribute__((address_space(4))) const float const_float;
+__device__ __forceinline__ AdamScalars hist_at_const(const const_float *h8) {
+    return AdamScalars{h8[0], h8[1], h8[2], h8[3], h8[4], h8[5], h8[6], h8[7]};
+}
+
+template <int N>
+__device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&v)[N],
+                                          const float *__restrict__ hist, int32_t from,
+                                          int32_t upto) {
+    int32_t s = from + 1;
+    bool start = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) start = start && v[k] <= 0x1p20f && fabsf(m[k]) <= 0x1p60f;
+    if (s <= upto && __all(start)) {
+        float p0[N], m0[N], v0[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            p0[k] = p[k];
+            m0[k] = m[k];
+            v0[k] = v[k];
+        }
+        const const_float *hc = (const const_float *)hist;
+        for (; s <= upto; ++s) {
+            const AdamScalars h = hist_at_const(hc + 8 * static_cast<int64_t>(s));
+            if (!box_step(h)) break;
+#pragma unroll
+            for (int k = 0; k < N; ++k) adam_elem_g0_box(p[k], m[k], v[k], h);
+        }
+        bool end = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            end = end && (__float_as_uint(v0[k]) == 0u || v[k] >= 0x1p-96f) &&
+                  (__float_as_uint(m0[k]) == 0u || fabsf(m[k]) >= 0x1p-100f);
+        if (!__all(end)) {
+            s = from + 1;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                p[k] = p0[k];
+                m[k] = m0[k];
+                v[k] = v0[k];
+            }
+        }
+    }
+    for (; s <= upto; ++s) {
+        const AdamScalars h = hist_at(hist, s);
+        if (h.wd == 0.f) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) adam_elem_g0(p[k], m[k], v[k], h);
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                float z = 0.f;
+                adam_elem(p[k], z, m[k], v[k], h);
+            }
+        }
+    }
+}
+
 // The Adam scalars a kernel uses: the bound step block's when there is one (graph replay),
 // else the launch's by-value ones.
 __device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
@@ -208,12 +336,6 @@ __device__ __forceinline__ float from_fixed(int64_t a, double fi) {
 
 __device__ __forceinline__ void fixed_add(int64_t *dst, int64_t v) {
     if (v) atomicAdd(reinterpret_cast<unsigned long long *>(dst), static_cast<unsigned long long>(v));
-}
-
-// Row s of a per-step Adam scalar history ([steps][8] fp32; the lazy exact Adam's replays).
-__device__ __forceinline__ AdamScalars hist_at(const float *__restrict__ hist, int64_t s) {
-    const float *h = hist + 8 * s;
-    return AdamScalars{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
 }
 
 }  // namespace dw

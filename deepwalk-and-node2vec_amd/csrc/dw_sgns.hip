@@ -816,19 +816,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
             }
         }
     } else {
-        for (int32_t t = from + 1; t < step; ++t) {
-            const dw::AdamScalars h = dw::hist_at(oa.hist, t);
-            if (h.wd == 0.f) {
-#pragma unroll
-                for (int m = 0; m < VPL; ++m) dw::adam_elem_g0(pp[m], mm[m], vv[m], h);
-            } else {
-#pragma unroll
-                for (int m = 0; m < VPL; ++m) {
-                    float z = 0.f;
-                    dw::adam_elem(pp[m], z, mm[m], vv[m], h);
-                }
-            }
-        }
+        dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1);
     }
     const dw::AdamScalars h = dw::hist_at(oa.hist, step);
 #pragma unroll

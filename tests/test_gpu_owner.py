@@ -582,21 +582,37 @@ def test_placed_records_equal_sorted_records(hip_device, d):
         assert_no_row_drift(got, exp)
 
 
-def test_adam_reciprocal_division_bit_identical(hip_device):
-    """dw::div_bc2s: sqrt(v) / sqrt(bias_correction2) through the host's correctly rounded
-    reciprocal (three operations) gives the IEEE quotient's bits — the same tables as the
-    division (a history without the reciprocal) over 40 replayed steps of rows lagging 0-39
-    steps, v spread over 80 binary orders of magnitude (some waves fall back to the division)."""
+@pytest.mark.parametrize('wd_tail', [False, True])
+def test_adam_reciprocal_division_bit_identical(hip_device, wd_tail):
+    """The replays' fast forms give the scaled IEEE sequences' bits: dw::div_bc2s (sqrt(v) /
+    sqrt(bias_correction2) through the host's correctly rounded reciprocal) and the box replay
+    (dw::replay_g0: sqrt and the division without range scaling while every operand stays in the
+    box) against a history without the reciprocal (every step on the scaled path), over 40
+    replayed steps of rows lagging 0-39 steps. Rows: v spread over 80 binary orders of magnitude
+    per element (waves falling back at the start or at the end of a run), row-scaled v and m
+    (m down to ~1e-33: runs ending under the box's 2^-100 restart on the scaled path), fresh
+    rows (m = v = +0), -0 entries in m, v past 2^20. wd_tail: weight decay from step 30 on (a
+    step outside the box ends the run mid-way)."""
     import numpy as np
     from shallow_encoders.word2vec.sharding import hip_rows_adam, hist_row
     g = torch.Generator().manual_seed(2)
     n, d, steps = 8192, 128, 40
+    h2 = n // 2
     p0 = torch.randn((n, d), generator=g)
     m0 = torch.randn((n, d), generator=g) * 1e-3
     v0 = torch.rand((n, d), generator=g) * torch.pow(10.0, -40 * torch.rand((n, d), generator=g))
     v0[::97] = 0.0
+    row_v = torch.pow(10.0, -20 * torch.rand((n - h2, 1), generator=g))
+    row_m = torch.pow(10.0, -30 * torch.rand((n - h2, 1), generator=g))
+    v0[h2:] = torch.rand((n - h2, d), generator=g) * row_v
+    m0[h2:] *= row_m
+    m0[h2::7] = 0.0                               # fresh rows
+    v0[h2::7] = 0.0
+    m0[h2 + 1::11, ::5] = -0.0
+    v0[h2 + 2::13, 3] = 4e6                       # v past 2^20
     last0 = torch.randint(0, steps, (n,), generator=g, dtype=torch.int32)
-    hist = np.stack([hist_row(max(s, 1), 0.01, (0.9, 0.999), 1e-8, 0.0)
+    hist = np.stack([hist_row(max(s, 1), 0.01, (0.9, 0.999), 1e-8,
+                              0.01 if wd_tail and s >= 30 else 0.0)
                      for s in range(steps + 1)])
     outs = []
     for recip in (True, False):
@@ -609,4 +625,4 @@ def test_adam_reciprocal_division_bit_identical(hip_device):
         torch.cuda.synchronize()
         outs.append((p.cpu(), m.cpu(), v.cpu()))
     for a, b in zip(*outs):
-        assert torch.equal(a, b)
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))   # bits (signed zeros)
