@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(256)
 // those updates and replays them here, one step at a time through the same adam_elem, when the
 // row is next read or at a flush: every element goes through the same fp32 operations in the
 // same order as under the dense update, so the tables are bit-for-bit the dense ones.
-//   hist[8 s + k]: step s's scalars (AdamScalars order; [7] = RN(1 / bc2s), 0: divide), s >= 1
+//   hist[8 s + k]: step s's scalars (AdamScalars order; [7] = RN(1 / bc2s), 0: divide), s >= 1;
+//                  row 0: the box header (dw::hist_box_from)
 //   last[r]:       the step up to which row r's (p, m, v) are current
 using dw::hist_at;
 
@@ -120,6 +121,7 @@ __global__ void __launch_bounds__(512)
         n = c < n_max ? c : n_max;
     }
     const int32_t upto = STEP ? step - 1 : step;
+    const int32_t box_from = dw::hist_box_from(hist);
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t r = rows ? static_cast<int64_t>(rows[i]) : i;
         // an out-of-range centre is reported by the SGNS pass
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(512)
         float pr[1] = {live ? p[o] : 0.f}, mr[1] = {live ? m[o] : 0.f};
         float vr[1] = {live ? v[o] : 0.f};
         float gg = (STEP && live) ? g_rows[i * d + e] : 0.f;
-        dw::replay_g0(pr, mr, vr, hist, from, upto);
+        dw::replay_g0(pr, mr, vr, hist, from, upto, box_from);
         float &pp = pr[0], &mm = mr[0], &vv = vr[0];
         if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
         if (live) {

@@ -204,18 +204,17 @@ __device__ __forceinline__ float div_box(float n, float d) {   // |n| in [2^-100
     return fmaf(e, r, q);
 }
 
-// A step whose scalars keep every replayed operand in the box (integer tests on the bits: the
-// step is wave-uniform, so they run on the scalar unit): weight_decay +0 (the g = 0 form), the
-// reciprocal present, eps in [2^-27, 1], bc2s in [2^-10, 1], w1 and b2 in [0, 1] — then |m| and v
-// only shrink, sqrt(v) <= 2^10 when v <= 2^20, and the denominator sqrt(v) / bc2s + eps lies in
-// [2^-27, 2^21).
-__device__ __forceinline__ bool in_bits(float x, float lo, float hi) {
-    return __float_as_uint(x) - __float_as_uint(lo) <= __float_as_uint(hi) - __float_as_uint(lo);
-}
-__device__ __forceinline__ bool box_step(const AdamScalars &h) {
-    return __float_as_uint(h.wd) == 0u && __float_as_uint(h.rbc2s) != 0u &&
-           in_bits(h.eps, 0x1p-27f, 1.f) && in_bits(h.bc2s, 0x1p-10f, 1.f) &&
-           in_bits(h.w1, 0.f, 1.f) && in_bits(h.b2, 0.f, 1.f);
+// A step whose scalars keep every replayed operand in the box: weight_decay +0 (the g = 0
+// form), the reciprocal present, eps in [2^-27, 1], bc2s in [2^-10, 1], w1 and b2 in [0, 1] —
+// then |m| and v only shrink, sqrt(v) <= 2^10 when v <= 2^20, and the denominator
+// sqrt(v) / bc2s + eps lies in [2^-27, 2^21). The host tests its rows when it writes them and
+// keeps the answer in the history's row 0, which no step uses (include/dw_hip.h,
+// DW_HIST_BOX_TAG): [0] the tag's bits, [1] the bits of the int32 step from which every written
+// row is in the box. Anything else there: no step is taken to be in the box.
+__device__ __forceinline__ int32_t hist_box_from(const float *__restrict__ hist) {
+    typedef __attribute__((address_space(4))) const uint32_t const_u32;
+    const const_u32 *h0 = (const const_u32 *)hist;
+    return h0[0] == DW_HIST_BOX_TAG ? static_cast<int32_t>(h0[1]) : INT32_MAX;
 }
 
 __device__ __forceinline__ void adam_elem_g0_box(float &p, float &m, float &v, const AdamScalars &s) {
@@ -229,12 +228,6 @@ __device__ __forceinline__ void adam_elem_g0_box(float &p, float &m, float &v, c
     p = p + s.nstep * div_box(m, denom);
 }
 
-// Replays steps from + 1 .. upto with g = 0 on N elements per lane, bit for bit adam_elem_g0 /
-// adam_elem. |m| and v are non-increasing over box steps, so the box holds for every step of a
-// run of them when it holds at both ends: at the start v <= 2^20 and |m| <= 2^60, at the end
-// v >= 2^-96 unless v started +0 (it stays +0) and |m| >= 2^-100 unless m started +0 (likewise).
-// A wave whose run ends outside restarts the run from its saved state on the scaled path; a step
-// outside the box ends the run and the rest replays on the scaled path.
 // The history read as constant memory: the scalar unit loads the step's scalars (uniform) and
 // tests them, where a generic pointer after the kernel's own stores gets vector loads.
 typedef __attribute__((address_space(4))) const float const_float;
@@ -242,15 +235,23 @@ __device__ __forceinline__ AdamScalars hist_at_const(const const_float *h8) {
     return AdamScalars{h8[0], h8[1], h8[2], h8[3], h8[4], h8[5], h8[6], h8[7]};
 }
 
+// Replays steps from + 1 .. upto with g = 0 on N elements per lane, bit for bit adam_elem_g0 /
+// adam_elem. Steps from box_from on (hist_box_from: read once per launch) are in the box; |m|
+// and v are non-increasing over them, so the box holds for every step of a run when it holds at
+// both ends: at the start v <= 2^20 and |m| <= 2^60, at the end v >= 2^-96 unless v started +0
+// (it stays +0) and |m| >= 2^-100 unless m started +0 (likewise). A row with an earlier step
+// replays on the scaled path, as does a wave whose run ends outside the box (from its saved
+// state). The run tests nothing per step: a test per step, on the scalar unit or not, made the
+// replays slower than the scaled path they replace (scripts/microbench/replay_bench.hip).
 template <int N>
 __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&v)[N],
                                           const float *__restrict__ hist, int32_t from,
-                                          int32_t upto) {
-    int32_t s = from + 1;
-    bool start = true;
+                                          int32_t upto, int32_t box_from) {
+    if (from >= upto) return;
+    bool start = from + 1 >= box_from;
 #pragma unroll
     for (int k = 0; k < N; ++k) start = start && v[k] <= 0x1p20f && fabsf(m[k]) <= 0x1p60f;
-    if (s <= upto && __all(start)) {
+    if (__all(start)) {
         float p0[N], m0[N], v0[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) {
@@ -259,9 +260,8 @@ __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&
             v0[k] = v[k];
         }
         const const_float *hc = (const const_float *)hist;
-        for (; s <= upto; ++s) {
+        for (int32_t s = from + 1; s <= upto; ++s) {
             const AdamScalars h = hist_at_const(hc + 8 * static_cast<int64_t>(s));
-            if (!box_step(h)) break;
 #pragma unroll
             for (int k = 0; k < N; ++k) adam_elem_g0_box(p[k], m[k], v[k], h);
         }
@@ -270,17 +270,15 @@ __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&
         for (int k = 0; k < N; ++k)
             end = end && (__float_as_uint(v0[k]) == 0u || v[k] >= 0x1p-96f) &&
                   (__float_as_uint(m0[k]) == 0u || fabsf(m[k]) >= 0x1p-100f);
-        if (!__all(end)) {
-            s = from + 1;
+        if (__all(end)) return;
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
-                p[k] = p0[k];
-                m[k] = m0[k];
-                v[k] = v0[k];
-            }
+        for (int k = 0; k < N; ++k) {
+            p[k] = p0[k];
+            m[k] = m0[k];
+            v[k] = v0[k];
         }
     }
-    for (; s <= upto; ++s) {
+    for (int32_t s = from + 1; s <= upto; ++s) {
         const AdamScalars h = hist_at(hist, s);
         if (h.wd == 0.f) {
 #pragma unroll

@@ -816,7 +816,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
             }
         }
     } else {
-        dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1);
+        dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1, dw::hist_box_from(oa.hist));
     }
     const dw::AdamScalars h = dw::hist_at(oa.hist, step);
 #pragma unroll

@@ -24,7 +24,7 @@ import torch
 
 from shallow_encoders import _native
 from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables, adam_scalars,
-                                                hist_row,
+                                                hist_header, hist_row,
                                                 owner_lazy_step, replicated_step)
 
 _STEP_DTYPE = np.dtype([('walk_id0', '<u8'), ('noise_offset', '<u8'), ('step', '<i8'),
@@ -32,10 +32,12 @@ _STEP_DTYPE = np.dtype([('walk_id0', '<u8'), ('noise_offset', '<u8'), ('step', '
 
 
 def adam_history(n_steps: int, lr: float, betas, eps: float, weight_decay: float) -> np.ndarray:
-    """float32 [n_steps + 1, 8]: row s = Adam step s's scalars (dw_adam_dense order)."""
+    """float32 [n_steps + 1, 8]: row s = Adam step s's scalars (dw_adam_dense order); row 0 the
+    box header (sharding.hist_header)."""
     h = np.zeros((n_steps + 1, 8), dtype=np.float32)
     for s in range(1, n_steps + 1):
         h[s] = hist_row(s, lr, betas, eps, weight_decay)
+    h[0] = hist_header(h, n_steps)
     return h
 
 

@@ -79,6 +79,42 @@ def hist_row(step: int, lr: float, betas, eps: float, weight_decay: float) -> np
     return h
 
 
+HIST_BOX_TAG = 0x58424457   # include/dw_hip.h DW_HIST_BOX_TAG
+
+
+def _bits_in(x: np.ndarray, lo: float, hi: float) -> np.ndarray:
+    """dw::in_bits: lo <= x <= hi on the float32 bits (x, lo, hi >= +0; a sign bit fails)."""
+    b = x.astype(np.float32).view(np.uint32)
+    lo_b = np.array(lo, dtype=np.float32).view(np.uint32)
+    hi_b = np.array(hi, dtype=np.float32).view(np.uint32)
+    return (b - lo_b) <= (hi_b - lo_b)   # uint32 wrap-around, as on the device
+
+
+def hist_rows_in_box(rows: np.ndarray) -> np.ndarray:
+    """bool per float32[8] history row: its scalars keep the lazy g = 0 replays in the box where
+    sqrt and the division run without range scaling (dw_common.h, dw::replay_g0): weight_decay
+    +0, the reciprocal present, eps in [2^-27, 1], sqrt(bias_correction2) in [2^-10, 1],
+    1-beta1 and beta2 in [0, 1]."""
+    r = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, 8)
+    u = r.view(np.uint32)
+    with np.errstate(over='ignore'):
+        return ((u[:, 6] == 0) & (u[:, 7] != 0) & _bits_in(r[:, 5], 2.0 ** -27, 1.0)
+                & _bits_in(r[:, 3], 2.0 ** -10, 1.0) & _bits_in(r[:, 0], 0.0, 1.0)
+                & _bits_in(r[:, 1], 0.0, 1.0))
+
+
+def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
+    """float32[8] row 0 of a lazy Adam history whose rows 1..last are written: the box tag and
+    the first step b such that rows b..last are all in the box (include/dw_hip.h)."""
+    ok = hist_rows_in_box(hist[1:last + 1])
+    bad = np.flatnonzero(~ok)
+    b = int(bad[-1]) + 2 if bad.size else 1
+    h0 = np.zeros(8, dtype=np.float32)
+    h0.view(np.uint32)[0] = HIST_BOX_TAG
+    h0.view(np.int32)[1] = b
+    return h0
+
+
 def hip_adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
              lr: float, betas, eps: float, weight_decay: float, zero_grad: bool) -> None:
     """One dense Adam step on flat fp32 buffers with torch.optim.Adam's scalar math."""
@@ -952,6 +988,9 @@ class OwnerLazyTables(OwnerTables):
         rows = np.stack([hist_row(t, self.lr, self.betas, self.eps, self.weight_decay)
                          for t in range(lo, hi + 1)])
         self._hist_host[lo:hi + 1] = torch.from_numpy(rows)
+        # row 0: the box header over rows 1..hi (the rows past hi are rewritten before use)
+        self._hist_host[0] = torch.from_numpy(hist_header(self._hist_host[:hi + 1].numpy(), hi))
+        self._hist[0].copy_(self._hist_host[0], non_blocking=True)
         self._hist[lo:hi + 1].copy_(self._hist_host[lo:hi + 1], non_blocking=True)
         self._hist_ready = hi
         self._hist_key = (self.lr, tuple(self.betas), self.eps, self.weight_decay)

@@ -288,6 +288,9 @@ int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const in
  * refused. frac: dw_exact_frac_bits(the launches' grad scale). Host-side registry, keyed by
  * the grad pointer (graph-captured launches keep the accumulator they were captured with). */
 #define DW_EXACT_DEFER 1
+
+/* Row 0 of a lazy Adam history (dw_adam_rows): the box header's tag ("WDBX"). */
+#define DW_HIST_BOX_TAG 0x58424457u
 int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t frac,
                       int32_t flags);
 int dw_exact_unregister(const float *grad);
@@ -667,6 +670,12 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         (1-beta1, beta2, 1-beta2, sqrt(bias_correction2), -lr/bias_correction1, eps,
  *         weight_decay), then fp32 1 / sqrt(bias_correction2) correctly rounded (0 = not given:
  *         the kernels divide; given, they take three operations for the same quotient);
+ *         row 0 (no step) may hold the box header: [0] = the bits of DW_HIST_BOX_TAG, [1] = the
+ *         bits of an int32 step b such that every row s >= b up to the last one a launch reads
+ *         has weight_decay +0, the reciprocal, eps in [2^-27, 1], sqrt(bias_correction2) in
+ *         [2^-10, 1] and 1-beta1, beta2 in [0, 1]: the g = 0 replays of rows last current at
+ *         b - 1 or later then run sqrt and the division without range scaling (the same bits,
+ *         fewer operations); any other row 0 = no step in the box;
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
  *         gradient grad_rows[i]. */

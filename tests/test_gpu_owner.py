@@ -582,19 +582,20 @@ def test_placed_records_equal_sorted_records(hip_device, d):
         assert_no_row_drift(got, exp)
 
 
-@pytest.mark.parametrize('wd_tail', [False, True])
-def test_adam_reciprocal_division_bit_identical(hip_device, wd_tail):
+@pytest.mark.parametrize('wd_head', [False, True])
+def test_adam_reciprocal_division_bit_identical(hip_device, wd_head):
     """The replays' fast forms give the scaled IEEE sequences' bits: dw::div_bc2s (sqrt(v) /
     sqrt(bias_correction2) through the host's correctly rounded reciprocal) and the box replay
     (dw::replay_g0: sqrt and the division without range scaling while every operand stays in the
-    box) against a history without the reciprocal (every step on the scaled path), over 40
-    replayed steps of rows lagging 0-39 steps. Rows: v spread over 80 binary orders of magnitude
+    box, from the step the history's row 0 names: sharding.hist_header) against a history
+    without the reciprocal (every step on the scaled path), over 40 replayed steps of rows
+    lagging 0-39 steps. Rows: v spread over 80 binary orders of magnitude
     per element (waves falling back at the start or at the end of a run), row-scaled v and m
     (m down to ~1e-33: runs ending under the box's 2^-100 restart on the scaled path), fresh
-    rows (m = v = +0), -0 entries in m, v past 2^20. wd_tail: weight decay from step 30 on (a
-    step outside the box ends the run mid-way)."""
+    rows (m = v = +0), -0 entries in m, v past 2^20. wd_head: weight decay in steps 1-10 (the
+    header's box starts at step 11: rows last current before step 10 take the scaled path)."""
     import numpy as np
-    from shallow_encoders.word2vec.sharding import hip_rows_adam, hist_row
+    from shallow_encoders.word2vec.sharding import hip_rows_adam, hist_header, hist_row
     g = torch.Generator().manual_seed(2)
     n, d, steps = 8192, 128, 40
     h2 = n // 2
@@ -612,13 +613,15 @@ def test_adam_reciprocal_division_bit_identical(hip_device, wd_tail):
     v0[h2 + 2::13, 3] = 4e6                       # v past 2^20
     last0 = torch.randint(0, steps, (n,), generator=g, dtype=torch.int32)
     hist = np.stack([hist_row(max(s, 1), 0.01, (0.9, 0.999), 1e-8,
-                              0.01 if wd_tail and s >= 30 else 0.0)
+                              0.01 if wd_head and s <= 10 else 0.0)
                      for s in range(steps + 1)])
     outs = []
     for recip in (True, False):
         h = hist.copy()
         if not recip:
             h[:, 7] = 0.0
+        h[0] = hist_header(h, steps)
+        assert h[0].view(np.int32)[1] == (steps + 1 if not recip else 11 if wd_head else 1)
         p, m, v, last = (x.clone().to(hip_device) for x in (p0, m0, v0, last0))
         hip_rows_adam(p, m, v, last, None, None, n, None, torch.from_numpy(h).to(hip_device),
                       steps)

@@ -525,3 +525,36 @@ def test_library_built_from_these_sources():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     assert _native.load().dw_build_id().decode() == b.source_id()
+
+
+def test_hist_box_header():
+    """Row 0 of a lazy Adam history (include/dw_hip.h DW_HIST_BOX_TAG): the tag and the first
+    step from which every written row keeps the g = 0 replays in the box (dw::replay_g0's
+    unscaled sqrt / division). The tests are dw::in_bits' on the float32 bits."""
+    from shallow_encoders.word2vec.sharding import (HIST_BOX_TAG, hist_header, hist_row,
+                                                    hist_rows_in_box)
+    def hist(n, wd_at=(), eps=1e-8, betas=(0.9, 0.999)):
+        h = np.zeros((n + 1, 8), dtype=np.float32)
+        for s in range(1, n + 1):
+            h[s] = hist_row(s, 0.01, betas, eps, 0.01 if s in wd_at else 0.0)
+        return h
+    h = hist(20)
+    h0 = hist_header(h, 20)
+    assert h0.view(np.uint32)[0] == HIST_BOX_TAG == 0x58424457 and h0.view(np.int32)[1] == 1
+    assert hist_header(hist(20, wd_at=(3, 7)), 20).view(np.int32)[1] == 8
+    assert hist_header(hist(20, wd_at=(20,)), 20).view(np.int32)[1] == 21
+    assert hist_header(hist(20, eps=1e-9), 20).view(np.int32)[1] == 21     # eps < 2^-27
+    assert hist_rows_in_box(hist(3, eps=2.0 ** -27)[1:]).all()
+    assert not hist_rows_in_box(hist(3, eps=1.5)[1:]).any()
+    # sqrt(bias_correction2) < 2^-10 (beta2 = 1 - 1e-7 at step 1): out; later steps in
+    hb = hist(40, betas=(0.9, 1 - 1e-7))
+    assert not hist_rows_in_box(hb[1:2]).any()
+    r = hb.copy()
+    r[:, 6] = -0.0                                                            # -0 is not +0
+    assert not hist_rows_in_box(r[1:]).any()
+    r = h.copy()
+    r[:, 7] = 0.0                                                             # no reciprocal
+    assert not hist_rows_in_box(r[1:]).any()
+    r = h.copy()
+    r[:, 0] = -0.1                                                            # a sign bit fails
+    assert not hist_rows_in_box(r[1:]).any()
