@@ -409,9 +409,14 @@ __device__ __forceinline__ float row_sum16(float x) {
 // EXACT: the centre-gradient terms enter g_in's int64 accumulator as fixed-point integers
 // (dw::to_fixed), each lane adding its 4 F4 elements of its group's centre straight from
 // registers (no LDS staging, no run summing: integer sums need no order).
-template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false>
+// COEFIN (the rows-major step, after k_out_rows; one owner or many, placed records): the
+// coefficients are already in the placed records (rec_val[place_off[row] + place_rank[slot]]'s
+// high word) and each row's pre-step values p^{s-1} in w_out[place_off[row]] (k_out_rows'
+// copy): only the centre gradient is formed — the same FMAs in the same order as the full pass.
+template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false, bool COEFIN = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
+    static_assert(!COEFIN || (OWNER && !EXACT), "the coefficients-in form is the owner path's");
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
@@ -564,8 +569,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int u = 0; u < CHR; ++u) {
                 const int t = t0 + u;
                 rid[u] = (t < n_own) ? s_id[wv][q][t] : -1;
-                const float *row = a.w_out + static_cast<int64_t>(rid[u] < 0 ? 0 : rid[u]) * D +
-                                   4 * gl;
+                const int64_t at = rid[u] < 0 ? 0
+                                   : COEFIN ? static_cast<int64_t>(a.place_off[rid[u]])
+                                            : static_cast<int64_t>(rid[u]);
+                const float *row = a.w_out + at * D + 4 * gl;
 #pragma unroll
                 for (int f = 0; f < F4; ++f)
                     o4[u][f] = rid[u] >= 0 ? *reinterpret_cast<const float4 *>(row + 64 * f)
@@ -575,17 +582,19 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         auto compute_chunk = [&](const float4(&o4)[CHR][F4], const int32_t(&rid)[CHR],
                                  int t0) {
             float dot[CHR];
+            if constexpr (!COEFIN) {
 #pragma unroll
-            for (int u = 0; u < CHR; ++u) {
-                float p = 0.f;
+                for (int u = 0; u < CHR; ++u) {
+                    float p = 0.f;
 #pragma unroll
-                for (int f = 0; f < F4; ++f) {
-                    p = fmaf(c4[f].x, o4[u][f].x, p);
-                    p = fmaf(c4[f].y, o4[u][f].y, p);
-                    p = fmaf(c4[f].z, o4[u][f].z, p);
-                    p = fmaf(c4[f].w, o4[u][f].w, p);
+                    for (int f = 0; f < F4; ++f) {
+                        p = fmaf(c4[f].x, o4[u][f].x, p);
+                        p = fmaf(c4[f].y, o4[u][f].y, p);
+                        p = fmaf(c4[f].z, o4[u][f].z, p);
+                        p = fmaf(c4[f].w, o4[u][f].w, p);
+                    }
+                    dot[u] = row_sum16(p);
                 }
-                dot[u] = row_sum16(p);
             }
             // lane gl < CHR owns row t0 + gl of its group
             float x = 0.f;
@@ -593,16 +602,21 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 #pragma unroll
             for (int u = 0; u < CHR; ++u)
                 if (gl == u) {
-                    x = dot[u];
+                    if constexpr (!COEFIN) x = dot[u];
                     xid = rid[u];
                 }
             float coef = 0.f;
             const int t = t0 + gl;
             if (gl < CHR && t < n_own && xid >= 0) {
                 const int slot = OWNER ? static_cast<int>(s_t[wv][q][t]) : t;
-                coef = row_coef(x, (slot % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg, acc_rec,
-                                acc_prec);
-                s_coef[wv][q][t] = coef;
+                if constexpr (COEFIN) {
+                    const uint32_t pos = a.place_off[xid] + a.place_rank[b * T + slot];
+                    coef = __uint_as_float(static_cast<uint32_t>(a.rec_val[pos] >> 32));
+                } else {
+                    coef = row_coef(x, (slot % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg,
+                                    acc_rec, acc_prec);
+                    s_coef[wv][q][t] = coef;
+                }
             }
 #pragma unroll
             for (int u = 0; u < CHR; ++u) {
@@ -640,7 +654,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int f = 0; f < F4; ++f) s_g[wv][q][gl + 16 * f] = g4[f];
         }
         dw::wave_lds_sync();
-        if constexpr (OWNER) {  // the wave's owned records, appended to its region
+        if constexpr (COEFIN) {
+            // (no records: k_out_rows wrote them)
+        } else if constexpr (OWNER) {  // the wave's owned records, appended to its region
             const int c0 = __builtin_amdgcn_readlane(n_own, 0);
             const int c1 = __builtin_amdgcn_readlane(n_own, 16);
             const int c2 = __builtin_amdgcn_readlane(n_own, 32);
@@ -734,8 +750,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 #pragma unroll
             for (int f = 0; f < F4; ++f) atomicAdd(dst + 64 * f, pend[f]);
         }
-        if (lane == 0) a.rec_counts[gw] = static_cast<uint32_t>(filled);
-        if (a.count_out && blockIdx.x == 0 && threadIdx.x == 0)
+        if (!COEFIN && lane == 0) a.rec_counts[gw] = static_cast<uint32_t>(filled);
+        if (!COEFIN && a.count_out && blockIdx.x == 0 && threadIdx.x == 0)
             *a.count_out = static_cast<uint32_t>(a.batch * T);
     }
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
@@ -1227,7 +1243,7 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
 
 // 16-lane-group pass 1 when d is a multiple of 64 (<= 512) and 2R(1+K) <= 64; otherwise
 // DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns). DW_SGNS_G16=0 disables it.
-template <bool FROM_WALKS, bool OWNER = false>
+template <bool FROM_WALKS, bool OWNER = false, bool COEFIN = false>
 int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     static const bool enabled = [] {
         const char *e = getenv("DW_SGNS_G16");
@@ -1239,6 +1255,19 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    if constexpr (COEFIN) {
+        DW_REQUIRE(!a.fx_in.acc, "dw_sgns_owner_pass1: the rows-major step has no deterministic "
+                   "form");
+        switch (a.d / 64) {
+            case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, true, false, true>), g, bl, 0, st, a); break;
+            case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
+            case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
+            case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, false, true>), g, bl, 0, st, a); break;
+            default: return DW_E_UNSUPPORTED;
+        }
+        DW_LAUNCH_CHECK("dw_sgns/g16_coefin");
+        return DW_OK;
+    }
     if (a.fx_in.acc) {   // deterministic mode
         switch (a.d / 64) {
             case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, OWNER, true>), g, bl, 0, st, a); break;
@@ -1364,6 +1393,207 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
         hipLaunchKernelGGL((k_lazy_boundary<VPL, true>), dim3((unsigned)blocks),
                            dim3(WAVES_PER_BLOCK * WAVE), 0, st, keys, n_rec, gch, g_out, d, oa,
                            range);
+}
+
+// ---- the rows-major lazy out step (dw_sgns_owner_out_rows) -----------------------------------
+// The 64-walk batch's out rows are ~224K distinct rows of 1M, each read and written as p, m, v
+// (3 x 512 B): the catch-up -> pass 1 -> lazy gather sequence moved each across HBM twice and
+// read p a third time. Here one kernel does a row's whole out-side step where its p / m / v sit
+// in registers: replay its deferred g = 0 steps (to p^{s-1}), the logit of each of its records
+// against the record's centre row (pass 1's 16-lane layout and FMA order: the same bits), the
+// coefficient (row_coef, the loss sums), the gradient sum over its records in placed order (the
+// gather's order) and the Adam step. It leaves each record's coefficient in the high word of its
+// placed value and the row's p^{s-1} in p_prev[off[row]] for the centre pass
+// (dw_sgns_owner_pass1 with order_ready & 4, k_sgns_g16's COEFIN form).
+// A wave takes gch <= 64 placed records (lane = record) and its rows four at a time, one per
+// 16-lane group (lane gl holds elements [4gl + 64f, +4) of p, m, v: float4 loads), so four rows'
+// loads are in flight together. A row that straddles the chunk (its first or last row
+// continues in the neighbouring chunk) is replayed by each chunk that holds records of it (the
+// same bits), adds its part of the gradient to g_out with float atomics and is stepped by
+// k_lazy_boundary (full replay, p_current false).
+template <int F4>
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
+    k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, uint64_t *__restrict__ vals,
+               const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
+               float *__restrict__ g_out, float *__restrict__ p_prev,
+               const uint32_t *__restrict__ off) {
+    constexpr int D = 64 * F4;
+    constexpr int E = 4 * F4;   // elements per lane
+    __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int q = lane >> 4, gl = lane & 15;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int64_t n_rec = range[1];
+    const int64_t n_chunks = (n_rec + gch - 1) / gch;
+    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int32_t step = dw::eff_step(oa.dyn, oa.step_delta, oa.step);
+    const int32_t upto = step - 1;
+    const dw::AdamScalars hs = dw::hist_at(oa.hist, step);
+    const int32_t box_from = dw::hist_box_from(oa.hist);
+    const dw::const_float *hc = (const dw::const_float *)oa.hist;
+    const int T = a.C * (1 + a.K), rpc = 1 + a.K;
+    const int64_t per = a.L - 2 * a.R;
+    float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
+
+    for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
+        const int64_t e0 = ch * gch;
+        const int n_in = static_cast<int>(n_rec - e0 < gch ? n_rec - e0 : gch);
+        const uint32_t before = e0 > 0 ? keys[e0 - 1] : 0xFFFFFFFFu;
+        const uint32_t after = e0 + n_in < n_rec ? keys[e0 + n_in] : 0xFFFFFFFFu;
+        const uint32_t my_key = lane < n_in ? keys[e0 + lane] : 0xFFFFFFFFu;
+        const uint32_t prev = __shfl_up(my_key, 1, WAVE);
+        const bool is_start = lane < n_in && (lane == 0 || my_key != prev);
+        const uint64_t starts = __ballot(is_start);
+        const int nrows = __popcll(starts);
+        if (is_start) s_rs[wv][__popcll(starts & lt)] = static_cast<uint8_t>(lane);
+        if (lane == 0) s_rs[wv][nrows] = static_cast<uint8_t>(n_in);
+        dw::wave_lds_sync();
+        for (int k0 = 0; k0 < nrows; k0 += 4) {
+            const int k = k0 + q;
+            const bool has = k < nrows;
+            const int rs = has ? s_rs[wv][k] : 0;
+            const int re = has ? s_rs[wv][k + 1] : 0;
+            const uint32_t row = __shfl(my_key, rs, WAVE);
+            const bool straddle = has && (row == before || row == after);
+            const int64_t ro = static_cast<int64_t>(has ? row : 0u) * D + 4 * gl;
+            const int32_t from = has ? oa.last[row] : upto;
+            float p[E], m[E], v[E];
+            auto load_row = [&]() {
+#pragma unroll
+                for (int f = 0; f < F4; ++f) {
+                    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 pf = has ? *reinterpret_cast<const float4 *>(oa.p + ro + 64 * f) : z;
+                    const float4 mf = has ? *reinterpret_cast<const float4 *>(oa.m + ro + 64 * f) : z;
+                    const float4 vf = has ? *reinterpret_cast<const float4 *>(oa.v + ro + 64 * f) : z;
+                    p[4 * f] = pf.x; p[4 * f + 1] = pf.y; p[4 * f + 2] = pf.z; p[4 * f + 3] = pf.w;
+                    m[4 * f] = mf.x; m[4 * f + 1] = mf.y; m[4 * f + 2] = mf.z; m[4 * f + 3] = mf.w;
+                    v[4 * f] = vf.x; v[4 * f + 1] = vf.y; v[4 * f + 2] = vf.z; v[4 * f + 3] = vf.w;
+                }
+            };
+            load_row();
+            // the deferred g = 0 steps, each group its own (from, upto]: the box forms while the
+            // whole wave's run stays in the box (dw::replay_g0's rule), else the scaled forms
+            {
+                const int32_t f0 = __builtin_amdgcn_readlane(from, 0);
+                const int32_t f1 = __builtin_amdgcn_readlane(from, 16);
+                const int32_t f2 = __builtin_amdgcn_readlane(from, 32);
+                const int32_t f3 = __builtin_amdgcn_readlane(from, 48);
+                const int32_t lo = min(min(f0, f1), min(f2, f3));
+                if (lo < upto) {
+                    bool fast = lo + 1 >= box_from;
+                    uint64_t zero = 0;   // bit e: m started +0; bit E + e: v started +0
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        fast = fast && v[e] <= 0x1p20f && fabsf(m[e]) <= 0x1p60f;
+                        zero |= (__float_as_uint(m[e]) == 0u ? 1ull : 0ull) << e;
+                        zero |= (__float_as_uint(v[e]) == 0u ? 1ull : 0ull) << (E + e);
+                    }
+                    if (__all(fast)) {
+                        for (int32_t s = lo + 1; s <= upto; ++s) {
+                            const dw::AdamScalars h = dw::hist_at_const(hc + 8 * static_cast<int64_t>(s));
+                            if (from < s) {
+#pragma unroll
+                                for (int e = 0; e < E; ++e) dw::adam_elem_g0_box(p[e], m[e], v[e], h);
+                            }
+                        }
+                        bool end = true;
+#pragma unroll
+                        for (int e = 0; e < E; ++e)
+                            end = end && (((zero >> (E + e)) & 1ull) || v[e] >= 0x1p-96f) &&
+                                  (((zero >> e) & 1ull) || fabsf(m[e]) >= 0x1p-100f);
+                        fast = __all(end);
+                        if (!fast) load_row();   // (the table is untouched: start again)
+                    }
+                    if (!fast) {
+                        for (int32_t s = lo + 1; s <= upto; ++s) {
+                            const dw::AdamScalars h = dw::hist_at(oa.hist, s);
+                            if (from >= s) continue;
+                            if (h.wd == 0.f) {
+#pragma unroll
+                                for (int e = 0; e < E; ++e) dw::adam_elem_g0(p[e], m[e], v[e], h);
+                            } else {
+#pragma unroll
+                                for (int e = 0; e < E; ++e) {
+                                    float z = 0.f;
+                                    dw::adam_elem(p[e], z, m[e], v[e], h);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            // the row's records in placed order: logit, coefficient, gradient sum
+            const int cnt = re - rs;
+            const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
+            const int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
+            const int nmax = max(max(c0, c1), max(c2, c3));
+            float g[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] = 0.f;
+            for (int j = 0; j < nmax; ++j) {
+                const bool in = has && j < cnt;
+                const int64_t pos = e0 + rs + j;
+                const uint32_t slot = in ? static_cast<uint32_t>(vals[pos]) : 0u;
+                const int64_t b = slot / T;
+                const int t = static_cast<int>(slot - b * T);
+                const int64_t w = b / per, i = a.R + (b - w * per);
+                const int64_t cid = in ? static_cast<int64_t>(a.walks[w * a.L + i]) : -1;
+                const bool ok = in && cid >= 0 && cid < a.V;
+                float c[E];
+                const float *crow = a.w_in + (ok ? cid : 0) * D + 4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f) {
+                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                    c[4 * f] = cf.x; c[4 * f + 1] = cf.y; c[4 * f + 2] = cf.z; c[4 * f + 3] = cf.w;
+                }
+                float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
+#pragma unroll
+                for (int e = 0; e < E; ++e) pr = fmaf(c[e], p[e], pr);
+                const float x = row_sum16(pr);
+                float coef = 0.f;
+                if (ok && gl == 0)
+                    coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
+                coef = __shfl(coef, q << 4, WAVE);
+                if (in && gl == 0) vals[pos] = pack_record(coef, static_cast<int64_t>(slot));
+#pragma unroll
+                for (int e = 0; e < E; ++e) g[e] += coef * c[e];
+            }
+            if (has) {
+                float *pv = p_prev + static_cast<int64_t>(off[row]) * D + 4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+                    *reinterpret_cast<float4 *>(pv + 64 * f) =
+                        make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
+                if (straddle) {
+                    float *dst = g_out + ro;
+#pragma unroll
+                    for (int f = 0; f < F4; ++f)
+#pragma unroll
+                        for (int cpt = 0; cpt < 4; ++cpt) atomicAdd(dst + 64 * f + cpt, g[4 * f + cpt]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) dw::adam_elem(p[e], g[e], m[e], v[e], hs);
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) {
+                        *reinterpret_cast<float4 *>(oa.p + ro + 64 * f) =
+                            make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
+                        *reinterpret_cast<float4 *>(oa.m + ro + 64 * f) =
+                            make_float4(m[4 * f], m[4 * f + 1], m[4 * f + 2], m[4 * f + 3]);
+                        *reinterpret_cast<float4 *>(oa.v + ro + 64 * f) =
+                            make_float4(v[4 * f], v[4 * f + 1], v[4 * f + 2], v[4 * f + 3]);
+                    }
+                    if (gl == 0) {
+                        oa.last[row] = step;
+                        if (oa.counts) oa.counts[row] = 0u;
+                    }
+                }
+            }
+        }
+        dw::wave_lds_sync();   // s_rs is rewritten by the next chunk
+    }
+    if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
 
 template <int VPL, bool EXACT>
@@ -2005,6 +2235,10 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     // placed (order_ready & 2, after dw_sgns_owner_out_catch_up with flags & 1): each record
     // straight to its row's segment of (k1, v1)
     const bool placed = (order_ready & 2) != 0;
+    // coefficients in (order_ready & 4, after dw_sgns_owner_out_rows): the centre gradient only
+    const bool coefin = (order_ready & 4) != 0;
+    DW_REQUIRE(!coefin || placed, "dw_sgns_owner_pass1: the coefficients come with the placed "
+               "records (order_ready & 2)");
     const bool dense = a.n_owners == 1 || placed;
     if (placed) {
         a.place_rank = pl.rank;
@@ -2025,7 +2259,8 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
         int32_t fl = 0;
         rc = exact_of(a.g_in, a.V * a.d, &a.fx_in, &fl, "dw_sgns_owner_pass1");
         if (rc != DW_OK) return rc;
-        rc = launch_pass1_g16<true, true>(a, st);
+        rc = coefin ? launch_pass1_g16<true, true, true>(a, st)
+                    : launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
         if (a.fx_in.acc && !(fl & DW_EXACT_DEFER)) {   // one rank: the centres' exact sums
             int64_t cb = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
@@ -2284,7 +2519,10 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // CLAIM_TRIPS centres per wave, their row ids and atomics issued together (independent chains
 // in flight), and ONE list atomic per block for all of them: a same-address atomic per block
 // serialises (1,120 blocks of one trip each were ~36 us at C3's 64-walk batch).
+// !CLAIM (the rows-major step, dw_sgns_owner_out_rows): the ranks alone — k_out_rows replays
+// every row right before its step, so no row is listed or caught up here.
 constexpr int CLAIM_TRIPS = 4;
+template <bool CLAIM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
@@ -2320,10 +2558,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             mine[k] = false;
             if (o[k] >= 0) {
                 const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
-                mine[k] = atomicMax(claim + o[k], step) < step - 1;
+                if (CLAIM) mine[k] = atomicMax(claim + o[k], step) < step - 1;
                 if (count) rank[b * T + lane] = atomicAdd(count + o[k], 1u);
             }
         }
+        if constexpr (!CLAIM) continue;
         uint32_t n_mine = 0;   // wave-uniform
 #pragma unroll
         for (int k = 0; k < CLAIM_TRIPS; ++k) {
@@ -2343,6 +2582,30 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         for (int k = 0; k < wv; ++k) base += s_cnt[k];
         for (uint32_t e = lane; e < n_mine; e += WAVE) list[base + e] = s_rows[wv][e];
         __syncthreads();   // s_rows / s_cnt / s_base are rewritten next tile
+    }
+}
+
+// The rows-major step, after the placement scan: slot s = b T + t (k_out_claim gave it its
+// rank among its row's slots) goes to off[row] + rank[s] — keys[pos] = the local row, vals[pos]
+// = s (k_out_rows adds the coefficient in the high word). The row ids are drawn again (Philox
+// for the negatives, the walk for the contexts), as pass 1 draws them.
+__global__ void __launch_bounds__(256)
+    k_place_slots(SgnsArgs a, const uint32_t *__restrict__ rank, const uint32_t *__restrict__ off,
+                  uint32_t *__restrict__ keys, uint64_t *__restrict__ vals) {
+    const int T = a.C * (1 + a.K);
+    const int64_t per = a.L - 2 * a.R;
+    const int64_t n = a.batch * T;
+    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n;
+         s += (int64_t)gridDim.x * 256) {
+        const int64_t b = s / T;
+        const int t = static_cast<int>(s - b * T);
+        const int64_t w = b / per, i = a.R + (b - w * per);
+        const int64_t r = row_id<true>(a, b, a.walks + w * a.L, i, t);
+        if (r < 0 || r >= a.V || r % a.n_owners != a.owner) continue;   // (counted by the claim)
+        const uint32_t o = static_cast<uint32_t>(r / a.n_owners);
+        const uint32_t pos = off[o] + rank[s];
+        keys[pos] = o;
+        vals[pos] = static_cast<uint64_t>(s);
     }
 }
 
@@ -2438,9 +2701,12 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     DW_REQUIRE(walks && w_out_local && m_out && v_out && last_step && claim && rows_buf &&
                    n_rows && hist && status,
                "dw_sgns_owner_out_catch_up: null pointer");
-    DW_REQUIRE((flags & ~3) == 0, "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2");
+    DW_REQUIRE((flags & ~7) == 0, "dw_sgns_owner_out_catch_up: flags must be a set of 1 | 2 | 4");
     const bool place = (flags & 1) != 0, p_only = (flags & 2) != 0;
+    const bool rows_major = (flags & 4) != 0;   // dw_sgns_owner_out_rows replays the rows itself
     DW_REQUIRE(!place || counts, "dw_sgns_owner_out_catch_up: placing needs the row counts");
+    DW_REQUIRE(!rows_major || place, "dw_sgns_owner_out_catch_up: the rows-major step places "
+               "the records (flags & 1)");
     hipStream_t st = dw::as_stream(stream);
     const dw_step_scalars *dyn = nullptr;
     int32_t delta = 0;
@@ -2472,10 +2738,15 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     int64_t blocks = (a.batch + ctile - 1) / ctile;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_out_claim, dim3((unsigned)blocks), dim3(WAVES_PER_BLOCK * WAVE), 0, st,
-                       a, claim, step, delta, rows_buf,
-                       reinterpret_cast<unsigned long long *>(n_rows), place ? counts : nullptr,
-                       place ? pl.rank : nullptr);
+    if (rows_major)
+        hipLaunchKernelGGL(k_out_claim<false>, dim3((unsigned)blocks),
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, a, claim, step, delta, rows_buf,
+                           reinterpret_cast<unsigned long long *>(n_rows), counts, pl.rank);
+    else
+        hipLaunchKernelGGL(k_out_claim<true>, dim3((unsigned)blocks),
+                           dim3(WAVES_PER_BLOCK * WAVE), 0, st, a, claim, step, delta, rows_buf,
+                           reinterpret_cast<unsigned long long *>(n_rows),
+                           place ? counts : nullptr, place ? pl.rank : nullptr);
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     if (place) {   // every row's segment of the records: the scan of the counts (+ the total)
         const int64_t nb = (local_rows + PLACE_TILE - 1) / PLACE_TILE;
@@ -2486,6 +2757,15 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
         hipLaunchKernelGGL(k_place_scan, dim3((unsigned)nb), dim3(256), 0, st, counts, local_rows,
                            sums, pl.off, ws.bounds);
         DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place");
+    }
+    if (rows_major) {   // the slots into their rows' segments; no catch-up
+        int64_t pb = (a.batch * T + 255) / 256;
+        if (pb > grid_cap(8)) pb = grid_cap(8);
+        if (pb < 1) pb = 1;
+        hipLaunchKernelGGL(k_place_slots, dim3((unsigned)pb), dim3(256), 0, st, a, pl.rank, pl.off,
+                           ws.k1, ws.v1);
+        DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place_slots");
+        return DW_OK;
     }
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1 (p_only:
     // only p is written back; the lazy gather replays m and v itself, cheaply, before the step)
@@ -2794,6 +3074,90 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     return launch_owner_pass2(n_walks * (walk_length - 2 * context_radius), T, local_rows, dim,
                               w_in, g_out_local, &oa, workspace, workspace_bytes, n_records,
                               dw::as_stream(stream), (flags & 1) != 0);
+}
+
+int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                           int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                           const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                           float grad_scale, const float *w_in, float *w_out_local,
+                           float *g_out_local, float *m_out, float *v_out, int32_t *last_step,
+                           uint32_t *counts, const float *hist, int32_t step, float *p_prev,
+                           int64_t p_prev_rows, double *loss_acc, int32_t *status,
+                           void *workspace, size_t workspace_bytes, void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
+                   owner >= 0 && owner < n_owners && local_rows >= 1 && step >= 1,
+               "dw_sgns_owner_out_rows: bad sizes");
+    DW_REQUIRE(dim % 64 == 0 && dim <= 512, "dw_sgns_owner_out_rows: needs dim a multiple of 64 "
+               "(<= 512)");
+    DW_REQUIRE(2 * (int64_t)context_radius * (1 + neg_samples) <= G16_TMAX,
+               "dw_sgns_owner_out_rows: 2R(1+K) must be <= %d", G16_TMAX);
+    DW_REQUIRE(local_rows * n_owners >= vocab_size && vocab_size <= 0x7FFFFFFF,
+               "dw_sgns_owner_out_rows: the owners' rows do not cover the vocabulary");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(walks && w_in && w_out_local && g_out_local && m_out && v_out && last_step &&
+                   counts && hist && p_prev && status,
+               "dw_sgns_owner_out_rows: null pointer");
+    const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
+    const int64_t n_centres = n_walks * (walk_length - 2 * context_radius);
+    DW_REQUIRE(p_prev_rows >= n_centres * T, "dw_sgns_owner_out_rows: p_prev holds %lld rows, "
+               "the batch places %lld records", (long long)p_prev_rows,
+               (long long)(n_centres * T));
+    hipStream_t st = dw::as_stream(stream);
+    SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out_local, nullptr, g_out_local,
+                           noise, seed, noise_offset, grad_scale, loss_acc, status);
+    a.walks = walks;
+    a.L = walk_length;
+    a.R = context_radius;
+    a.batch = n_centres;
+    a.C = 2 * context_radius;
+    a.owner = owner;
+    a.n_owners = n_owners;
+    int32_t fl = 0;
+    dw::Fixed fx;
+    int rc = exact_of(g_out_local, local_rows * dim, &fx, &fl, "dw_sgns_owner_out_rows");
+    if (rc != DW_OK) return rc;
+    DW_REQUIRE(!fx.acc, "dw_sgns_owner_out_rows: the rows-major step has no deterministic form");
+    Workspace ws;
+    OwnerLayout lay;
+    PlaceSpace pl;
+    rc = owner_workspace(n_centres, T, local_rows, workspace, workspace_bytes, &ws, &lay, st,
+                         "dw_sgns_owner_out_rows", vocab_size, nullptr, &pl);
+    if (rc != DW_OK) return rc;
+    OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
+    oa.counts = counts;   // (p_current false: k_lazy_boundary replays the straddling rows whole)
+    rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
+    if (rc != DW_OK) return rc;
+    // records per chunk (<= 64: one per lane): 64, halved to 32 while the chunks would not give
+    // every SIMD of the chip eight waves
+    const int64_t bound = n_centres * T;
+    static const int32_t gch_env = [] {   // DW_ROWS_GCH: tuning sweeps only
+        const char *e = getenv("DW_ROWS_GCH");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 8 && v <= 64) ? v : 0;
+    }();
+    int32_t gch = gch_env ? gch_env : (bound / 64 < grid_cap(32) ? 32 : 64);
+    int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
+    switch (dim / 64) {
+        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
+        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
+        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
+        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
+        default: return DW_E_UNSUPPORTED;
+    }
+    DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
+    switch (dim / 64) {   // the straddling rows (g in g_out)
+        case 1: launch_boundary<1>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
+        case 2: launch_boundary<2>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
+        case 4: launch_boundary<4>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
+        default: launch_boundary<8>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
+    }
+    DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/boundary");
+    return DW_OK;
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,

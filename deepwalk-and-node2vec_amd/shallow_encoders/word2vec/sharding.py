@@ -807,8 +807,7 @@ def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
                          context_radius=context_radius, out_adam=spec, status=status,
                          read_count=tables.world > 1)
     if n is None:   # one owner keeps every slot (no count readback)
-        n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
-            1 + neg_samples)
+        n = slots
     if spec is None:
         tables.out_step()
     tables.sync()
@@ -886,6 +885,18 @@ class OwnerLazyTables(OwnerTables):
                       and os.environ.get('DW_OUT_PLACE', '1') != '0')   # (A/B, round 4)
         # any step with weight decay: the p-only catch-up no longer holds
         self._wd_seen = os.environ.get('DW_OUT_P_ONLY', '1') == '0'   # (A/B, round 4)
+        # placed records: the rows-major step (dw_sgns_owner_out_rows) reads and writes each
+        # touched out row once; the catch-up -> pass 1 -> lazy gather sequence otherwise
+        self.rows_major = self.place and os.environ.get('DW_OUT_ROWS', '1') != '0'
+        self._p_prev = None        # [slots, d]: the rows' pre-step values for the centre pass
+        self._rows_step = False    # this step goes rows-major (set by catch_up_out)
+
+    def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
+        """The rows-major step applies: placed records, d a multiple of 64 (<= 512),
+        2R(1+K) <= 64, no deterministic mode."""
+        return (self.rows_major and self.d % 64 == 0 and self.d <= 512
+                and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64
+                and getattr(self, '_exact', None) is None)
 
     def out_flags(self) -> int:
         """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
@@ -914,6 +925,8 @@ class OwnerLazyTables(OwnerTables):
         if self._out_rows is None or self._out_rows.numel() < cap:
             self._out_rows = torch.empty(cap, dtype=torch.int32, device=self.device)
         ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
+        self._rows_step = self.rows_major_ok(R, K)
+        flags = (self.out_flags() & 3) | (4 if self._rows_step else 0)
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_catch_up', _native.ptr(walks), n, L,
                          int(context_radius), int(neg_samples), self.V, self.d, self.rank,
@@ -923,8 +936,35 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._claim_out), _native.ptr(self._count_out),
                          _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
-                         self.out_flags() & 3, _native.ptr(status), _native.ptr(ws), ws.numel(),
+                         flags, _native.ptr(status), _native.ptr(ws), ws.numel(),
                          _native.stream(self.device))
+
+    def out_rows_step(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
+                      seed: int, noise_offset: int, grad_scale: float, loss_acc: torch.Tensor,
+                      status: torch.Tensor, noise: Optional[torch.Tensor] = None) -> None:
+        """The rows-major out step of the batch ``walks`` (after catch_up_out chose it):
+        dw_sgns_owner_out_rows — each touched out row replayed, its records' coefficients and
+        loss terms, its gradient and Adam step; the rows' pre-step values into ``_p_prev`` for
+        the centre pass (sgns_owner_pass1 with coef_in)."""
+        from shallow_encoders.word2vec.sgns import workspace_for
+        n, L = walks.shape
+        R, K = int(context_radius), int(neg_samples)
+        slots = n * (L - 2 * R) * 2 * R * (1 + K)
+        if self._p_prev is None or self._p_prev.shape[0] < max(slots, 1):
+            self._p_prev = torch.empty((max(slots, 1), self.d), dtype=torch.float32,
+                                       device=self.device)
+        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
+        with torch.cuda.device(self.device):
+            _native.call('dw_sgns_owner_out_rows', _native.ptr(walks), n, L, R, K, self.V,
+                         self.d, self.rank, self.world, self.S, _native.ptr(noise),
+                         seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(grad_scale),
+                         _native.ptr(self.w_in_raw), _native.ptr(self.w_out),
+                         _native.ptr(self.g_out), _native.ptr(self.m_out),
+                         _native.ptr(self.v_out), _native.ptr(self.last_out),
+                         _native.ptr(self._count_out), _native.ptr(self._hist),
+                         self.step_count, _native.ptr(self._p_prev), self._p_prev.shape[0],
+                         _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws),
+                         ws.numel(), _native.stream(self.device))
 
     def _alloc_in(self, f32: dict) -> None:
         self.params_in = torch.zeros((1, self.V_pad, self.d), **f32)
@@ -1173,6 +1213,20 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
+    slots = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
+        1 + neg_samples)
+    if tables.lazy_out and tables._rows_step:
+        # rows-major: the out rows' whole step, then the centre gradient from its coefficients
+        tables.out_rows_step(walks, context_radius, neg_samples, seed, noise_offset,
+                             grad_scale, loss_acc, status)
+        sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples,
+                         walks=walks, context_radius=context_radius, owner=tables.rank,
+                         n_owners=tables.world, vocab_size=tables.V, seed=seed,
+                         noise_offset=noise_offset, grad_scale=grad_scale, status=status,
+                         order_ready=True, placed=True, coef_in=tables._p_prev)
+        tables.exchange_touched()
+        tables.update_touched()
+        return slots
     sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples, walks=walks,
                      context_radius=context_radius, owner=tables.rank, n_owners=tables.world,
                      vocab_size=tables.V, seed=seed, noise_offset=noise_offset,
@@ -1184,8 +1238,7 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
                          context_radius=context_radius, out_adam=spec, status=status,
                          read_count=tables.world > 1)
     if n is None:   # one owner keeps every slot (no count readback)
-        n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
-            1 + neg_samples)
+        n = slots
     if spec is None:
         tables.out_step()
     tables.update_touched()

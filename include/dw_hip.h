@@ -487,7 +487,10 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
  * dw_sgns_owner_pass1's order_ready is a bit set: 1 = this order is ready (else pass 1 builds
  * it); 2 = the records are placed (dw_sgns_owner_out_catch_up ran with flags & 1 on this batch
  * and workspace): pass 1 writes each record straight into its row's segment, and
- * dw_sgns_owner_pass2_lazy (flags & 1) gathers them without a sort. */
+ * dw_sgns_owner_pass2_lazy (flags & 1) gathers them without a sort; 4 (with 2) = coefficients in:
+ * dw_sgns_owner_out_rows already formed every record's coefficient and left each row's
+ * pre-step values in p_prev, which is passed as w_out_local — pass 1 forms the centre gradient
+ * alone (no loss sums, no records written; loss_acc may be NULL). */
 int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           int64_t local_rows, uint32_t *touched, int64_t *n_touched,
@@ -523,7 +526,10 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
  *       no sort (the order of one row's records is the order the atomics resolved);
  *   2 = replay p only: m, v and last_step stay behind, and dw_sgns_owner_pass2_lazy (flags | 2)
  *       replays m and v (a multiply each per step) before the step — valid while every step has
- *       weight_decay 0.
+ *       weight_decay 0;
+ *   4 (with 1) = the rows-major step follows (dw_sgns_owner_out_rows): only the ranks and the
+ *       scan — no claim, no list, no replay — then every slot is placed (its row and slot id in
+ *       the workspace's records); claim and rows_buf are not touched.
  * 2R(1+K) <= 64, dim <= 512. */
 int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                                int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
@@ -551,6 +557,26 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t step, int32_t flags, uint32_t *counts, int32_t *status,
                              void *workspace, size_t workspace_bytes, int64_t *n_records,
                              void *stream);
+
+/* The rows-major lazy out step (OwnerLazyTables, one device; after dw_sgns_owner_out_catch_up
+ * with flags 1 | 4 on the same batch and workspace, before dw_sgns_owner_pass1 with order_ready
+ * 1 | 2 | 4): each owned out row the batch touches is read once and written once — its deferred
+ * g = 0 steps replayed (hist, as for dw_adam_rows), the logits of its records against their
+ * centre rows, the coefficients and loss sums (loss_acc float64[4] as for dw_sgns_walks), its
+ * gradient and the Adam step `step` — the same arithmetic as the catch-up / pass 1 /
+ * dw_sgns_owner_pass2_lazy sequence. Leaves each record's coefficient in the placed records and
+ * the row's pre-step values in p_prev (float32 [p_prev_rows >= B' * 2R(1+K), dim], at the row's
+ * first record position) for dw_sgns_owner_pass1's centre gradient. counts: the catch-up's, cleared
+ * as the rows step. dim a multiple of 64 (<= 512), 2R(1+K) <= 64; no deterministic form. */
+int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
+                           int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
+                           const int64_t *noise, uint64_t seed, uint64_t noise_offset,
+                           float grad_scale, const float *w_in, float *w_out_local,
+                           float *g_out_local, float *m_out, float *v_out, int32_t *last_step,
+                           uint32_t *counts, const float *hist, int32_t step, float *p_prev,
+                           int64_t p_prev_rows, double *loss_acc, int32_t *status,
+                           void *workspace, size_t workspace_bytes, void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
  * inputs int64[B], targets int64[B, C], noise int64[B, C, K] or NULL (Philox as above). */

@@ -582,6 +582,40 @@ def test_placed_records_equal_sorted_records(hip_device, d):
         assert_no_row_drift(got, exp)
 
 
+@pytest.mark.parametrize('d,wd,hub', [(64, 0.0, False), (128, 0.0, True), (128, 0.01, False),
+                                      (256, 0.0, True)])
+def test_rows_major_equals_gather_path(hip_device, d, wd, hub):
+    """The rows-major lazy out step (dw_sgns_owner_out_rows: each touched out row replayed,
+    its records' logits / coefficients, its gradient and Adam step in one pass, then the
+    centre gradient from the coefficients) equals the catch-up -> pass 1 -> lazy gather path:
+    the same rows stepped at the same steps (last_out), the losses to float64 order and the
+    tables to the order a row's records are summed in (the claim's atomics). hub: a few nodes
+    fill a third of the walks, so their rows hold hundreds of records and straddle chunks
+    (float atomics into g_out, k_lazy_boundary's full replay)."""
+    V, R, K, L, n, steps, lr = 4000, 2, 4, 14, 32, 8, 0.02
+    g = torch.Generator().manual_seed(23)
+    walks = torch.randint(1, V, (steps, n, L), generator=g, dtype=torch.int32)
+    if hub:
+        mask = torch.rand((steps, n, L), generator=g) < 0.33
+        walks[mask] = torch.randint(1, 4, (int(mask.sum()),), generator=g, dtype=torch.int32)
+    runs = []
+    for rows_major in (True, False):
+        def cfg(t, rows_major=rows_major):
+            t.rows_major = rows_major
+        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, wd=wd,
+                                configure=cfg)
+        assert t._rows_step == rows_major
+        runs.append((t.last_out.clone(), t.w_in.cpu().numpy(), t.full_w_out().cpu().numpy(),
+                     acc.cpu().numpy()))
+    (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
+    assert torch.equal(l0, l1)
+    np.testing.assert_allclose(a0, a1, rtol=1e-6)
+    for got, exp in ((i0, i1), (o0, o1)):
+        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
+                            max_abs=2.05 * lr * steps)
+        assert_no_row_drift(got, exp)
+
+
 @pytest.mark.parametrize('wd_head', [False, True])
 def test_adam_reciprocal_division_bit_identical(hip_device, wd_head):
     """The replays' fast forms give the scaled IEEE sequences' bits: dw::div_bc2s (sqrt(v) /
