@@ -894,7 +894,7 @@ class OwnerLazyTables(OwnerTables):
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
         """The rows-major step applies: placed records, d a multiple of 64 (<= 512),
         2R(1+K) <= 64, no deterministic mode."""
-        return (self.rows_major and self.d % 64 == 0 and self.d <= 512
+        return (self.rows_major and self.place and self.d % 64 == 0 and self.d <= 512
                 and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64
                 and getattr(self, '_exact', None) is None)
 

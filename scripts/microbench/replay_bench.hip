@@ -6,6 +6,10 @@
 //   3: one wave per row, 2 elements per lane (more loads in flight per wave)
 //   4: one wave per two rows
 //   5: as 3 with a 2048-block grid
+//   6: no replay (the row loads and the p store alone: the traffic's floor)
+//   7-8: the traffic alone with dwordx2 / dwordx4 loads (a row per wave / two)
+//   9-11: mode 1 software-pipelined (the next row's loads before this row's replay), grids
+//         of 16384 / 4096 / 65536 blocks
 // Prints the mean kernel time per variant and checks every variant gives variant 0's bits.
 //   hipcc -O3 --offload-arch=gfx950 -I include scripts/microbench/replay_bench.hip \
 //         -o scripts/microbench/replay_bench
@@ -45,6 +49,8 @@ __global__ void __launch_bounds__(512)
             }
         } else if (MODE == 1) {
             dw::replay_g0(pr, mr, vr, hist, from, upto, dw::hist_box_from(hist));
+        } else if (MODE == 6) {   // no replay: the loads and the store alone
+            pr[0] = pr[0] + mr[0] * vr[0] * static_cast<float>(upto - from) * 0.f;
         } else {
             const dw::const_float *hc = (const dw::const_float *)hist;
             for (int32_t s = from + 1; s <= upto; ++s)
@@ -93,6 +99,62 @@ __global__ void __launch_bounds__(256)
                 if (i0 + j < n && e < d && fr[j] < upto) p[rr[j] * d + e] = pr[j][k];
             }
         }
+    }
+}
+
+// The traffic alone with wider loads: each lane loads VEC floats of a row (dword / dwordx2 /
+// dwordx4), 128 / VEC lanes per row, 64 / (128 / VEC) rows per wave.
+template <int VEC>
+__global__ void __launch_bounds__(256)
+    k_traffic(float *__restrict__ p, const float *__restrict__ m, const float *__restrict__ v,
+              const int32_t *__restrict__ last, const uint32_t *__restrict__ rows, int64_t n,
+              int32_t upto) {
+    typedef float __attribute__((ext_vector_type(VEC))) fv;
+    constexpr int LPR = 128 / VEC;            // lanes per row
+    constexpr int RPW = 64 / LPR;             // rows per wave
+    const int lane = threadIdx.x & 63;
+    const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const int64_t i = w * RPW + lane / LPR;
+    if (i >= n) return;
+    const int64_t r = rows[i];
+    const int32_t from = last[r];
+    const int64_t o = r * 128 + (lane % LPR) * VEC;
+    fv pp = *reinterpret_cast<const fv *>(p + o);
+    const fv mm = *reinterpret_cast<const fv *>(m + o);
+    const fv vv = *reinterpret_cast<const fv *>(v + o);
+    pp = pp + mm * vv * static_cast<float>(upto - from) * 0.f;
+    *reinterpret_cast<fv *>(p + o) = pp;
+}
+
+// k_replay<1> with the next row's loads issued before the current row's replay (software
+// pipelined: a wave's loads stay in flight while it computes).
+__global__ void __launch_bounds__(512)
+    k_replay_pf(float *__restrict__ p, const float *__restrict__ m, const float *__restrict__ v,
+                const int32_t *__restrict__ last, int32_t d, const uint32_t *__restrict__ rows,
+                int64_t n, const float *__restrict__ hist, int32_t upto) {
+    const int e = threadIdx.x;
+    const bool live = e < d;
+    const int32_t box_from = dw::hist_box_from(hist);
+    int64_t i = blockIdx.x;
+    if (i >= n) return;
+    int64_t r = rows[i];
+    int32_t from = __builtin_amdgcn_readfirstlane(last[r]);
+    float pn = live ? p[r * d + e] : 0.f, mn = live ? m[r * d + e] : 0.f;
+    float vn = live ? v[r * d + e] : 0.f;
+    for (; i < n; i += gridDim.x) {
+        float pr[1] = {pn}, mr[1] = {mn}, vr[1] = {vn};
+        const int64_t rc = r;
+        const int32_t fc = from;
+        const int64_t j = i + gridDim.x;
+        if (j < n) {   // the next row's loads, in flight during this row's replay
+            r = rows[j];
+            from = __builtin_amdgcn_readfirstlane(last[r]);
+            pn = live ? p[r * d + e] : 0.f;
+            mn = live ? m[r * d + e] : 0.f;
+            vn = live ? v[r * d + e] : 0.f;
+        }
+        dw::replay_g0(pr, mr, vr, hist, fc, upto, box_from);
+        if (live) p[rc * d + e] = pr[0];
     }
 }
 
@@ -159,9 +221,9 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    std::vector<float> out[6];
+    std::vector<float> out[12];
     const unsigned grid = R < 65536 ? (unsigned)R : 65536u;
-    for (int mode = 0; mode < 6; ++mode) {
+    for (int mode = 0; mode < 12; ++mode) {
         float tot = 0.f;
         for (int k = 0; k < reps + 2; ++k) {
             hipMemcpy(dp, dp0, V * d * 4, hipMemcpyDeviceToDevice);
@@ -181,9 +243,27 @@ int main(int argc, char **argv) {
             else if (mode == 4)   // two rows per wave
                 hipLaunchKernelGGL((k_replay_wave<2, 2>), dim3((R + 7) / 8), dim3(256), 0, 0, dp,
                                    dm, dv, dl, d, dr, R, dh, T - 1);
-            else                  // wave per row, capped grid (grid-stride)
+            else if (mode == 5)   // wave per row, capped grid (grid-stride)
                 hipLaunchKernelGGL((k_replay_wave<2, 1>), dim3(2048), dim3(256), 0, 0, dp, dm, dv,
                                    dl, d, dr, R, dh, T - 1);
+            else if (mode == 6)   // the memory traffic alone
+                hipLaunchKernelGGL(k_replay<6>, dim3(grid), dim3(d), 0, 0, dp, dm, dv, dl, d, dr,
+                                   R, dh, T - 1);
+            else if (mode == 7)   // dwordx2, a row per wave
+                hipLaunchKernelGGL(k_traffic<2>, dim3((R + 3) / 4), dim3(256), 0, 0, dp, dm, dv,
+                                   dl, dr, R, T - 1);
+            else if (mode == 9)   // pipelined, 16384 blocks
+                hipLaunchKernelGGL(k_replay_pf, dim3(16384), dim3(d), 0, 0, dp, dm, dv, dl, d, dr,
+                                   R, dh, T - 1);
+            else if (mode == 10)  // pipelined, 4096 blocks
+                hipLaunchKernelGGL(k_replay_pf, dim3(4096), dim3(d), 0, 0, dp, dm, dv, dl, d, dr,
+                                   R, dh, T - 1);
+            else if (mode == 11)  // pipelined, 65536 blocks
+                hipLaunchKernelGGL(k_replay_pf, dim3(grid), dim3(d), 0, 0, dp, dm, dv, dl, d, dr,
+                                   R, dh, T - 1);
+            else                  // dwordx4, two rows per wave
+                hipLaunchKernelGGL(k_traffic<4>, dim3((R / 2 + 3) / 4), dim3(256), 0, 0, dp, dm,
+                                   dv, dl, dr, R, T - 1);
             hipEventRecord(b, 0);
             hipEventSynchronize(b);
             float ms;
@@ -195,7 +275,7 @@ int main(int argc, char **argv) {
         printf("mode %d: %.1f us per launch (%lld rows)\n", mode, 1e3 * tot / reps, (long long)R);
     }
     bool all = true;
-    for (int mode = 1; mode < 6; ++mode) {
+    for (int mode : {1, 2, 3, 4, 5, 9, 10, 11}) {
         const bool same = memcmp(out[0].data(), out[mode].data(), V * d * 4) == 0;
         printf("mode %d == mode 0 bits: %s\n", mode, same ? "yes" : "NO");
         all = all && same;
