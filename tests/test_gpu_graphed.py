@@ -141,8 +141,11 @@ def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
     np.testing.assert_array_equal(walks_g, walks_e)
     # float64 atomic loss sums over tables with fp32 atomic-order noise: measured 1.03e-9
     np.testing.assert_allclose(acc_g, acc_e, rtol=1e-8)
+    # a row's records are summed in the order the claim's atomics ranked them, which differs
+    # between the two runs, and 12 Adam steps can amplify an ulp of a near-zero gradient entry:
+    # a run measured 1.4e-4 on one entry against lr/100; lr/10 there (the atomic scatter's bar)
     for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
-        assert_params_close(got, exp, LR)
+        assert_params_close(got, exp, LR, max_abs=LR / 10)
         assert_no_row_drift(got, exp)
 
 

@@ -616,6 +616,39 @@ def test_rows_major_equals_gather_path(hip_device, d, wd, hub):
         assert_no_row_drift(got, exp)
 
 
+@pytest.mark.parametrize('d,wd', [(128, 0.0), (64, 0.01)])
+def test_rows_major_bit_identical_without_collisions(hip_device, d, wd):
+    """Where no two records of a step share an out row and no two centres share a node, nothing
+    depends on the order of atomics, and the rows-major step equals the catch-up -> pass 1 ->
+    lazy gather path bit for bit — the same logits (pass 1's 16-lane layout and FMA order),
+    coefficients, gradient sums, replays and Adam steps. Walks of length 2R + 1 (one centre
+    each) over distinct nodes, and none of a step's negatives (oracle.philox.device_noise, the
+    device's draws) among its contexts or each other."""
+    from oracle.philox import device_noise
+    V, R, K, L, n, steps, lr = 2_000_000, 2, 2, 5, 16, 6, 0.02
+    g = torch.Generator().manual_seed(5)
+    walks = torch.empty((steps, n, L), dtype=torch.int32)
+    for s in range(steps):
+        neg = device_noise(11, s * n, n, 2 * R, K, V).ravel()   # _lazy_vs_dense's seed, offsets
+        assert np.unique(neg).size == neg.size
+        pool = torch.randperm(V - 1, generator=g)[:4 * n * L].add_(1)
+        pool = pool[~torch.from_numpy(np.isin(pool.numpy(), neg))][:n * L]
+        walks[s] = pool.view(n, L).to(torch.int32)
+    runs = []
+    for rows_major in (True, False):
+        def cfg(t, rows_major=rows_major):
+            t.rows_major = rows_major
+        t, acc = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, wd=wd,
+                                configure=cfg)
+        assert t._rows_step == rows_major
+        runs.append((t.last_out.clone(), t.w_in.cpu(), t.full_w_out().cpu(), acc.cpu()))
+    (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
+    assert torch.equal(l0, l1)
+    torch.testing.assert_close(a0, a1, rtol=1e-12, atol=0)
+    assert torch.equal(i0.view(torch.int32), i1.view(torch.int32))
+    assert torch.equal(o0.view(torch.int32), o1.view(torch.int32))
+
+
 @pytest.mark.parametrize('wd_head', [False, True])
 def test_adam_reciprocal_division_bit_identical(hip_device, wd_head):
     """The replays' fast forms give the scaled IEEE sequences' bits: dw::div_bc2s (sqrt(v) /
