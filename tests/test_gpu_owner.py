@@ -644,7 +644,8 @@ def test_rows_major_bit_identical_without_collisions(hip_device, d, wd):
         runs.append((t.last_out.clone(), t.w_in.cpu(), t.full_w_out().cpu(), acc.cpu()))
     (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
     assert torch.equal(l0, l1)
-    torch.testing.assert_close(a0, a1, rtol=1e-12, atol=0)
+    # (the loss terms are summed per lane in fp32, grouped differently by the two paths)
+    torch.testing.assert_close(a0, a1, rtol=1e-6, atol=0)
     assert torch.equal(i0.view(torch.int32), i1.view(torch.int32))
     assert torch.equal(o0.view(torch.int32), o1.view(torch.int32))
 
