@@ -409,10 +409,11 @@ __device__ __forceinline__ float row_sum16(float x) {
 // EXACT: the centre-gradient terms enter g_in's int64 accumulator as fixed-point integers
 // (dw::to_fixed), each lane adding its 4 F4 elements of its group's centre straight from
 // registers (no LDS staging, no run summing: integer sums need no order).
-// COEFIN (the rows-major step, after k_out_rows; one owner or many, placed records): the
-// coefficients are already in the placed records (rec_val[place_off[row] + place_rank[slot]]'s
-// high word) and each row's pre-step values p^{s-1} in w_out[place_off[row]] (k_out_rows'
-// copy): only the centre gradient is formed — the same FMAs in the same order as the full pass.
+// COEFIN (the rows-major step, after k_out_rows; one owner or many, placed records): slot
+// b T + t's coefficient is already in ((float *) rec_val)[b T + t] and its row's pre-step
+// values p^{s-1} in w_out[b T + t] (k_out_rows' copies, by slot: the same addressing as the
+// table rows, no indirection): only the centre gradient is formed — the same FMAs in the same
+// order as the full pass.
 template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false, bool COEFIN = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
@@ -569,8 +570,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int u = 0; u < CHR; ++u) {
                 const int t = t0 + u;
                 rid[u] = (t < n_own) ? s_id[wv][q][t] : -1;
+                // COEFIN: the row's pre-step values as k_out_rows left them, by slot
                 const int64_t at = rid[u] < 0 ? 0
-                                   : COEFIN ? static_cast<int64_t>(a.place_off[rid[u]])
+                                   : COEFIN ? b * T + static_cast<int64_t>(s_t[wv][q][t])
                                             : static_cast<int64_t>(rid[u]);
                 const float *row = a.w_out + at * D + 4 * gl;
 #pragma unroll
@@ -610,8 +612,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             if (gl < CHR && t < n_own && xid >= 0) {
                 const int slot = OWNER ? static_cast<int>(s_t[wv][q][t]) : t;
                 if constexpr (COEFIN) {
-                    const uint32_t pos = a.place_off[xid] + a.place_rank[b * T + slot];
-                    coef = __uint_as_float(static_cast<uint32_t>(a.rec_val[pos] >> 32));
+                    coef = reinterpret_cast<const float *>(a.rec_val)[b * T + slot];
                 } else {
                     coef = row_coef(x, (slot % rows_per_ctx) == 0, a.scale, acc_pos, acc_neg,
                                     acc_rec, acc_prec);
@@ -1413,10 +1414,10 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // k_lazy_boundary (full replay, p_current false).
 template <int F4>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
-    k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, uint64_t *__restrict__ vals,
+    k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
                float *__restrict__ g_out, float *__restrict__ p_prev,
-               const uint32_t *__restrict__ off) {
+               float *__restrict__ coef_slot) {
     constexpr int D = 64 * F4;
     constexpr int E = 4 * F4;   // elements per lane
     __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
@@ -1442,6 +1443,13 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         const uint32_t before = e0 > 0 ? keys[e0 - 1] : 0xFFFFFFFFu;
         const uint32_t after = e0 + n_in < n_rec ? keys[e0 + n_in] : 0xFFFFFFFFu;
         const uint32_t my_key = lane < n_in ? keys[e0 + lane] : 0xFFFFFFFFu;
+        // lane = record: its slot s = b T + t and its centre node, all 64 in one round trip
+        const uint32_t my_slot = lane < n_in ? static_cast<uint32_t>(vals[e0 + lane]) : 0u;
+        const uint32_t my_b = my_slot / static_cast<uint32_t>(T);
+        const uint32_t my_w = my_b / static_cast<uint32_t>(per);
+        const int32_t my_cid = lane < n_in
+            ? a.walks[static_cast<int64_t>(my_w) * a.L + a.R + (my_b - my_w * static_cast<uint32_t>(per))]
+            : -1;
         const uint32_t prev = __shfl_up(my_key, 1, WAVE);
         const bool is_start = lane < n_in && (lane == 0 || my_key != prev);
         const uint64_t starts = __ballot(is_start);
@@ -1523,7 +1531,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                     }
                 }
             }
-            // the row's records in placed order: logit, coefficient, gradient sum
+            // the row's records in placed order: logit, coefficient, gradient sum; RU records'
+            // centre rows in flight at a time (a hub row holds hundreds of a chunk's records)
             const int cnt = re - rs;
             const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
             const int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
@@ -1531,41 +1540,54 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             float g[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) g[e] = 0.f;
-            for (int j = 0; j < nmax; ++j) {
-                const bool in = has && j < cnt;
-                const int64_t pos = e0 + rs + j;
-                const uint32_t slot = in ? static_cast<uint32_t>(vals[pos]) : 0u;
-                const int64_t b = slot / T;
-                const int t = static_cast<int>(slot - b * T);
-                const int64_t w = b / per, i = a.R + (b - w * per);
-                const int64_t cid = in ? static_cast<int64_t>(a.walks[w * a.L + i]) : -1;
-                const bool ok = in && cid >= 0 && cid < a.V;
-                float c[E];
-                const float *crow = a.w_in + (ok ? cid : 0) * D + 4 * gl;
+            constexpr int RU = 4;
+            for (int j0 = 0; j0 < nmax; j0 += RU) {
+                float c[RU][E];
+                uint32_t slot[RU];
+                bool ok[RU];
 #pragma unroll
-                for (int f = 0; f < F4; ++f) {
-                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                    c[4 * f] = cf.x; c[4 * f + 1] = cf.y; c[4 * f + 2] = cf.z; c[4 * f + 3] = cf.w;
+                for (int u = 0; u < RU; ++u) {
+                    const int src = rs + j0 + u;
+                    const bool in = has && j0 + u < cnt;
+                    slot[u] = __shfl(my_slot, src & 63, WAVE);
+                    const int32_t cid = __shfl(my_cid, src & 63, WAVE);
+                    ok[u] = in && cid >= 0 && cid < a.V;
+                    const float *crow = a.w_in + static_cast<int64_t>(ok[u] ? cid : 0) * D + 4 * gl;
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) {
+                        const float4 cf = ok[u] ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                        c[u][4 * f] = cf.x; c[u][4 * f + 1] = cf.y;
+                        c[u][4 * f + 2] = cf.z; c[u][4 * f + 3] = cf.w;
+                    }
                 }
-                float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
-                for (int e = 0; e < E; ++e) pr = fmaf(c[e], p[e], pr);
-                const float x = row_sum16(pr);
-                float coef = 0.f;
-                if (ok && gl == 0)
-                    coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
-                coef = __shfl(coef, q << 4, WAVE);
-                if (in && gl == 0) vals[pos] = pack_record(coef, static_cast<int64_t>(slot));
+                for (int u = 0; u < RU; ++u) {
+                    if (j0 + u >= nmax) break;
+                    const bool in = has && j0 + u < cnt;
+                    float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
-                for (int e = 0; e < E; ++e) g[e] += coef * c[e];
+                    for (int e = 0; e < E; ++e) pr = fmaf(c[u][e], p[e], pr);
+                    const float x = row_sum16(pr);
+                    const int t = static_cast<int>(slot[u] % static_cast<uint32_t>(T));
+                    float coef = 0.f;
+                    if (ok[u] && gl == 0)
+                        coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec,
+                                        acc_prec);
+                    coef = __shfl(coef, q << 4, WAVE);
+#pragma unroll
+                    for (int e = 0; e < E; ++e) g[e] += coef * c[u][e];
+                    if (in) {   // the centre pass's inputs, by slot
+                        if (gl == 0) coef_slot[slot[u]] = coef;
+                        float *pv = p_prev + static_cast<int64_t>(slot[u]) * D + 4 * gl;
+#pragma unroll
+                        for (int f = 0; f < F4; ++f)
+                            *reinterpret_cast<float4 *>(pv + 64 * f) =
+                                make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
+                    }
+                }
             }
             if (has) {
-                float *pv = p_prev + static_cast<int64_t>(off[row]) * D + 4 * gl;
-#pragma unroll
-                for (int f = 0; f < F4; ++f)
-                    *reinterpret_cast<float4 *>(pv + 64 * f) =
-                        make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
                 if (straddle) {
                     float *dst = g_out + ro;
 #pragma unroll
@@ -2246,6 +2268,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     }
     a.rec_key = dense ? ws.k1 : ws.k0;
     a.rec_val = dense ? ws.v1 : ws.v0;
+    if (coefin) a.rec_val = ws.v0;   // k_out_rows' coefficients by slot (float) there
     a.count_out = dense ? ws.count : nullptr;
     a.rec_counts = ws.wave_counts;
     a.region = lay.region;
@@ -3143,10 +3166,10 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     switch (dim / 64) {
-        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
-        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
-        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
-        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, pl.off); break;
+        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
+        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
+        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
+        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
         default: return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
