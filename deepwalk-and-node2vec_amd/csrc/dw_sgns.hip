@@ -1400,18 +1400,21 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // The 64-walk batch's out rows are ~224K distinct rows of 1M, each read and written as p, m, v
 // (3 x 512 B): the catch-up -> pass 1 -> lazy gather sequence moved each across HBM twice and
 // read p a third time. Here one kernel does a row's whole out-side step where its p / m / v sit
-// in registers: replay its deferred g = 0 steps (to p^{s-1}), the logit of each of its records
-// against the record's centre row (pass 1's 16-lane layout and FMA order: the same bits), the
-// coefficient (row_coef, the loss sums), the gradient sum over its records in placed order (the
-// gather's order) and the Adam step. It leaves each record's coefficient in the high word of its
-// placed value and the row's p^{s-1} in p_prev[off[row]] for the centre pass
-// (dw_sgns_owner_pass1 with order_ready & 4, k_sgns_g16's COEFIN form).
-// A wave takes gch <= 64 placed records (lane = record) and its rows four at a time, one per
-// 16-lane group (lane gl holds elements [4gl + 64f, +4) of p, m, v: float4 loads), so four rows'
-// loads are in flight together. A row that straddles the chunk (its first or last row
-// continues in the neighbouring chunk) is replayed by each chunk that holds records of it (the
-// same bits), adds its part of the gradient to g_out with float atomics and is stepped by
-// k_lazy_boundary (full replay, p_current false).
+// in registers: replay its deferred g = 0 steps (dw::replay_g0, to p^{s-1}), the logit of each
+// of its records against the record's centre row (pass 1's 16-lane layout and FMA order, the
+// row staged in LDS: the same bits), the coefficient (row_coef, the loss sums), the gradient
+// sum over its records in placed order (the gather's order) and the Adam step. For the centre
+// pass (dw_sgns_owner_pass1 with order_ready & 4, k_sgns_g16's COEFIN form) it leaves, by slot,
+// each record's coefficient in coef_slot and its row's p^{s-1} in p_prev.
+// A wave takes gch <= 64 placed records (lane = record: slots and centre nodes looked up in one
+// round trip) and their rows one at a time, four records' centre rows in flight (one per 16-lane
+// group for the logits). A row that straddles the chunk (its first or last row continues in the
+// neighbouring chunk) is replayed by each chunk that holds records of it (the same bits), adds
+// its part of the gradient to g_out with float atomics and is stepped by k_lazy_boundary (full
+// replay, p_current false).
+// (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
+// ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
+// 138-VGPR kernel ran three waves per SIMD.)
 template <int F4>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
@@ -1419,8 +1422,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                float *__restrict__ g_out, float *__restrict__ p_prev,
                float *__restrict__ coef_slot) {
     constexpr int D = 64 * F4;
-    constexpr int E = 4 * F4;   // elements per lane
+    constexpr int RU = 4;   // records per round (one per 16-lane group)
     __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
+    __shared__ float4 s_p[WAVES_PER_BLOCK][D / 4];        // the row's p^{s-1}
+    __shared__ float4 s_c[WAVES_PER_BLOCK][RU][D / 4];    // the round's centre rows
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int q = lane >> 4, gl = lane & 15;
@@ -1429,12 +1434,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     const int64_t n_chunks = (n_rec + gch - 1) / gch;
     const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int32_t step = dw::eff_step(oa.dyn, oa.step_delta, oa.step);
-    const int32_t upto = step - 1;
     const dw::AdamScalars hs = dw::hist_at(oa.hist, step);
     const int32_t box_from = dw::hist_box_from(oa.hist);
-    const dw::const_float *hc = (const dw::const_float *)oa.hist;
     const int T = a.C * (1 + a.K), rpc = 1 + a.K;
     const int64_t per = a.L - 2 * a.R;
+    float *sp = reinterpret_cast<float *>(&s_p[wv][0]);
     float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
 
     for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
@@ -1443,13 +1447,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         const uint32_t before = e0 > 0 ? keys[e0 - 1] : 0xFFFFFFFFu;
         const uint32_t after = e0 + n_in < n_rec ? keys[e0 + n_in] : 0xFFFFFFFFu;
         const uint32_t my_key = lane < n_in ? keys[e0 + lane] : 0xFFFFFFFFu;
-        // lane = record: its slot s = b T + t and its centre node, all 64 in one round trip
+        // lane = record: its slot s = b T + t and its centre node, all of them in one round trip
         const uint32_t my_slot = lane < n_in ? static_cast<uint32_t>(vals[e0 + lane]) : 0u;
         const uint32_t my_b = my_slot / static_cast<uint32_t>(T);
         const uint32_t my_w = my_b / static_cast<uint32_t>(per);
-        const int32_t my_cid = lane < n_in
-            ? a.walks[static_cast<int64_t>(my_w) * a.L + a.R + (my_b - my_w * static_cast<uint32_t>(per))]
-            : -1;
+        const int32_t my_cid =
+            lane < n_in ? a.walks[static_cast<int64_t>(my_w) * a.L + a.R +
+                                  (my_b - my_w * static_cast<uint32_t>(per))]
+                        : -1;
         const uint32_t prev = __shfl_up(my_key, 1, WAVE);
         const bool is_start = lane < n_in && (lane == 0 || my_key != prev);
         const uint64_t starts = __ballot(is_start);
@@ -1457,159 +1462,85 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         if (is_start) s_rs[wv][__popcll(starts & lt)] = static_cast<uint8_t>(lane);
         if (lane == 0) s_rs[wv][nrows] = static_cast<uint8_t>(n_in);
         dw::wave_lds_sync();
-        for (int k0 = 0; k0 < nrows; k0 += 4) {
-            const int k = k0 + q;
-            const bool has = k < nrows;
-            const int rs = has ? s_rs[wv][k] : 0;
-            const int re = has ? s_rs[wv][k + 1] : 0;
-            const uint32_t row = __shfl(my_key, rs, WAVE);
-            const bool straddle = has && (row == before || row == after);
-            const int64_t ro = static_cast<int64_t>(has ? row : 0u) * D + 4 * gl;
-            const int32_t from = has ? oa.last[row] : upto;
-            float p[E], m[E], v[E];
-            auto load_row = [&]() {
+        for (int k = 0; k < nrows; ++k) {
+            const int rs = s_rs[wv][k], re = s_rs[wv][k + 1];   // (wave-uniform)
+            const uint32_t row = __builtin_amdgcn_readlane(my_key, rs);
+            const bool straddle = row == before || row == after;
+            const int64_t ro = static_cast<int64_t>(row) * D + lane;
+            const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
+            float p[F4], m[F4], v[F4], g[F4];
+#pragma unroll
+            for (int f = 0; f < F4; ++f) {
+                p[f] = oa.p[ro + 64 * f];
+                m[f] = oa.m[ro + 64 * f];
+                v[f] = oa.v[ro + 64 * f];
+                g[f] = 0.f;
+            }
+            dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
+#pragma unroll
+            for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
+            dw::wave_lds_sync();
+            const int cnt = re - rs;
+            for (int j0 = 0; j0 < cnt; j0 += RU) {
+                // group q: record j0 + q's logit in pass 1's layout (lane gl: elements
+                // [4gl + 64f, +4)) and coefficient
+                const int src = (rs + j0 + q) & (WAVE - 1);
+                const bool in = j0 + q < cnt;
+                const uint32_t slot = __shfl(my_slot, src, WAVE);
+                const int32_t cid = __shfl(my_cid, src, WAVE);
+                const bool ok = in && cid >= 0 && cid < a.V;
+                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+                float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
-                    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-                    const float4 pf = has ? *reinterpret_cast<const float4 *>(oa.p + ro + 64 * f) : z;
-                    const float4 mf = has ? *reinterpret_cast<const float4 *>(oa.m + ro + 64 * f) : z;
-                    const float4 vf = has ? *reinterpret_cast<const float4 *>(oa.v + ro + 64 * f) : z;
-                    p[4 * f] = pf.x; p[4 * f + 1] = pf.y; p[4 * f + 2] = pf.z; p[4 * f + 3] = pf.w;
-                    m[4 * f] = mf.x; m[4 * f + 1] = mf.y; m[4 * f + 2] = mf.z; m[4 * f + 3] = mf.w;
-                    v[4 * f] = vf.x; v[4 * f + 1] = vf.y; v[4 * f + 2] = vf.z; v[4 * f + 3] = vf.w;
+                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 of = s_p[wv][gl + 16 * f];
+                    pr = fmaf(cf.x, of.x, pr);
+                    pr = fmaf(cf.y, of.y, pr);
+                    pr = fmaf(cf.z, of.z, pr);
+                    pr = fmaf(cf.w, of.w, pr);
+                    s_c[wv][q][gl + 16 * f] = cf;
                 }
-            };
-            load_row();
-            // the deferred g = 0 steps, each group its own (from, upto]: the box forms while the
-            // whole wave's run stays in the box (dw::replay_g0's rule), else the scaled forms
-            {
-                const int32_t f0 = __builtin_amdgcn_readlane(from, 0);
-                const int32_t f1 = __builtin_amdgcn_readlane(from, 16);
-                const int32_t f2 = __builtin_amdgcn_readlane(from, 32);
-                const int32_t f3 = __builtin_amdgcn_readlane(from, 48);
-                const int32_t lo = min(min(f0, f1), min(f2, f3));
-                if (lo < upto) {
-                    bool fast = lo + 1 >= box_from;
-                    uint64_t zero = 0;   // bit e: m started +0; bit E + e: v started +0
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        fast = fast && v[e] <= 0x1p20f && fabsf(m[e]) <= 0x1p60f;
-                        zero |= (__float_as_uint(m[e]) == 0u ? 1ull : 0ull) << e;
-                        zero |= (__float_as_uint(v[e]) == 0u ? 1ull : 0ull) << (E + e);
-                    }
-                    if (__all(fast)) {
-                        for (int32_t s = lo + 1; s <= upto; ++s) {
-                            const dw::AdamScalars h = dw::hist_at_const(hc + 8 * static_cast<int64_t>(s));
-                            if (from < s) {
-#pragma unroll
-                                for (int e = 0; e < E; ++e) dw::adam_elem_g0_box(p[e], m[e], v[e], h);
-                            }
-                        }
-                        bool end = true;
-#pragma unroll
-                        for (int e = 0; e < E; ++e)
-                            end = end && (((zero >> (E + e)) & 1ull) || v[e] >= 0x1p-96f) &&
-                                  (((zero >> e) & 1ull) || fabsf(m[e]) >= 0x1p-100f);
-                        fast = __all(end);
-                        if (!fast) load_row();   // (the table is untouched: start again)
-                    }
-                    if (!fast) {
-                        for (int32_t s = lo + 1; s <= upto; ++s) {
-                            const dw::AdamScalars h = dw::hist_at(oa.hist, s);
-                            if (from >= s) continue;
-                            if (h.wd == 0.f) {
-#pragma unroll
-                                for (int e = 0; e < E; ++e) dw::adam_elem_g0(p[e], m[e], v[e], h);
-                            } else {
-#pragma unroll
-                                for (int e = 0; e < E; ++e) {
-                                    float z = 0.f;
-                                    dw::adam_elem(p[e], z, m[e], v[e], h);
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-            // the row's records in placed order: logit, coefficient, gradient sum; RU records'
-            // centre rows in flight at a time (a hub row holds hundreds of a chunk's records)
-            const int cnt = re - rs;
-            const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
-            const int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
-            const int nmax = max(max(c0, c1), max(c2, c3));
-            float g[E];
-#pragma unroll
-            for (int e = 0; e < E; ++e) g[e] = 0.f;
-            constexpr int RU = 4;
-            for (int j0 = 0; j0 < nmax; j0 += RU) {
-                float c[RU][E];
-                uint32_t slot[RU];
-                bool ok[RU];
+                const float x = row_sum16(pr);
+                const int t = static_cast<int>(slot % static_cast<uint32_t>(T));
+                float coef = 0.f;
+                if (ok && gl == 0)
+                    coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec,
+                                    acc_prec);
+                if (in && gl == 0) coef_slot[slot] = coef;
+                dw::wave_lds_sync();
+                // the gradient over the round's records in placed order (lane-strided elements,
+                // the gather's accumulation), and each record's copy of p^{s-1}
 #pragma unroll
                 for (int u = 0; u < RU; ++u) {
-                    const int src = rs + j0 + u;
-                    const bool in = has && j0 + u < cnt;
-                    slot[u] = __shfl(my_slot, src & 63, WAVE);
-                    const int32_t cid = __shfl(my_cid, src & 63, WAVE);
-                    ok[u] = in && cid >= 0 && cid < a.V;
-                    const float *crow = a.w_in + static_cast<int64_t>(ok[u] ? cid : 0) * D + 4 * gl;
+                    if (j0 + u >= cnt) break;
+                    const float cu = __shfl(coef, u << 4, WAVE);
+                    const uint32_t su = __shfl(slot, u << 4, WAVE);
+                    const float *cr = reinterpret_cast<const float *>(&s_c[wv][u][0]);
+                    float *pv = p_prev + static_cast<int64_t>(su) * D + lane;
 #pragma unroll
                     for (int f = 0; f < F4; ++f) {
-                        const float4 cf = ok[u] ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
-                        c[u][4 * f] = cf.x; c[u][4 * f + 1] = cf.y;
-                        c[u][4 * f + 2] = cf.z; c[u][4 * f + 3] = cf.w;
+                        g[f] += cu * cr[lane + 64 * f];
+                        pv[64 * f] = p[f];
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < RU; ++u) {
-                    if (j0 + u >= nmax) break;
-                    const bool in = has && j0 + u < cnt;
-                    float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
-#pragma unroll
-                    for (int e = 0; e < E; ++e) pr = fmaf(c[u][e], p[e], pr);
-                    const float x = row_sum16(pr);
-                    const int t = static_cast<int>(slot[u] % static_cast<uint32_t>(T));
-                    float coef = 0.f;
-                    if (ok[u] && gl == 0)
-                        coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec,
-                                        acc_prec);
-                    coef = __shfl(coef, q << 4, WAVE);
-#pragma unroll
-                    for (int e = 0; e < E; ++e) g[e] += coef * c[u][e];
-                    if (in) {   // the centre pass's inputs, by slot
-                        if (gl == 0) coef_slot[slot[u]] = coef;
-                        float *pv = p_prev + static_cast<int64_t>(slot[u]) * D + 4 * gl;
-#pragma unroll
-                        for (int f = 0; f < F4; ++f)
-                            *reinterpret_cast<float4 *>(pv + 64 * f) =
-                                make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
-                    }
-                }
+                dw::wave_lds_sync();   // s_c is rewritten next round
             }
-            if (has) {
-                if (straddle) {
-                    float *dst = g_out + ro;
+            if (straddle) {
 #pragma unroll
-                    for (int f = 0; f < F4; ++f)
+                for (int f = 0; f < F4; ++f) atomicAdd(g_out + ro + 64 * f, g[f]);
+            } else {
 #pragma unroll
-                        for (int cpt = 0; cpt < 4; ++cpt) atomicAdd(dst + 64 * f + cpt, g[4 * f + cpt]);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < E; ++e) dw::adam_elem(p[e], g[e], m[e], v[e], hs);
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) {
-                        *reinterpret_cast<float4 *>(oa.p + ro + 64 * f) =
-                            make_float4(p[4 * f], p[4 * f + 1], p[4 * f + 2], p[4 * f + 3]);
-                        *reinterpret_cast<float4 *>(oa.m + ro + 64 * f) =
-                            make_float4(m[4 * f], m[4 * f + 1], m[4 * f + 2], m[4 * f + 3]);
-                        *reinterpret_cast<float4 *>(oa.v + ro + 64 * f) =
-                            make_float4(v[4 * f], v[4 * f + 1], v[4 * f + 2], v[4 * f + 3]);
-                    }
-                    if (gl == 0) {
-                        oa.last[row] = step;
-                        if (oa.counts) oa.counts[row] = 0u;
-                    }
+                for (int f = 0; f < F4; ++f) {
+                    dw::adam_elem(p[f], g[f], m[f], v[f], hs);
+                    oa.p[ro + 64 * f] = p[f];
+                    oa.m[ro + 64 * f] = m[f];
+                    oa.v[ro + 64 * f] = v[f];
+                }
+                if (lane == 0) {
+                    oa.last[row] = step;
+                    if (oa.counts) oa.counts[row] = 0u;
                 }
             }
         }
