@@ -1415,13 +1415,11 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
 // ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
 // 138-VGPR kernel ran three waves per SIMD.)
-// (waves per SIMD the register allocation must allow where the rows are 64 or 128 wide: the
-// kernel is latency-bound, a row or two in flight per wave)
 #ifndef DW_ROWS_MIN_WAVES
-#define DW_ROWS_MIN_WAVES 5
+#define DW_ROWS_MIN_WAVES 8   // waves per SIMD the register allocation must allow
 #endif
 template <int F4>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? DW_ROWS_MIN_WAVES : 2)
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, DW_ROWS_MIN_WAVES)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
                float *__restrict__ g_out, float *__restrict__ p_prev,
