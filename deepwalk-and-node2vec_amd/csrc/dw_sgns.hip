@@ -1465,84 +1465,45 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, DW_ROWS_MIN_WAVES)
         if (is_start) s_rs[wv][__popcll(starts & lt)] = static_cast<uint8_t>(lane);
         if (lane == 0) s_rs[wv][nrows] = static_cast<uint8_t>(n_in);
         dw::wave_lds_sync();
-        // software-pipelined over the chunk's rows: row k + 1's p, m, v loads are issued after
-        // row k's first round of centre rows and before its replay, so they are in flight while
-        // row k computes (vector loads return in order: issued before the centre rows, a wait
-        // for those would wait for them too)
-        uint32_t row_n = 0;
-        int32_t from_n = 0;
-        float pn[F4], mn[F4], vn[F4];
-        auto load_row = [&](int kk) {
-            row_n = __builtin_amdgcn_readlane(my_key, s_rs[wv][kk]);
-            from_n = __builtin_amdgcn_readfirstlane(oa.last[row_n]);
-            const int64_t rn = static_cast<int64_t>(row_n) * D + lane;
-#pragma unroll
-            for (int f = 0; f < F4; ++f) {
-                pn[f] = oa.p[rn + 64 * f];
-                mn[f] = oa.m[rn + 64 * f];
-                vn[f] = oa.v[rn + 64 * f];
-            }
-        };
-        // group q's record j0 + q of the row starting at rs: slot, centre row (pass 1's layout)
-        auto load_rec = [&](int rs, int cnt, int j0, uint32_t &slot, bool &in, bool &ok,
-                            float4 (&cf)[F4]) {
-            const int src = (rs + j0 + q) & (WAVE - 1);
-            in = j0 + q < cnt;
-            slot = __shfl(my_slot, src, WAVE);
-            const int32_t cid = __shfl(my_cid, src, WAVE);
-            ok = in && cid >= 0 && cid < a.V;
-            const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
-#pragma unroll
-            for (int f = 0; f < F4; ++f)
-                cf[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-        };
-        if (nrows > 0) load_row(0);
         for (int k = 0; k < nrows; ++k) {
             const int rs = s_rs[wv][k], re = s_rs[wv][k + 1];   // (wave-uniform)
-            const int cnt = re - rs;
-            const uint32_t row = row_n;
-            const int32_t from = from_n;
+            const uint32_t row = __builtin_amdgcn_readlane(my_key, rs);
             const bool straddle = row == before || row == after;
             const int64_t ro = static_cast<int64_t>(row) * D + lane;
+            const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
             float p[F4], m[F4], v[F4], g[F4];
 #pragma unroll
             for (int f = 0; f < F4; ++f) {
-                p[f] = pn[f];
-                m[f] = mn[f];
-                v[f] = vn[f];
+                p[f] = oa.p[ro + 64 * f];
+                m[f] = oa.m[ro + 64 * f];
+                v[f] = oa.v[ro + 64 * f];
                 g[f] = 0.f;
             }
-            uint32_t slot0;
-            bool in0, ok0;
-            float4 cf0[F4];
-            load_rec(rs, cnt, 0, slot0, in0, ok0, cf0);
-            if (k + 1 < nrows) load_row(k + 1);
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
             for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
             dw::wave_lds_sync();
+            const int cnt = re - rs;
             for (int j0 = 0; j0 < cnt; j0 += RU) {
-                uint32_t slot = slot0;
-                bool in = in0, ok = ok0;
-                float4 cf[F4];
-                if (j0 == 0) {
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) cf[f] = cf0[f];
-                } else {
-                    load_rec(rs, cnt, j0, slot, in, ok, cf);
-                }
-                // group q: record j0 + q's logit in pass 1's order (x, y, z, w of each float4,
-                // then the DPP sum) and coefficient
-                float pr = 0.f;
+                // group q: record j0 + q's logit in pass 1's layout (lane gl: elements
+                // [4gl + 64f, +4)) and coefficient
+                const int src = (rs + j0 + q) & (WAVE - 1);
+                const bool in = j0 + q < cnt;
+                const uint32_t slot = __shfl(my_slot, src, WAVE);
+                const int32_t cid = __shfl(my_cid, src, WAVE);
+                const bool ok = in && cid >= 0 && cid < a.V;
+                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+                float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
+                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
                     const float4 of = s_p[wv][gl + 16 * f];
-                    pr = fmaf(cf[f].x, of.x, pr);
-                    pr = fmaf(cf[f].y, of.y, pr);
-                    pr = fmaf(cf[f].z, of.z, pr);
-                    pr = fmaf(cf[f].w, of.w, pr);
-                    s_c[wv][q][gl + 16 * f] = cf[f];
+                    pr = fmaf(cf.x, of.x, pr);
+                    pr = fmaf(cf.y, of.y, pr);
+                    pr = fmaf(cf.z, of.z, pr);
+                    pr = fmaf(cf.w, of.w, pr);
+                    s_c[wv][q][gl + 16 * f] = cf;
                 }
                 const float x = row_sum16(pr);
                 const int t = static_cast<int>(slot % static_cast<uint32_t>(T));
