@@ -1415,11 +1415,12 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
 // ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
 // 138-VGPR kernel ran three waves per SIMD.)
-#ifndef DW_ROWS_MIN_WAVES
-#define DW_ROWS_MIN_WAVES 8   // waves per SIMD the register allocation must allow
-#endif
+// The kernel is latency-bound — a row's load, replay, centre rows and step in sequence, one
+// row in flight per wave — so at d <= 128 the register allocation is held to eight waves per
+// SIMD (276 us at C3's 64-walk batch; 296 us at five waves unbounded; the next row's loads
+// issued ahead of the replay measured 279-306 us at five to eight waves).
 template <int F4>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, DW_ROWS_MIN_WAVES)
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
                float *__restrict__ g_out, float *__restrict__ p_prev,
