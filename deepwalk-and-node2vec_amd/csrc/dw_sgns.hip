@@ -1243,15 +1243,11 @@ int launch_pass1(const SgnsArgs &a, hipStream_t st) {
 }
 
 // 16-lane-group pass 1 when d is a multiple of 64 (<= 512) and 2R(1+K) <= 64; otherwise
-// DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns). DW_SGNS_G16=0 disables it.
+// DW_E_UNSUPPORTED (the caller falls back to the 64-lane k_sgns).
 template <bool FROM_WALKS, bool OWNER = false, bool COEFIN = false>
 int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
-    static const bool enabled = [] {
-        const char *e = getenv("DW_SGNS_G16");
-        return !(e && e[0] == '0');
-    }();
     const int64_t T = (int64_t)a.C * (1 + a.K);
-    if (!enabled || a.d % 64 != 0 || a.d > 512 || T > G16_TMAX) return DW_E_UNSUPPORTED;
+    if (a.d % 64 != 0 || a.d > 512 || T > G16_TMAX) return DW_E_UNSUPPORTED;
     int64_t blocks = (a.batch + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
@@ -1617,12 +1613,8 @@ int launch_pass2(const uint32_t *keys, const uint64_t *vals, int64_t n_rec, cons
     // chunk size: GCH for large batches (balanced, few boundary rows); halved down to 32 while
     // the chunks would not give every SIMD of the chip a few waves — a 9K-record batch (C2 shape)
     // in 512-record chunks ran as 18 waves, 240 us of latency-bound gathers
-    static const int32_t gch0 = [] {   // DW_GCH: records per chunk, for tuning sweeps only
-        const char *e = getenv("DW_GCH");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 32 && v <= 8192) ? v : GCH;
-    }();
-    int32_t gch = gch0;
+    // (scripts/experiments/gch_sweep.sh measured the sizes)
+    int32_t gch = GCH;
     {
         const int64_t want = grid_cap(16);   // 4 waves per SIMD
         while (gch > 32 && (n_rec + gch - 1) / gch < want) gch >>= 1;
@@ -3090,12 +3082,7 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     // records per chunk (<= 64: one per lane): 64, halved to 32 while the chunks would not give
     // every SIMD of the chip eight waves
     const int64_t bound = n_centres * T;
-    static const int32_t gch_env = [] {   // DW_ROWS_GCH: tuning sweeps only
-        const char *e = getenv("DW_ROWS_GCH");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 8 && v <= 64) ? v : 0;
-    }();
-    int32_t gch = gch_env ? gch_env : (bound / 64 < grid_cap(32) ? 32 : 64);
+    const int32_t gch = bound / 64 < grid_cap(32) ? 32 : 64;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;

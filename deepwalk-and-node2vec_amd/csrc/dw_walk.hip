@@ -1946,18 +1946,13 @@ int launch_node2vec(const int64_t *row_ptr, const int32_t *col, const int32_t *n
     // latency-bound, so a batch that fits on the chip at 16 lanes per walker (fewer blocks of
     // proposals per step) runs at 16, one that fits at 8 at 8, a larger one at 4 (the most
     // walkers in flight). Measured at C3, 1M walks: G=4 116M, G=8 101M, G=16 79M walks/s;
-    // 8,192 walks: 17M / 27M / 32M. DW_N2V_GROUP=4|8|16 forces a size.
-    static const int forced = [] {
-        const char *e = getenv("DW_N2V_GROUP");
-        const int g = e ? atoi(e) : 0;
-        return (g == 4 || g == 8 || g == 16) ? g : 0;
-    }();
+    // 8,192 walks: 17M / 27M / 32M.
     // resident walkers at 16 and 8 lanes (occupancy query once per process: one GPU model)
     static const int64_t cap16 = node2vec_capacity(
         reinterpret_cast<const void *>(&k_walk_node2vec_fast<16, HASH, false>), 16);
     static const int64_t cap8 = node2vec_capacity(
         reinterpret_cast<const void *>(&k_walk_node2vec_fast<8, HASH, false>), 8);
-    const int group = forced ? forced : n_walks <= cap16 ? 16 : n_walks <= cap8 ? 8 : 4;
+    const int group = n_walks <= cap16 ? 16 : n_walks <= cap8 ? 8 : 4;
     const int64_t per_block = N2V_WAVES * (WAVE / group);
     int64_t blocks = (n_walks + per_block - 1) / per_block;
     if (blocks > 8192) blocks = 8192;
@@ -2073,15 +2068,11 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
                               stream);
     int64_t blocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
     if (blocks > 16384) blocks = 16384;
-    // N(prev) mapped into N(v) when deg(v) > b_factor deg(prev); DW_N2V_BFACTOR overrides.
-    // With the per-edge class counts a classification scans ~deg(v)/4 entries, so the mapping
-    // pays only for a much shorter N(prev): 64 (C3, 65,536 walks: 14.5 ms at 16, 13.5 at 64,
-    // 13.6 at 256, 17.8 at 4); without the counts 16 (scripts/gpu_n2v_cn.sh)
-    const int32_t b_factor = [edge_cn] {
-        const char *e = getenv("DW_N2V_BFACTOR");
-        const int f = e ? atoi(e) : 0;
-        return f > 0 ? f : (edge_cn ? 64 : 16);
-    }();
+    // N(prev) mapped into N(v) when deg(v) > b_factor deg(prev). With the per-edge class counts
+    // a classification scans ~deg(v)/4 entries, so the mapping pays only for a much shorter
+    // N(prev): 64 (C3, 65,536 walks: 14.5 ms at 16, 13.5 at 64, 13.6 at 256, 17.8 at 4);
+    // without the counts 16 (scripts/gpu_n2v_cn.sh, measured with a factor override since removed)
+    const int32_t b_factor = edge_cn ? 64 : 16;
     DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
                "dw_walk_replay_indexed: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
     const N2VIndex ix{adj_off, adj_hash, adj_hpos, b_factor,

@@ -163,9 +163,6 @@ def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> in
     (0 = full grid, when no estimate is given)."""
     if not overlap_bytes:
         return 0
-    forced = int(os.environ.get('DW_OVERLAP_BLOCKS', '0') or 0)   # (tuning sweeps only)
-    if forced > 0:
-        return forced
     t = overlap_bytes / OVERLAP_PHASE_BPS
     need = OVERLAP_MARGIN * adam_bytes / t / ADAM_BLOCK_BPS
     return int(min(8192, max(32, math.ceil(need))))
@@ -881,13 +878,13 @@ class OwnerLazyTables(OwnerTables):
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
         # one rank: the records placed by the claim (no sort before the lazy gather)
-        self.place = (self.lazy_out and not self.multi
-                      and os.environ.get('DW_OUT_PLACE', '1') != '0')   # (A/B, round 4)
+        self.place = self.lazy_out and not self.multi
         # any step with weight decay: the p-only catch-up no longer holds
-        self._wd_seen = os.environ.get('DW_OUT_P_ONLY', '1') == '0'   # (A/B, round 4)
+        self._wd_seen = False
         # placed records: the rows-major step (dw_sgns_owner_out_rows) reads and writes each
-        # touched out row once; the catch-up -> pass 1 -> lazy gather sequence otherwise
-        self.rows_major = self.place and os.environ.get('DW_OUT_ROWS', '1') != '0'
+        # touched out row once; the catch-up -> pass 1 -> lazy gather sequence otherwise (the
+        # tests set these attributes to compare the forms)
+        self.rows_major = self.place
         self._p_prev = None        # [slots, d]: the rows' pre-step values for the centre pass
         self._rows_step = False    # this step goes rows-major (set by catch_up_out)
 
