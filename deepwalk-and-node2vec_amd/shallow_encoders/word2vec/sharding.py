@@ -804,7 +804,8 @@ def owner_step(tables: 'OwnerTables', walks: torch.Tensor, context_radius: int,
                          context_radius=context_radius, out_adam=spec, status=status,
                          read_count=tables.world > 1)
     if n is None:   # one owner keeps every slot (no count readback)
-        n = slots
+        n = walks.shape[0] * (walks.shape[1] - 2 * context_radius) * 2 * context_radius * (
+            1 + neg_samples)
     if spec is None:
         tables.out_step()
     tables.sync()
