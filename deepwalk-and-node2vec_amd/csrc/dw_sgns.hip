@@ -1476,25 +1476,44 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
                 v[f] = oa.v[ro + 64 * f];
                 g[f] = 0.f;
             }
+            const int cnt = re - rs;
+            // group q: record j0 + q's slot, centre and centre row in pass 1's layout (lane gl:
+            // elements [4gl + 64f, +4)); the first round's rows are loaded with the row's own,
+            // ahead of the replay
+            auto load_rec = [&](int j0, uint32_t &slot, bool &in, bool &ok, float4 (&cf)[F4]) {
+                const int src = (rs + j0 + q) & (WAVE - 1);
+                in = j0 + q < cnt;
+                slot = __shfl(my_slot, src, WAVE);
+                const int32_t cid = __shfl(my_cid, src, WAVE);
+                ok = in && cid >= 0 && cid < a.V;
+                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+                    cf[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            };
+            uint32_t slot0;
+            bool in0, ok0;
+            float4 cf0[F4];
+            load_rec(0, slot0, in0, ok0, cf0);
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
             for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
             dw::wave_lds_sync();
-            const int cnt = re - rs;
             for (int j0 = 0; j0 < cnt; j0 += RU) {
-                // group q: record j0 + q's logit in pass 1's layout (lane gl: elements
-                // [4gl + 64f, +4)) and coefficient
-                const int src = (rs + j0 + q) & (WAVE - 1);
-                const bool in = j0 + q < cnt;
-                const uint32_t slot = __shfl(my_slot, src, WAVE);
-                const int32_t cid = __shfl(my_cid, src, WAVE);
-                const bool ok = in && cid >= 0 && cid < a.V;
-                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+                uint32_t slot = slot0;
+                bool in = in0, ok = ok0;
+                float4 cfr[F4];
+                if (j0 == 0) {
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) cfr[f] = cf0[f];
+                } else {
+                    load_rec(j0, slot, in, ok, cfr);
+                }
                 float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
-                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 cf = cfr[f];
                     const float4 of = s_p[wv][gl + 16 * f];
                     pr = fmaf(cf.x, of.x, pr);
                     pr = fmaf(cf.y, of.y, pr);
@@ -2476,7 +2495,8 @@ template <bool CLAIM>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
-                uint32_t *__restrict__ count, uint32_t *__restrict__ rank) {
+                uint32_t *__restrict__ count, uint32_t *__restrict__ rank,
+                uint32_t *__restrict__ rowid) {
     const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
     __shared__ uint32_t s_rows[WAVES_PER_BLOCK][CLAIM_TRIPS * WAVE];
     __shared__ uint32_t s_cnt[WAVES_PER_BLOCK];
@@ -2511,6 +2531,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                 if (CLAIM) mine[k] = atomicMax(claim + o[k], step) < step - 1;
                 if (count) rank[b * T + lane] = atomicAdd(count + o[k], 1u);
             }
+            if (!CLAIM) {   // every slot's local row (~0: none) for k_place_slots
+                const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
+                if (b < a.batch && lane < T)
+                    rowid[b * T + lane] = o[k] >= 0 ? static_cast<uint32_t>(o[k]) : 0xFFFFFFFFu;
+            }
         }
         if constexpr (!CLAIM) continue;
         uint32_t n_mine = 0;   // wave-uniform
@@ -2536,23 +2561,16 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 }
 
 // The rows-major step, after the placement scan: slot s = b T + t (k_out_claim gave it its
-// rank among its row's slots) goes to off[row] + rank[s] — keys[pos] = the local row, vals[pos]
-// = s (k_out_rows adds the coefficient in the high word). The row ids are drawn again (Philox
-// for the negatives, the walk for the contexts), as pass 1 draws them.
+// local row rowid[s] and its rank among that row's slots) goes to off[row] + rank[s] —
+// keys[pos] = the row, vals[pos] = s.
 __global__ void __launch_bounds__(256)
-    k_place_slots(SgnsArgs a, const uint32_t *__restrict__ rank, const uint32_t *__restrict__ off,
+    k_place_slots(int64_t n_slots, const uint32_t *__restrict__ rowid,
+                  const uint32_t *__restrict__ rank, const uint32_t *__restrict__ off,
                   uint32_t *__restrict__ keys, uint64_t *__restrict__ vals) {
-    const int T = a.C * (1 + a.K);
-    const int64_t per = a.L - 2 * a.R;
-    const int64_t n = a.batch * T;
-    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n;
+    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n_slots;
          s += (int64_t)gridDim.x * 256) {
-        const int64_t b = s / T;
-        const int t = static_cast<int>(s - b * T);
-        const int64_t w = b / per, i = a.R + (b - w * per);
-        const int64_t r = row_id<true>(a, b, a.walks + w * a.L, i, t);
-        if (r < 0 || r >= a.V || r % a.n_owners != a.owner) continue;   // (counted by the claim)
-        const uint32_t o = static_cast<uint32_t>(r / a.n_owners);
+        const uint32_t o = rowid[s];
+        if (o == 0xFFFFFFFFu) continue;   // a bad id or another owner's row
         const uint32_t pos = off[o] + rank[s];
         keys[pos] = o;
         vals[pos] = static_cast<uint64_t>(s);
@@ -2671,7 +2689,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     a.C = 2 * context_radius;
     a.owner = owner;
     a.n_owners = n_owners;
-    if (hipMemsetAsync(n_rows, 0, sizeof(int64_t), st) != hipSuccess) {
+    if (!(flags & 4) && hipMemsetAsync(n_rows, 0, sizeof(int64_t), st) != hipSuccess) {
         dw::set_error("dw_sgns_owner_out_catch_up: counter reset failed");
         return DW_E_HIP;
     }
@@ -2688,15 +2706,17 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     int64_t blocks = (a.batch + ctile - 1) / ctile;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
+    // (rows-major: every slot's row into the records' spare key buffer, k0)
     if (rows_major)
         hipLaunchKernelGGL(k_out_claim<false>, dim3((unsigned)blocks),
                            dim3(WAVES_PER_BLOCK * WAVE), 0, st, a, claim, step, delta, rows_buf,
-                           reinterpret_cast<unsigned long long *>(n_rows), counts, pl.rank);
+                           reinterpret_cast<unsigned long long *>(n_rows), counts, pl.rank,
+                           ws.k0);
     else
         hipLaunchKernelGGL(k_out_claim<true>, dim3((unsigned)blocks),
                            dim3(WAVES_PER_BLOCK * WAVE), 0, st, a, claim, step, delta, rows_buf,
                            reinterpret_cast<unsigned long long *>(n_rows),
-                           place ? counts : nullptr, place ? pl.rank : nullptr);
+                           place ? counts : nullptr, place ? pl.rank : nullptr, nullptr);
     DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/claim");
     if (place) {   // every row's segment of the records: the scan of the counts (+ the total)
         const int64_t nb = (local_rows + PLACE_TILE - 1) / PLACE_TILE;
@@ -2712,8 +2732,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
         int64_t pb = (a.batch * T + 255) / 256;
         if (pb > grid_cap(8)) pb = grid_cap(8);
         if (pb < 1) pb = 1;
-        hipLaunchKernelGGL(k_place_slots, dim3((unsigned)pb), dim3(256), 0, st, a, pl.rank, pl.off,
-                           ws.k1, ws.v1);
+        hipLaunchKernelGGL(k_place_slots, dim3((unsigned)pb), dim3(256), 0, st, a.batch * T,
+                           ws.k0, pl.rank, pl.off, ws.k1, ws.v1);
         DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place_slots");
         return DW_OK;
     }
