@@ -1476,44 +1476,26 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
                 v[f] = oa.v[ro + 64 * f];
                 g[f] = 0.f;
             }
-            const int cnt = re - rs;
-            // group q: record j0 + q's slot, centre and centre row in pass 1's layout (lane gl:
-            // elements [4gl + 64f, +4)); the first round's rows are loaded with the row's own,
-            // ahead of the replay
-            auto load_rec = [&](int j0, uint32_t &slot, bool &in, bool &ok, float4 (&cf)[F4]) {
-                const int src = (rs + j0 + q) & (WAVE - 1);
-                in = j0 + q < cnt;
-                slot = __shfl(my_slot, src, WAVE);
-                const int32_t cid = __shfl(my_cid, src, WAVE);
-                ok = in && cid >= 0 && cid < a.V;
-                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
-#pragma unroll
-                for (int f = 0; f < F4; ++f)
-                    cf[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-            };
-            uint32_t slot0;
-            bool in0, ok0;
-            float4 cf0[F4];
-            load_rec(0, slot0, in0, ok0, cf0);
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
             for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
             dw::wave_lds_sync();
+            const int cnt = re - rs;
             for (int j0 = 0; j0 < cnt; j0 += RU) {
-                uint32_t slot = slot0;
-                bool in = in0, ok = ok0;
-                float4 cfr[F4];
-                if (j0 == 0) {
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) cfr[f] = cf0[f];
-                } else {
-                    load_rec(j0, slot, in, ok, cfr);
-                }
+                // group q: record j0 + q's logit in pass 1's layout (lane gl: elements
+                // [4gl + 64f, +4)) and coefficient (the first round's centre rows loaded with
+                // the row's own, ahead of the replay, measured 300 vs 276 us: more spills)
+                const int src = (rs + j0 + q) & (WAVE - 1);
+                const bool in = j0 + q < cnt;
+                const uint32_t slot = __shfl(my_slot, src, WAVE);
+                const int32_t cid = __shfl(my_cid, src, WAVE);
+                const bool ok = in && cid >= 0 && cid < a.V;
+                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
                 float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
-                    const float4 cf = cfr[f];
+                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
                     const float4 of = s_p[wv][gl + 16 * f];
                     pr = fmaf(cf.x, of.x, pr);
                     pr = fmaf(cf.y, of.y, pr);
