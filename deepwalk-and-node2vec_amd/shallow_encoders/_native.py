@@ -37,7 +37,7 @@ DW_EXACT_DEFER = 1
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
