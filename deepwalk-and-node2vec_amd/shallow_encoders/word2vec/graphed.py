@@ -275,18 +275,11 @@ class GraphedOwnerStep:
                                status=self.status)
         for k in range(self.unroll):
             # the step numbers the lazy kernels get are relative to block k's (begin_step, inside
-            # owner_lazy_step, makes the host's count step_count + 1); the rows-major claim of
-            # step k + 1 runs inside step k, with block k + 1 bound while it is launched
+            # owner_lazy_step, makes the host's count step_count + 1)
             _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count + 1)
-            nxt = self.walks[(k + 1) * B:(k + 2) * B] if k + 1 < self.unroll else None
-            owner_lazy_step(
-                t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
-                noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
-                status=self.status, next_walks=nxt, next_noise_offset=0,
-                bind_next=lambda k=k: _native.call('dw_step_scalars_bind_at',
-                                                   self._step_blk(k + 1), t.step_count + 1),
-                rebind=lambda k=k: _native.call('dw_step_scalars_bind_at', self._step_blk(k),
-                                                t.step_count))
+            owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
+                            noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
+                            status=self.status)
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host

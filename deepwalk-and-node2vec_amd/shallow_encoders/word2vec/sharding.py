@@ -888,11 +888,6 @@ class OwnerLazyTables(OwnerTables):
         self.rows_major = self.place
         self._p_prev = None        # [slots, d]: the rows' pre-step values for the centre pass
         self._rows_step = False    # this step goes rows-major (set by catch_up_out)
-        # the next step's rows-major claim, issued during this step (claim_ahead): its key
-        # (walks pointer, noise offset, step) and completion event
-        self._ahead = None
-        self._side_ahead = (torch.cuda.Stream(self.device)
-                            if self.lazy_out and self._cuda else None)
 
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
         """The rows-major step applies: placed records, d a multiple of 64 (<= 512),
@@ -923,14 +918,6 @@ class OwnerLazyTables(OwnerTables):
         step = self.step_count if step is None else int(step)
         n, L = walks.shape
         R, K = int(context_radius), int(neg_samples)
-        if self._ahead is not None:   # claimed during the previous step (claim_ahead)
-            ptr, off, st, done = self._ahead
-            self._ahead = None
-            if (ptr, off, st) != (walks.data_ptr(), int(noise_offset), step):
-                raise RuntimeError('OwnerLazyTables: the step claimed ahead was for other walks')
-            torch.cuda.current_stream(self.device).wait_event(done)
-            self._rows_step = True
-            return
         slots = n * (L - 2 * R) * 2 * R * (1 + K)
         cap = max(1, min(self.S, slots))
         if self._out_rows is None or self._out_rows.numel() < cap:
@@ -949,23 +936,6 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
                          flags, _native.ptr(status), _native.ptr(ws), ws.numel(),
                          _native.stream(self.device))
-
-    def claim_ahead(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
-                    seed: int, noise_offset: int, status: torch.Tensor, step: int) -> None:
-        """The rows-major claim of the NEXT step's batch ``walks`` (Adam step ``step``), on a
-        side stream forked here — after this step's out rows were stepped (they clear the
-        counts the claim adds to), beside this step's centre pass and in-table update, which
-        read none of the placement buffers. The next catch_up_out then only waits for it."""
-        main = torch.cuda.current_stream(self.device)
-        fork = torch.cuda.Event()
-        fork.record(main)
-        with torch.cuda.stream(self._side_ahead):
-            self._side_ahead.wait_event(fork)
-            self.catch_up_out(walks, context_radius, neg_samples, seed, noise_offset, status,
-                              step=step)
-            done = torch.cuda.Event()
-            done.record(self._side_ahead)
-        self._ahead = (walks.data_ptr(), int(noise_offset), int(step), done)
 
     def out_rows_step(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                       seed: int, noise_offset: int, grad_scale: float, loss_acc: torch.Tensor,
@@ -1235,14 +1205,9 @@ class OwnerLazyTables(OwnerTables):
 
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,
                     neg_samples: int, *, seed: int, noise_offset: int, grad_scale: float,
-                    loss_acc: torch.Tensor, status: torch.Tensor,
-                    next_walks: Optional[torch.Tensor] = None, next_noise_offset: int = 0,
-                    bind_next=None, rebind=None) -> int:
+                    loss_acc: torch.Tensor, status: torch.Tensor) -> int:
     """One owner-computes step with the touched-row in-table exchange (every rank passes the
-    same global batch). Returns this rank's record count. ``next_walks`` (the rows-major step):
-    the next step's batch, whose claim then runs beside this step's centre pass
-    (OwnerLazyTables.claim_ahead; ``bind_next`` / ``rebind``: called around it, e.g. to bind
-    the next step's scalar block in a graph capture)."""
+    same global batch). Returns this rank's record count."""
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     tables.begin_step()
     tables.before_pass1(walks, context_radius, neg_samples, seed, noise_offset, status)
@@ -1252,13 +1217,6 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
         # rows-major: the out rows' whole step, then the centre gradient from its coefficients
         tables.out_rows_step(walks, context_radius, neg_samples, seed, noise_offset,
                              grad_scale, loss_acc, status)
-        if next_walks is not None and tables.rows_major_ok(context_radius, neg_samples):
-            if bind_next is not None:
-                bind_next()
-            tables.claim_ahead(next_walks, context_radius, neg_samples, seed, next_noise_offset,
-                               status, tables.step_count + 1)
-            if rebind is not None:
-                rebind()
         sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, neg_samples,
                          walks=walks, context_radius=context_radius, owner=tables.rank,
                          n_owners=tables.world, vocab_size=tables.V, seed=seed,
