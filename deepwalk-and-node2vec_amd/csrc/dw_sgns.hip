@@ -3081,10 +3081,14 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     oa.counts = counts;   // (p_current false: k_lazy_boundary replays the straddling rows whole)
     rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;
-    // records per chunk (<= 64: one per lane): 64, halved to 32 while the chunks would not give
-    // every SIMD of the chip eight waves
+    // records per chunk (<= 64: one per lane): as few as keep every chunk's wave resident at
+    // once (eight waves per SIMD, k_out_rows' bound) — every wave then runs from the start, where
+    // 32-record chunks left C3's 64-walk batch (269K records) ~200 waves for a second round that
+    // doubled the kernel — and no fewer than 16
     const int64_t bound = n_centres * T;
-    const int32_t gch = bound / 64 < grid_cap(32) ? 32 : 64;
+    const int64_t resident = grid_cap(32);
+    int32_t gch = static_cast<int32_t>((bound + resident - 1) / resident);
+    gch = gch < 16 ? 16 : gch > 64 ? 64 : gch;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
