@@ -1255,13 +1255,13 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if constexpr (COEFIN) {
         DW_REQUIRE(!a.fx_in.acc, "dw_sgns_owner_pass1: the rows-major step has no deterministic "
                    "form");
-        // (the rows-major step's batches are small: a wave per four centres leaves about one
-        // wave per SIMD, so the chunks hold more rows in flight — the same FMAs in the same order)
+        // (eight and sixteen rows per chunk measured 45 and 59 us against 42 at C3's 64-walk
+        // batch: the pass-1 chunking stays)
         switch (a.d / 64) {
             case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, true, false, true>), g, bl, 0, st, a); break;
-            case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 8, true, false, true>), g, bl, 0, st, a); break;
-            case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
-            case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
+            case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
+            case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
+            case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, false, true>), g, bl, 0, st, a); break;
             default: return DW_E_UNSUPPORTED;
         }
         DW_LAUNCH_CHECK("dw_sgns/g16_coefin");
