@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: the rows-major lazy out step (dw_sgns_owner_out_rows + the coefficients-in centre
 # pass) — its tests against the gather path and dense training, C3 at 64 walks rows-major vs
-# the catch-up / pass 1 / gather path (DW_OUT_ROWS=0), and the kernel trace.
+# the catch-up / pass 1 / gather path (DW_OUT_ROWS=0, an A/B switch since removed), and the kernel trace.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out

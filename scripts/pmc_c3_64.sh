@@ -1,7 +1,8 @@
 #!/bin/bash
 # HBM bytes per kernel of the 64-walk C3 step (rocprofv3 --pmc, one counter per pass: FETCH_SIZE
 # and WRITE_SIZE cannot share a pass on gfx950), the rows-major step and the catch-up / pass 1 /
-# gather sequence (DW_OUT_ROWS=0). Output: gpurun_out/pmc64/<rows>_<counter>.csv
+# gather sequence (DW_OUT_ROWS=0: an A/B switch while round 4 measured it, since removed — a rerun
+# now measures the default form twice). Output: gpurun_out/pmc64/<rows>_<counter>.csv
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/pmc64
