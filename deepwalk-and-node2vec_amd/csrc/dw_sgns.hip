@@ -2475,26 +2475,27 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // !CLAIM (the rows-major step, dw_sgns_owner_out_rows): the ranks alone — k_out_rows replays
 // every row right before its step, so no row is listed or caught up here.
 constexpr int CLAIM_TRIPS = 4;
-template <bool CLAIM>
+// (the ranks alone: one centre per wave, four times the waves — the atomics are the chain)
+template <bool CLAIM, int TRIPS = CLAIM ? CLAIM_TRIPS : 1>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
     k_out_claim(SgnsArgs a, int32_t *__restrict__ claim, int32_t step_arg, int32_t delta,
                 uint32_t *__restrict__ list, unsigned long long *__restrict__ n_list,
                 uint32_t *__restrict__ count, uint32_t *__restrict__ rank,
                 uint32_t *__restrict__ rowid) {
     const int32_t step = dw::eff_step(a.dyn, delta, step_arg);   // graph replay: from the block
-    __shared__ uint32_t s_rows[WAVES_PER_BLOCK][CLAIM_TRIPS * WAVE];
+    __shared__ uint32_t s_rows[WAVES_PER_BLOCK][TRIPS * WAVE];
     __shared__ uint32_t s_cnt[WAVES_PER_BLOCK];
     __shared__ unsigned long long s_base;
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int T = a.C * (1 + a.K);
     const int64_t per = a.L - 2 * a.R;
-    const int64_t tile = (int64_t)WAVES_PER_BLOCK * CLAIM_TRIPS;
+    const int64_t tile = (int64_t)WAVES_PER_BLOCK * TRIPS;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (int64_t b0 = (int64_t)blockIdx.x * tile; b0 < a.batch; b0 += (int64_t)gridDim.x * tile) {
-        int64_t o[CLAIM_TRIPS];   // each trip's row (-1: none)
+        int64_t o[TRIPS];   // each trip's row (-1: none)
 #pragma unroll
-        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+        for (int k = 0; k < TRIPS; ++k) {
             const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
             o[k] = -1;
             if (b < a.batch && lane < T) {
@@ -2506,9 +2507,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                     o[k] = r / a.n_owners;
             }
         }
-        bool mine[CLAIM_TRIPS];
+        bool mine[TRIPS];
 #pragma unroll
-        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+        for (int k = 0; k < TRIPS; ++k) {
             mine[k] = false;
             if (o[k] >= 0) {
                 const int64_t b = b0 + k * WAVES_PER_BLOCK + wv;
@@ -2524,7 +2525,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
         if constexpr (!CLAIM) continue;
         uint32_t n_mine = 0;   // wave-uniform
 #pragma unroll
-        for (int k = 0; k < CLAIM_TRIPS; ++k) {
+        for (int k = 0; k < TRIPS; ++k) {
             const uint64_t mask = __ballot(mine[k]);
             if (mine[k]) s_rows[wv][n_mine + __popcll(mask & lt)] = static_cast<uint32_t>(o[k]);
             n_mine += __popcll(mask);
@@ -2686,7 +2687,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
                              "dw_sgns_owner_out_catch_up", vocab_size, nullptr, &pl);
         if (rc != DW_OK) return rc;
     }
-    const int64_t ctile = (int64_t)WAVES_PER_BLOCK * CLAIM_TRIPS;
+    const int64_t ctile = (int64_t)WAVES_PER_BLOCK * (rows_major ? 1 : CLAIM_TRIPS);
     int64_t blocks = (a.batch + ctile - 1) / ctile;
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     if (blocks < 1) blocks = 1;
