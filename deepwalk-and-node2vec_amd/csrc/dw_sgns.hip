@@ -2051,8 +2051,7 @@ int plan_occ(int64_t n_centres, int64_t V, void *base, OccSpace *o, hipStream_t 
 // the records' placement (k_out_claim's ranks, one owner or many): rank[slot], off[row] (the
 // exclusive scan of the per-row counts, with one zero past the rows: off[local_rows] = their
 // total) and the scan's temporary storage; between the records part and OccSpace
-constexpr int PLACE_TILE = 1024;   // placement-scan counts per block (4 per thread; k_place_scan)
-constexpr int PLACE_PER = PLACE_TILE / 256;
+constexpr int PLACE_TILE = 4096;   // placement-scan counts per block (16 per thread; k_place_scan)
 
 struct PlaceSpace {
     uint32_t *rank, *off;
@@ -2598,11 +2597,11 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
     if (threadIdx.x == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
     __syncthreads();
-    // thread k holds counts [a + PER k, a + PER (k + 1)): its sum, the block's exclusive scan of them
-    const int64_t a = (int64_t)blockIdx.x * PLACE_TILE + PLACE_PER * threadIdx.x;
-    uint32_t c[PLACE_PER], t = 0;
+    // thread k holds counts [a + 16k, a + 16k + 16): its sum, the block's exclusive scan of them
+    const int64_t a = (int64_t)blockIdx.x * PLACE_TILE + 16 * threadIdx.x;
+    uint32_t c[16], t = 0;
 #pragma unroll
-    for (int k = 0; k < PLACE_PER; ++k) {
+    for (int k = 0; k < 16; ++k) {
         c[k] = a + k < n ? counts[a + k] : 0u;
         t += c[k];
     }
@@ -2619,7 +2618,7 @@ __global__ void __launch_bounds__(256)
     for (int w = 0; w < wv; ++w) pre += s_w[w];
     uint32_t run = pre + x - t;   // exclusive prefix of this thread's first count
 #pragma unroll
-    for (int k = 0; k < PLACE_PER; ++k) {
+    for (int k = 0; k < 16; ++k) {
         if (a + k < n) off[a + k] = run;
         run += c[k];
     }
