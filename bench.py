@@ -173,6 +173,121 @@ def cpu_baseline(csr, args, budget_s: float, walk_methods):
     }
 
 
+def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) -> dict:
+    """The reference configs' own batch (configs/sge_sg_cora.yaml:24, sge_sg_karate_club.yaml:24:
+    64 walks per step) on the headline graph, timed by the driver's run.
+
+    The one-GPU composition bench.py takes for that shape (`--batch-walks 64`): OwnerLazyTables
+    on one rank with the lazy exact Adam of both tables (only the rows a step touches are read
+    and updated; deferred g = 0 steps replayed bit-exactly), the records placed by the claim and
+    the rows-major out step, replayed as HIP graphs of 16 steps (GraphedOwnerStep) with the
+    Philox walker in front. After the timed replays one more step is run eagerly from a
+    flushed pre-state and checked on ~256 in and ~256 out rows against the float64 restatement
+    (word2vec/verify.py; the parity tests' single-step bars); a miss fails the bench.
+
+    roofline: SURVEY §8d's per-pair SGNS bytes plus the dense-Adam figure (7 x 4 B per entry)
+    on the rows the step touches (the checked step's |U| in rows and stepped out rows), over the
+    HIP-event window of the replays."""
+    from shallow_encoders import _native
+    from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
+    from shallow_encoders.word2vec import verify
+    from shallow_encoders.word2vec.graphed import GraphedOwnerStep
+    from shallow_encoders.word2vec.sgns import loss_terms
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    V, d, R, K, L = csr.vocab_size, args.dim, args.radius, args.neg, args.walk_length
+    B, unroll, warm, seed = 64, 16, 8, 99
+    n_steps = max(unroll, n_steps // unroll * unroll)
+    per = L - 2 * R
+    pairs = B * per * 2 * R
+    grad_scale = 1.0 / pairs
+    walks_total = (V - 1) * args.walks_per_node
+    walker = (Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=1234, device=dev)
+              if args.method == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=1234,
+                                                         device=dev))
+    tables = OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=0, lazy_out=True)
+    loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def eager_step(s: int) -> torch.Tensor:
+        g0 = s * B
+        a = g0 % walks_total
+        walks = walker.walk_batch(epoch_starts[a:a + B], walk_id0=g0, check=False,
+                                  status=status)
+        owner_lazy_step(tables, walks, R, K, seed=seed, noise_offset=g0 * per,
+                        grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+        return walks
+
+    for s in range(warm):
+        eager_step(s)
+    graphed = GraphedOwnerStep(tables, walker, epoch_starts, B, R, K, seed=seed,
+                               grad_scale=grad_scale, loss_acc=loss_acc, status=status,
+                               first_walk_id=warm * B, n_steps=n_steps + unroll, unroll=unroll)
+    graphed.replay()                      # one untimed replay (first-launch costs)
+    torch.cuda.synchronize(dev)
+    loss_acc.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a = time.perf_counter()
+    e0.record()
+    for _ in range(n_steps // unroll):
+        graphed.replay()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - a
+    _native.check_status(status, 'bench batch64')
+    kern_ms = e0.elapsed_time(e1) / n_steps
+    mean_loss = float(loss_terms(loss_acc, pairs * n_steps, K)['loss'])
+
+    # one more step, eager, checked from its (flushed) pre-state
+    s = warm + unroll + n_steps
+    g0 = s * B
+    pre = tables.full_state()
+    walks = eager_step(s)
+    torch.cuda.synchronize(dev)
+    _native.check_status(status, 'bench batch64 step check')
+    n_in = int(tables._n_touched.item())                       # |U|: distinct centre rows
+    n_out = int((tables.last_out[:V] == tables.step_count).sum())   # out rows stepped
+    rows_in, rows_out = verify.sample_rows(walks, R, K, V, seed, g0 * per, 256)
+    if os.environ.get('DW_BENCH_CORRUPT') == '1':   # test aid: the check must then fail
+        tables.m_out[int(rows_out[0])] += 1e-3
+    post = tables.full_state()
+    gi, go = verify.sampled_grads(pre[0], pre[3], walks, R, K, seed, g0 * per, rows_in, rows_out)
+    kw = dict(step=tables.step_count, lr=args.lr, betas=tables.betas, eps=tables.eps,
+              weight_decay=tables.weight_decay)
+    res = {'in': verify.check_rows(gi, tuple(x[rows_in] for x in pre[:3]),
+                                   tuple(x[rows_in] for x in post[:3]), **kw),
+           'out': verify.check_rows(go, tuple(x[rows_out] for x in pre[3:]),
+                                    tuple(x[rows_out] for x in post[3:]), **kw)}
+    step_check = dict(verify.summarize(res), rows_in=int(rows_in.numel()),
+                      rows_out=int(rows_out.numel()), step=tables.step_count)
+    del pre, post, graphed, tables
+    torch.cuda.empty_cache()
+
+    bpp = sgns_bytes_per_pair(d, K, R)
+    adam_bytes = (n_in + n_out) * d * 4 * 7
+    alg = pairs * bpp + adam_bytes
+    gbs = alg / (kern_ms * 1e-3) / 1e9
+    return {
+        'workload': (f'C3 graph, the reference configs\' batch: {B} walks/step ({args.method}, '
+                     f'L={L}), R={R}, K={K}, d={d}; one GPU, lazy exact Adam of both tables '
+                     f'(OwnerLazyTables, rows-major out step), HIP graphs of {unroll} steps'),
+        'value': pairs * n_steps / elapsed, 'unit': 'positive-pairs/s',
+        'ms_per_step': elapsed / n_steps * 1e3, 'steps': n_steps, 'warmup': warm + unroll,
+        'positive_pairs_per_step': pairs, 'mean_loss': mean_loss,
+        'roofline': {
+            'kernel': ('GraphedOwnerStep replay: Philox walker, k_out_claim + placement, '
+                       'k_out_rows (rows-major out step), k_sgns_g16 centre pass, in-table '
+                       'catch-up / update (k_rows_adam)'),
+            'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': gbs / HBM_PEAK_GBS, 'traffic': None,
+            'measured_copy_GBps': copy_gbs, 'frac_of_measured': gbs / copy_gbs,
+            'ms_per_step_events': kern_ms, 'bytes_per_step': alg,
+            'sgns_bytes': pairs * bpp, 'touched_rows_adam_bytes': adam_bytes,
+            'touched_in_rows': n_in, 'touched_out_rows': n_out},
+        'step_check': step_check,
+        'cpu_baseline': None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -279,6 +394,10 @@ def main():
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
                          'saves, 6.89 vs 6.89 ms/step at C3; on by default on the one-GPU lazy '
                          'path of small batches)')
+    ap.add_argument('--batch64-steps', type=int, default=400,
+                    help='the one-GPU C3 line: then also time this many steps at the reference '
+                         'configs\' 64-walk batch (lazy exact Adam, graph-replayed) and report '
+                         'them as batch64, with a checked step; 0 = skip')
     ap.add_argument('--deterministic', action='store_true',
                     help='the deterministic accumulation mode (word2vec/exact.py: int64 '
                          'fixed-point gradient sums, bit-identical tables run to run and across '
@@ -1071,12 +1190,39 @@ def main():
                     result['roofline']['phases'][k]['traffic'] = per_k.get('sgns_' + k)
         except (OSError, ValueError):
             pass
+    # ---- the reference configs' own 64-walk batch on the same graph ---------
+    b64 = None
+    if (args.batch64_steps > 0 and not dist_on and not owner and not emulate
+            and args.config == 'c3' and B != 64 and not args.deterministic):
+        del tables
+        torch.cuda.empty_cache()
+        b64 = batch64_line(csr, args, dev, epoch_starts, copy_gbs, args.batch64_steps)
+        prof64 = os.path.join(REPO, 'profiles', 'sgns_pmc.json')
+        try:
+            with open(prof64) as f:
+                ent = [e for e in json.load(f).get('entries', [])
+                       if e.get('workload') == 'c3_batch64']
+            if ent:
+                b64['roofline']['traffic'] = ent[-1].get('hbm_bytes_per_launch')
+                b64['roofline']['traffic_source'] = f"profiles/sgns_pmc.json ({ent[-1].get('round')})"
+        except (OSError, ValueError):
+            pass
+        result['batch64'] = b64
     if rank == 0 and not dist_on and not args.no_cpu_baseline and args.config in ('c2', 'c3'):
         cb = cpu_baseline(csr, args, args.cpu_budget, walk_methods)
         result['cpu_baseline'] = cb
+        if b64 is not None:
+            s64 = next(x for x in cb['batches'] if x['batch_walks'] == 64)
+            b64['cpu_baseline'] = {
+                'value': s64['pairs_per_s'], 'unit': 'positive-pairs/s', 'cores': cb['cores'],
+                'kind': 'port', 'sample': (f'the oracle SGNS step at 64 walks/step ({s64["steps"]} '
+                                           f'steps, {s64["seconds"]:.1f}s; see cpu_baseline)')}
     if rank == 0:
         print(json.dumps(result), flush=True)
     failed = bool(step_check) and not step_check['ok']
+    if b64 is not None and not b64['step_check']['ok']:
+        log(rank, f'[bench] batch64 step check FAILED: {b64["step_check"]}')
+        failed = True
     if dist_on:
         flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)   # every rank exits with rank 0's verdict

@@ -105,7 +105,9 @@ using dw::hist_at;
 // the barrier; thread 0 writes it after. STEP: replay the missed steps up to step - 1, then
 // apply `step` with the row's gradient g_rows[i]; else replay up to `step`. The step loop is
 // uniform: lanes past d carry zeros and are not stored.
-template <bool STEP, bool P_ONLY = false>
+// E = 2 (even d): two adjacent elements per thread (8-B accesses), replayed as pairs on the
+// packed fp32 instructions (dw::replay_g0 with N = 2): half the threads, half the issue slots.
+template <bool STEP, bool P_ONLY = false, int E = 1>
 __global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
                 int32_t *__restrict__ last, int64_t n_table, int32_t d,
@@ -113,7 +115,7 @@ __global__ void __launch_bounds__(512)
                 int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
                 int32_t step_arg, const dw_step_scalars *__restrict__ dyn, int32_t delta) {
     const int32_t step = dw::eff_step(dyn, delta, step_arg);   // graph replay: from the block
-    const int e = threadIdx.x;
+    const int e = threadIdx.x * E;
     const bool live = e < d;
     int64_t n = n_max;
     if (n_dev) {
@@ -129,17 +131,41 @@ __global__ void __launch_bounds__(512)
         __syncthreads();   // every wave has read last[r] before thread 0 advances it
         if (from >= (STEP ? step : upto)) continue;   // already current (or stepped)
         const int64_t o = r * d + e;
-        float pr[1] = {live ? p[o] : 0.f}, mr[1] = {live ? m[o] : 0.f};
-        float vr[1] = {live ? v[o] : 0.f};
-        float gg = (STEP && live) ? g_rows[i * d + e] : 0.f;
+        float pr[E], mr[E], vr[E], gg[E];
+        if constexpr (E == 2) {   // (d even: o is 8-B aligned)
+            const float2 zero = make_float2(0.f, 0.f);
+            const float2 p2 = live ? *reinterpret_cast<const float2 *>(p + o) : zero;
+            const float2 m2 = live ? *reinterpret_cast<const float2 *>(m + o) : zero;
+            const float2 v2 = live ? *reinterpret_cast<const float2 *>(v + o) : zero;
+            const float2 g2 = (STEP && live) ? *reinterpret_cast<const float2 *>(g_rows + i * d + e)
+                                             : zero;
+            pr[0] = p2.x, pr[1] = p2.y, mr[0] = m2.x, mr[1] = m2.y;
+            vr[0] = v2.x, vr[1] = v2.y, gg[0] = g2.x, gg[1] = g2.y;
+        } else {
+            pr[0] = live ? p[o] : 0.f;
+            mr[0] = live ? m[o] : 0.f;
+            vr[0] = live ? v[o] : 0.f;
+            gg[0] = (STEP && live) ? g_rows[i * d + e] : 0.f;
+        }
         dw::replay_g0(pr, mr, vr, hist, from, upto, box_from);
-        float &pp = pr[0], &mm = mr[0], &vv = vr[0];
-        if (STEP) dw::adam_elem(pp, gg, mm, vv, hist_at(hist, step));
+        if (STEP) {
+            const dw::AdamScalars hs = hist_at(hist, step);
+#pragma unroll
+            for (int k = 0; k < E; ++k) dw::adam_elem(pr[k], gg[k], mr[k], vr[k], hs);
+        }
         if (live) {
-            p[o] = pp;
-            if (!P_ONLY) {
-                m[o] = mm;
-                v[o] = vv;
+            if constexpr (E == 2) {
+                *reinterpret_cast<float2 *>(p + o) = make_float2(pr[0], pr[1]);
+                if (!P_ONLY) {
+                    *reinterpret_cast<float2 *>(m + o) = make_float2(mr[0], mr[1]);
+                    *reinterpret_cast<float2 *>(v + o) = make_float2(vr[0], vr[1]);
+                }
+            } else {
+                p[o] = pr[0];
+                if (!P_ONLY) {
+                    m[o] = mr[0];
+                    v[o] = vr[0];
+                }
             }
         }
         if (e == 0 && !P_ONLY) last[r] = STEP ? step : upto;
@@ -290,19 +316,29 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
     DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
-    const int threads = 64 * ((dim + 63) / 64);
+    // even d: two elements per thread on the packed instructions
+    const bool pair = dim % 2 == 0;
+    const int threads = pair ? 64 * ((dim / 2 + 63) / 64) : 64 * ((dim + 63) / 64);
+#define DW_ROWS_ADAM(STEP_, PONLY_)                                                              \
+    do {                                                                                        \
+        if (pair)                                                                               \
+            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 2>), dim3((unsigned)blocks),         \
+                               dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
+                               n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, \
+                               step, dyn, delta);                                               \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 1>), dim3((unsigned)blocks),         \
+                               dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
+                               n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, \
+                               step, dyn, delta);                                               \
+    } while (0)
     if (grad_rows)
-        hipLaunchKernelGGL((k_rows_adam<true>), dim3((unsigned)blocks), dim3(threads), 0, st,
-                           param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
-                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
+        DW_ROWS_ADAM(true, false);
     else if (p_only)
-        hipLaunchKernelGGL((k_rows_adam<false, true>), dim3((unsigned)blocks), dim3(threads), 0,
-                           st, param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
-                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
+        DW_ROWS_ADAM(false, true);
     else
-        hipLaunchKernelGGL((k_rows_adam<false>), dim3((unsigned)blocks), dim3(threads), 0, st,
-                           param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
-                           n_rows_dev, n_rows_max, grad_rows, hist, step, dyn, delta);
+        DW_ROWS_ADAM(false, false);
+#undef DW_ROWS_ADAM
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
 }

@@ -72,6 +72,7 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 // Stream tags keep the counter spaces of different consumers disjoint.
 constexpr uint32_t TAG_DEEPWALK = 0x44570000u;   // 'DW'
 constexpr uint32_t TAG_NODE2VEC = 0x4E320000u;   // 'N2'
+constexpr uint32_t TAG_N2V_POS = 0x4E500000u;    // 'NP' (node2vec over the position index)
 
 // Uniform index in [0, n) from 32 random bits (multiply-high; bias <= n / 2^32).
 __device__ __forceinline__ uint32_t bounded32(uint32_t r, uint32_t n) { return __umulhi(r, n); }
@@ -228,6 +229,62 @@ __device__ __forceinline__ void adam_elem_g0_box(float &p, float &m, float &v, c
     p = p + s.nstep * div_box(m, denom);
 }
 
+// The box step on two elements at once: the same IEEE operations per element as
+// adam_elem_g0_box — the multiplies, adds and fmas as gfx950's packed fp32 instructions
+// (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two elements per lane and issue slot, each
+// rounded as the scalar instruction rounds it), the sqrt and reciprocal seeds and the sqrt's
+// rounding selects per element. ~18 issue slots per element-step instead of ~30: the replays
+// are ALU-bound (every row's deferred steps are eventually replayed, ~V x d element-steps per
+// training step in the steady state of the lazy exact Adam).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 sqrt_box2(f32x2 x) {
+#pragma clang fp contract(off)
+    f32x2 s;
+    s.x = __builtin_amdgcn_sqrtf(x.x);
+    s.y = __builtin_amdgcn_sqrtf(x.y);
+    f32x2 sd, su;
+    sd.x = __uint_as_float(__float_as_uint(s.x) - 1u);
+    sd.y = __uint_as_float(__float_as_uint(s.y) - 1u);
+    su.x = __uint_as_float(__float_as_uint(s.x) + 1u);
+    su.y = __uint_as_float(__float_as_uint(s.y) + 1u);
+    const f32x2 rd = __builtin_elementwise_fma(-sd, s, x);
+    const f32x2 ru = __builtin_elementwise_fma(-su, s, x);
+    f32x2 r;
+    r.x = ru.x > 0.f ? su.x : (rd.x <= 0.f ? sd.x : s.x);
+    r.y = ru.y > 0.f ? su.y : (rd.y <= 0.f ? sd.y : s.y);
+    return r;
+}
+
+__device__ __forceinline__ f32x2 div_box2(f32x2 n, f32x2 d) {
+#pragma clang fp contract(off)
+    f32x2 r;
+    r.x = __builtin_amdgcn_rcpf(d.x);
+    r.y = __builtin_amdgcn_rcpf(d.y);
+    const f32x2 one = {1.0f, 1.0f};
+    f32x2 e = __builtin_elementwise_fma(-d, r, one);
+    r = __builtin_elementwise_fma(e, r, r);
+    f32x2 q = n * r;
+    e = __builtin_elementwise_fma(-d, q, n);
+    q = __builtin_elementwise_fma(e, r, q);
+    e = __builtin_elementwise_fma(-d, q, n);
+    return __builtin_elementwise_fma(e, r, q);
+}
+
+__device__ __forceinline__ void adam_elem_g0_box2(f32x2 &p, f32x2 &m, f32x2 &v,
+                                                  const AdamScalars &s) {
+#pragma clang fp contract(off)
+    const f32x2 w1 = {s.w1, s.w1}, b2 = {s.b2, s.b2}, rb = {s.rbc2s, s.rbc2s};
+    const f32x2 bc = {s.bc2s, s.bc2s}, eps = {s.eps, s.eps}, ns = {s.nstep, s.nstep};
+    m = __builtin_elementwise_fma(w1, -m, m);
+    v = v * b2;
+    const f32x2 x = sqrt_box2(v);
+    const f32x2 q = x * rb;
+    const f32x2 c = __builtin_elementwise_fma(-bc, q, x);
+    const f32x2 denom = __builtin_elementwise_fma(c, rb, q) + eps;
+    p = p + ns * div_box2(m, denom);
+}
+
 // The history read as constant memory: the scalar unit loads the step's scalars (uniform) and
 // tests them, where a generic pointer after the kernel's own stores gets vector loads.
 typedef __attribute__((address_space(4))) const float const_float;
@@ -260,10 +317,34 @@ __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&
             v0[k] = v[k];
         }
         const const_float *hc = (const const_float *)hist;
-        for (int32_t s = from + 1; s <= upto; ++s) {
-            const AdamScalars h = hist_at_const(hc + 8 * static_cast<int64_t>(s));
+        if constexpr (N % 2 == 0) {   // element pairs on the packed fp32 instructions
+            f32x2 P[N / 2], M[N / 2], W[N / 2];
 #pragma unroll
-            for (int k = 0; k < N; ++k) adam_elem_g0_box(p[k], m[k], v[k], h);
+            for (int k = 0; k < N / 2; ++k) {
+                P[k] = f32x2{p[2 * k], p[2 * k + 1]};
+                M[k] = f32x2{m[2 * k], m[2 * k + 1]};
+                W[k] = f32x2{v[2 * k], v[2 * k + 1]};
+            }
+            for (int32_t s = from + 1; s <= upto; ++s) {
+                const AdamScalars h = hist_at_const(hc + 8 * static_cast<int64_t>(s));
+#pragma unroll
+                for (int k = 0; k < N / 2; ++k) adam_elem_g0_box2(P[k], M[k], W[k], h);
+            }
+#pragma unroll
+            for (int k = 0; k < N / 2; ++k) {
+                p[2 * k] = P[k].x;
+                p[2 * k + 1] = P[k].y;
+                m[2 * k] = M[k].x;
+                m[2 * k + 1] = M[k].y;
+                v[2 * k] = W[k].x;
+                v[2 * k + 1] = W[k].y;
+            }
+        } else {
+            for (int32_t s = from + 1; s <= upto; ++s) {
+                const AdamScalars h = hist_at_const(hc + 8 * static_cast<int64_t>(s));
+#pragma unroll
+                for (int k = 0; k < N; ++k) adam_elem_g0_box(p[k], m[k], v[k], h);
+            }
         }
         bool end = true;
 #pragma unroll

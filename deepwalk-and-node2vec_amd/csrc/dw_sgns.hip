@@ -1262,7 +1262,9 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
             case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
             case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
             case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, false, true>), g, bl, 0, st, a); break;
-            default: return DW_E_UNSUPPORTED;
+            default:
+                dw::set_error("dw_sgns: the coefficient-input pass 1 needs d in {64, 128, 256, 512}, got %d", a.d);
+                return DW_E_UNSUPPORTED;
         }
         DW_LAUNCH_CHECK("dw_sgns/g16_coefin");
         return DW_OK;
@@ -1273,7 +1275,7 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
             case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER, true>), g, bl, 0, st, a); break;
             case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, OWNER, true>), g, bl, 0, st, a); break;
             case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER, true>), g, bl, 0, st, a); break;
-            default: return DW_E_UNSUPPORTED;
+            default: return DW_E_UNSUPPORTED;   // the caller falls back to k_sgns
         }
         DW_LAUNCH_CHECK("dw_sgns/g16");
         return DW_OK;
@@ -1283,7 +1285,7 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
         case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, OWNER>), g, bl, 0, st, a); break;
         case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, OWNER>), g, bl, 0, st, a); break;
         case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, OWNER>), g, bl, 0, st, a); break;
-        default: return DW_E_UNSUPPORTED;
+        default: return DW_E_UNSUPPORTED;   // the caller falls back to k_sgns
     }
     DW_LAUNCH_CHECK("dw_sgns/g16");
     return DW_OK;
@@ -2171,9 +2173,9 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     DW_REQUIRE(local_rows * a.n_owners >= a.V, "dw_sgns_owner_pass1: %lld local rows x %d owners "
                "do not cover %lld rows", (long long)local_rows, a.n_owners, (long long)a.V);
     DW_REQUIRE(a.V <= 0x7FFFFFFF, "dw_sgns_owner_pass1: vocab_size must be < 2^31");
-    DW_REQUIRE(a.d % 64 == 0 && a.d <= 512 && T <= G16_TMAX,
-               "dw_sgns_owner_pass1: needs d a multiple of 64 (<= 512) and 2R(1+K) <= %d",
-               G16_TMAX);
+    DW_REQUIRE((a.d == 64 || a.d == 128 || a.d == 256 || a.d == 512) && T <= G16_TMAX,
+               "dw_sgns_owner_pass1: needs d in {64, 128, 256, 512} (got %d) and 2R(1+K) <= %d",
+               a.d, G16_TMAX);
     Workspace ws;
     OwnerLayout lay;
     OccSpace occ;
@@ -3101,7 +3103,9 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
         case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
         case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
         case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
-        default: return DW_E_UNSUPPORTED;
+        default:
+            dw::set_error("dw_sgns_owner_out_rows: d must be one of 64, 128, 256, 512 (got %d)", dim);
+            return DW_E_UNSUPPORTED;
     }
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
     switch (dim / 64) {   // the straddling rows (g in g_out)

@@ -1316,14 +1316,18 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // (P[j-1], P[j]] where c is j (j + 1 at P[j] itself) by a search with no loads. The D values,
 // T, M and the bracketing test are the expressions of node2vec_pick_exact on the same
 // integers, so the pick — or the hand-over where the margin fails — is the same.
+// EXACT = false (the Philox walker, k_walk_node2vec_positions): no margin tests — the pick is
+// the first i at which the fp64 D_i turns positive, an exact draw from W_i / T up to the fp64
+// rounding of D (relative 2^-50), the same expressions as the oracle's (oracle/philox.py).
+template <bool EXACT = true>
 __device__ __forceinline__ int64_t n2v_pick_pos(const int32_t *__restrict__ P, int64_t C,
                                                 int64_t pt, int64_t n, double U, double ip,
                                                 double iq, uint32_t &loads) {
     const int64_t A = pt >= 0 ? 1 : 0;
     const double T = n2v_w(A, n - A - C, C, ip, iq);
     const double UT = U * T;
-    const double M = exact_margin(n, T);
-    if (!(T - UT > 0.0)) return -1;   // D_{n-1} <= 0: rounding at the top end
+    const double M = EXACT ? exact_margin(n, T) : 0.0;
+    if (EXACT && !(T - UT > 0.0)) return -1;   // D_{n-1} <= 0: rounding at the top end
     auto D = [&](int64_t i, int64_t c) {
         const int64_t a = (pt >= 0 && pt <= i) ? 1 : 0;
         return n2v_w(a, (i + 1) - a - c, c, ip, iq) - UT;
@@ -1350,9 +1354,11 @@ __device__ __forceinline__ int64_t n2v_pick_pos(const int32_t *__restrict__ P, i
             a = mid + 1;
     }
     const int64_t k = a;
-    const double d_k = D(k, (j < C && k == pj) ? j + 1 : j);
-    if (k >= 1 && fabs(D(k - 1, j)) <= M) return -1;
-    if (k <= n - 2 && fabs(d_k) <= M) return -1;
+    if constexpr (EXACT) {
+        const double d_k = D(k, (j < C && k == pj) ? j + 1 : j);
+        if (k >= 1 && fabs(D(k - 1, j)) <= M) return -1;
+        if (k <= n - 2 && fabs(d_k) <= M) return -1;
+    }
     return k;
 }
 
@@ -1571,6 +1577,110 @@ __global__ void __launch_bounds__(256)
     } else {
         o[0] = v;
         for (int32_t s = 1; s < L; ++s) o[s] = step(s);
+    }
+}
+
+// node2vec (Philox) over the per-edge position index (dw_n2v_edge_index_build), one lane per
+// walker: the exact replay walker's step (k_walk_replay_n2v_pos) with its uniform drawn from
+// Philox instead of CPython's stream — one 32-B edge record per step (the next row and the
+// step's index entry), log2 C dependent 4-B position loads, no rejection rounds and no
+// adjacency tests. The first step picks bounded32(r.x, n) (the unbiased first step,
+// random_walk_generator.py:97), later steps U = 53 bits of (r.x, r.y) (genrand_res53's split)
+// against the prefix weights of the reference rule (:100-108) through n2v_pick_pos<false>.
+// Counter (walk id lo, hi, step << 8, TAG_N2V_POS); restated in oracle/philox.py
+// (fast_walks_positions). The next step's draw is computed while the record load is in flight.
+// COUNT: realised bytes (the 32-B record and 4-B output per step, 4 B per position load, the
+// start's row_ptr pair) and steps into counters[0], counters[1], position loads in counters[3].
+template <bool COUNT>
+__global__ void __launch_bounds__(256)
+    k_walk_node2vec_positions(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ rec,
+                              const int32_t *__restrict__ pos, int64_t n_rows,
+                              const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
+                              double ip, double iq, uint32_t k0, uint32_t k1, uint64_t walk_id0,
+                              int32_t *__restrict__ out, int32_t *status,
+                              const dw_step_scalars *__restrict__ dyn,
+                              unsigned long long *counters) {
+    const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    uint32_t loads = 0, steps = 0;
+    if (w < n_walks) {
+        const uint64_t wid = (dyn ? dyn->walk_id0 : walk_id0) + static_cast<uint64_t>(w);
+        int32_t *o = out + w * (int64_t)L;
+        int32_t v = starts[w];
+        bool ok = v >= 0 && (int64_t)v < n_rows;
+        if (!ok) dw::status_or(status, DW_S_BAD_CSR);
+        int64_t a = ok ? row_ptr[v] : 0;
+        int64_t n = ok ? row_ptr[v + 1] - a : 0;
+        bool second = false;                 // a previous node exists (steps >= 2)
+        int64_t p_off = 0;
+        uint32_t cw = 0;                     // the counts word of the edge taken
+        int32_t pt = -1;                     // the previous node's position in N(v)
+        auto draw = [&](int32_t s) {
+            return dw::philox(dw::U4{static_cast<uint32_t>(wid), static_cast<uint32_t>(wid >> 32),
+                                     static_cast<uint32_t>(s) << 8, dw::TAG_N2V_POS},
+                              k0, k1);
+        };
+        dw::U4 r = draw(1);
+        auto step = [&](int32_t s) -> int32_t {   // node at step s >= 1 (-1 once aborted)
+            if (!ok) return -1;
+            if (n <= 0) {
+                dw::status_or(status, DW_S_ISOLATED_NODE);
+                ok = false;
+                return -1;
+            }
+            int64_t k;
+            if (!second) {
+                k = dw::bounded32(r.x, static_cast<uint32_t>(n));
+            } else {
+                const double U = static_cast<double>((static_cast<uint64_t>(r.x >> 5) << 26) |
+                                                     static_cast<uint64_t>(r.y >> 6)) *
+                                 0x1p-53;
+                k = n2v_pick_pos<false>(pos + p_off, cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n,
+                                        U, ip, iq, loads);
+            }
+            const int64_t e = a + k;
+            const int4 r0 = rec[2 * e], r1 = rec[2 * e + 1];
+            r = draw(s + 1);   // independent of the record: overlaps its latency
+            if (COUNT) ++steps;
+            v = r0.x;
+            n = r0.y;
+            a = static_cast<int64_t>(static_cast<uint32_t>(r0.z)) |
+                (static_cast<int64_t>(r0.w) << 32);
+            p_off = static_cast<int64_t>(static_cast<uint32_t>(r1.x)) |
+                    (static_cast<int64_t>(r1.y) << 32);
+            cw = static_cast<uint32_t>(r1.z);
+            pt = r1.w;
+            second = true;
+            return v;
+        };
+        if ((L & 3) == 0) {
+            int4 *o4 = reinterpret_cast<int4 *>(o);
+            const int32_t v0 = v;
+            for (int32_t s0 = 0; s0 < L; s0 += 4) {
+                int4 pk;
+                pk.x = s0 == 0 ? v0 : step(s0);
+                pk.y = step(s0 + 1);
+                pk.z = step(s0 + 2);
+                pk.w = step(s0 + 3);
+                o4[s0 >> 2] = pk;
+            }
+        } else {
+            o[0] = v;
+            for (int32_t s = 1; s < L; ++s) o[s] = step(s);
+        }
+    }
+    if (COUNT) {
+        const int lane = threadIdx.x & (WAVE - 1);
+        unsigned long long v3[3] = {
+            (unsigned long long)loads * 4ull + (unsigned long long)steps * 36ull +
+                (w < n_walks ? 20ull : 0ull),
+            (unsigned long long)steps, (unsigned long long)loads};
+        for (int k = 0; k < 3; ++k)
+            for (int off = WAVE / 2; off > 0; off >>= 1) v3[k] += __shfl_xor(v3[k], off, WAVE);
+        if (lane == 0) {
+            atomicAdd(counters + 0, v3[0]);
+            atomicAdd(counters + 1, v3[1]);
+            atomicAdd(counters + 3, v3[2]);
+        }
     }
 }
 
@@ -2385,6 +2495,38 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
                                  starts, n_walks, walk_length, p, q, k0, k1, walk_id0, out,
                                  status, stream,
                                  reinterpret_cast<unsigned long long *>(counters));
+}
+
+int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const int32_t *n2v_pos,
+                           int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                           int32_t walk_length, double p, double q, uint64_t seed,
+                           uint64_t walk_id0, int32_t *out, int32_t *status, uint64_t *counters,
+                           void *stream) {
+    DW_REQUIRE(walk_length >= 1 && walk_length < (1 << 24),
+               "dw_walk_fast_positions: walk_length must be in [1, 2^24)");
+    DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_fast_positions: negative size");
+    if (n_walks == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && n2v_rec && starts && out && status,
+               "dw_walk_fast_positions: null pointer");
+    DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_fast_positions: p and q must be positive");
+    const double ip = 1.0 / p, iq = 1.0 / q;
+    DW_REQUIRE(ip < 1e300 && iq < 1e300, "dw_walk_fast_positions: p, q too small");
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    const int64_t blocks = (n_walks + 255) / 256;
+    DW_REQUIRE(blocks < (int64_t(1) << 31), "dw_walk_fast_positions: too many walks");
+    auto *cnt = reinterpret_cast<unsigned long long *>(counters);
+    if (cnt)
+        hipLaunchKernelGGL(k_walk_node2vec_positions<true>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), row_ptr, reinterpret_cast<const int4 *>(n2v_rec),
+                           n2v_pos, n_rows, starts, n_walks, walk_length, ip, iq, k0, k1, walk_id0,
+                           out, status, dw::bound_step_scalars(), cnt);
+    else
+        hipLaunchKernelGGL(k_walk_node2vec_positions<false>, dim3((unsigned)blocks), dim3(256), 0,
+                           dw::as_stream(stream), row_ptr, reinterpret_cast<const int4 *>(n2v_rec),
+                           n2v_pos, n_rows, starts, n_walks, walk_length, ip, iq, k0, k1, walk_id0,
+                           out, status, dw::bound_step_scalars(), cnt);
+    DW_LAUNCH_CHECK("dw_walk_fast_positions");
+    return DW_OK;
 }
 
 int dw_step_starts(const dw_step_scalars *dev, const int32_t *epoch_starts, int64_t n_epoch,

@@ -37,7 +37,7 @@ DW_EXACT_DEFER = 1
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -80,6 +80,8 @@ SIGNATURES = {
                                             _i32, _f64, _f64, _u64, _u64, _p, _p, _p]),
     'dw_walk_fast_counted': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i32, _f64,
                                             _f64, _u64, _u64, _p, _p, _p, _p]),
+    'dw_walk_fast_positions': (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _i32, _f64, _f64,
+                                              _u64, _u64, _p, _p, _p, _p]),
     'dw_edges_inline_build': (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p]),
     'dw_sgns_walks': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p,
                                      _p, _u64, _u64, _f32, _p, _p, _p, ctypes.c_size_t, _p]),

@@ -250,8 +250,9 @@ class CSRGraph:
             self._build_n2v_index(dev)
         return d
 
-    # the position index is built when its entries, scratch and records fit this many bytes
-    # (DW_N2V_INDEX_BYTES overrides); above it the walker keeps the counted classification
+    # the position index is built when its entries, scratch and records fit this many bytes and
+    # half the device's free memory (DW_N2V_INDEX_BYTES overrides both); above it the walker
+    # keeps the counted classification
     N2V_INDEX_BYTES = 48 << 30
 
     def _build_n2v_index(self, dev) -> None:
@@ -288,15 +289,26 @@ class CSRGraph:
                 _native.call('dw_n2v_edge_index_build', *args, None, None, None, None,
                              ctypes.byref(nb), None, s)
             need = 8 * n_pos + 32 * E + int(nb.value)
-            budget = int(os.environ.get('DW_N2V_INDEX_BYTES', self.N2V_INDEX_BYTES))
+            # the budget: DW_N2V_INDEX_BYTES, else N2V_INDEX_BYTES capped at half the device's
+            # free memory (the walker's other buffers and the training tables share it)
+            env = os.environ.get('DW_N2V_INDEX_BYTES')
+            budget = (int(env) if env is not None else
+                      min(self.N2V_INDEX_BYTES, torch.cuda.mem_get_info(dev)[0] // 2))
+            skipped = {'entries': n_pos, 'bytes': need, 'skipped': True}
             if not fits or need > budget:
                 d['n2v_rec'], d['n2v_pos'] = None, None
-                d['n2v_index_info'] = {'entries': n_pos, 'bytes': need, 'skipped': True}
+                d['n2v_index_info'] = skipped
                 return
-            pos = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
-            scratch = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
-            rec = torch.empty((max(E, 1), 8), dtype=torch.int32, device=dev)
-            tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            try:
+                pos = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
+                scratch = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
+                rec = torch.empty((max(E, 1), 8), dtype=torch.int32, device=dev)
+                tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            except torch.OutOfMemoryError:   # the wave walker needs none of it
+                d['n2v_rec'], d['n2v_pos'] = None, None
+                d['n2v_index_info'] = dict(skipped, out_of_memory=True)
+                torch.cuda.empty_cache()
+                return
             _native.call('dw_n2v_edge_index_build', *args, _native.ptr(pos), _native.ptr(scratch),
                          _native.ptr(rec), _native.ptr(tmp), ctypes.byref(nb),
                          _native.ptr(d['status']), s)

@@ -121,18 +121,23 @@ class RandomWalk(ABC):
             rng: 'python' (bit-exact replay of the global ``random`` stream) or 'philox'
             seed: Philox key (rng='philox')
             device: HIP device (default: current)
-            layout: rng='philox' — 'indexed' (default, dw_walk_fast_indexed: DeepWalk over the
-                edge-inline CSR, one dependent load per step; node2vec adjacency tests in the
-                per-row hash) or 'csr' (dw_walk_fast: row_ptr / col, node2vec tests by search of
-                the sorted lists). Both give the same walks bit for bit. rng='python':
+            layout: rng='philox' — 'indexed' (default: DeepWalk over the edge-inline CSR,
+                dw_walk_fast_indexed, one dependent load per step; node2vec on an unweighted
+                graph over the per-edge position index, dw_walk_fast_positions — one Philox
+                uniform and a search of the step's positions, no rejection rounds — where the
+                index fits (CSRGraph.N2V_INDEX_BYTES), else as 'hash'), 'hash' (node2vec by
+                rejection with the adjacency tests in the per-row hash, dw_walk_fast_indexed) or
+                'csr' (dw_walk_fast: row_ptr / col, node2vec's tests by search of the sorted
+                lists; the same walks as 'hash' bit for bit). The position walker samples the
+                same law from a different use of the Philox stream. rng='python':
                 'indexed' runs DeepWalk on unweighted graphs over the edge-inline CSR
                 (dw_walk_replay_inline), 'csr' keeps dw_walk_replay; the same walks.
         """
         assert length >= 1, 'Minimum walk length is 1!'
         if rng not in ('python', 'philox'):
             raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
-        if layout not in ('indexed', 'csr'):
-            raise ValueError(f'unknown layout "{layout}" (expected "indexed" or "csr")')
+        if layout not in ('indexed', 'hash', 'csr'):
+            raise ValueError(f'unknown layout "{layout}" (expected "indexed", "hash" or "csr")')
         self._layout = layout
         self._graph = graph
         self._length = length
@@ -217,7 +222,9 @@ class RandomWalk(ABC):
         # replay: the CSR, adjacency by search of the sorted lists; philox: DeepWalk over the
         # edge-inline CSR, node2vec with the per-row adjacency hash (the same walks as
         # dw_walk_fast, bit for bit; layout='csr' selects that one)
-        indexed = self._rng == 'philox' and self._layout == 'indexed'
+        indexed = self._rng == 'philox' and self._layout in ('indexed', 'hash')
+        # Philox node2vec on an unweighted graph: over the position index where it fits
+        pos_fast = self._positions_walker(dev)
         # replay, DeepWalk on an unweighted graph: the same walks over the edge-inline CSR
         # (dw_walk_replay_inline; layout='csr' keeps dw_walk_replay)
         replay_inline = (self._rng == 'python' and not n2v and self._layout == 'indexed'
@@ -229,11 +236,12 @@ class RandomWalk(ABC):
         d = self._csr.device_tensors(dev, need_sorted=n2v and not indexed,
                                      need_alias=self._rng == 'philox',
                                      need_edges=(indexed and not n2v) or replay_inline,
-                                     need_adj=indexed and n2v, need_adj_pos=replay_n2v_idx,
+                                     need_adj=indexed and n2v and not pos_fast,
+                                     need_adj_pos=replay_n2v_idx,
                                      need_hub_bits=replay_n2v_idx,
                                      need_edge_cn=replay_n2v_idx and _edge_cn_enabled(),
                                      need_n2v_index=replay_n2v_idx and _n2v_index_enabled())
-        if self._rng == 'python' and n2v:
+        if (self._rng == 'python' and n2v) or pos_fast:
             self._csr.require_simple(dev)   # no repeated neighbour (nx.Graph's invariant)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
@@ -273,7 +281,13 @@ class RandomWalk(ABC):
                     commit()
             else:
                 wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
-                if indexed:
+                if pos_fast:
+                    _native.call('dw_walk_fast_positions', _native.ptr(d['row_ptr']),
+                                 _native.ptr(d['n2v_rec']), _native.ptr(d['n2v_pos']),
+                                 self._csr.vocab_size, _native.ptr(starts), n, L, float(p),
+                                 float(q), self._seed & 0xFFFFFFFFFFFFFFFF, wid0,
+                                 _native.ptr(out), _native.ptr(status), None, s)
+                elif indexed:
                     _native.call('dw_walk_fast_indexed', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d.get('edges')),
                                  _native.ptr(d.get('adj_off')), _native.ptr(d.get('adj_hash')),
@@ -293,6 +307,16 @@ class RandomWalk(ABC):
         if check:
             _native.check_status(status, f'{type(self).__name__}.walk')
         return out
+
+    def _positions_walker(self, dev) -> bool:
+        """rng='philox', node2vec, layout='indexed', unweighted: True when the per-edge position
+        index is (or can be) built for this graph and device — then dw_walk_fast_positions
+        walks; else the rejection walker over the adjacency hash."""
+        if not (self._rng == 'philox' and self.METHOD == _native.DW_METHOD_NODE2VEC
+                and self._layout == 'indexed' and self._csr.weights is None):
+            return False
+        d = self._csr.device_tensors(dev, need_n2v_index=True)
+        return d.get('n2v_rec') is not None
 
     def count_replay_traffic(self, start_ids: torch.Tensor, uniforms: torch.Tensor,
                              out: Optional[torch.Tensor] = None) -> dict:
@@ -351,11 +375,29 @@ class RandomWalk(ABC):
         walkers' realised memory traffic counted (dw_walk_fast_counted; a diagnostic launch):
         {'bytes', 'steps', 'blocks', 'tests'} summed over the walks."""
         if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'philox' \
-                or self._layout != 'indexed':
-            raise ValueError('count_traffic: node2vec with rng="philox", layout="indexed"')
+                or self._layout not in ('indexed', 'hash'):
+            raise ValueError('count_traffic: node2vec with rng="philox", layout="indexed" or '
+                             '"hash"')
         dev = _native.require_device(self._device)
         starts = torch.as_tensor(start_ids, dtype=torch.int32).to(dev).contiguous()
         n, L = int(starts.numel()), self._length
+        if self._positions_walker(dev):   # {'bytes', 'steps', 0, position loads}
+            d = self._csr.device_tensors(dev)
+            if out is None:
+                out = torch.empty((n, L), dtype=torch.int32, device=dev)
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            counters = torch.zeros(4, dtype=torch.int64, device=dev)
+            p, q = self._params()
+            with torch.cuda.device(dev):
+                _native.call('dw_walk_fast_positions', _native.ptr(d['row_ptr']),
+                             _native.ptr(d['n2v_rec']), _native.ptr(d['n2v_pos']),
+                             self._csr.vocab_size, _native.ptr(starts), n, L, float(p), float(q),
+                             self._seed & 0xFFFFFFFFFFFFFFFF, int(walk_id0), _native.ptr(out),
+                             _native.ptr(status), _native.ptr(counters), _native.stream(dev))
+            _native.check_status(status, f'{type(self).__name__}.count_traffic')
+            c = counters.cpu().tolist()
+            return {'bytes': c[0], 'steps': c[1], 'blocks': 0, 'tests': 0,
+                    'position_loads': c[3], 'walker': 'dw_walk_fast_positions'}
         d = self._csr.device_tensors(dev, need_alias=True, need_adj=True)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)

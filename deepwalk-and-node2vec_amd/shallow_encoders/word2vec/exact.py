@@ -25,7 +25,7 @@ Not covered (refused): the atomic output scatter, pooled (CBOW) inputs, the repl
 layout's row pieces, the lazy Adam tables.
 """
 import os
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -55,12 +55,26 @@ class FixedAccumulator:
         self.frac = frac_bits(grad_scale)
         self.defer = bool(defer)
         self.acc = torch.zeros(grad.shape, dtype=torch.int64, device=grad.device)
-        self._ptr = grad.data_ptr()
-        _native.call('dw_exact_register', _native.ptr(grad), _native.ptr(self.acc), grad.numel(),
-                     self.frac, _native.DW_EXACT_DEFER if self.defer else 0)
+        self._grad_ptr = grad.data_ptr()
+        self._ptr = None            # the registered grad pointer while this one is active
+        self.activate()
+
+    def activate(self) -> None:
+        """(Re-)register this accumulator as the one the library adds ``grad``'s terms into.
+        Its int64 sums are zero between steps (every conversion clears them), so a cached
+        accumulator is taken up again without clearing."""
+        if self._ptr is None:
+            _native.call('dw_exact_register', _native.ptr(self.grad), _native.ptr(self.acc),
+                         self.grad.numel(), self.frac,
+                         _native.DW_EXACT_DEFER if self.defer else 0)
+            self._ptr = self._grad_ptr
+
+    @property
+    def active(self) -> bool:
+        return self._ptr is not None
 
     def matches(self, grad: torch.Tensor, grad_scale: float) -> bool:
-        return grad.data_ptr() == self._ptr and self.frac == frac_bits(grad_scale)
+        return grad.data_ptr() == self._grad_ptr and self.frac == frac_bits(grad_scale)
 
     def convert(self, acc: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                 accumulate: bool = False) -> None:
@@ -74,6 +88,7 @@ class FixedAccumulator:
                          self.frac, 1 if accumulate else 0, _native.stream(out.device))
 
     def release(self) -> None:
+        """Unregister (only while active: another accumulator may hold the buffer since)."""
         if self._ptr is not None:
             _native.load().dw_exact_unregister(self._ptr)
             self._ptr = None
@@ -86,26 +101,48 @@ class FixedAccumulator:
 
 
 class Registry:
-    """Accumulators per gradient buffer, re-registered when a buffer moves or the batch shape
-    (grad_scale) changes."""
+    """Accumulators per gradient buffer. A buffer's accumulator depends on the batch shape
+    (grad_scale sets frac), and an epoch's short last batch changes it for one step and back:
+    the accumulators are kept per (buffer, frac) for the registry's lifetime (at most
+    ``MAX_PER_KEY`` per buffer; the least recently used inactive one is dropped past that) and
+    re-registered, not reallocated, when the shape changes back. A captured graph keeps its
+    own references (``live``), so its accumulators stay allocated whatever the registry does."""
+
+    MAX_PER_KEY = 4
 
     def __init__(self):
-        self._acc: Dict[int, FixedAccumulator] = {}
+        self._acc: Dict[int, FixedAccumulator] = {}                  # the active one per key
+        self._cache: Dict[int, List[FixedAccumulator]] = {}          # per key, most recent last
 
     def ensure(self, key: int, grad: torch.Tensor, grad_scale: float,
                defer: bool = False) -> FixedAccumulator:
         a = self._acc.get(key)
-        if a is None or not a.matches(grad, grad_scale) or a.defer != defer:
-            if a is not None:
-                a.release()
-            a = FixedAccumulator(grad, grad_scale, defer)
-            self._acc[key] = a
-        return a
+        if a is not None and a.active and a.matches(grad, grad_scale) and a.defer == defer:
+            return a
+        if a is not None:
+            a.release()
+        cache = self._cache.setdefault(key, [])
+        hit = next((c for c in cache if c.matches(grad, grad_scale) and c.defer == defer), None)
+        if hit is not None:
+            cache.remove(hit)
+            hit.activate()
+        else:
+            hit = FixedAccumulator(grad, grad_scale, defer)
+            while len(cache) >= self.MAX_PER_KEY:
+                cache.pop(0)
+        cache.append(hit)
+        self._acc[key] = hit
+        return hit
 
     def get(self, key: int) -> Optional[FixedAccumulator]:
         return self._acc.get(key)
+
+    def live(self) -> List[FixedAccumulator]:
+        """The active accumulators (what a graph captured now adds into)."""
+        return [a for a in self._acc.values() if a.active]
 
     def release(self) -> None:
         for a in self._acc.values():
             a.release()
         self._acc = {}
+        self._cache = {}

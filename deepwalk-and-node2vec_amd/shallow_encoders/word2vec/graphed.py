@@ -442,6 +442,10 @@ class GraphedTrainerStep:
             trainer._noise_offset = snap[1]
         if w_in.data_ptr() != snap[2]:
             raise RuntimeError('GraphedTrainerStep: the in table did not end in its buffer')
+        # the deterministic mode's int64 accumulators the captured kernels add into: held here,
+        # so a replay never reaches freed memory whatever batch shapes the eager steps meet
+        reg = getattr(trainer, '_exact', None)
+        self._exact_refs = reg.live() if reg is not None else []
         torch.cuda.synchronize(dev)
 
     def _step_blk(self, k: int) -> int:

@@ -157,6 +157,9 @@ OVERLAP_MARGIN = 1.25
 # 1/8 of the table (64 MB at C3) while exposing only the last piece's exchange.
 DEFAULT_OUT_PIECES = 8
 
+# widths the owner passes (dw_sgns_owner_pass1/2, dw_sgns_owner_out_rows) are built for
+OWNER_DIMS = ROWS_MAJOR_DIMS = (64, 128, 256, 512)
+
 
 def overlap_adam_blocks(adam_bytes: float, overlap_bytes: Optional[float]) -> int:
     """Grid cap for an Adam of ``adam_bytes`` overlapping a phase of ``overlap_bytes``
@@ -546,6 +549,11 @@ class OwnerTables:
         self.adam_impl = adam_impl or hip_adam
         self.step_count = 0
         self._cuda = self.device.type == 'cuda'
+        if self._cuda and self.d not in OWNER_DIMS:
+            # the owner passes' kernels (k_sgns_g16 owner / COEFIN forms, k_out_rows) exist for
+            # these widths only: refuse here rather than fail inside a step
+            raise ValueError(f'the owner layout needs d in {OWNER_DIMS} (got {self.d}); use '
+                             f'ShardedTables (the replicated layout) for other widths')
         f32 = dict(dtype=torch.float32, device=self.device)
         self._alloc_in(f32)
         self.w_out = torch.zeros((self.S, self.d), **f32)
@@ -890,9 +898,11 @@ class OwnerLazyTables(OwnerTables):
         self._rows_step = False    # this step goes rows-major (set by catch_up_out)
 
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
-        """The rows-major step applies: placed records, d a multiple of 64 (<= 512),
-        2R(1+K) <= 64, no deterministic mode."""
-        return (self.rows_major and self.place and self.d % 64 == 0 and self.d <= 512
+        """The rows-major step applies: placed records, d one of the widths its kernels are
+        built for (dw_sgns_owner_out_rows and the COEFIN pass 1: 64, 128, 256, 512),
+        2R(1+K) <= 64, no deterministic mode. Other widths keep the catch-up -> pass 1 ->
+        lazy gather sequence."""
+        return (self.rows_major and self.place and self.d in ROWS_MAJOR_DIMS
                 and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64
                 and getattr(self, '_exact', None) is None)
 

@@ -371,6 +371,21 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
                          uint64_t walk_id0, int32_t *out, int32_t *status,
                          uint64_t *counters, void *stream);
 
+/* node2vec with Philox draws over the per-edge position index (n2v_rec / n2v_pos from
+ * dw_n2v_edge_index_build): one lane per walker, one 32-B edge record and log2 C dependent 4-B
+ * position loads per step, no rejection rounds. The law is Node2Vec.walk's
+ * (random_walk_generator.py:94-119, the reference's inverted q rule): step 1 picks
+ * bounded32(r.x, deg) (:97, prev None), later steps the first neighbour i whose exact prefix
+ * weight W_i = a_i/p + b_i + c_i/q exceeds U*T, U = 53 bits of (r.x, r.y), with the fp64
+ * expressions of the exact replay's pick; Philox counter (walk id lo, hi, step << 8, 'NP').
+ * Unweighted graphs (the index has no weights). counters: NULL, or uint64[4] += {load + store
+ * bytes, steps, 0, position loads}. Reads walk_id0 from a bound dw_step_scalars block. */
+int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const int32_t *n2v_pos,
+                           int64_t n_rows, const int32_t *starts, int64_t n_walks,
+                           int32_t walk_length, double p, double q, uint64_t seed,
+                           uint64_t walk_id0, int32_t *out, int32_t *status, uint64_t *counters,
+                           void *stream);
+
 /* Edge-inline CSR for DeepWalk in dw_walk_fast_indexed: edges int32[nnz][4], entry e of row u =
  * {x = col[e], deg(x), row_ptr[x] low 32 bits, row_ptr[x] high 32 bits}. The pick of the next
  * node then also yields its row: one dependent load per walk step instead of two — the
@@ -724,7 +739,7 @@ int dw_scale(float *x, int64_t n_elem, float alpha, const float *alpha_dev, void
  * the host it is launch-bound. To replay a captured step (hipGraph), the values that change from
  * step to step live in device memory instead of kernel arguments: while a dw_step_scalars block
  * is BOUND (dw_step_scalars_bind, per host thread), every launch of
- *   dw_walk_fast / dw_walk_fast_indexed   reads walk_id0 from it,
+ *   dw_walk_fast / dw_walk_fast_indexed / dw_walk_fast_positions   reads walk_id0 from it,
  *   dw_sgns_walks_phase (pass 1)          reads noise_offset from it,
  *   dw_adam_dense(_to), dw_sgns_walks_phase2_adam   read the Adam scalars adam[0..6],
  * and ignores the corresponding host arguments. dw_step_scalars_advance, the last node of a

@@ -17,6 +17,7 @@ ALWAYS = 0xFFFFFFFF
 TAG_DEEPWALK = 0x44570000
 TAG_NODE2VEC = 0x4E320000
 TAG_SGNS = 0x53470000
+TAG_N2V_POS = 0x4E500000
 
 
 def philox(c0, c1, c2, c3, k0, k1):
@@ -141,6 +142,96 @@ def fast_walks(row_ptr, col, starts: Sequence[int], length: int, method: str, p:
                             nxt = x
                             break
                     rnd += 1
+            out[w, s] = nxt
+            prev, v = v, nxt
+    return out
+
+
+def n2v_w(na: int, nb: int, nc: int, ip: float, iq: float) -> float:
+    """dw_walk.hip n2v_w: the exact prefix weight of na 1/p-, nb 1-, nc 1/q-neighbours, in the
+    kernel's fp64 evaluation order (no contraction)."""
+    return float(na) * ip + float(nb) + float(nc) * iq
+
+
+def n2v_pick_pos(P: Sequence[int], C: int, pt: int, n: int, U: float, ip: float,
+                 iq: float) -> int:
+    """dw_walk.hip n2v_pick_pos<false> (the Philox position walker's pick): with t's position pt
+    in N(v) (or -1) and the ascending positions P of the C common neighbours, the first i with
+    D_i = W(a_i, i + 1 - a_i - c_i, c_i) - U*T > 0 — a binary search over j of D at P[j], then
+    one inside the gap (P[j-1], P[j]]; the same fp64 expressions (Python floats are IEEE
+    doubles)."""
+    A = 1 if pt >= 0 else 0
+    T = n2v_w(A, n - A - C, C, ip, iq)
+    UT = U * T
+
+    def D(i: int, c: int) -> float:
+        a = 1 if (pt >= 0 and pt <= i) else 0
+        return n2v_w(a, (i + 1) - a - c, c, ip, iq) - UT
+    lo, hi = 0, C
+    while lo < hi:
+        mid = (lo + hi) >> 1
+        if D(int(P[mid]), mid + 1) > 0.0:
+            hi = mid
+        else:
+            lo = mid + 1
+    j = lo
+    pj = int(P[j]) if j < C else n - 1
+    a = int(P[j - 1]) + 1 if j > 0 else 0
+    b = pj
+    while a < b:
+        mid = (a + b) >> 1
+        if D(mid, j) > 0.0:
+            b = mid
+        else:
+            a = mid + 1
+    return a
+
+
+def uniform53(r0: int, r1: int) -> float:
+    """U from two Philox words as genrand_res53 splits them: (r0 >> 5) * 2^26 + (r1 >> 6),
+    times 2^-53 (exact)."""
+    return float(((int(r0) >> 5) << 26) | (int(r1) >> 6)) * 2.0 ** -53
+
+
+def fast_walks_positions(row_ptr, col, starts: Sequence[int], length: int, p: float, q: float,
+                         seed: int, walk_id0: int) -> np.ndarray:
+    """The walks dw_walk_fast_positions returns (node2vec, unweighted): counter (walk id lo, hi,
+    step << 8, TAG_N2V_POS); step 1 bounded32(r.x, deg) (the reference's unbiased first step,
+    random_walk_generator.py:97), later steps n2v_pick_pos with U = uniform53(r.x, r.y) over the
+    classes of the reference rule (:100-108: x == prev -> 1/p; x in N(prev) -> 1/q), positions
+    found here from the neighbour lists (what the device's per-edge index stores)."""
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    k0, k1 = seed & MASK, (seed >> 32) & MASK
+    ip, iq = 1.0 / p, 1.0 / q
+    out = np.full((len(starts), length), -1, dtype=np.int32)
+    nsets = {}
+
+    def nset(v):
+        st = nsets.get(v)
+        if st is None:
+            st = set(col[row_ptr[v]:row_ptr[v + 1]].tolist())
+            nsets[v] = st
+        return st
+    for w, start in enumerate(starts):
+        wid = walk_id0 + w
+        c0, c1 = wid & MASK, (wid >> 32) & MASK
+        v, prev = int(start), -1
+        out[w, 0] = v
+        for s in range(1, length):
+            a, b = int(row_ptr[v]), int(row_ptr[v + 1])
+            n = b - a
+            if n <= 0:
+                break
+            r = philox(c0, c1, s << 8, TAG_N2V_POS, k0, k1)
+            if prev < 0:
+                k = int(bounded32(int(r[0]), n))
+            else:
+                nb = col[a:b].tolist()
+                pt = nb.index(prev) if prev in nset(v) else -1
+                P = [i for i, x in enumerate(nb) if x != prev and x in nset(prev)]
+                k = n2v_pick_pos(P, len(P), pt, n, uniform53(int(r[0]), int(r[1])), ip, iq)
+            nxt = int(col[a + k])
             out[w, s] = nxt
             prev, v = v, nxt
     return out

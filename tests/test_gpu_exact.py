@@ -248,3 +248,38 @@ def test_exact_train_loop_eager_twice_and_graphs_bit_identical(tmp_path, hip_dev
         assert s['global_step'] == s0['global_step']
         for k, v in s0['state_dict'].items():
             assert torch.equal(v, s['state_dict'][k]), k
+
+
+def test_registry_keeps_accumulators_across_batch_shapes(hip_device):
+    """An epoch's short last batch changes grad_scale (so frac) for one step and back: the
+    registry re-registers the accumulator it already has for each (buffer, frac) instead of
+    allocating and zeroing new ones, so the buffers a captured graph adds into
+    stay allocated; and a step after the switch back gives the same gradients as a fresh
+    registry at that shape."""
+    V, d, R, K, L = 1201, 64, 2, 3, 12
+    w_in0, w_out0, walks, ins, tgt, noise = _batch(V, d, 24, L, R, K, 3)
+    w_in, w_out = torch.as_tensor(w_in0).cuda(), torch.as_tensor(w_out0).cuda()
+    wk, nz = torch.as_tensor(walks).cuda(), torch.as_tensor(noise).cuda()
+    g_in, g_out = torch.zeros_like(w_in), torch.zeros_like(w_out)
+    full, short = 1.0 / tgt.size, 1.0 / (3 * tgt.size // 8)
+    assert exact.frac_bits(full) != exact.frac_bits(short)
+    reg = exact.Registry()
+    a0 = reg.ensure(0, g_in, full)
+    acc_ptr = a0.acc.data_ptr()
+    b0 = reg.ensure(0, g_in, short)
+    assert b0 is not a0 and not a0.active and b0.active
+    a1 = reg.ensure(0, g_in, full)
+    assert a1 is a0 and a1.active and not b0.active and a1.acc.data_ptr() == acc_ptr
+    assert reg.live() == [a1]
+    reg.ensure(1, g_out, full)
+    sgns_accumulate(w_in, w_out, g_in, g_out, K, walks=wk, context_radius=R, noise=nz)
+    torch.cuda.synchronize()
+    reg.release()
+    assert int(a1.acc.abs().sum()) == 0          # the conversion left the sums cleared
+    ref_in, ref_out, _ = _exact_grads(w_in, w_out, wk, nz, R, K, full)
+    assert torch.equal(g_in.view(torch.int32), ref_in.view(torch.int32))
+    assert torch.equal(g_out.view(torch.int32), ref_out.view(torch.int32))
+    for _ in range(2 * exact.Registry.MAX_PER_KEY):      # bounded per buffer
+        reg.ensure(0, g_in, 1.0 / (tgt.size * np.random.default_rng().integers(2, 1 << 20)))
+    assert len(reg._cache[0]) <= exact.Registry.MAX_PER_KEY
+    reg.release()

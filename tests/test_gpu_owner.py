@@ -616,6 +616,25 @@ def test_rows_major_equals_gather_path(hip_device, d, wd, hub):
         assert_no_row_drift(got, exp)
 
 
+def test_owner_tables_refuse_unbuilt_width(hip_device):
+    """d = 192 is a multiple of 64, but the owner passes' kernels (k_sgns_g16's owner and
+    coefficient-input forms, k_out_rows) are built for d in {64, 128, 256, 512} only (ADVICE
+    r04): the owner tables refuse other widths when they are made, before any step could leave
+    the claim or counts changed, and the C ABI says why (no stale error text)."""
+    from shallow_encoders.word2vec.sgns import sgns_owner_pass1
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, OwnerTables
+    for cls, kw in ((OwnerTables, {}), (OwnerLazyTables, {'lazy_out': True})):
+        with pytest.raises(ValueError, match='owner layout needs d in'):
+            cls(3000, 192, hip_device, lr=0.01, init_seed=4, **kw)
+    V, d = 3000, 192
+    w_in = torch.zeros((V, d), device=hip_device)
+    walks = torch.randint(1, V, (4, 12), dtype=torch.int32).to(hip_device)
+    with pytest.raises(_native.DWError, match=r'd in \{64, 128, 256, 512\} \(got 192\)'):
+        sgns_owner_pass1(w_in, torch.zeros_like(w_in), torch.zeros_like(w_in), 3, walks=walks,
+                         context_radius=2, owner=0, n_owners=1, vocab_size=V, seed=1,
+                         noise_offset=0)
+
+
 @pytest.mark.parametrize('d,wd', [(128, 0.0), (64, 0.01)])
 def test_rows_major_bit_identical_without_collisions(hip_device, d, wd):
     """Where no two records of a step share an out row and no two centres share a node, nothing

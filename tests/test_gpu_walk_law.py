@@ -14,10 +14,12 @@ rule, restated by oracle/walk_ref.node2vec_transition and pinned by the referenc
   * node2vec first step (prev = None) and DeepWalk: uniform over N(v); chi-square over every
     neighbour of a hub (R-MAT 12 / 16, and C3's 44,848-neighbour hub for DeepWalk).
 
-The lane-group size (16 / 8 / 4 lanes per walker, picked from the batch size) and the layout
-(edge-inline + adjacency hash vs plain CSR + sorted search) do not change a walk (walks are pure
-functions of the walk id): each test asserts that on the first walks of its batch, so the law
-shown for one holds for all of them.
+Two node2vec walkers: the default over the per-edge position index (one Philox uniform against
+the exact prefix weights) and the ballot-rejection walker (layout 'hash' / 'csr'). For the
+latter the lane-group size (16 / 8 / 4 lanes per walker, picked from the batch size) and the
+layout (edge-inline + adjacency hash vs plain CSR + sorted search) do not change a walk (walks
+are pure functions of the walk id): each test asserts that on the first walks of its batch, so
+the law shown for one holds for all of them.
 
 Significance: family-wise alpha = 1e-3 with a Bonferroni correction over the N_TESTS tests of
 this module: each test passes when its p-value > 1e-3 / N_TESTS. Seeds are fixed, so the
@@ -38,7 +40,8 @@ PQ = [(0.25, 4.0), (1.0, 1.0)]
 PAIR_KINDS = ['hub-hub', 'hub-low', 'low-hub', 'mid-mid']
 GRAPHS = ['rmat12', 'rmat16']
 DW_GRAPHS = ['rmat12', 'rmat16', 'rmat20']
-N_TESTS = len(PQ) * len(GRAPHS) * (len(PAIR_KINDS) + 1) + len(DW_GRAPHS)
+WALKERS = ['positions', 'rejection']
+N_TESTS = len(PQ) * len(GRAPHS) * (len(WALKERS) * len(PAIR_KINDS) + 1) + len(DW_GRAPHS)
 ALPHA = 1e-3 / N_TESTS
 TARGET = 4000          # samples of x per (t, v) pair
 MAX_WALKS = 40_000_000
@@ -101,14 +104,16 @@ def _chi2_p(counts, expected):
     return float(chi2.sf(stat, len(counts) - 1)), stat
 
 
-def _same_across_lanes_and_layouts(make, starts, big):
-    """The walks of the first starts are the same with 16-lane batches and with the plain-CSR
-    layout as in the big (4-lane) batch."""
+def _same_across_lanes_and_layouts(make, starts, big, layout):
+    """The walks of the first starts are the same in a small batch (the rejection walker: 16
+    lanes per walker) as in the big one (4 lanes), and the rejection walker's are the same with
+    the plain-CSR layout."""
     n = min(4096, len(starts))
-    small = make('indexed').walk_batch(starts[:n], walk_id0=0)
+    small = make(layout).walk_batch(starts[:n], walk_id0=0)
     assert torch.equal(small, big[:n])
-    plain = make('csr').walk_batch(starts[:n], walk_id0=0)
-    assert torch.equal(plain, big[:n])
+    if layout == 'hash':
+        plain = make('csr').walk_batch(starts[:n], walk_id0=0)
+        assert torch.equal(plain, big[:n])
 
 
 def _bins(law, t, v, ref, n_samples):
@@ -129,12 +134,17 @@ def _bins(law, t, v, ref, n_samples):
     return bins
 
 
+@pytest.mark.parametrize('walker', WALKERS)
 @pytest.mark.parametrize('graph', GRAPHS)
 @pytest.mark.parametrize('kind', PAIR_KINDS)
 @pytest.mark.parametrize('p,q', PQ)
-def test_node2vec_second_order_law_vs_reference(graph, kind, p, q, hip_device):
+def test_node2vec_second_order_law_vs_reference(graph, kind, p, q, walker, hip_device):
+    """walker: 'positions' (the default layout on unweighted graphs: dw_walk_fast_positions,
+    one Philox uniform against the prefix weights over the position index) or 'rejection'
+    (layout 'hash' / 'csr': the ballot-rejection walker)."""
     from shallow_encoders.graph.random_walk_generator import Node2Vec
     csr, ref = _graph(graph)
+    layout = 'indexed' if walker == 'positions' else 'hash'
     t, v = _pair(csr, kind)
     deg_t, deg_v = len(ref.neighbors(t)), len(ref.neighbors(v))
     n = min(MAX_WALKS, TARGET * deg_t)
@@ -143,8 +153,10 @@ def test_node2vec_second_order_law_vs_reference(graph, kind, p, q, hip_device):
     def make(layout):
         return Node2Vec(csr, 3, p=p, q=q, rng='philox', seed=2024, layout=layout,
                         device=hip_device)
-    out = make('indexed').walk_batch(starts, walk_id0=0)
-    _same_across_lanes_and_layouts(make, starts, out)
+    out = make(layout).walk_batch(starts, walk_id0=0)
+    if walker == 'positions':
+        assert csr.device_tensors(hip_device).get('n2v_rec') is not None
+    _same_across_lanes_and_layouts(make, starts, out, layout)
     x = out[out[:, 1] == v][:, 2].cpu().numpy()
     law = walk_ref.node2vec_transition(ref, t, v, p, q)
     assert set(np.unique(x).tolist()) <= set(law), 'a step left N(v)'

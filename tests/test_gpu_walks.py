@@ -140,13 +140,14 @@ def test_replay_hub_rows_vs_oracle(method, hip_device):
     assert (got == 1).sum() > 16
 
 
-@pytest.mark.parametrize('layout,L', [('indexed', 16), ('csr', 16), ('indexed', 1),
-                                      ('indexed', 5), ('indexed', 11)])
+@pytest.mark.parametrize('layout,L', [('indexed', 16), ('hash', 16), ('csr', 16), ('indexed', 1),
+                                      ('indexed', 5), ('indexed', 11), ('hash', 5)])
 @pytest.mark.parametrize('method,weighted', [('deepwalk', False), ('deepwalk', True),
                                              ('node2vec', False), ('node2vec', True)])
 def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, layout, L, hip_device):
-    """Fast walkers vs the Philox oracle, both layouts; the inline DeepWalk walker's packed
-    stores at walk lengths that are not multiples of 4."""
+    """Fast walkers vs the Philox oracle, every layout; the inline walkers' packed stores at
+    walk lengths that are not multiples of 4. Unweighted node2vec on the default layout walks
+    over the position index (oracle fast_walks_positions), else by rejection (fast_walks)."""
     f = golden('walks_karate_deepwalk.npz')
     csr = _csr(f) if weighted else CSRGraph.from_arrays(f['row_ptr'], f['col'], None)
     starts = np.arange(1, 35, dtype=np.int32).repeat(3)
@@ -158,22 +159,53 @@ def test_fast_kernel_bit_exact_vs_philox_oracle(method, weighted, layout, L, hip
         d = csr.device_tensors(need_alias=True)
         np.testing.assert_array_equal(d['prob_thr'].cpu().numpy().view(np.uint32), prob)
         np.testing.assert_array_equal(d['alias'].cpu().numpy(), alias)
-    exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, method, 0.25, 4.0, seed=77,
-                        walk_id0=1000, prob_thr=prob, alias=alias)
+    if method == 'node2vec' and not weighted and layout == 'indexed':
+        assert csr.device_tensors().get('n2v_rec') is not None
+        exp = ph.fast_walks_positions(csr.row_ptr, csr.col, starts, L, 0.25, 4.0, seed=77,
+                                      walk_id0=1000)
+    else:
+        exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, method, 0.25, 4.0, seed=77,
+                            walk_id0=1000, prob_thr=prob, alias=alias)
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize('layout', ['indexed', 'csr'])
+@pytest.mark.parametrize('layout', ['indexed', 'hash', 'csr'])
 def test_fast_node2vec_hub_staging_vs_oracle(layout, hip_device):
-    """A hub as prev (6-level 8-ary search / a 126-bucket hash row); same walks as the oracle."""
+    """A hub as prev (6-level 8-ary search / a 126-bucket hash row; on the default layout a
+    1,500-entry position list); same walks as the oracle."""
     csr = _hub_graph(n_leaves=1500, seed=3)
     L = 8
     starts = np.array([1] * 8 + [6] * 8, dtype=np.int32)   # vocab id 1 is the hub (node 0)
     assert csr.degree()[1] > 1024
     w = Node2Vec(csr, L, p=2.0, q=0.5, rng='philox', seed=5, layout=layout)
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=0).cpu().numpy()
-    exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, 'node2vec', 2.0, 0.5, seed=5, walk_id0=0)
+    if layout == 'indexed':
+        exp = ph.fast_walks_positions(csr.row_ptr, csr.col, starts, L, 2.0, 0.5, seed=5,
+                                      walk_id0=0)
+    else:
+        exp = ph.fast_walks(csr.row_ptr, csr.col, starts, L, 'node2vec', 2.0, 0.5, seed=5,
+                            walk_id0=0)
     np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0), (0.3, 3.0), (4.0, 0.25)])
+def test_fast_positions_walker_vs_oracle_rmat12(p, q, hip_device):
+    """The Philox walker over the position index (dw_walk_fast_positions) on the R-MAT-12
+    fixture graph (hubs of ~1,000 neighbours, long position lists) from every node, bit-exact
+    against oracle/philox.fast_walks_positions; and batch-independent (a walk is a function of
+    its walk id)."""
+    f = golden('walks_rmat12_node2vec_p0.25_q4.npz')
+    csr = CSRGraph.from_arrays(f['row_ptr'], f['col'], None)
+    V = csr.vocab_size
+    starts = np.arange(1, V, dtype=np.int32)
+    starts = starts[np.diff(csr.row_ptr)[1:] > 0][:600]
+    L = 12
+    w = Node2Vec(csr, L, p=p, q=q, rng='philox', seed=31)
+    got = w.walk_batch(torch.as_tensor(starts), walk_id0=5).cpu().numpy()
+    exp = ph.fast_walks_positions(csr.row_ptr, csr.col, starts, L, p, q, seed=31, walk_id0=5)
+    np.testing.assert_array_equal(got, exp)
+    part = w.walk_batch(torch.as_tensor(starts[100:164]), walk_id0=105).cpu().numpy()
+    np.testing.assert_array_equal(part, got[100:164])
 
 
 def _probe_ok(tab, nb, key):
@@ -269,10 +301,14 @@ def test_fast_walks_rmat20_properties(hip_device):
         out = w.walk_batch(starts[:m], walk_id0=0)
         again = w.walk_batch(starts[:m], walk_id0=0)
         assert torch.equal(out, again)
-        # indexed layout (default) == plain CSR + sorted search, at scale
+        # the edge-inline / hash layout == plain CSR + sorted search, at scale (node2vec's
+        # default walks over the position index: its own stream, checked below like the rest)
         plain = (Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1, layout='csr')
                  if method == 'node2vec' else DeepWalk(csr, 80, rng='philox', seed=1, layout='csr'))
-        assert torch.equal(out, plain.walk_batch(starts[:m], walk_id0=0))
+        hashed = (Node2Vec(csr, 80, p=0.25, q=4.0, rng='philox', seed=1, layout='hash')
+                  if method == 'node2vec' else w)
+        assert torch.equal(hashed.walk_batch(starts[:m], walk_id0=0),
+                           plain.walk_batch(starts[:m], walk_id0=0))
         o = out.cpu().numpy()
         assert (o > 0).all()
         sample = o[:: max(1, m // 512)]
@@ -312,7 +348,7 @@ def test_node2vec_lane_groups_give_identical_walks(hip_device):
     csr = rmat_graph(16, 500_000, 0)
     n_big = 300_000
     starts = (torch.arange(n_big, dtype=torch.int64) % (csr.vocab_size - 1) + 1).to(torch.int32)
-    for layout in ('indexed', 'csr'):
+    for layout in ('hash', 'csr', 'indexed'):   # ('indexed': the position walker, lane per walk)
         w = Node2Vec(csr, 20, p=0.25, q=4.0, rng='philox', seed=3, layout=layout)
         big = w.walk_batch(starts, walk_id0=0)               # 4 lanes per walker
         mid = w.walk_batch(starts[:40_000], walk_id0=0)      # 8 (or 16) lanes
@@ -349,19 +385,29 @@ def test_cora_epoch_end_to_end_bit_exact(tmp_path, monkeypatch, hip_device):
 
 
 def test_counted_node2vec_walks_equal_and_count(hip_device):
-    """dw_walk_fast_counted (bench.py's walk roofline): the same walks as the indexed walker,
-    every step counted, at least the fixed per-step loads / store counted as bytes."""
+    """The counted launches (bench.py's walk roofline): the same walks as the walker, every step
+    counted, at least the fixed per-step loads / store counted as bytes — dw_walk_fast_counted
+    for the rejection walker (layout 'hash'), dw_walk_fast_positions with counters for the
+    default position walker (one 32-B record and a 4-B output per step, 4 B per position
+    load, no proposal blocks)."""
     csr = rmat_graph(16, 600_000, 0)
-    w = Node2Vec(csr, 20, p=0.25, q=4.0, rng='philox', seed=3)
-    for n in (4096, 200_000):                     # 16-lane and 4-lane groups
-        starts = (torch.arange(n, dtype=torch.int64) % (csr.vocab_size - 1) + 1).to(torch.int32)
-        ref = w.walk_batch(starts, walk_id0=5)
-        out = torch.empty_like(ref)
-        c = w.count_traffic(starts, walk_id0=5, out=out)
-        assert torch.equal(out, ref)
-        assert c['steps'] == n * 19
-        assert c['blocks'] >= c['steps'] - n        # >= one proposal block per biased step
-        assert c['bytes'] >= c['steps'] * 36 + c['blocks'] * 16
+    for layout in ('hash', 'indexed'):
+        w = Node2Vec(csr, 20, p=0.25, q=4.0, rng='philox', seed=3, layout=layout)
+        for n in (4096, 200_000):                     # 16-lane and 4-lane groups
+            starts = (torch.arange(n, dtype=torch.int64) % (csr.vocab_size - 1) + 1).to(
+                torch.int32)
+            ref = w.walk_batch(starts, walk_id0=5)
+            out = torch.empty_like(ref)
+            c = w.count_traffic(starts, walk_id0=5, out=out)
+            assert torch.equal(out, ref)
+            assert c['steps'] == n * 19
+            if layout == 'hash':
+                assert c['blocks'] >= c['steps'] - n    # >= one proposal block per biased step
+                assert c['bytes'] >= c['steps'] * 36 + c['blocks'] * 16
+            else:
+                assert c['walker'] == 'dw_walk_fast_positions' and c['blocks'] == 0
+                assert c['bytes'] == c['steps'] * 36 + 4 * c['position_loads'] + n * 20
+                assert c['position_loads'] > 0
 
 
 @pytest.mark.parametrize('method,p,q,n_walks,L', [('deepwalk', 1.0, 1.0, 65_536, 40),
