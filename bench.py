@@ -370,6 +370,12 @@ def main():
                     help='lazy in-table exchange: keep the out slice\'s Adam lazy (exact) too; '
                          'auto = when a step\'s records touch under ~half of the slice\'s rows '
                          '(C3 at 64-walk batches)')
+    ap.add_argument('--layout-calib', default='auto', choices=['auto', 'on', 'off'],
+                    help='N > 1, owner layout: also time --calib-steps steps of the replicated '
+                         'layout (north_star\'s: node-id-range Adam shards, reduce-scatter + '
+                         'all-gather = an all-reduce of both tables\' gradients) on this job, '
+                         'report both (layout_calibration_ms_per_step) and run the faster; '
+                         'auto = at C3 (C5\'s dense exchange is 2 x 17 GB per step)')
     ap.add_argument('--calib-steps', type=int, default=8,
                     help='--in-exchange auto: timed steps per protocol')
     ap.add_argument('--graph-unroll', type=int, default=0,
@@ -434,7 +440,18 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device('cuda', local_rank)
     torch.cuda.set_device(dev)
+    rc = run(args, world, rank, local_rank, backend, dist_on, dev)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rc:
+        sys.exit(rc)
 
+
+def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: bool, dev) -> int:
+    """The benchmark on this rank (process group already up when dist_on); prints the JSON line
+    on rank 0 and returns the exit status (3: a step check failed). The N > 1 layout calibration
+    may hand the run over to a fresh call with the faster layout."""
     from shallow_encoders import _native
     from shallow_encoders.graph.random_walk_generator import DeepWalk, Node2Vec
     from shallow_encoders.graph.rmat import rmat_graph
@@ -736,6 +753,56 @@ def main():
         tables = owner_tables(lazy)
         log(rank, f'[bench] in-table exchange calibration (ms/step): {calib_ms} -> '
                   f'{args.in_exchange}')
+    # ---- north_star's layout timed beside the owner layout on this job --------
+    layout_ms = getattr(args, 'layout_result', None)
+    want_layout = (dist_on and owner and not emulate and args.layout_calib != 'off'
+                   and (args.layout_calib == 'on' or args.config == 'c3'))
+    if want_layout:
+        def timed_steps(step_fn) -> float:
+            for _ in range(max(1, args.warmup)):
+                step_fn()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            a = time.perf_counter()
+            for _ in range(args.calib_steps):
+                step_fn()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - a], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t) / args.calib_steps * 1e3
+
+        owner_ms = min(calib_ms.values()) if calib_ms else timed_steps(lambda: one_step(False))
+        rt = ShardedTables(V, d, dev, lr=args.lr, init_seed=0,
+                           out_pieces=None if args.no_out_pieces else args.out_pieces)
+        r_walks = torch.empty((B, L), dtype=torch.int32, device=dev)
+        r_starts = torch.empty(B, dtype=torch.int32, device=dev)
+        r_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        r_status = torch.zeros(1, dtype=torch.int32, device=dev)
+        r_idx = [0]
+
+        def repl_step():   # the replicated layout's step (bench.py --dist-mode replicated)
+            g0 = (r_idx[0] * world + rank) * B
+            r_idx[0] += 1
+            walker.walk_batch(step_starts(g0, B, r_starts), walk_id0=g0, out=r_walks,
+                              check=False)
+            replicated_step(rt, r_walks, R, K, seed=99, noise_offset=g0 * (L - 2 * R),
+                            grad_scale=1.0 / (pairs_per_step * world), loss_acc=r_acc,
+                            status=r_status, scatter='sorted', fuse_out_adam=False,
+                            pieces=not args.no_out_pieces)
+        repl_ms = timed_steps(repl_step)
+        _native.check_status(r_status, 'bench layout calibration')
+        del rt, r_walks
+        torch.cuda.empty_cache()
+        layout_ms = {'owner': owner_ms, 'replicated': repl_ms}
+        log(rank, f'[bench] layout calibration (ms/step): {layout_ms}')
+        if repl_ms < owner_ms:   # north_star's layout is faster on this job: run it instead
+            import copy
+            del tables
+            torch.cuda.empty_cache()
+            a2 = copy.copy(args)
+            a2.dist_mode, a2.layout_calib, a2.layout_result = 'replicated', 'off', layout_ms
+            return run(a2, world, rank, local_rank, backend, dist_on, dev)
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize(dev)
@@ -854,21 +921,39 @@ def main():
     # perturbs one sampled out row in the last rank's shard after the step: the check must fail.
     step_check = None
     want_check = (args.verify_step == 'on' or
-                  (args.verify_step == 'auto' and owner and dist_on))
-    if want_check and owner and not emulate and graphed is None and \
-            args.owner_walks == 'gather' and V * d * 4 * 6 <= (16 << 30):
+                  (args.verify_step == 'auto' and dist_on))
+    if want_check and (owner or dist_on) and not emulate and graphed is None and \
+            (not owner or args.owner_walks == 'gather') and V * d * 4 * 6 <= (16 << 30):
         from shallow_encoders.word2vec import verify
         loss_keep = loss_acc.clone()
-        g0 = step_idx[0] * BG
+        # the checked step's global batch: owner — every rank's walks_buf; replicated — rank r's
+        # B walks are global ids (s * world + r) * B.., gathered in rank order below
+        g0 = step_idx[0] * (BG if owner else world * B)
         pre = tables.full_state()
         one_step(False)
         torch.cuda.synchronize(dev)
         _native.check_status(status, 'bench step check')
-        walks_chk = walks_buf.clone()
+        if owner:
+            walks_chk = walks_buf.clone()
+        else:
+            mine = feed.walks[0][:B].contiguous()
+            walks_chk = torch.empty((world * B, L), dtype=torch.int32, device=dev)
+            if dist_on:
+                if backend == 'nccl':
+                    dist.all_gather_into_tensor(walks_chk.view(-1), mine.view(-1))
+                else:
+                    dist.all_gather(list(walks_chk.view(world, B, L).unbind(0)), mine.clone())
+            else:
+                walks_chk.copy_(mine)
         rows_in, rows_out = verify.sample_rows(walks_chk, R, K, V, 99, g0 * (L - 2 * R), 256)
         if os.environ.get('DW_BENCH_CORRUPT') == '1' and tables.rank == tables.world - 1:
-            bad = rows_out[rows_out % tables.world == tables.rank][0]
-            tables.m_out[int(bad) // tables.world] += 1e-3   # a corrupted shard row (test aid)
+            if owner:
+                bad = rows_out[rows_out % tables.world == tables.rank][0]
+                tables.m_out[int(bad) // tables.world] += 1e-3   # a corrupted shard row
+            else:   # an out row whose Adam state this rank holds
+                mine_rows = tables.state_rows(1).to(dev)
+                hit = torch.nonzero(torch.isin(mine_rows, rows_out)).flatten()
+                tables.m[1][int(hit[0])] += 1e-3
         post = tables.full_state()
         loss_acc.copy_(loss_keep)
         if rank == 0:
@@ -1118,6 +1203,8 @@ def main():
                 f'in-table exchange overlapped'
                 + (f', out table in {tables.P} pieces pipelined' if pieces else '') + ')'),
         },
+        'layout': args.dist_mode if dist_on else None,
+        'layout_calibration_ms_per_step': layout_ms,
         'deterministic': bool(args.deterministic),
         'in_exchange': args.in_exchange if owner else None,
         'in_exchange_calibration_ms_per_step': calib_ms,
@@ -1227,11 +1314,10 @@ def main():
         flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)   # every rank exits with rank 0's verdict
         failed = bool(flag.item())
-        dist.barrier()
-        dist.destroy_process_group()
     if failed:
         log(rank, f'[bench] step check FAILED: {step_check}')
-        sys.exit(3)
+        return 3
+    return 0
 
 
 if __name__ == '__main__':

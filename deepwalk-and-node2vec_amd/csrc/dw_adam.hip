@@ -110,7 +110,7 @@ using dw::hist_at;
 template <bool STEP, bool P_ONLY = false, int E = 1>
 __global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
-                int32_t *__restrict__ last, int64_t n_table, int32_t d,
+                int32_t *__restrict__ last, uint8_t *__restrict__ pend, int64_t n_table, int32_t d,
                 const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
                 int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
                 int32_t step_arg, const dw_step_scalars *__restrict__ dyn, int32_t delta) {
@@ -128,8 +128,10 @@ __global__ void __launch_bounds__(512)
         const int64_t r = rows ? static_cast<int64_t>(rows[i]) : i;
         // an out-of-range centre is reported by the SGNS pass
         const int32_t from = r < n_table ? __builtin_amdgcn_readfirstlane(last[r]) : step;
+        // a row the lazy out step left pending: p lags m and v by the parameter half of `from`
+        const bool pd = pend && r < n_table && __builtin_amdgcn_readfirstlane(pend[r]) != 0;
         __syncthreads();   // every wave has read last[r] before thread 0 advances it
-        if (from >= (STEP ? step : upto)) continue;   // already current (or stepped)
+        if (from >= (STEP ? step : upto) && !pd) continue;   // already current (or stepped)
         const int64_t o = r * d + e;
         float pr[E], mr[E], vr[E], gg[E];
         if constexpr (E == 2) {   // (d even: o is 8-B aligned)
@@ -147,6 +149,7 @@ __global__ void __launch_bounds__(512)
             vr[0] = live ? v[o] : 0.f;
             gg[0] = (STEP && live) ? g_rows[i * d + e] : 0.f;
         }
+        if (pd) dw::settle_pending(pr, mr, vr, hist, from);
         dw::replay_g0(pr, mr, vr, hist, from, upto, box_from);
         if (STEP) {
             const dw::AdamScalars hs = hist_at(hist, step);
@@ -168,7 +171,10 @@ __global__ void __launch_bounds__(512)
                 }
             }
         }
-        if (e == 0 && !P_ONLY) last[r] = STEP ? step : upto;
+        if (e == 0 && !P_ONLY) {
+            last[r] = STEP ? step : upto;
+            if (pd) pend[r] = 0;
+        }
     }
 }
 
@@ -299,7 +305,7 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
 }  // extern "C"
 
 int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                         int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                         uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                          const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                          const float *hist, int32_t step, bool p_only, hipStream_t st) {
     DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0 && step >= 0,
@@ -316,6 +322,7 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     int64_t blocks = n_rows_max;   // one block per row (grid-stride beyond the cap)
     if (blocks > 65536) blocks = 65536;
     DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
+    DW_REQUIRE(!(p_only && pending), "dw_adam_rows: p_only replays do not settle pending rows");
     // even d: two elements per thread on the packed instructions
     const bool pair = dim % 2 == 0;
     const int threads = pair ? 64 * ((dim / 2 + 63) / 64) : 64 * ((dim + 63) / 64);
@@ -324,12 +331,14 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
         if (pair)                                                                               \
             hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 2>), dim3((unsigned)blocks),         \
                                dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
-                               n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, \
+                               pending, n_table_rows, dim, rows, n_rows_dev, n_rows_max,        \
+                               grad_rows, hist,                                                 \
                                step, dyn, delta);                                               \
         else                                                                                    \
             hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 1>), dim3((unsigned)blocks),         \
                                dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
-                               n_table_rows, dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, \
+                               pending, n_table_rows, dim, rows, n_rows_dev, n_rows_max,        \
+                               grad_rows, hist,                                                 \
                                step, dyn, delta);                                               \
     } while (0)
     if (grad_rows)
@@ -346,10 +355,11 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
 extern "C" {
 
 int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                 uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                  const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                  const float *hist, int32_t step, void *stream) {
-    return dw::adam_rows_launch(param, exp_avg, exp_avg_sq, last_step, n_table_rows, dim, rows,
+    return dw::adam_rows_launch(param, exp_avg, exp_avg_sq, last_step, pending, n_table_rows,
+                                dim, rows,
                                 n_rows_dev, n_rows_max, grad_rows, hist, step, false,
                                 dw::as_stream(stream));
 }

@@ -141,18 +141,32 @@ __device__ __forceinline__ float div_bc2s(float x, const AdamScalars &s) {
     return x / s.bc2s;
 }
 
-__device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
-                                          const AdamScalars &s) {
-    // No implicit FMA contraction: each element rounds the same way whichever unrolled slot,
-    // grid size or fused kernel (k_rec_gather) updates it; the lerp's fmaf is explicit.
+// adam_elem in its two halves: the moments (adam_mv: m and v from g, weight decay reading p as
+// it was before the step) and the parameter (adam_p: p from the new m and v). The lazy out step
+// (dw_sgns_owner_out_rows) applies the first at step s and leaves the second pending until the
+// row is next read (dw::settle_pending): the same operations on the same values, the same bits.
+__device__ __forceinline__ void adam_mv(float p, float &g, float &m, float &v,
+                                        const AdamScalars &s) {
 #pragma clang fp contract(off)
     float gg = g;
     if (s.wd != 0.f) gg = gg + s.wd * p;
     m = fmaf(s.w1, gg - m, m);  // lerp with weight < 0.5: self + weight * (end - self)
     v = v * s.b2;
     v = v + s.omb2 * gg * gg;
+}
+
+__device__ __forceinline__ void adam_p(float &p, float m, float v, const AdamScalars &s) {
+#pragma clang fp contract(off)
     const float denom = div_bc2s(sqrtf(v), s) + s.eps;
     p = p + s.nstep * (m / denom);
+}
+
+__device__ __forceinline__ void adam_elem(float &p, float &g, float &m, float &v,
+                                          const AdamScalars &s) {
+    // No implicit FMA contraction: each element rounds the same way whichever unrolled slot,
+    // grid size or fused kernel (k_rec_gather) updates it; the lerp's fmaf is explicit.
+    adam_mv(p, g, m, v, s);
+    adam_p(p, m, v, s);
 }
 
 // adam_elem with g = 0 when weight_decay == 0 (the lazy replays' deferred steps; callers test
@@ -374,6 +388,19 @@ __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&
     }
 }
 
+// A row left pending by the lazy out step (m, v at step `at`, p at at - 1): the parameter half
+// of step `at` (adam_p with that step's scalars), which makes the row current to `at`.
+template <int N>
+__device__ __forceinline__ void settle_pending(float (&p)[N], const float (&m)[N],
+                                               const float (&v)[N],
+                                               const float *__restrict__ hist, int32_t at) {
+    // (the scalars through the scalar unit: a vector load here would make the wave wait for
+    // every load issued before it — vector loads return in order)
+    const AdamScalars h = hist_at_const((const const_float *)hist + 8 * static_cast<int64_t>(at));
+#pragma unroll
+    for (int k = 0; k < N; ++k) adam_p(p[k], m[k], v[k], h);
+}
+
 // The Adam scalars a kernel uses: the bound step block's when there is one (graph replay),
 // else the launch's by-value ones.
 __device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
@@ -387,7 +414,7 @@ __device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
 // (m, v and last[] untouched) — the lazy out slice's catch-up before pass 1, whose lazy gather
 // then replays m and v itself (their g = 0 recurrences are a multiply each) before the step.
 int adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                     int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                     uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                      const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                      const float *hist, int32_t step, bool p_only, hipStream_t stream);
 

@@ -410,9 +410,9 @@ __device__ __forceinline__ float row_sum16(float x) {
 // (dw::to_fixed), each lane adding its 4 F4 elements of its group's centre straight from
 // registers (no LDS staging, no run summing: integer sums need no order).
 // COEFIN (the rows-major step, after k_out_rows; one owner or many, placed records): slot
-// b T + t's coefficient is already in ((float *) rec_val)[b T + t] and its row's pre-step
-// values p^{s-1} in w_out[b T + t] (k_out_rows' copies, by slot: the same addressing as the
-// table rows, no indirection): only the centre gradient is formed — the same FMAs in the same
+// b T + t's coefficient is already in ((float *) rec_val)[b T + t] and its row holds its
+// pre-step values p^{s-1} (k_out_rows leaves the rows it steps pending: m and v at step s, the
+// parameter half deferred): only the centre gradient is formed — the same FMAs in the same
 // order as the full pass.
 template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false, bool COEFIN = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
@@ -570,10 +570,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             for (int u = 0; u < CHR; ++u) {
                 const int t = t0 + u;
                 rid[u] = (t < n_own) ? s_id[wv][q][t] : -1;
-                // COEFIN: the row's pre-step values as k_out_rows left them, by slot
-                const int64_t at = rid[u] < 0 ? 0
-                                   : COEFIN ? b * T + static_cast<int64_t>(s_t[wv][q][t])
-                                            : static_cast<int64_t>(rid[u]);
+                // (COEFIN: the table row holds p^{s-1}, k_out_rows left it pending)
+                const int64_t at = rid[u] < 0 ? 0 : static_cast<int64_t>(rid[u]);
                 const float *row = a.w_out + at * D + 4 * gl;
 #pragma unroll
                 for (int f = 0; f < F4; ++f)
@@ -784,6 +782,10 @@ struct OutAdam {
     bool p_current = false;   // lazy form: the catch-up brought p (not m, v, last) to step - 1
     bool betas_const = false; //   and every step had the same betas: m, v replay with step's
     uint32_t *counts = nullptr;   // placed records: the rows' counts, cleared as they step
+    // the rows-major step (dw_sgns_owner_out_rows): rows end PENDING — m, v at `step`, p at
+    // step - 1 (the centre pass then reads p^{s-1} from the table itself), pend[row] = 1; a
+    // pending row is settled (dw::settle_pending) before its next replay
+    uint8_t *pend = nullptr;
 };
 
 // One row's lazy Adam step (one wave, VPL elements per lane): replay the missed steps, apply
@@ -793,6 +795,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
                                               int32_t d, int lane, const float (&g)[VPL]) {
     // (row is wave-uniform; lanes past d carry zeros through a uniform replay loop)
     const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
+    const bool pd = oa.pend && __builtin_amdgcn_readfirstlane(oa.pend[row]) != 0;
     const int64_t o = static_cast<int64_t>(row) * d + lane;
     float pp[VPL], mm[VPL], vv[VPL], gg[VPL];
 #pragma unroll
@@ -833,13 +836,17 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
             }
         }
     } else {
+        if (pd) dw::settle_pending(pp, mm, vv, oa.hist, from);
         dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1, dw::hist_box_from(oa.hist));
     }
     const dw::AdamScalars h = dw::hist_at(oa.hist, step);
 #pragma unroll
     for (int m = 0; m < VPL; ++m) {
         if (MASKED && lane + WAVE * m >= d) continue;
-        dw::adam_elem(pp[m], gg[m], mm[m], vv[m], h);
+        if (oa.pend)   // the rows-major step's boundary rows: leave the parameter half pending
+            dw::adam_mv(pp[m], gg[m], mm[m], vv[m], h);
+        else
+            dw::adam_elem(pp[m], gg[m], mm[m], vv[m], h);
         const int64_t i = o + WAVE * m;
         oa.p[i] = pp[m];
         oa.m[i] = mm[m];
@@ -848,6 +855,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
     if (lane == 0) {
         oa.last[row] = step;
         if (oa.counts) oa.counts[row] = 0u;   // placed records: the count back to zero
+        if (oa.pend) oa.pend[row] = 1;
     }
 }
 
@@ -1405,7 +1413,10 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // row staged in LDS: the same bits), the coefficient (row_coef, the loss sums), the gradient
 // sum over its records in placed order (the gather's order) and the Adam step. For the centre
 // pass (dw_sgns_owner_pass1 with order_ready & 4, k_sgns_g16's COEFIN form) it leaves, by slot,
-// each record's coefficient in coef_slot and its row's p^{s-1} in p_prev.
+// each record's coefficient in coef_slot, and each row PENDING: m and v at step s, p at s - 1 in
+// the table (oa.pend[row] = 1), where the centre pass reads it; the parameter half of step s is
+// applied (dw::settle_pending) when the row is next replayed or flushed — the same operations
+// as adam_elem's, so the same bits, without a per-slot copy of p^{s-1} (138 MB at C3/64).
 // A wave takes gch <= 64 placed records (lane = record: slots and centre nodes looked up in one
 // round trip) and their rows one at a time, four records' centre rows in flight (one per 16-lane
 // group for the logits). A row that straddles the chunk (its first or last row continues in the
@@ -1415,16 +1426,20 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
 // ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
 // 138-VGPR kernel ran three waves per SIMD.)
-// The kernel is latency-bound — a row's load, replay, centre rows and step in sequence, one
-// row in flight per wave — so at d <= 128 the register allocation is held to eight waves per
-// SIMD (276 us at C3's 64-walk batch; 296 us at five waves unbounded; the next row's loads
-// issued ahead of the replay measured 279-306 us at five to eight waves).
+// The kernel is latency-bound (SQ counters at C3's 64-walk batch: waves parked on memory 68% of
+// their cycles): a row took three dependent round trips — its p / m / v, then its records'
+// centre rows (two loads, one after the other) — and a chunk of ~30 rows ran them in sequence.
+// Now each row's first-round centre rows (independent of the replay) are issued together with
+// the row, and the next row's p / m / v / last / pend are issued before this row's replay (after
+// its centre rows, so waiting for those never waits for the prefetch: loads return in order),
+// so one round trip is left exposed per row; the registers this takes hold the kernel at six
+// waves per SIMD (OUT_ROWS_WAVES; the chunks are sized so that every wave is resident at once).
+constexpr int OUT_ROWS_WAVES = 6;
 template <int F4>
-__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
+__global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
-               float *__restrict__ g_out, float *__restrict__ p_prev,
-               float *__restrict__ coef_slot) {
+               float *__restrict__ g_out, float *__restrict__ coef_slot) {
     constexpr int D = 64 * F4;
     constexpr int RU = 4;   // records per round (one per 16-lane group)
     __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
@@ -1466,46 +1481,84 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
         if (is_start) s_rs[wv][__popcll(starts & lt)] = static_cast<uint8_t>(lane);
         if (lane == 0) s_rs[wv][nrows] = static_cast<uint8_t>(n_in);
         dw::wave_lds_sync();
+        // the next row's state, loaded one row ahead
+        float np[F4], nm[F4], nv[F4];
+        int32_t nlast = 0;
+        uint32_t npend = 0;
+        auto prefetch = [&](int k) {
+            const uint32_t r = __builtin_amdgcn_readlane(my_key, s_rs[wv][k]);
+            const int64_t o = static_cast<int64_t>(r) * D + lane;
+            nlast = oa.last[r];
+            npend = oa.pend[r];
+#pragma unroll
+            for (int f = 0; f < F4; ++f) {
+                np[f] = oa.p[o + 64 * f];
+                nm[f] = oa.m[o + 64 * f];
+                nv[f] = oa.v[o + 64 * f];
+            }
+        };
+        if (nrows > 0) prefetch(0);
         for (int k = 0; k < nrows; ++k) {
             const int rs = s_rs[wv][k], re = s_rs[wv][k + 1];   // (wave-uniform)
             const uint32_t row = __builtin_amdgcn_readlane(my_key, rs);
             const bool straddle = row == before || row == after;
             const int64_t ro = static_cast<int64_t>(row) * D + lane;
-            const int32_t from = __builtin_amdgcn_readfirstlane(oa.last[row]);
+            const int cnt = re - rs;
             float p[F4], m[F4], v[F4], g[F4];
 #pragma unroll
             for (int f = 0; f < F4; ++f) {
-                p[f] = oa.p[ro + 64 * f];
-                m[f] = oa.m[ro + 64 * f];
-                v[f] = oa.v[ro + 64 * f];
+                p[f] = np[f];
+                m[f] = nm[f];
+                v[f] = nv[f];
                 g[f] = 0.f;
             }
+            const int32_t from = __builtin_amdgcn_readfirstlane(nlast);
+            const bool pd = __builtin_amdgcn_readfirstlane(npend) != 0;
+            // this row's prefetched loads (issued a row ago) are complete before the next loads
+            // go out, so that waiting for those never waits for these and the compiler does not
+            // hold them back behind this row's (vector loads return in order)
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) (gfx9 encoding; expcnt, lgkmcnt free)
+            // round 0's centre rows (group q: record q of the row; lane gl: elements
+            // [4gl + 64f, +4)), then the next row's loads — both in flight during the replay
+            float4 c4[F4];
+            {
+                const int32_t cid = __shfl(my_cid, (rs + q) & (WAVE - 1), WAVE);
+                const bool ok = q < cnt && cid >= 0 && cid < a.V;
+                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+#pragma unroll
+                for (int f = 0; f < F4; ++f)
+                    c4[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            prefetch(k + 1 < nrows ? k + 1 : k);   // (unconditional: no register copies)
+            if (pd) dw::settle_pending(p, m, v, oa.hist, from);     // the previous step's p half
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
             for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
             dw::wave_lds_sync();
-            const int cnt = re - rs;
             for (int j0 = 0; j0 < cnt; j0 += RU) {
-                // group q: record j0 + q's logit in pass 1's layout (lane gl: elements
-                // [4gl + 64f, +4)) and coefficient (the first round's centre rows loaded with
-                // the row's own, ahead of the replay, measured 300 vs 276 us: more spills)
+                // group q: record j0 + q's logit in pass 1's layout and its coefficient
                 const int src = (rs + j0 + q) & (WAVE - 1);
                 const bool in = j0 + q < cnt;
                 const uint32_t slot = __shfl(my_slot, src, WAVE);
                 const int32_t cid = __shfl(my_cid, src, WAVE);
                 const bool ok = in && cid >= 0 && cid < a.V;
-                const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+                if (j0 > 0) {   // later rounds (rows of more than RU records)
+                    const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
+#pragma unroll
+                    for (int f = 0; f < F4; ++f)
+                        c4[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
                 float pr = 0.f;   // pass 1's order: x, y, z, w of each float4, then the DPP sum
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
-                    const float4 cf = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
                     const float4 of = s_p[wv][gl + 16 * f];
-                    pr = fmaf(cf.x, of.x, pr);
-                    pr = fmaf(cf.y, of.y, pr);
-                    pr = fmaf(cf.z, of.z, pr);
-                    pr = fmaf(cf.w, of.w, pr);
-                    s_c[wv][q][gl + 16 * f] = cf;
+                    pr = fmaf(c4[f].x, of.x, pr);
+                    pr = fmaf(c4[f].y, of.y, pr);
+                    pr = fmaf(c4[f].z, of.z, pr);
+                    pr = fmaf(c4[f].w, of.w, pr);
+                    s_c[wv][q][gl + 16 * f] = c4[f];
                 }
                 const float x = row_sum16(pr);
                 const int t = static_cast<int>(slot % static_cast<uint32_t>(T));
@@ -1516,19 +1569,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
                 if (in && gl == 0) coef_slot[slot] = coef;
                 dw::wave_lds_sync();
                 // the gradient over the round's records in placed order (lane-strided elements,
-                // the gather's accumulation), and each record's copy of p^{s-1}
+                // the gather's accumulation)
 #pragma unroll
                 for (int u = 0; u < RU; ++u) {
                     if (j0 + u >= cnt) break;
                     const float cu = __shfl(coef, u << 4, WAVE);
-                    const uint32_t su = __shfl(slot, u << 4, WAVE);
                     const float *cr = reinterpret_cast<const float *>(&s_c[wv][u][0]);
-                    float *pv = p_prev + static_cast<int64_t>(su) * D + lane;
 #pragma unroll
-                    for (int f = 0; f < F4; ++f) {
-                        g[f] += cu * cr[lane + 64 * f];
-                        pv[64 * f] = p[f];
-                    }
+                    for (int f = 0; f < F4; ++f) g[f] += cu * cr[lane + 64 * f];
                 }
                 dw::wave_lds_sync();   // s_c is rewritten next round
             }
@@ -1536,15 +1584,18 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? 8 : 2)
 #pragma unroll
                 for (int f = 0; f < F4; ++f) atomicAdd(g_out + ro + 64 * f, g[f]);
             } else {
+                // the moments of step s; p stays p^{s-1} for the centre pass, which reads it from
+                // the table (no per-slot copies), and the parameter half waits (pend[row])
 #pragma unroll
                 for (int f = 0; f < F4; ++f) {
-                    dw::adam_elem(p[f], g[f], m[f], v[f], hs);
+                    dw::adam_mv(p[f], g[f], m[f], v[f], hs);
                     oa.p[ro + 64 * f] = p[f];
                     oa.m[ro + 64 * f] = m[f];
                     oa.v[ro + 64 * f] = v[f];
                 }
                 if (lane == 0) {
                     oa.last[row] = step;
+                    oa.pend[row] = 1;
                     if (oa.counts) oa.counts[row] = 0u;
                 }
             }
@@ -2727,7 +2778,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     // the listed rows (at most min(local_rows, B' * T)) replay their steps up to step - 1 (p_only:
     // only p is written back; the lazy gather replays m and v itself, cheaply, before the step)
     const int64_t n_max = std::min<int64_t>(local_rows, a.batch * T);
-    return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, local_rows, dim, rows_buf,
+    return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, nullptr, local_rows, dim,
+                                rows_buf,
                                 n_rows, n_max, nullptr, hist, step - 1, p_only, st);
 }
 
@@ -3039,8 +3091,8 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
                            const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                            float grad_scale, const float *w_in, float *w_out_local,
                            float *g_out_local, float *m_out, float *v_out, int32_t *last_step,
-                           uint32_t *counts, const float *hist, int32_t step, float *p_prev,
-                           int64_t p_prev_rows, double *loss_acc, int32_t *status,
+                           uint32_t *counts, uint8_t *pending, const float *hist,
+                           int32_t step, double *loss_acc, int32_t *status,
                            void *workspace, size_t workspace_bytes, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    dim >= 1 && vocab_size >= 1 && neg_samples >= 0 && n_owners >= 1 &&
@@ -3054,13 +3106,10 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
                "dw_sgns_owner_out_rows: the owners' rows do not cover the vocabulary");
     if (n_walks == 0) return DW_OK;
     DW_REQUIRE(walks && w_in && w_out_local && g_out_local && m_out && v_out && last_step &&
-                   counts && hist && p_prev && status,
+                   counts && pending && hist && status,
                "dw_sgns_owner_out_rows: null pointer");
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
     const int64_t n_centres = n_walks * (walk_length - 2 * context_radius);
-    DW_REQUIRE(p_prev_rows >= n_centres * T, "dw_sgns_owner_out_rows: p_prev holds %lld rows, "
-               "the batch places %lld records", (long long)p_prev_rows,
-               (long long)(n_centres * T));
     hipStream_t st = dw::as_stream(stream);
     SgnsArgs a = base_args(vocab_size, dim, neg_samples, w_in, w_out_local, nullptr, g_out_local,
                            noise, seed, noise_offset, grad_scale, loss_acc, status);
@@ -3084,14 +3133,15 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     if (rc != DW_OK) return rc;
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
     oa.counts = counts;   // (p_current false: k_lazy_boundary replays the straddling rows whole)
+    oa.pend = pending;    // the stepped rows are left pending (p at step - 1 for the centre pass)
     rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;
     // records per chunk (<= 64: one per lane): as few as keep every chunk's wave resident at
-    // once (eight waves per SIMD, k_out_rows' bound) — every wave then runs from the start, where
+    // once (OUT_ROWS_WAVES per SIMD, k_out_rows' bound) — every wave then runs from the start, where
     // 32-record chunks left C3's 64-walk batch (269K records) ~200 waves for a second round that
     // doubled the kernel — and no fewer than 16
     const int64_t bound = n_centres * T;
-    const int64_t resident = grid_cap(32);
+    const int64_t resident = grid_cap(4 * OUT_ROWS_WAVES);
     int32_t gch = static_cast<int32_t>((bound + resident - 1) / resident);
     gch = gch < 16 ? 16 : gch > 64 ? 64 : gch;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
@@ -3099,10 +3149,10 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     switch (dim / 64) {
-        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
-        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
-        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
-        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, p_prev, reinterpret_cast<float *>(ws.v0)); break;
+        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
+        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
+        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
+        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
         default:
             dw::set_error("dw_sgns_owner_out_rows: d must be one of 64, 128, 256, 512 (got %d)", dim);
             return DW_E_UNSUPPORTED;

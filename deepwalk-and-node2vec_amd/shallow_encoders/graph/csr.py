@@ -411,8 +411,16 @@ class CSRGraph:
         d = self.device_tensors(device, need_sorted=True)
         if d.get('simple_ok'):
             return
+        d.pop('simple_ok', None)
         _native.check_status(d['simple_status'], 'CSR check (node2vec replay)')
         d['simple_ok'] = True
+
+    def is_simple(self, device=None) -> bool:
+        """require_simple without raising (the Philox walker then keeps the rejection form)."""
+        d = self.device_tensors(device, need_sorted=True)
+        if 'simple_ok' not in d:
+            d['simple_ok'] = int(d['simple_status'].item()) == 0   # one synchronisation
+        return bool(d['simple_ok'])
 
     def _build_alias(self, dev) -> None:
         d = self._dev

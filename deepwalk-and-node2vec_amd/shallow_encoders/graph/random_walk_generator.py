@@ -241,7 +241,7 @@ class RandomWalk(ABC):
                                      need_hub_bits=replay_n2v_idx,
                                      need_edge_cn=replay_n2v_idx and _edge_cn_enabled(),
                                      need_n2v_index=replay_n2v_idx and _n2v_index_enabled())
-        if (self._rng == 'python' and n2v) or pos_fast:
+        if self._rng == 'python' and n2v:
             self._csr.require_simple(dev)   # no repeated neighbour (nx.Graph's invariant)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
@@ -309,11 +309,13 @@ class RandomWalk(ABC):
         return out
 
     def _positions_walker(self, dev) -> bool:
-        """rng='philox', node2vec, layout='indexed', unweighted: True when the per-edge position
-        index is (or can be) built for this graph and device — then dw_walk_fast_positions
-        walks; else the rejection walker over the adjacency hash."""
+        """rng='philox', node2vec, layout='indexed', unweighted, simple rows: True when the
+        per-edge position index is (or can be) built for this graph and device — then
+        dw_walk_fast_positions walks; else the rejection walker over the adjacency hash."""
         if not (self._rng == 'philox' and self.METHOD == _native.DW_METHOD_NODE2VEC
                 and self._layout == 'indexed' and self._csr.weights is None):
+            return False
+        if not self._csr.is_simple(dev):   # a repeated neighbour: the index assumes simple rows
             return False
         d = self._csr.device_tensors(dev, need_n2v_index=True)
         return d.get('n2v_rec') is not None

@@ -323,7 +323,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
                      order_ready: bool = False, placed: bool = False,
-                     coef_in: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                     coefficients_in: bool = False) -> Optional[torch.Tensor]:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
@@ -331,10 +331,10 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     (owned terms only). The records stay in the per-device workspace for sgns_owner_pass2.
     ``order_ready``: sgns_owner_prepare already built the centre order for these walks;
     ``placed``: dw_sgns_owner_out_catch_up placed this batch's records (flags & 1): each goes
-    straight into its row's segment. ``coef_in`` (with ``placed``): the rows-major step
-    (OwnerLazyTables.out_rows_step) already formed the coefficients and left the rows' pre-step
-    values in this [slots, d] tensor — only the centre gradient is formed (no loss sums: returns
-    None)."""
+    straight into its row's segment. ``coefficients_in`` (with ``placed``): the rows-major step
+    (OwnerLazyTables.out_rows_step) already formed the coefficients and left the rows it stepped
+    pending, their pre-step values in ``w_out_local`` — only the centre gradient is formed (no
+    loss sums: returns None)."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -354,9 +354,9 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     if noise is not None and noise.numel() != n_centres * 2 * R * K:
         raise ValueError('noise must have B\' * 2R * K entries')
     scale = 1.0 / max(n_centres * 2 * R, 1) if grad_scale is None else grad_scale
-    if coef_in is not None:
-        if not placed or coef_in.shape[1] != d or coef_in.shape[0] < n_centres * 2 * R * (1 + K):
-            raise ValueError('coef_in needs placed records and [slots, d] pre-step rows')
+    if coefficients_in:
+        if not placed:
+            raise ValueError('coefficients_in needs the placed records (placed=True)')
         loss_acc = None
     elif loss_acc is None:
         loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
@@ -367,9 +367,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows,
                      (1 if order_ready else 0) | (2 if placed else 0)
-                     | (4 if coef_in is not None else 0),
-                     _native.ptr(w_in),
-                     _native.ptr(w_out_local if coef_in is None else coef_in), _native.ptr(g_in),
+                     | (4 if coefficients_in else 0),
+                     _native.ptr(w_in), _native.ptr(w_out_local), _native.ptr(g_in),
                      _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),
                      _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws), ws.numel(),

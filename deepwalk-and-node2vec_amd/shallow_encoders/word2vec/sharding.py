@@ -254,12 +254,41 @@ class ShardedTables:
         a = p * self.PL
         return (a, a + self.PL), (a + self.rank * self.SL, a + (self.rank + 1) * self.SL)
 
-    def state_rows(self, t: int) -> torch.Tensor:
-        """Global row of each row of m[t] / v[t] (this rank's rows of table t, in order)."""
+    def state_rows(self, t: int, rank: Optional[int] = None) -> torch.Tensor:
+        """Global row of each row of m[t] / v[t] (rank ``rank``'s rows of table t, in order;
+        default this rank)."""
+        r = self.rank if rank is None else int(rank)
         if t == 0:
-            a, b = self.shard_range()
-            return torch.arange(a, b)
-        return torch.cat([torch.arange(*self.out_piece_rows(p)[1]) for p in range(self.P)])
+            return torch.arange(r * self.S, (r + 1) * self.S)
+        return torch.cat([torch.arange(p * self.PL + r * self.SL, p * self.PL + (r + 1) * self.SL)
+                          for p in range(self.P)])
+
+    def full_state(self):
+        """(w_in, m_in, v_in, w_out, m_out, v_out), each the whole (V, d) table, on every rank:
+        the tables are replicated; the Adam state shards (node ranges of the in table, piece
+        sub-ranges of the out table) are all-gathered when N > 1 (collectives: every rank calls
+        it). Between steps only (no exchange pending): bench.py's step check of the layout."""
+        res = []
+        for t in (0, 1):
+            for st in (self.m[t], self.v[t]):
+                if not self.multi:
+                    full = torch.empty((self.V_pad, self.d), dtype=torch.float32,
+                                       device=self.device)
+                    full[self.state_rows(t).to(self.device)] = st
+                else:
+                    parts = torch.empty((self.world, self.S, self.d), dtype=torch.float32,
+                                        device=self.device)
+                    if dist.get_backend(self.group) == 'nccl':
+                        dist.all_gather_into_tensor(parts.view(-1), st.reshape(-1),
+                                                    group=self.group)
+                    else:
+                        dist.all_gather(list(parts.unbind(0)), st.clone(), group=self.group)
+                    full = torch.empty((self.V_pad, self.d), dtype=torch.float32,
+                                       device=self.device)
+                    for r in range(self.world):
+                        full[self.state_rows(t, r).to(self.device)] = parts[r]
+                res.append(full[:self.V].clone())
+        return (self.w_in.clone(), res[0], res[1], self.w_out.clone(), res[2], res[3])
 
     def xavier_(self, seed: int) -> None:
         """W2VBase init (model.py:26-27): U(-a, a), a = sqrt(6/(V+d)); identical on all ranks."""
@@ -826,11 +855,14 @@ HIST_AHEAD = 256   # history rows written per host-to-device copy (begin_step)
 
 def hip_rows_adam(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor,
                   rows: Optional[torch.Tensor], n_dev: Optional[torch.Tensor], n_max: int,
-                  g_rows: Optional[torch.Tensor], hist: torch.Tensor, step: int) -> None:
-    """dw_adam_rows on [n_table, d] tables (see include/dw_hip.h)."""
+                  g_rows: Optional[torch.Tensor], hist: torch.Tensor, step: int,
+                  pending: Optional[torch.Tensor] = None) -> None:
+    """dw_adam_rows on [n_table, d] tables (see include/dw_hip.h); ``pending``: the rows-major
+    step's uint8 marks (settled and cleared on the listed rows)."""
     with torch.cuda.device(p.device):
         _native.call('dw_adam_rows', _native.ptr(p), _native.ptr(m), _native.ptr(v),
-                     _native.ptr(last), p.shape[0], p.shape[1], _native.ptr(rows),
+                     _native.ptr(last), _native.ptr(pending), p.shape[0], p.shape[1],
+                     _native.ptr(rows),
                      _native.ptr(n_dev), int(n_max), _native.ptr(g_rows), _native.ptr(hist),
                      int(step), _native.stream(p.device))
 
@@ -894,7 +926,11 @@ class OwnerLazyTables(OwnerTables):
         # touched out row once; the catch-up -> pass 1 -> lazy gather sequence otherwise (the
         # tests set these attributes to compare the forms)
         self.rows_major = self.place
-        self._p_prev = None        # [slots, d]: the rows' pre-step values for the centre pass
+        # the rows-major step leaves the rows it steps pending (m, v at the step, p one behind
+        # for the centre pass; pend_out[row] = 1); the next replay or a flush settles them
+        self.pend_out = (torch.zeros(self.S, dtype=torch.uint8, device=self.device)
+                         if self.lazy_out else None)
+        self._pend_dirty = False   # some out row may be pending
         self._rows_step = False    # this step goes rows-major (set by catch_up_out)
 
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
@@ -934,6 +970,8 @@ class OwnerLazyTables(OwnerTables):
             self._out_rows = torch.empty(cap, dtype=torch.int32, device=self.device)
         ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
         self._rows_step = self.rows_major_ok(R, K)
+        if not self._rows_step and self._pend_dirty:
+            self._flush_out()   # the other form reads the rows as current: settle them first
         flags = (self.out_flags() & 3) | (4 if self._rows_step else 0)
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_catch_up', _native.ptr(walks), n, L,
@@ -952,16 +990,14 @@ class OwnerLazyTables(OwnerTables):
                       status: torch.Tensor, noise: Optional[torch.Tensor] = None) -> None:
         """The rows-major out step of the batch ``walks`` (after catch_up_out chose it):
         dw_sgns_owner_out_rows — each touched out row replayed, its records' coefficients and
-        loss terms, its gradient and Adam step; the rows' pre-step values into ``_p_prev`` for
-        the centre pass (sgns_owner_pass1 with coef_in)."""
+        loss terms, its gradient and the moments of its Adam step; the rows are left pending
+        (p at step - 1 in the table, for the centre pass: sgns_owner_pass1 with
+        coefficients_in)."""
         from shallow_encoders.word2vec.sgns import workspace_for
         n, L = walks.shape
         R, K = int(context_radius), int(neg_samples)
-        slots = n * (L - 2 * R) * 2 * R * (1 + K)
-        if self._p_prev is None or self._p_prev.shape[0] < max(slots, 1):
-            self._p_prev = torch.empty((max(slots, 1), self.d), dtype=torch.float32,
-                                       device=self.device)
         ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
+        self._pend_dirty = True
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_rows', _native.ptr(walks), n, L, R, K, self.V,
                          self.d, self.rank, self.world, self.S, _native.ptr(noise),
@@ -969,8 +1005,8 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self.w_in_raw), _native.ptr(self.w_out),
                          _native.ptr(self.g_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._count_out), _native.ptr(self._hist),
-                         self.step_count, _native.ptr(self._p_prev), self._p_prev.shape[0],
+                         _native.ptr(self._count_out), _native.ptr(self.pend_out),
+                         _native.ptr(self._hist), self.step_count,
                          _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws),
                          ws.numel(), _native.stream(self.device))
 
@@ -1183,7 +1219,8 @@ class OwnerLazyTables(OwnerTables):
         """lazy_out: every out-slice row up to the current step."""
         if self.lazy_out and self.step_count > 0:
             hip_rows_adam(self.w_out, self.m_out, self.v_out, self.last_out, None, None,
-                          self.S, None, self._hist, self.step_count)
+                          self.S, None, self._hist, self.step_count, pending=self.pend_out)
+            self._pend_dirty = False
 
     def out_adam_spec(self) -> Optional[dict]:
         spec = super().out_adam_spec()
@@ -1231,7 +1268,7 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
                          walks=walks, context_radius=context_radius, owner=tables.rank,
                          n_owners=tables.world, vocab_size=tables.V, seed=seed,
                          noise_offset=noise_offset, grad_scale=grad_scale, status=status,
-                         order_ready=True, placed=True, coef_in=tables._p_prev)
+                         order_ready=True, placed=True, coefficients_in=True)
         tables.exchange_touched()
         tables.update_touched()
         return slots

@@ -579,18 +579,22 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
  * g = 0 steps replayed (hist, as for dw_adam_rows), the logits of its records against their
  * centre rows, the coefficients and loss sums (loss_acc float64[4] as for dw_sgns_walks), its
  * gradient and the Adam step `step` — the same arithmetic as the catch-up / pass 1 /
- * dw_sgns_owner_pass2_lazy sequence. Leaves each record's coefficient in the placed records and
- * the row's pre-step values in p_prev (float32 [p_prev_rows >= B' * 2R(1+K), dim], at the row's
- * first record position) for dw_sgns_owner_pass1's centre gradient. counts: the catch-up's, cleared
- * as the rows step. dim a multiple of 64 (<= 512), 2R(1+K) <= 64; no deterministic form. */
+ * dw_sgns_owner_pass2_lazy sequence. Leaves each record's coefficient in the placed records
+ * and every row it steps PENDING for dw_sgns_owner_pass1's centre gradient: exp_avg and
+ * exp_avg_sq at `step`, the parameter row still at step - 1 (what the centre gradient reads),
+ * pending[row] = 1 (uint8 [local_rows], zero-initialised by the caller). The parameter half of
+ * a pending row's step (torch Adam's p update from its m and v, the same operations) is applied
+ * when the row is next replayed — by the next rows-major step, or by dw_adam_rows given the same
+ * `pending` (the flush before the table is read whole). counts: the catch-up's, cleared as the
+ * rows step. dim in {64, 128, 256, 512}, 2R(1+K) <= 64; no deterministic form. */
 int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                            int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                            int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
                            const int64_t *noise, uint64_t seed, uint64_t noise_offset,
                            float grad_scale, const float *w_in, float *w_out_local,
                            float *g_out_local, float *m_out, float *v_out, int32_t *last_step,
-                           uint32_t *counts, const float *hist, int32_t step, float *p_prev,
-                           int64_t p_prev_rows, double *loss_acc, int32_t *status,
+                           uint32_t *counts, uint8_t *pending, const float *hist,
+                           int32_t step, double *loss_acc, int32_t *status,
                            void *workspace, size_t workspace_bytes, void *stream);
 
 /* Same computation over explicit pairs (the reference's collate output):
@@ -719,9 +723,11 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         fewer operations); any other row 0 = no step in the box;
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
- *         gradient grad_rows[i]. */
+ *         gradient grad_rows[i];
+ *   pending: NULL, or uint8 [n_table_rows] (dw_sgns_owner_out_rows): a listed row marked there
+ *         first gets the parameter half of step last_step[r], and its mark is cleared. */
 int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
-                 int64_t n_table_rows, int32_t dim, const uint32_t *rows,
+                 uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                  const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
                  const float *hist, int32_t step, void *stream);
 

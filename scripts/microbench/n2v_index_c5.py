@@ -50,7 +50,7 @@ def main():
     emit(stage='counts', edge_cn_build_ms=(time.perf_counter() - a) * 1e3,
          hubs_with_bitmaps=int((d['hub_idx'] >= 0).sum()))
 
-    cn = d['edge_cn'][:E].to(torch.int64)
+    cn = d['edge_cn'][:E].to(torch.int64) & 0x7FFFFFFF    # bit 31: t in N(v); bits 0-30: C
     deg = d['row_ptr'][1:] - d['row_ptr'][:-1]
     deg_t = deg[d['col'][:E].long()]                  # deg(v) of every directed edge t -> v
     n_pos = int(cn.sum())
@@ -78,7 +78,27 @@ def main():
     torch.cuda.synchronize(dev)
     info = dict(d.get('n2v_index_info', {}))
     emit(stage='build', seconds=time.perf_counter() - a, **info)
-    if d.get('n2v_rec') is None:
+    if d.get('n2v_rec') is None:   # the wave walker with the per-edge counts (the fallback)
+        L, n = args.L, args.check_walks
+        w = Node2Vec(csr, L, p=args.p, q=args.q, device=dev)
+        st = (torch.randperm(V - 1, generator=torch.Generator().manual_seed(1))[:n] + 1).to(
+            torch.int32).to(dev)
+        u = torch.from_numpy(draw_uniforms(n * (L - 1), random.Random(0))).to(dev)
+        out = torch.empty((n, L), dtype=torch.int32, device=dev)
+        w.walk_batch(st[:64], uniforms=u[:64 * (L - 1)], out=out[:64])
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        w.walk_batch(st, uniforms=u, out=out, check=False)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1)
+        c = w.count_replay_traffic(st, u, out=torch.empty_like(out))
+        emit(stage='rate', walker='dw_walk_replay_indexed (wave walker, per-edge counts)',
+             walks=n, kernel_ms=ms, walks_per_s=n / (ms * 1e-3),
+             bytes_per_step=c['bytes'] / max(c['steps'], 1),
+             list_entries_per_step=c['entries'] / max(c['steps'], 1),
+             hash_probes_per_step=c['probes'] / max(c['steps'], 1))
         return
 
     L = args.L

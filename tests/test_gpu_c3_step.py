@@ -102,11 +102,13 @@ class _Lazy:
         t = self.t
         lagging = [t.params_in, t.m_in, t.v_in, t.last_in]
         if t.lazy_out:
-            lagging += [t.w_out, t.m_out, t.v_out, t.last_out]
+            lagging += [t.w_out, t.m_out, t.v_out, t.last_out, t.pend_out]
         keep = [x.clone() for x in lagging]
+        dirty = t._pend_dirty
         snap = [x.clone() for x in self.state()]
         for dst, src in zip(lagging, keep):
             dst.copy_(src)
+        t._pend_dirty = dirty
         return snap
 
     def step(self, walks, g0, loss_acc, status):

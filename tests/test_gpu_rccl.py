@@ -95,7 +95,7 @@ def _child(port, q):
                 # the state with every deferred step applied, the tables left lagging
                 lag = [tl.params_in, tl.m_in, tl.v_in, tl.last_in]
                 if tl.lazy_out:
-                    lag += [tl.w_out, tl.m_out, tl.v_out, tl.last_out]
+                    lag += [tl.w_out, tl.m_out, tl.v_out, tl.last_out, tl.pend_out]
                 keep = [x.clone() for x in lag]
                 tl.flush()
                 snaps.append(owner_snap(tl))
