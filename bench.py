@@ -458,7 +458,8 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
     from shallow_encoders.word2vec.sgns import loss_terms, phase_ms, phase_timing, sgns_phase_bytes
     from shallow_encoders.word2vec.sgns import sgns_owner_pass1, sgns_owner_pass2
     from shallow_encoders.word2vec.sharding import (OwnerLazyTables, OwnerTables, ShardedTables,
-                                                    overlap_adam_blocks, replicated_step)
+                                                    overlap_adam_blocks, owner_lazy_step,
+                                                    replicated_step)
     _native.require_device(dev)
 
     copy_gbs = measured_copy_gbs(dev)   # before the tables take the memory
@@ -649,19 +650,27 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
         if record:
             e[1].record()
         if lazy:
-            tables.begin_step()
-            tables.before_pass1(walks, R, K, 99, g0 * (L - 2 * R), status)
+            # the lazy step as the library composes it (sharding.owner_lazy_step: on one rank the
+            # rows-major out step, else catch-up -> pass 1 -> touched-row exchange -> lazy gather
+            # -> touched-row update); its window is 'sgns' (no separate Adam phase)
+            n_rec[0] = owner_lazy_step(tables, walks, R, K, seed=99, noise_offset=g0 * (L - 2 * R),
+                                       grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+            if not gather:
+                feed.next(s)
+                feed.release(s)
+            if record:
+                e[2].record()
+                ev['walk'].append((e[0], e[1]))
+                ev['sgns'].append((e[1], e[2]))
+                ev['adam'].append((e[2], e[2]))
+            return
         sgns_owner_pass1(tables.w_in_raw, tables.w_out, tables.grads_in, K, walks=walks,
                          context_radius=R, owner=tables.rank, n_owners=tables.world,
                          vocab_size=V, seed=99, noise_offset=g0 * (L - 2 * R),
-                         grad_scale=grad_scale, loss_acc=loss_acc, status=status,
-                         order_ready=lazy, placed=lazy and bool(tables.out_flags() & 1))
+                         grad_scale=grad_scale, loss_acc=loss_acc, status=status)
         if not gather:
             feed.next(s)
-        if lazy:
-            tables.exchange_touched()
-        else:
-            tables.exchange_in()        # full grid: 1/W of the in table, between RS and AG
+        tables.exchange_in()        # full grid: 1/W of the in table, between RS and AG
         spec = tables.out_adam_spec() if fuse else None
         # one owner keeps every slot: no record-count readback (the host runs ahead)
         n = sgns_owner_pass2(tables.w_in_raw, tables.w_out, tables.g_out, K, walks=walks,
@@ -674,10 +683,7 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
             tables.out_step()
         if record:
             e[2].record()
-        if lazy:
-            tables.update_touched()
-        else:
-            tables.sync()
+        tables.sync()
         if record:
             e[3].record()
             ev['walk'].append((e[0], e[1]))

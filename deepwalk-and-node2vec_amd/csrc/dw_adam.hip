@@ -107,12 +107,14 @@ using dw::hist_at;
 // uniform: lanes past d carry zeros and are not stored.
 // E = 2 (even d): two adjacent elements per thread (8-B accesses), replayed as pairs on the
 // packed fp32 instructions (dw::replay_g0 with N = 2): half the threads, half the issue slots.
-template <bool STEP, bool P_ONLY = false, int E = 1>
+// BY_ROW (with STEP): the gradient is the table's own row g_rows[r] (the dense gradient buffer),
+// cleared as it is used — one rank's touched in rows, with no gather in between.
+template <bool STEP, bool P_ONLY = false, int E = 1, bool BY_ROW = false>
 __global__ void __launch_bounds__(512)
     k_rows_adam(float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
                 int32_t *__restrict__ last, uint8_t *__restrict__ pend, int64_t n_table, int32_t d,
                 const uint32_t *__restrict__ rows, const int64_t *__restrict__ n_dev,
-                int64_t n_max, const float *__restrict__ g_rows, const float *__restrict__ hist,
+                int64_t n_max, float *__restrict__ g_rows, const float *__restrict__ hist,
                 int32_t step_arg, const dw_step_scalars *__restrict__ dyn, int32_t delta) {
     const int32_t step = dw::eff_step(dyn, delta, step_arg);   // graph replay: from the block
     const int e = threadIdx.x * E;
@@ -133,21 +135,24 @@ __global__ void __launch_bounds__(512)
         __syncthreads();   // every wave has read last[r] before thread 0 advances it
         if (from >= (STEP ? step : upto) && !pd) continue;   // already current (or stepped)
         const int64_t o = r * d + e;
+        const int64_t og = (BY_ROW ? r : i) * d + e;   // the gradient row
         float pr[E], mr[E], vr[E], gg[E];
         if constexpr (E == 2) {   // (d even: o is 8-B aligned)
             const float2 zero = make_float2(0.f, 0.f);
             const float2 p2 = live ? *reinterpret_cast<const float2 *>(p + o) : zero;
             const float2 m2 = live ? *reinterpret_cast<const float2 *>(m + o) : zero;
             const float2 v2 = live ? *reinterpret_cast<const float2 *>(v + o) : zero;
-            const float2 g2 = (STEP && live) ? *reinterpret_cast<const float2 *>(g_rows + i * d + e)
+            const float2 g2 = (STEP && live) ? *reinterpret_cast<const float2 *>(g_rows + og)
                                              : zero;
+            if (BY_ROW && live) *reinterpret_cast<float2 *>(g_rows + og) = zero;
             pr[0] = p2.x, pr[1] = p2.y, mr[0] = m2.x, mr[1] = m2.y;
             vr[0] = v2.x, vr[1] = v2.y, gg[0] = g2.x, gg[1] = g2.y;
         } else {
             pr[0] = live ? p[o] : 0.f;
             mr[0] = live ? m[o] : 0.f;
             vr[0] = live ? v[o] : 0.f;
-            gg[0] = (STEP && live) ? g_rows[i * d + e] : 0.f;
+            gg[0] = (STEP && live) ? g_rows[og] : 0.f;
+            if (BY_ROW && live) g_rows[og] = 0.f;
         }
         if (pd) dw::settle_pending(pr, mr, vr, hist, from);
         dw::replay_g0(pr, mr, vr, hist, from, upto, box_from);
@@ -306,8 +311,9 @@ int dw_adam_dense(float *param, float *grad, float *exp_avg, float *exp_avg_sq, 
 
 int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
                          uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                         const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                         const float *hist, int32_t step, bool p_only, hipStream_t st) {
+                         const int64_t *n_rows_dev, int64_t n_rows_max, float *grad_rows,
+                         const float *hist, int32_t step, bool p_only, hipStream_t st,
+                         bool grad_by_row) {
     DW_REQUIRE(n_table_rows >= 0 && dim >= 1 && n_rows_max >= 0 && step >= 0,
                "dw_adam_rows: bad sizes");
     if (n_rows_max == 0) return DW_OK;
@@ -323,30 +329,33 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     if (blocks > 65536) blocks = 65536;
     DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
     DW_REQUIRE(!(p_only && pending), "dw_adam_rows: p_only replays do not settle pending rows");
+    DW_REQUIRE(!grad_by_row || grad_rows, "dw_adam_rows: grad_by_row needs the gradient table");
     // even d: two elements per thread on the packed instructions
     const bool pair = dim % 2 == 0;
     const int threads = pair ? 64 * ((dim / 2 + 63) / 64) : 64 * ((dim + 63) / 64);
-#define DW_ROWS_ADAM(STEP_, PONLY_)                                                              \
+#define DW_ROWS_ADAM(STEP_, PONLY_, BYROW_)                                                      \
     do {                                                                                        \
         if (pair)                                                                               \
-            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 2>), dim3((unsigned)blocks),         \
+            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 2, BYROW_>), dim3((unsigned)blocks), \
                                dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
                                pending, n_table_rows, dim, rows, n_rows_dev, n_rows_max,        \
                                grad_rows, hist,                                                 \
                                step, dyn, delta);                                               \
         else                                                                                    \
-            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 1>), dim3((unsigned)blocks),         \
+            hipLaunchKernelGGL((k_rows_adam<STEP_, PONLY_, 1, BYROW_>), dim3((unsigned)blocks), \
                                dim3(threads), 0, st, param, exp_avg, exp_avg_sq, last_step,     \
                                pending, n_table_rows, dim, rows, n_rows_dev, n_rows_max,        \
                                grad_rows, hist,                                                 \
                                step, dyn, delta);                                               \
     } while (0)
-    if (grad_rows)
-        DW_ROWS_ADAM(true, false);
+    if (grad_rows && grad_by_row)
+        DW_ROWS_ADAM(true, false, true);
+    else if (grad_rows)
+        DW_ROWS_ADAM(true, false, false);
     else if (p_only)
-        DW_ROWS_ADAM(false, true);
+        DW_ROWS_ADAM(false, true, false);
     else
-        DW_ROWS_ADAM(false, false);
+        DW_ROWS_ADAM(false, false, false);
 #undef DW_ROWS_ADAM
     DW_LAUNCH_CHECK("dw_adam_rows");
     return DW_OK;
@@ -356,12 +365,11 @@ extern "C" {
 
 int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
                  uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                 const float *hist, int32_t step, void *stream) {
+                 const int64_t *n_rows_dev, int64_t n_rows_max, float *grad_rows,
+                 int32_t grad_by_row, const float *hist, int32_t step, void *stream) {
     return dw::adam_rows_launch(param, exp_avg, exp_avg_sq, last_step, pending, n_table_rows,
-                                dim, rows,
-                                n_rows_dev, n_rows_max, grad_rows, hist, step, false,
-                                dw::as_stream(stream));
+                                dim, rows, n_rows_dev, n_rows_max, grad_rows, hist, step, false,
+                                dw::as_stream(stream), grad_by_row != 0);
 }
 
 int dw_rows_gather(float *table, int64_t n_table_rows, int32_t dim, const uint32_t *rows,

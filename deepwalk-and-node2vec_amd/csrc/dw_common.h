@@ -415,8 +415,9 @@ __device__ __forceinline__ AdamScalars step_adam(const dw_step_scalars *dyn,
 // then replays m and v itself (their g = 0 recurrences are a multiply each) before the step.
 int adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
                      uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                     const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                     const float *hist, int32_t step, bool p_only, hipStream_t stream);
+                     const int64_t *n_rows_dev, int64_t n_rows_max, float *grad_rows,
+                     const float *hist, int32_t step, bool p_only, hipStream_t stream,
+                     bool grad_by_row = false);
 
 // ---- deterministic accumulation (dw_exact_register) -----------------------------------------
 // A gradient term t (fp32) enters an int64 accumulator as round(t * 2^frac): integer sums are

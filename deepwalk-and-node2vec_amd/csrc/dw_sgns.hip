@@ -446,8 +446,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
 
     for (int64_t base = base0; base < o_end; base += step) {
         const int64_t jb = base + q;
-        const bool active = jb < o_end;
-        const int64_t b = OWNER ? (active ? static_cast<int64_t>(a.occ[jb]) : 0) : jb;
+        // (OWNER with occ NULL: the centres in walk order — the rows-major step's centre pass)
+        const int64_t b0 =
+            OWNER ? (jb < o_end ? (a.occ ? static_cast<int64_t>(a.occ[jb]) : jb) : 0) : jb;
+        // an order entry outside the batch (an order never built for these walks) reads no walk
+        const bool bad_b = OWNER && jb < o_end && (b0 < 0 || b0 >= a.batch);
+        if (bad_b && gl == 0) dw::status_or(a.status, DW_S_BAD_INDEX);
+        const bool active = jb < o_end && !bad_b;
+        const int64_t b = bad_b ? 0 : b0;
         const int32_t *walk = nullptr;
         int64_t i = 0, cid = -1;
         if (active) {
@@ -2244,6 +2250,8 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     const bool coefin = (order_ready & 4) != 0;
     DW_REQUIRE(!coefin || placed, "dw_sgns_owner_pass1: the coefficients come with the placed "
                "records (order_ready & 2)");
+    DW_REQUIRE(!(order_ready & 8) || coefin, "dw_sgns_owner_pass1: walk order (order_ready & 8) "
+               "is the coefficients-in form's (order_ready & 4)");
     const bool dense = a.n_owners == 1 || placed;
     if (placed) {
         a.place_rank = pl.rank;
@@ -2257,11 +2265,15 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
     a.region = lay.region;
     a.occ_per_wave = lay.region / T;
     if (a.batch > 0) {
-        if (!(order_ready & 1)) {  // the centres in node order (stable: walk order within a node)
-            rc = owner_order(a, occ, nullptr, nullptr, st);
-            if (rc != DW_OK) return rc;
+        if (order_ready & 8) {     // walk order (one rank, coefficients in: no node order needed)
+            a.occ = nullptr;
+        } else {
+            if (!(order_ready & 1)) {  // the centres in node order (stable: walk order in a node)
+                rc = owner_order(a, occ, nullptr, nullptr, st);
+                if (rc != DW_OK) return rc;
+            }
+            a.occ = occ.v0;
         }
-        a.occ = occ.v0;
         int32_t fl = 0;
         rc = exact_of(a.g_in, a.V * a.d, &a.fx_in, &fl, "dw_sgns_owner_pass1");
         if (rc != DW_OK) return rc;
@@ -2527,6 +2539,42 @@ SgnsArgs base_args(int64_t V, int32_t dim, int32_t K, const float *w_in, const f
 // serialises (1,120 blocks of one trip each were ~36 us at C3's 64-walk batch).
 // !CLAIM (the rows-major step, dw_sgns_owner_out_rows): the ranks alone — k_out_rows replays
 // every row right before its step, so no row is listed or caught up here.
+// dw_sgns_owner_touch_claim: the batch's distinct centre nodes (the in rows a step touches),
+// unsorted — one rank needs no common order of them. claim[node] = step by atomicMax; the
+// first claimer of a node appends it, one list atomic per wave. (k_occ_small's one-block sort +
+// unique gave the sorted list in 30-40 us at C3's 64-walk batch, on the step's critical path
+// before the in-table catch-up; this takes a few microseconds.)
+__global__ void __launch_bounds__(256)
+    k_touch_claim(const int32_t *__restrict__ walks, int64_t n_centres, int32_t L, int32_t R,
+                  int64_t V, int32_t *__restrict__ claim, int32_t step_arg,
+                  const dw_step_scalars *__restrict__ dyn, int32_t delta,
+                  uint32_t *__restrict__ touched, unsigned long long *__restrict__ n_touched) {
+    const int32_t step = dw::eff_step(dyn, delta, step_arg);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int64_t per = L - 2 * R;
+    for (int64_t base = ((int64_t)blockIdx.x * 4 + threadIdx.x / WAVE) * WAVE; base < n_centres;
+         base += (int64_t)gridDim.x * 4 * WAVE) {
+        const int64_t b = base + lane;
+        bool mine = false;
+        int32_t node = 0;
+        if (b < n_centres) {
+            const int64_t w = b / per;
+            node = walks[w * L + R + (b - w * per)];
+            // (an out-of-range id is reported by the SGNS pass)
+            if (node >= 0 && node < V) mine = atomicMax(claim + node, step) < step;
+        }
+        const uint64_t mask = __ballot(mine);
+        if (mask == 0) continue;
+        unsigned long long at = 0;
+        if (lane == 0) at = atomicAdd(n_touched, static_cast<unsigned long long>(__popcll(mask)));
+        at = (static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
+                  static_cast<uint32_t>(at >> 32))) << 32) |
+             __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(at));
+        if (mine) touched[at + __popcll(mask & lt)] = static_cast<uint32_t>(node);
+    }
+}
+
 constexpr int CLAIM_TRIPS = 4;
 // (the ranks alone: one centre per wave, four times the waves — the atomics are the chain)
 template <bool CLAIM, int TRIPS = CLAIM ? CLAIM_TRIPS : 1>
@@ -3002,6 +3050,35 @@ int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_le
     a.C = 2 * context_radius;
     return launch_owner_prepare(a, local_rows, touched, n_touched, workspace, workspace_bytes,
                                 dw::as_stream(stream));
+}
+
+int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                              int32_t context_radius, int64_t vocab_size, int32_t *claim,
+                              int32_t step, uint32_t *touched, int64_t *n_touched,
+                              void *stream) {
+    DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
+                   vocab_size >= 1 && step >= 1,
+               "dw_sgns_owner_touch_claim: bad sizes");
+    DW_REQUIRE(claim && touched && n_touched && (walks || n_walks == 0),
+               "dw_sgns_owner_touch_claim: null pointer");
+    const hipStream_t st = dw::as_stream(stream);
+    const dw_step_scalars *dyn = nullptr;
+    int32_t delta = 0;
+    const int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_sgns_owner_touch_claim");
+    if (rc != DW_OK) return rc;
+    if (hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess) {
+        dw::set_error("dw_sgns_owner_touch_claim: counter reset failed");
+        return DW_E_HIP;
+    }
+    const int64_t n_centres = n_walks * (walk_length - 2 * context_radius);
+    if (n_centres == 0) return DW_OK;
+    int64_t blocks = (n_centres + 255) / 256;
+    if (blocks > grid_cap(8)) blocks = grid_cap(8);
+    hipLaunchKernelGGL(k_touch_claim, dim3((unsigned)blocks), dim3(256), 0, st, walks, n_centres,
+                       walk_length, context_radius, vocab_size, claim, step, dyn, delta, touched,
+                       reinterpret_cast<unsigned long long *>(n_touched));
+    DW_LAUNCH_CHECK("dw_sgns_owner_touch_claim");
+    return DW_OK;
 }
 
 int dw_sgns_owner_pass1(const int32_t *walks, int64_t n_walks, int32_t walk_length,

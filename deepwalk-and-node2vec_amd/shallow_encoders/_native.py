@@ -97,8 +97,10 @@ SIGNATURES = {
     'dw_sgns_owner_pass1': (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32,
                                            _i64, _i32, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p,
                                            _p, ctypes.c_size_t, _p]),
-    'dw_adam_rows': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _p, _i32,
-                                    _p]),
+    'dw_sgns_owner_touch_claim': (ctypes.c_int, [_p, _i64, _i32, _i32, _i64, _p, _i32, _p, _p,
+                                                 _p]),
+    'dw_adam_rows': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _i32, _p,
+                                    _i32, _p]),
     'dw_rows_gather': (ctypes.c_int, [_p, _i64, _i32, _p, _p, _i64, _p, _i32, _p]),
     'dw_sgns_owner_pass2': (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p, _p, _p,
                                            _p, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p,

@@ -323,7 +323,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      loss_acc: Optional[torch.Tensor] = None,
                      status: Optional[torch.Tensor] = None,
                      order_ready: bool = False, placed: bool = False,
-                     coefficients_in: bool = False) -> Optional[torch.Tensor]:
+                     coefficients_in: bool = False,
+                     walk_order: bool = False) -> Optional[torch.Tensor]:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
@@ -334,7 +335,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     straight into its row's segment. ``coefficients_in`` (with ``placed``): the rows-major step
     (OwnerLazyTables.out_rows_step) already formed the coefficients and left the rows it stepped
     pending, their pre-step values in ``w_out_local`` — only the centre gradient is formed (no
-    loss sums: returns None)."""
+    loss sums: returns None); ``walk_order`` (with it): the centres in walk order, no node order
+    built or read."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -358,6 +360,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
         if not placed:
             raise ValueError('coefficients_in needs the placed records (placed=True)')
         loss_acc = None
+    elif walk_order:
+        raise ValueError('walk_order is the coefficients_in form\'s')
     elif loss_acc is None:
         loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     if status is None:
@@ -367,7 +371,7 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows,
                      (1 if order_ready else 0) | (2 if placed else 0)
-                     | (4 if coefficients_in else 0),
+                     | (4 if coefficients_in else 0) | (8 if walk_order else 0),
                      _native.ptr(w_in), _native.ptr(w_out_local), _native.ptr(g_in),
                      _native.ptr(noise),
                      seed & 0xFFFFFFFFFFFFFFFF, int(noise_offset), float(scale),

@@ -70,12 +70,37 @@ def adam_scalars(step: int, lr: float, betas, eps: float, weight_decay: float):
             weight_decay)
 
 
+# betas[1] values whose every step's sqrt(bias_correction2) c is PROVEN to give, through the
+# reciprocal division of dw::div_bc2s (q = x RN(1/c); q + (x - c q) RN(1/c)), the IEEE quotient
+# x / c for every fp32 x the replays divide (all 2^23 mantissas of [1, 2) and 0, per c; scaling
+# by powers of two is exact there): scripts/microbench/div_proof.py on MI355X,
+# profiles/r05_div_proof.jsonl (the random sample before it was not a proof). Other
+# betas get no reciprocal (h[7] = 0): the kernels divide.
+RECIPROCAL_PROVEN_BETA2 = (0.999, 0.99)
+
+
+def bc2s_pairs(beta2: float) -> np.ndarray:
+    """float32 [T, 2]: (sqrt(bias_correction2), RN(1 / it)) of steps 1..T as hist_row writes them,
+    T the first step at which the first rounds to 1 (from there on y = 1 and q = x exactly)."""
+    out = []
+    t = 1
+    while True:
+        c = np.float32(adam_scalars(t, 1.0, (0.9, beta2), 1e-8, 0.0)[3])
+        out.append((c, np.float32(1.0) / c))
+        if c == np.float32(1.0) or t > 10_000_000:
+            break
+        t += 1
+    return np.asarray(out, dtype=np.float32)
+
+
 def hist_row(step: int, lr: float, betas, eps: float, weight_decay: float) -> np.ndarray:
     """float32[8]: adam_scalars as the kernels take them, then RN(1 / sqrt(bias_correction2))
-    (the replays divide by the step's uniform sqrt(bias_correction2) through it: dw::div_bc2s)."""
+    (the replays divide by the step's uniform sqrt(bias_correction2) through it: dw::div_bc2s)
+    where betas[1] is proven for it (RECIPROCAL_PROVEN_BETA2), else 0 (divide)."""
     h = np.zeros(8, dtype=np.float32)
     h[:7] = np.asarray(adam_scalars(step, lr, betas, eps, weight_decay), dtype=np.float32)
-    h[7] = np.float32(1.0) / h[3]
+    if float(betas[1]) in RECIPROCAL_PROVEN_BETA2:
+        h[7] = np.float32(1.0) / h[3]
     return h
 
 
@@ -856,15 +881,16 @@ HIST_AHEAD = 256   # history rows written per host-to-device copy (begin_step)
 def hip_rows_adam(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor,
                   rows: Optional[torch.Tensor], n_dev: Optional[torch.Tensor], n_max: int,
                   g_rows: Optional[torch.Tensor], hist: torch.Tensor, step: int,
-                  pending: Optional[torch.Tensor] = None) -> None:
+                  pending: Optional[torch.Tensor] = None, grad_by_row: bool = False) -> None:
     """dw_adam_rows on [n_table, d] tables (see include/dw_hip.h); ``pending``: the rows-major
-    step's uint8 marks (settled and cleared on the listed rows)."""
+    step's uint8 marks (settled and cleared on the listed rows); ``grad_by_row``: ``g_rows`` is
+    the table's dense gradient, row r's step reads (and clears) g_rows[r]."""
     with torch.cuda.device(p.device):
         _native.call('dw_adam_rows', _native.ptr(p), _native.ptr(m), _native.ptr(v),
                      _native.ptr(last), _native.ptr(pending), p.shape[0], p.shape[1],
-                     _native.ptr(rows),
-                     _native.ptr(n_dev), int(n_max), _native.ptr(g_rows), _native.ptr(hist),
-                     int(step), _native.stream(p.device))
+                     _native.ptr(rows), _native.ptr(n_dev), int(n_max), _native.ptr(g_rows),
+                     1 if grad_by_row else 0, _native.ptr(hist), int(step),
+                     _native.stream(p.device))
 
 
 class OwnerLazyTables(OwnerTables):
@@ -1023,6 +1049,7 @@ class OwnerLazyTables(OwnerTables):
         self._lr_hist = [0.0]
         self._hist_ready, self._hist_key = 0, None
         self._touched = None
+        self._claim_in = None      # one rank, rows-major steps: dw_sgns_owner_touch_claim's marks
         self._n_max = 0
         self._n_touched = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._n_host = torch.zeros(1, dtype=torch.int64, pin_memory=pin)
@@ -1090,13 +1117,26 @@ class OwnerLazyTables(OwnerTables):
             self._write_hist(self._hist_ready + 1, last_step)
 
     def prepare(self, walks: torch.Tensor, context_radius: int, neg_samples: int) -> None:
-        """The batch's centre order (for pass 1 with order_ready) and its touched rows U."""
+        """The batch's centre order (for pass 1 with order_ready) and its touched rows U. The
+        rows-major step on one rank needs neither the order (its centre pass takes the centres
+        in walk order) nor a sorted U: the distinct centres are claimed (dw_sgns_owner_touch_claim,
+        a few microseconds where the one-block sort took 30-40 on the step's critical path)."""
         from shallow_encoders.word2vec.sgns import sgns_owner_prepare
         n = walks.shape[0] * (walks.shape[1] - 2 * int(context_radius))
         if self._touched is None or self._touched.numel() < max(n, 1):
             self._touched = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
-        sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
-                           touched=self._touched, n_touched=self._n_touched)
+        if self._rows_step and not self.multi:
+            if self._claim_in is None:
+                self._claim_in = torch.zeros(self.V_pad, dtype=torch.int32, device=self.device)
+            with torch.cuda.device(self.device):
+                _native.call('dw_sgns_owner_touch_claim', _native.ptr(walks), walks.shape[0],
+                             walks.shape[1], int(context_radius), self.V,
+                             _native.ptr(self._claim_in), self.step_count,
+                             _native.ptr(self._touched), _native.ptr(self._n_touched),
+                             _native.stream(self.device))
+        else:
+            sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
+                               touched=self._touched, n_touched=self._n_touched)
         self._n_max = n
         if self.multi:   # |U| sizes the all-reduce (exchange_touched)
             self._n_host.copy_(self._n_touched, non_blocking=True)
@@ -1118,7 +1158,7 @@ class OwnerLazyTables(OwnerTables):
             else:
                 hip_rows_adam(self.params_in[0], self.m_in, self.v_in, self.last_in,
                               self._touched, self._n_touched, self._n_max, g_rows, self._hist,
-                              step)
+                              step, grad_by_row=g_rows is self.grads_in)
             return
         rows = torch.arange(self.V_pad, device=self.device) if all_rows else self._touched
         upto = step - 1 if g_rows is not None else step
@@ -1176,6 +1216,11 @@ class OwnerLazyTables(OwnerTables):
         stream behind the output-table phase."""
         n_max = self._n_max
         multi = self.multi
+        if self._hip() and not multi:
+            # one rank: nothing to exchange — update_touched steps each row straight from its
+            # g_in row (dw_adam_rows grad_by_row, which clears it): no gather
+            self._G = self.grads_in
+            return
         if self._hip():
             if self._G is None or self._G.shape[0] < max(n_max, 1):
                 self._G = torch.empty((max(n_max, 1), self.d), dtype=torch.float32,
@@ -1268,7 +1313,8 @@ def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius
                          walks=walks, context_radius=context_radius, owner=tables.rank,
                          n_owners=tables.world, vocab_size=tables.V, seed=seed,
                          noise_offset=noise_offset, grad_scale=grad_scale, status=status,
-                         order_ready=True, placed=True, coefficients_in=True)
+                         order_ready=True, placed=True, coefficients_in=True,
+                         walk_order=not tables.multi)
         tables.exchange_touched()
         tables.update_touched()
         return slots

@@ -503,9 +503,10 @@ int dw_sgns_owner_workspace_bytes(int64_t n_centres, int32_t n_ctx, int32_t neg_
  * it); 2 = the records are placed (dw_sgns_owner_out_catch_up ran with flags & 1 on this batch
  * and workspace): pass 1 writes each record straight into its row's segment, and
  * dw_sgns_owner_pass2_lazy (flags & 1) gathers them without a sort; 4 (with 2) = coefficients in:
- * dw_sgns_owner_out_rows already formed every record's coefficient and left each row's
- * pre-step values in p_prev, which is passed as w_out_local — pass 1 forms the centre gradient
- * alone (no loss sums, no records written; loss_acc may be NULL). */
+ * dw_sgns_owner_out_rows already formed every record's coefficient and left each row it stepped
+ * pending, its pre-step values in w_out_local — pass 1 forms the centre gradient alone (no loss
+ * sums, no records written; loss_acc may be NULL); 8 (with 4) = the centres in walk order (no
+ * node order is built or read: one atomic row per centre occurrence). */
 int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                           int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                           int64_t local_rows, uint32_t *touched, int64_t *n_touched,
@@ -572,6 +573,17 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
                              int32_t step, int32_t flags, uint32_t *counts, int32_t *status,
                              void *workspace, size_t workspace_bytes, int64_t *n_records,
                              void *stream);
+
+/* The distinct centre nodes of a batch (the in rows one step touches), UNSORTED, for the lazy
+ * in-table update on one rank (dw_sgns_owner_prepare gives them sorted, the order every rank
+ * agrees on when N > 1): claim int32 [vocab_size] (zero-initialised, kept across steps) gets
+ * claim[node] = step and the first claimer lists the node in touched (uint32 [>= B']);
+ * n_touched (int64, device) their count. Reads step from a bound dw_step_scalars block
+ * (relative form). Replaces nothing in the reference (its optimizer steps every row). */
+int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
+                              int32_t context_radius, int64_t vocab_size, int32_t *claim,
+                              int32_t step, uint32_t *touched, int64_t *n_touched,
+                              void *stream);
 
 /* The rows-major lazy out step (OwnerLazyTables, one device; after dw_sgns_owner_out_catch_up
  * with flags 1 | 4 on the same batch and workspace, before dw_sgns_owner_pass1 with order_ready
@@ -724,12 +736,15 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
  *         gradient grad_rows[i];
+ *   grad_by_row (with grad_rows): grad_rows is the table's dense gradient [n_table_rows, dim]
+ *         and row r steps with grad_rows[r], which is cleared as it is read (one rank's touched
+ *         rows: no gather);
  *   pending: NULL, or uint8 [n_table_rows] (dw_sgns_owner_out_rows): a listed row marked there
  *         first gets the parameter half of step last_step[r], and its mark is cleared. */
 int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
                  uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
-                 const int64_t *n_rows_dev, int64_t n_rows_max, const float *grad_rows,
-                 const float *hist, int32_t step, void *stream);
+                 const int64_t *n_rows_dev, int64_t n_rows_max, float *grad_rows,
+                 int32_t grad_by_row, const float *hist, int32_t step, void *stream);
 
 /* out[i] = table[rows[i]] for i < min(*n_rows_dev, n_rows_max) (float32 rows of dim); with
  * zero_source the table rows are cleared in the same pass (the touched rows of the in-table
