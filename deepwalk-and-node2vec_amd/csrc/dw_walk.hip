@@ -796,6 +796,20 @@ __device__ __forceinline__ int64_t row_of_edge(const int64_t *__restrict__ row_p
     return lo;
 }
 
+// One edge's positions in the compact index (dw_n2v_edge_index_build): uint16 when the target
+// row has at most N2V_U16_MAX_DEG neighbours (every position fits), else int32 — half the
+// bytes for all but the hubs' lists (C5: 116 GB instead of 222 GB of positions). `wide` follows
+// from deg(v), which the step's record carries.
+constexpr int64_t N2V_U16_MAX_DEG = 65536;
+struct PosList {
+    const uint8_t *__restrict__ p;
+    bool wide;
+    __device__ __forceinline__ int64_t operator[](int64_t i) const {
+        return wide ? static_cast<int64_t>(reinterpret_cast<const int32_t *>(p)[i])
+                    : static_cast<int64_t>(reinterpret_cast<const uint16_t *>(p)[i]);
+    }
+};
+
 struct EdgeIndex {   // the membership tests' index (dw_edge_common_counts)
     const int32_t *col;
     const int64_t *adj_off;
@@ -890,17 +904,20 @@ __global__ void __launch_bounds__(256)
 // of its entries tested against N(t) in order. One lane per edge when the shorter list has
 // <= 16 entries, else the wave over that edge (ballot compaction keeps the list order). An
 // edge whose positions do not add up to its counted C sets DW_S_BAD_CSR.
+// (edges [e_begin, e_end) of a chunk: pos is the chunk's scratch, entry i of edge e at
+// off[e] - base + i)
 __global__ void __launch_bounds__(256)
     k_edge_cn_positions(EdgeIndex x, const int64_t *__restrict__ row_ptr, int64_t n_rows,
-                        int64_t n_edges, const uint32_t *__restrict__ cn,
-                        const int64_t *__restrict__ off, int32_t *__restrict__ pos,
+                        int64_t e_begin, int64_t e_end, const uint32_t *__restrict__ cn,
+                        const int64_t *__restrict__ off, int64_t base, int32_t *__restrict__ pos,
                         int32_t *__restrict__ pos_t, int32_t *status) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / WAVE;
     const uint64_t lt = (1ull << lane) - 1;   // lanes below this one
+    const int64_t n_edges = e_end;
     uint32_t probes = 0;
-    for (int64_t e0 = wave * WAVE; e0 < n_edges; e0 += n_waves * WAVE) {
+    for (int64_t e0 = e_begin + wave * WAVE; e0 < n_edges; e0 += n_waves * WAVE) {
         const int64_t e = e0 + lane;
         const bool valid = e < n_edges;
         int32_t t = 0;
@@ -915,7 +932,7 @@ __global__ void __launch_bounds__(256)
             rv = adj_row(row_ptr, x.adj_off, v);
             bt = row_bits(x, t);
             w = cn[e];
-            o = off[e];
+            o = off[e] - base;
             int32_t pt = -1;
             if (w >> 31) {
                 const int64_t p = lane_position(x.col, x.adj_hash, x.adj_hpos, rv, t, probes);
@@ -988,8 +1005,56 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// The sorted positions of a chunk's edges into the compact index: edge e's list at byte
+// boff[e] as uint16 (deg(col[e]) <= N2V_U16_MAX_DEG) or int32; one lane per edge for short
+// lists, the wave over a long one (coalesced stores).
+__global__ void __launch_bounds__(256)
+    k_n2v_pos_compact(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                      int64_t e_begin, int64_t e_end, const int64_t *__restrict__ off,
+                      int64_t base, const int64_t *__restrict__ boff,
+                      const int32_t *__restrict__ sorted, uint8_t *__restrict__ out) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int64_t n_waves = (int64_t)gridDim.x * blockDim.x / WAVE;
+    for (int64_t e0 = e_begin + wave * WAVE; e0 < e_end; e0 += n_waves * WAVE) {
+        const int64_t e = e0 + lane;
+        int64_t a = 0, c = 0, b = 0;
+        bool wide = false;
+        if (e < e_end) {
+            a = off[e] - base;
+            c = off[e + 1] - off[e];
+            b = boff[e];
+            const int32_t v = col[e];
+            wide = row_ptr[v + 1] - row_ptr[v] > N2V_U16_MAX_DEG;
+            if (c <= 32) {
+                for (int64_t i = 0; i < c; ++i) {
+                    if (wide)
+                        reinterpret_cast<int32_t *>(out + b)[i] = sorted[a + i];
+                    else
+                        reinterpret_cast<uint16_t *>(out + b)[i] =
+                            static_cast<uint16_t>(sorted[a + i]);
+                }
+            }
+        }
+        uint64_t heavy = __ballot(e < e_end && c > 32);
+        while (heavy) {
+            const int src = __ffsll((unsigned long long)heavy) - 1;
+            heavy &= heavy - 1;
+            const int64_t ha = __shfl(a, src), hc = __shfl(c, src), hb = __shfl(b, src);
+            const bool hw = __shfl(wide ? 1 : 0, src) != 0;
+            for (int64_t i = lane; i < hc; i += WAVE) {
+                if (hw)
+                    reinterpret_cast<int32_t *>(out + hb)[i] = sorted[ha + i];
+                else
+                    reinterpret_cast<uint16_t *>(out + hb)[i] = static_cast<uint16_t>(sorted[ha + i]);
+            }
+        }
+    }
+}
+
 // The walker's 32-B edge record: {x, deg(x), row_ptr[x] lo, hi} (the edge-inline CSR entry)
-// then {off lo, off hi, counts word, t's position in N(x)} — one line per step.
+// then {byte offset of its positions lo, hi, counts word, t's position in N(x)} — one line per
+// step.
 __global__ void k_n2v_edge_records(const int64_t *__restrict__ row_ptr,
                                    const int32_t *__restrict__ col, const uint32_t *__restrict__ cn,
                                    const int64_t *__restrict__ off,
@@ -1012,6 +1077,17 @@ __global__ void k_n2v_edge_records(const int64_t *__restrict__ row_ptr,
 struct CnCount64 {   // C(e) of a counts word, widened for the offsets' scan
     __host__ __device__ __forceinline__ int64_t operator()(uint32_t w) const {
         return static_cast<int64_t>(w & 0x7FFFFFFFu);
+    }
+};
+
+struct CnBytes {     // edge e's bytes in the compact index: C(e) entries of 2 or 4 B, to 4 B
+    const uint32_t *cn;
+    const int64_t *row_ptr;
+    const int32_t *col;
+    __host__ __device__ __forceinline__ int64_t operator()(int64_t e) const {
+        const int32_t v = col[e];
+        const int64_t w = row_ptr[v + 1] - row_ptr[v] > N2V_U16_MAX_DEG ? 4 : 2;
+        return ((static_cast<int64_t>(cn[e] & 0x7FFFFFFFu) * w) + 3) & ~int64_t(3);
     }
 };
 
@@ -1320,9 +1396,9 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // the first i at which the fp64 D_i turns positive, an exact draw from W_i / T up to the fp64
 // rounding of D (relative 2^-50), the same expressions as the oracle's (oracle/philox.py).
 template <bool EXACT = true>
-__device__ __forceinline__ int64_t n2v_pick_pos(const int32_t *__restrict__ P, int64_t C,
-                                                int64_t pt, int64_t n, double U, double ip,
-                                                double iq, uint32_t &loads) {
+__device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt, int64_t n,
+                                                double U, double ip, double iq,
+                                                uint32_t &loads) {   // loads: += 2-B units read (1 per uint16 entry, 2 per int32)
     const int64_t A = pt >= 0 ? 1 : 0;
     const double T = n2v_w(A, n - A - C, C, ip, iq);
     const double UT = U * T;
@@ -1335,16 +1411,16 @@ __device__ __forceinline__ int64_t n2v_pick_pos(const int32_t *__restrict__ P, i
     int64_t lo = 0, hi = C;           // first j with D(P[j], j + 1) > 0, else C
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        ++loads;
+        loads += P.wide ? 2u : 1u;
         if (D(P[mid], mid + 1) > 0.0)
             hi = mid;
         else
             lo = mid + 1;
     }
     const int64_t j = lo;
-    const int64_t pj = j < C ? static_cast<int64_t>(P[j]) : n - 1;   // D(pj) > 0
-    int64_t a = j > 0 ? static_cast<int64_t>(P[j - 1]) + 1 : 0;       // D(P[j-1]) <= 0
-    if (j > 0) ++loads;
+    const int64_t pj = j < C ? P[j] : n - 1;   // D(pj) > 0
+    int64_t a = j > 0 ? P[j - 1] + 1 : 0;       // D(P[j-1]) <= 0
+    if (j > 0) loads += P.wide ? 2u : 1u;
     int64_t b = pj;
     while (a < b) {                   // i < pj: c_i = j
         const int64_t mid = (a + b) >> 1;
@@ -1373,7 +1449,7 @@ constexpr int RP_T = 8;
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
     k_walk_replay_n2v_pos(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ rec,
-                          const int32_t *__restrict__ pos, int64_t n_rows,
+                          const uint8_t *__restrict__ pos, int64_t n_rows,
                           const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
                           const double *__restrict__ uniforms, double ip, double iq,
                           int32_t *__restrict__ out, int32_t *status, N2VDefer *__restrict__ defer,
@@ -1424,8 +1500,9 @@ __global__ void __launch_bounds__(256)
                         if (COUNT) ++steps;
                         const int64_t k =
                             prev < 0 ? uniform_pick_exact(U, n)
-                                     : n2v_pick_pos(pos + p_off, cw & 0x7FFFFFFFu,
-                                                    (cw >> 31) ? pt : -1, n, U, ip, iq, loads);
+                                     : n2v_pick_pos(PosList{pos + p_off, n > N2V_U16_MAX_DEG},
+                                                    cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n, U,
+                                                    ip, iq, loads);
                         if (k < 0) {   // the wave walker takes it from here
                             const uint32_t slot = atomicAdd(n_defer, 1u);
                             defer[slot] = N2VDefer{wk, e_in, st, v, prev, 0};
@@ -1461,12 +1538,12 @@ __global__ void __launch_bounds__(256)
             }
         }
     }
-    if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); 4 B per search load
+    if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); the positions read
         unsigned long long v2[2] = {(unsigned long long)loads, (unsigned long long)steps};
         for (int k = 0; k < 2; ++k)
             for (int off = WAVE / 2; off > 0; off >>= 1) v2[k] += __shfl_xor(v2[k], off, WAVE);
         if ((tid & (WAVE - 1)) == 0) {
-            atomicAdd(counters + 0, v2[0] * 4ull + v2[1] * 44ull);
+            atomicAdd(counters + 0, v2[0] * 2ull + v2[1] * 44ull);
             atomicAdd(counters + 2, v2[0]);
             atomicAdd(counters + 3, v2[1]);
         }
@@ -1583,18 +1660,19 @@ __global__ void __launch_bounds__(256)
 // node2vec (Philox) over the per-edge position index (dw_n2v_edge_index_build), one lane per
 // walker: the exact replay walker's step (k_walk_replay_n2v_pos) with its uniform drawn from
 // Philox instead of CPython's stream — one 32-B edge record per step (the next row and the
-// step's index entry), log2 C dependent 4-B position loads, no rejection rounds and no
+// step's index entry), log2 C dependent 2- or 4-B position loads, no rejection rounds and no
 // adjacency tests. The first step picks bounded32(r.x, n) (the unbiased first step,
 // random_walk_generator.py:97), later steps U = 53 bits of (r.x, r.y) (genrand_res53's split)
 // against the prefix weights of the reference rule (:100-108) through n2v_pick_pos<false>.
 // Counter (walk id lo, hi, step << 8, TAG_N2V_POS); restated in oracle/philox.py
 // (fast_walks_positions). The next step's draw is computed while the record load is in flight.
-// COUNT: realised bytes (the 32-B record and 4-B output per step, 4 B per position load, the
-// start's row_ptr pair) and steps into counters[0], counters[1], position loads in counters[3].
+// COUNT: realised bytes (the 32-B record and 4-B output per step, 2 or 4 B per position load,
+// the start's row_ptr pair) and steps into counters[0], counters[1], the positions read in 2-B
+// units in counters[3].
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
     k_walk_node2vec_positions(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ rec,
-                              const int32_t *__restrict__ pos, int64_t n_rows,
+                              const uint8_t *__restrict__ pos, int64_t n_rows,
                               const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
                               double ip, double iq, uint32_t k0, uint32_t k1, uint64_t walk_id0,
                               int32_t *__restrict__ out, int32_t *status,
@@ -1634,8 +1712,9 @@ __global__ void __launch_bounds__(256)
                 const double U = static_cast<double>((static_cast<uint64_t>(r.x >> 5) << 26) |
                                                      static_cast<uint64_t>(r.y >> 6)) *
                                  0x1p-53;
-                k = n2v_pick_pos<false>(pos + p_off, cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n,
-                                        U, ip, iq, loads);
+                k = n2v_pick_pos<false>(PosList{pos + p_off, n > N2V_U16_MAX_DEG},
+                                        cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n, U, ip, iq,
+                                        loads);
             }
             const int64_t e = a + k;
             const int4 r0 = rec[2 * e], r1 = rec[2 * e + 1];
@@ -1671,7 +1750,7 @@ __global__ void __launch_bounds__(256)
     if (COUNT) {
         const int lane = threadIdx.x & (WAVE - 1);
         unsigned long long v3[3] = {
-            (unsigned long long)loads * 4ull + (unsigned long long)steps * 36ull +
+            (unsigned long long)loads * 2ull + (unsigned long long)steps * 36ull +
                 (w < n_walks ? 20ull : 0ull),
             (unsigned long long)steps, (unsigned long long)loads};
         for (int k = 0; k < 3; ++k)
@@ -2223,85 +2302,131 @@ int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int6
     return DW_OK;
 }
 
-int dw_n2v_edge_offsets(const uint32_t *edge_cn, int64_t n_edges, int64_t *off, void *tmp,
+int dw_n2v_edge_offsets(const int64_t *row_ptr, const int32_t *col, const uint32_t *edge_cn,
+                        int64_t n_edges, int64_t *off, int64_t *byte_off, void *tmp,
                         size_t *tmp_bytes, void *stream) {
     DW_REQUIRE(n_edges >= 0 && tmp_bytes, "dw_n2v_edge_offsets: bad arguments");
     DW_REQUIRE(n_edges < (int64_t(1) << 32), "dw_n2v_edge_offsets: too many edges");
     const auto in = rocprim::make_transform_iterator(edge_cn, CnCount64{});
+    const auto inb = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0),
+                                                      CnBytes{edge_cn, row_ptr, col});
     const hipStream_t st = dw::as_stream(stream);
-    size_t need = 0;
-    if (n_edges > 0)
+    size_t need = 0, need_b = 0;
+    if (n_edges > 0) {
         DW_WALK_HIP_OK(rocprim::inclusive_scan(nullptr, need, in, static_cast<int64_t *>(nullptr),
                                                static_cast<size_t>(n_edges),
                                                rocprim::plus<int64_t>(), st),
                        "dw_n2v_edge_offsets: scan");
+        DW_WALK_HIP_OK(rocprim::inclusive_scan(nullptr, need_b, inb,
+                                               static_cast<int64_t *>(nullptr),
+                                               static_cast<size_t>(n_edges),
+                                               rocprim::plus<int64_t>(), st),
+                       "dw_n2v_edge_offsets: byte scan");
+        if (need_b > need) need = need_b;
+    }
     if (!tmp) {
         *tmp_bytes = need > 0 ? need : 1;
         return DW_OK;
     }
     DW_REQUIRE(*tmp_bytes >= need, "dw_n2v_edge_offsets: tmp too small");
-    DW_REQUIRE(off && (n_edges == 0 || edge_cn), "dw_n2v_edge_offsets: null pointer");
+    DW_REQUIRE(off && byte_off && (n_edges == 0 || (edge_cn && row_ptr && col)),
+               "dw_n2v_edge_offsets: null pointer");
     DW_WALK_HIP_OK(hipMemsetAsync(off, 0, sizeof(int64_t), st), "dw_n2v_edge_offsets: memset");
-    if (n_edges > 0)
+    DW_WALK_HIP_OK(hipMemsetAsync(byte_off, 0, sizeof(int64_t), st),
+                   "dw_n2v_edge_offsets: memset");
+    if (n_edges > 0) {
         DW_WALK_HIP_OK(rocprim::inclusive_scan(tmp, need, in, off + 1,
                                                static_cast<size_t>(n_edges),
                                                rocprim::plus<int64_t>(), st),
                        "dw_n2v_edge_offsets: scan");
+        DW_WALK_HIP_OK(rocprim::inclusive_scan(tmp, need, inb, byte_off + 1,
+                                               static_cast<size_t>(n_edges),
+                                               rocprim::plus<int64_t>(), st),
+                       "dw_n2v_edge_offsets: byte scan");
+    }
     return DW_OK;
 }
+
+namespace {
+struct MinusBase {   // a chunk's segment offsets relative to its first entry
+    int64_t base;
+    __host__ __device__ __forceinline__ int64_t operator()(int64_t o) const { return o - base; }
+};
+}  // namespace
 
 int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
                             const int32_t *adj_hash, const int32_t *adj_hpos,
                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
-                            const uint32_t *edge_cn, const int64_t *off, int64_t n_rows,
-                            int64_t n_edges, int64_t n_pos, int32_t *pos, int32_t *pos_unsorted,
-                            int32_t *rec, void *tmp, size_t *tmp_bytes, int32_t *status,
+                            const uint32_t *edge_cn, const int64_t *off, const int64_t *byte_off,
+                            int64_t n_rows, int64_t n_edges, int64_t e_begin, int64_t e_end,
+                            int64_t base, int64_t n_chunk_pos, uint8_t *pos, int32_t *scratch,
+                            int32_t *pos_t, void *tmp, size_t *tmp_bytes, int32_t *status,
                             void *stream) {
-    DW_REQUIRE(n_rows >= 0 && n_edges >= 0 && n_pos >= 0 && tmp_bytes,
+    DW_REQUIRE(n_rows >= 0 && n_edges >= 0 && tmp_bytes && 0 <= e_begin && e_begin <= e_end &&
+                   e_end <= n_edges && n_chunk_pos >= 0,
                "dw_n2v_edge_index_build: bad arguments");
-    DW_REQUIRE(n_edges < (int64_t(1) << 31) && n_pos < (int64_t(1) << 32),
-               "dw_n2v_edge_index_build: index too large for one segmented sort");
+    DW_REQUIRE(n_edges < (int64_t(1) << 31) && n_chunk_pos < (int64_t(1) << 31),
+               "dw_n2v_edge_index_build: a chunk of < 2^31 entries (and edges) per call");
     const hipStream_t st = dw::as_stream(stream);
     uint32_t end_bit = 1;
     while (end_bit < 31 && (int64_t(1) << end_bit) < n_rows) ++end_bit;   // positions < deg <= V
-    // tmp: t's positions (int32 per edge), then the segmented sort's storage
-    const size_t pt_bytes = ((static_cast<size_t>(n_edges) * 4 + 255) / 256) * 256;
+    const int64_t n_seg = e_end - e_begin;
     size_t sort_bytes = 0;
-    if (n_pos > 0)
+    const auto sb = rocprim::make_transform_iterator(off + e_begin, MinusBase{base});
+    const auto se = rocprim::make_transform_iterator(off + e_begin + 1, MinusBase{base});
+    if (n_chunk_pos > 0)
         DW_WALK_HIP_OK(rocprim::segmented_radix_sort_keys(
                            nullptr, sort_bytes, static_cast<const int32_t *>(nullptr),
-                           static_cast<int32_t *>(nullptr), static_cast<unsigned>(n_pos),
-                           static_cast<unsigned>(n_edges), static_cast<const int64_t *>(nullptr),
-                           static_cast<const int64_t *>(nullptr), 0, end_bit, st),
+                           static_cast<int32_t *>(nullptr), static_cast<unsigned>(n_chunk_pos),
+                           static_cast<unsigned>(n_seg > 0 ? n_seg : 1), sb, se, 0, end_bit, st),
                        "dw_n2v_edge_index_build: sort");
+    // tmp: the unsorted positions (n_chunk_pos int32), then the segmented sort's storage
+    const size_t un_bytes = ((static_cast<size_t>(n_chunk_pos) * 4 + 255) / 256) * 256;
     if (!tmp) {
-        *tmp_bytes = pt_bytes + sort_bytes + 256;
+        *tmp_bytes = un_bytes + sort_bytes + 256;
         return DW_OK;
     }
-    DW_REQUIRE(*tmp_bytes >= pt_bytes + sort_bytes, "dw_n2v_edge_index_build: tmp too small");
-    if (n_edges == 0 || n_rows == 0) return DW_OK;
-    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && adj_hpos && edge_cn && off && rec &&
-                   status && (n_pos == 0 || (pos && pos_unsorted)),
+    DW_REQUIRE(*tmp_bytes >= un_bytes + sort_bytes, "dw_n2v_edge_index_build: tmp too small");
+    if (n_seg == 0 || n_rows == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && adj_off && adj_hash && adj_hpos && edge_cn && off && byte_off &&
+                   pos_t && status && (n_chunk_pos == 0 || (pos && scratch)),
                "dw_n2v_edge_index_build: null pointer");
     DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
                "dw_n2v_edge_index_build: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
-    int32_t *pos_t = static_cast<int32_t *>(tmp);
-    int64_t blocks = (n_edges + 255) / 256;
+    int32_t *unsorted = static_cast<int32_t *>(tmp);
+    int64_t blocks = (n_seg + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     const EdgeIndex x{col, adj_off, adj_hash, adj_hpos, hub_idx, hub_bits, hub_words};
     hipLaunchKernelGGL(k_edge_cn_positions, dim3((unsigned)blocks), dim3(256), 0, st, x, row_ptr,
-                       n_rows, n_edges, edge_cn, off, pos_unsorted, pos_t, status);
+                       n_rows, e_begin, e_end, edge_cn, off, base, unsorted, pos_t, status);
     DW_LAUNCH_CHECK("dw_n2v_edge_index_build/positions");
-    if (n_pos > 0)
+    if (n_chunk_pos > 0) {
         DW_WALK_HIP_OK(rocprim::segmented_radix_sort_keys(
-                           static_cast<char *>(tmp) + pt_bytes, sort_bytes,
-                           static_cast<const int32_t *>(pos_unsorted), pos,
-                           static_cast<unsigned>(n_pos), static_cast<unsigned>(n_edges), off,
-                           off + 1, 0, end_bit, st),
+                           static_cast<char *>(tmp) + un_bytes, sort_bytes,
+                           static_cast<const int32_t *>(unsorted), scratch,
+                           static_cast<unsigned>(n_chunk_pos), static_cast<unsigned>(n_seg), sb,
+                           se, 0, end_bit, st),
                        "dw_n2v_edge_index_build: sort");
-    hipLaunchKernelGGL(k_n2v_edge_records, dim3((unsigned)blocks), dim3(256), 0, st, row_ptr, col,
-                       edge_cn, off, pos_t, n_edges, reinterpret_cast<int4 *>(rec));
-    DW_LAUNCH_CHECK("dw_n2v_edge_index_build/records");
+        hipLaunchKernelGGL(k_n2v_pos_compact, dim3((unsigned)blocks), dim3(256), 0, st, row_ptr,
+                           col, e_begin, e_end, off, base, byte_off, scratch, pos);
+        DW_LAUNCH_CHECK("dw_n2v_edge_index_build/compact");
+    }
+    return DW_OK;
+}
+
+int dw_n2v_edge_records(const int64_t *row_ptr, const int32_t *col, const uint32_t *edge_cn,
+                        const int64_t *byte_off, const int32_t *pos_t, int64_t n_edges,
+                        int32_t *rec, void *stream) {
+    DW_REQUIRE(n_edges >= 0, "dw_n2v_edge_records: bad size");
+    if (n_edges == 0) return DW_OK;
+    DW_REQUIRE(row_ptr && col && edge_cn && byte_off && pos_t && rec,
+               "dw_n2v_edge_records: null pointer");
+    int64_t blocks = (n_edges + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_n2v_edge_records, dim3((unsigned)blocks), dim3(256), 0,
+                       dw::as_stream(stream), row_ptr, col, edge_cn, byte_off, pos_t, n_edges,
+                       reinterpret_cast<int4 *>(rec));
+    DW_LAUNCH_CHECK("dw_n2v_edge_records");
     return DW_OK;
 }
 
@@ -2314,7 +2439,7 @@ int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
                              const int32_t *adj_hash, const int32_t *adj_hpos,
                              const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
                              const uint32_t *edge_cn, const int32_t *n2v_rec,
-                             const int32_t *n2v_pos, int64_t n_rows, const int32_t *starts,
+                             const uint8_t *n2v_pos, int64_t n_rows, const int32_t *starts,
                              int64_t n_walks, int32_t walk_length, double p, double q,
                              const double *uniforms, int32_t *out, int32_t *status,
                              void *workspace, size_t workspace_bytes, uint64_t *counters,
@@ -2497,7 +2622,7 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
                                  reinterpret_cast<unsigned long long *>(counters));
 }
 
-int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const int32_t *n2v_pos,
+int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const uint8_t *n2v_pos,
                            int64_t n_rows, const int32_t *starts, int64_t n_walks,
                            int32_t walk_length, double p, double q, uint64_t seed,
                            uint64_t walk_id0, int32_t *out, int32_t *status, uint64_t *counters,

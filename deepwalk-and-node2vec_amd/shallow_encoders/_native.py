@@ -37,7 +37,7 @@ DW_EXACT_DEFER = 1
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -155,9 +155,11 @@ SIGNATURES = {
     'dw_edge_common_counts': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
                                              _p]),
     'dw_hub_bitmaps': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _i64, _p, _p]),
-    'dw_n2v_edge_offsets': (ctypes.c_int, [_p, _i64, _p, _p, _szp, _p]),
-    'dw_n2v_edge_index_build': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _i64,
-                                               _i64, _i64, _p, _p, _p, _p, _szp, _p, _p]),
+    'dw_n2v_edge_offsets': (ctypes.c_int, [_p, _p, _p, _i64, _p, _p, _p, _szp, _p]),
+    'dw_n2v_edge_index_build': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p,
+                                               _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p,
+                                               _p, _szp, _p, _p]),
+    'dw_n2v_edge_records': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _p]),
     'dw_walk_replay_positions_workspace_bytes': (ctypes.c_size_t, [_i64]),
     'dw_exact_register': (ctypes.c_int, [_p, _p, _i64, _i32, _i32]),
     'dw_exact_unregister': (ctypes.c_int, [_p]),

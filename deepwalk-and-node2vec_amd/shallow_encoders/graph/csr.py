@@ -250,72 +250,104 @@ class CSRGraph:
             self._build_n2v_index(dev)
         return d
 
-    # the position index is built when its entries, scratch and records fit this many bytes and
-    # half the device's free memory (DW_N2V_INDEX_BYTES overrides both); above it the walker
-    # keeps the counted classification
-    N2V_INDEX_BYTES = 48 << 30
+    # the position index is built when its entries, records and build scratch fit this many
+    # bytes and the device's free memory less a reserve (DW_N2V_INDEX_BYTES overrides both);
+    # above it the walker keeps the counted classification
+    N2V_INDEX_BYTES = 192 << 30
+    N2V_INDEX_RESERVE = 16 << 30
+    # entries sorted per build launch (the scratch: 8 B each plus the sort's storage)
+    N2V_CHUNK_ENTRIES = 1 << 28
 
     def _build_n2v_index(self, dev) -> None:
-        """n2v_rec int32[nnz, 8] / n2v_pos int32[entries] (dw_n2v_edge_offsets +
-        dw_n2v_edge_index_build): per directed edge t -> v, t's position in N(v) and the sorted
-        positions of N(t) ∩ N(v) — the exact node2vec pick's binary search
-        (dw_walk_replay_positions). Both None when the index would exceed the byte budget;
-        n2v_index_info = {'entries', 'bytes', 'build_ms'} or {'entries', 'bytes', 'skipped'}."""
+        """n2v_rec int32[nnz, 8] / n2v_pos uint8[bytes] (dw_n2v_edge_offsets +
+        dw_n2v_edge_index_build + dw_n2v_edge_records): per directed edge t -> v, t's position in
+        N(v) and the sorted positions of N(t) ∩ N(v) — uint16 where deg(v) <= 65536, else int32 —
+        the exact node2vec pick's binary search (dw_walk_replay_positions,
+        dw_walk_fast_positions). Built in chunks of about N2V_CHUNK_ENTRIES entries, so the
+        scratch stays bounded while the index grows to the graph's size (C5: 132 GB). Both None
+        when the index would exceed the byte budget; n2v_index_info = {'entries', 'bytes',
+        'chunks', 'build_ms'} or {'entries', 'bytes', 'skipped'}."""
         import ctypes
         import os
         import time
         d = self.device_tensors(dev, need_edge_cn=True)
         E = self.nnz
+        colp = _native.ptr(d['col']) if E else None
         with torch.cuda.device(dev):
             s = _native.stream(dev)
             t0 = time.perf_counter()
             off = torch.empty(E + 1, dtype=torch.int64, device=dev)
+            boff = torch.empty(E + 1, dtype=torch.int64, device=dev)
             nb = ctypes.c_size_t(0)
-            _native.call('dw_n2v_edge_offsets', _native.ptr(d['edge_cn']), E, _native.ptr(off),
-                         None, ctypes.byref(nb), s)
+            oargs = [_native.ptr(d['row_ptr']), colp, _native.ptr(d['edge_cn']), E,
+                     _native.ptr(off), _native.ptr(boff)]
+            _native.call('dw_n2v_edge_offsets', *oargs, None, ctypes.byref(nb), s)
             tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
-            _native.call('dw_n2v_edge_offsets', _native.ptr(d['edge_cn']), E, _native.ptr(off),
-                         _native.ptr(tmp), ctypes.byref(nb), s)
+            _native.call('dw_n2v_edge_offsets', *oargs, _native.ptr(tmp), ctypes.byref(nb), s)
             del tmp
-            n_pos = int(off[E])            # synchronises: the index size
-            nb = ctypes.c_size_t(0)
-            args = [_native.ptr(d['row_ptr']), _native.ptr(d['col']) if E else None,
-                    _native.ptr(d['adj_off']), _native.ptr(d['adj_hash']),
-                    _native.ptr(d['adj_hpos']), _native.ptr(d['hub_idx']),
-                    _native.ptr(d['hub_bits']), d['hub_words'], _native.ptr(d['edge_cn']),
-                    _native.ptr(off), self.vocab_size, E, n_pos]
-            fits = n_pos < (1 << 32) and E < (1 << 31)
+            n_pos, n_bytes = (int(x) for x in torch.stack([off[E], boff[E]]).tolist())
+            # chunk c = the edges [e_c, e_{c+1}), e_c = the first edge whose entries start at or
+            # after c * K: at most K + max C(e) entries each
+            K = self.N2V_CHUNK_ENTRIES
+            cuts = torch.arange(0, max(n_pos, 1), K, dtype=torch.int64, device=dev)
+            starts = torch.searchsorted(off, cuts).clamp_(max=E)
+            bounds = torch.unique(torch.cat([starts, torch.tensor([0, E], device=dev)]))
+            b_host = bounds.tolist()
+            o_host = off[bounds].tolist()
+            chunks = [(b_host[k], b_host[k + 1], o_host[k], o_host[k + 1] - o_host[k])
+                      for k in range(len(b_host) - 1)]
+            max_pos = max([c[3] for c in chunks] + [0])
+            fits = E < (1 << 31) and max_pos < (1 << 31)
+            tmp_need = 1
+            args = [_native.ptr(d['row_ptr']), colp, _native.ptr(d['adj_off']),
+                    _native.ptr(d['adj_hash']), _native.ptr(d['adj_hpos']),
+                    _native.ptr(d['hub_idx']), _native.ptr(d['hub_bits']), d['hub_words'],
+                    _native.ptr(d['edge_cn']), _native.ptr(off), _native.ptr(boff),
+                    self.vocab_size, E]
             if fits:
-                _native.call('dw_n2v_edge_index_build', *args, None, None, None, None,
-                             ctypes.byref(nb), None, s)
-            need = 8 * n_pos + 32 * E + int(nb.value)
-            # the budget: DW_N2V_INDEX_BYTES, else N2V_INDEX_BYTES capped at half the device's
-            # free memory (the walker's other buffers and the training tables share it)
+                for e0, e1, base, cnt in chunks:
+                    _native.call('dw_n2v_edge_index_build', *args, e0, e1, base, cnt, None, None,
+                                 None, None, ctypes.byref(nb), None, s)
+                    tmp_need = max(tmp_need, int(nb.value))
+            index_bytes = n_bytes + 32 * E
+            need = index_bytes + 4 * E + 4 * max_pos + tmp_need
+            # the budget: DW_N2V_INDEX_BYTES, else N2V_INDEX_BYTES capped at the device's free
+            # memory less a reserve (the walker's other buffers and the training tables share it)
             env = os.environ.get('DW_N2V_INDEX_BYTES')
             budget = (int(env) if env is not None else
-                      min(self.N2V_INDEX_BYTES, torch.cuda.mem_get_info(dev)[0] // 2))
-            skipped = {'entries': n_pos, 'bytes': need, 'skipped': True}
+                      min(self.N2V_INDEX_BYTES,
+                          torch.cuda.mem_get_info(dev)[0] - self.N2V_INDEX_RESERVE))
+            skipped = {'entries': n_pos, 'bytes': index_bytes, 'build_bytes': need,
+                       'skipped': True}
             if not fits or need > budget:
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = skipped
                 return
             try:
-                pos = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
-                scratch = torch.empty(max(n_pos, 1), dtype=torch.int32, device=dev)
+                pos = torch.empty(max(n_bytes, 4), dtype=torch.uint8, device=dev)
                 rec = torch.empty((max(E, 1), 8), dtype=torch.int32, device=dev)
-                tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+                pos_t = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+                scratch = torch.empty(max(max_pos, 1), dtype=torch.int32, device=dev)
+                tmp = torch.empty(tmp_need, dtype=torch.uint8, device=dev)
             except torch.OutOfMemoryError:   # the wave walker needs none of it
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = dict(skipped, out_of_memory=True)
                 torch.cuda.empty_cache()
                 return
-            _native.call('dw_n2v_edge_index_build', *args, _native.ptr(pos), _native.ptr(scratch),
-                         _native.ptr(rec), _native.ptr(tmp), ctypes.byref(nb),
-                         _native.ptr(d['status']), s)
-            del tmp, scratch, off
+            for e0, e1, base, cnt in chunks:
+                nb.value = tmp_need
+                _native.call('dw_n2v_edge_index_build', *args, e0, e1, base, cnt,
+                             _native.ptr(pos), _native.ptr(scratch), _native.ptr(pos_t),
+                             _native.ptr(tmp), ctypes.byref(nb), _native.ptr(d['status']), s)
+            del tmp, scratch
+            _native.call('dw_n2v_edge_records', _native.ptr(d['row_ptr']), colp,
+                         _native.ptr(d['edge_cn']), _native.ptr(boff), _native.ptr(pos_t), E,
+                         _native.ptr(rec), s)
+            del pos_t, off, boff
             _native.check_status(d['status'], 'node2vec position index build')
             d['n2v_rec'], d['n2v_pos'] = rec, pos
-            d['n2v_index_info'] = {'entries': n_pos, 'bytes': 4 * n_pos + 32 * E,
+            d['n2v_index_info'] = {'entries': n_pos, 'bytes': index_bytes,
+                                   'chunks': len(chunks),
                                    'build_ms': (time.perf_counter() - t0) * 1e3}
 
     # rows longer than the replay walker's LDS stage (1,024) get a V-bit neighbour map, the

@@ -383,7 +383,7 @@ class RandomWalk(ABC):
         dev = _native.require_device(self._device)
         starts = torch.as_tensor(start_ids, dtype=torch.int32).to(dev).contiguous()
         n, L = int(starts.numel()), self._length
-        if self._positions_walker(dev):   # {'bytes', 'steps', 0, position loads}
+        if self._positions_walker(dev):   # {'bytes', 'steps', 0, position 2-B units read}
             d = self._csr.device_tensors(dev)
             if out is None:
                 out = torch.empty((n, L), dtype=torch.int32, device=dev)

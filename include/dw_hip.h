@@ -254,27 +254,40 @@ int dw_edge_common_counts(const int64_t *row_ptr, const int32_t *col, const int6
                           int64_t n_rows, int64_t n_edges, uint32_t *edge_cn, void *stream);
 
 /* The node2vec position index, step 1: off int64[n_edges + 1] = exclusive prefix sums of the
- * common-neighbour counts C(e) (edge_cn bits 0-30); off[n_edges] = the index's entry count.
- * tmp == NULL: *tmp_bytes = the scan's scratch size, nothing launched. */
-int dw_n2v_edge_offsets(const uint32_t *edge_cn, int64_t n_edges, int64_t *off, void *tmp,
+ * common-neighbour counts C(e) (edge_cn bits 0-30; off[n_edges] = the index's entry count) and
+ * byte_off int64[n_edges + 1] = those of the edges' byte sizes in the compact index: C(e)
+ * entries of 2 B (uint16) when the target row col[e] has <= 65536 neighbours, else 4 B
+ * (int32), rounded up to 4 B (byte_off[n_edges] = the index's size). tmp == NULL: *tmp_bytes =
+ * the scans' scratch size, nothing launched. n_edges < 2^32. */
+int dw_n2v_edge_offsets(const int64_t *row_ptr, const int32_t *col, const uint32_t *edge_cn,
+                        int64_t n_edges, int64_t *off, int64_t *byte_off, void *tmp,
                         size_t *tmp_bytes, void *stream);
 
-/* The node2vec position index, step 2 (random_walk_generator.py:100-108: at a step t -> v only
- * the 1/p neighbour t and the 1/q neighbours N(t) ∩ N(v) weigh other than 1): pos int32[n_pos]
- * (n_pos = off[n_edges]) holds, at off[e], the positions in N(v) of the C(e) common neighbours
- * of edge e = (t -> v), ascending; rec int32[n_edges][8] the walker's 32-B edge records {v,
- * deg(v), row_ptr[v] lo, hi, off[e] lo, hi, edge_cn[e], position of t in N(v) or -1}.
- * pos_unsorted int32[n_pos] is scratch. Positions come from the shorter list as the counts do
- * (same adjacency index arguments as dw_edge_common_counts); a row whose positions disagree
- * with its count sets DW_S_BAD_CSR in *status. tmp == NULL: *tmp_bytes = the scratch size.
- * n_pos < 2^32 and n_edges < 2^31. */
+/* The node2vec position index, step 2, for the edges [e_begin, e_end) (random_walk_generator.py:
+ * 100-108: at a step t -> v only the 1/p neighbour t and the 1/q neighbours N(t) ∩ N(v) weigh
+ * other than 1): writes, at pos + byte_off[e], the positions in N(v) of the C(e) common
+ * neighbours of edge e = (t -> v), ascending, as uint16 or int32 (dw_n2v_edge_offsets), and
+ * pos_t[e] = the position of t in N(v) or -1. The chunk's entries are off[e_begin] - base ..
+ * off[e_end] - base (base = off[e_begin], n_chunk_pos = off[e_end] - base < 2^31); scratch
+ * int32[n_chunk_pos] holds the chunk's sorted positions. A caller bounds the scratch by cutting
+ * the edges into chunks. Positions come from the shorter list as the counts do (same adjacency
+ * index arguments as dw_edge_common_counts); a row whose positions disagree with its count sets
+ * DW_S_BAD_CSR in *status. tmp == NULL: *tmp_bytes = the scratch size for n_chunk_pos entries
+ * and e_end - e_begin edges. n_edges < 2^31. */
 int dw_n2v_edge_index_build(const int64_t *row_ptr, const int32_t *col, const int64_t *adj_off,
                             const int32_t *adj_hash, const int32_t *adj_hpos,
                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
-                            const uint32_t *edge_cn, const int64_t *off, int64_t n_rows,
-                            int64_t n_edges, int64_t n_pos, int32_t *pos, int32_t *pos_unsorted,
-                            int32_t *rec, void *tmp, size_t *tmp_bytes, int32_t *status,
+                            const uint32_t *edge_cn, const int64_t *off, const int64_t *byte_off,
+                            int64_t n_rows, int64_t n_edges, int64_t e_begin, int64_t e_end,
+                            int64_t base, int64_t n_chunk_pos, uint8_t *pos, int32_t *scratch,
+                            int32_t *pos_t, void *tmp, size_t *tmp_bytes, int32_t *status,
                             void *stream);
+
+/* The node2vec position index, step 3: rec int32[n_edges][8], the walker's 32-B edge records
+ * {v, deg(v), row_ptr[v] lo, hi, byte_off[e] lo, hi, edge_cn[e], pos_t[e]}. */
+int dw_n2v_edge_records(const int64_t *row_ptr, const int32_t *col, const uint32_t *edge_cn,
+                        const int64_t *byte_off, const int32_t *pos_t, int64_t n_edges,
+                        int32_t *rec, void *stream);
 
 /* ---- deterministic accumulation (SURVEY.md §5 "race detection": run-to-run, eager / graph
  * and 1 / N-rank bit-identical tables) --------------------------------------------------------
@@ -317,7 +330,7 @@ int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
                              const int32_t *adj_hash, const int32_t *adj_hpos,
                              const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
                              const uint32_t *edge_cn, const int32_t *n2v_rec,
-                             const int32_t *n2v_pos, int64_t n_rows, const int32_t *starts,
+                             const uint8_t *n2v_pos, int64_t n_rows, const int32_t *starts,
                              int64_t n_walks, int32_t walk_length, double p, double q,
                              const double *uniforms, int32_t *out, int32_t *status,
                              void *workspace, size_t workspace_bytes, uint64_t *counters,
@@ -372,15 +385,15 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
                          uint64_t *counters, void *stream);
 
 /* node2vec with Philox draws over the per-edge position index (n2v_rec / n2v_pos from
- * dw_n2v_edge_index_build): one lane per walker, one 32-B edge record and log2 C dependent 4-B
- * position loads per step, no rejection rounds. The law is Node2Vec.walk's
+ * dw_n2v_edge_index_build): one lane per walker, one 32-B edge record and log2 C dependent 2-B
+ * (4-B for a hub target's list) position loads per step, no rejection rounds. The law is Node2Vec.walk's
  * (random_walk_generator.py:94-119, the reference's inverted q rule): step 1 picks
  * bounded32(r.x, deg) (:97, prev None), later steps the first neighbour i whose exact prefix
  * weight W_i = a_i/p + b_i + c_i/q exceeds U*T, U = 53 bits of (r.x, r.y), with the fp64
  * expressions of the exact replay's pick; Philox counter (walk id lo, hi, step << 8, 'NP').
  * Unweighted graphs (the index has no weights). counters: NULL, or uint64[4] += {load + store
- * bytes, steps, 0, position loads}. Reads walk_id0 from a bound dw_step_scalars block. */
-int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const int32_t *n2v_pos,
+ * bytes, steps, 0, position 2-B units read}. Reads walk_id0 from a bound dw_step_scalars block. */
+int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const uint8_t *n2v_pos,
                            int64_t n_rows, const int32_t *starts, int64_t n_walks,
                            int32_t walk_length, double p, double q, uint64_t seed,
                            uint64_t walk_id0, int32_t *out, int32_t *status, uint64_t *counters,

@@ -124,6 +124,24 @@ def main():
          walks_per_s=n / (best * 1e-3), bytes_per_step=c['bytes'] / max(c['steps'], 1),
          entries_per_step=c['entries'] / max(c['steps'], 1),
          frac_hbm=c['bytes'] / (best * 1e-3) / 8e12)
+    # the Philox walker over the same index (dw_walk_fast_positions), walks from every start
+    wp = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=3, device=dev)
+    wp.walk_batch(st[:64], walk_id0=0, out=out[:64])
+    best = None
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        wp.walk_batch(st, walk_id0=0, out=out, check=False)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    c = wp.count_traffic(st, walk_id0=0, out=torch.empty_like(out))
+    emit(stage='rate_philox', walker=c.get('walker'), walks=n, kernel_ms=best,
+         walks_per_s=n / (best * 1e-3), bytes_per_step=c['bytes'] / max(c['steps'], 1),
+         position_units_per_step=c.get('position_loads', 0) / max(c['steps'], 1),
+         frac_hbm=c['bytes'] / (best * 1e-3) / 8e12)
+    w.walk_batch(st, uniforms=u, out=out, check=False)
     # the same walks through the wave walker (DW_N2V_POS=0) on a sample: bit-equal
     k = args.check_walks
     os.environ['DW_N2V_POS'] = '0'

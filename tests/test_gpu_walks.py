@@ -188,6 +188,28 @@ def test_fast_node2vec_hub_staging_vs_oracle(layout, hip_device):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (4.0, 0.5)])
+def test_positions_walkers_int32_lists_vs_oracle(p, q, hip_device):
+    """A hub of 66,000 neighbours (> 65,536: its edges' position lists are int32, the rest
+    uint16): both position walkers — Philox (dw_walk_fast_positions) and the exact replay
+    (dw_walk_replay_positions) — equal their oracles bit for bit on walks through the hub."""
+    csr = _hub_graph(n_leaves=66_000, seed=2)
+    L = 8
+    starts = np.array([1] * 24 + [2, 3, 70, 65_999, 65_500, 40_000, 12, 9] * 3, dtype=np.int32)
+    w = Node2Vec(csr, L, p=p, q=q, rng='philox', seed=9)
+    got = w.walk_batch(torch.as_tensor(starts), walk_id0=0).cpu().numpy()
+    assert csr.device_tensors(hip_device).get('n2v_rec') is not None
+    exp = ph.fast_walks_positions(csr.row_ptr, csr.col, starts, L, p, q, seed=9, walk_id0=0)
+    np.testing.assert_array_equal(got, exp)
+    assert (got[:, 1:] > 65_536).any() and (got == 1).sum() > 24
+    u = np.random.default_rng(4).random((len(starts), L - 1))
+    got = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(
+        torch.as_tensor(starts), uniforms=u).cpu().numpy()
+    ref = walk_ref.walks_replay(walk_ref.CSR(csr.row_ptr, csr.host_col(), None), starts, L,
+                                'node2vec', p, q, u)
+    np.testing.assert_array_equal(got, ref)
+
+
 @pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0), (0.3, 3.0), (4.0, 0.25)])
 def test_fast_positions_walker_vs_oracle_rmat12(p, q, hip_device):
     """The Philox walker over the position index (dw_walk_fast_positions) on the R-MAT-12
@@ -406,7 +428,7 @@ def test_counted_node2vec_walks_equal_and_count(hip_device):
                 assert c['bytes'] >= c['steps'] * 36 + c['blocks'] * 16
             else:
                 assert c['walker'] == 'dw_walk_fast_positions' and c['blocks'] == 0
-                assert c['bytes'] == c['steps'] * 36 + 4 * c['position_loads'] + n * 20
+                assert c['bytes'] == c['steps'] * 36 + 2 * c['position_loads'] + n * 20
                 assert c['position_loads'] > 0
 
 
@@ -581,39 +603,69 @@ def test_node2vec_replay_edge_counts_same_walks(p, q, hip_device, monkeypatch):
     assert c1['steps'] == c0['steps'] and c1['entries'] < c0['entries']
 
 
-@pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops', 'self_looped_leaves'])
-def test_n2v_position_index_vs_oracle(which, hip_device):
+def _decode_n2v_pos(pos_bytes, boff, cnt, wide):
+    """The compact index's lists, flattened in edge order: C(e) uint16 (int32 where wide[e])
+    entries at byte boff[e]."""
+    out = []
+    for e in np.nonzero(cnt)[0]:
+        o, c = int(boff[e]), int(cnt[e])
+        dt = np.int32 if wide[e] else np.uint16
+        out.append(pos_bytes[o:o + c * np.dtype(dt).itemsize].view(dt).astype(np.int64))
+    return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+
+@pytest.mark.parametrize('which', ['karate', 'rmat12', 'self_loops', 'self_looped_leaves',
+                                   'hub_66k', 'rmat12_chunked'])
+def test_n2v_position_index_vs_oracle(which, hip_device, monkeypatch):
     """dw_n2v_edge_index_build (the node2vec position index: per directed edge t -> v, t's
-    position in N(v) and the ascending positions of N(t) ∩ N(v) \\ {t}) equals the oracle's
-    restatement of the reference rule (walk_ref.edge_class_positions) on every edge; the 32-B
-    records carry the edge-inline entry, the offset and the counts word."""
-    if which == 'karate':
+    position in N(v) and the ascending positions of N(t) ∩ N(v) \\ {t}, uint16 — int32 where
+    deg(v) > 65536) equals the oracle's restatement of the reference rule
+    (walk_ref.edge_class_positions) on every edge; the 32-B records carry the edge-inline entry,
+    the byte offset and the counts word. hub_66k: a hub of 66,000 neighbours (int32 lists);
+    rmat12_chunked: the build cut into chunks of 4,096 entries."""
+    from shallow_encoders.graph.csr import CSRGraph as _C
+    if which == 'rmat12_chunked':
+        monkeypatch.setattr(_C, 'N2V_CHUNK_ENTRIES', 4096)
+    if which == 'hub_66k':
+        csr = _hub_graph(n_leaves=66_000, seed=2)
+    elif which == 'karate':
         csr = _csr(golden('walks_karate_node2vec_p1_q0.5.npz'))
-    elif which == 'rmat12':
+    elif which.startswith('rmat12'):
         csr = _csr(golden('walks_rmat12_node2vec_p0.25_q4.npz'))
     elif which == 'self_loops':
         csr = _self_loop_graph()
     else:
         csr = _self_looped_leaves_graph()
     d = csr.device_tensors(hip_device, need_n2v_index=True)
+    if which == 'rmat12_chunked':
+        assert d['n2v_index_info']['chunks'] > 4
     assert d['n2v_rec'] is not None
     E = csr.nnz
     rec = d['n2v_rec'][:E].cpu().numpy()
-    off_ref, pos_ref, pt_ref = walk_ref.edge_class_positions(
-        walk_ref.CSR(csr.row_ptr, csr.host_col(), None))
+    positions = (walk_ref.edge_class_positions_fast if which == 'hub_66k'
+                 else walk_ref.edge_class_positions)
+    off_ref, pos_ref, pt_ref = positions(walk_ref.CSR(csr.row_ptr, csr.host_col(), None))
     col = csr.host_col()
     rp = np.asarray(csr.row_ptr, dtype=np.int64)
     np.testing.assert_array_equal(rec[:, 0], col)
     np.testing.assert_array_equal(rec[:, 1], rp[col + 1] - rp[col])
     np.testing.assert_array_equal(rec[:, 2].view(np.uint32).astype(np.int64)
                                   | (rec[:, 3].astype(np.int64) << 32), rp[col])
-    off = rec[:, 4].view(np.uint32).astype(np.int64) | (rec[:, 5].astype(np.int64) << 32)
-    np.testing.assert_array_equal(off, off_ref[:-1])
+    boff = rec[:, 4].view(np.uint32).astype(np.int64) | (rec[:, 5].astype(np.int64) << 32)
+    cnt = np.diff(off_ref)
+    wide = (rp[col + 1] - rp[col]) > 65536
+    width = np.where(wide, 4, 2)
+    boff_ref = np.concatenate([[0], np.cumsum((cnt * width + 3) // 4 * 4)])
+    np.testing.assert_array_equal(boff, boff_ref[:-1])
     cn = walk_ref.edge_class_counts(walk_ref.CSR(csr.row_ptr, col, None))
     np.testing.assert_array_equal(rec[:, 6].view(np.uint32), cn)
     np.testing.assert_array_equal(rec[:, 7], pt_ref)
     assert d['n2v_index_info']['entries'] == len(pos_ref)
-    np.testing.assert_array_equal(d['n2v_pos'][:len(pos_ref)].cpu().numpy(), pos_ref)
+    assert d['n2v_index_info']['bytes'] == boff_ref[-1] + 32 * E
+    if which == 'hub_66k':
+        assert wide.sum() == 66_000 and cnt[wide].sum() > 0
+    got = _decode_n2v_pos(d['n2v_pos'].cpu().numpy(), boff, cnt, wide)
+    np.testing.assert_array_equal(got, pos_ref)
 
 
 def _boundary_uniforms(csr, starts, L, p, q, rng):

@@ -296,6 +296,17 @@ def test_edge_class_counts_follow_the_reference_weight_rule(name):
 
 @pytest.mark.parametrize('name', ['walks_karate_node2vec_p1_q0.5.npz',
                                   'walks_rmat12_node2vec_p0.25_q4.npz'])
+def test_edge_class_positions_fast_equals_direct(name):
+    """The hub-graph restatement (list intersection) equals the direct scan on undirected
+    graphs."""
+    f = golden(name)
+    g = walk_ref.CSR(f['row_ptr'], f['col'], None)
+    for a, b in zip(walk_ref.edge_class_positions(g), walk_ref.edge_class_positions_fast(g)):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('name', ['walks_karate_node2vec_p1_q0.5.npz',
+                                  'walks_rmat12_node2vec_p0.25_q4.npz'])
 def test_edge_class_positions_follow_the_reference_weight_rule(name):
     """oracle.walk_ref.edge_class_positions (what dw_n2v_edge_index_build stores: t's position
     in N(v) and the ascending positions of the 1/q neighbours) reads, for every directed edge
