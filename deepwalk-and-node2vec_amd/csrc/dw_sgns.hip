@@ -2548,7 +2548,8 @@ __global__ void __launch_bounds__(256)
     k_touch_claim(const int32_t *__restrict__ walks, int64_t n_centres, int32_t L, int32_t R,
                   int64_t V, int32_t *__restrict__ claim, int32_t step_arg,
                   const dw_step_scalars *__restrict__ dyn, int32_t delta,
-                  uint32_t *__restrict__ touched, unsigned long long *__restrict__ n_touched) {
+                  uint32_t *__restrict__ touched, unsigned long long *__restrict__ n_touched,
+                  uint32_t *__restrict__ fresh, unsigned long long *__restrict__ n_fresh) {
     const int32_t step = dw::eff_step(dyn, delta, step_arg);
     const int lane = threadIdx.x & (WAVE - 1);
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -2556,13 +2557,17 @@ __global__ void __launch_bounds__(256)
     for (int64_t base = ((int64_t)blockIdx.x * 4 + threadIdx.x / WAVE) * WAVE; base < n_centres;
          base += (int64_t)gridDim.x * 4 * WAVE) {
         const int64_t b = base + lane;
-        bool mine = false;
+        bool mine = false, cold = false;
         int32_t node = 0;
         if (b < n_centres) {
             const int64_t w = b / per;
             node = walks[w * L + R + (b - w * per)];
             // (an out-of-range id is reported by the SGNS pass)
-            if (node >= 0 && node < V) mine = atomicMax(claim + node, step) < step;
+            if (node >= 0 && node < V) {
+                const int32_t old = atomicMax(claim + node, step);
+                mine = old < step;
+                cold = mine && old < step - 1;   // not a centre of step - 1
+            }
         }
         const uint64_t mask = __ballot(mine);
         if (mask == 0) continue;
@@ -2572,6 +2577,15 @@ __global__ void __launch_bounds__(256)
                   static_cast<uint32_t>(at >> 32))) << 32) |
              __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(at));
         if (mine) touched[at + __popcll(mask & lt)] = static_cast<uint32_t>(node);
+        if (!fresh) continue;
+        const uint64_t cmask = __ballot(cold);
+        if (cmask == 0) continue;
+        unsigned long long ct = 0;
+        if (lane == 0) ct = atomicAdd(n_fresh, static_cast<unsigned long long>(__popcll(cmask)));
+        ct = (static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
+                  static_cast<uint32_t>(ct >> 32))) << 32) |
+             __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ct));
+        if (cold) fresh[ct + __popcll(cmask & lt)] = static_cast<uint32_t>(node);
     }
 }
 
@@ -3055,18 +3069,19 @@ int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_le
 int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                               int32_t context_radius, int64_t vocab_size, int32_t *claim,
                               int32_t step, uint32_t *touched, int64_t *n_touched,
-                              void *stream) {
+                              uint32_t *fresh, int64_t *n_fresh, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    vocab_size >= 1 && step >= 1,
                "dw_sgns_owner_touch_claim: bad sizes");
-    DW_REQUIRE(claim && touched && n_touched && (walks || n_walks == 0),
+    DW_REQUIRE(claim && touched && n_touched && (walks || n_walks == 0) && (!fresh || n_fresh),
                "dw_sgns_owner_touch_claim: null pointer");
     const hipStream_t st = dw::as_stream(stream);
     const dw_step_scalars *dyn = nullptr;
     int32_t delta = 0;
     const int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_sgns_owner_touch_claim");
     if (rc != DW_OK) return rc;
-    if (hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess) {
+    if (hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess ||
+        (fresh && hipMemsetAsync(n_fresh, 0, sizeof(int64_t), st) != hipSuccess)) {
         dw::set_error("dw_sgns_owner_touch_claim: counter reset failed");
         return DW_E_HIP;
     }
@@ -3076,7 +3091,8 @@ int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t wal
     if (blocks > grid_cap(8)) blocks = grid_cap(8);
     hipLaunchKernelGGL(k_touch_claim, dim3((unsigned)blocks), dim3(256), 0, st, walks, n_centres,
                        walk_length, context_radius, vocab_size, claim, step, dyn, delta, touched,
-                       reinterpret_cast<unsigned long long *>(n_touched));
+                       reinterpret_cast<unsigned long long *>(n_touched), fresh,
+                       reinterpret_cast<unsigned long long *>(n_fresh));
     DW_LAUNCH_CHECK("dw_sgns_owner_touch_claim");
     return DW_OK;
 }

@@ -25,7 +25,8 @@ import torch
 from shallow_encoders import _native
 from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables, adam_scalars,
                                                 hist_header, hist_row,
-                                                owner_lazy_step, replicated_step)
+                                                owner_lazy_step, owner_lazy_steps,
+                                                replicated_step)
 
 _STEP_DTYPE = np.dtype([('walk_id0', '<u8'), ('noise_offset', '<u8'), ('step', '<i8'),
                         ('adam', '<f4', (8,))])   # == dw_step_scalars (56 bytes)
@@ -247,6 +248,8 @@ class GraphedOwnerStep:
                           check=False, status=torch.zeros(1, dtype=torch.int32, device=dev))
         walker._next_walk_id = next_wid
         torch.cuda.synchronize(dev)
+        if tables.pipeline_ok(R, K):   # owner_lazy_steps' second buffers, outside the capture
+            tables._pipe_alloc(self.B, L, R, K)
         steps0, lr0 = tables.step_count, len(tables._lr_hist)
         self.graph = torch.cuda.CUDAGraph()
         try:
@@ -273,13 +276,16 @@ class GraphedOwnerStep:
         _native.call('dw_step_scalars_bind', self._step_blk(0))
         self.walker.walk_batch(self.starts, walk_id0=0, out=self.walks, check=False,
                                status=self.status)
-        for k in range(self.unroll):
-            # the step numbers the lazy kernels get are relative to block k's (begin_step, inside
-            # owner_lazy_step, makes the host's count step_count + 1)
-            _native.call('dw_step_scalars_bind_at', self._step_blk(k), t.step_count + 1)
-            owner_lazy_step(t, self.walks[k * B:(k + 1) * B], self.R, self.K, seed=self.seed,
-                            noise_offset=0, grad_scale=self.grad_scale, loss_acc=self.loss_acc,
-                            status=self.status)
+        # the step numbers the lazy kernels get are relative to block k's (begin_step, inside
+        # the steps, makes the host's count steps0 + k + 1 at step k)
+        steps0 = t.step_count
+
+        def bind(k):
+            _native.call('dw_step_scalars_bind_at', self._step_blk(k), steps0 + k + 1)
+        owner_lazy_steps(t, [self.walks[k * B:(k + 1) * B] for k in range(self.unroll)], self.R,
+                         self.K, seed=self.seed, noise_offsets=[0] * self.unroll,
+                         grad_scale=self.grad_scale, loss_acc=self.loss_acc, status=self.status,
+                         bind=bind)
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host

@@ -48,10 +48,13 @@ def _use_records(scatter: str, n_ctx: int, neg_samples: int, vocab_size: int) ->
 
 
 def workspace_for(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int,
-                  device: torch.device, local_rows: Optional[int] = None) -> torch.Tensor:
+                  device: torch.device, local_rows: Optional[int] = None,
+                  slot: int = 0) -> torch.Tensor:
     """Device workspace of the atomic-free (records) output-table path, cached per device and
     grown on demand (allocated outside any timed region after the first call). ``local_rows``:
-    sized for dw_sgns_owner_pass1 (records keyed by the rank's local out-table rows)."""
+    sized for dw_sgns_owner_pass1 (records keyed by the rank's local out-table rows). ``slot``:
+    a second workspace (1) for the pipelined step (owner_lazy_steps: the next batch's records
+    are placed while this one's are read)."""
     import ctypes
     nbytes = ctypes.c_size_t(0)
     if local_rows is None:
@@ -60,11 +63,12 @@ def workspace_for(n_centres: int, n_ctx: int, neg_samples: int, vocab_size: int,
     else:
         _native.call('dw_sgns_owner_workspace_bytes', int(n_centres), int(n_ctx),
                      int(neg_samples), int(vocab_size), int(local_rows), ctypes.byref(nbytes))
-    ws = _WORKSPACES.get(device)
+    key = device if slot == 0 else (device, int(slot))
+    ws = _WORKSPACES.get(key)
     if ws is None or ws.numel() < nbytes.value:
-        _WORKSPACES.pop(device, None)
+        _WORKSPACES.pop(key, None)
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=device)
-        _WORKSPACES[device] = ws
+        _WORKSPACES[key] = ws
     return ws
 
 
@@ -324,7 +328,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
                      status: Optional[torch.Tensor] = None,
                      order_ready: bool = False, placed: bool = False,
                      coefficients_in: bool = False,
-                     walk_order: bool = False) -> Optional[torch.Tensor]:
+                     walk_order: bool = False,
+                     workspace_slot: int = 0) -> Optional[torch.Tensor]:
     """Pass 1 of the owner-computes step (dw_sgns_owner_pass1, N > 1): over the WHOLE global
     batch ``walks`` (int32 [n, L]), only the output slots whose row o has o % n_owners == owner;
     ``w_out_local`` holds those rows (local row o // n_owners). ``g_in`` ([>= V, d]) receives the
@@ -336,7 +341,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
     (OwnerLazyTables.out_rows_step) already formed the coefficients and left the rows it stepped
     pending, their pre-step values in ``w_out_local`` — only the centre gradient is formed (no
     loss sums: returns None); ``walk_order`` (with it): the centres in walk order, no node order
-    built or read."""
+    built or read. ``workspace_slot``: the workspace the batch's records were placed in
+    (workspace_for)."""
     dev = w_in.device
     d = w_in.shape[1]
     local_rows = w_out_local.shape[0]
@@ -366,7 +372,8 @@ def sgns_owner_pass1(w_in: torch.Tensor, w_out_local: torch.Tensor, g_in: torch.
         loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows)
+    ws = workspace_for(n_centres, 2 * R, K, vocab_size, dev, local_rows=local_rows,
+                       slot=workspace_slot)
     with torch.cuda.device(dev):
         _native.call('dw_sgns_owner_pass1', _native.ptr(walks), n, L, R, K, int(vocab_size), d,
                      int(owner), int(n_owners), local_rows,

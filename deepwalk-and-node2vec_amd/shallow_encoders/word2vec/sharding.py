@@ -958,6 +958,10 @@ class OwnerLazyTables(OwnerTables):
                          if self.lazy_out else None)
         self._pend_dirty = False   # some out row may be pending
         self._rows_step = False    # this step goes rows-major (set by catch_up_out)
+        # the pipelined steps (owner_lazy_steps): the odd steps' row counts, touched lists and
+        # catch-up lists (allocated by _pipe_alloc, outside any capture)
+        self._count_out2 = None
+        self._pipe = None
 
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
         """The rows-major step applies: placed records, d one of the widths its kernels are
@@ -967,6 +971,53 @@ class OwnerLazyTables(OwnerTables):
         return (self.rows_major and self.place and self.d in ROWS_MAJOR_DIMS
                 and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64
                 and getattr(self, '_exact', None) is None)
+
+    def pipeline_ok(self, context_radius: int, neg_samples: int) -> bool:
+        """owner_lazy_steps pipelines the steps: one rank, the HIP lazy Adam of both tables and
+        the rows-major out step."""
+        return (self.lazy_out and not self.multi and self._hip()
+                and self.rows_major_ok(context_radius, neg_samples))
+
+    def _pipe_alloc(self, n_walks: int, walk_length: int, context_radius: int,
+                    neg_samples: int) -> None:
+        """The pipelined steps' second buffers (before a capture: a graph must not allocate)."""
+        from shallow_encoders.word2vec.sgns import workspace_for
+        n = max(n_walks * (walk_length - 2 * int(context_radius)), 1)
+        for slot in (0, 1):
+            workspace_for(n, 2 * int(context_radius), int(neg_samples), self.V, self.device,
+                          local_rows=self.S, slot=slot)
+        if self._count_out2 is None:
+            self._count_out2 = torch.zeros_like(self._count_out)
+        if self._claim_in is None:
+            self._claim_in = torch.zeros(self.V_pad, dtype=torch.int32, device=self.device)
+        p = self._pipe
+        if p is None or p['touched'][0].numel() < n:
+            i32 = dict(dtype=torch.int32, device=self.device)
+            i64 = dict(dtype=torch.int64, device=self.device)
+            self._pipe = {'touched': [torch.empty(n, **i32) for _ in range(2)],
+                          'n_touched': [torch.zeros(1, **i64) for _ in range(2)],
+                          'fresh': [torch.empty(n, **i32) for _ in range(2)],
+                          'n_fresh': [torch.zeros(1, **i64) for _ in range(2)],
+                          'side_in': torch.cuda.Stream(self.device)}
+        if self._touched is None or self._touched.numel() < n:
+            self._touched = torch.empty(n, dtype=torch.int32, device=self.device)
+
+    def _touch_ahead(self, walks: torch.Tensor, context_radius: int, step: int,
+                     slot: int) -> None:
+        """The pipelined step ``step``'s in rows, while step - 1 may still run: its distinct
+        centres U (touched list ``slot``) and, of them, those that were not centres of step - 1
+        (the fresh list) replayed up to step - 1 — nothing of step - 1 writes those rows."""
+        p = self._pipe
+        with torch.cuda.device(self.device):
+            _native.call('dw_sgns_owner_touch_claim', _native.ptr(walks), walks.shape[0],
+                         walks.shape[1], int(context_radius), self.V,
+                         _native.ptr(self._claim_in), int(step),
+                         _native.ptr(p['touched'][slot]), _native.ptr(p['n_touched'][slot]),
+                         _native.ptr(p['fresh'][slot]), _native.ptr(p['n_fresh'][slot]),
+                         _native.stream(self.device))
+        n_max = walks.shape[0] * (walks.shape[1] - 2 * int(context_radius))
+        hip_rows_adam(self.params_in[0], self.m_in, self.v_in, self.last_in, p['fresh'][slot],
+                      p['n_fresh'][slot], n_max, None, self._hist, int(step) - 1)
 
     def out_flags(self) -> int:
         """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
@@ -980,10 +1031,13 @@ class OwnerLazyTables(OwnerTables):
 
     def catch_up_out(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                      seed: int, noise_offset: int, status: torch.Tensor,
-                     noise: Optional[torch.Tensor] = None, step: Optional[int] = None) -> None:
+                     noise: Optional[torch.Tensor] = None, step: Optional[int] = None,
+                     slot: int = 0) -> None:
         """lazy_out, before pass 1 of the batch ``walks``: the owned out rows its slots
         reference replay their deferred steps up to step - 1 (dw_sgns_owner_out_catch_up).
-        ``step``: the Adam step of that batch (default: the current one)."""
+        ``step``: the Adam step of that batch (default: the current one). ``slot``: the
+        workspace and row counts the records are placed with (owner_lazy_steps: 0 / 1 by the
+        step's parity)."""
         if not self.lazy_out:
             return
         from shallow_encoders.word2vec.sgns import workspace_for
@@ -994,7 +1048,9 @@ class OwnerLazyTables(OwnerTables):
         cap = max(1, min(self.S, slots))
         if self._out_rows is None or self._out_rows.numel() < cap:
             self._out_rows = torch.empty(cap, dtype=torch.int32, device=self.device)
-        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
+        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S,
+                           slot=slot)
+        counts = self._count_out if slot == 0 else self._count_out2
         self._rows_step = self.rows_major_ok(R, K)
         if not self._rows_step and self._pend_dirty:
             self._flush_out()   # the other form reads the rows as current: settle them first
@@ -1005,7 +1061,7 @@ class OwnerLazyTables(OwnerTables):
                          self.world, self.S, _native.ptr(noise), seed & 0xFFFFFFFFFFFFFFFF,
                          int(noise_offset), _native.ptr(self.w_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._claim_out), _native.ptr(self._count_out),
+                         _native.ptr(self._claim_out), _native.ptr(counts),
                          _native.ptr(self._out_rows),
                          _native.ptr(self._n_out), _native.ptr(self._hist), step,
                          flags, _native.ptr(status), _native.ptr(ws), ws.numel(),
@@ -1013,7 +1069,8 @@ class OwnerLazyTables(OwnerTables):
 
     def out_rows_step(self, walks: torch.Tensor, context_radius: int, neg_samples: int,
                       seed: int, noise_offset: int, grad_scale: float, loss_acc: torch.Tensor,
-                      status: torch.Tensor, noise: Optional[torch.Tensor] = None) -> None:
+                      status: torch.Tensor, noise: Optional[torch.Tensor] = None,
+                      slot: int = 0) -> None:
         """The rows-major out step of the batch ``walks`` (after catch_up_out chose it):
         dw_sgns_owner_out_rows — each touched out row replayed, its records' coefficients and
         loss terms, its gradient and the moments of its Adam step; the rows are left pending
@@ -1022,7 +1079,9 @@ class OwnerLazyTables(OwnerTables):
         from shallow_encoders.word2vec.sgns import workspace_for
         n, L = walks.shape
         R, K = int(context_radius), int(neg_samples)
-        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S)
+        ws = workspace_for(n * (L - 2 * R), 2 * R, K, self.V, self.device, local_rows=self.S,
+                           slot=slot)
+        counts = self._count_out if slot == 0 else self._count_out2
         self._pend_dirty = True
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_out_rows', _native.ptr(walks), n, L, R, K, self.V,
@@ -1031,7 +1090,7 @@ class OwnerLazyTables(OwnerTables):
                          _native.ptr(self.w_in_raw), _native.ptr(self.w_out),
                          _native.ptr(self.g_out), _native.ptr(self.m_out),
                          _native.ptr(self.v_out), _native.ptr(self.last_out),
-                         _native.ptr(self._count_out), _native.ptr(self.pend_out),
+                         _native.ptr(counts), _native.ptr(self.pend_out),
                          _native.ptr(self._hist), self.step_count,
                          _native.ptr(loss_acc), _native.ptr(status), _native.ptr(ws),
                          ws.numel(), _native.stream(self.device))
@@ -1132,8 +1191,8 @@ class OwnerLazyTables(OwnerTables):
                 _native.call('dw_sgns_owner_touch_claim', _native.ptr(walks), walks.shape[0],
                              walks.shape[1], int(context_radius), self.V,
                              _native.ptr(self._claim_in), self.step_count,
-                             _native.ptr(self._touched), _native.ptr(self._n_touched),
-                             _native.stream(self.device))
+                             _native.ptr(self._touched), _native.ptr(self._n_touched), None,
+                             None, _native.stream(self.device))
         else:
             sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
                                touched=self._touched, n_touched=self._n_touched)
@@ -1293,6 +1352,97 @@ class OwnerLazyTables(OwnerTables):
 
     def sync(self) -> None:
         """Nothing is pending between steps (update_touched waits for the all-reduce)."""
+
+
+def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
+                     neg_samples: int, *, seed: int, noise_offsets, grad_scale: float,
+                     loss_acc: torch.Tensor, status: torch.Tensor, bind=None) -> int:
+    """Consecutive owner_lazy_step calls over ``batches`` (int32 [n, L] walks each, known up
+    front: GraphedOwnerStep's unrolled steps), pipelined on one rank with the rows-major out
+    step (OwnerLazyTables.pipeline_ok; otherwise the plain sequence). Step k + 1's
+    preparation — its out records' claim and placement (dw_sgns_owner_out_catch_up, flags 4),
+    its centres' touch claim and the catch-up of the centres step k does not touch — runs on two
+    side streams while step k's out rows, centre pass and in-table update run, from the moment
+    step k - 1 has finished (the buffers alternate by step parity: workspace slot, row counts,
+    touched list). Only the out rows' step, the centre pass and the in rows' update stay on the
+    step's critical path. The results equal the sequential steps': each kernel reads and writes
+    what it would there (the catch-up of step k + 1 skips the centres of step k, which step k
+    updates itself). ``bind(k)``: called before enqueueing anything of step k (graph capture:
+    binds step k's dw_step_scalars block). Returns the record count of the steps."""
+    R, K = int(context_radius), int(neg_samples)
+    batches = list(batches)
+    offs = list(noise_offsets)
+    n_steps = len(batches)
+    if n_steps == 0:
+        return 0
+    if not tables.pipeline_ok(R, K) or any(b.shape != batches[0].shape for b in batches):
+        n = 0
+        for k, w in enumerate(batches):
+            if bind is not None:
+                bind(k)
+            n += owner_lazy_step(tables, w, R, K, seed=seed, noise_offset=offs[k],
+                                 grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+        return n
+    from shallow_encoders.word2vec.sgns import sgns_owner_pass1
+    t = tables
+    dev = t.device
+    nw, L = batches[0].shape
+    t._pipe_alloc(nw, L, R, K)
+    s0 = t.step_count + 1
+    # every Adam-scalar row the steps read, written before the first side launch (begin_step
+    # then copies nothing while a side stream reads the history)
+    t.reserve_history(s0 + n_steps - 1)
+    if t._pend_dirty and not t._rows_step:
+        t._flush_out()
+    t._rows_step = True
+    main = torch.cuda.current_stream(dev)
+    side_out, side_in = t._side, t._pipe['side_in']
+
+    def ahead(k: int):
+        """Step k's preparation on the side streams, after everything enqueued so far."""
+        fork = torch.cuda.Event()
+        fork.record(main)
+        if bind is not None:
+            bind(k)
+        slot = k & 1
+        with torch.cuda.stream(side_out):
+            side_out.wait_event(fork)
+            t.catch_up_out(batches[k], R, K, seed, offs[k], status, step=s0 + k, slot=slot)
+            ro = torch.cuda.Event()
+            ro.record(side_out)
+        with torch.cuda.stream(side_in):
+            side_in.wait_event(fork)
+            t._touch_ahead(batches[k], R, s0 + k, slot)
+            ri = torch.cuda.Event()
+            ri.record(side_in)
+        return ro, ri
+
+    ready = ahead(0)
+    slots = batches[0].shape[0] * (L - 2 * R) * 2 * R * (1 + K)
+    p = t._pipe
+    for k in range(n_steps):
+        slot = k & 1
+        if bind is not None:
+            bind(k)
+        t.begin_step()
+        for ev in ready:
+            main.wait_event(ev)
+        if k + 1 < n_steps:
+            ready = ahead(k + 1)
+            if bind is not None:
+                bind(k)
+        w = batches[k]
+        t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
+        sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
+                         owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
+                         noise_offset=offs[k], grad_scale=grad_scale, status=status,
+                         order_ready=True, placed=True, coefficients_in=True, walk_order=True,
+                         workspace_slot=slot)
+        # the step's in rows with their gradient rows (dw_adam_rows grad_by_row clears them)
+        hip_rows_adam(t.params_in[0], t.m_in, t.v_in, t.last_in, p['touched'][slot],
+                      p['n_touched'][slot], nw * (L - 2 * R), t.grads_in, t._hist,
+                      t.step_count, grad_by_row=True)
+    return slots * n_steps
 
 
 def owner_lazy_step(tables: OwnerLazyTables, walks: torch.Tensor, context_radius: int,

@@ -591,12 +591,15 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
  * in-table update on one rank (dw_sgns_owner_prepare gives them sorted, the order every rank
  * agrees on when N > 1): claim int32 [vocab_size] (zero-initialised, kept across steps) gets
  * claim[node] = step and the first claimer lists the node in touched (uint32 [>= B']);
- * n_touched (int64, device) their count. Reads step from a bound dw_step_scalars block
- * (relative form). Replaces nothing in the reference (its optimizer steps every row). */
+ * n_touched (int64, device) their count. fresh / n_fresh (NULL = not wanted): the listed
+ * nodes whose claim was below step - 1 — not centres of the step before, so nothing of that
+ * step writes their rows (the pipelined step catches them up while step - 1 still runs). Reads
+ * step from a bound dw_step_scalars block (relative form). Replaces nothing in the reference
+ * (its optimizer steps every row). */
 int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                               int32_t context_radius, int64_t vocab_size, int32_t *claim,
                               int32_t step, uint32_t *touched, int64_t *n_touched,
-                              void *stream);
+                              uint32_t *fresh, int64_t *n_fresh, void *stream);
 
 /* The rows-major lazy out step (OwnerLazyTables, one device; after dw_sgns_owner_out_catch_up
  * with flags 1 | 4 on the same batch and workspace, before dw_sgns_owner_pass1 with order_ready

@@ -89,7 +89,7 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
         assert_no_row_drift(got, exp)
 
 
-@pytest.mark.parametrize('lazy_out,unroll', [(True, 1), (True, 4), (False, 3)])
+@pytest.mark.parametrize('lazy_out,unroll', [(True, 1), (True, 4), (False, 3), (True, 12)])
 def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
     """The one-GPU lazy owner step (bench.py's path for the reference's 64-walk batch on a large
     graph) replayed as a HIP graph (GraphedOwnerStep: the lazy kernels' step numbers bound
@@ -145,6 +145,58 @@ def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
     # between the two runs, and 12 Adam steps can amplify an ulp of a near-zero gradient entry:
     # a run measured 1.4e-4 on one entry against lr/100; lr/10 there (the atomic scatter's bar)
     for got, exp in ((wi_g, wi_e), (wo_g, wo_e)):
+        assert_params_close(got, exp, LR, max_abs=LR / 10)
+        assert_no_row_drift(got, exp)
+
+
+@pytest.mark.parametrize('n_steps', [1, 2, 7])
+def test_pipelined_owner_steps_equal_sequential(hip_device, n_steps):
+    """owner_lazy_steps (step k + 1's claims, touch claim and catch-up on side streams while
+    step k runs) equals the sequential owner_lazy_step calls on the same batches: the small
+    graph's batches share most centre rows from step to step, so the catch-up of step k + 1 must
+    skip exactly the centres step k updates. Losses to float64-atomic order, tables to fp32
+    atomic-order noise; and the pipelined run leaves the tables ready for an eager step."""
+    from shallow_encoders.word2vec.sharding import (OwnerLazyTables, owner_lazy_step,
+                                                    owner_lazy_steps)
+    dev = hip_device
+    csr, walker, epoch = _setup(dev)
+    V = csr.vocab_size
+    grad_scale = 1.0 / (B * (L - 2 * R) * 2 * R)
+    warm = 2
+    batches = []
+    for s in range(warm + n_steps + 1):
+        g0 = s * B
+        st = epoch[torch.arange(g0, g0 + B, device=dev) % epoch.numel()]
+        batches.append((walker.walk_batch(st, walk_id0=g0, check=False), g0 * (L - 2 * R)))
+    runs = []
+    for mode in ('sequential', 'pipelined'):
+        t = OwnerLazyTables(V, D, dev, lr=LR, init_seed=0, emulate_world=1, lazy_out=True)
+        assert t.pipeline_ok(R, K)
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def one(k):
+            owner_lazy_step(t, batches[k][0], R, K, seed=SEED, noise_offset=batches[k][1],
+                            grad_scale=grad_scale, loss_acc=acc, status=status)
+        for k in range(warm):
+            one(k)
+        run = range(warm, warm + n_steps)
+        if mode == 'sequential':
+            for k in run:
+                one(k)
+        else:
+            owner_lazy_steps(t, [batches[k][0] for k in run], R, K, seed=SEED,
+                             noise_offsets=[batches[k][1] for k in run],
+                             grad_scale=grad_scale, loss_acc=acc, status=status)
+        one(warm + n_steps)     # an eager step after the run
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0
+        assert t.step_count == warm + n_steps + 1
+        t._flush_out()
+        runs.append((t.w_in.cpu().numpy(), t.w_out[:V].cpu().numpy(), acc.cpu().numpy()))
+    (wi_s, wo_s, acc_s), (wi_p, wo_p, acc_p) = runs
+    np.testing.assert_allclose(acc_p, acc_s, rtol=1e-8)
+    for got, exp in ((wi_p, wi_s), (wo_p, wo_s)):
         assert_params_close(got, exp, LR, max_abs=LR / 10)
         assert_no_row_drift(got, exp)
 
