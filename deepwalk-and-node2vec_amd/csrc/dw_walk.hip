@@ -1125,22 +1125,13 @@ __device__ __forceinline__ uint32_t ceil_log2(int64_t x) {
 // takes n2v_pick_counted, so the full classification (node2vec_pick_exact) and its class-mask
 // cache are not compiled in; CH then only sizes the serial fallback's weight cache (hub rows
 // past it recompute their weights in lane 0) and, with the N(prev) stage, the positions buffer.
-// A walk the lane-per-walk position walker (k_walk_replay_n2v_pos) handed over at step s (a
-// pick its margin could not decide): the wave walker resumes it from (v, prev, e_in).
-struct N2VDefer {
-    int64_t wk, e_in;
-    int32_t s, v, prev, pad;
-};
-
 template <int CH, int NCAP, bool COUNTS>
 __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
                                                  const int32_t *__restrict__ starts,
                                                  int64_t n_walks, int32_t L,
                                                  const double *__restrict__ uniforms,
                                                  int32_t *__restrict__ out, int32_t *status,
-                                                 int fast, N2VIndex ix,
-                                                 const N2VDefer *__restrict__ resume,
-                                                 const uint32_t *__restrict__ n_resume) {
+                                                 int fast, N2VIndex ix) {
     // per wave: CH doubles (the serial replay's weights / the exact picks' ballots) followed by
     // the NCAP-entry N(prev) stage; the ballots take both halves when nothing is staged
     __shared__ uint64_t s_lds[REPLAY_WAVES][CH + NCAP / 2];
@@ -1152,25 +1143,12 @@ __device__ __forceinline__ void walk_replay_body(ReplayCtx c, int64_t n_rows,
     const int64_t n_waves = (int64_t)gridDim.x * REPLAY_WAVES;
     const bool counted = ix.counters != nullptr;
     uint32_t probes = 0, loads = 0, steps = 0;   // counted launches only
-    const int64_t n_items = resume ? static_cast<int64_t>(*n_resume) : n_walks;
-
-    for (int64_t it = (int64_t)blockIdx.x * REPLAY_WAVES + wv; it < n_items; it += n_waves) {
-        int64_t wk = it;
-        int32_t v, prev = -1;
+    for (int64_t wk = (int64_t)blockIdx.x * REPLAY_WAVES + wv; wk < n_walks; wk += n_waves) {
+        int32_t v = starts[wk], prev = -1;
         int64_t e_in = -1;   // the edge prev -> v (its class counts: ix.edge_cn)
         int32_t s = 1;
-        if (resume) {        // a handed-over walk: steps < s are written
-            const N2VDefer r = resume[it];
-            wk = r.wk;
-            v = r.v;
-            prev = r.prev;
-            e_in = r.e_in;
-            s = r.s;
-        } else {
-            v = starts[wk];
-        }
         int32_t *o = out + wk * (int64_t)L;
-        if (!resume && lane == 0) o[0] = v;
+        if (lane == 0) o[0] = v;
         const double *u = uniforms + wk * (int64_t)(L - 1);
         for (; s < L; ++s) {
             if (v < 0 || (int64_t)v >= n_rows) {
@@ -1365,7 +1343,7 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
                   int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
                   int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
     walk_replay_body<CH, NCAP, false>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
-                                      ix, nullptr, nullptr);
+                                      ix);
 }
 
 // The COUNTS form is latency-bound on each walker's dependent chain and its LDS (4.6 KiB per
@@ -1378,10 +1356,9 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
     __attribute__((amdgpu_waves_per_eu(DW_N2V_CN_WAVES, 8)))
     k_walk_replay_cn(ReplayCtx c, int64_t n_rows, const int32_t *__restrict__ starts,
                      int64_t n_walks, int32_t L, const double *__restrict__ uniforms,
-                     int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix,
-                     const N2VDefer *__restrict__ resume, const uint32_t *__restrict__ n_resume) {
+                     int32_t *__restrict__ out, int32_t *status, int fast, N2VIndex ix) {
     walk_replay_body<CH, NCAP, true>(c, n_rows, starts, n_walks, L, uniforms, out, status, fast,
-                                     ix, resume, n_resume);
+                                     ix);
 }
 
 // ---- node2vec over the position index: one lane per walker ----------------------------------
@@ -1395,6 +1372,116 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // EXACT = false (the Philox walker, k_walk_node2vec_positions): no margin tests — the pick is
 // the first i at which the fp64 D_i turns positive, an exact draw from W_i / T up to the fp64
 // rounding of D (relative 2^-50), the same expressions as the oracle's (oracle/philox.py).
+// ---- the exact serial pick, run by run ---------------------------------------------------
+// Where the margin cannot decide, the pick is the reference's own arithmetic: sum(w) left to
+// right, normalized = w / s, accumulate, bisect_right (random_walk_generator.py:109-111,
+// random.choices). Over N(v) the weights are 1 except at t's position (1/p) and the C common
+// positions (1/q), so each sequential fp64 sum is a few runs of equal terms, and a run of m equal
+// terms y advances in one step per binade of the running sum S: within [B, 2B) (ulp u) every
+// addition rounds alike, fl(S + y) = S + D u with D = floor(y / u) (+1 when the remainder
+// exceeds u / 2; on a tie the even neighbour, constant once S / u is even). The pick then costs
+// O(C + log n) instead of O(n) dependent adds with an adjacency test each (a 393K-neighbour
+// hub's serial replay took ~0.5 s in one lane). tests/test_serial_runs.py restates ff_run /
+// runs_pass / the pick and checks them bit for bit against the sequential sums and the
+// oracle's choices_index.
+// m additions of y (> 0) to S: returns the first addition (1-based) after which S > x (S left
+// there), or 0 (S after all m).
+__device__ int64_t ff_run(double &S, const double y, const int64_t m, const double x) {
+    int64_t done = 0;
+    while (done < m) {
+        if (S > 0.0 && y < S) {
+            const int e =
+                static_cast<int>((__double_as_longlong(S) >> 52) & 0x7FF) - 1022;   // S in [2^(e-1), 2^e)
+            const double B2 = ldexp(1.0, e);
+            const double u = ldexp(1.0, e - 53);
+            const double qd = floor(y / u);
+            const double r = y - qd * u;                 // exact
+            const int64_t q = static_cast<int64_t>(qd);
+            const int64_t k = static_cast<int64_t>(S / u);
+            const bool tie = r == 0.5 * u;
+            if (!tie || (k & 1) == 0) {
+                const int64_t D = q + ((r > 0.5 * u || (tie && (q & 1))) ? 1 : 0);
+                if (D == 0) return S > x ? done + 1 : 0;   // the rest add nothing
+                const int64_t jmax = static_cast<int64_t>((B2 - S) / u) / D;
+                if (jmax > 0) {
+                    const int64_t j = jmax < m - done ? jmax : m - done;
+                    const double Sj = S + static_cast<double>(j * D) * u;
+                    if (x < B2 && x < Sj) {   // the crossing is inside the chunk
+                        const int64_t js =
+                            x < S ? 1 : static_cast<int64_t>((x - S) / u) / D + 1;
+                        S = S + static_cast<double>(js * D) * u;
+                        return done + js;
+                    }
+                    S = Sj;
+                    done += j;
+                    continue;
+                }
+            }
+        }
+        const double t = S + y;   // one addition as it is
+        ++done;
+        if (t == S) return t > x ? done : 0;
+        S = t;
+        if (S > x) return done;
+    }
+    return 0;
+}
+
+// The fp64 left-to-right sum of the n terms (`one`, vp at pt, vq at the ascending P[0..C)) in
+// S; returns the first index < hi whose partial sum exceeds x, or -1.
+__device__ int64_t runs_pass(PosList P, int64_t C, int64_t pt, double vp, double vq, int64_t n,
+                             int64_t hi, double one, double x, double &S, uint32_t &loads) {
+    S = 0.0;
+    int64_t i = 0, j = 0;
+    bool p_left = pt >= 0;
+    int64_t pj = C > 0 ? P[0] : n;
+    if (C > 0) loads += P.wide ? 2u : 1u;
+    while (true) {
+        int64_t pos;
+        double val;
+        if (p_left && pt < pj) {
+            pos = pt;
+            val = vp;
+            p_left = false;
+        } else if (j < C) {
+            pos = pj;
+            val = vq;
+            if (++j < C) {
+                pj = P[j];
+                loads += P.wide ? 2u : 1u;
+            } else {
+                pj = n;
+            }
+        } else {
+            pos = n;
+            val = 0.0;
+        }
+        const int64_t end = pos < hi ? pos : hi;
+        if (end > i) {
+            const int64_t k = ff_run(S, one, end - i, x);
+            if (k) return i + k - 1;
+        }
+        if (pos >= hi) return -1;
+        S = S + val;
+        if (S > x) return pos;
+        i = pos + 1;
+    }
+}
+
+// The reference's pick over N(v) (n neighbours; t at pt or -1; the 1/q neighbours at P), by
+// its own fp64 arithmetic: the serial replay the margin tests fall back to.
+__device__ int64_t n2v_pick_serial_runs(PosList P, int64_t C, int64_t pt, int64_t n, double U,
+                                        double ip, double iq, uint32_t &loads) {
+    const double inf = __builtin_huge_val();
+    double s, total, S;
+    runs_pass(P, C, pt, ip, iq, n, n, 1.0, inf, s, loads);            // sum(w)
+    const double n1 = 1.0 / s, np = ip / s, nq = iq / s;              // normalized
+    runs_pass(P, C, pt, np, nq, n, n, n1, inf, total, loads);         // accumulate
+    total = total + 0.0;
+    const int64_t k = runs_pass(P, C, pt, np, nq, n, n - 1, n1, U * total, S, loads);
+    return k < 0 ? n - 1 : k;                                         // bisect_right(.., 0, n-1)
+}
+
 template <bool EXACT = true>
 __device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt, int64_t n,
                                                 double U, double ip, double iq,
@@ -1442,7 +1529,7 @@ __device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt
 // (k_n2v_edge_records): a step is the record of the edge it arrived by (its next row and its
 // index entry in one line), the search of its positions, and nothing else. The uniforms are
 // staged in LDS per tile of steps as in k_walk_replay_uniform_inline. A pick the margin leaves
-// open hands the walk to the wave walker (k_walk_replay_cn over `defer`), which finishes it.
+// open is made by the reference's arithmetic itself, run by run (n2v_pick_serial_runs).
 // 8 staged steps per tile (17 KiB of LDS per block): the walk is latency-bound, so blocks
 // per CU count for more than the uniforms' reload rate
 constexpr int RP_T = 8;
@@ -1452,13 +1539,13 @@ __global__ void __launch_bounds__(256)
                           const uint8_t *__restrict__ pos, int64_t n_rows,
                           const int32_t *__restrict__ starts, int64_t n_walks, int32_t L,
                           const double *__restrict__ uniforms, double ip, double iq,
-                          int32_t *__restrict__ out, int32_t *status, N2VDefer *__restrict__ defer,
-                          uint32_t *__restrict__ n_defer, unsigned long long *counters) {
+                          int32_t *__restrict__ out, int32_t *status,
+                          unsigned long long *counters) {
     __shared__ double tile[256][RP_T + 1];
     const int tid = threadIdx.x;
     const int64_t n_chunks = (n_walks + 255) / 256;
     const int64_t UL = L - 1;
-    uint32_t loads = 0, steps = 0;
+    uint32_t loads = 0, steps = 0, serial = 0;
     for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
         const int64_t w0 = ch * 256;
         const int n_here = (n_walks - w0 < 256) ? static_cast<int>(n_walks - w0) : 256;
@@ -1498,16 +1585,16 @@ __global__ void __launch_bounds__(256)
                     } else {
                         const double U = tile[tid][j];
                         if (COUNT) ++steps;
-                        const int64_t k =
-                            prev < 0 ? uniform_pick_exact(U, n)
-                                     : n2v_pick_pos(PosList{pos + p_off, n > N2V_U16_MAX_DEG},
-                                                    cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n, U,
-                                                    ip, iq, loads);
-                        if (k < 0) {   // the wave walker takes it from here
-                            const uint32_t slot = atomicAdd(n_defer, 1u);
-                            defer[slot] = N2VDefer{wk, e_in, st, v, prev, 0};
-                            ok = false;
-                        } else {
+                        const PosList PL{pos + p_off, n > N2V_U16_MAX_DEG};
+                        const int64_t C = prev < 0 ? 0 : (cw & 0x7FFFFFFFu);
+                        const int64_t ptv = (prev >= 0 && (cw >> 31)) ? pt : -1;
+                        int64_t k = prev < 0 ? uniform_pick_exact(U, n)
+                                             : n2v_pick_pos(PL, C, ptv, n, U, ip, iq, loads);
+                        if (k < 0) {   // the margin cannot decide: the reference's arithmetic
+                            k = n2v_pick_serial_runs(PL, C, ptv, n, U, ip, iq, loads);
+                            if (COUNT) ++serial;
+                        }
+                        {
                             const int64_t e = a + k;
                             const int4 r0 = rec[2 * e], r1 = rec[2 * e + 1];
                             prev = v;
@@ -1538,12 +1625,15 @@ __global__ void __launch_bounds__(256)
             }
         }
     }
-    if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); the positions read
-        unsigned long long v2[2] = {(unsigned long long)loads, (unsigned long long)steps};
-        for (int k = 0; k < 2; ++k)
+    if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); the positions
+                   // read (2-B units); the serial picks
+        unsigned long long v2[3] = {(unsigned long long)loads, (unsigned long long)steps,
+                                    (unsigned long long)serial};
+        for (int k = 0; k < 3; ++k)
             for (int off = WAVE / 2; off > 0; off >>= 1) v2[k] += __shfl_xor(v2[k], off, WAVE);
         if ((tid & (WAVE - 1)) == 0) {
             atomicAdd(counters + 0, v2[0] * 2ull + v2[1] * 44ull);
+            atomicAdd(counters + 1, v2[2]);
             atomicAdd(counters + 2, v2[0]);
             atomicAdd(counters + 3, v2[1]);
         }
@@ -2273,7 +2363,7 @@ int dw_walk_replay_indexed(const int64_t *row_ptr, const int32_t *col, const int
         hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
                            dw::as_stream(stream), c, n_rows, starts, n_walks, walk_length,
-                           uniforms, out, status, 1, ix, nullptr, nullptr);
+                           uniforms, out, status, 1, ix);
     else
         hipLaunchKernelGGL((k_walk_replay<REPLAY_CH_EXACT, REPLAY_NCAP_EXACT>),
                            dim3((unsigned)blocks), dim3(REPLAY_WAVES * WAVE), 0,
@@ -2430,68 +2520,33 @@ int dw_n2v_edge_records(const int64_t *row_ptr, const int32_t *col, const uint32
     return DW_OK;
 }
 
-size_t dw_walk_replay_positions_workspace_bytes(int64_t n_walks) {
-    return 256 + static_cast<size_t>(n_walks > 0 ? n_walks : 0) * sizeof(N2VDefer);
-}
-
-int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
-                             const int32_t *col_sorted, const int64_t *adj_off,
-                             const int32_t *adj_hash, const int32_t *adj_hpos,
-                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
-                             const uint32_t *edge_cn, const int32_t *n2v_rec,
+int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *n2v_rec,
                              const uint8_t *n2v_pos, int64_t n_rows, const int32_t *starts,
                              int64_t n_walks, int32_t walk_length, double p, double q,
                              const double *uniforms, int32_t *out, int32_t *status,
-                             void *workspace, size_t workspace_bytes, uint64_t *counters,
-                             void *stream) {
+                             uint64_t *counters, void *stream) {
     DW_REQUIRE(walk_length >= 1, "dw_walk_replay_positions: Minimum walk length is 1!");
     DW_REQUIRE(n_walks >= 0 && n_rows >= 0, "dw_walk_replay_positions: negative size");
     if (n_walks == 0) return DW_OK;
-    DW_REQUIRE(row_ptr && col && col_sorted && adj_off && adj_hash && adj_hpos && edge_cn &&
-                   n2v_rec && starts && out && status && workspace,
+    DW_REQUIRE(row_ptr && n2v_rec && n2v_pos && starts && out && status,
                "dw_walk_replay_positions: null pointer");
-    DW_REQUIRE(workspace_bytes >= dw_walk_replay_positions_workspace_bytes(n_walks),
-               "dw_walk_replay_positions: workspace too small");
     DW_REQUIRE(walk_length == 1 || uniforms, "dw_walk_replay_positions: uniforms is null");
     DW_REQUIRE(p > 0.0 && q > 0.0, "dw_walk_replay_positions: p and q must be positive");
-    DW_REQUIRE(!hub_idx || (hub_bits && hub_words >= (n_rows + 31) / 32),
-               "dw_walk_replay_positions: hub bitmaps need hub_bits of >= ceil(n_rows / 32) words");
-    ReplayCtx c;
-    c.row_ptr = row_ptr;
-    c.col = col;
-    c.col_sorted = col_sorted;
-    c.w = nullptr;
-    c.node2vec = true;
-    c.inv_p = 1.0 / p;   // `1 / self._p` (host IEEE division)
-    c.inv_q = 1.0 / q;
-    DW_REQUIRE(c.inv_p < 1e300 && c.inv_q < 1e300, "dw_walk_replay_positions: p, q too small");
+    const double ip = 1.0 / p, iq = 1.0 / q;   // `1 / self._p` (host IEEE division)
+    DW_REQUIRE(ip < 1e300 && iq < 1e300, "dw_walk_replay_positions: p, q too small");
     const hipStream_t st = dw::as_stream(stream);
-    uint32_t *n_defer = static_cast<uint32_t *>(workspace);
-    N2VDefer *defer = reinterpret_cast<N2VDefer *>(static_cast<char *>(workspace) + 256);
-    DW_WALK_HIP_OK(hipMemsetAsync(n_defer, 0, sizeof(uint32_t), st),
-                   "dw_walk_replay_positions: memset");
     int64_t blocks = (n_walks + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     auto *cnt = reinterpret_cast<unsigned long long *>(counters);
     if (counters)
         hipLaunchKernelGGL(k_walk_replay_n2v_pos<true>, dim3((unsigned)blocks), dim3(256), 0, st,
                            row_ptr, reinterpret_cast<const int4 *>(n2v_rec), n2v_pos, n_rows,
-                           starts, n_walks, walk_length, uniforms, c.inv_p, c.inv_q, out, status,
-                           defer, n_defer, cnt);
+                           starts, n_walks, walk_length, uniforms, ip, iq, out, status, cnt);
     else
         hipLaunchKernelGGL(k_walk_replay_n2v_pos<false>, dim3((unsigned)blocks), dim3(256), 0, st,
                            row_ptr, reinterpret_cast<const int4 *>(n2v_rec), n2v_pos, n_rows,
-                           starts, n_walks, walk_length, uniforms, c.inv_p, c.inv_q, out, status,
-                           defer, n_defer, cnt);
+                           starts, n_walks, walk_length, uniforms, ip, iq, out, status, cnt);
     DW_LAUNCH_CHECK("dw_walk_replay_positions");
-    // the handed-over walks (the count stays on the device: a fixed grid, graph-capturable)
-    const N2VIndex ix{adj_off, adj_hash, adj_hpos, 64, cnt, hub_idx, hub_bits, hub_words, edge_cn};
-    int64_t rblocks = (n_walks + REPLAY_WAVES - 1) / REPLAY_WAVES;
-    if (rblocks > 1024) rblocks = 1024;
-    hipLaunchKernelGGL((k_walk_replay_cn<REPLAY_CH_CN, REPLAY_NCAP_EXACT>), dim3((unsigned)rblocks),
-                       dim3(REPLAY_WAVES * WAVE), 0, st, c, n_rows, starts, n_walks, walk_length,
-                       uniforms, out, status, 1, ix, defer, n_defer);
-    DW_LAUNCH_CHECK("dw_walk_replay_positions/handed over");
     return DW_OK;
 }
 

@@ -37,7 +37,7 @@ DW_EXACT_DEFER = 1
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -160,14 +160,12 @@ SIGNATURES = {
                                                _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p,
                                                _p, _szp, _p, _p]),
     'dw_n2v_edge_records': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _p]),
-    'dw_walk_replay_positions_workspace_bytes': (ctypes.c_size_t, [_i64]),
     'dw_exact_register': (ctypes.c_int, [_p, _p, _i64, _i32, _i32]),
     'dw_exact_unregister': (ctypes.c_int, [_p]),
     'dw_exact_frac_bits': (ctypes.c_int32, [_f64]),
     'dw_fixed_to_float': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),
-    'dw_walk_replay_positions': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p,
-                                                _i64, _p, _i64, _i32, _f64, _f64, _p, _p, _p, _p,
-                                                ctypes.c_size_t, _p, _p]),
+    'dw_walk_replay_positions': (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _i32, _f64, _f64,
+                                                _p, _p, _p, _p, _p]),
     'dw_adj_hash_positions': (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     'dw_step_scalars_expand': (ctypes.c_int, [_p, _p, _i64, _p, _i64, _u64, _u64, _p, _p, _i64,
                                               _p, _i64, _p]),

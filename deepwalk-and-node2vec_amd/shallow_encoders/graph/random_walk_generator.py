@@ -324,7 +324,9 @@ class RandomWalk(ABC):
                              out: Optional[torch.Tensor] = None) -> dict:
         """node2vec, rng='python', unweighted: the same walks as ``walk_batch(start_ids,
         uniforms)`` with the replay walker's realised traffic counted (dw_walk_replay_indexed
-        with counters; a diagnostic launch): {'bytes', 'probes', 'entries', 'steps'}."""
+        with counters; a diagnostic launch): {'bytes', 'probes', 'entries', 'steps'} (over the
+        position index: 'probes' counts the picks made by the serial arithmetic, 'entries' the
+        2-B position units read)."""
         if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'python' \
                 or self._csr.weights is not None:
             raise ValueError('count_replay_traffic: node2vec with rng="python", unweighted')
@@ -360,12 +362,10 @@ class RandomWalk(ABC):
                   _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None)]
         uptr = _native.ptr(u) if u.numel() else None
         if _n2v_index_enabled() and d.get('n2v_rec') is not None:
-            nb = int(_native.load().dw_walk_replay_positions_workspace_bytes(n))
-            ws = torch.empty(nb, dtype=torch.uint8, device=out.device)
-            _native.call('dw_walk_replay_positions', *common, _native.ptr(d['n2v_rec']),
-                         _native.ptr(d['n2v_pos']), self._csr.vocab_size, _native.ptr(starts),
-                         n, L, float(p), float(q), uptr, _native.ptr(out), _native.ptr(status),
-                         _native.ptr(ws), nb, _native.ptr(counters), s)
+            _native.call('dw_walk_replay_positions', _native.ptr(d['row_ptr']),
+                         _native.ptr(d['n2v_rec']), _native.ptr(d['n2v_pos']),
+                         self._csr.vocab_size, _native.ptr(starts), n, L, float(p), float(q),
+                         uptr, _native.ptr(out), _native.ptr(status), _native.ptr(counters), s)
             return
         _native.call('dw_walk_replay_indexed', *common, self._csr.vocab_size,
                      _native.ptr(starts), n, L, float(p), float(q), uptr, _native.ptr(out),

@@ -1365,7 +1365,8 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     side streams while step k's out rows, centre pass and in-table update run, from the moment
     step k - 1 has finished (the buffers alternate by step parity: workspace slot, row counts,
     touched list). Only the out rows' step, the centre pass and the in rows' update stay on the
-    step's critical path. The results equal the sequential steps': each kernel reads and writes
+    step's critical path. The preparation forks after step k's out rows by default
+    (DW_PIPE_FORK=before: at step k's start). The results equal the sequential steps': each kernel reads and writes
     what it would there (the catch-up of step k + 1 skips the centres of step k, which step k
     updates itself). ``bind(k)``: called before enqueueing anything of step k (graph capture:
     binds step k's dw_step_scalars block). Returns the record count of the steps."""
@@ -1420,6 +1421,10 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     ready = ahead(0)
     slots = batches[0].shape[0] * (L - 2 * R) * 2 * R * (1 + K)
     p = t._pipe
+    # where step k + 1's preparation forks: after step k's out rows (default; beside the centre
+    # pass and the in rows' update) or at step k's start (beside the out rows, whose resident
+    # grid it then competes with)
+    fork_early = os.environ.get('DW_PIPE_FORK', 'after') == 'before'
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
@@ -1427,12 +1432,16 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
         t.begin_step()
         for ev in ready:
             main.wait_event(ev)
-        if k + 1 < n_steps:
+        if fork_early and k + 1 < n_steps:
             ready = ahead(k + 1)
             if bind is not None:
                 bind(k)
         w = batches[k]
         t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
+        if not fork_early and k + 1 < n_steps:
+            ready = ahead(k + 1)
+            if bind is not None:
+                bind(k)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,

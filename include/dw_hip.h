@@ -314,27 +314,18 @@ int32_t dw_exact_frac_bits(double scale);
 int dw_fixed_to_float(int64_t *acc, float *grad, int64_t n, int32_t frac, int32_t accumulate,
                       void *stream);
 
-/* Bytes of dw_walk_replay_positions' workspace for n_walks walks. */
-size_t dw_walk_replay_positions_workspace_bytes(int64_t n_walks);
-
 /* dw_walk_replay_indexed's walks, bit for bit, over the position index (n2v_rec / n2v_pos of
  * dw_n2v_edge_index_build): one lane per walker, a step reads its edge's 32-B record and
- * binary-searches that edge's positions (log2 C loads), the pick by the same margin rule. A walk
- * whose pick the margin cannot decide is handed, from that step, to the wave walker of
- * dw_walk_replay_indexed (the remaining arguments serve it) in a second launch whose grid does
- * not depend on how many were handed over (graph-capturable). counters: NULL, or uint64[4]
- * (caller-zeroed) += {bytes, hash probes, list / position entries read, steps}. Replaces
- * random_walk_generator.py:94-119 on unweighted graphs. */
-int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *col,
-                             const int32_t *col_sorted, const int64_t *adj_off,
-                             const int32_t *adj_hash, const int32_t *adj_hpos,
-                             const int32_t *hub_idx, const uint32_t *hub_bits, int64_t hub_words,
-                             const uint32_t *edge_cn, const int32_t *n2v_rec,
+ * binary-searches that edge's positions (log2 C loads), the pick by the margin rule; a pick the
+ * margin cannot decide is made by the reference's own fp64 arithmetic (sum, normalise,
+ * accumulate, bisect_right) replayed run by run over the position list, O(C + log n) in the
+ * walker's lane. counters: NULL, or uint64[4] (caller-zeroed) += {bytes, serial picks, position
+ * 2-B units read, steps}. Replaces random_walk_generator.py:94-119 on unweighted graphs. */
+int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *n2v_rec,
                              const uint8_t *n2v_pos, int64_t n_rows, const int32_t *starts,
                              int64_t n_walks, int32_t walk_length, double p, double q,
                              const double *uniforms, int32_t *out, int32_t *status,
-                             void *workspace, size_t workspace_bytes, uint64_t *counters,
-                             void *stream);
+                             uint64_t *counters, void *stream);
 
 /* Neighbour bitmaps of hub rows for dw_walk_replay_indexed (hub_idx / hub_bits; NULL = none):
  * bits[k * hub_words + (x >> 5)] bit (x & 31) = x in N(hub_rows[k]); hub_words >=

@@ -122,7 +122,7 @@ def main():
     c = w.count_replay_traffic(st, u, out=torch.empty_like(out))
     emit(stage='rate', walker='dw_walk_replay_positions', walks=n, kernel_ms=best,
          walks_per_s=n / (best * 1e-3), bytes_per_step=c['bytes'] / max(c['steps'], 1),
-         entries_per_step=c['entries'] / max(c['steps'], 1),
+         entries_per_step=c['entries'] / max(c['steps'], 1), serial_picks=c['probes'],
          frac_hbm=c['bytes'] / (best * 1e-3) / 8e12)
     # the Philox walker over the same index (dw_walk_fast_positions), walks from every start
     wp = Node2Vec(csr, L, p=args.p, q=args.q, rng='philox', seed=3, device=dev)

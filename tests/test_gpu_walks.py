@@ -657,7 +657,11 @@ def test_n2v_position_index_vs_oracle(which, hip_device, monkeypatch):
     width = np.where(wide, 4, 2)
     boff_ref = np.concatenate([[0], np.cumsum((cnt * width + 3) // 4 * 4)])
     np.testing.assert_array_equal(boff, boff_ref[:-1])
-    cn = walk_ref.edge_class_counts(walk_ref.CSR(csr.row_ptr, col, None))
+    if which == 'hub_66k':   # (the direct count is O(sum deg^2): from the positions)
+        cn = (np.diff(off_ref).astype(np.uint32)
+              | np.where(pt_ref >= 0, np.uint32(1 << 31), np.uint32(0)))
+    else:
+        cn = walk_ref.edge_class_counts(walk_ref.CSR(csr.row_ptr, col, None))
     np.testing.assert_array_equal(rec[:, 6].view(np.uint32), cn)
     np.testing.assert_array_equal(rec[:, 7], pt_ref)
     assert d['n2v_index_info']['entries'] == len(pos_ref)
@@ -671,8 +675,8 @@ def test_n2v_position_index_vs_oracle(which, hip_device, monkeypatch):
 def _boundary_uniforms(csr, starts, L, p, q, rng):
     """Uniforms with a quarter of the walks' first draws exactly on k / deg (the first step's
     margin declines) and a quarter of the second draws on an exact node2vec prefix W_k / T of
-    the step the oracle takes there (the position walker's margin declines): those walks are
-    handed to the wave walker."""
+    the step the oracle takes there (the position walker's margin declines): those picks are
+    made by the serial arithmetic."""
     g = walk_ref.CSR(csr.row_ptr, csr.host_col(), None)
     deg = csr.degree()
     n = len(starts)
@@ -692,27 +696,36 @@ def _boundary_uniforms(csr, starts, L, p, q, rng):
     return u
 
 
-@pytest.mark.parametrize('p,q', [(0.25, 4.0), (2.0, 0.5), (1.0, 1.0)])
-def test_n2v_positions_hand_over_vs_oracle(p, q, hip_device):
-    """dw_walk_replay_positions hands a walk whose pick its margin cannot decide (uniforms on
-    exact class boundaries, at the first step and at a second-order step) to the wave walker,
-    which finishes it from that step: the walks equal the oracle's serial replay bit for bit,
-    and equal the wave walker's (DW_N2V_POS=0)."""
+@pytest.mark.parametrize('which', ['rmat12', 'hub_66k'])
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (2.0, 0.5), (1.0, 1.0), (0.3, 3.0)])
+def test_n2v_positions_serial_picks_vs_oracle(p, q, which, hip_device):
+    """dw_walk_replay_positions makes a pick its margin cannot decide (uniforms on exact class
+    boundaries, at the first step and at a second-order step) by the reference's own fp64
+    arithmetic replayed run by run over the position list: the walks equal the oracle's serial
+    replay bit for bit (and, on R-MAT 12, the wave walker's, DW_N2V_POS=0), and the counters
+    show the serial picks were taken. hub_66k: boundary draws at a 66,000-neighbour hub (its
+    int32 lists), non-dyadic 1/p, 1/q included."""
     import os
-    f = golden('walks_rmat12_node2vec_p0.25_q4.npz')
-    csr = _csr(f)
     rng = np.random.default_rng(17)
-    deg = csr.degree()
-    nodes = np.nonzero(deg > 0)[0]
-    starts = rng.choice(nodes, 512).astype(np.int32)
-    L = 12
+    if which == 'rmat12':
+        csr = _csr(golden('walks_rmat12_node2vec_p0.25_q4.npz'))
+        deg = csr.degree()
+        starts = rng.choice(np.nonzero(deg > 0)[0], 512).astype(np.int32)
+    else:
+        csr = _hub_graph(n_leaves=66_000, seed=2)
+        starts = np.concatenate([np.full(24, 1), rng.integers(2, 66_001, 40)]).astype(np.int32)
+    L = 12 if which == 'rmat12' else 6
     u = _boundary_uniforms(csr, starts, L, p, q, rng)
-    got = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(torch.as_tensor(starts),
-                                                                   uniforms=u).cpu().numpy()
+    w = Node2Vec(csr, L, p=p, q=q, device=hip_device)
+    got = w.walk_batch(torch.as_tensor(starts), uniforms=u).cpu().numpy()
     assert csr.device_tensors(hip_device).get('n2v_rec') is not None
     ref = walk_ref.walks_replay(walk_ref.CSR(csr.row_ptr, csr.host_col(), None), starts, L,
                                 'node2vec', p, q, u)
     np.testing.assert_array_equal(got, ref)
+    c = w.count_replay_traffic(torch.as_tensor(starts), torch.from_numpy(u).to(hip_device))
+    assert c['probes'] > 0, c   # the serial picks
+    if which != 'rmat12':
+        return
     os.environ['DW_N2V_POS'] = '0'
     try:
         wave = Node2Vec(csr, L, p=p, q=q, device=hip_device).walk_batch(
