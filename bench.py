@@ -205,6 +205,8 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
               if args.method == 'node2vec' else DeepWalk(csr, L, rng='philox', seed=1234,
                                                          device=dev))
     tables = OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=0, lazy_out=True)
+    if args.deterministic:   # the integer sums of the rows-major step (word2vec/exact.py)
+        tables.enable_exact(grad_scale)
     loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -284,6 +286,7 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
             'sgns_bytes': pairs * bpp, 'touched_rows_adam_bytes': adam_bytes,
             'touched_in_rows': n_in, 'touched_out_rows': n_out},
         'step_check': step_check,
+        'deterministic': bool(args.deterministic),
         'cpu_baseline': None,
     }
 
@@ -410,7 +413,11 @@ def main():
                          'ranks); dense in-table Adam and the records path, as that mode needs')
     args = ap.parse_args()
     if args.deterministic:
-        args.n1_in_adam, args.scatter = 'dense', 'sorted'
+        # one GPU, sparse batches keep the lazy owner path (its rows-major step has the integer
+        # sums); otherwise the dense in-table Adam and the records path
+        if args.n1_in_adam != 'lazy':
+            args.n1_in_adam = 'auto'
+        args.scatter = 'sorted'
     for k, v in CONFIGS[args.config].items():   # explicit flags override the preset
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -533,9 +540,10 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
     pairs_per_step = centres * 2 * R
     grad_scale = 1.0 / (pairs_per_step * W_eff)   # mean over the GLOBAL batch
     if args.deterministic:
-        if lazy or auto_in:
+        if auto_in or (lazy and not (n1_lazy and getattr(tables, 'lazy_out', False))):
             raise SystemExit('--deterministic needs the dense in-table exchange '
-                             '(--in-exchange sharded)')
+                             '(--in-exchange sharded), or one GPU\'s lazy owner path with the '
+                             'lazy out table')
         tables.enable_exact(grad_scale)
     walks_total = N * args.walks_per_node
     BG = B * W_eff if owner else B      # walks each rank generates per step (owner: all ranks')
@@ -1286,7 +1294,7 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
     # ---- the reference configs' own 64-walk batch on the same graph ---------
     b64 = None
     if (args.batch64_steps > 0 and not dist_on and not owner and not emulate
-            and args.config == 'c3' and B != 64 and not args.deterministic):
+            and args.config == 'c3' and B != 64):
         del tables
         torch.cuda.empty_cache()
         b64 = batch64_line(csr, args, dev, epoch_starts, copy_gbs, args.batch64_steps)

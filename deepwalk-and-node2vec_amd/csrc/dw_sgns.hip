@@ -417,7 +417,7 @@ __device__ __forceinline__ float row_sum16(float x) {
 template <int F4, bool FROM_WALKS, int CHR, bool OWNER, bool EXACT = false, bool COEFIN = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_WAVES)
     k_sgns_g16(SgnsArgs a) {
-    static_assert(!COEFIN || (OWNER && !EXACT), "the coefficients-in form is the owner path's");
+    static_assert(!COEFIN || OWNER, "the coefficients-in form is the owner path's");
     constexpr int D = 64 * F4;
     __shared__ int32_t s_id[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
@@ -1267,15 +1267,17 @@ int launch_pass1_g16(const SgnsArgs &a, hipStream_t st) {
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
     if constexpr (COEFIN) {
-        DW_REQUIRE(!a.fx_in.acc, "dw_sgns_owner_pass1: the rows-major step has no deterministic "
-                   "form");
         // (eight and sixteen rows per chunk measured 45 and 59 us against 42 at C3's 64-walk
         // batch: the pass-1 chunking stays)
-        switch (a.d / 64) {
-            case 1: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, true, false, true>), g, bl, 0, st, a); break;
-            case 2: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
-            case 4: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
-            case 8: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, false, true>), g, bl, 0, st, a); break;
+        switch ((a.d / 64) * 2 + (a.fx_in.acc ? 1 : 0)) {
+            case 2: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, true, false, true>), g, bl, 0, st, a); break;
+            case 3: hipLaunchKernelGGL((k_sgns_g16<1, FROM_WALKS, 8, true, true, true>), g, bl, 0, st, a); break;
+            case 4: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, false, true>), g, bl, 0, st, a); break;
+            case 5: hipLaunchKernelGGL((k_sgns_g16<2, FROM_WALKS, 4, true, true, true>), g, bl, 0, st, a); break;
+            case 8: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, false, true>), g, bl, 0, st, a); break;
+            case 9: hipLaunchKernelGGL((k_sgns_g16<4, FROM_WALKS, 2, true, true, true>), g, bl, 0, st, a); break;
+            case 16: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, false, true>), g, bl, 0, st, a); break;
+            case 17: hipLaunchKernelGGL((k_sgns_g16<8, FROM_WALKS, 1, true, true, true>), g, bl, 0, st, a); break;
             default:
                 dw::set_error("dw_sgns: the coefficient-input pass 1 needs d in {64, 128, 256, 512}, got %d", a.d);
                 return DW_E_UNSUPPORTED;
@@ -1440,13 +1442,18 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // its centre rows, so waiting for those never waits for the prefetch: loads return in order),
 // so one round trip is left exposed per row; the registers this takes hold the kernel at six
 // waves per SIMD (OUT_ROWS_WAVES; the chunks are sized so that every wave is resident at once).
+// EXACT (the deterministic mode, g_out registered): each term coef * w_in enters the row's sum
+// as a fixed-point integer (dw::to_fixed, the records gather's rule), so the sum is the same
+// whatever order the claim's atomics ranked the records in; a straddling row adds its integer
+// part into fo.acc, which k_fixed_boundary converts once every chunk has.
 constexpr int OUT_ROWS_WAVES = 6;
-template <int F4>
+template <int F4, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
-               float *__restrict__ g_out, float *__restrict__ coef_slot) {
+               float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo) {
     constexpr int D = 64 * F4;
+    bool fx_range = false;
     constexpr int RU = 4;   // records per round (one per 16-lane group)
     __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
     __shared__ float4 s_p[WAVES_PER_BLOCK][D / 4];        // the row's p^{s-1}
@@ -1511,6 +1518,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             const int64_t ro = static_cast<int64_t>(row) * D + lane;
             const int cnt = re - rs;
             float p[F4], m[F4], v[F4], g[F4];
+            int64_t gx[EXACT ? F4 : 1];
 #pragma unroll
             for (int f = 0; f < F4; ++f) {
                 p[f] = np[f];
@@ -1518,6 +1526,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                 v[f] = nv[f];
                 g[f] = 0.f;
             }
+#pragma unroll
+            for (int f = 0; f < (EXACT ? F4 : 1); ++f) gx[f] = 0;
             const int32_t from = __builtin_amdgcn_readfirstlane(nlast);
             const bool pd = __builtin_amdgcn_readfirstlane(npend) != 0;
             // this row's prefetched loads (issued a row ago) are complete before the next loads
@@ -1581,14 +1591,31 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     if (j0 + u >= cnt) break;
                     const float cu = __shfl(coef, u << 4, WAVE);
                     const float *cr = reinterpret_cast<const float *>(&s_c[wv][u][0]);
+                    if constexpr (EXACT) {
 #pragma unroll
-                    for (int f = 0; f < F4; ++f) g[f] += cu * cr[lane + 64 * f];
+                        for (int f = 0; f < F4; ++f)
+                            gx[f] += dw::to_fixed(cu * cr[lane + 64 * f], fo.fs, fx_range);
+                    } else {
+#pragma unroll
+                        for (int f = 0; f < F4; ++f) g[f] += cu * cr[lane + 64 * f];
+                    }
                 }
                 dw::wave_lds_sync();   // s_c is rewritten next round
             }
-            if (straddle) {
+            if constexpr (EXACT) {
+                if (straddle) {
 #pragma unroll
-                for (int f = 0; f < F4; ++f) atomicAdd(g_out + ro + 64 * f, g[f]);
+                    for (int f = 0; f < F4; ++f) dw::fixed_add(fo.acc + ro + 64 * f, gx[f]);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) g[f] = dw::from_fixed(gx[f], fo.fi);
+                }
+            }
+            if (straddle) {
+                if constexpr (!EXACT) {
+#pragma unroll
+                    for (int f = 0; f < F4; ++f) atomicAdd(g_out + ro + 64 * f, g[f]);
+                }
             } else {
                 // the moments of step s; p stays p^{s-1} for the centre pass, which reads it from
                 // the table (no per-slot copies), and the parameter half waits (pend[row])
@@ -1608,6 +1635,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
         }
         dw::wave_lds_sync();   // s_rs is rewritten by the next chunk
     }
+    if constexpr (EXACT)
+        if (__ballot(fx_range) && lane == 0) dw::status_or(a.status, DW_S_FIXED_RANGE);
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
 
@@ -3217,7 +3246,6 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     dw::Fixed fx;
     int rc = exact_of(g_out_local, local_rows * dim, &fx, &fl, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;
-    DW_REQUIRE(!fx.acc, "dw_sgns_owner_out_rows: the rows-major step has no deterministic form");
     Workspace ws;
     OwnerLayout lay;
     PlaceSpace pl;
@@ -3241,16 +3269,30 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), bl(WAVES_PER_BLOCK * WAVE);
-    switch (dim / 64) {
-        case 1: hipLaunchKernelGGL(k_out_rows<1>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
-        case 2: hipLaunchKernelGGL(k_out_rows<2>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
-        case 4: hipLaunchKernelGGL(k_out_rows<4>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
-        case 8: hipLaunchKernelGGL(k_out_rows<8>, g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa, g_out_local, reinterpret_cast<float *>(ws.v0)); break;
+    float *cs = reinterpret_cast<float *>(ws.v0);
+#define DW_OUT_ROWS(F, X)                                                                       \
+    hipLaunchKernelGGL((k_out_rows<F, X>), g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa,    \
+                       g_out_local, cs, fx)
+    switch ((dim / 64) * 2 + (fx.acc ? 1 : 0)) {
+        case 2: DW_OUT_ROWS(1, false); break;
+        case 3: DW_OUT_ROWS(1, true); break;
+        case 4: DW_OUT_ROWS(2, false); break;
+        case 5: DW_OUT_ROWS(2, true); break;
+        case 8: DW_OUT_ROWS(4, false); break;
+        case 9: DW_OUT_ROWS(4, true); break;
+        case 16: DW_OUT_ROWS(8, false); break;
+        case 17: DW_OUT_ROWS(8, true); break;
         default:
             dw::set_error("dw_sgns_owner_out_rows: d must be one of 64, 128, 256, 512 (got %d)", dim);
             return DW_E_UNSUPPORTED;
     }
+#undef DW_OUT_ROWS
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
+    if (fx.acc) {   // the straddling rows' exact sums into g_out, before their step
+        hipLaunchKernelGGL(k_fixed_boundary, g, bl, 0, st, ws.k1, bound, gch, ws.bounds, fx,
+                           g_out_local, dim);
+        DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/fixed_boundary");
+    }
     switch (dim / 64) {   // the straddling rows (g in g_out)
         case 1: launch_boundary<1>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
         case 2: launch_boundary<2>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;

@@ -966,11 +966,26 @@ class OwnerLazyTables(OwnerTables):
     def rows_major_ok(self, context_radius: int, neg_samples: int) -> bool:
         """The rows-major step applies: placed records, d one of the widths its kernels are
         built for (dw_sgns_owner_out_rows and the COEFIN pass 1: 64, 128, 256, 512),
-        2R(1+K) <= 64, no deterministic mode. Other widths keep the catch-up -> pass 1 ->
-        lazy gather sequence."""
+        2R(1+K) <= 64 (the deterministic mode included: both kernels have its integer sums).
+        Other widths keep the catch-up -> pass 1 -> lazy gather sequence."""
         return (self.rows_major and self.place and self.d in ROWS_MAJOR_DIMS
-                and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64
-                and getattr(self, '_exact', None) is None)
+                and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64)
+
+    def enable_exact(self, grad_scale: float) -> None:
+        """The deterministic mode (word2vec/exact.py) on one rank with the HIP lazy Adam of both
+        tables: grads_in and g_out get int64 fixed-point accumulators, so the rows-major step
+        sums every out row's terms (k_out_rows) and every centre's (the COEFIN pass) as integers
+        — the same sums whatever order the claim's atomics ranked the records in — and the
+        tables are bit-identical run to run, and to the dense deterministic step's (the lazy
+        replays are the dense g = 0 steps bit for bit). N > 1 is not covered: the touched rows'
+        all-reduce is a float sum."""
+        from shallow_encoders.word2vec import exact
+        if self.multi or not self._hip() or not self.lazy_out:
+            raise NotImplementedError('the lazy deterministic mode covers one rank with the HIP '
+                                      'lazy Adam of both tables (lazy_out)')
+        self._exact = exact.Registry()
+        self._exact.ensure(0, self.grads_in, grad_scale)
+        self._exact.ensure(1, self.g_out, grad_scale)
 
     def pipeline_ok(self, context_radius: int, neg_samples: int) -> bool:
         """owner_lazy_steps pipelines the steps: one rank, the HIP lazy Adam of both tables and

@@ -134,6 +134,70 @@ def test_exact_tables_repeatable(hip_device):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize('form', ['sequential', 'pipelined'])
+def test_exact_lazy_rows_major_repeatable_and_equal_dense(form, hip_device):
+    """OwnerLazyTables on one rank with the lazy Adam of both tables (the rows-major out step,
+    the reference's small-batch path) in the deterministic mode: two runs give bit-identical
+    tables and Adam state, and they equal the dense deterministic step's (ShardedTables:
+    every row's Adam every step) bit for bit once flushed — the integer sums make the claim's
+    record order irrelevant, and the lazy replays are the dense g = 0 steps. 'pipelined':
+    owner_lazy_steps (the next step's claims beside this one)."""
+    from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables,
+                                                    owner_lazy_step, owner_lazy_steps,
+                                                    replicated_step)
+    V, d, R, K, L, n, steps = 4000, 128, 3, 5, 40, 64, 6
+    g = torch.Generator().manual_seed(3)
+    walks = torch.randint(1, V, (steps, n, L), generator=g, dtype=torch.int32)
+    walks[:, :, ::5] = 9                     # a hub out row straddling the out-rows chunks
+    per = L - 2 * R
+    scale = 1.0 / (n * per * 2 * R)
+    offs = [s * n * per for s in range(steps)]
+
+    def lazy():
+        t = OwnerLazyTables(V, d, hip_device, lr=0.01, init_seed=2, emulate_world=1,
+                            lazy_out=True)
+        t.enable_exact(scale)
+        assert t.rows_major_ok(R, K) and t.pipeline_ok(R, K)
+        acc = torch.zeros(4, dtype=torch.float64, device=hip_device)
+        st = torch.zeros(1, dtype=torch.int32, device=hip_device)
+        owner_lazy_step(t, walks[0].cuda(), R, K, seed=5, noise_offset=0, grad_scale=scale,
+                        loss_acc=acc, status=st)
+        if form == 'pipelined':
+            owner_lazy_steps(t, [walks[s].cuda() for s in range(1, steps)], R, K, seed=5,
+                             noise_offsets=offs[1:], grad_scale=scale, loss_acc=acc,
+                             status=st)
+        else:
+            for s in range(1, steps):
+                owner_lazy_step(t, walks[s].cuda(), R, K, seed=5, noise_offset=offs[s],
+                                grad_scale=scale, loss_acc=acc, status=st)
+        torch.cuda.synchronize()
+        _native.check_status(st, 'owner_lazy_step')
+        t.flush()
+        return [x.cpu().clone() for x in (t.params_in[0, :V], t.w_out[:V], t.m_in[:V],
+                                          t.v_in[:V], t.m_out[:V], t.v_out[:V])]
+
+    def dense():
+        t = ShardedTables(V, d, hip_device, lr=0.01, init_seed=2)
+        t.enable_exact(scale)
+        acc = torch.zeros(4, dtype=torch.float64, device=hip_device)
+        st = torch.zeros(1, dtype=torch.int32, device=hip_device)
+        for s in range(steps):
+            replicated_step(t, walks[s].cuda(), R, K, seed=5, noise_offset=offs[s],
+                            grad_scale=scale, loss_acc=acc, status=st)
+        torch.cuda.synchronize()
+        _native.check_status(st, 'replicated_step')
+        return [x.cpu().clone() for x in (t.w_in, t.w_out, t.m[0, :V], t.v[0, :V], t.m[1, :V],
+                                          t.v[1, :V])]
+
+    a, b, c = lazy(), lazy(), dense()
+    names = ('w_in', 'w_out', 'm_in', 'v_in', 'm_out', 'v_out')
+    for name, x, y in zip(names, a, b):
+        assert torch.equal(x, y), f'{name}: two lazy runs differ'
+    for name, x, y in zip(names, a, c):
+        diff = int((x != y).sum())
+        assert diff == 0, f'{name}: {diff} entries differ from the dense deterministic step'
+
+
 # ---- two ranks on one GPU (gloo), deterministic mode: bit-identical to one process ---------
 V2, D2, R2, K2, L2, NW2, STEPS2, LR2 = 900, 64, 2, 3, 14, 48, 4, 5e-3
 
