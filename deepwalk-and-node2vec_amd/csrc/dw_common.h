@@ -389,14 +389,55 @@ __device__ __forceinline__ void replay_g0(float (&p)[N], float (&m)[N], float (&
 }
 
 // A row left pending by the lazy out step (m, v at step `at`, p at at - 1): the parameter half
-// of step `at` (adam_p with that step's scalars), which makes the row current to `at`.
+// of step `at` (adam_p with that step's scalars), which makes the row current to `at`. When the
+// step is in the box (at >= box_from: its scalars certified by the host) and every element's
+// operands are — v +0 or in [2^-96, 2^20], m +0 or |m| in [2^-100, 2^60], so the denominator
+// lies in [2^-27, 2^21) — the unscaled sqrt and division (the box replay's, packed two elements
+// per instruction) give the same bits for about half the issue slots: nearly every row the
+// rows-major step touches was left pending by an earlier step.
 template <int N>
 __device__ __forceinline__ void settle_pending(float (&p)[N], const float (&m)[N],
                                                const float (&v)[N],
-                                               const float *__restrict__ hist, int32_t at) {
+                                               const float *__restrict__ hist, int32_t at,
+                                               int32_t box_from = INT32_MAX) {
+#pragma clang fp contract(off)
     // (the scalars through the scalar unit: a vector load here would make the wave wait for
     // every load issued before it — vector loads return in order)
     const AdamScalars h = hist_at_const((const const_float *)hist + 8 * static_cast<int64_t>(at));
+    bool ok = at >= box_from;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        ok = ok &&
+             (__float_as_uint(v[k]) == 0u || (v[k] >= 0x1p-96f && v[k] <= 0x1p20f)) &&
+             (__float_as_uint(m[k]) == 0u ||
+              (fabsf(m[k]) >= 0x1p-100f && fabsf(m[k]) <= 0x1p60f));
+    if (__all(ok)) {
+        if constexpr (N % 2 == 0) {
+            const f32x2 rb = {h.rbc2s, h.rbc2s}, bc = {h.bc2s, h.bc2s};
+            const f32x2 eps = {h.eps, h.eps}, ns = {h.nstep, h.nstep};
+#pragma unroll
+            for (int k = 0; k < N / 2; ++k) {
+                const f32x2 M = {m[2 * k], m[2 * k + 1]};
+                const f32x2 x = sqrt_box2(f32x2{v[2 * k], v[2 * k + 1]});
+                const f32x2 q = x * rb;
+                const f32x2 c = __builtin_elementwise_fma(-bc, q, x);
+                const f32x2 denom = __builtin_elementwise_fma(c, rb, q) + eps;
+                const f32x2 P = f32x2{p[2 * k], p[2 * k + 1]} + ns * div_box2(M, denom);
+                p[2 * k] = P.x;
+                p[2 * k + 1] = P.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const float x = sqrt_box(v[k]);
+                const float q = x * h.rbc2s;
+                const float c = fmaf(-h.bc2s, q, x);
+                const float denom = fmaf(c, h.rbc2s, q) + h.eps;
+                p[k] = p[k] + h.nstep * div_box(m[k], denom);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k) adam_p(p[k], m[k], v[k], h);
 }

@@ -842,8 +842,9 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
             }
         }
     } else {
-        if (pd) dw::settle_pending(pp, mm, vv, oa.hist, from);
-        dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1, dw::hist_box_from(oa.hist));
+        const int32_t box_from = dw::hist_box_from(oa.hist);
+        if (pd) dw::settle_pending(pp, mm, vv, oa.hist, from, box_from);
+        dw::replay_g0(pp, mm, vv, oa.hist, from, step - 1, box_from);
     }
     const dw::AdamScalars h = dw::hist_at(oa.hist, step);
 #pragma unroll
@@ -1547,7 +1548,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                                : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             prefetch(k + 1 < nrows ? k + 1 : k);   // (unconditional: no register copies)
-            if (pd) dw::settle_pending(p, m, v, oa.hist, from);     // the previous step's p half
+            if (pd) dw::settle_pending(p, m, v, oa.hist, from, box_from);   // the previous step's p half
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
             for (int f = 0; f < F4; ++f) sp[lane + 64 * f] = p[f];
