@@ -1384,31 +1384,57 @@ __global__ void __launch_bounds__(REPLAY_WAVES *WAVE)
 // hub's serial replay took ~0.5 s in one lane). tests/test_serial_runs.py restates ff_run /
 // runs_pass / the pick and checks them bit for bit against the sequential sums and the
 // oracle's choices_index.
+// ff_run's constants for one term y in one binade [lo, hi) of S (not a tie, D >= 1): every
+// addition there adds D ulps, so a run that stays inside costs a multiply and a compare. A pass
+// keeps one (its runs all add the same term).
+struct RunBinade {
+    double lo = 1.0, hi = 0.0, u = 0.0, iu = 0.0, D = 0.0;
+};
+
 // m additions of y (> 0) to S: returns the first addition (1-based) after which S > x (S left
 // there), or 0 (S after all m).
-__device__ int64_t ff_run(double &S, const double y, const int64_t m, const double x) {
+__device__ int64_t ff_run(double &S, const double y, const int64_t m, const double x,
+                          RunBinade &bc) {
     int64_t done = 0;
     while (done < m) {
+        if (S >= bc.lo && S < bc.hi) {   // the cached binade: does the rest of the run fit?
+            const double room = (bc.hi - S) * bc.iu;   // exact: ulps to the binade's top
+            const double left = static_cast<double>(m - done);
+            if (left * bc.D <= room) {
+                const double Sj = S + (left * bc.D) * bc.u;   // exact (on the grid, <= hi)
+                if (x < Sj) {
+                    const int64_t js =
+                        x < S ? 1
+                              : static_cast<int64_t>((x - S) * bc.iu) /
+                                        static_cast<int64_t>(bc.D) + 1;
+                    S = S + static_cast<double>(js) * bc.D * bc.u;
+                    return done + js;
+                }
+                S = Sj;
+                return 0;
+            }
+        }
         if (S > 0.0 && y < S) {
             const int e =
                 static_cast<int>((__double_as_longlong(S) >> 52) & 0x7FF) - 1022;   // S in [2^(e-1), 2^e)
             const double B2 = ldexp(1.0, e);
-            const double u = ldexp(1.0, e - 53);
-            const double qd = floor(y / u);
+            const double u = ldexp(1.0, e - 53), iu = ldexp(1.0, 53 - e);
+            const double qd = floor(y * iu);             // (powers of two: exact)
             const double r = y - qd * u;                 // exact
             const int64_t q = static_cast<int64_t>(qd);
-            const int64_t k = static_cast<int64_t>(S / u);
+            const int64_t k = static_cast<int64_t>(S * iu);
             const bool tie = r == 0.5 * u;
             if (!tie || (k & 1) == 0) {
                 const int64_t D = q + ((r > 0.5 * u || (tie && (q & 1))) ? 1 : 0);
                 if (D == 0) return S > x ? done + 1 : 0;   // the rest add nothing
-                const int64_t jmax = static_cast<int64_t>((B2 - S) / u) / D;
+                if (!tie) bc = RunBinade{0.5 * B2, B2, u, iu, static_cast<double>(D)};
+                const int64_t jmax = static_cast<int64_t>((B2 - S) * iu) / D;
                 if (jmax > 0) {
                     const int64_t j = jmax < m - done ? jmax : m - done;
                     const double Sj = S + static_cast<double>(j * D) * u;
                     if (x < B2 && x < Sj) {   // the crossing is inside the chunk
                         const int64_t js =
-                            x < S ? 1 : static_cast<int64_t>((x - S) / u) / D + 1;
+                            x < S ? 1 : static_cast<int64_t>((x - S) * iu) / D + 1;
                         S = S + static_cast<double>(js * D) * u;
                         return done + js;
                     }
@@ -1428,37 +1454,40 @@ __device__ int64_t ff_run(double &S, const double y, const int64_t m, const doub
 }
 
 // The fp64 left-to-right sum of the n terms (`one`, vp at pt, vq at the ascending P[0..C)) in
-// S; returns the first index < hi whose partial sum exceeds x, or -1.
+// S; returns the first index < hi whose partial sum exceeds x, or -1. The positions are read
+// four ahead (independent loads in flight while the runs are summed).
 __device__ int64_t runs_pass(PosList P, int64_t C, int64_t pt, double vp, double vq, int64_t n,
                              int64_t hi, double one, double x, double &S, uint32_t &loads) {
     S = 0.0;
-    int64_t i = 0, j = 0;
+    RunBinade bc;
+    int64_t i = 0, j = 0;   // j: the P entries consumed
     bool p_left = pt >= 0;
-    int64_t pj = C > 0 ? P[0] : n;
-    if (C > 0) loads += P.wide ? 2u : 1u;
+    auto ld = [&](int64_t k) -> int64_t { return k < C ? P[k] : n; };
+    int64_t q0 = ld(0), q1 = ld(1), q2 = ld(2), q3 = ld(3);
+    loads += (P.wide ? 2u : 1u) * static_cast<uint32_t>(C < 4 ? C : 4);
     while (true) {
         int64_t pos;
         double val;
-        if (p_left && pt < pj) {
+        if (p_left && pt < q0) {
             pos = pt;
             val = vp;
             p_left = false;
         } else if (j < C) {
-            pos = pj;
+            pos = q0;
             val = vq;
-            if (++j < C) {
-                pj = P[j];
-                loads += P.wide ? 2u : 1u;
-            } else {
-                pj = n;
-            }
+            ++j;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = ld(j + 3);
+            if (j + 3 < C) loads += P.wide ? 2u : 1u;
         } else {
             pos = n;
             val = 0.0;
         }
         const int64_t end = pos < hi ? pos : hi;
         if (end > i) {
-            const int64_t k = ff_run(S, one, end - i, x);
+            const int64_t k = ff_run(S, one, end - i, x, bc);
             if (k) return i + k - 1;
         }
         if (pos >= hi) return -1;

@@ -18,29 +18,50 @@ import pytest
 from oracle import walk_ref
 
 
-def ff_run(S: float, y: float, m: int, x: float = math.inf):
+class Binade:
+    """ff_run's constants for one term y in one binade [lo, hi) of S (non-tie, D >= 1): every
+    addition there adds D ulps (dw_walk.hip RunBinade)."""
+    def __init__(self):
+        self.lo, self.hi, self.u, self.iu, self.D = 1.0, 0.0, 0.0, 0.0, 0
+
+
+def ff_run(S: float, y: float, m: int, x: float = math.inf, bc: Binade = None):
     """m additions of y to S in fp64 round-to-nearest-even. Returns (S_after, j): j = the first
-    addition (1-based) after which S > x (S then stops there), or 0 when none."""
+    addition (1-based) after which S > x (S then stops there), or 0 when none. ``bc``: the
+    binade cache of the pass (the device keeps one per pass)."""
+    bc = Binade() if bc is None else bc
     done = 0
     while done < m:
+        if bc.lo <= S < bc.hi:                 # the cached binade: whole rest of the run?
+            room = (bc.hi - S) * bc.iu         # exact: integer ulps to the binade's top
+            left = m - done
+            if left * bc.D <= room:
+                Sj = S + (left * bc.D) * bc.u
+                if x < Sj:
+                    js = 1 if x < S else int((x - S) * bc.iu) // bc.D + 1
+                    return S + (js * bc.D) * bc.u, done + js
+                return Sj, 0
         if S > 0.0 and y < S:   # (y >= S: the single step below)
             f, e = math.frexp(S)               # S in [2^(e-1), 2^e)
             B2 = math.ldexp(1.0, e)
             u = math.ldexp(1.0, e - 53)
-            q = math.floor(y / u)
+            iu = math.ldexp(1.0, 53 - e)
+            q = math.floor(y * iu)
             r = y - q * u
-            k = int(S / u)
+            k = int(S * iu)
             tie = r == 0.5 * u
             if not tie or k % 2 == 0:
                 D = q + (1 if (r > 0.5 * u or (tie and q % 2 == 1)) else 0)
                 if D == 0:                     # every remaining addition leaves S as it is
                     return S, (done + 1 if S > x else 0)
-                G = int((B2 - S) / u)
+                if not tie:
+                    bc.lo, bc.hi, bc.u, bc.iu, bc.D = 0.5 * B2, B2, u, iu, D
+                G = int((B2 - S) * iu)
                 jmax = G // D
                 if jmax > 0:
                     j = min(jmax, m - done)
                     if x < B2 and x < S + (j * D) * u:   # the crossing is inside the chunk
-                        js = 1 if x < S else int((x - S) / u) // D + 1
+                        js = 1 if x < S else int((x - S) * iu) // D + 1
                         return S + (js * D) * u, done + js
                     S = S + (j * D) * u
                     done += j
@@ -81,6 +102,22 @@ def test_ff_run_equals_sequential_sum(seed):
             assert ff_run(S, y, m, x) == seq_sum(S, y, m, x), (S, y, m, x)
 
 
+def test_ff_run_cached_binade_reuse():
+    """One cache across many runs of the same term (as a pass uses it), interleaved with other
+    additions: the same sums as the plain sequence."""
+    rng = random.Random(5)
+    for y in (1.0, 1 / 3, 1.0 / 70_001, 0.1, 2 ** -20 * 3):
+        bc = Binade()
+        S = S2 = 0.0
+        for _ in range(400):
+            m = rng.choice([1, 2, 5, 40, 300, rng.randint(1, 5000)])
+            S, _ = ff_run(S, y, m, math.inf, bc)
+            S2, _ = seq_sum(S2, y, m)
+            assert S == S2
+            z = rng.choice([y * 4, y * 0.25, y * 3, y / 3])
+            S, S2 = S + z, S2 + z
+
+
 def test_ff_run_ties():
     """Terms with few significant bits reach binades where y sits exactly half an ulp off the
     grid: the rounding alternates to the even neighbour."""
@@ -99,10 +136,11 @@ def seq_pass(specials, n, one, x=math.inf, hi=None):
     or None); hi defaults to n."""
     hi = n if hi is None else hi
     S, i = 0.0, 0
+    bc = Binade()
     for pos, val in list(specials) + [(n, None)]:
         end = min(pos, hi)
         if end > i:                            # the run of ``one`` over [i, end)
-            S, j = ff_run(S, one, end - i, x)
+            S, j = ff_run(S, one, end - i, x, bc)
             if j:
                 return S, i + j - 1
         if pos >= hi or val is None:
