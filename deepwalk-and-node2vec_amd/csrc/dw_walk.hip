@@ -1497,17 +1497,133 @@ __device__ int64_t runs_pass(PosList P, int64_t C, int64_t pt, double vp, double
     }
 }
 
+// runs_pass for long lists (tests/test_serial_runs.py seq_pass_bs): inside one binade of S
+// (ulp u, none of `one` / vq a tie or above its bottom) every addition adds a fixed number of
+// ulps, D1 for a one and Dq for a special, so k(t) = S / u after the elements [i, t) is
+// k0 + D1 (ones) + Dq (specials) — increasing in t. The binade's end and the crossing of x are
+// then a binary search over P and a division in the run of ones before the special found; the
+// element that leaves the binade, t's position and any tie are added as they are. O(binades x
+// log C) loads per pass (~20 binades from the first term to the sum) instead of O(C).
+__device__ __forceinline__ int64_t k_mul_sat(int64_t d, int64_t c) {   // d, c >= 0; capped 2^60
+    return (c > 0 && d > (int64_t(1) << 60) / c) ? (int64_t(1) << 60) : d * c;
+}
+
+__device__ int64_t runs_pass_bs(PosList P, int64_t C, int64_t pt, double vp, double vq,
+                                int64_t n, int64_t hi, double one, double x, double &S,
+                                uint32_t &loads) {
+    const uint32_t unit = P.wide ? 2u : 1u;
+    S = 0.0;
+    int64_t i = 0, j = 0;
+    bool p_left = pt >= 0;
+    const int64_t KT = int64_t(1) << 53;
+    while (i < hi) {
+        const int64_t seg_end = (p_left && pt < hi) ? pt : hi;
+        if (S > 0.0 && i < seg_end) {
+            const int e =
+                static_cast<int>((__double_as_longlong(S) >> 52) & 0x7FF) - 1022;   // S in [2^(e-1), 2^e)
+            const double u = ldexp(1.0, e - 53), iu = ldexp(1.0, 53 - e);
+            const double B = ldexp(1.0, e - 1);
+            int64_t D1 = 0, Dq = 0;
+            bool ok = one < B && vq < B;
+            if (ok) {
+                const double q1 = floor(one * iu), r1 = one - q1 * u;
+                const double qq = floor(vq * iu), rq = vq - qq * u;
+                ok = r1 != 0.5 * u && rq != 0.5 * u;
+                D1 = static_cast<int64_t>(q1) + (r1 > 0.5 * u ? 1 : 0);
+                Dq = static_cast<int64_t>(qq) + (rq > 0.5 * u ? 1 : 0);
+                ok = ok && D1 > 0 && Dq > 0;
+            }
+            if (ok) {
+                const int64_t k0 = static_cast<int64_t>(S * iu);
+                const bool xin = x < 2.0 * B;   // (x >= S >= B: x on this binade's grid)
+                const int64_t XT = xin ? static_cast<int64_t>(x * iu) : KT;
+                const int64_t LIM = XT < KT ? XT : KT;
+                auto k_after = [&](int64_t jj) -> int64_t {   // k after special jj (>= j)
+                    const int64_t pj = P[jj];
+                    loads += unit;
+                    return k0 + k_mul_sat(D1, pj + 1 - i - (jj + 1 - j)) +
+                           k_mul_sat(Dq, jj + 1 - j);
+                };
+                int64_t lo = j, up = C;   // jc: the first special at or past seg_end
+                while (lo < up) {
+                    const int64_t mid = (lo + up) >> 1;
+                    loads += unit;
+                    if (P[mid] < seg_end)
+                        lo = mid + 1;
+                    else
+                        up = mid;
+                }
+                const int64_t jc = lo;
+                lo = j, up = jc;          // jf: the first special whose k passes LIM
+                while (lo < up) {
+                    const int64_t mid = (lo + up) >> 1;
+                    if (k_after(mid) > LIM)
+                        up = mid;
+                    else
+                        lo = mid + 1;
+                }
+                const int64_t jf = lo;
+                const int64_t t0 = jf > j ? P[jf - 1] + 1 : i;
+                const int64_t kb = jf > j ? k_after(jf - 1) : k0;
+                const int64_t nxt = jf < jc ? P[jf] : seg_end;
+                const int64_t run = nxt - t0;   // the ones before special jf
+                const int64_t fit = (LIM - kb) / D1;
+                const int64_t m = run < fit ? run : fit;
+                if (xin && m < run && kb + D1 * (m + 1) <= KT) {   // a one crosses x
+                    S = static_cast<double>(kb + D1 * (m + 1)) * u;
+                    return t0 + m;
+                }
+                if (xin && m == run && jf < jc) {
+                    const int64_t kf = k_after(jf);
+                    if (kf <= KT) {                                  // special jf crosses x
+                        S = static_cast<double>(kf) * u;
+                        return nxt;
+                    }
+                }
+                if (t0 + m > i) {   // progress inside the binade
+                    S = static_cast<double>(kb + D1 * m) * u;
+                    i = t0 + m;
+                    j = jf;
+                    continue;
+                }
+            }
+        }
+        // one element as it is
+        double val = one;
+        if (p_left && pt == i) {
+            val = vp;
+            p_left = false;
+        } else if (j < C) {
+            loads += unit;
+            if (P[j] == i) {
+                val = vq;
+                ++j;
+            }
+        }
+        S = S + val;
+        if (S > x) return i;
+        ++i;
+    }
+    return -1;
+}
+
 // The reference's pick over N(v) (n neighbours; t at pt or -1; the 1/q neighbours at P), by
 // its own fp64 arithmetic: the serial replay the margin tests fall back to.
+constexpr int64_t RUNS_BS_MIN = 48;   // lists longer than this: by binades
 __device__ int64_t n2v_pick_serial_runs(PosList P, int64_t C, int64_t pt, int64_t n, double U,
                                         double ip, double iq, uint32_t &loads) {
     const double inf = __builtin_huge_val();
     double s, total, S;
-    runs_pass(P, C, pt, ip, iq, n, n, 1.0, inf, s, loads);            // sum(w)
+    // (short lists run by run; long ones by binades)
+    auto pass = [&](double vp, double vq, int64_t hi, double one, double x, double &out) {
+        return C > RUNS_BS_MIN ? runs_pass_bs(P, C, pt, vp, vq, n, hi, one, x, out, loads)
+                               : runs_pass(P, C, pt, vp, vq, n, hi, one, x, out, loads);
+    };
+    pass(ip, iq, n, 1.0, inf, s);                                      // sum(w)
     const double n1 = 1.0 / s, np = ip / s, nq = iq / s;              // normalized
-    runs_pass(P, C, pt, np, nq, n, n, n1, inf, total, loads);         // accumulate
+    pass(np, nq, n, n1, inf, total);                                  // accumulate
     total = total + 0.0;
-    const int64_t k = runs_pass(P, C, pt, np, nq, n, n - 1, n1, U * total, S, loads);
+    const int64_t k = pass(np, nq, n - 1, n1, U * total, S);
     return k < 0 ? n - 1 : k;                                         // bisect_right(.., 0, n-1)
 }
 

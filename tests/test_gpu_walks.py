@@ -735,6 +735,47 @@ def test_n2v_positions_serial_picks_vs_oracle(p, q, which, hip_device):
     np.testing.assert_array_equal(wave, ref)
 
 
+@pytest.mark.parametrize('p,q', [(0.25, 4.0), (0.3, 3.0)])
+def test_n2v_serial_pick_long_common_list(p, q, hip_device):
+    """Twin hubs A, B sharing 70,000 leaves (and the edge A - B): a step B <- A has C = 70,000
+    common positions (int32 lists, deg(B) > 65,536). Walks A -> B with the second draw exactly
+    on class boundaries of that step: the serial picks run by binades (runs_pass_bs) and equal
+    the oracle's replay bit for bit; the walks' other steps too."""
+    from shallow_encoders.graph.rmat import csr_from_edges
+    n_leaves = 70_000
+    A, B = 0, n_leaves + 1
+    edges = ([(A, i) for i in range(1, n_leaves + 1)] + [(B, i) for i in range(1, n_leaves + 1)]
+             + [(A, B)])
+    rng = np.random.default_rng(5)
+    chords = rng.integers(1, n_leaves + 1, size=(20_000, 2))
+    edges += [(int(a), int(b)) for a, b in chords if a != b]
+    edges = sorted({(min(a, b), max(a, b)) for a, b in edges})
+    csr = csr_from_edges(n_leaves + 2, np.asarray(edges, dtype=np.int64))
+    col = csr.host_col()
+    a_id, b_id = A + 1, B + 1                          # vocab ids
+    ra = slice(int(csr.row_ptr[a_id]), int(csr.row_ptr[a_id + 1]))
+    pos_b = int(np.nonzero(col[ra] == b_id)[0][0])
+    deg_a = ra.stop - ra.start
+    g = walk_ref.CSR(csr.row_ptr, col, None)
+    L, n = 5, 48
+    starts = np.full(n, a_id, dtype=np.int32)
+    u = rng.random((n, L - 1))
+    u[:, 0] = (pos_b + 0.5) / deg_a                     # A -> B
+    nbrs, wt = walk_ref.node2vec_weights(g, a_id, b_id, p, q)
+    cum = np.cumsum(np.asarray(wt, dtype=np.float64))
+    for w in range(n):                                  # B's step on exact class boundaries
+        k = int(rng.integers(0, len(nbrs) - 1))
+        u[w, 1] = float(np.sum(wt[:k + 1])) / float(np.sum(wt)) if w % 2 == 0 else \
+            float(cum[k]) / float(cum[-1])
+    wlk = Node2Vec(csr, L, p=p, q=q, device=hip_device)
+    got = wlk.walk_batch(torch.as_tensor(starts), uniforms=u).cpu().numpy()
+    assert (got[:, 1] == b_id).all()
+    ref = walk_ref.walks_replay(g, starts, L, 'node2vec', p, q, u)
+    np.testing.assert_array_equal(got, ref)
+    c = wlk.count_replay_traffic(torch.as_tensor(starts), torch.from_numpy(u).to(hip_device))
+    assert c['probes'] > 0, c
+
+
 @pytest.mark.parametrize('p,q', [(0.25, 4.0), (1.0, 1.0)])
 def test_n2v_positions_equal_wave_walker_c3(p, q, hip_device, monkeypatch):
     """C3's graph (R-MAT 20, hubs of 44,848): the position walker gives the wave walker's walks

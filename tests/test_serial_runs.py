@@ -152,6 +152,17 @@ def seq_pass(specials, n, one, x=math.inf, hi=None):
     return S, None
 
 
+def runs_pick_bs(P, pt, n, U, ip, iq):
+    """runs_pick with the binade passes (the device's form for lists longer than 48)."""
+    P = [int(i) for i in P]
+    s, _ = seq_pass_bs(P, pt, ip, iq, n, 1.0)
+    n1, np_, nq = 1.0 / s, ip / s, iq / s
+    total, _ = seq_pass_bs(P, pt, np_, nq, n, n1)
+    total = total + 0.0
+    _, hit = seq_pass_bs(P, pt, np_, nq, n, n1, U * total, hi=n - 1)
+    return n - 1 if hit is None else hit
+
+
 def runs_pick(P, pt, n, U, ip, iq):
     """The reference's pick (node2vec_weights + sum + choices) over N(v) whose weights are 1
     except ip at position pt (-1: none) and iq at the ascending positions P, in O(len(P))
@@ -171,7 +182,7 @@ def test_runs_pick_equals_choices(seed):
     rng = np.random.default_rng(seed)
     for _ in range(150):
         n = int(rng.choice([1, 2, 3, 10, 64, 1000, 5000, 70_000]))
-        C = int(rng.integers(0, min(n, 40) + 1))
+        C = int(rng.integers(0, min(n, int(rng.choice([40, 40, 3000]))) + 1))
         P = np.sort(rng.choice(n, C, replace=False)) if C else np.zeros(0, np.int64)
         pt = -1
         if rng.random() < 0.7 and C < n:
@@ -190,6 +201,7 @@ def test_runs_pick_equals_choices(seed):
         for U in [rng.random(), 0.0, 1 - 2 ** -53] + [float(rng.random()) for _ in range(2)]:
             exp = walk_ref.choices_index(normalized, U)
             assert runs_pick(P, pt, n, U, ip, iq) == exp, (n, C, pt, p, q, U)
+            assert runs_pick_bs(P, pt, n, U, ip, iq) == exp, (n, C, pt, p, q, U)
         # uniforms exactly on the cumulative boundaries (where the fast margin declines)
         cum = np.cumsum(np.asarray(normalized, dtype=np.float64))
         for k in rng.integers(0, n, 3):
@@ -197,3 +209,121 @@ def test_runs_pick_equals_choices(seed):
             U = min(U, 1 - 2 ** -53)
             exp = walk_ref.choices_index(normalized, U)
             assert runs_pick(P, pt, n, U, ip, iq) == exp
+            assert runs_pick_bs(P, pt, n, U, ip, iq) == exp
+
+
+# ---- the closed form per binade with a binary search over the specials (long lists) --------
+def _consts(S, vals):
+    """Binade constants when every value adds a fixed number of ulps in S's binade: (u, iu,
+    KT, [D per value]) or None (S == 0, a value >= the binade's bottom, or a tie)."""
+    if S <= 0.0:
+        return None
+    f, e = math.frexp(S)
+    u, iu = math.ldexp(1.0, e - 53), math.ldexp(1.0, 53 - e)
+    B = math.ldexp(1.0, e - 1)
+    Ds = []
+    for y in vals:
+        if y >= B:
+            return None
+        q = math.floor(y * iu)
+        r = y - q * u
+        if r == 0.5 * u:
+            return None
+        Ds.append(q + (1 if r > 0.5 * u else 0))
+    return u, iu, 2 ** 53, Ds
+
+
+def seq_pass_bs(P, pt, vp, vq, n, one, x=math.inf, hi=None):
+    """seq_pass over (P: ascending 1/q positions, pt: the 1/p position or -1) by binades: inside
+    one, k(t) = S / u after the elements [i, t) is k0 + D1 ones + Dq specials — increasing in
+    t — so the binade's end and the crossing of x are found by a binary search over P and a
+    division in the run of ones before it; the element that leaves the binade is added as it
+    is. pt is added singly. Same (S, index) as seq_pass (dw_walk.hip runs_pass_bs)."""
+    hi = n if hi is None else hi
+    C = len(P)
+    S, i, j = 0.0, 0, 0
+    p_left = pt >= 0
+    while i < hi:
+        cs = _consts(S, (one, vq))
+        seg_end = pt if (p_left and pt < hi) else hi
+        if cs is not None and i < seg_end:
+            u, iu, KT, (D1, Dq) = cs
+            k0 = int(S * iu)
+            XT = int(x * iu) if x < math.ldexp(KT, 0) * u else None   # x inside the binade
+
+            def k_after(jj):      # k after special jj (j <= jj), counting from i
+                return k0 + D1 * (P[jj] + 1 - i - (jj + 1 - j)) + Dq * (jj + 1 - j)
+            # specials of this segment: P[j .. jc)
+            lo_, hi_ = j, C
+            while lo_ < hi_:
+                mid = (lo_ + hi_) // 2
+                if P[mid] < seg_end:
+                    lo_ = mid + 1
+                else:
+                    hi_ = mid
+            jc = lo_
+            LIM = KT if XT is None else min(KT, XT)   # the first special past LIM stops
+            # first special index in [j, jc) with k_after > LIM
+            lo_, hi_ = j, jc
+            while lo_ < hi_:
+                mid = (lo_ + hi_) // 2
+                if k_after(mid) > LIM:
+                    hi_ = mid
+                else:
+                    lo_ = mid + 1
+            jf = lo_
+            t0 = P[jf - 1] + 1 if jf > j else i
+            kb = k_after(jf - 1) if jf > j else k0
+            run = (P[jf] if jf < jc else seg_end) - t0          # ones before special jf
+            # ones of that run that keep k <= LIM
+            m = min(run, (LIM - kb) // D1)
+            if XT is not None and m < run and kb + D1 * (m + 1) <= KT:
+                # the (m+1)-th one crosses x inside the binade
+                S = (kb + D1 * (m + 1)) * u
+                return S, t0 + m
+            if XT is not None and m == run and jf < jc and k_after(jf) <= KT:
+                S = k_after(jf) * u                             # special jf crosses x
+                return S, P[jf]
+            t = t0 + m
+            if t > i:                                           # progress inside the binade
+                S = (kb + D1 * m) * u
+                i, j = t, jf
+                continue
+        # one element as it is
+        if p_left and pt == i:
+            val = vp
+            p_left = False
+        elif j < C and P[j] == i:
+            val = vq
+            j += 1
+        else:
+            val = one
+        S = S + val
+        if S > x:
+            return S, i
+        i += 1
+    return S, None
+
+
+@pytest.mark.parametrize('seed', range(8))
+def test_binade_pass_equals_sequential(seed):
+    rng = np.random.default_rng(seed)
+    for _ in range(120):
+        n = int(rng.choice([1, 2, 5, 64, 1000, 20_000, 200_000]))
+        C = int(rng.integers(0, min(n, int(rng.choice([5, 60, 3000]))) + 1))
+        P = np.sort(rng.choice(n, C, replace=False)).tolist() if C else []
+        pt = -1
+        if rng.random() < 0.7 and C < n:
+            cand = int(rng.integers(0, n))
+            while cand in set(P[:0]) or cand in P:
+                cand = int(rng.integers(0, n))
+            pt = cand
+        one = float(rng.choice([1.0, 1 / n, 1 / (n + 3), 0.1, 1 / 3]))
+        vq = one * float(rng.choice([0.25, 4.0, 1 / 3, 3.0, 2.0, 0.7]))
+        vp = one * float(rng.choice([4.0, 0.25, 10 / 3, 1.0]))
+        sp = sorted([(i, vq) for i in P] + ([(pt, vp)] if pt >= 0 else []))
+        S_ref, _ = seq_pass(sp, n, one)
+        assert seq_pass_bs(P, pt, vp, vq, n, one) == (S_ref, None)
+        for x in [S_ref * float(rng.random()) for _ in range(3)] + [S_ref, S_ref * 0.5]:
+            for hi in (n, max(n - 1, 0)):
+                assert seq_pass_bs(P, pt, vp, vq, n, one, x, hi) == seq_pass(sp, n, one, x, hi)
