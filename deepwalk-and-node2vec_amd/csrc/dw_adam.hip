@@ -86,6 +86,49 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// k_adam with the gradient read from a deterministic-mode accumulator (DW_EXACT_ADAM): g =
+// fl(acc * 2^-frac) (dw::from_fixed, the conversion pass's rule, so the same floats), acc cleared
+// (ZERO) and the float buffer not touched. One streaming pass where the conversion after pass 1
+// read and wrote every centre's row with atomics.
+template <bool ZERO>
+__global__ void __launch_bounds__(256)
+    k_adam_fixed(const float *p, float *pd, long long *__restrict__ acc, float *__restrict__ m,
+                 float *__restrict__ v, int64_t n, dw::AdamScalars s0, double fi,
+                 const dw_step_scalars *__restrict__ dyn) {
+    const dw::AdamScalars s = dw::step_adam(dyn, s0);
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const float4 *p4 = reinterpret_cast<const float4 *>(p);
+    float4 *pd4 = reinterpret_cast<float4 *>(pd);
+    longlong2 *a2 = reinterpret_cast<longlong2 *>(acc);
+    float4 *m4 = reinterpret_cast<float4 *>(m);
+    float4 *v4 = reinterpret_cast<float4 *>(v);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pp = ld(p4 + i, true), mm = ld(m4 + i, true), vv = ld(v4 + i, true);
+        const longlong2 a0 = a2[2 * i], a1 = a2[2 * i + 1];
+        float g0 = dw::from_fixed(a0.x, fi), g1 = dw::from_fixed(a0.y, fi);
+        float g2 = dw::from_fixed(a1.x, fi), g3 = dw::from_fixed(a1.y, fi);
+        dw::adam_elem(pp.x, g0, mm.x, vv.x, s);
+        dw::adam_elem(pp.y, g1, mm.y, vv.y, s);
+        dw::adam_elem(pp.z, g2, mm.z, vv.z, s);
+        dw::adam_elem(pp.w, g3, mm.w, vv.w, s);
+        st(pd4 + i, pp, true);
+        st(m4 + i, mm, true);
+        st(v4 + i, vv, true);
+        if (ZERO) {
+            a2[2 * i] = make_longlong2(0, 0);
+            a2[2 * i + 1] = make_longlong2(0, 0);
+        }
+    }
+    for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += stride) {
+        float pp = p[i], gg = dw::from_fixed(acc[i], fi);
+        dw::adam_elem(pp, gg, m[i], v[i], s);
+        pd[i] = pp;
+        if (ZERO) acc[i] = 0;
+    }
+}
+
 // ---- lazy exact Adam over selected rows (the touched-row in-table exchange, N > 1) ------------
 // A row that no centre of a batch touched has g = 0 for that step, and torch's update with
 // g = 0 is a fixed recurrence in (p, m, v) driven by the step's scalars. OwnerLazyTables defers
@@ -286,6 +329,27 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
     if (blocks < 1) blocks = 1;
     if (blocks > 8192) blocks = 8192;  // 256 CUs x 8 resident blocks, grid-stride beyond
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+    {   // the deterministic mode's fused conversion (DW_EXACT_ADAM): the sums from the accumulator
+        dw::Fixed fx;
+        int64_t fn = 0;
+        int32_t ffl = 0;
+        if (dw::exact_lookup(grad, &fx, &fn, &ffl) && (ffl & DW_EXACT_ADAM)) {
+            DW_REQUIRE(fn >= n_elem, "dw_adam_dense: the accumulator registered for grad holds "
+                       "%lld elements, the update covers %lld", (long long)fn, (long long)n_elem);
+            DW_REQUIRE(((uintptr_t)fx.acc % 16) == 0, "dw_adam_dense: accumulator alignment");
+            auto *acc = reinterpret_cast<long long *>(fx.acc);
+            if (zero_grad)
+                hipLaunchKernelGGL(k_adam_fixed<true>, dim3((unsigned)blocks), dim3(256), 0,
+                                   dw::as_stream(stream), param_src, param_dst, acc, exp_avg,
+                                   exp_avg_sq, n_elem, s, fx.fi, dw::bound_step_scalars());
+            else
+                hipLaunchKernelGGL(k_adam_fixed<false>, dim3((unsigned)blocks), dim3(256), 0,
+                                   dw::as_stream(stream), param_src, param_dst, acc, exp_avg,
+                                   exp_avg_sq, n_elem, s, fx.fi, dw::bound_step_scalars());
+            DW_LAUNCH_CHECK("dw_adam_dense/fixed");
+            return DW_OK;
+        }
+    }
     if (zero_grad)
         hipLaunchKernelGGL((k_adam<true, true, 2>), dim3((unsigned)blocks), dim3(256), 0,
                            dw::as_stream(stream), param_src, param_dst, grad, exp_avg,

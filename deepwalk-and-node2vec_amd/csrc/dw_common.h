@@ -482,6 +482,10 @@ __device__ __forceinline__ float from_fixed(int64_t a, double fi) {
     return static_cast<float>(static_cast<double>(a) * fi);
 }
 
+// The accumulator registered for gradient buffer g (dw_exact_register): 1 and its Fixed, size
+// and flags, or 0 (dw_sgns.hip).
+int exact_lookup(const float *g, Fixed *fx, int64_t *n, int32_t *flags);
+
 __device__ __forceinline__ void fixed_add(int64_t *dst, int64_t v) {
     if (v) atomicAdd(reinterpret_cast<unsigned long long *>(dst), static_cast<unsigned long long>(v));
 }

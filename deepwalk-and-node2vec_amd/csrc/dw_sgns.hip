@@ -423,6 +423,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
     __shared__ float s_coef[WAVES_PER_BLOCK][4][G16_TMAX];
     __shared__ uint8_t s_t[WAVES_PER_BLOCK][4][OWNER ? G16_TMAX : 1];
     __shared__ float4 s_g[WAVES_PER_BLOCK][4][EXACT ? 1 : 16 * F4];
+    __shared__ int64_t s_gx[WAVES_PER_BLOCK][EXACT ? D : 1];   // EXACT: one centre's sums
     bool range = false;   // EXACT: a term past the fixed-point range
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
@@ -699,13 +700,27 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                 }
             }
         }
-        if constexpr (EXACT) {   // the group's centre, 4 F4 elements per lane
-            if (ok_c && n_own > 0) {
-                int64_t *dst = a.fx_in.acc + cid * D + 4 * gl;
+        if constexpr (EXACT) {
+            // the four centres one after the other through the wave's LDS row: each centre's
+            // sums leave as F4 coalesced 64-lane int64 atomics (512 contiguous bytes each) where
+            // the group's own layout (elements 4 gl + 64 f + k) gave 4 F4 atomics per lane at a
+            // 32-B stride over four centres — a quarter of the cache-line requests
+            const int32_t cq_self = (ok_c && n_own > 0) ? static_cast<int32_t>(cid) : -1;
 #pragma unroll
-                for (int f = 0; f < F4; ++f)
+            for (int qq = 0; qq < 4; ++qq) {
+                const int32_t cq = __builtin_amdgcn_readlane(cq_self, qq * 16);
+                if (cq < 0) continue;
+                if (q == qq) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) dw::fixed_add(dst + 64 * f + k, gx[4 * f + k]);
+                    for (int f = 0; f < F4; ++f)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) s_gx[wv][64 * f + 4 * gl + k] = gx[4 * f + k];
+                }
+                dw::wave_lds_sync();
+                int64_t *dst = a.fx_in.acc + static_cast<int64_t>(cq) * D + lane;
+#pragma unroll
+                for (int f = 0; f < F4; ++f) dw::fixed_add(dst + 64 * f, s_gx[wv][lane + 64 * f]);
+                dw::wave_lds_sync();
             }
             dw::wave_lds_sync();
             continue;
@@ -1218,6 +1233,25 @@ int exact_of(const float *g, int64_t need, dw::Fixed *fx, int32_t *flags, const 
     if (flags) *flags = it->second.flags;
     return DW_OK;
 }
+
+}  // namespace
+
+// (dw_common.h) the registry's entry for a gradient buffer, for the dense Adam's fused conversion
+int dw::exact_lookup(const float *g, dw::Fixed *fx, int64_t *n, int32_t *flags) {
+    *fx = dw::Fixed{};
+    *n = 0;
+    *flags = 0;
+    if (!g) return 0;
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    const auto it = g_exact.find(g);
+    if (it == g_exact.end()) return 0;
+    *fx = dw::Fixed{it->second.acc, ldexp(1.0, it->second.frac), ldexp(1.0, -it->second.frac)};
+    *n = it->second.n;
+    *flags = it->second.flags;
+    return 1;
+}
+
+namespace {
 
 template <bool FROM_WALKS, bool RECORDS>
 int launch_pass1(const SgnsArgs &a, hipStream_t st) {
@@ -1837,7 +1871,7 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
         rc = launch_pass1_g16<FROM_WALKS>(a, st);
         if (rc == DW_E_UNSUPPORTED) rc = launch_pass1<FROM_WALKS, true>(a, st);
         if (rc != DW_OK) return rc;
-        if (a.fx_in.acc && !(fl & DW_EXACT_DEFER)) {   // the centres' exact sums into g_in
+        if (a.fx_in.acc && !(fl & (DW_EXACT_DEFER | DW_EXACT_ADAM))) {   // the centres' exact
             int64_t cb = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
             if (cb > grid_cap(8)) cb = grid_cap(8);
             hipLaunchKernelGGL(k_fixed_centres<FROM_WALKS>, dim3((unsigned)cb),
@@ -2310,7 +2344,7 @@ int launch_owner_pass1(SgnsArgs a, int64_t local_rows, int32_t order_ready, void
         rc = coefin ? launch_pass1_g16<true, true, true>(a, st)
                     : launch_pass1_g16<true, true>(a, st);
         if (rc != DW_OK) return rc;
-        if (a.fx_in.acc && !(fl & DW_EXACT_DEFER)) {   // one rank: the centres' exact sums
+        if (a.fx_in.acc && !(fl & (DW_EXACT_DEFER | DW_EXACT_ADAM))) {   // one rank: the centres' exact sums
             int64_t cb = (a.batch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
             if (cb > grid_cap(8)) cb = grid_cap(8);
             hipLaunchKernelGGL(k_fixed_centres<true>, dim3((unsigned)cb),
@@ -2879,7 +2913,8 @@ int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t 
                       int32_t flags) {
     DW_REQUIRE(grad && acc && n_elems >= 0, "dw_exact_register: bad arguments");
     DW_REQUIRE(frac >= 0 && frac <= 62, "dw_exact_register: frac %d outside [0, 62]", frac);
-    DW_REQUIRE((flags & ~DW_EXACT_DEFER) == 0, "dw_exact_register: unknown flags %d", flags);
+    DW_REQUIRE((flags & ~(DW_EXACT_DEFER | DW_EXACT_ADAM)) == 0,
+               "dw_exact_register: unknown flags %d", flags);
     std::lock_guard<std::mutex> lk(g_exact_mu);
     g_exact[grad] = ExactEntry{acc, n_elems, frac, flags};
     return DW_OK;

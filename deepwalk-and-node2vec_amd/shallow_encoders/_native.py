@@ -33,6 +33,7 @@ DW_S_RECORDS_FULL = 32
 DW_S_DUP_NEIGHBOR = 64
 DW_S_FIXED_RANGE = 128
 DW_EXACT_DEFER = 1
+DW_EXACT_ADAM = 2
 
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1

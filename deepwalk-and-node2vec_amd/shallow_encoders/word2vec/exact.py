@@ -18,7 +18,8 @@ it) and a term stays inside the conversion's 2^51 for entries below 2^19; a term
 DW_S_FIXED_RANGE (OverflowError at the next status check).
 
 Cost: two int64 atomics or adds per term instead of one float FMA, the accumulators (8 B per
-table entry) and one conversion pass over the touched rows; bench.py --deterministic measures it.
+table entry) and one conversion of the sums (on the one-GPU dense path fused into the in-table
+Adam: DW_EXACT_ADAM); bench.py --deterministic measures it.
 Covered: the records (sorted) output path of dw_sgns_walks_phase / dw_sgns_pairs (skip-gram),
 the fused output-table Adam, the owner layout (the centre sums reduce-scattered as int64).
 Not covered (refused): the atomic output scatter, pooled (CBOW) inputs, the replicated N > 1
@@ -48,12 +49,15 @@ class FixedAccumulator:
     ``grad`` (``defer``: the centre sums stay in ``acc`` for the caller's cross-rank reduction,
     then ``convert``)."""
 
-    def __init__(self, grad: torch.Tensor, grad_scale: float, defer: bool = False):
+    def __init__(self, grad: torch.Tensor, grad_scale: float, defer: bool = False,
+                 adam: bool = False):
         if grad.dtype != torch.float32 or not grad.is_contiguous():
             raise TypeError('the gradient buffer must be contiguous float32')
         self.grad = grad
         self.frac = frac_bits(grad_scale)
         self.defer = bool(defer)
+        # DW_EXACT_ADAM: the dense Adam over this buffer reads (and clears) the sums itself
+        self.adam = bool(adam)
         self.acc = torch.zeros(grad.shape, dtype=torch.int64, device=grad.device)
         self._grad_ptr = grad.data_ptr()
         self._ptr = None            # the registered grad pointer while this one is active
@@ -66,7 +70,8 @@ class FixedAccumulator:
         if self._ptr is None:
             _native.call('dw_exact_register', _native.ptr(self.grad), _native.ptr(self.acc),
                          self.grad.numel(), self.frac,
-                         _native.DW_EXACT_DEFER if self.defer else 0)
+                         (_native.DW_EXACT_DEFER if self.defer else 0)
+                         | (_native.DW_EXACT_ADAM if self.adam else 0))
             self._ptr = self._grad_ptr
 
     @property
@@ -115,19 +120,21 @@ class Registry:
         self._cache: Dict[int, List[FixedAccumulator]] = {}          # per key, most recent last
 
     def ensure(self, key: int, grad: torch.Tensor, grad_scale: float,
-               defer: bool = False) -> FixedAccumulator:
+               defer: bool = False, adam: bool = False) -> FixedAccumulator:
+        def same(c):
+            return c.matches(grad, grad_scale) and c.defer == defer and c.adam == adam
         a = self._acc.get(key)
-        if a is not None and a.active and a.matches(grad, grad_scale) and a.defer == defer:
+        if a is not None and a.active and same(a):
             return a
         if a is not None:
             a.release()
         cache = self._cache.setdefault(key, [])
-        hit = next((c for c in cache if c.matches(grad, grad_scale) and c.defer == defer), None)
+        hit = next((c for c in cache if same(c)), None)
         if hit is not None:
             cache.remove(hit)
             hit.activate()
         else:
-            hit = FixedAccumulator(grad, grad_scale, defer)
+            hit = FixedAccumulator(grad, grad_scale, defer, adam)
             while len(cache) >= self.MAX_PER_KEY:
                 cache.pop(0)
         cache.append(hit)

@@ -336,7 +336,10 @@ class ShardedTables:
             raise NotImplementedError('the deterministic mode covers the owner layout at N > 1 '
                                       '(OwnerTables), not the replicated one')
         self._exact = exact.Registry()
-        self._exact.ensure(0, self.grads[0], grad_scale)
+        # the in table's sums converted by its Adam (one streaming pass; _adam_both then
+        # launches the two tables' updates separately)
+        self._exact.ensure(0, self.grads[0], grad_scale,
+                           adam=self._cuda and self.adam_impl is hip_adam)
         self._exact.ensure(1, self.grads[1], grad_scale)
 
     # ---- one table's exchange -------------------------------------------------------------------
@@ -346,7 +349,8 @@ class ShardedTables:
 
     def _adam_both(self) -> None:
         """One device: Adam on both tables in place (one launch when they are adjacent)."""
-        if self.params.shape[0] == 2 and self._cur_in == 0:
+        if (self.params.shape[0] == 2 and self._cur_in == 0
+                and getattr(self, '_exact', None) is None):
             self.adam_impl(self.params.view(-1), self.grads.view(-1), self.m.view(-1),
                            self.v.view(-1), self.step_count, self.lr, self.betas, self.eps,
                            self.weight_decay, True)

@@ -301,6 +301,11 @@ int dw_n2v_edge_records(const int64_t *row_ptr, const int32_t *col, const uint32
  * refused. frac: dw_exact_frac_bits(the launches' grad scale). Host-side registry, keyed by
  * the grad pointer (graph-captured launches keep the accumulator they were captured with). */
 #define DW_EXACT_DEFER 1
+/* (flags, a centre-table buffer of the one-GPU dense path) the dense Adam converts: pass 1 leaves
+ * the centre sums in acc, and dw_adam_dense / dw_adam_dense_to on this buffer read each
+ * gradient as fl(acc * 2^-frac) and clear acc (zero_grad) — one streaming pass instead of a
+ * conversion pass after pass 1. */
+#define DW_EXACT_ADAM 2
 
 /* Row 0 of a lazy Adam history (dw_adam_rows): the box header's tag ("WDBX"). */
 #define DW_HIST_BOX_TAG 0x58424457u
