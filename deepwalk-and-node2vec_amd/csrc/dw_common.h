@@ -478,6 +478,21 @@ __device__ __forceinline__ int64_t to_fixed(float t, double fs, bool &range) {
     return __double_as_longlong(r) - 0x4338000000000000LL;
 }
 
+// to_fixed in three issue slots per term: a run of terms adds the raw bits of fma(t, fs, M)
+// (M = 1.5 * 2^52: the same double as to_fixed's r, since t * fs is exact) and the run's
+// n * bits(M) is subtracted once (fixed_finish) — the same integers, with the int64 sums
+// wrapping harmlessly; the range test runs once on the run's largest |t| (fixed_range).
+__device__ __forceinline__ int64_t fixed_bits(float t, double fs) {
+    return __double_as_longlong(fma(static_cast<double>(t), fs, 6755399441055744.0));
+}
+__device__ __forceinline__ int64_t fixed_finish(int64_t acc, int64_t n_terms) {
+    return static_cast<int64_t>(static_cast<uint64_t>(acc) -
+                                static_cast<uint64_t>(n_terms) * 0x4338000000000000ULL);
+}
+__device__ __forceinline__ bool fixed_range(float tmax, double fs) {
+    return !(static_cast<double>(tmax) * fs < 0x1p51);
+}
+
 __device__ __forceinline__ float from_fixed(int64_t a, double fi) {
     return static_cast<float>(static_cast<double>(a) * fi);
 }

@@ -425,6 +425,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
     __shared__ float4 s_g[WAVES_PER_BLOCK][4][EXACT ? 1 : 16 * F4];
     __shared__ int64_t s_gx[WAVES_PER_BLOCK][EXACT ? D : 1];   // EXACT: one centre's sums
     bool range = false;   // EXACT: a term past the fixed-point range
+    float tmax = 0.f;     // EXACT: the largest |term| (the range test, once at the end)
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int q = lane >> 4, gl = lane & 15;
@@ -631,10 +632,14 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                     const double fs = a.fx_in.fs;
 #pragma unroll
                     for (int f = 0; f < F4; ++f) {
-                        gx[4 * f + 0] += dw::to_fixed(cu * o4[u][f].x, fs, range);
-                        gx[4 * f + 1] += dw::to_fixed(cu * o4[u][f].y, fs, range);
-                        gx[4 * f + 2] += dw::to_fixed(cu * o4[u][f].z, fs, range);
-                        gx[4 * f + 3] += dw::to_fixed(cu * o4[u][f].w, fs, range);
+                        const float t0 = cu * o4[u][f].x, t1 = cu * o4[u][f].y;
+                        const float t2 = cu * o4[u][f].z, t3 = cu * o4[u][f].w;
+                        gx[4 * f + 0] += dw::fixed_bits(t0, fs);
+                        gx[4 * f + 1] += dw::fixed_bits(t1, fs);
+                        gx[4 * f + 2] += dw::fixed_bits(t2, fs);
+                        gx[4 * f + 3] += dw::fixed_bits(t3, fs);
+                        tmax = fmaxf(fmaxf(tmax, fmaxf(fabsf(t0), fabsf(t1))),
+                                     fmaxf(fabsf(t2), fabsf(t3)));
                     }
                     continue;
                 }
@@ -654,6 +659,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
             int32_t rid[CHR];
             load_chunk(o4, rid, t0);
             compute_chunk(o4, rid, t0);
+        }
+        if constexpr (EXACT) {   // every chunk added CHR terms per element
+            const int64_t nt = static_cast<int64_t>((n_loop + CHR - 1) / CHR) * CHR;
+#pragma unroll
+            for (int k = 0; k < 4 * F4; ++k) gx[k] = dw::fixed_finish(gx[k], nt);
         }
         if constexpr (!EXACT) {
 #pragma unroll
@@ -762,8 +772,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
         }
         dw::wave_lds_sync();
     }
-    if constexpr (EXACT)
+    if constexpr (EXACT) {
+        range = range || dw::fixed_range(tmax, a.fx_in.fs);
         if (__ballot(range) && lane == 0) dw::status_or(a.status, DW_S_FIXED_RANGE);
+    }
     if constexpr (OWNER) {
         if (!EXACT && pend_c >= 0) {
             float *dst = a.g_in + static_cast<int64_t>(pend_c) * D + lane;
@@ -893,6 +905,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                  int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch,
                  dw::Fixed fo, int32_t *status) {
     bool fx_range = false;
+    float fx_tmax = 0.f;   // EXACT: the largest |term| (the range test, once at the end)
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t lo = range ? range[0] : 0;
@@ -923,9 +936,12 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
             gx[m] = 0;
         }
 
+        int64_t nt = 0;   // EXACT: the terms added to gx since the row began
         auto flush = [&](uint32_t row) {
             float *dst = g_out + static_cast<int64_t>(row) * d + lane;
             if constexpr (EXACT) {
+#pragma unroll
+                for (int m = 0; m < VPL; ++m) gx[m] = dw::fixed_finish(gx[m], nt);
                 if (row == before || row == after) {   // the integer part of a straddling row
                     int64_t *acc = fo.acc + static_cast<int64_t>(row) * d + lane;
 #pragma unroll
@@ -983,25 +999,32 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                 if (k[u] != cur) {
                     flush(cur);
                     cur = k[u];
+                    nt = 0;
 #pragma unroll
                     for (int m = 0; m < VPL; ++m) {
                         g[m] = 0.f;
                         gx[m] = 0;
                     }
                 }
+                ++nt;
 #pragma unroll
                 for (int m = 0; m < VPL; ++m) {
-                    if constexpr (EXACT)
-                        gx[m] += dw::to_fixed(coef[u] * x[u][m], fo.fs, fx_range);
-                    else
+                    if constexpr (EXACT) {
+                        const float t = coef[u] * x[u][m];
+                        gx[m] += dw::fixed_bits(t, fo.fs);
+                        fx_tmax = fmaxf(fx_tmax, fabsf(t));
+                    } else {
                         g[m] += coef[u] * x[u][m];
+                    }
                 }
             }
         }
         flush(cur);
     }
-    if constexpr (EXACT)
+    if constexpr (EXACT) {
+        fx_range = fx_range || dw::fixed_range(fx_tmax, fo.fs);
         if (__ballot(fx_range) && lane == 0) dw::status_or(status, DW_S_FIXED_RANGE);
+    }
 }
 
 // Deterministic mode, after k_rec_gather: the rows that straddle chunks hold their sums in the
@@ -1489,6 +1512,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo) {
     constexpr int D = 64 * F4;
     bool fx_range = false;
+    float fx_tmax = 0.f;   // EXACT: the largest |term| (the range test, once at the end)
     constexpr int RU = 4;   // records per round (one per 16-lane group)
     __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
     __shared__ float4 s_p[WAVES_PER_BLOCK][D / 4];        // the row's p^{s-1}
@@ -1628,8 +1652,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     const float *cr = reinterpret_cast<const float *>(&s_c[wv][u][0]);
                     if constexpr (EXACT) {
 #pragma unroll
-                        for (int f = 0; f < F4; ++f)
-                            gx[f] += dw::to_fixed(cu * cr[lane + 64 * f], fo.fs, fx_range);
+                        for (int f = 0; f < F4; ++f) {
+                            const float t = cu * cr[lane + 64 * f];
+                            gx[f] += dw::fixed_bits(t, fo.fs);
+                            fx_tmax = fmaxf(fx_tmax, fabsf(t));
+                        }
                     } else {
 #pragma unroll
                         for (int f = 0; f < F4; ++f) g[f] += cu * cr[lane + 64 * f];
@@ -1638,6 +1665,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                 dw::wave_lds_sync();   // s_c is rewritten next round
             }
             if constexpr (EXACT) {
+#pragma unroll
+                for (int f = 0; f < F4; ++f) gx[f] = dw::fixed_finish(gx[f], cnt);   // cnt terms
                 if (straddle) {
 #pragma unroll
                     for (int f = 0; f < F4; ++f) dw::fixed_add(fo.acc + ro + 64 * f, gx[f]);
@@ -1670,8 +1699,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
         }
         dw::wave_lds_sync();   // s_rs is rewritten by the next chunk
     }
-    if constexpr (EXACT)
+    if constexpr (EXACT) {
+        fx_range = fx_range || dw::fixed_range(fx_tmax, fo.fs);
         if (__ballot(fx_range) && lane == 0) dw::status_or(a.status, DW_S_FIXED_RANGE);
+    }
     if (a.loss_acc) flush_loss(a.loss_acc, acc_pos, acc_neg, acc_rec, acc_prec);
 }
 
