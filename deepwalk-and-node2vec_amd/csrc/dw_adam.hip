@@ -115,7 +115,9 @@ __global__ void __launch_bounds__(256)
         st(pd4 + i, pp, true);
         st(m4 + i, mm, true);
         st(v4 + i, vv, true);
-        if (ZERO) {
+        // (cleared only where a sum was left: most rows are no centre of the step, and their
+        // zeros need no store — a third of the update's writes)
+        if (ZERO && ((a0.x | a0.y | a1.x | a1.y) != 0)) {
             a2[2 * i] = make_longlong2(0, 0);
             a2[2 * i + 1] = make_longlong2(0, 0);
         }

@@ -437,7 +437,9 @@ class ShardedTables:
         self._next_in = 2 - self._cur_in
         if not self.multi:
             def adam_to(_async):
-                blocks = overlap_adam_blocks(self.V_pad * self.d * 4 * 7, overlap_bytes)
+                # (the deterministic mode's update reads and clears the 8-B sums instead of g)
+                per = 4 * 7 + (8 if getattr(self, '_exact', None) is not None else 0)
+                blocks = overlap_adam_blocks(self.V_pad * self.d * per, overlap_bytes)
                 hip_adam_to(self.params[self._cur_in], self.params[self._next_in],
                             self.grads[0], self.m[0], self.v[0], self.step_count, self.lr,
                             self.betas, self.eps, self.weight_decay, True, blocks)
