@@ -66,6 +66,10 @@ __global__ void __launch_bounds__(256)
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i < n4) {
+                // g is re-zeroed only where its bits are not all +0: a sparse step's untouched
+                // rows (most of the in table at C3) need no store — the same bits either way
+                const bool dirty = (__float_as_uint(gg[u].x) | __float_as_uint(gg[u].y) |
+                                    __float_as_uint(gg[u].z) | __float_as_uint(gg[u].w)) != 0u;
                 dw::adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, s);
                 dw::adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, s);
                 dw::adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, s);
@@ -73,7 +77,7 @@ __global__ void __launch_bounds__(256)
                 st(pd4 + i, pp[u], NTS);
                 st(m4 + i, mm[u], NTS);
                 st(v4 + i, vv[u], NTS);
-                if (ZERO) st(g4 + i, make_float4(0.f, 0.f, 0.f, 0.f), NTS);
+                if (ZERO && dirty) st(g4 + i, make_float4(0.f, 0.f, 0.f, 0.f), NTS);
             }
         }
     }
