@@ -2793,8 +2793,10 @@ __global__ void __launch_bounds__(256)
     if (threadIdx.x == 0) sums[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
+// The counts are cleared here once read (coalesced, the tile's own lines) — the step's kernels
+// then leave them alone, where each stepped row's reset was a scattered 4-B write.
 __global__ void __launch_bounds__(256)
-    k_place_scan(const uint32_t *__restrict__ counts, int64_t n, const uint32_t *__restrict__ sums,
+    k_place_scan(uint32_t *__restrict__ counts, int64_t n, const uint32_t *__restrict__ sums,
                  uint32_t *__restrict__ off, int64_t *__restrict__ range) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_base;
@@ -2815,6 +2817,9 @@ __global__ void __launch_bounds__(256)
         c[k] = a + k < n ? counts[a + k] : 0u;
         t += c[k];
     }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (c[k] != 0u) counts[a + k] = 0u;
     uint32_t x = t;   // inclusive wave scan
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -3265,7 +3270,8 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
     oa.p_current = (flags & 2) != 0;
     oa.betas_const = (flags & 4) != 0;
-    oa.counts = (flags & 1) ? counts : nullptr;
+    oa.counts = nullptr;   // (placed records: the catch-up's scan cleared the counts)
+    (void)counts;
     const int rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_pass2_lazy");
     if (rc != DW_OK) return rc;
     const int64_t T = 2 * (int64_t)context_radius * (1 + neg_samples);
@@ -3320,7 +3326,8 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
                          "dw_sgns_owner_out_rows", vocab_size, nullptr, &pl);
     if (rc != DW_OK) return rc;
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
-    oa.counts = counts;   // (p_current false: k_lazy_boundary replays the straddling rows whole)
+    (void)counts;   // (cleared by the placement scan; p_current false: k_lazy_boundary replays
+                    // the straddling rows whole)
     oa.pend = pending;    // the stepped rows are left pending (p at step - 1 for the centre pass)
     rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;

@@ -543,8 +543,8 @@ int dw_sgns_owner_pass2(int64_t n_walks, int32_t walk_length, int32_t context_ra
  * row is listed once per step, claimed via atomicMax(claim[row], step), when its last claim is
  * older than step - 1; rows_buf uint32 [min(local_rows, B' * 2R(1+K))] and n_rows (int64,
  * device) receive the list, which is then replayed. flags (a bit set):
- *   1 = place the records: counts uint32 [local_rows + 1] (zero-initialised; the lazy gather
- *       clears the rows it steps, so it is zero between steps) counts every row's slots, each
+ *   1 = place the records: counts uint32 [local_rows + 1] (zero-initialised; the placement
+ *       scan clears it once read, so it is zero between steps) counts every row's slots, each
  *       slot's rank among them and the exclusive scan of the counts go to `workspace` (the owner
  *       form's, dw_sgns_owner_workspace_bytes), for dw_sgns_owner_pass1 (order_ready | 2) and
  *       dw_sgns_owner_pass2_lazy (flags | 1, the same counts): the records land grouped by row,
@@ -573,7 +573,7 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
  * (dw_adam_rows with rows = NULL). last_step int32 [local_rows]: the step each row is current
  * to; step: this step (>= 1). torch.optim.Adam semantics (config_parser/core.py:43-53).
  * flags: 1 = the records were placed (see dw_sgns_owner_out_catch_up; n_records NULL; counts:
- * its row counts, cleared here as the rows step), 2 = the catch-up replayed p only (m, v are
+ * its row counts, already cleared by its scan), 2 = the catch-up replayed p only (m, v are
  * replayed here), 4 = every step so far had the same betas (those replays use this step's). */
 int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t context_radius,
                              int32_t neg_samples, int64_t local_rows, int32_t dim,
@@ -609,8 +609,9 @@ int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t wal
  * pending[row] = 1 (uint8 [local_rows], zero-initialised by the caller). The parameter half of
  * a pending row's step (torch Adam's p update from its m and v, the same operations) is applied
  * when the row is next replayed — by the next rows-major step, or by dw_adam_rows given the same
- * `pending` (the flush before the table is read whole). counts: the catch-up's, cleared as the
- * rows step. dim in {64, 128, 256, 512}, 2R(1+K) <= 64; no deterministic form. */
+ * `pending` (the flush before the table is read whole). counts: the catch-up's (already cleared
+ * by its placement scan; not written here). dim in {64, 128, 256, 512}, 2R(1+K) <= 64; the
+ * deterministic mode (g_out registered) sums each row's terms as integers. */
 int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                            int32_t context_radius, int32_t neg_samples, int64_t vocab_size,
                            int32_t dim, int32_t owner, int32_t n_owners, int64_t local_rows,
