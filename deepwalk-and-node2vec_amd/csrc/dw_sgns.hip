@@ -889,7 +889,7 @@ __device__ __forceinline__ void lazy_row_step(const OutAdam &oa, int32_t step, u
     if (lane == 0) {
         oa.last[row] = step;
         if (oa.counts) oa.counts[row] = 0u;   // placed records: the count back to zero
-        if (oa.pend) oa.pend[row] = 1;
+        if (oa.pend && !pd) oa.pend[row] = 1;   // (already 1 where it was pending)
     }
 }
 
@@ -1692,7 +1692,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                 }
                 if (lane == 0) {
                     oa.last[row] = step;
-                    oa.pend[row] = 1;
+                    if (!pd) oa.pend[row] = 1;   // (already 1 where the row was pending)
                     if (oa.counts) oa.counts[row] = 0u;
                 }
             }
