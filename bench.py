@@ -180,8 +180,9 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
     The one-GPU composition bench.py takes for that shape (`--batch-walks 64`): OwnerLazyTables
     on one rank with the lazy exact Adam of both tables (only the rows a step touches are read
     and updated; deferred g = 0 steps replayed bit-exactly), the records placed by the claim and
-    the rows-major out step, replayed as HIP graphs of 16 steps (GraphedOwnerStep) with the
-    Philox walker in front. After the timed replays one more step is run eagerly from a
+    the rows-major out step, replayed as HIP graphs of 16 pipelined steps (GraphedOwnerStep /
+    owner_lazy_steps: the next step's placement and in-row catch-up beside this one) with the
+    Philox walker in front; `--deterministic` runs it with the integer sums. After the timed replays one more step is run eagerly from a
     flushed pre-state and checked on ~256 in and ~256 out rows against the float64 restatement
     (word2vec/verify.py; the parity tests' single-step bars); a miss fails the bench.
 

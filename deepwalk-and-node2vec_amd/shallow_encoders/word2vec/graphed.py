@@ -195,6 +195,10 @@ class GraphedOwnerStep:
     The tables' Adam-scalar history is written ahead for ``n_steps`` steps before the capture,
     so begin_step copies nothing inside it.
 
+    With the rows-major out step on one rank (OwnerLazyTables.pipeline_ok) the captured steps are
+    pipelined (sharding.owner_lazy_steps): step k + 1's out-record placement, touch claim and
+    catch-up run on side streams beside step k, and the graph's first step prepares its own.
+
     The tables must have run one eager step at this batch shape first (it allocates the
     touched-row, gather and workspace buffers the capture then reuses); the walker's device
     tensors are built here by one eager launch into a scratch buffer, and its walk-id counter
