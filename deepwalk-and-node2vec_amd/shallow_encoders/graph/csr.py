@@ -192,7 +192,8 @@ class CSRGraph:
                        need_adj: bool = False, need_adj_pos: bool = False,
                        need_hub_bits: bool = False,
                        need_edge_cn: bool = False,
-                       need_n2v_index: bool = False) -> Dict[str, torch.Tensor]:
+                       need_n2v_index: bool = False,
+                       n2v_budget: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """Copy the CSR to HBM once (and derive col_sorted / alias tables / the edge-inline CSR /
         the per-row adjacency hash / its slots' neighbour positions on the device)."""
         dev = _native.require_device(device)
@@ -246,8 +247,14 @@ class CSRGraph:
                              _native.ptr(d['hub_bits']), d['hub_words'], self.vocab_size,
                              self.nnz, _native.ptr(cn), _native.stream(dev))
             d['edge_cn'] = cn
-        if need_n2v_index and 'n2v_rec' not in d:
-            self._build_n2v_index(dev)
+        if need_n2v_index:
+            info = d.get('n2v_index_info') or {}
+            # (a skipped index is tried again under a larger budget: the Philox walker asks with
+            # a small one, the exact walker with the default)
+            if 'n2v_rec' not in d or (d['n2v_rec'] is None and
+                                      self._n2v_budget(dev, n2v_budget) > info.get('budget', 0)
+                                      and not info.get('unsupported')):
+                self._build_n2v_index(dev, n2v_budget)
         return d
 
     # the position index is built when its entries, records and build scratch fit this many
@@ -257,8 +264,22 @@ class CSRGraph:
     N2V_INDEX_RESERVE = 16 << 30
     # entries sorted per build launch (the scratch: 8 B each plus the sort's storage)
     N2V_CHUNK_ENTRIES = 1 << 28
+    # the Philox walker's budget: it has the rejection walker to fall back on, so it builds the
+    # index only where it is small next to the device (C3's 4 GB, not C5's 150: that memory
+    # belongs to the training tables)
+    N2V_PHILOX_INDEX_BYTES = 32 << 30
 
-    def _build_n2v_index(self, dev) -> None:
+    def _n2v_budget(self, dev, budget: Optional[int]) -> int:
+        """The byte budget of the position index: ``budget`` (None: N2V_INDEX_BYTES), capped at
+        the device's free memory less N2V_INDEX_RESERVE; DW_N2V_INDEX_BYTES overrides both."""
+        import os
+        env = os.environ.get('DW_N2V_INDEX_BYTES')
+        if env is not None:
+            return int(env)
+        cap = self.N2V_INDEX_BYTES if budget is None else int(budget)
+        return min(cap, torch.cuda.mem_get_info(dev)[0] - self.N2V_INDEX_RESERVE)
+
+    def _build_n2v_index(self, dev, budget: Optional[int] = None) -> None:
         """n2v_rec int32[nnz, 8] / n2v_pos uint8[bytes] (dw_n2v_edge_offsets +
         dw_n2v_edge_index_build + dw_n2v_edge_records): per directed edge t -> v, t's position in
         N(v) and the sorted positions of N(t) ∩ N(v) — uint16 where deg(v) <= 65536, else int32 —
@@ -266,23 +287,33 @@ class CSRGraph:
         dw_walk_fast_positions). Built in chunks of about N2V_CHUNK_ENTRIES entries, so the
         scratch stays bounded while the index grows to the graph's size (C5: 132 GB). Both None
         when the index would exceed the byte budget; n2v_index_info = {'entries', 'bytes',
-        'chunks', 'build_ms'} or {'entries', 'bytes', 'skipped'}."""
+        'chunks', 'budget', 'build_ms'} or {'entries', 'bytes', 'skipped', 'budget'}; ``budget``:
+        its byte budget (_n2v_budget)."""
         import ctypes
-        import os
         import time
         d = self.device_tensors(dev, need_edge_cn=True)
         E = self.nnz
         colp = _native.ptr(d['col']) if E else None
+        budget_b = self._n2v_budget(dev, budget)
         with torch.cuda.device(dev):
             s = _native.stream(dev)
             t0 = time.perf_counter()
-            off = torch.empty(E + 1, dtype=torch.int64, device=dev)
-            boff = torch.empty(E + 1, dtype=torch.int64, device=dev)
             nb = ctypes.c_size_t(0)
-            oargs = [_native.ptr(d['row_ptr']), colp, _native.ptr(d['edge_cn']), E,
-                     _native.ptr(off), _native.ptr(boff)]
-            _native.call('dw_n2v_edge_offsets', *oargs, None, ctypes.byref(nb), s)
-            tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            try:   # (the offsets: 16 B per edge, before the index's size is known)
+                if 16 * (E + 1) > budget_b:
+                    raise torch.OutOfMemoryError('the offsets alone exceed the budget')
+                off = torch.empty(E + 1, dtype=torch.int64, device=dev)
+                boff = torch.empty(E + 1, dtype=torch.int64, device=dev)
+                oargs = [_native.ptr(d['row_ptr']), colp, _native.ptr(d['edge_cn']), E,
+                         _native.ptr(off), _native.ptr(boff)]
+                _native.call('dw_n2v_edge_offsets', *oargs, None, ctypes.byref(nb), s)
+                tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+            except torch.OutOfMemoryError:   # the wave walker needs none of it
+                d['n2v_rec'], d['n2v_pos'] = None, None
+                d['n2v_index_info'] = {'skipped': True, 'out_of_memory': True,
+                                       'budget': budget_b}
+                torch.cuda.empty_cache()
+                return
             _native.call('dw_n2v_edge_offsets', *oargs, _native.ptr(tmp), ctypes.byref(nb), s)
             del tmp
             n_pos, n_bytes = (int(x) for x in torch.stack([off[E], boff[E]]).tolist())
@@ -311,15 +342,10 @@ class CSRGraph:
                     tmp_need = max(tmp_need, int(nb.value))
             index_bytes = n_bytes + 32 * E
             need = index_bytes + 4 * E + 4 * max_pos + tmp_need
-            # the budget: DW_N2V_INDEX_BYTES, else N2V_INDEX_BYTES capped at the device's free
-            # memory less a reserve (the walker's other buffers and the training tables share it)
-            env = os.environ.get('DW_N2V_INDEX_BYTES')
-            budget = (int(env) if env is not None else
-                      min(self.N2V_INDEX_BYTES,
-                          torch.cuda.mem_get_info(dev)[0] - self.N2V_INDEX_RESERVE))
             skipped = {'entries': n_pos, 'bytes': index_bytes, 'build_bytes': need,
-                       'skipped': True}
-            if not fits or need > budget:
+                       'skipped': True, 'budget': budget_b,
+                       'unsupported': not fits}
+            if not fits or need > budget_b:
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = skipped
                 return
@@ -347,7 +373,7 @@ class CSRGraph:
             _native.check_status(d['status'], 'node2vec position index build')
             d['n2v_rec'], d['n2v_pos'] = rec, pos
             d['n2v_index_info'] = {'entries': n_pos, 'bytes': index_bytes,
-                                   'chunks': len(chunks),
+                                   'chunks': len(chunks), 'budget': budget_b,
                                    'build_ms': (time.perf_counter() - t0) * 1e3}
 
     # rows longer than the replay walker's LDS stage (1,024) get a V-bit neighbour map, the

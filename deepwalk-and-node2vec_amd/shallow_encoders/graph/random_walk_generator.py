@@ -317,7 +317,8 @@ class RandomWalk(ABC):
             return False
         if not self._csr.is_simple(dev):   # a repeated neighbour: the index assumes simple rows
             return False
-        d = self._csr.device_tensors(dev, need_n2v_index=True)
+        budget = min(self._csr.N2V_PHILOX_INDEX_BYTES, torch.cuda.mem_get_info(dev)[0] // 4)
+        d = self._csr.device_tensors(dev, need_n2v_index=True, n2v_budget=budget)
         return d.get('n2v_rec') is not None
 
     def count_replay_traffic(self, start_ids: torch.Tensor, uniforms: torch.Tensor,

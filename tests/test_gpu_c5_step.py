@@ -51,7 +51,11 @@ def c5(hip_device):
     from shallow_encoders.graph.rmat import rmat_graph
     csr = rmat_graph(SCALE, EDGES, 0, device=hip_device)
     walker = Node2Vec(csr, L, p=P, q=Q, rng='philox', seed=WALK_SEED, device=hip_device)
-    return csr, walker
+    yield csr, walker
+    import gc
+    del csr, walker
+    gc.collect()
+    torch.cuda.empty_cache()
 
 
 def _walks(csr, walker, s, dev):

@@ -22,7 +22,9 @@ SCALE, EDGES, P, Q = 24, 256_000_000, 0.25, 4.0
 
 @pytest.fixture(scope='module')
 def c5_index(hip_device):
+    import gc
     from shallow_encoders.graph.rmat import rmat_graph
+    gc.collect()
     torch.cuda.empty_cache()
     csr = rmat_graph(SCALE, EDGES, 0, device=hip_device)
     d = csr.device_tensors(hip_device, need_n2v_index=True)
