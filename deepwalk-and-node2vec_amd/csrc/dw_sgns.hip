@@ -1232,9 +1232,6 @@ int64_t grid_cap(int per_cu) {
     return (int64_t)n_cu[dev] * per_cu;
 }
 
-// The event the next records gather waits for (dw_sgns_gather_wait; NULL: none).
-thread_local hipEvent_t g_gather_wait = nullptr;
-
 // ---- deterministic mode: gradient buffers with an int64 fixed-point accumulator -------------
 struct ExactEntry {
     int64_t *acc;
@@ -1925,14 +1922,6 @@ int launch_sgns_impl(SgnsArgs a, void *workspace, size_t workspace_bytes, int ph
         return DW_E_HIP;
     }
     g_timer.mark(2, st);
-    {   // dw_sgns_gather_wait: the gather after an event of another stream (one call)
-        const hipEvent_t ev = g_gather_wait;
-        g_gather_wait = nullptr;
-        if (ev && hipStreamWaitEvent(st, ev, 0) != hipSuccess) {
-            dw::set_error("dw_sgns: waiting for the gather's event failed");
-            return DW_E_HIP;
-        }
-    }
     return launch_pass2(kb.current(), vb.current(), n_rec, a.w_in, a.g_out, a.d, oa, a.V, st,
                         nullptr, 1.0, a.status);
 }
@@ -2954,11 +2943,6 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
     return dw::adam_rows_launch(w_out_local, m_out, v_out, last_step, nullptr, local_rows, dim,
                                 rows_buf,
                                 n_rows, n_max, nullptr, hist, step - 1, p_only, st);
-}
-
-int dw_sgns_gather_wait(void *event) {
-    g_gather_wait = static_cast<hipEvent_t>(event);
-    return DW_OK;
 }
 
 int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t frac,

@@ -38,7 +38,7 @@ DW_EXACT_ADAM = 2
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 24
+ABI_VERSION = 23
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -162,7 +162,6 @@ SIGNATURES = {
                                                _p, _szp, _p, _p]),
     'dw_n2v_edge_records': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _p, _p]),
     'dw_exact_register': (ctypes.c_int, [_p, _p, _i64, _i32, _i32]),
-    'dw_sgns_gather_wait': (ctypes.c_int, [_p]),
     'dw_exact_unregister': (ctypes.c_int, [_p]),
     'dw_exact_frac_bits': (ctypes.c_int32, [_f64]),
     'dw_fixed_to_float': (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),

@@ -436,31 +436,19 @@ class ShardedTables:
             return                              # exchange_out does the Adam
         self._next_in = 2 - self._cur_in
         if not self.multi:
-            sort_window = self.adam_window() == 'sort'
-
             def adam_to(_async):
                 # (the deterministic mode's update reads and clears the 8-B sums instead of g)
                 per = 4 * 7 + (8 if getattr(self, '_exact', None) is not None else 0)
-                blocks = 0 if sort_window else overlap_adam_blocks(self.V_pad * self.d * per,
-                                                                   overlap_bytes)
+                blocks = overlap_adam_blocks(self.V_pad * self.d * per, overlap_bytes)
                 hip_adam_to(self.params[self._cur_in], self.params[self._next_in],
                             self.grads[0], self.m[0], self.v[0], self.step_count, self.lr,
                             self.betas, self.eps, self.weight_decay, True, blocks)
                 done = torch.cuda.Event()
                 done.record(self._side)
-                self._in_done = done if sort_window else None
                 return done
             self._on_side(adam_to)
             return
         self._on_side(lambda a: self._exchange_in(self._cur_in, self._next_in, a))
-
-    # where the one-GPU in-table Adam runs: 'sort' — at full rate beside the records sort, the
-    # gather after it (dw_sgns_gather_wait); 'pass2' — its grid capped so that it spreads over
-    # the sort and the gather (DW_ADAM_WINDOW overrides)
-    ADAM_WINDOW = 'pass2'
-
-    def adam_window(self) -> str:
-        return os.environ.get('DW_ADAM_WINDOW', self.ADAM_WINDOW)
 
     def out_pieces_spec(self):
         """(n_pieces, piece_rows) for sgns_phase2_pieces."""
@@ -555,10 +543,6 @@ def replicated_step(tables: ShardedTables, walks: torch.Tensor, context_radius: 
         after_pass1()
     tables.exchange_in(overlap_bytes=pb['sort'] + pb['pass2'])
     spec = tables.out_adam_spec() if fuse else None
-    done = getattr(tables, '_in_done', None)
-    if done is not None and scatter == 'sorted' and not pieces:
-        _native.call('dw_sgns_gather_wait', done._as_parameter_)   # the gather after the Adam
-        tables._in_done = None
     if pieces:
         n_pieces, rows = tables.out_pieces_spec()
         sgns_phase2_pieces(tables.w_in, tables.g_out, K, walks=walks, context_radius=R,

@@ -307,12 +307,6 @@ int dw_n2v_edge_records(const int64_t *row_ptr, const int32_t *col, const uint32
  * conversion pass after pass 1. */
 #define DW_EXACT_ADAM 2
 
-/* The next dw_sgns_walks_phase / dw_sgns_walks_phase2_adam call on this host thread makes its
- * records gather (after the sort) wait for `event` (a hipEvent_t recorded on another stream):
- * one call, then cleared. The one-GPU step uses it to run the in table's Adam beside the sort at
- * full rate and the gather after it. */
-int dw_sgns_gather_wait(void *event);
-
 /* Row 0 of a lazy Adam history (dw_adam_rows): the box header's tag ("WDBX"). */
 #define DW_HIST_BOX_TAG 0x58424457u
 int dw_exact_register(const float *grad, int64_t *acc, int64_t n_elems, int32_t frac,
