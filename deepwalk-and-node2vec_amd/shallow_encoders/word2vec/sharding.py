@@ -1420,10 +1420,12 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     main = torch.cuda.current_stream(dev)
     side_out, side_in = t._side, t._pipe['side_in']
 
-    def ahead(k: int):
-        """Step k's preparation on the side streams, after everything enqueued so far."""
-        fork = torch.cuda.Event()
-        fork.record(main)
+    def ahead(k: int, fork: Optional[torch.cuda.Event] = None):
+        """Step k's preparation on the side streams, after everything enqueued so far (or after
+        ``fork``, an event recorded on the main stream)."""
+        if fork is None:
+            fork = torch.cuda.Event()
+            fork.record(main)
         if bind is not None:
             bind(k)
         slot = k & 1
@@ -1446,6 +1448,7 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     # pass and the in rows' update) or at step k's start (beside the out rows, whose resident
     # grid it then competes with)
     fork_early = os.environ.get('DW_PIPE_FORK', 'after') == 'before'
+    main_first = os.environ.get('DW_PIPE_ORDER', 'side') == 'main'
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
@@ -1459,15 +1462,23 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
                 bind(k)
         w = batches[k]
         t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
+        fork = None
         if not fork_early and k + 1 < n_steps:
-            ready = ahead(k + 1)
-            if bind is not None:
-                bind(k)
+            fork = torch.cuda.Event()
+            fork.record(main)
+            if not main_first:
+                ready = ahead(k + 1, fork)
+                if bind is not None:
+                    bind(k)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,
                          order_ready=True, placed=True, coefficients_in=True, walk_order=True,
                          workspace_slot=slot)
+        if fork is not None and main_first:   # the centre pass enqueued first (its queue)
+            ready = ahead(k + 1, fork)
+            if bind is not None:
+                bind(k)
         # the step's in rows with their gradient rows (dw_adam_rows grad_by_row clears them)
         hip_rows_adam(t.params_in[0], t.m_in, t.v_in, t.last_in, p['touched'][slot],
                       p['n_touched'][slot], nw * (L - 2 * R), t.grads_in, t._hist,
