@@ -1386,8 +1386,7 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     side streams while step k's out rows, centre pass and in-table update run, from the moment
     step k - 1 has finished (the buffers alternate by step parity: workspace slot, row counts,
     touched list). Only the out rows' step, the centre pass and the in rows' update stay on the
-    step's critical path. The preparation forks after step k's out rows by default
-    (DW_PIPE_FORK=before: at step k's start). The results equal the sequential steps': each kernel reads and writes
+    step's critical path; the preparation forks after step k's out rows. The results equal the sequential steps': each kernel reads and writes
     what it would there (the catch-up of step k + 1 skips the centres of step k, which step k
     updates itself). ``bind(k)``: called before enqueueing anything of step k (graph capture:
     binds step k's dw_step_scalars block). Returns the record count of the steps."""
@@ -1420,12 +1419,10 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     main = torch.cuda.current_stream(dev)
     side_out, side_in = t._side, t._pipe['side_in']
 
-    def ahead(k: int, fork: Optional[torch.cuda.Event] = None):
-        """Step k's preparation on the side streams, after everything enqueued so far (or after
-        ``fork``, an event recorded on the main stream)."""
-        if fork is None:
-            fork = torch.cuda.Event()
-            fork.record(main)
+    def ahead(k: int):
+        """Step k's preparation on the side streams, after everything enqueued so far."""
+        fork = torch.cuda.Event()
+        fork.record(main)
         if bind is not None:
             bind(k)
         slot = k & 1
@@ -1444,11 +1441,10 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     ready = ahead(0)
     slots = batches[0].shape[0] * (L - 2 * R) * 2 * R * (1 + K)
     p = t._pipe
-    # where step k + 1's preparation forks: after step k's out rows (default; beside the centre
-    # pass and the in rows' update) or at step k's start (beside the out rows, whose resident
-    # grid it then competes with)
-    fork_early = os.environ.get('DW_PIPE_FORK', 'after') == 'before'
-    main_first = os.environ.get('DW_PIPE_ORDER', 'side') == 'main'
+    # step k + 1's preparation forks after step k's out rows, beside the centre pass and the in
+    # rows' update. (At step k's start, beside the out rows, it measured slower — its waves take
+    # the CU slots k_out_rows sizes its resident grid for: 0.336 vs 0.332 ms at C3 / 64; the
+    # centre pass captured before the side chains, 0.332-0.334 vs 0.324-0.330.)
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
@@ -1456,29 +1452,17 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
         t.begin_step()
         for ev in ready:
             main.wait_event(ev)
-        if fork_early and k + 1 < n_steps:
+        w = batches[k]
+        t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
+        if k + 1 < n_steps:
             ready = ahead(k + 1)
             if bind is not None:
                 bind(k)
-        w = batches[k]
-        t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
-        fork = None
-        if not fork_early and k + 1 < n_steps:
-            fork = torch.cuda.Event()
-            fork.record(main)
-            if not main_first:
-                ready = ahead(k + 1, fork)
-                if bind is not None:
-                    bind(k)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,
                          order_ready=True, placed=True, coefficients_in=True, walk_order=True,
                          workspace_slot=slot)
-        if fork is not None and main_first:   # the centre pass enqueued first (its queue)
-            ready = ahead(k + 1, fork)
-            if bind is not None:
-                bind(k)
         # the step's in rows with their gradient rows (dw_adam_rows grad_by_row clears them)
         hip_rows_adam(t.params_in[0], t.m_in, t.v_in, t.last_in, p['touched'][slot],
                       p['n_touched'][slot], nw * (L - 2 * R), t.grads_in, t._hist,

@@ -149,9 +149,8 @@ def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
         assert_no_row_drift(got, exp)
 
 
-@pytest.mark.parametrize('n_steps,fork', [(1, 'after'), (2, 'after'), (7, 'after'),
-                                          (7, 'before')])
-def test_pipelined_owner_steps_equal_sequential(hip_device, n_steps, fork, monkeypatch):
+@pytest.mark.parametrize('n_steps', [1, 2, 7])
+def test_pipelined_owner_steps_equal_sequential(hip_device, n_steps):
     """owner_lazy_steps (step k + 1's claims, touch claim and catch-up on side streams while
     step k runs) equals the sequential owner_lazy_step calls on the same batches: the small
     graph's batches share most centre rows from step to step, so the catch-up of step k + 1 must
@@ -159,7 +158,6 @@ def test_pipelined_owner_steps_equal_sequential(hip_device, n_steps, fork, monke
     atomic-order noise; and the pipelined run leaves the tables ready for an eager step."""
     from shallow_encoders.word2vec.sharding import (OwnerLazyTables, owner_lazy_step,
                                                     owner_lazy_steps)
-    monkeypatch.setenv('DW_PIPE_FORK', fork)
     dev = hip_device
     csr, walker, epoch = _setup(dev)
     V = csr.vocab_size
