@@ -426,3 +426,36 @@ def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
     assert r0 == r1 and torch.equal(t0, t1)
     for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
         np.testing.assert_allclose(l1[k], l0[k], rtol=3e-2)
+
+
+def test_reference_streams_c2_loop_graphed_deterministic(tmp_path, hip_device, monkeypatch):
+    """The same loop with the reference's own streams (rng: python walks, noise: torch) in the
+    deterministic mode (DW_DETERMINISTIC=1): the eager run and the run replayed as graphs of 16
+    end with bit-identical tables — the float mode's 3% envelope above is the atomics' order,
+    not the graphs — and leave `random` and torch's generator in the same state."""
+    import random
+    from tools import train as train_tool
+    monkeypatch.setenv('DW_DETERMINISTIC', '1')
+    base = ['datamodule.dataset_name=graph_rmat', 'datamodule.additional_parameters.scale=12',
+            'datamodule.additional_parameters.n_edges=5429',
+            'datamodule.additional_parameters.graph_seed=0',
+            'datamodule.additional_parameters.walks_per_node=1',
+            'datamodule.additional_parameters.method_params.q=1',
+            'datamodule.additional_parameters.rng=python', 'train.noise=torch',
+            'model.embedding_size=128', 'train.optimizer.lr=0.01', 'train.max_epochs=2']
+    runs = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
+        out = str(tmp_path / f'det{mode}')
+        random.seed(5)
+        torch.manual_seed(0)
+        train_tool.main(['--config-name', 'sge_sg_cora', f'path.output_dir={out}',
+                         f'output_dir={out}', f'train.experiment=d{mode}'] + base)
+        ck = os.path.join(out, 'graph_rmat', f'd{mode}', 'checkpoints', 'last.ckpt')
+        runs.append((torch.load(ck, weights_only=True), random.getstate(),
+                     torch.get_rng_state()))
+    (s0, r0, t0), (s1, r1, t1) = runs
+    assert s0['global_step'] == s1['global_step'] == 128
+    assert r0 == r1 and torch.equal(t0, t1)
+    for k, v in s0['state_dict'].items():
+        assert torch.equal(v, s1['state_dict'][k]), k
