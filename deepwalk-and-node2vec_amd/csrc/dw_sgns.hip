@@ -1546,6 +1546,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             lane < n_in ? a.walks[static_cast<int64_t>(my_w) * a.L + a.R +
                                   (my_b - my_w * static_cast<uint32_t>(per))]
                         : -1;
+        // the record's row is a context (slot t = 0 mod 1 + K), not a negative: once per record
+        // here, not per round in the group leaders (two integer divisions each)
+        const uint32_t my_t = my_slot - my_b * static_cast<uint32_t>(T);
+        const int my_pos = (my_t % static_cast<uint32_t>(rpc)) == 0u ? 1 : 0;
         const uint32_t prev = __shfl_up(my_key, 1, WAVE);
         const bool is_start = lane < n_in && (lane == 0 || my_key != prev);
         const uint64_t starts = __ballot(is_start);
@@ -1636,11 +1640,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     s_c[wv][q][gl + 16 * f] = c4[f];
                 }
                 const float x = row_sum16(pr);
-                const int t = static_cast<int>(slot % static_cast<uint32_t>(T));
+                const bool pos = __shfl(my_pos, src, WAVE) != 0;
                 float coef = 0.f;
                 if (ok && gl == 0)
-                    coef = row_coef(x, (t % rpc) == 0, a.scale, acc_pos, acc_neg, acc_rec,
-                                    acc_prec);
+                    coef = row_coef(x, pos, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
                 if (in && gl == 0) coef_slot[slot] = coef;
                 dw::wave_lds_sync();
                 // the gradient over the round's records in placed order (lane-strided elements,
