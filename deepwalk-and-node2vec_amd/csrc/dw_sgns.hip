@@ -1483,27 +1483,29 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // the table (oa.pend[row] = 1), where the centre pass reads it; the parameter half of step s is
 // applied (dw::settle_pending) when the row is next replayed or flushed — the same operations
 // as adam_elem's, so the same bits, without a per-slot copy of p^{s-1} (138 MB at C3/64).
-// A wave takes gch <= 64 placed records (lane = record: slots and centre nodes looked up in one
-// round trip) and their rows one at a time, four records' centre rows in flight (one per 16-lane
-// group for the logits). A row that straddles the chunk (its first or last row continues in the
-// neighbouring chunk) is replayed by each chunk that holds records of it (the same bits), adds
+// A block takes a range of 4 gch <= 256 placed records: its waves read them (one per lane: slots,
+// centre nodes and context flags looked up in one round trip) into LDS with the rows' starts,
+// then take the range's rows one at a time from a block counter (an LDS atomic) — a row's time is
+// set by its deferred steps, ~4 on average but geometric, so four waves sharing ~150 rows finish
+// together where each wave's own fixed chunk left the slowest waves running alone — and ranges
+// small enough that there are about twice as many blocks as resident slots, which the hardware
+// hands out as blocks finish. Per row: four records' centre rows in flight (one per 16-lane group
+// for the logits). A row that straddles the range (its first or last row continues in the
+// neighbouring range) is replayed by each range that holds records of it (the same bits), adds
 // its part of the gradient to g_out with float atomics and is stepped by k_lazy_boundary (full
 // replay, p_current false).
 // (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
 // ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
 // 138-VGPR kernel ran three waves per SIMD.)
-// The kernel is latency-bound (SQ counters at C3's 64-walk batch: waves parked on memory 68% of
-// their cycles): a row took three dependent round trips — its p / m / v, then its records'
-// centre rows (two loads, one after the other) — and a chunk of ~30 rows ran them in sequence.
-// Now each row's first-round centre rows (independent of the replay) are issued together with
-// the row, and the next row's p / m / v / last / pend are issued before this row's replay (after
-// its centre rows, so waiting for those never waits for the prefetch: loads return in order),
-// so one round trip is left exposed per row; the registers this takes hold the kernel at six
-// waves per SIMD (OUT_ROWS_WAVES; the chunks are sized so that every wave is resident at once).
+// Each row's first-round centre rows (independent of the replay) are issued together with the
+// row, and the next row's p / m / v / last / pend are issued before this row's replay (after its
+// centre rows, so waiting for those never waits for the prefetch: loads return in order), so one
+// round trip is left exposed per row; the registers this takes hold the kernel at six waves per
+// SIMD (OUT_ROWS_WAVES).
 // EXACT (the deterministic mode, g_out registered): each term coef * w_in enters the row's sum
 // as a fixed-point integer (dw::to_fixed, the records gather's rule), so the sum is the same
 // whatever order the claim's atomics ranked the records in; a straddling row adds its integer
-// part into fo.acc, which k_fixed_boundary converts once every chunk has.
+// part into fo.acc, which k_fixed_boundary converts once every range has.
 constexpr int OUT_ROWS_WAVES = 6;
 template <int F4, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
@@ -1511,10 +1513,17 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
                float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo) {
     constexpr int D = 64 * F4;
+    constexpr int BR = WAVES_PER_BLOCK * WAVE;   // records per block range, at most
     bool fx_range = false;
     float fx_tmax = 0.f;   // EXACT: the largest |term| (the range test, once at the end)
     constexpr int RU = 4;   // records per round (one per 16-lane group)
-    __shared__ uint8_t s_rs[WAVES_PER_BLOCK][WAVE + 1];
+    // the block range's records (slot, centre node, context flag) and its rows' starts
+    __shared__ uint32_t s_key[BR], s_slot[BR];
+    __shared__ int32_t s_cid[BR];
+    __shared__ uint8_t s_pos[BR];
+    __shared__ uint16_t s_rs[BR + 1];
+    __shared__ int32_t s_wrows[WAVES_PER_BLOCK];
+    __shared__ int32_t s_next;   // the next row to take
     __shared__ float4 s_p[WAVES_PER_BLOCK][D / 4];        // the row's p^{s-1}
     __shared__ float4 s_c[WAVES_PER_BLOCK][RU][D / 4];    // the round's centre rows
     const int lane = threadIdx.x & (WAVE - 1);
@@ -1522,8 +1531,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
     const int q = lane >> 4, gl = lane & 15;
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t n_rec = range[1];
-    const int64_t n_chunks = (n_rec + gch - 1) / gch;
-    const int64_t n_waves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int32_t br_len = WAVES_PER_BLOCK * gch;   // (gch <= 64)
+    const int64_t n_ranges = (n_rec + br_len - 1) / br_len;
     const int32_t step = dw::eff_step(oa.dyn, oa.step_delta, oa.step);
     const dw::AdamScalars hs = dw::hist_at(oa.hist, step);
     const int32_t box_from = dw::hist_box_from(oa.hist);
@@ -1532,37 +1541,60 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
     float *sp = reinterpret_cast<float *>(&s_p[wv][0]);
     float acc_pos = 0.f, acc_neg = 0.f, acc_rec = 0.f, acc_prec = 0.f;
 
-    for (int64_t ch = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv; ch < n_chunks; ch += n_waves) {
-        const int64_t e0 = ch * gch;
-        const int n_in = static_cast<int>(n_rec - e0 < gch ? n_rec - e0 : gch);
-        const uint32_t before = e0 > 0 ? keys[e0 - 1] : 0xFFFFFFFFu;
-        const uint32_t after = e0 + n_in < n_rec ? keys[e0 + n_in] : 0xFFFFFFFFu;
-        const uint32_t my_key = lane < n_in ? keys[e0 + lane] : 0xFFFFFFFFu;
-        // lane = record: its slot s = b T + t and its centre node, all of them in one round trip
-        const uint32_t my_slot = lane < n_in ? static_cast<uint32_t>(vals[e0 + lane]) : 0u;
-        const uint32_t my_b = my_slot / static_cast<uint32_t>(T);
-        const uint32_t my_w = my_b / static_cast<uint32_t>(per);
-        const int32_t my_cid =
-            lane < n_in ? a.walks[static_cast<int64_t>(my_w) * a.L + a.R +
-                                  (my_b - my_w * static_cast<uint32_t>(per))]
-                        : -1;
-        // the record's row is a context (slot t = 0 mod 1 + K), not a negative: once per record
-        // here, not per round in the group leaders (two integer divisions each)
-        const uint32_t my_t = my_slot - my_b * static_cast<uint32_t>(T);
-        const int my_pos = (my_t % static_cast<uint32_t>(rpc)) == 0u ? 1 : 0;
-        const uint32_t prev = __shfl_up(my_key, 1, WAVE);
-        const bool is_start = lane < n_in && (lane == 0 || my_key != prev);
-        const uint64_t starts = __ballot(is_start);
-        const int nrows = __popcll(starts);
-        if (is_start) s_rs[wv][__popcll(starts & lt)] = static_cast<uint8_t>(lane);
-        if (lane == 0) s_rs[wv][nrows] = static_cast<uint8_t>(n_in);
-        dw::wave_lds_sync();
+    for (int64_t br = blockIdx.x; br < n_ranges; br += gridDim.x) {
+        const int64_t r0 = br * br_len;
+        const int n_blk = static_cast<int>(n_rec - r0 < br_len ? n_rec - r0 : br_len);
+        const uint32_t before = r0 > 0 ? keys[r0 - 1] : 0xFFFFFFFFu;
+        const uint32_t after = r0 + n_blk < n_rec ? keys[r0 + n_blk] : 0xFFFFFFFFu;
+        {   // wave wv reads records [64 wv, 64 wv + 64) of the range: one per lane, all at once
+            const int i = WAVE * wv + lane;
+            const bool in = i < n_blk;
+            const uint32_t key = in ? keys[r0 + i] : 0xFFFFFFFFu;
+            const uint32_t prev = i == 0 ? 0u : lane > 0 ? 0u : (in ? keys[r0 + i - 1] : 0u);
+            const uint32_t slot = in ? static_cast<uint32_t>(vals[r0 + i]) : 0u;
+            const uint32_t b = slot / static_cast<uint32_t>(T);
+            const uint32_t w = b / static_cast<uint32_t>(per);
+            const int32_t cid =
+                in ? a.walks[static_cast<int64_t>(w) * a.L + a.R + (b - w * static_cast<uint32_t>(per))]
+                   : -1;
+            // the record's row is a context (slot t = 0 mod 1 + K), not a negative
+            const uint32_t t = slot - b * static_cast<uint32_t>(T);
+            const uint32_t up = __shfl_up(key, 1, WAVE);
+            const bool is_start = in && (i == 0 || key != (lane > 0 ? up : prev));
+            const uint64_t starts = __ballot(is_start);
+            s_key[i] = key;
+            s_slot[i] = slot;
+            s_cid[i] = cid;
+            s_pos[i] = (t % static_cast<uint32_t>(rpc)) == 0u ? 1 : 0;
+            if (lane == 0) s_wrows[wv] = __popcll(starts);
+            __syncthreads();
+            int base = 0, nr = 0;
+#pragma unroll
+            for (int x = 0; x < WAVES_PER_BLOCK; ++x) {
+                base += x < wv ? s_wrows[x] : 0;
+                nr += s_wrows[x];
+            }
+            if (is_start) s_rs[base + __popcll(starts & lt)] = static_cast<uint16_t>(i);
+            if (threadIdx.x == 0) {
+                s_rs[nr] = static_cast<uint16_t>(n_blk);
+                s_next = 0;
+            }
+            __syncthreads();
+        }
+        const int nrows = s_wrows[0] + s_wrows[1] + s_wrows[2] + s_wrows[3];
+        // rows one at a time from the block's counter: a row's time is set by its deferred steps,
+        // so the four waves share the range's rows instead of each running a fixed quarter
+        auto take = [&]() {
+            int k = 0;
+            if (lane == 0) k = atomicAdd(&s_next, 1);
+            return __builtin_amdgcn_readfirstlane(k);
+        };
         // the next row's state, loaded one row ahead
         float np[F4], nm[F4], nv[F4];
         int32_t nlast = 0;
         uint32_t npend = 0;
         auto prefetch = [&](int k) {
-            const uint32_t r = __builtin_amdgcn_readlane(my_key, s_rs[wv][k]);
+            const uint32_t r = s_key[s_rs[k]];
             const int64_t o = static_cast<int64_t>(r) * D + lane;
             nlast = oa.last[r];
             npend = oa.pend[r];
@@ -1573,10 +1605,11 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                 nv[f] = oa.v[o + 64 * f];
             }
         };
-        if (nrows > 0) prefetch(0);
-        for (int k = 0; k < nrows; ++k) {
-            const int rs = s_rs[wv][k], re = s_rs[wv][k + 1];   // (wave-uniform)
-            const uint32_t row = __builtin_amdgcn_readlane(my_key, rs);
+        int k = take();
+        if (k < nrows) prefetch(k);
+        while (k < nrows) {
+            const int rs = s_rs[k], re = s_rs[k + 1];   // (wave-uniform)
+            const uint32_t row = s_key[rs];
             const bool straddle = row == before || row == after;
             const int64_t ro = static_cast<int64_t>(row) * D + lane;
             const int cnt = re - rs;
@@ -1601,15 +1634,16 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             // [4gl + 64f, +4)), then the next row's loads — both in flight during the replay
             float4 c4[F4];
             {
-                const int32_t cid = __shfl(my_cid, (rs + q) & (WAVE - 1), WAVE);
-                const bool ok = q < cnt && cid >= 0 && cid < a.V;
+                const int32_t cid = q < cnt ? s_cid[rs + q] : -1;
+                const bool ok = cid >= 0 && cid < a.V;
                 const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
 #pragma unroll
                 for (int f = 0; f < F4; ++f)
                     c4[f] = ok ? *reinterpret_cast<const float4 *>(crow + 64 * f)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            prefetch(k + 1 < nrows ? k + 1 : k);   // (unconditional: no register copies)
+            const int kn = take();
+            prefetch(kn < nrows ? kn : k);   // (unconditional: no register copies)
             if (pd) dw::settle_pending(p, m, v, oa.hist, from, box_from);   // the previous step's p half
             dw::replay_g0(p, m, v, oa.hist, from, step - 1, box_from);   // -> p^{s-1}
 #pragma unroll
@@ -1617,10 +1651,10 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             dw::wave_lds_sync();
             for (int j0 = 0; j0 < cnt; j0 += RU) {
                 // group q: record j0 + q's logit in pass 1's layout and its coefficient
-                const int src = (rs + j0 + q) & (WAVE - 1);
                 const bool in = j0 + q < cnt;
-                const uint32_t slot = __shfl(my_slot, src, WAVE);
-                const int32_t cid = __shfl(my_cid, src, WAVE);
+                const int src = in ? rs + j0 + q : rs;
+                const uint32_t slot = s_slot[src];
+                const int32_t cid = s_cid[src];
                 const bool ok = in && cid >= 0 && cid < a.V;
                 if (j0 > 0) {   // later rounds (rows of more than RU records)
                     const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
@@ -1640,7 +1674,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     s_c[wv][q][gl + 16 * f] = c4[f];
                 }
                 const float x = row_sum16(pr);
-                const bool pos = __shfl(my_pos, src, WAVE) != 0;
+                const bool pos = s_pos[src] != 0;
                 float coef = 0.f;
                 if (ok && gl == 0)
                     coef = row_coef(x, pos, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
@@ -1699,8 +1733,9 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     if (oa.counts) oa.counts[row] = 0u;
                 }
             }
+            k = kn;
         }
-        dw::wave_lds_sync();   // s_rs is rewritten by the next chunk
+        __syncthreads();   // the range's LDS is rewritten by the next one
     }
     if constexpr (EXACT) {
         fx_range = fx_range || dw::fixed_range(fx_tmax, fo.fs);
@@ -3334,14 +3369,16 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     oa.pend = pending;    // the stepped rows are left pending (p at step - 1 for the centre pass)
     rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;
-    // records per chunk (<= 64: one per lane): as few as keep every chunk's wave resident at
-    // once (OUT_ROWS_WAVES per SIMD, k_out_rows' bound) — every wave then runs from the start, where
-    // 32-record chunks left C3's 64-walk batch (269K records) ~200 waves for a second round that
-    // doubled the kernel — and no fewer than 16
+    // a block range of 4 gch records (gch <= 64): about two blocks per resident slot
+    // (OUT_ROWS_WAVES per SIMD, k_out_rows' bound), so that the hardware hands the second half
+    // out as blocks finish — at C3's 64-walk batch (269K records) 88-record ranges, 0.302-0.308
+    // ms per step against 0.320-0.321 with one range per slot; 48 / 64 / 88 / 176 / 128 records
+    // measured 0.303-0.305 / 0.305-0.306 / 0.302-0.308 / 0.316 / 0.322, 32 0.310
+    // (profiles/r05_out_rows_ab.txt) — and no fewer than 12 per wave
     const int64_t bound = n_centres * T;
     const int64_t resident = grid_cap(4 * OUT_ROWS_WAVES);
-    int32_t gch = static_cast<int32_t>((bound + resident - 1) / resident);
-    gch = gch < 16 ? 16 : gch > 64 ? 64 : gch;
+    int32_t gch = static_cast<int32_t>((bound + 2 * resident - 1) / (2 * resident));
+    gch = gch < 12 ? 12 : gch > 64 ? 64 : gch;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
@@ -3365,16 +3402,17 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     }
 #undef DW_OUT_ROWS
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
+    const int32_t brl = WAVES_PER_BLOCK * gch;   // k_out_rows' block ranges: the straddle unit
     if (fx.acc) {   // the straddling rows' exact sums into g_out, before their step
-        hipLaunchKernelGGL(k_fixed_boundary, g, bl, 0, st, ws.k1, bound, gch, ws.bounds, fx,
+        hipLaunchKernelGGL(k_fixed_boundary, g, bl, 0, st, ws.k1, bound, brl, ws.bounds, fx,
                            g_out_local, dim);
         DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/fixed_boundary");
     }
     switch (dim / 64) {   // the straddling rows (g in g_out)
-        case 1: launch_boundary<1>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
-        case 2: launch_boundary<2>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
-        case 4: launch_boundary<4>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
-        default: launch_boundary<8>(st, ws.k1, bound, gch, g_out_local, dim, oa, ws.bounds); break;
+        case 1: launch_boundary<1>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
+        case 2: launch_boundary<2>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
+        case 4: launch_boundary<4>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
+        default: launch_boundary<8>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
     }
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/boundary");
     return DW_OK;
