@@ -3374,11 +3374,12 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     // out as blocks finish — at C3's 64-walk batch (269K records) 88-record ranges, 0.302-0.308
     // ms per step against 0.320-0.321 with one range per slot; 48 / 64 / 88 / 176 / 128 records
     // measured 0.303-0.305 / 0.305-0.306 / 0.302-0.308 / 0.316 / 0.322, 32 0.310
-    // (profiles/r05_out_rows_ab.txt) — and no fewer than 12 per wave
+    // (profiles/r05_out_rows_ab.txt) — and no fewer than 16 per wave (small batches: fewer
+    // straddling rows)
     const int64_t bound = n_centres * T;
     const int64_t resident = grid_cap(4 * OUT_ROWS_WAVES);
     int32_t gch = static_cast<int32_t>((bound + 2 * resident - 1) / (2 * resident));
-    gch = gch < 12 ? 12 : gch > 64 ? 64 : gch;
+    gch = gch < 16 ? 16 : gch > 64 ? 64 : gch;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
