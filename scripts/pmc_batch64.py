@@ -22,11 +22,10 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r['Counter_Name'] != counter:
             continue
-        name = r['Kernel_Name']
+        name = r['Kernel_Name'].replace('(anonymous namespace)::', '')
         if name.startswith('void '):
             name = name[5:]
-        name = name.split('(')[0].replace('(anonymous namespace)::', '')
-        name = name.replace('anonymous namespace)::', '')
+        name = name.split('(')[0]
         acc[name].append(float(r['Counter_Value']))
     return acc
 
@@ -44,7 +43,7 @@ def main():
         f = 1024.0 * sum(fe[k]) / len(fe[k])
         w = 1024.0 * sum(wr[k]) / len(wr[k])
         per_step = len(fe[k]) / n_steps
-        out[k] = {'fetch_bytes': round(2 * f), 'write_bytes': round(w),
+        out[k] = {'fetch_bytes': round(f), 'write_bytes': round(w),
                   'hbm_bytes': round(2 * f + w), 'launches_per_step': round(per_step, 3)}
         total += (2 * f + w) * per_step
     d = json.load(open(PMC))
