@@ -92,6 +92,31 @@ def walk_line_rates(table_bytes: int):
     return dict(r, source=f'profiles/r02_random_lines.json ({r["table_MiB"]} MiB table)')
 
 
+def dependent_line_roofline(steps: int, kern_s: float, lines_per_step: float, table_bytes: int,
+                            what: str):
+    """A latency-bound walker's random-line bound: ``lines_per_step`` dependent line loads per
+    step (from the walker's counted launch of the same walks) x steps / kernel time, against
+    the dependent-chain rate measured for a table of that size (walk_line_rates). frac_of_chase
+    near 1: the walker runs at the chip's rate of dependent random lines, not bound by bytes."""
+    rate = walk_line_rates(table_bytes)
+    if not rate:
+        return None
+    lines_s = steps * lines_per_step / kern_s
+    return {'steps_per_s': steps / kern_s, 'dependent_lines_per_step': lines_per_step,
+            'dependent_lines_per_s': lines_s,
+            'chase_lines_per_s': rate['chase_lines_per_s'],
+            'gather_lines_per_s': rate['gather_lines_per_s'],
+            'frac_of_chase': lines_s / rate['chase_lines_per_s'],
+            'lines': what, 'source': rate['source']}
+
+
+_RESULT = {}   # run()'s JSON line, printed by main()
+# the position walkers' dependent lines per step: the edge's 32-B record, then each move of the
+# pick's binary search to another 128-B line of the position list (counted launch)
+POS_LINES = 'edge record + the position search\'s line moves'
+
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -292,6 +317,217 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
     }
 
 
+def c5_line(args, dev, n_walks: int, n_steps: int) -> dict:
+    """BASELINE configs[4] (C5, the biased second-order walk stress config) on one GPU, timed by
+    the driver's run: R-MAT 24 built on the device (16,777,216 nodes, 256M edge
+    draws, 513M directed edges, hubs of 392,747 neighbours), node2vec p = .25, q = 4, L = 80.
+
+    walks (``n_walks`` walks, one per node from node 1): the exact walker (rng='python':
+    CPython's random.random() stream generated in HBM, dw_walk_replay_positions over the per-edge
+    position index, built here and timed) and the Philox walker over the same index
+    (dw_walk_fast_positions, layout='positions'); each with its realised bytes per step (a counted
+    launch of the same walks), HBM fraction and dependent-line fraction (dependent_line_roofline).
+    The index (132.6 GB) is then freed.
+
+    step: ``n_steps`` steps of the one-GPU composition tests/test_gpu_c5_step.py checks
+    (OwnerLazyTables on one rank: the in table's Adam lazy and exact, the out table's dense Adam
+    fused into the records gather; d = 256, K = 5, R = 5, 8,192 Philox node2vec walks per step;
+    random uniform Xavier-law init on the device), HIP-event and wall timed; roofline: SURVEY §8d's
+    per-pair SGNS bytes + the out table's dense Adam (V d 28 B) + the touched in rows' (|U| d 28 B)
+    over the event window. Then one more step checked from its pre-state on ~256 in and ~256 out
+    rows against the float64 restatement (word2vec/verify.py, the single-step bars); a miss fails
+    the bench."""
+    import gc
+    import random as _random
+    from shallow_encoders import _native
+    from shallow_encoders.graph.random_walk_generator import Node2Vec
+    from shallow_encoders.graph.rmat import rmat_graph
+    from shallow_encoders.graph.rng import draw_uniforms_device
+    from shallow_encoders.word2vec import verify
+    from shallow_encoders.word2vec.sgns import loss_terms
+    from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    cfg = CONFIGS['c5']
+    L, p, q = cfg['walk_length'], cfg['p'], cfg['q']
+    d, R, K, B = cfg['dim'], cfg['radius'], args.neg, cfg['batch_walks']
+    out = {'workload': (f'C5 (BASELINE configs[4]) on one GPU: R-MAT scale {cfg["scale"]} / '
+                        f'{cfg["edges"]} edge draws, node2vec p={p:g} q={q:g} L={L}; step d={d}, '
+                        f'R={R}, K={K}, {B} walks/step')}
+    t0 = time.perf_counter()
+    csr = rmat_graph(cfg['scale'], cfg['edges'], 0, device=dev)
+    V = csr.vocab_size
+    torch.cuda.synchronize(dev)
+    out['graph'] = {'nodes': V - 1, 'edges': csr.nnz // 2, 'build_s': time.perf_counter() - t0,
+                    'max_degree': int(csr.degree().max())}
+    n_walks = min(n_walks, V - 1)
+    st = torch.arange(1, n_walks + 1, dtype=torch.int32, device=dev)
+    walks = torch.empty((n_walks, L), dtype=torch.int32, device=dev)
+    steps = n_walks * (L - 1)
+    # ---- the exact walker over the position index -------------------------------------------
+    a = time.perf_counter()
+    dt = csr.device_tensors(dev, need_sorted=True, need_adj_pos=True, need_hub_bits=True,
+                            need_edge_cn=True, need_n2v_index=True)
+    torch.cuda.synchronize(dev)
+    info = dict(dt.get('n2v_index_info') or {})
+    out['position_index'] = dict(info, aux_and_index_build_s=time.perf_counter() - a)
+    if dt.get('n2v_rec') is None:
+        out['skipped'] = f'the position index does not fit this device: {info}'
+        return out
+    csr.philox_positions(dev)   # decided now (from the index's size: the rejection walker)
+    ex = Node2Vec(csr, L, p=p, q=q, device=dev)
+    _random.seed(0)
+    ex.walk_batch(st[:64])                                # warm-up (jump tables)
+    ex.walk_batch(st, out=walks)
+    torch.cuda.synchronize(dev)
+    a = time.perf_counter()
+    ex.walk_batch(st, out=walks)                          # end to end from the generator state
+    torch.cuda.synchronize(dev)
+    e2e = time.perf_counter() - a
+    u = torch.empty(steps, dtype=torch.float64, device=dev)
+    draw_uniforms_device(u.numel(), dev, out=u)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    ex.walk_batch(st, uniforms=u, out=walks, check=False)
+    e[1].record()
+    torch.cuda.synchronize(dev)
+    kern_s = e[0].elapsed_time(e[1]) * 1e-3
+    c = ex.count_replay_traffic(st, u, out=walks)
+    cs = max(c['steps'], 1)
+    gbs = c['bytes'] / kern_s / 1e9
+    out['walks_per_s_exact'] = n_walks / e2e
+    out['exact_walker'] = {
+        'walker': ex.last_walker, 'walks': n_walks, 'walks_per_s': n_walks / e2e,
+        'kernel_walks_per_s': n_walks / kern_s, 'kernel_ms': kern_s * 1e3,
+        'bytes': c['bytes'], 'bytes_per_step': c['bytes'] / cs,
+        'position_units_per_step': c['entries'] / cs, 'serial_picks': c['probes'],
+        'roofline': {'bound': 'dependent random lines', 'achieved': gbs, 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
+                     'random_line_roofline': dependent_line_roofline(
+                         c['steps'], kern_s, 1.0 + c['lines'] / cs, info['bytes'],
+                         POS_LINES)}}
+    del u
+    # ---- the Philox walker over the same index ------------------------------------------------
+    px = Node2Vec(csr, L, p=p, q=q, rng='philox', seed=7, device=dev, layout='positions')
+    px.walk_batch(st[:1024], walk_id0=0, out=walks[:1024], check=False)
+    torch.cuda.synchronize(dev)
+    a = time.perf_counter()
+    e[0].record()
+    px.walk_batch(st, walk_id0=0, out=walks)
+    e[1].record()
+    torch.cuda.synchronize(dev)
+    e2e = time.perf_counter() - a
+    kern_s = e[0].elapsed_time(e[1]) * 1e-3
+    c = px.count_traffic(st, walk_id0=0, out=walks)
+    cs = max(c['steps'], 1)
+    gbs = c['bytes'] / kern_s / 1e9
+    out['walks_per_s_philox'] = n_walks / e2e
+    out['philox_walker'] = {
+        'walker': px.last_walker, 'walks': n_walks, 'walks_per_s': n_walks / e2e,
+        'kernel_walks_per_s': n_walks / kern_s, 'kernel_ms': kern_s * 1e3,
+        'bytes': c['bytes'], 'bytes_per_step': c['bytes'] / cs,
+        'position_units_per_step': c['position_loads'] / cs,
+        'roofline': {'bound': 'dependent random lines', 'achieved': gbs, 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
+                     'random_line_roofline': dependent_line_roofline(
+                         c['steps'], kern_s, 1.0 + c['position_lines'] / cs, info['bytes'],
+                         POS_LINES)}}
+    del walks, st, ex, px
+    # the index and the exact walker's other structures make room for the tables
+    for k in ('n2v_rec', 'n2v_pos', 'edge_cn', 'adj_hpos', 'hub_bits', 'hub_idx', 'col_sorted'):
+        dt.pop(k, None)
+    del dt
+    gc.collect()
+    torch.cuda.empty_cache()
+    # ---- the SGNS step (test_gpu_c5_step's composition) ---------------------------------------
+    walker = Node2Vec(csr, L, p=p, q=q, rng='philox', seed=1234, device=dev)
+    tables = OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=None, emulate_world=1)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    lim = math.sqrt(6.0 / (V + d))                        # W2VBase's Xavier law (model.py:26-27)
+    tables.params_in[0, :V].uniform_(-lim, lim, generator=gen)
+    tables.w_out[:V].uniform_(-lim, lim, generator=gen)
+    per = L - 2 * R
+    pairs = B * per * 2 * R
+    grad_scale = 1.0 / pairs
+    walks_total = (V - 1) * cfg['walks_per_node']
+    loss_acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    seed = 99
+
+    def batch(s: int) -> torch.Tensor:
+        g0 = s * B
+        ids = (torch.arange(g0, g0 + B, device=dev, dtype=torch.int64) % walks_total) \
+            // cfg['walks_per_node'] + 1
+        return walker.walk_batch(ids.to(torch.int32), walk_id0=g0, check=False, status=status)
+
+    def step(s: int, w: torch.Tensor) -> None:
+        owner_lazy_step(tables, w, R, K, seed=seed, noise_offset=s * B * per,
+                        grad_scale=grad_scale, loss_acc=loss_acc, status=status)
+
+    warm = 3
+    for s in range(warm):
+        step(s, batch(s))
+    torch.cuda.synchronize(dev)
+    _native.check_status(status, 'bench c5 warmup')
+    loss_acc.zero_()
+    a = time.perf_counter()
+    e[0].record()
+    for s in range(warm, warm + n_steps):
+        step(s, batch(s))
+    e[1].record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - a
+    _native.check_status(status, 'bench c5')
+    ev_ms = e[0].elapsed_time(e[1]) / n_steps
+    mean_loss = float(loss_terms(loss_acc, pairs * n_steps, K)['loss'])
+    # one more step, checked from its pre-state (the sampled rows; the tables are 17 GB each)
+    s = warm + n_steps
+    w = batch(s)
+    rows_in, rows_out = verify.sample_rows(w, R, K, V, seed, s * B * per, 256)
+    w_in = tables.w_in                                    # (flushes: every row current)
+    gi, go = verify.sampled_grads(w_in, tables.w_out[:V], w, R, K, seed, s * B * per, rows_in,
+                                  rows_out)
+    pre_in = tuple(x[rows_in].clone() for x in (tables.params_in[0], tables.m_in, tables.v_in))
+    pre_out = tuple(x[rows_out].clone() for x in (tables.w_out, tables.m_out, tables.v_out))
+    step(s, w)
+    torch.cuda.synchronize(dev)
+    _native.check_status(status, 'bench c5 step check')
+    n_in = int(tables._n_touched.item())
+    tables.flush()
+    if os.environ.get('DW_BENCH_CORRUPT') == '1':   # test aid: the check must then fail
+        tables.m_out[int(rows_out[0])] += 1e-3
+    post_in = tuple(x[rows_in] for x in (tables.params_in[0], tables.m_in, tables.v_in))
+    post_out = tuple(x[rows_out] for x in (tables.w_out, tables.m_out, tables.v_out))
+    kw = dict(step=tables.step_count, lr=args.lr, betas=tables.betas, eps=tables.eps,
+              weight_decay=tables.weight_decay)
+    res = {'in': verify.check_rows(gi, pre_in, post_in, **kw),
+           'out': verify.check_rows(go, pre_out, post_out, **kw)}
+    step_check = dict(verify.summarize(res), rows_in=int(rows_in.numel()),
+                      rows_out=int(rows_out.numel()), step=tables.step_count)
+    bpp = sgns_bytes_per_pair(d, K, R)
+    out_adam, in_adam = V * d * 4 * 7, n_in * d * 4 * 7
+    alg = pairs * bpp + out_adam + in_adam
+    gbs = alg / (ev_ms * 1e-3) / 1e9
+    out.update({
+        'value': pairs * n_steps / elapsed, 'unit': 'positive-pairs/s',
+        'ms_per_step': elapsed / n_steps * 1e3, 'steps': n_steps, 'warmup': warm,
+        'positive_pairs_per_step': pairs, 'mean_loss': mean_loss,
+        'step_composition': ('sharding.owner_lazy_step on one rank (OwnerLazyTables: lazy exact '
+                             'in-table Adam, out-table dense Adam fused into the records gather); '
+                             'Philox node2vec walks (rejection walker: the index is freed)'),
+        'roofline': {'kernel': ('walker + k_sgns_g16<owner> + rocprim onesweep sort + '
+                                'k_rec_gather with the out-table Adam fused + k_adam_rest + '
+                                'touched in rows (k_rows_adam)'),
+                     'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': gbs / HBM_PEAK_GBS, 'traffic': None, 'ms_per_step_events': ev_ms,
+                     'bytes_per_step': alg, 'sgns_bytes': pairs * bpp,
+                     'out_table_adam_bytes': out_adam, 'touched_in_rows': n_in,
+                     'touched_in_rows_adam_bytes': in_adam},
+        'step_check': step_check})
+    del tables, walker, csr
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -408,6 +644,11 @@ def main():
                     help='the one-GPU C3 line: then also time this many steps at the reference '
                          'configs\' 64-walk batch (lazy exact Adam, graph-replayed) and report '
                          'them as batch64, with a checked step; 0 = skip')
+    ap.add_argument('--c5-walks', type=int, default=1 << 20,
+                    help='the one-GPU C3 line: then also run BASELINE configs[4] (C5) — this many '
+                         'exact and Philox node2vec walks over the position index, and '
+                         '--c5-steps checked SGNS steps at d=256 — reported as c5')
+    ap.add_argument('--c5-steps', type=int, default=16, help='0 = skip the c5 part')
     ap.add_argument('--deterministic', action='store_true',
                     help='the deterministic accumulation mode (word2vec/exact.py: int64 '
                          'fixed-point gradient sums, bit-identical tables run to run and across '
@@ -449,6 +690,20 @@ def main():
     dev = torch.device('cuda', local_rank)
     torch.cuda.set_device(dev)
     rc = run(args, world, rank, local_rank, backend, dist_on, dev)
+    line = _RESULT.pop('line', None)
+    if (rc == 0 and line is not None and not dist_on and args.config == 'c3'
+            and args.c5_steps > 0 and args.c5_walks > 0 and not args.deterministic
+            and args.batch_walks == CONFIGS['c3']['batch_walks'] and not args.emulate_world):
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        c5 = c5_line(args, dev, args.c5_walks, args.c5_steps)
+        line['c5'] = c5
+        if c5.get('step_check') is not None and not c5['step_check']['ok']:
+            log(rank, f'[bench] c5 step check FAILED: {c5["step_check"]}')
+            rc = 3
+    if line is not None and rank == 0:
+        print(json.dumps(line), flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
@@ -1085,9 +1340,25 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
                 # realised traffic of the same walks (dw_walk_fast_counted, untimed launch)
                 c = w.count_traffic(st, walk_id0=rank * n_walks, out=out)
                 nbytes = c['bytes']
-                extra = {'bytes_per_step': c['bytes'] / max(c['steps'], 1),
-                         'proposal_blocks_per_step': c['blocks'] / max(c['steps'], 1),
-                         'adjacency_tests_per_step': c['tests'] / max(c['steps'], 1)}
+                cs = max(c['steps'], 1)
+                extra = {'bytes_per_step': c['bytes'] / cs,
+                         'proposal_blocks_per_step': c['blocks'] / cs,
+                         'adjacency_tests_per_step': c['tests'] / cs,
+                         'walker': w.last_walker}
+                info = csr.device_tensors(dev).get('n2v_index_info') or {}
+                if 'position_loads' in c:
+                    # over the position index: the step's 32-B edge record (one line), then the
+                    # pick's binary-search probes, each a dependent 2-B load (C3's lists are
+                    # uint16: one probe per unit)
+                    extra['position_loads_per_step'] = c['position_loads'] / cs
+                    extra['random_line_roofline'] = dependent_line_roofline(
+                        steps, kern_s, 1.0 + c['position_lines'] / cs,
+                        int(info.get('bytes') or csr.nnz * 32), POS_LINES)
+                else:
+                    # rejection: the row pair, a line per proposal block, a bucket per test
+                    extra['random_line_roofline'] = dependent_line_roofline(
+                        steps, kern_s, 1.0 + (c['blocks'] + c['tests']) / cs, csr.nnz * 4,
+                        'row pair + proposal blocks + hash buckets')
             gbs = nbytes / kern_s / 1e9
             walk_roof[meth] = dict({'kernel_ms': kern_s * 1e3, 'walks': n_walks, 'bytes': nbytes,
                                     'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -1175,7 +1446,17 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
                         'frac': gbs / HBM_PEAK_GBS, 'p': p, 'q': q,
                         'bytes_per_step': c['bytes'] / max(c['steps'], 1),
                         'hash_probes_per_step': c['probes'] / max(c['steps'], 1),
-                        'list_entries_per_step': c['entries'] / max(c['steps'], 1)}
+                        'list_entries_per_step': c['entries'] / max(c['steps'], 1),
+                        'walker': w.last_walker}
+                    if w.last_walker == 'dw_walk_replay_positions':
+                        # one lane per walker: the 32-B edge record, then the exact pick's
+                        # dependent position probes (2-B units; the rare serial picks' run
+                        # loads counted with them); the step's uniform is an independent load
+                        info = csr.device_tensors(dev).get('n2v_index_info') or {}
+                        walk_roof['node2vec_replay']['random_line_roofline'] = \
+                            dependent_line_roofline(
+                                c['steps'], kern_s, 1.0 + c['lines'] / max(c['steps'], 1),
+                                int(info.get('bytes') or csr.nnz * 32), POS_LINES)
                 del out, u_dev, u
 
     result = {
@@ -1319,8 +1600,8 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
                 'value': s64['pairs_per_s'], 'unit': 'positive-pairs/s', 'cores': cb['cores'],
                 'kind': 'port', 'sample': (f'the oracle SGNS step at 64 walks/step ({s64["steps"]} '
                                            f'steps, {s64["seconds"]:.1f}s; see cpu_baseline)')}
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    if rank == 0:   # printed by main (after the c5 part)
+        _RESULT['line'] = result
     failed = bool(step_check) and not step_check['ok']
     if b64 is not None and not b64['step_check']['ok']:
         log(rank, f'[bench] batch64 step check FAILED: {b64["step_check"]}')

@@ -400,6 +400,9 @@ int dw::adam_rows_launch(float *param, float *exp_avg, float *exp_avg_sq, int32_
     DW_REQUIRE(!(p_only && grad_rows), "dw_adam_rows: p_only replays carry no gradient step");
     DW_REQUIRE(!(p_only && pending), "dw_adam_rows: p_only replays do not settle pending rows");
     DW_REQUIRE(!grad_by_row || grad_rows, "dw_adam_rows: grad_by_row needs the gradient table");
+    // a pending row current to `step` would be settled and then stepped a second time
+    DW_REQUIRE(!(pending && grad_rows), "dw_adam_rows: pending rows are settled without a "
+               "gradient step (flush); step them through the rows-major out step");
     // even d: two elements per thread on the packed instructions
     const bool pair = dim % 2 == 0;
     const int threads = pair ? 64 * ((dim / 2 + 63) / 64) : 64 * ((dim + 63) / 64);

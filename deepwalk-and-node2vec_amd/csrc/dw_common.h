@@ -125,11 +125,12 @@ struct AdamScalars {
 
 // sqrt(v) / bias_correction2_sqrt, bit for bit the IEEE quotient: with y = RN(1 / c) computed on
 // the host, q = x y, the remainder r = fma(-c, q, x) is exact and fma(r, y, q) is the correctly
-// rounded x / c (Markstein) for x in [2^-64, 2^64] — checked on MI355X against the division for
-// every step's c of 200,000 steps (beta2 .999) and 20,000 (beta2 .99), 65,536 x per step over
-// that range, no mismatch (scripts/microbench/div_check.hip). Three operations for the ~12 of
-// the IEEE sequence (its rcp is quarter rate): the lazy replays are ALU-bound on these steps.
-// Outside the range, or without y, the wave divides (the same bits either way).
+// rounded x / c (Markstein) for x in [2^-64, 2^64] — proved on MI355X for every fp32 mantissa
+// and every step's c at beta2 .999 and .99 (1.53e11 checks, 0 mismatches: scripts/microbench/
+// div_proof.py, profiles/r05_div_proof.jsonl); the host writes y into the history only for those
+// betas (sharding.RECIPROCAL_PROVEN_BETA2), else 0. Three operations for the ~12 of the IEEE
+// sequence (its rcp is quarter rate): the lazy replays are ALU-bound on these steps. Outside the
+// range, or without y, the wave divides (the same bits either way).
 __device__ __forceinline__ float div_bc2s(float x, const AdamScalars &s) {
 #pragma clang fp contract(off)
     const bool ok = s.rbc2s != 0.f && ((x >= 0x1p-64f && x <= 0x1p64f) || x == 0.f);
@@ -489,8 +490,15 @@ __device__ __forceinline__ int64_t fixed_finish(int64_t acc, int64_t n_terms) {
     return static_cast<int64_t>(static_cast<uint64_t>(acc) -
                                 static_cast<uint64_t>(n_terms) * 0x4338000000000000ULL);
 }
-__device__ __forceinline__ bool fixed_range(float tmax, double fs) {
-    return !(static_cast<double>(tmax) * fs < 0x1p51);
+// The run's largest |t| is tracked as its bit pattern (fixed_track): an unsigned max orders NaN
+// above +inf above every finite |t|, so a NaN term is kept (fmaxf would drop it) and fails the
+// range test like an infinite or too large one.
+__device__ __forceinline__ uint32_t fixed_track(uint32_t tbits, float t) {
+    const uint32_t b = __float_as_uint(t) & 0x7FFFFFFFu;
+    return b > tbits ? b : tbits;
+}
+__device__ __forceinline__ bool fixed_range(uint32_t tbits, double fs) {
+    return !(static_cast<double>(__uint_as_float(tbits)) * fs < 0x1p51);
 }
 
 __device__ __forceinline__ float from_fixed(int64_t a, double fi) {

@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
     __shared__ float4 s_g[WAVES_PER_BLOCK][4][EXACT ? 1 : 16 * F4];
     __shared__ int64_t s_gx[WAVES_PER_BLOCK][EXACT ? D : 1];   // EXACT: one centre's sums
     bool range = false;   // EXACT: a term past the fixed-point range
-    float tmax = 0.f;     // EXACT: the largest |term| (the range test, once at the end)
+    uint32_t tmax = 0u;   // EXACT: the largest |term|'s bits (the range test, once at the end)
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
     const int q = lane >> 4, gl = lane & 15;
@@ -638,8 +638,8 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, CHR >= 8 ? 3 : G16_MIN_
                         gx[4 * f + 1] += dw::fixed_bits(t1, fs);
                         gx[4 * f + 2] += dw::fixed_bits(t2, fs);
                         gx[4 * f + 3] += dw::fixed_bits(t3, fs);
-                        tmax = fmaxf(fmaxf(tmax, fmaxf(fabsf(t0), fabsf(t1))),
-                                     fmaxf(fabsf(t2), fabsf(t3)));
+                        tmax = dw::fixed_track(dw::fixed_track(tmax, t0), t1);
+                        tmax = dw::fixed_track(dw::fixed_track(tmax, t2), t3);
                     }
                     continue;
                 }
@@ -905,7 +905,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                  int32_t d, OutAdam oa, const int64_t *__restrict__ range, int32_t gch,
                  dw::Fixed fo, int32_t *status) {
     bool fx_range = false;
-    float fx_tmax = 0.f;   // EXACT: the largest |term| (the range test, once at the end)
+    uint32_t fx_tmax = 0u;   // EXACT: the largest |term|'s bits (the range test, at the end)
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t lo = range ? range[0] : 0;
@@ -1012,7 +1012,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
                     if constexpr (EXACT) {
                         const float t = coef[u] * x[u][m];
                         gx[m] += dw::fixed_bits(t, fo.fs);
-                        fx_tmax = fmaxf(fx_tmax, fabsf(t));
+                        fx_tmax = dw::fixed_track(fx_tmax, t);
                     } else {
                         g[m] += coef[u] * x[u][m];
                     }
@@ -1515,7 +1515,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
     constexpr int D = 64 * F4;
     constexpr int BR = WAVES_PER_BLOCK * WAVE;   // records per block range, at most
     bool fx_range = false;
-    float fx_tmax = 0.f;   // EXACT: the largest |term| (the range test, once at the end)
+    uint32_t fx_tmax = 0u;   // EXACT: the largest |term|'s bits (the range test, at the end)
     constexpr int RU = 4;   // records per round (one per 16-lane group)
     // the block range's records (slot, centre node, context flag) and its rows' starts
     __shared__ uint32_t s_key[BR], s_slot[BR];
@@ -1692,7 +1692,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                         for (int f = 0; f < F4; ++f) {
                             const float t = cu * cr[lane + 64 * f];
                             gx[f] += dw::fixed_bits(t, fo.fs);
-                            fx_tmax = fmaxf(fx_tmax, fabsf(t));
+                            fx_tmax = dw::fixed_track(fx_tmax, t);
                         }
                     } else {
 #pragma unroll

@@ -1627,10 +1627,23 @@ __device__ int64_t n2v_pick_serial_runs(PosList P, int64_t C, int64_t pt, int64_
     return k < 0 ? n - 1 : k;                                         // bisect_right(.., 0, n-1)
 }
 
+// lines (counted launches; NULL otherwise): += the 128-B lines the search's dependent loads
+// move to — a probe in the line of the one before it is a cache hit, not another random line
 template <bool EXACT = true>
 __device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt, int64_t n,
                                                 double U, double ip, double iq,
-                                                uint32_t &loads) {   // loads: += 2-B units read (1 per uint16 entry, 2 per int32)
+                                                uint32_t &loads,   // += 2-B units read (1 per uint16 entry, 2 per int32)
+                                                uint32_t *lines = nullptr) {
+    uint64_t last_line = ~0ull;
+    auto touch = [&](int64_t i) {
+        if (!lines) return;
+        const uint64_t ln = (reinterpret_cast<uint64_t>(P.p) + static_cast<uint64_t>(i) *
+                                                                   (P.wide ? 4u : 2u)) >> 7;
+        if (ln != last_line) {
+            ++*lines;
+            last_line = ln;
+        }
+    };
     const int64_t A = pt >= 0 ? 1 : 0;
     const double T = n2v_w(A, n - A - C, C, ip, iq);
     const double UT = U * T;
@@ -1644,6 +1657,7 @@ __device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         loads += P.wide ? 2u : 1u;
+        touch(mid);
         if (D(P[mid], mid + 1) > 0.0)
             hi = mid;
         else
@@ -1652,7 +1666,10 @@ __device__ __forceinline__ int64_t n2v_pick_pos(PosList P, int64_t C, int64_t pt
     const int64_t j = lo;
     const int64_t pj = j < C ? P[j] : n - 1;   // D(pj) > 0
     int64_t a = j > 0 ? P[j - 1] + 1 : 0;       // D(P[j-1]) <= 0
-    if (j > 0) loads += P.wide ? 2u : 1u;
+    if (j > 0) {
+        loads += P.wide ? 2u : 1u;
+        touch(j - 1);
+    }
     int64_t b = pj;
     while (a < b) {                   // i < pj: c_i = j
         const int64_t mid = (a + b) >> 1;
@@ -1690,7 +1707,7 @@ __global__ void __launch_bounds__(256)
     const int tid = threadIdx.x;
     const int64_t n_chunks = (n_walks + 255) / 256;
     const int64_t UL = L - 1;
-    uint32_t loads = 0, steps = 0, serial = 0;
+    uint32_t loads = 0, steps = 0, serial = 0, lines = 0;
     for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
         const int64_t w0 = ch * 256;
         const int n_here = (n_walks - w0 < 256) ? static_cast<int>(n_walks - w0) : 256;
@@ -1734,7 +1751,8 @@ __global__ void __launch_bounds__(256)
                         const int64_t C = prev < 0 ? 0 : (cw & 0x7FFFFFFFu);
                         const int64_t ptv = (prev >= 0 && (cw >> 31)) ? pt : -1;
                         int64_t k = prev < 0 ? uniform_pick_exact(U, n)
-                                             : n2v_pick_pos(PL, C, ptv, n, U, ip, iq, loads);
+                                             : n2v_pick_pos(PL, C, ptv, n, U, ip, iq, loads,
+                                                            COUNT ? &lines : nullptr);
                         if (k < 0) {   // the margin cannot decide: the reference's arithmetic
                             k = n2v_pick_serial_runs(PL, C, ptv, n, U, ip, iq, loads);
                             if (COUNT) ++serial;
@@ -1771,16 +1789,17 @@ __global__ void __launch_bounds__(256)
         }
     }
     if (COUNT) {   // per step the 32-B record, the uniform and the output (44 B); the positions
-                   // read (2-B units); the serial picks
-        unsigned long long v2[3] = {(unsigned long long)loads, (unsigned long long)steps,
-                                    (unsigned long long)serial};
-        for (int k = 0; k < 3; ++k)
+                   // read (2-B units); the serial picks; the searches' line moves
+        unsigned long long v2[4] = {(unsigned long long)loads, (unsigned long long)steps,
+                                    (unsigned long long)serial, (unsigned long long)lines};
+        for (int k = 0; k < 4; ++k)
             for (int off = WAVE / 2; off > 0; off >>= 1) v2[k] += __shfl_xor(v2[k], off, WAVE);
         if ((tid & (WAVE - 1)) == 0) {
             atomicAdd(counters + 0, v2[0] * 2ull + v2[1] * 44ull);
             atomicAdd(counters + 1, v2[2]);
             atomicAdd(counters + 2, v2[0]);
             atomicAdd(counters + 3, v2[1]);
+            atomicAdd(counters + 4, v2[3]);
         }
     }
 }
@@ -1902,8 +1921,8 @@ __global__ void __launch_bounds__(256)
 // Counter (walk id lo, hi, step << 8, TAG_N2V_POS); restated in oracle/philox.py
 // (fast_walks_positions). The next step's draw is computed while the record load is in flight.
 // COUNT: realised bytes (the 32-B record and 4-B output per step, 2 or 4 B per position load,
-// the start's row_ptr pair) and steps into counters[0], counters[1], the positions read in 2-B
-// units in counters[3].
+// the start's row_ptr pair) and steps into counters[0], counters[1], the searches' 128-B line
+// moves in counters[2], the positions read in 2-B units in counters[3].
 template <bool COUNT>
 __global__ void __launch_bounds__(256)
     k_walk_node2vec_positions(const int64_t *__restrict__ row_ptr, const int4 *__restrict__ rec,
@@ -1914,7 +1933,7 @@ __global__ void __launch_bounds__(256)
                               const dw_step_scalars *__restrict__ dyn,
                               unsigned long long *counters) {
     const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    uint32_t loads = 0, steps = 0;
+    uint32_t loads = 0, steps = 0, lines = 0;
     if (w < n_walks) {
         const uint64_t wid = (dyn ? dyn->walk_id0 : walk_id0) + static_cast<uint64_t>(w);
         int32_t *o = out + w * (int64_t)L;
@@ -1949,7 +1968,7 @@ __global__ void __launch_bounds__(256)
                                  0x1p-53;
                 k = n2v_pick_pos<false>(PosList{pos + p_off, n > N2V_U16_MAX_DEG},
                                         cw & 0x7FFFFFFFu, (cw >> 31) ? pt : -1, n, U, ip, iq,
-                                        loads);
+                                        loads, COUNT ? &lines : nullptr);
             }
             const int64_t e = a + k;
             const int4 r0 = rec[2 * e], r1 = rec[2 * e + 1];
@@ -1984,16 +2003,17 @@ __global__ void __launch_bounds__(256)
     }
     if (COUNT) {
         const int lane = threadIdx.x & (WAVE - 1);
-        unsigned long long v3[3] = {
+        unsigned long long v3[4] = {
             (unsigned long long)loads * 2ull + (unsigned long long)steps * 36ull +
                 (w < n_walks ? 20ull : 0ull),
-            (unsigned long long)steps, (unsigned long long)loads};
-        for (int k = 0; k < 3; ++k)
+            (unsigned long long)steps, (unsigned long long)lines, (unsigned long long)loads};
+        for (int k = 0; k < 4; ++k)
             for (int off = WAVE / 2; off > 0; off >>= 1) v3[k] += __shfl_xor(v3[k], off, WAVE);
         if (lane == 0) {
             atomicAdd(counters + 0, v3[0]);
             atomicAdd(counters + 1, v3[1]);
-            atomicAdd(counters + 3, v3[2]);
+            atomicAdd(counters + 2, v3[2]);
+            atomicAdd(counters + 3, v3[3]);
         }
     }
 }

@@ -249,12 +249,61 @@ class CSRGraph:
             d['edge_cn'] = cn
         if need_n2v_index:
             info = d.get('n2v_index_info') or {}
-            # (a skipped index is tried again under a larger budget: the Philox walker asks with
-            # a small one, the exact walker with the default)
-            if 'n2v_rec' not in d or (d['n2v_rec'] is None and
-                                      self._n2v_budget(dev, n2v_budget) > info.get('budget', 0)
-                                      and not info.get('unsupported')):
+            # a skipped index is tried again only when a larger cap is asked for (the exact
+            # walker's default after a smaller explicit one) — not because free memory grew (an
+            # out-of-memory skip empties the cache, which would retry the whole build at every
+            # call) and never inside a graph capture
+            cap = self.N2V_INDEX_BYTES if n2v_budget is None else int(n2v_budget)
+            if 'n2v_rec' not in d or (d['n2v_rec'] is None and cap > info.get('cap', 0)
+                                      and not info.get('unsupported')
+                                      and not torch.cuda.is_current_stream_capturing()):
                 self._build_n2v_index(dev, n2v_budget)
+        return d
+
+    def philox_positions(self, device=None) -> bool:
+        """Whether rng='philox' node2vec (layout='indexed') walks over the position index
+        (dw_walk_fast_positions) or by rejection (dw_walk_fast_indexed) on this graph: the two
+        use the Philox stream differently, so they give different walks, and the choice must not
+        depend on the device's free memory. It is decided once per graph and device from the
+        graph alone — the index's size (entries + records, a function of the graph) against
+        N2V_PHILOX_INDEX_BYTES — and cached; the index is then built without the free-memory
+        cap (torch.OutOfMemoryError if it cannot be; layout='hash' selects the rejection walker
+        explicitly). Weighted graphs and rows with a repeated neighbour keep the rejection
+        walker."""
+        dev = _native.require_device(device)
+        d = self.device_tensors(dev)
+        if 'philox_positions' in d:
+            return d['philox_positions']
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError('the Philox node2vec walker is chosen (and its index built) '
+                               'before a graph capture: walk once first')
+        use = False
+        if self.weights is None and self.is_simple(dev) and 16 * (self.nnz + 1) <= \
+                self.N2V_PHILOX_INDEX_BYTES:
+            info = d.get('n2v_index_info') or {}
+            if 'bytes' not in info:   # the size is known once the offsets have been scanned
+                self._build_n2v_index(dev, self.N2V_PHILOX_INDEX_BYTES, fixed=True)
+                info = d['n2v_index_info']
+            use = not info.get('unsupported') and info['bytes'] <= self.N2V_PHILOX_INDEX_BYTES
+            if use and d.get('n2v_rec') is None:
+                self._build_n2v_index(dev, info['bytes'], fixed=True)
+        d['philox_positions'] = use
+        return use
+
+    def require_n2v_index(self, device=None) -> Dict[str, torch.Tensor]:
+        """The position index built whatever its size (layout='positions'): OutOfMemoryError
+        when the device cannot hold it, ValueError on a weighted graph or a repeated
+        neighbour."""
+        dev = _native.require_device(device)
+        if self.weights is not None:
+            raise ValueError('the node2vec position index needs an unweighted graph')
+        self.require_simple(dev)
+        d = self.device_tensors(dev)
+        if d.get('n2v_rec') is None:
+            self._build_n2v_index(dev, 1 << 62, fixed=True)
+            if d.get('n2v_rec') is None:
+                raise ValueError(f'the node2vec position index cannot be built for this graph: '
+                                 f'{d.get("n2v_index_info")}')
         return d
 
     # the position index is built when its entries, records and build scratch fit this many
@@ -279,7 +328,7 @@ class CSRGraph:
         cap = self.N2V_INDEX_BYTES if budget is None else int(budget)
         return min(cap, torch.cuda.mem_get_info(dev)[0] - self.N2V_INDEX_RESERVE)
 
-    def _build_n2v_index(self, dev, budget: Optional[int] = None) -> None:
+    def _build_n2v_index(self, dev, budget: Optional[int] = None, fixed: bool = False) -> None:
         """n2v_rec int32[nnz, 8] / n2v_pos uint8[bytes] (dw_n2v_edge_offsets +
         dw_n2v_edge_index_build + dw_n2v_edge_records): per directed edge t -> v, t's position in
         N(v) and the sorted positions of N(t) ∩ N(v) — uint16 where deg(v) <= 65536, else int32 —
@@ -288,13 +337,16 @@ class CSRGraph:
         scratch stays bounded while the index grows to the graph's size (C5: 132 GB). Both None
         when the index would exceed the byte budget; n2v_index_info = {'entries', 'bytes',
         'chunks', 'budget', 'build_ms'} or {'entries', 'bytes', 'skipped', 'budget'}; ``budget``:
-        its byte budget (_n2v_budget)."""
+        its byte budget (_n2v_budget). ``fixed`` (philox_positions): the index is built when its
+        own bytes fit ``budget``, whatever the device's free memory, and an allocation failure
+        raises instead of skipping."""
         import ctypes
         import time
         d = self.device_tensors(dev, need_edge_cn=True)
         E = self.nnz
         colp = _native.ptr(d['col']) if E else None
-        budget_b = self._n2v_budget(dev, budget)
+        budget_b = int(budget) if fixed else self._n2v_budget(dev, budget)
+        cap = self.N2V_INDEX_BYTES if budget is None else int(budget)
         with torch.cuda.device(dev):
             s = _native.stream(dev)
             t0 = time.perf_counter()
@@ -309,9 +361,11 @@ class CSRGraph:
                 _native.call('dw_n2v_edge_offsets', *oargs, None, ctypes.byref(nb), s)
                 tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
             except torch.OutOfMemoryError:   # the wave walker needs none of it
+                if fixed:
+                    raise
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = {'skipped': True, 'out_of_memory': True,
-                                       'budget': budget_b}
+                                       'budget': budget_b, 'cap': cap}
                 torch.cuda.empty_cache()
                 return
             _native.call('dw_n2v_edge_offsets', *oargs, _native.ptr(tmp), ctypes.byref(nb), s)
@@ -343,9 +397,9 @@ class CSRGraph:
             index_bytes = n_bytes + 32 * E
             need = index_bytes + 4 * E + 4 * max_pos + tmp_need
             skipped = {'entries': n_pos, 'bytes': index_bytes, 'build_bytes': need,
-                       'skipped': True, 'budget': budget_b,
+                       'skipped': True, 'budget': budget_b, 'cap': cap,
                        'unsupported': not fits}
-            if not fits or need > budget_b:
+            if not fits or (index_bytes if fixed else need) > budget_b:
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = skipped
                 return
@@ -356,6 +410,8 @@ class CSRGraph:
                 scratch = torch.empty(max(max_pos, 1), dtype=torch.int32, device=dev)
                 tmp = torch.empty(tmp_need, dtype=torch.uint8, device=dev)
             except torch.OutOfMemoryError:   # the wave walker needs none of it
+                if fixed:
+                    raise
                 d['n2v_rec'], d['n2v_pos'] = None, None
                 d['n2v_index_info'] = dict(skipped, out_of_memory=True)
                 torch.cuda.empty_cache()
@@ -373,6 +429,7 @@ class CSRGraph:
             _native.check_status(d['status'], 'node2vec position index build')
             d['n2v_rec'], d['n2v_pos'] = rec, pos
             d['n2v_index_info'] = {'entries': n_pos, 'bytes': index_bytes,
+                                   'build_bytes': need, 'cap': cap,
                                    'chunks': len(chunks), 'budget': budget_b,
                                    'build_ms': (time.perf_counter() - t0) * 1e3}
 

@@ -125,7 +125,9 @@ class RandomWalk(ABC):
                 dw_walk_fast_indexed, one dependent load per step; node2vec on an unweighted
                 graph over the per-edge position index, dw_walk_fast_positions — one Philox
                 uniform and a search of the step's positions, no rejection rounds — where the
-                index fits (CSRGraph.N2V_INDEX_BYTES), else as 'hash'), 'hash' (node2vec by
+                index is small enough — CSRGraph.philox_positions, decided from the graph's
+                size alone — else as 'hash'), 'positions' (node2vec over the index whatever its
+                size, e.g. C5's 132 GB; an error where it cannot be built), 'hash' (node2vec by
                 rejection with the adjacency tests in the per-row hash, dw_walk_fast_indexed) or
                 'csr' (dw_walk_fast: row_ptr / col, node2vec's tests by search of the sorted
                 lists; the same walks as 'hash' bit for bit). The position walker samples the
@@ -136,8 +138,12 @@ class RandomWalk(ABC):
         assert length >= 1, 'Minimum walk length is 1!'
         if rng not in ('python', 'philox'):
             raise ValueError(f'unknown rng "{rng}" (expected "python" or "philox")')
-        if layout not in ('indexed', 'hash', 'csr'):
-            raise ValueError(f'unknown layout "{layout}" (expected "indexed", "hash" or "csr")')
+        if layout not in ('indexed', 'hash', 'csr', 'positions'):
+            raise ValueError(f'unknown layout "{layout}" (expected "indexed", "hash", "csr" or '
+                             f'"positions")')
+        if layout == 'positions' and (rng != 'philox' or self.METHOD != _native.DW_METHOD_NODE2VEC):
+            raise ValueError("layout='positions' is the Philox node2vec walker's")
+        self.last_walker = None   # the kernel of the last walk_batch call
         self._layout = layout
         self._graph = graph
         self._length = length
@@ -222,7 +228,7 @@ class RandomWalk(ABC):
         # replay: the CSR, adjacency by search of the sorted lists; philox: DeepWalk over the
         # edge-inline CSR, node2vec with the per-row adjacency hash (the same walks as
         # dw_walk_fast, bit for bit; layout='csr' selects that one)
-        indexed = self._rng == 'philox' and self._layout in ('indexed', 'hash')
+        indexed = self._rng == 'philox' and self._layout in ('indexed', 'hash', 'positions')
         # Philox node2vec on an unweighted graph: over the position index where it fits
         pos_fast = self._positions_walker(dev)
         # replay, DeepWalk on an unweighted graph: the same walks over the edge-inline CSR
@@ -263,6 +269,7 @@ class RandomWalk(ABC):
                     raise ValueError('uniforms must have n_walks * (length - 1) values')
                 u = u.to(dev)
                 if replay_inline:
+                    self.last_walker = 'dw_walk_replay_inline'
                     _native.call('dw_walk_replay_inline', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['edges']), self._csr.vocab_size,
                                  _native.ptr(starts), n, L,
@@ -271,6 +278,7 @@ class RandomWalk(ABC):
                 elif replay_n2v_idx:
                     self._replay_n2v(d, starts, n, u, out, status, None, s)
                 else:
+                    self.last_walker = 'dw_walk_replay'
                     _native.call('dw_walk_replay', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d.get('col_sorted')),
                                  _native.ptr(d['weights']), self._csr.vocab_size,
@@ -282,12 +290,14 @@ class RandomWalk(ABC):
             else:
                 wid0 = self._next_walk_id if walk_id0 is None else int(walk_id0)
                 if pos_fast:
+                    self.last_walker = 'dw_walk_fast_positions'
                     _native.call('dw_walk_fast_positions', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['n2v_rec']), _native.ptr(d['n2v_pos']),
                                  self._csr.vocab_size, _native.ptr(starts), n, L, float(p),
                                  float(q), self._seed & 0xFFFFFFFFFFFFFFFF, wid0,
                                  _native.ptr(out), _native.ptr(status), None, s)
                 elif indexed:
+                    self.last_walker = 'dw_walk_fast_indexed'
                     _native.call('dw_walk_fast_indexed', _native.ptr(d['row_ptr']),
                                  _native.ptr(d['col']), _native.ptr(d.get('edges')),
                                  _native.ptr(d.get('adj_off')), _native.ptr(d.get('adj_hash')),
@@ -297,6 +307,7 @@ class RandomWalk(ABC):
                                  self._seed & 0xFFFFFFFFFFFFFFFF, wid0, _native.ptr(out),
                                  _native.ptr(status), s)
                 else:
+                    self.last_walker = 'dw_walk_fast'
                     _native.call('dw_walk_fast', _native.ptr(d['row_ptr']), _native.ptr(d['col']),
                                  _native.ptr(d.get('col_sorted')), _native.ptr(d.get('prob_thr')),
                                  _native.ptr(d.get('alias')), self._csr.vocab_size,
@@ -309,17 +320,17 @@ class RandomWalk(ABC):
         return out
 
     def _positions_walker(self, dev) -> bool:
-        """rng='philox', node2vec, layout='indexed', unweighted, simple rows: True when the
-        per-edge position index is (or can be) built for this graph and device — then
-        dw_walk_fast_positions walks; else the rejection walker over the adjacency hash."""
-        if not (self._rng == 'philox' and self.METHOD == _native.DW_METHOD_NODE2VEC
-                and self._layout == 'indexed' and self._csr.weights is None):
+        """rng='philox', node2vec: True when dw_walk_fast_positions walks — layout='positions'
+        (the index built whatever its size, or an error), or layout='indexed' on a graph whose
+        index is small enough (CSRGraph.philox_positions: decided once per graph from its size,
+        never from the device's free memory, so the same seed gives the same walks on any
+        device); else the rejection walker over the adjacency hash."""
+        if not (self._rng == 'philox' and self.METHOD == _native.DW_METHOD_NODE2VEC):
             return False
-        if not self._csr.is_simple(dev):   # a repeated neighbour: the index assumes simple rows
-            return False
-        budget = min(self._csr.N2V_PHILOX_INDEX_BYTES, torch.cuda.mem_get_info(dev)[0] // 4)
-        d = self._csr.device_tensors(dev, need_n2v_index=True, n2v_budget=budget)
-        return d.get('n2v_rec') is not None
+        if self._layout == 'positions':
+            self._csr.require_n2v_index(dev)
+            return True
+        return self._layout == 'indexed' and self._csr.philox_positions(dev)
 
     def count_replay_traffic(self, start_ids: torch.Tensor, uniforms: torch.Tensor,
                              out: Optional[torch.Tensor] = None) -> dict:
@@ -327,7 +338,7 @@ class RandomWalk(ABC):
         uniforms)`` with the replay walker's realised traffic counted (dw_walk_replay_indexed
         with counters; a diagnostic launch): {'bytes', 'probes', 'entries', 'steps'} (over the
         position index: 'probes' counts the picks made by the serial arithmetic, 'entries' the
-        2-B position units read)."""
+        2-B position units read, 'lines' the searches' dependent 128-B line moves)."""
         if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'python' \
                 or self._csr.weights is not None:
             raise ValueError('count_replay_traffic: node2vec with rng="python", unweighted')
@@ -344,12 +355,12 @@ class RandomWalk(ABC):
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
-        counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        counters = torch.zeros(5, dtype=torch.int64, device=dev)
         with torch.cuda.device(dev):
             self._replay_n2v(d, starts, n, u, out, status, counters, _native.stream(dev))
         _native.check_status(status, f'{type(self).__name__}.count_replay_traffic')
         c = counters.cpu().tolist()
-        return {'bytes': c[0], 'probes': c[1], 'entries': c[2], 'steps': c[3]}
+        return {'bytes': c[0], 'probes': c[1], 'entries': c[2], 'steps': c[3], 'lines': c[4]}
 
     def _replay_n2v(self, d, starts, n, u, out, status, counters, s) -> None:
         """The exact node2vec walks on an unweighted graph: over the position index when it is
@@ -363,11 +374,13 @@ class RandomWalk(ABC):
                   _native.ptr(d.get('edge_cn') if _edge_cn_enabled() else None)]
         uptr = _native.ptr(u) if u.numel() else None
         if _n2v_index_enabled() and d.get('n2v_rec') is not None:
+            self.last_walker = 'dw_walk_replay_positions'
             _native.call('dw_walk_replay_positions', _native.ptr(d['row_ptr']),
                          _native.ptr(d['n2v_rec']), _native.ptr(d['n2v_pos']),
                          self._csr.vocab_size, _native.ptr(starts), n, L, float(p), float(q),
                          uptr, _native.ptr(out), _native.ptr(status), _native.ptr(counters), s)
             return
+        self.last_walker = 'dw_walk_replay_indexed'
         _native.call('dw_walk_replay_indexed', *common, self._csr.vocab_size,
                      _native.ptr(starts), n, L, float(p), float(q), uptr, _native.ptr(out),
                      _native.ptr(status), _native.ptr(counters), s)
@@ -378,7 +391,7 @@ class RandomWalk(ABC):
         walkers' realised memory traffic counted (dw_walk_fast_counted; a diagnostic launch):
         {'bytes', 'steps', 'blocks', 'tests'} summed over the walks."""
         if self.METHOD != _native.DW_METHOD_NODE2VEC or self._rng != 'philox' \
-                or self._layout not in ('indexed', 'hash'):
+                or self._layout not in ('indexed', 'hash', 'positions'):
             raise ValueError('count_traffic: node2vec with rng="philox", layout="indexed" or '
                              '"hash"')
         dev = _native.require_device(self._device)
@@ -400,7 +413,8 @@ class RandomWalk(ABC):
             _native.check_status(status, f'{type(self).__name__}.count_traffic')
             c = counters.cpu().tolist()
             return {'bytes': c[0], 'steps': c[1], 'blocks': 0, 'tests': 0,
-                    'position_loads': c[3], 'walker': 'dw_walk_fast_positions'}
+                    'position_loads': c[3], 'position_lines': c[2],
+                    'walker': 'dw_walk_fast_positions'}
         d = self._csr.device_tensors(dev, need_alias=True, need_adj=True)
         if out is None:
             out = torch.empty((n, L), dtype=torch.int32, device=dev)

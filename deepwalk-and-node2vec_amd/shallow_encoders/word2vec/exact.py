@@ -21,9 +21,12 @@ Cost: two int64 atomics or adds per term instead of one float FMA, the accumulat
 table entry) and one conversion of the sums (on the one-GPU dense path fused into the in-table
 Adam: DW_EXACT_ADAM); bench.py --deterministic measures it.
 Covered: the records (sorted) output path of dw_sgns_walks_phase / dw_sgns_pairs (skip-gram),
-the fused output-table Adam, the owner layout (the centre sums reduce-scattered as int64).
+the fused output-table Adam, the owner layout (the centre sums reduce-scattered as int64), and
+the lazy Adam tables (OwnerLazyTables.enable_exact: the rows-major out step's k_out_rows and
+the COEFIN centre pass sum as integers, the pipelined steps included; at N > 1 the touched in
+rows' sums are all-reduced as int64 and converted on every rank alike).
 Not covered (refused): the atomic output scatter, pooled (CBOW) inputs, the replicated N > 1
-layout's row pieces, the lazy Adam tables.
+layout's row pieces.
 """
 import os
 from typing import Dict, List, Optional

@@ -950,8 +950,9 @@ class OwnerLazyTables(OwnerTables):
         self._betas0 = tuple(self.betas)
         self._out_rows = None
         self._n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
-        # one rank: the records placed by the claim (no sort before the lazy gather)
-        self.place = self.lazy_out and not self.multi
+        # the records placed by the claim (no sort before the lazy gather; N > 1: each rank
+        # places its own o % W slots into its slice's row segments)
+        self.place = self.lazy_out
         # any step with weight decay: the p-only catch-up no longer holds
         self._wd_seen = False
         # placed records: the rows-major step (dw_sgns_owner_out_rows) reads and writes each
@@ -978,19 +979,22 @@ class OwnerLazyTables(OwnerTables):
                 and 2 * int(context_radius) * (1 + int(neg_samples)) <= 64)
 
     def enable_exact(self, grad_scale: float) -> None:
-        """The deterministic mode (word2vec/exact.py) on one rank with the HIP lazy Adam of both
-        tables: grads_in and g_out get int64 fixed-point accumulators, so the rows-major step
-        sums every out row's terms (k_out_rows) and every centre's (the COEFIN pass) as integers
-        — the same sums whatever order the claim's atomics ranked the records in — and the
-        tables are bit-identical run to run, and to the dense deterministic step's (the lazy
-        replays are the dense g = 0 steps bit for bit). N > 1 is not covered: the touched rows'
-        all-reduce is a float sum."""
+        """The deterministic mode (word2vec/exact.py) with the HIP lazy Adam of both tables:
+        grads_in and g_out get int64 fixed-point accumulators, so the rows-major step sums every
+        out row's terms (k_out_rows) and every centre's (the COEFIN pass) as integers — the same
+        sums whatever order the claim's atomics ranked the records in — and the tables are
+        bit-identical run to run, and to the dense deterministic step's (the lazy replays are
+        the dense g = 0 steps bit for bit). N > 1: each rank's centre sums stay integers
+        (DW_EXACT_DEFER), the touched rows' sums are all-reduced as int64 (exact) and converted
+        alike on every rank — the tables equal one rank's bit for bit."""
         from shallow_encoders.word2vec import exact
-        if self.multi or not self._hip() or not self.lazy_out:
-            raise NotImplementedError('the lazy deterministic mode covers one rank with the HIP '
-                                      'lazy Adam of both tables (lazy_out)')
+        if not self._hip() or not self.lazy_out:
+            raise NotImplementedError('the lazy deterministic mode covers the HIP lazy Adam of '
+                                      'both tables (lazy_out)')
+        if self.emulated:
+            raise NotImplementedError('the deterministic mode needs the real collectives')
         self._exact = exact.Registry()
-        self._exact.ensure(0, self.grads_in, grad_scale)
+        self._exact.ensure(0, self.grads_in, grad_scale, defer=self.multi)
         self._exact.ensure(1, self.g_out, grad_scale)
 
     def pipeline_ok(self, context_radius: int, neg_samples: int) -> bool:
@@ -1301,6 +1305,28 @@ class OwnerLazyTables(OwnerTables):
             # g_in row (dw_adam_rows grad_by_row, which clears it): no gather
             self._G = self.grads_in
             return
+        fx = self._exact.get(0) if getattr(self, '_exact', None) is not None else None
+        if self._hip() and multi and fx is not None:
+            # deterministic, N > 1: the touched rows' integer centre sums (deferred by pass 1),
+            # gathered and cleared, all-reduced as int64 on the side stream; update_touched
+            # converts them (the same floats on every rank as one rank's conversion)
+            if self._G is None or self._G.shape[0] < max(n_max, 1):
+                self._G = torch.empty((max(n_max, 1), self.d), dtype=torch.float32,
+                                      device=self.device)
+            self._n_event.synchronize()
+            n = int(self._n_host[0])
+            rows = self._touched[:n].long()
+            self._G64 = fx.acc.index_select(0, rows)
+            fx.acc.index_fill_(0, rows, 0)
+            self._G_n = n
+            if n > 0:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self._side):
+                    self._side.wait_event(ev)
+                    self._ar = dist.all_reduce(self._G64, op=dist.ReduceOp.SUM,
+                                               group=self.group, async_op=True)
+            return
         if self._hip():
             if self._G is None or self._G.shape[0] < max(n_max, 1):
                 self._G = torch.empty((max(n_max, 1), self.d), dtype=torch.float32,
@@ -1331,6 +1357,11 @@ class OwnerLazyTables(OwnerTables):
         if self._ar is not None:
             self._ar.wait()            # the current stream waits for the all-reduce
             self._ar = None
+        if getattr(self, '_G64', None) is not None:   # deterministic N > 1: convert the sums
+            n = self._G_n
+            if n > 0:
+                self._exact.get(0).convert(acc=self._G64, out=self._G[:n])
+            self._G64 = None
         self._rows(self._G, self.step_count)
 
     def flush(self) -> None:

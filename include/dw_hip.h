@@ -324,8 +324,9 @@ int dw_fixed_to_float(int64_t *acc, float *grad, int64_t n, int32_t frac, int32_
  * binary-searches that edge's positions (log2 C loads), the pick by the margin rule; a pick the
  * margin cannot decide is made by the reference's own fp64 arithmetic (sum, normalise,
  * accumulate, bisect_right) replayed run by run over the position list, O(C + log n) in the
- * walker's lane. counters: NULL, or uint64[4] (caller-zeroed) += {bytes, serial picks, position
- * 2-B units read, steps}. Replaces random_walk_generator.py:94-119 on unweighted graphs. */
+ * walker's lane. counters: NULL, or uint64[5] (caller-zeroed) += {bytes, serial picks, position
+ * 2-B units read, steps, the searches' dependent 128-B line moves (a probe in the line of the
+ * probe before it not counted)}. Replaces random_walk_generator.py:94-119 on unweighted graphs. */
 int dw_walk_replay_positions(const int64_t *row_ptr, const int32_t *n2v_rec,
                              const uint8_t *n2v_pos, int64_t n_rows, const int32_t *starts,
                              int64_t n_walks, int32_t walk_length, double p, double q,
@@ -388,7 +389,8 @@ int dw_walk_fast_counted(const int64_t *row_ptr, const int32_t *col, const int64
  * weight W_i = a_i/p + b_i + c_i/q exceeds U*T, U = 53 bits of (r.x, r.y), with the fp64
  * expressions of the exact replay's pick; Philox counter (walk id lo, hi, step << 8, 'NP').
  * Unweighted graphs (the index has no weights). counters: NULL, or uint64[4] += {load + store
- * bytes, steps, 0, position 2-B units read}. Reads walk_id0 from a bound dw_step_scalars block. */
+ * bytes, steps, the searches' dependent 128-B line moves, position 2-B units read}. Reads
+ * walk_id0 from a bound dw_step_scalars block. */
 int dw_walk_fast_positions(const int64_t *row_ptr, const int32_t *n2v_rec, const uint8_t *n2v_pos,
                            int64_t n_rows, const int32_t *starts, int64_t n_walks,
                            int32_t walk_length, double p, double q, uint64_t seed,
@@ -753,7 +755,9 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         and row r steps with grad_rows[r], which is cleared as it is read (one rank's touched
  *         rows: no gather);
  *   pending: NULL, or uint8 [n_table_rows] (dw_sgns_owner_out_rows): a listed row marked there
- *         first gets the parameter half of step last_step[r], and its mark is cleared. */
+ *         first gets the parameter half of step last_step[r], and its mark is cleared; only
+ *         with grad_rows NULL (a settle-and-replay: a gradient step on a pending row current to
+ *         `step` would apply that step twice) — DW_E_INVALID_ARG otherwise. */
 int dw_adam_rows(float *param, float *exp_avg, float *exp_avg_sq, int32_t *last_step,
                  uint8_t *pending, int64_t n_table_rows, int32_t dim, const uint32_t *rows,
                  const int64_t *n_rows_dev, int64_t n_rows_max, float *grad_rows,

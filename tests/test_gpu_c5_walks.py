@@ -5,8 +5,10 @@ index (uint16 / int32 lists, 132.6 GB, built in chunks).
   * the exact walker (dw_walk_replay_positions, the reference's pick law and arithmetic) equals
     the wave walker with the per-edge counts (DW_N2V_POS=0, the round-3 walker) bit for bit,
     from the largest hubs and from random nodes, uniforms drawn from numpy;
-  * the Philox walker over the index (dw_walk_fast_positions) equals its oracle
-    (oracle/philox.fast_walks_positions) on walks through the hubs.
+  * the exact walker equals the oracle's replay (oracle/walk_ref.py) bit for bit, its serial
+    picks on the hub's int32 lists included;
+  * the Philox walker over the index (dw_walk_fast_positions, layout='positions') equals its
+    oracle (oracle/philox.fast_walks_positions) on walks through the hubs.
 Skipped when the device cannot hold the index next to the graph (CSRGraph._build_n2v_index's
 budget)."""
 import numpy as np
@@ -64,13 +66,65 @@ def test_c5_exact_positions_walker_equals_wave_walker(c5_index, hip_device, monk
     assert (deg[got[:, 1:]] > 65_536).sum() > 100
 
 
+def test_c5_exact_walker_vs_oracle(c5_index, hip_device):
+    """The exact walker (dw_walk_replay_positions) against the oracle's replay
+    (walk_ref.walks_replay over the host CSR, numpy-backed, the undirected membership test) at
+    R-MAT 24 itself, bit for bit: walks from the 16 largest hubs (the 392,747-neighbour one
+    first), from 16 random nodes, and 16 walks from neighbours t of the largest hub H whose
+    first draw picks H and whose second draw lies exactly on a class boundary of the step
+    t -> H — a pick the margin cannot decide, so the lane's serial arithmetic decides it over
+    H's int32 position list (deg H > 65,536). A quarter of the other walks' second draws are on
+    boundaries too. The counted launch shows the serial picks were taken."""
+    from oracle import walk_ref
+    from shallow_encoders.graph.random_walk_generator import Node2Vec
+    csr = c5_index
+    rng = np.random.default_rng(29)
+    L = 8
+    g = walk_ref.ArrayCSR(csr.row_ptr, csr.host_col(), None, undirected=True)
+    deg = csr.degree()
+    hub = int(np.argmax(deg))
+    assert deg[hub] == 392_747
+    starts = list(_starts(csr, 16, 16, 13))
+    nb_h = np.asarray(g.neighbors(hub))
+    ts = rng.choice(nb_h, 16, replace=False)
+    starts += [int(t) for t in ts]
+    starts = np.asarray(starts, dtype=np.int32)
+    u = rng.random((starts.size, L - 1))
+    for w in range(32, starts.size):      # t -> H, then a boundary draw at H
+        t = int(starts[w])
+        nt = g.neighbors(t)
+        u[w, 0] = (nt.index(hub) + 0.5) / len(nt)
+        nbrs, wt = walk_ref.node2vec_weights(g, t, hub, P, Q)
+        k = int(rng.integers(0, len(nbrs) - 1))
+        u[w, 1] = float(np.sum(wt[:k + 1])) / float(np.sum(wt))
+    for w in range(1, 32, 4):             # boundary second draws elsewhere
+        s = int(starts[w])
+        v1 = int(walk_ref.walks_replay(g, [s], 2, 'node2vec', P, Q, u[w:w + 1, :1])[0, 1])
+        nbrs, wt = walk_ref.node2vec_weights(g, s, v1, P, Q)
+        if len(nbrs) >= 2:
+            k = int(rng.integers(0, len(nbrs) - 1))
+            u[w, 1] = float(np.sum(wt[:k + 1])) / float(np.sum(wt))
+    w = Node2Vec(csr, L, p=P, q=Q, device=hip_device)
+    got = w.walk_batch(torch.as_tensor(starts), uniforms=u).cpu().numpy()
+    assert w.last_walker == 'dw_walk_replay_positions'
+    ref = walk_ref.walks_replay(g, starts, L, 'node2vec', P, Q, u)
+    np.testing.assert_array_equal(got, ref)
+    assert (got[32:, 1] == hub).all()
+    c = w.count_replay_traffic(torch.as_tensor(starts), torch.from_numpy(u).to(hip_device))
+    print(f'C5 exact walker vs oracle: {starts.size} walks of {L}, serial picks {c["probes"]}')
+    assert c['probes'] > 0, c
+
+
 def test_c5_philox_positions_walker_vs_oracle(c5_index, hip_device):
     from shallow_encoders.graph.random_walk_generator import Node2Vec
     csr = c5_index
     starts = _starts(csr, 8, 8, 3)
     L = 6
-    w = Node2Vec(csr, L, p=P, q=Q, rng='philox', seed=21, device=hip_device)
+    w = Node2Vec(csr, L, p=P, q=Q, rng='philox', seed=21, device=hip_device,
+                 layout='positions')   # (C5's 132 GB index: above the 'indexed' size rule)
     got = w.walk_batch(torch.as_tensor(starts), walk_id0=1000).cpu().numpy()
+    assert w.last_walker == 'dw_walk_fast_positions'
+    assert not csr.philox_positions(hip_device)   # the default there: the rejection walker
     exp = ph.fast_walks_positions(csr.row_ptr, csr.host_col(), starts, L, P, Q, seed=21,
                                   walk_id0=1000)
     np.testing.assert_array_equal(got, exp)

@@ -198,6 +198,54 @@ def test_exact_lazy_rows_major_repeatable_and_equal_dense(form, hip_device):
         assert diff == 0, f'{name}: {diff} entries differ from the dense deterministic step'
 
 
+@pytest.mark.parametrize('path', ['dense', 'lazy'])
+@pytest.mark.parametrize('table', ['in', 'out'])
+@pytest.mark.parametrize('value', ['nan', 'huge'])
+def test_exact_range_flags_nan_and_huge_terms(path, table, value, hip_device):
+    """A gradient term past the fixed-point range — a NaN from a diverged row, or a finite term
+    with |t| 2^frac >= 2^51 — sets DW_S_FIXED_RANGE and the step's status check raises
+    OverflowError, in every EXACT kernel: 'dense' (ShardedTables: k_sgns_g16's centre sums over
+    out rows, k_rec_gather's out sums over centre rows), 'lazy' (the rows-major step: k_out_rows
+    over centre rows, the COEFIN centre pass over out rows). Element 0 of the other table is
+    zeroed, so the logits stay finite and moderate and only the terms carry the bad value (a NaN
+    would otherwise also poison the coefficient, a huge logit saturate it to 0)."""
+    from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables,
+                                                    owner_lazy_step, replicated_step)
+    V, d, R, K, L, n = 600, 128, 2, 2, 20, 16
+    g = torch.Generator().manual_seed(11)
+    walks = torch.randint(1, V, (n, L), generator=g, dtype=torch.int32)
+    node = int(walks[0, 5])
+    per = L - 2 * R
+    scale = 1.0 / (n * per * 2 * R)
+    w_in, w_out = sgns_ref.xavier_tables(V, d, seed=4)
+    w_in, w_out = torch.as_tensor(w_in).clone(), torch.as_tensor(w_out).clone()
+    bad = float('nan') if value == 'nan' else 2.0 ** 24   # 2^24 * coef * 2^frac >> 2^51
+    if table == 'in':
+        w_in[node, 0], w_out[:, 0] = bad, 0.0
+    else:
+        w_out[node, 0], w_in[:, 0] = bad, 0.0
+    acc = torch.zeros(4, dtype=torch.float64, device=hip_device)
+    st = torch.zeros(1, dtype=torch.int32, device=hip_device)
+    wk = walks.cuda()
+    if path == 'dense':
+        t = ShardedTables(V, d, hip_device, lr=0.01, init_seed=2)
+        t.load_(w_in.cuda(), w_out.cuda())
+        t.enable_exact(scale)
+        replicated_step(t, wk, R, K, seed=5, noise_offset=0, grad_scale=scale, loss_acc=acc,
+                        status=st)
+    else:
+        t = OwnerLazyTables(V, d, hip_device, lr=0.01, init_seed=2, emulate_world=1,
+                            lazy_out=True)
+        t.load_(w_in.cuda(), w_out.cuda())
+        t.enable_exact(scale)
+        assert t.rows_major_ok(R, K)
+        owner_lazy_step(t, wk, R, K, seed=5, noise_offset=0, grad_scale=scale, loss_acc=acc,
+                        status=st)
+    torch.cuda.synchronize()
+    with pytest.raises(OverflowError):
+        _native.check_status(st, f'{path} step')
+
+
 # ---- two ranks on one GPU (gloo), deterministic mode: bit-identical to one process ---------
 V2, D2, R2, K2, L2, NW2, STEPS2, LR2 = 900, 64, 2, 3, 14, 48, 4, 5e-3
 

@@ -412,19 +412,91 @@ def test_owner_lazy_single_rank_equals_dense(hip_device, lazy_out, wd):
         assert_no_row_drift(got, exp)
 
 
-def _lazy_run(rank, world, port, q):
+def _lazy_configure(lazy_out: bool, exact: bool):
+    """_lazy_vs_dense's configure: the rows-major out step is asserted (lazy_out: placed records
+    per owner slice, k_out_rows, the COEFIN centre pass) and the deterministic mode enabled."""
+    def cfg(t):
+        if lazy_out:
+            assert t.rows_major_ok(R2, K2)
+        if exact:
+            t.enable_exact(1.0 / (NW2 * (L2 - 2 * R2) * 2 * R2))
+    return cfg
+
+
+def _lazy_run(rank, world, port, q, lazy_out=False, exact=False):
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
         dist.init_process_group('gloo', rank=rank, world_size=world)
         snaps = []
-        t, acc = _lazy_vs_dense('cuda:0', _walks_all(), V2, D2, R2, K2, LR2, snaps=snaps)
+        t, acc = _lazy_vs_dense('cuda:0', _walks_all(), V2, D2, R2, K2, LR2, snaps=snaps,
+                                lazy_out=lazy_out, configure=_lazy_configure(lazy_out, exact))
+        assert t.multi and t.lazy_out == lazy_out and t._rows_step == lazy_out
         q.put((rank, t.w_in.cpu().numpy().copy(), t.full_w_out().cpu().numpy(),
                acc.cpu().numpy(), None, snaps))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # report, the parent asserts
         q.put((rank, None, None, None, repr(e), None))
+
+
+def _two_lazy_ranks(lazy_out: bool, exact: bool):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lazy_run, args=(r, 2, port, q, lazy_out, exact))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs
+    return res
+
+
+@pytest.mark.timeout(600)
+def test_owner_lazy_rows_major_two_ranks(hip_device):
+    """the reference's small-batch path at N > 1 — OwnerLazyTables(lazy_out)
+    on two ranks (gloo on one GPU) takes the rows-major out step per owner slice (each rank
+    places and steps only its o % 2 rows; the COEFIN centre pass forms its partial centre
+    gradients; the touched in rows all-reduced): both ranks gather the same state every step,
+    the loss terms sum to one process's, and every step from the state before it is at the
+    single-step bars (tests/stepcheck.py)."""
+    res = _two_lazy_ranks(True, False)
+    (_, i0, o0, a0, _, s0), (_, i1, o1, a1, _, s1) = res
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(o0, o1)
+    _, acc1 = _lazy_vs_dense(hip_device, _walks_all(), V2, D2, R2, K2, LR2, lazy_out=True)
+    np.testing.assert_allclose(a0 + a1, acc1.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    for a, b in zip(s0, s1):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    from stepcheck import check_trajectory
+    worst = check_trajectory('owner lazy rows-major 2 ranks', _init2(), s0, _walks_all(), R2,
+                             K2, 11, LR2, NW2 * (L2 - 2 * R2))
+    print({k: round(v, 3) for k, v in sorted(worst.items())})
+
+
+@pytest.mark.timeout(600)
+def test_owner_lazy_rows_major_two_ranks_deterministic_equal_one_process(hip_device):
+    """The deterministic mode at N > 1 on the lazy path: two ranks with the
+    rows-major out step, the in rows' integer centre sums all-reduced as int64 and converted on
+    every rank, end every step bit-identical to one process's deterministic lazy run — tables and
+    Adam state (flushed snapshots) and the final tables."""
+    snaps1 = []
+    t1, _ = _lazy_vs_dense(hip_device, _walks_all(), V2, D2, R2, K2, LR2, lazy_out=True,
+                           snaps=snaps1, configure=_lazy_configure(True, True))
+    w_in1, w_out1 = t1.w_in.cpu().numpy().copy(), t1.full_w_out().cpu().numpy()
+    res = _two_lazy_ranks(True, True)
+    for rank, w_in, w_out, _, _, snaps in res:
+        np.testing.assert_array_equal(w_in, w_in1)
+        np.testing.assert_array_equal(w_out, w_out1)
+        for k, (a, b) in enumerate(zip(snaps, snaps1)):
+            for name, x, y in zip(('w_in', 'w_out', 'm_in', 'v_in', 'm_out', 'v_out'), a, b):
+                diff = int((x != y).sum())
+                assert diff == 0, f'rank {rank} step {k}: {name} differs in {diff} entries'
 
 
 @pytest.mark.timeout(600)

@@ -251,13 +251,51 @@ def test_d128_trajectory_matches_reference(hip_device):
         assert np.abs(got - exp).max() <= lr / 10
 
 
+def _record_step_losses(monkeypatch):
+    """Records the loss of every eager training_step (1 step) and of every graph replay (the
+    mean over its n steps) as (n, loss) in call order."""
+    rec = []
+    orig_step = Word2VecTrainer.training_step
+    orig_push = Word2VecTrainer.push_replayed
+
+    def step(self, batch, *a, **k):
+        out = orig_step(self, batch, *a, **k)
+        if out is not None:   # (None: a step being captured into a graph)
+            rec.append((1, out['loss'].detach().clone()))
+        return out
+
+    def push(self, terms, n):
+        rec.append((n, terms['loss'].detach().clone()))
+        return orig_push(self, terms, n)
+    monkeypatch.setattr(Word2VecTrainer, 'training_step', step)
+    monkeypatch.setattr(Word2VecTrainer, 'push_replayed', push)
+    return rec
+
+
+def _first_step_losses(rec, unroll: int = 16):
+    """(loss of step 0, mean loss of steps 1..unroll) of the first epoch from a _record_step_losses
+    record: an eager run logs them one by one, a graphed run as step 0 and one replay."""
+    if rec[1][0] == unroll:
+        return float(rec[0][1]), float(rec[1][1])
+    assert all(n == 1 for n, _ in rec[:unroll + 1])
+    return float(rec[0][1]), float(np.mean([float(x) for _, x in rec[1:unroll + 1]]))
+
+
+# The float-mode loops hold the graphed runs to the eager run step by step over the first 17
+# steps (step 0, then the first graph's 16), at the per-step bar: before float-atomic order
+# differences compound through Adam's normalised steps. The whole loop is pinned bit for bit in
+# the deterministic mode (test_gpu_exact.py::test_exact_train_loop_eager_twice_and_graphs_
+# bit_identical, test_reference_streams_c2_loop_graphed_deterministic below).
+FIRST_STEPS_RTOL = 1e-4
+
+
 def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypatch):
     """tools/train.py on the C2 shape (Cora-sized R-MAT, node2vec, L = 10, R = 2, 64-walk
     batches, d = 128) with Philox walks and device negatives: word2vec/fit.py replays the steps
     as HIP graphs of 16 (GraphedTrainerStep) after each epoch's first batch, and trains what the
     eager loop (DW_TRAIN_GRAPH=0) trains — the same number of steps, Adam step counts and walks
-    (the dataset's epoch position), and epoch losses within the loop's own run-to-run envelope
-    (below)."""
+    (the dataset's epoch position), and the same losses over the first 17 steps at the per-step
+    bar (below)."""
     from tools import train as train_tool
     from shallow_encoders.word2vec import graphed
     replays = []
@@ -267,6 +305,7 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
         replays.append(self.unroll)
         return orig(self)
     monkeypatch.setattr(graphed.GraphedTrainerStep, 'replay', counting)
+    rec = _record_step_losses(monkeypatch)
     lr = 0.01
     base = ['datamodule.dataset_name=graph_rmat', 'datamodule.additional_parameters.scale=12',
             'datamodule.additional_parameters.n_edges=5429',
@@ -275,8 +314,9 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
             'datamodule.additional_parameters.method_params.q=1',
             'datamodule.additional_parameters.rng=philox', 'train.noise=device',
             'model.embedding_size=128', f'train.optimizer.lr={lr}', 'train.max_epochs=2']
-    runs = []
+    runs, firsts = [], []
     for mode, scatter in (('0', 'auto'), ('1', 'records'), ('1', 'auto')):
+        rec.clear()
         monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
         monkeypatch.setenv('DW_TRAIN_GRAPH_SCATTER', scatter)
         out = str(tmp_path / f'runs{mode}{scatter}')
@@ -287,6 +327,7 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
         ck = os.path.join(out, 'graph_rmat', f'g{mode}', 'checkpoints', 'last.ckpt')
         state = torch.load(ck, weights_only=True)
         runs.append((last, state))
+        firsts.append(_first_step_losses(rec))
     # 4,096 walks / 64 = 64 batches per epoch: 1 eager + 3 graphs of 16 + 15 eager, two epochs
     assert replays == [16] * 12
     (l0, s0), (l1, s1), (l2, s2) = runs
@@ -294,15 +335,14 @@ def test_train_loop_replays_graphs_equal_to_eager(tmp_path, hip_device, monkeypa
     # In the float mode the loop is not bit-reproducible run to run, eager or graphed: float
     # atomics (the centre gradients, chunk-boundary rows) sum in a run-dependent order, and
     # Adam's normalised steps turn the resulting sign noise on g ~ 0 entries into lr-sized moves
-    # that compound over 128 steps at lr = 0.01. So here the graphs (records step, and the default
-    # atomic scatter) are held to an envelope: the same steps, walks, negatives and Adam step
-    # counts (above), epoch losses within 3%. Each graphed step itself is checked against the
-    # eager step from the same state in test_gpu_graphed.py, and in the deterministic mode the
-    # same loop's eager and graphed runs end with bit-identical tables
-    # (test_gpu_exact.py::test_exact_train_loop_eager_twice_and_graphs_bit_identical).
-    for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
-        np.testing.assert_allclose(l1[k], l0[k], rtol=3e-2)
-        np.testing.assert_allclose(l2[k], l0[k], rtol=3e-2)
+    # that compound over 128 steps at lr = 0.01. So the graphs (records step, and the default
+    # atomic scatter) are held to the eager loop at the per-step bar over the first 17 steps
+    # (FIRST_STEPS_RTOL), with the same steps, walks, negatives and Adam step counts (above).
+    # Each graphed step itself is checked against the eager step from the same state in
+    # test_gpu_graphed.py, and in the deterministic mode the same loop's eager and graphed runs
+    # end with bit-identical tables.
+    for f in firsts[1:]:
+        np.testing.assert_allclose(f, firsts[0], rtol=FIRST_STEPS_RTOL)
 
 
 def _karate_fit(f, graph: str, monkeypatch):
@@ -391,7 +431,7 @@ def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
     own streams (rng: python walks, noise: torch) replays its steps as graphs of 16 and leaves
     `random` and torch's generator exactly where the eager loop leaves them (the same walks and
     negatives, step for step), with the same step count and epoch losses within the loop's
-    run-to-run envelope."""
+    per-step losses over the first 17 steps."""
     import random
     from tools import train as train_tool
     from shallow_encoders.word2vec import graphed
@@ -402,6 +442,7 @@ def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
         replays.append(self.unroll)
         return orig(self)
     monkeypatch.setattr(graphed.GraphedTrainerStep, 'replay', counting)
+    rec = _record_step_losses(monkeypatch)
     base = ['datamodule.dataset_name=graph_rmat', 'datamodule.additional_parameters.scale=12',
             'datamodule.additional_parameters.n_edges=5429',
             'datamodule.additional_parameters.graph_seed=0',
@@ -409,8 +450,9 @@ def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
             'datamodule.additional_parameters.method_params.q=1',
             'datamodule.additional_parameters.rng=python', 'train.noise=torch',
             'model.embedding_size=128', 'train.optimizer.lr=0.01', 'train.max_epochs=2']
-    runs = []
+    runs, firsts = [], []
     for mode in ('0', '1'):
+        rec.clear()
         monkeypatch.setenv('DW_TRAIN_GRAPH', mode)
         out = str(tmp_path / f'runs{mode}')
         random.seed(5)
@@ -420,19 +462,19 @@ def test_reference_streams_c2_loop_graphed(tmp_path, hip_device, monkeypatch):
         ck = os.path.join(out, 'graph_rmat', f'g{mode}', 'checkpoints', 'last.ckpt')
         state = torch.load(ck, weights_only=True)
         runs.append((last, state, random.getstate(), torch.get_rng_state()))
+        firsts.append(_first_step_losses(rec))
     assert replays == [16] * 6
     (l0, s0, r0, t0), (l1, s1, r1, t1) = runs
     assert s0['global_step'] == s1['global_step'] == 128
     assert r0 == r1 and torch.equal(t0, t1)
-    for k in ('train-epoch/loss', 'train-epoch/positive-loss', 'train-epoch/negative-loss'):
-        np.testing.assert_allclose(l1[k], l0[k], rtol=3e-2)
+    np.testing.assert_allclose(firsts[1], firsts[0], rtol=FIRST_STEPS_RTOL)
 
 
 def test_reference_streams_c2_loop_graphed_deterministic(tmp_path, hip_device, monkeypatch):
     """The same loop with the reference's own streams (rng: python walks, noise: torch) in the
     deterministic mode (DW_DETERMINISTIC=1): the eager run and the run replayed as graphs of 16
-    end with bit-identical tables — the float mode's 3% envelope above is the atomics' order,
-    not the graphs — and leave `random` and torch's generator in the same state."""
+    end with bit-identical tables — the float mode's divergence past the first steps above is the
+    atomics' order, not the graphs — and leave `random` and torch's generator in the same state."""
     import random
     from tools import train as train_tool
     monkeypatch.setenv('DW_DETERMINISTIC', '1')

@@ -430,6 +430,9 @@ def test_counted_node2vec_walks_equal_and_count(hip_device):
                 assert c['walker'] == 'dw_walk_fast_positions' and c['blocks'] == 0
                 assert c['bytes'] == c['steps'] * 36 + 2 * c['position_loads'] + n * 20
                 assert c['position_loads'] > 0
+                # each search's line moves: at least one per search that loads, at most a
+                # move per probe
+                assert 0 < c['position_lines'] <= c['position_loads']
 
 
 @pytest.mark.parametrize('method,p,q,n_walks,L', [('deepwalk', 1.0, 1.0, 65_536, 40),

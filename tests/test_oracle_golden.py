@@ -210,6 +210,12 @@ def test_oracle_replays_reference_hub_walks_rmat16(m):
     out = walk_ref.walks_replay(g, f['starts'], int(f['walk_length']), str(f['method']),
                                 float(f['p']), float(f['q']), f['uniforms'])
     np.testing.assert_array_equal(out, f['walks'])
+    # the numpy-backed undirected form (test_gpu_c5_walks' oracle at R-MAT 24) on the same
+    # reference walks
+    ga = walk_ref.ArrayCSR(csr.row_ptr, csr.col, None, undirected=True)
+    out = walk_ref.walks_replay(ga, f['starts'], int(f['walk_length']), str(f['method']),
+                                float(f['p']), float(f['q']), f['uniforms'])
+    np.testing.assert_array_equal(out, f['walks'])
 
 
 def test_column_chunked_closed_form_equals_numpy_form():
