@@ -45,7 +45,7 @@ extern "C" {
 
 const char *dw_last_error_string(void) { return dw::g_err; }
 
-int dw_abi_version(void) { return 23; }
+int dw_abi_version(void) { return 24; }
 
 #ifndef DW_BUILD_ID
 #define DW_BUILD_ID "unknown"

@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(512)
             if (BY_ROW && live) g_rows[og] = 0.f;
         }
         if (pd) dw::settle_pending(pr, mr, vr, hist, from, box_from);
-        dw::replay_g0(pr, mr, vr, hist, from, upto, box_from);
+        dw::replay_g0<E, true>(pr, mr, vr, hist, from, upto, box_from);
         if (STEP) {
             const dw::AdamScalars hs = hist_at(hist, step);
 #pragma unroll

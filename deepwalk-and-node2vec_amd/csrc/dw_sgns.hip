@@ -3208,7 +3208,7 @@ int dw_sgns_owner_prepare(const int32_t *walks, int64_t n_walks, int32_t walk_le
 int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                               int32_t context_radius, int64_t vocab_size, int32_t *claim,
                               int32_t step, uint32_t *touched, int64_t *n_touched,
-                              uint32_t *fresh, int64_t *n_fresh, void *stream) {
+                              uint32_t *fresh, int64_t *n_fresh, int32_t flags, void *stream) {
     DW_REQUIRE(context_radius >= 1 && walk_length >= 2 * context_radius + 1 && n_walks >= 0 &&
                    vocab_size >= 1 && step >= 1,
                "dw_sgns_owner_touch_claim: bad sizes");
@@ -3219,8 +3219,12 @@ int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t wal
     int32_t delta = 0;
     const int rc = dw::bound_step_rel(step, &dyn, &delta, "dw_sgns_owner_touch_claim");
     if (rc != DW_OK) return rc;
-    if (hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess ||
-        (fresh && hipMemsetAsync(n_fresh, 0, sizeof(int64_t), st) != hipSuccess)) {
+    DW_REQUIRE((flags & ~1) == 0, "dw_sgns_owner_touch_claim: flags must be 0 or 1");
+    // flags & 1: the caller zeroed the counters (owner_lazy_steps: one ring of counters per
+    // call, cleared by one memset at its head — no memset node per captured step)
+    if (!(flags & 1) &&
+        (hipMemsetAsync(n_touched, 0, sizeof(int64_t), st) != hipSuccess ||
+         (fresh && hipMemsetAsync(n_fresh, 0, sizeof(int64_t), st) != hipSuccess))) {
         dw::set_error("dw_sgns_owner_touch_claim: counter reset failed");
         return DW_E_HIP;
     }

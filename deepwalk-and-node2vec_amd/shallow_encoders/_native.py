@@ -38,7 +38,7 @@ DW_EXACT_ADAM = 2
 DW_METHOD_DEEPWALK = 0
 DW_METHOD_NODE2VEC = 1
 
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -99,7 +99,7 @@ SIGNATURES = {
                                            _i64, _i32, _p, _p, _p, _p, _u64, _u64, _f32, _p, _p,
                                            _p, ctypes.c_size_t, _p]),
     'dw_sgns_owner_touch_claim': (ctypes.c_int, [_p, _i64, _i32, _i32, _i64, _p, _i32, _p, _p,
-                                                 _p, _p, _p]),
+                                                 _p, _p, _i32, _p]),
     'dw_adam_rows': (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _i32, _p,
                                     _i32, _p]),
     'dw_rows_gather': (ctypes.c_int, [_p, _i64, _i32, _p, _p, _i64, _p, _i32, _p]),

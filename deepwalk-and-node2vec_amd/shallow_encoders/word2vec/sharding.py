@@ -129,14 +129,26 @@ def hist_rows_in_box(rows: np.ndarray) -> np.ndarray:
 
 
 def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
-    """float32[8] row 0 of a lazy Adam history whose rows 1..last are written: the box tag and
-    the first step b such that rows b..last are all in the box (include/dw_hip.h)."""
+    """float32[8] row 0 of a lazy Adam history whose rows 1..last are written: the box tag, the
+    first step b such that rows b..last are all in the box, and the frozen-parameter bound of
+    those rows (include/dw_hip.h; dw_common.h, dw::frozen_el): [2] F = max |nstep| when every
+    box row has the same eps and (1 - beta1)(1 + 2^-20) <= sqrt(beta2) (m then shrinks at least
+    as fast as RN(sqrt(v)) over g = 0 steps), else +inf (no replay tail is frozen); [3] that
+    eps."""
     ok = hist_rows_in_box(hist[1:last + 1])
     bad = np.flatnonzero(~ok)
     b = int(bad[-1]) + 2 if bad.size else 1
     h0 = np.zeros(8, dtype=np.float32)
     h0.view(np.uint32)[0] = HIST_BOX_TAG
     h0.view(np.int32)[1] = b
+    h0[2] = np.inf
+    rows = np.ascontiguousarray(hist[b:last + 1], dtype=np.float32).reshape(-1, 8)
+    if rows.shape[0]:
+        w1, b2 = rows[:, 0].astype(np.float64), rows[:, 1].astype(np.float64)
+        eps = rows[:, 5]
+        if (eps == eps[0]).all() and ((1.0 - w1) * (1.0 + 2.0 ** -20) <= np.sqrt(b2)).all():
+            h0[2] = np.abs(rows[:, 4]).max()
+            h0[3] = eps[0]
     return h0
 
 
@@ -176,7 +188,10 @@ def adam_to_scalars(p_src: torch.Tensor, p_dst: torch.Tensor, g: torch.Tensor, m
 # Adam block moves ~22 GB/s next to it; 25% margin.
 OVERLAP_PHASE_BPS = 5.0e12
 ADAM_BLOCK_BPS = 22e9
-OVERLAP_MARGIN = 1.25
+# (round 6: 1.25 -> 1.375, 47 -> 51 blocks at C3: the capped Adam then ends inside the sort +
+# gather window instead of ~0.1 ms after it; 6.85 -> 6.75 ms per step, 56 blocks 6.78, 42 7.20;
+# profiles/r06_pipe_order_ab.txt)
+OVERLAP_MARGIN = 1.375
 
 # N > 1: out-table pieces exchanged behind the output-table phase; 8 keeps each collective at
 # 1/8 of the table (64 MB at C3) while exposing only the last piece's exchange.
@@ -991,7 +1006,7 @@ class OwnerLazyTables(OwnerTables):
         if not self._hip() or not self.lazy_out:
             raise NotImplementedError('the lazy deterministic mode covers the HIP lazy Adam of '
                                       'both tables (lazy_out)')
-        if self.emulated:
+        if self.emulated and self.world > 1:
             raise NotImplementedError('the deterministic mode needs the real collectives')
         self._exact = exact.Registry()
         self._exact.ensure(0, self.grads_in, grad_scale, defer=self.multi)
@@ -1004,8 +1019,9 @@ class OwnerLazyTables(OwnerTables):
                 and self.rows_major_ok(context_radius, neg_samples))
 
     def _pipe_alloc(self, n_walks: int, walk_length: int, context_radius: int,
-                    neg_samples: int) -> None:
-        """The pipelined steps' second buffers (before a capture: a graph must not allocate)."""
+                    neg_samples: int, n_steps: int = 64) -> None:
+        """The pipelined steps' second buffers and their counter ring (one (|U|, fresh) pair per
+        step of an owner_lazy_steps call; before a capture: a graph must not allocate)."""
         from shallow_encoders.word2vec.sgns import workspace_for
         n = max(n_walks * (walk_length - 2 * int(context_radius)), 1)
         for slot in (0, 1):
@@ -1016,33 +1032,34 @@ class OwnerLazyTables(OwnerTables):
         if self._claim_in is None:
             self._claim_in = torch.zeros(self.V_pad, dtype=torch.int32, device=self.device)
         p = self._pipe
-        if p is None or p['touched'][0].numel() < n:
+        if p is None or p['touched'][0].numel() < n or p['ctr'].shape[0] < n_steps:
             i32 = dict(dtype=torch.int32, device=self.device)
             i64 = dict(dtype=torch.int64, device=self.device)
             self._pipe = {'touched': [torch.empty(n, **i32) for _ in range(2)],
-                          'n_touched': [torch.zeros(1, **i64) for _ in range(2)],
                           'fresh': [torch.empty(n, **i32) for _ in range(2)],
-                          'n_fresh': [torch.zeros(1, **i64) for _ in range(2)],
+                          # step k's [|U|, fresh] counters, cleared by one memset per call
+                          'ctr': torch.zeros((max(n_steps, 64), 2), **i64),
                           'side_in': torch.cuda.Stream(self.device)}
         if self._touched is None or self._touched.numel() < n:
             self._touched = torch.empty(n, dtype=torch.int32, device=self.device)
 
     def _touch_ahead(self, walks: torch.Tensor, context_radius: int, step: int,
-                     slot: int) -> None:
+                     slot: int, ctr: torch.Tensor) -> None:
         """The pipelined step ``step``'s in rows, while step - 1 may still run: its distinct
-        centres U (touched list ``slot``) and, of them, those that were not centres of step - 1
-        (the fresh list) replayed up to step - 1 — nothing of step - 1 writes those rows."""
+        centres U (touched list ``slot``, its count ctr[0]) and, of them, those that were not
+        centres of step - 1 (the fresh list, count ctr[1]) replayed up to step - 1 — nothing of
+        step - 1 writes those rows. ``ctr`` is zero on entry (the call's counter ring)."""
         p = self._pipe
         with torch.cuda.device(self.device):
             _native.call('dw_sgns_owner_touch_claim', _native.ptr(walks), walks.shape[0],
                          walks.shape[1], int(context_radius), self.V,
                          _native.ptr(self._claim_in), int(step),
-                         _native.ptr(p['touched'][slot]), _native.ptr(p['n_touched'][slot]),
-                         _native.ptr(p['fresh'][slot]), _native.ptr(p['n_fresh'][slot]),
+                         _native.ptr(p['touched'][slot]), _native.ptr(ctr[0:1]),
+                         _native.ptr(p['fresh'][slot]), _native.ptr(ctr[1:2]), 1,
                          _native.stream(self.device))
         n_max = walks.shape[0] * (walks.shape[1] - 2 * int(context_radius))
         hip_rows_adam(self.params_in[0], self.m_in, self.v_in, self.last_in, p['fresh'][slot],
-                      p['n_fresh'][slot], n_max, None, self._hist, int(step) - 1)
+                      ctr[1:2], n_max, None, self._hist, int(step) - 1)
 
     def out_flags(self) -> int:
         """dw_sgns_owner_out_catch_up / _pass2_lazy flags of the current step: 1 = place the
@@ -1217,7 +1234,7 @@ class OwnerLazyTables(OwnerTables):
                              walks.shape[1], int(context_radius), self.V,
                              _native.ptr(self._claim_in), self.step_count,
                              _native.ptr(self._touched), _native.ptr(self._n_touched), None,
-                             None, _native.stream(self.device))
+                             None, 0, _native.stream(self.device))
         else:
             sgns_owner_prepare(walks, context_radius, neg_samples, self.V, self.S,
                                touched=self._touched, n_touched=self._n_touched)
@@ -1439,7 +1456,7 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     t = tables
     dev = t.device
     nw, L = batches[0].shape
-    t._pipe_alloc(nw, L, R, K)
+    t._pipe_alloc(nw, L, R, K, n_steps)
     s0 = t.step_count + 1
     # every Adam-scalar row the steps read, written before the first side launch (begin_step
     # then copies nothing while a side stream reads the history)
@@ -1449,33 +1466,39 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     t._rows_step = True
     main = torch.cuda.current_stream(dev)
     side_out, side_in = t._side, t._pipe['side_in']
+    p = t._pipe
+    ring = p['ctr'][:n_steps]
+    ring.zero_()   # every step's touch-claim counters: one memset node, not two per step
 
-    def ahead(k: int):
-        """Step k's preparation on the side streams, after everything enqueued so far."""
+    def fork_on(stream, fn, k):
         fork = torch.cuda.Event()
         fork.record(main)
         if bind is not None:
             bind(k)
-        slot = k & 1
-        with torch.cuda.stream(side_out):
-            side_out.wait_event(fork)
-            t.catch_up_out(batches[k], R, K, seed, offs[k], status, step=s0 + k, slot=slot)
-            ro = torch.cuda.Event()
-            ro.record(side_out)
-        with torch.cuda.stream(side_in):
-            side_in.wait_event(fork)
-            t._touch_ahead(batches[k], R, s0 + k, slot)
-            ri = torch.cuda.Event()
-            ri.record(side_in)
-        return ro, ri
+        with torch.cuda.stream(stream):
+            stream.wait_event(fork)
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ev
 
-    ready = ahead(0)
+    def ahead_out(k: int):
+        """Step k's out-record placement on side_out, after everything enqueued so far."""
+        return fork_on(side_out, lambda: t.catch_up_out(batches[k], R, K, seed, offs[k], status,
+                                                        step=s0 + k, slot=k & 1), k)
+
+    def ahead_in(k: int):
+        """Step k's touch claim and fresh-row catch-up on side_in."""
+        return fork_on(side_in, lambda: t._touch_ahead(batches[k], R, s0 + k, k & 1, ring[k]), k)
+
+    ready = [ahead_out(0), ahead_in(0)]
     slots = batches[0].shape[0] * (L - 2 * R) * 2 * R * (1 + K)
-    p = t._pipe
-    # step k + 1's preparation forks after step k's out rows, beside the centre pass and the in
-    # rows' update. (At step k's start, beside the out rows, it measured slower — its waves take
-    # the CU slots k_out_rows sizes its resident grid for: 0.336 vs 0.332 ms at C3 / 64; the
-    # centre pass captured before the side chains, 0.332-0.334 vs 0.324-0.330.)
+    # step k + 1's touch claim and fresh-row catch-up fork at step k's start (beside its out
+    # rows: that chain was the step's critical branch after them; 0.293-0.295 against
+    # 0.295-0.301 ms at C3 / 64), its out-record placement after step k's out rows, beside the
+    # centre pass and the in rows' update (at step k's start its claims' waves take the CU slots
+    # k_out_rows sizes its resident grid for: 0.336 vs 0.332 ms, round 5). The centre pass
+    # captured before the placement fork: 0.324 (profiles/r06_pipe_order_ab.txt).
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
@@ -1483,20 +1506,25 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
         t.begin_step()
         for ev in ready:
             main.wait_event(ev)
+        ready = []
         w = batches[k]
+        if k + 1 < n_steps:
+            ready.append(ahead_in(k + 1))
+            if bind is not None:
+                bind(k)
         t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
         if k + 1 < n_steps:
-            ready = ahead(k + 1)
+            ready.append(ahead_out(k + 1))
             if bind is not None:
                 bind(k)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,
-                         order_ready=True, placed=True, coefficients_in=True, walk_order=True,
-                         workspace_slot=slot)
+                         order_ready=True, placed=True, coefficients_in=True,
+                         walk_order=True, workspace_slot=slot)
         # the step's in rows with their gradient rows (dw_adam_rows grad_by_row clears them)
         hip_rows_adam(t.params_in[0], t.m_in, t.v_in, t.last_in, p['touched'][slot],
-                      p['n_touched'][slot], nw * (L - 2 * R), t.grads_in, t._hist,
+                      ring[k, 0:1], nw * (L - 2 * R), t.grads_in, t._hist,
                       t.step_count, grad_by_row=True)
     return slots * n_steps
 

@@ -592,12 +592,13 @@ int dw_sgns_owner_pass2_lazy(int64_t n_walks, int32_t walk_length, int32_t conte
  * n_touched (int64, device) their count. fresh / n_fresh (NULL = not wanted): the listed
  * nodes whose claim was below step - 1 — not centres of the step before, so nothing of that
  * step writes their rows (the pipelined step catches them up while step - 1 still runs). Reads
- * step from a bound dw_step_scalars block (relative form). Replaces nothing in the reference
- * (its optimizer steps every row). */
+ * step from a bound dw_step_scalars block (relative form). flags: 0, or 1 = the counters are
+ * already zero (not reset here: a caller that clears many steps' counters at once). Replaces
+ * nothing in the reference (its optimizer steps every row). */
 int dw_sgns_owner_touch_claim(const int32_t *walks, int64_t n_walks, int32_t walk_length,
                               int32_t context_radius, int64_t vocab_size, int32_t *claim,
                               int32_t step, uint32_t *touched, int64_t *n_touched,
-                              uint32_t *fresh, int64_t *n_fresh, void *stream);
+                              uint32_t *fresh, int64_t *n_fresh, int32_t flags, void *stream);
 
 /* The rows-major lazy out step (OwnerLazyTables, one device; after dw_sgns_owner_out_catch_up
  * with flags 1 | 4 on the same batch and workspace, before dw_sgns_owner_pass1 with order_ready
@@ -747,7 +748,11 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         has weight_decay +0, the reciprocal, eps in [2^-27, 1], sqrt(bias_correction2) in
  *         [2^-10, 1] and 1-beta1, beta2 in [0, 1]: the g = 0 replays of rows last current at
  *         b - 1 or later then run sqrt and the division without range scaling (the same bits,
- *         fewer operations); any other row 0 = no step in the box;
+ *         fewer operations); [2] = F, [3] = eps of those rows: with every box row's eps equal to
+ *         it, (1 - beta1)(1 + 2^-20) <= sqrt(beta2) and |nstep| <= F, a replay whose parameter
+ *         can provably no longer move (|m| F / max(RN(sqrt(v)), eps) below |p| 2^-26) steps m
+ *         and v alone for the rest of the run (the same bits; F = +inf: never); any other row
+ *         0 = no step in the box;
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
  *         gradient grad_rows[i];
