@@ -143,7 +143,8 @@ def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
     h0.view(np.int32)[1] = b
     h0[2] = np.inf
     rows = np.ascontiguousarray(hist[b:last + 1], dtype=np.float32).reshape(-1, 8)
-    if rows.shape[0]:
+    import os
+    if rows.shape[0] and os.environ.get('DW_NO_FREEZE') != '1':   # (A/B, round 6)
         w1, b2 = rows[:, 0].astype(np.float64), rows[:, 1].astype(np.float64)
         eps = rows[:, 5]
         if (eps == eps[0]).all() and ((1.0 - w1) * (1.0 + 2.0 ** -20) <= np.sqrt(b2)).all():
@@ -1038,8 +1039,7 @@ class OwnerLazyTables(OwnerTables):
             self._pipe = {'touched': [torch.empty(n, **i32) for _ in range(2)],
                           'fresh': [torch.empty(n, **i32) for _ in range(2)],
                           # step k's [|U|, fresh] counters, cleared by one memset per call
-                          'ctr': torch.zeros((max(n_steps, 64), 2), **i64),
-                          'side_in': torch.cuda.Stream(self.device)}
+                          'ctr': torch.zeros((max(n_steps, 64), 2), **i64)}
         if self._touched is None or self._touched.numel() < n:
             self._touched = torch.empty(n, dtype=torch.int32, device=self.device)
 
@@ -1465,7 +1465,9 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
         t._flush_out()
     t._rows_step = True
     main = torch.cuda.current_stream(dev)
-    side_out, side_in = t._side, t._pipe['side_in']
+    side = t._side   # both preparation chains, one after the other
+    import os
+    out_first = os.environ.get('DW_PIPE_OUT_FIRST') == '1'   # A/B (round 6)
     p = t._pipe
     ring = p['ctr'][:n_steps]
     ring.zero_()   # every step's touch-claim counters: one memset node, not two per step
@@ -1482,41 +1484,38 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
             ev.record(stream)
         return ev
 
-    def ahead_out(k: int):
-        """Step k's out-record placement on side_out, after everything enqueued so far."""
-        return fork_on(side_out, lambda: t.catch_up_out(batches[k], R, K, seed, offs[k], status,
-                                                        step=s0 + k, slot=k & 1), k)
+    def ahead(k: int):
+        """Step k's preparation on the side stream, after everything enqueued so far: its touch
+        claim and fresh-row catch-up, then its out-record placement (claim, sums, scan, slots)."""
+        def chains():
+            if out_first:
+                t.catch_up_out(batches[k], R, K, seed, offs[k], status, step=s0 + k, slot=k & 1)
+            t._touch_ahead(batches[k], R, s0 + k, k & 1, ring[k])
+            if not out_first:
+                t.catch_up_out(batches[k], R, K, seed, offs[k], status, step=s0 + k, slot=k & 1)
+        return fork_on(side, chains, k)
 
-    def ahead_in(k: int):
-        """Step k's touch claim and fresh-row catch-up on side_in."""
-        return fork_on(side_in, lambda: t._touch_ahead(batches[k], R, s0 + k, k & 1, ring[k]), k)
-
-    ready = [ahead_out(0), ahead_in(0)]
+    ready = ahead(0)
     slots = batches[0].shape[0] * (L - 2 * R) * 2 * R * (1 + K)
-    # step k + 1's touch claim and fresh-row catch-up fork at step k's start (beside its out
-    # rows: that chain was the step's critical branch after them; 0.293-0.295 against
-    # 0.295-0.301 ms at C3 / 64), its out-record placement after step k's out rows, beside the
-    # centre pass and the in rows' update (at step k's start its claims' waves take the CU slots
-    # k_out_rows sizes its resident grid for: 0.336 vs 0.332 ms, round 5). The centre pass
-    # captured before the placement fork: 0.324 (profiles/r06_pipe_order_ab.txt).
+    # step k + 1's preparation forks at step k's start, beside its out rows, on ONE side stream
+    # (the out rows then wait for one side branch and the centre pass follows the out rows with no
+    # fork in between): 0.279-0.280 against 0.293-0.296 ms at C3 / 64 with the in-row chain there
+    # and the placement on a second stream forked after the out rows (round 5's form, both after
+    # the out rows: 0.295-0.301; two streams both at the start: 0.299; one stream after the out
+    # rows: 0.300-0.306; the centre pass captured before the forks: 0.324;
+    # profiles/r06_pipe_order_ab.txt).
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
             bind(k)
         t.begin_step()
-        for ev in ready:
-            main.wait_event(ev)
-        ready = []
+        main.wait_event(ready)
         w = batches[k]
         if k + 1 < n_steps:
-            ready.append(ahead_in(k + 1))
+            ready = ahead(k + 1)
             if bind is not None:
                 bind(k)
         t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
-        if k + 1 < n_steps:
-            ready.append(ahead_out(k + 1))
-            if bind is not None:
-                bind(k)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,
