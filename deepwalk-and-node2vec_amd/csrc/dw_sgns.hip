@@ -3386,6 +3386,8 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     // straddling rows)
     const int64_t bound = n_centres * T;
     const int64_t resident = grid_cap(4 * OUT_ROWS_WAVES);
+    // (three or four ranges per slot with the next step's preparation beside the kernel: within
+    // 0.3%, profiles/r06_pipe_order_ab.txt)
     int32_t gch = static_cast<int32_t>((bound + 2 * resident - 1) / (2 * resident));
     gch = gch < 16 ? 16 : gch > 64 ? 64 : gch;
     int64_t blocks = ((bound + gch - 1) / gch + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
