@@ -1506,30 +1506,36 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // as a fixed-point integer (dw::to_fixed, the records gather's rule), so the sum is the same
 // whatever order the claim's atomics ranked the records in; a straddling row adds its integer
 // part into fo.acc, which k_fixed_boundary converts once every range has.
-// (Stepping a straddling row inside this kernel by the range that finishes it last — a device
-// fence and a part counter per straddling row, no boundary launch — measured 0.41 against 0.295
-// ms per step at C3's 64-walk batch: an agent-scope release on MI355X writes back the XCD's L2.
-// k_lazy_boundary stays; profiles/r06_pipe_order_ab.txt.)
+// Whole rows (round 6): a range steps the rows that START in it, whole — the records of its last
+// row that continue past the range end (up to off[row + 1], the placement's segment end) are
+// read from the placed arrays 64 at a time into the wave's registers — and skips the records of a
+// row begun in an earlier range. No row is split, so no g_out atomics, no k_lazy_boundary /
+// k_fixed_boundary launch between this kernel and the centre pass (one range finishing a hub row
+// alone: the hubs have the low ids, so their ranges start first). (Stepping a straddling row by
+// the range that finishes it last — a device fence and a part counter per row — measured 0.41
+// against 0.295 ms: an agent-scope release on MI355X writes back the XCD's L2.)
 constexpr int OUT_ROWS_WAVES = 6;
 template <int F4, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
-               float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo) {
+               float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo,
+               const uint32_t *__restrict__ off) {
     constexpr int D = 64 * F4;
     constexpr int BR = WAVES_PER_BLOCK * WAVE;   // records per block range, at most
     bool fx_range = false;
     uint32_t fx_tmax = 0u;   // EXACT: the largest |term|'s bits (the range test, at the end)
     constexpr int RU = 4;   // records per round (one per 16-lane group)
     // the block range's records (slot, centre node, context flag) and its rows' starts
-    __shared__ uint32_t s_key[BR], s_slot[BR];
+    __shared__ uint32_t s_key[BR], s_slot[BR];   // (slot | context flag << 31)
     __shared__ int32_t s_cid[BR];
-    __shared__ uint8_t s_pos[BR];
     __shared__ uint16_t s_rs[BR + 1];
     __shared__ int32_t s_wrows[WAVES_PER_BLOCK];
     __shared__ int32_t s_next;   // the next row to take
     __shared__ float4 s_p[WAVES_PER_BLOCK][D / 4];        // the row's p^{s-1}
     __shared__ float4 s_c[WAVES_PER_BLOCK][RU][D / 4];    // the round's centre rows
+    __shared__ uint32_t s_ovs[WAVES_PER_BLOCK][WAVE];     // a continuing row's records, 64 at a
+    __shared__ int32_t s_ovc[WAVES_PER_BLOCK][WAVE];      // time (slot | context << 31, centre)
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int q = lane >> 4, gl = lane & 15;
@@ -1548,28 +1554,24 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
     for (int64_t br = blockIdx.x; br < n_ranges; br += gridDim.x) {
         const int64_t r0 = br * br_len;
         const int n_blk = static_cast<int>(n_rec - r0 < br_len ? n_rec - r0 : br_len);
-        const uint32_t before = r0 > 0 ? keys[r0 - 1] : 0xFFFFFFFFu;
+        // the record past the range: its row continues the range's last row or not
         const uint32_t after = r0 + n_blk < n_rec ? keys[r0 + n_blk] : 0xFFFFFFFFu;
         {   // wave wv reads records [64 wv, 64 wv + 64) of the range: one per lane, all at once
             const int i = WAVE * wv + lane;
             const bool in = i < n_blk;
             const uint32_t key = in ? keys[r0 + i] : 0xFFFFFFFFu;
-            const uint32_t prev = i == 0 ? 0u : lane > 0 ? 0u : (in ? keys[r0 + i - 1] : 0u);
-            const uint32_t slot = in ? static_cast<uint32_t>(vals[r0 + i]) : 0u;
-            const uint32_t b = slot / static_cast<uint32_t>(T);
-            const uint32_t w = b / static_cast<uint32_t>(per);
-            const int32_t cid =
-                in ? a.walks[static_cast<int64_t>(w) * a.L + a.R + (b - w * static_cast<uint32_t>(per))]
-                   : -1;
-            // the record's row is a context (slot t = 0 mod 1 + K), not a negative
-            const uint32_t t = slot - b * static_cast<uint32_t>(T);
+            // (record 0 starts a row unless the row began in the range before: not ours)
+            const uint32_t prev = lane > 0 ? 0u
+                                  : i == 0 ? (r0 > 0 ? keys[r0 - 1] : 0xFFFFFFFFu)
+                                           : (in ? keys[r0 + i - 1] : 0u);
+            // (k_place_slots: centre << 32 | slot | context flag << 31)
+            const uint64_t rec = in ? vals[r0 + i] : 0xFFFFFFFF00000000ull;
             const uint32_t up = __shfl_up(key, 1, WAVE);
-            const bool is_start = in && (i == 0 || key != (lane > 0 ? up : prev));
+            const bool is_start = in && key != (lane > 0 ? up : prev);
             const uint64_t starts = __ballot(is_start);
             s_key[i] = key;
-            s_slot[i] = slot;
-            s_cid[i] = cid;
-            s_pos[i] = (t % static_cast<uint32_t>(rpc)) == 0u ? 1 : 0;
+            s_slot[i] = static_cast<uint32_t>(rec);
+            s_cid[i] = static_cast<int32_t>(rec >> 32);
             if (lane == 0) s_wrows[wv] = __popcll(starts);
             __syncthreads();
             int base = 0, nr = 0;
@@ -1614,9 +1616,23 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
         while (k < nrows) {
             const int rs = s_rs[k], re = s_rs[k + 1];   // (wave-uniform)
             const uint32_t row = s_key[rs];
-            const bool straddle = row == before || row == after;
             const int64_t ro = static_cast<int64_t>(row) * D + lane;
-            const int cnt = re - rs;
+            // the range's last row continuing past it: all its records from the placed arrays
+            const bool glob = re == n_blk && after == row;
+            const int cnt = glob ? static_cast<int>(off[row + 1] - static_cast<uint32_t>(r0 + rs))
+                                 : re - rs;
+            auto window = [&](int j) {   // glob: records [j, j + 64) of the row into the LDS
+                const uint64_t rec = j + lane < cnt ? vals[r0 + rs + j + lane]
+                                                    : 0xFFFFFFFF00000000ull;
+                s_ovs[wv][lane] = static_cast<uint32_t>(rec);
+                s_ovc[wv][lane] = static_cast<int32_t>(rec >> 32);
+                dw::wave_lds_sync();
+            };
+            if (glob) window(0);
+            // the row's records in the LDS: the range's staging, or the wave's window (64 at a time)
+            const uint32_t *Ls = glob ? &s_ovs[wv][0] : &s_slot[rs];
+            const int32_t *Lc = glob ? &s_ovc[wv][0] : &s_cid[rs];
+            const int msk = glob ? WAVE - 1 : 0x7FFFFFFF;
             float p[F4], m[F4], v[F4], g[F4];
             int64_t gx[EXACT ? F4 : 1];
 #pragma unroll
@@ -1638,7 +1654,7 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             // [4gl + 64f, +4)), then the next row's loads — both in flight during the replay
             float4 c4[F4];
             {
-                const int32_t cid = q < cnt ? s_cid[rs + q] : -1;
+                const int32_t cid = q < cnt ? Lc[q] : -1;
                 const bool ok = cid >= 0 && cid < a.V;
                 const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
 #pragma unroll
@@ -1656,9 +1672,12 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             for (int j0 = 0; j0 < cnt; j0 += RU) {
                 // group q: record j0 + q's logit in pass 1's layout and its coefficient
                 const bool in = j0 + q < cnt;
-                const int src = in ? rs + j0 + q : rs;
-                const uint32_t slot = s_slot[src];
-                const int32_t cid = s_cid[src];
+                if (glob && j0 > 0 && (j0 & (WAVE - 1)) == 0) window(j0);   // (wave-uniform)
+                const int l = in ? (j0 & msk) + q : 0;
+                const uint32_t spx = Ls[l];
+                const uint32_t slot = spx & 0x7FFFFFFFu;
+                const bool pos = (spx >> 31) != 0u;
+                const int32_t cid = in ? Lc[l] : -1;
                 const bool ok = in && cid >= 0 && cid < a.V;
                 if (j0 > 0) {   // later rounds (rows of more than RU records)
                     const float *crow = a.w_in + static_cast<int64_t>(ok ? cid : 0) * D + 4 * gl;
@@ -1678,7 +1697,6 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
                     s_c[wv][q][gl + 16 * f] = c4[f];
                 }
                 const float x = row_sum16(pr);
-                const bool pos = s_pos[src] != 0;
                 float coef = 0.f;
                 if (ok && gl == 0)
                     coef = row_coef(x, pos, a.scale, acc_pos, acc_neg, acc_rec, acc_prec);
@@ -1707,21 +1725,12 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVE
             }
             if constexpr (EXACT) {
 #pragma unroll
-                for (int f = 0; f < F4; ++f) gx[f] = dw::fixed_finish(gx[f], cnt);   // cnt terms
-                if (straddle) {
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) dw::fixed_add(fo.acc + ro + 64 * f, gx[f]);
-                } else {
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) g[f] = dw::from_fixed(gx[f], fo.fi);
+                for (int f = 0; f < F4; ++f) {
+                    gx[f] = dw::fixed_finish(gx[f], cnt);   // cnt terms
+                    g[f] = dw::from_fixed(gx[f], fo.fi);
                 }
             }
-            if (straddle) {
-                if constexpr (!EXACT) {
-#pragma unroll
-                    for (int f = 0; f < F4; ++f) atomicAdd(g_out + ro + 64 * f, g[f]);
-                }
-            } else {
+            {
                 // the moments of step s; p stays p^{s-1} for the centre pass, which reads it from
                 // the table (no per-slot copies), and the parameter half waits (pend[row])
 #pragma unroll
@@ -2799,18 +2808,28 @@ __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE)
 
 // The rows-major step, after the placement scan: slot s = b T + t (k_out_claim gave it its
 // local row rowid[s] and its rank among that row's slots) goes to off[row] + rank[s] —
-// keys[pos] = the row, vals[pos] = s.
+// keys[pos] = the row, vals[pos] = (the slot's centre node << 32) | s | (t is a context, not a
+// negative) << 31: k_out_rows reads a record in one load, with no walk lookup behind it.
 __global__ void __launch_bounds__(256)
     k_place_slots(int64_t n_slots, const uint32_t *__restrict__ rowid,
                   const uint32_t *__restrict__ rank, const uint32_t *__restrict__ off,
-                  uint32_t *__restrict__ keys, uint64_t *__restrict__ vals) {
+                  uint32_t *__restrict__ keys, uint64_t *__restrict__ vals,
+                  const int32_t *__restrict__ walks, int32_t L, int32_t R, int32_t T,
+                  int32_t rpc) {
+    const uint32_t per = static_cast<uint32_t>(L - 2 * R);
     for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n_slots;
          s += (int64_t)gridDim.x * 256) {
         const uint32_t o = rowid[s];
         if (o == 0xFFFFFFFFu) continue;   // a bad id or another owner's row
         const uint32_t pos = off[o] + rank[s];
+        const uint32_t su = static_cast<uint32_t>(s);
+        const uint32_t b = su / static_cast<uint32_t>(T);
+        const uint32_t w = b / per;
+        const int32_t cid = walks[static_cast<int64_t>(w) * L + R + (b - w * per)];
+        const uint32_t ctx = ((su - b * static_cast<uint32_t>(T)) % static_cast<uint32_t>(rpc)) == 0u
+                                 ? 0x80000000u : 0u;
         keys[pos] = o;
-        vals[pos] = static_cast<uint64_t>(s);
+        vals[pos] = (static_cast<uint64_t>(static_cast<uint32_t>(cid)) << 32) | su | ctx;
     }
 }
 
@@ -2975,7 +2994,8 @@ int dw_sgns_owner_out_catch_up(const int32_t *walks, int64_t n_walks, int32_t wa
         if (pb > grid_cap(8)) pb = grid_cap(8);
         if (pb < 1) pb = 1;
         hipLaunchKernelGGL(k_place_slots, dim3((unsigned)pb), dim3(256), 0, st, a.batch * T,
-                           ws.k0, pl.rank, pl.off, ws.k1, ws.v1);
+                           ws.k0, pl.rank, pl.off, ws.k1, ws.v1, walks, walk_length,
+                           context_radius, static_cast<int32_t>(T), 1 + neg_samples);
         DW_LAUNCH_CHECK("dw_sgns_owner_out_catch_up/place_slots");
         return DW_OK;
     }
@@ -3372,8 +3392,7 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
                          "dw_sgns_owner_out_rows", vocab_size, nullptr, &pl);
     if (rc != DW_OK) return rc;
     OutAdam oa{w_out_local, m_out, v_out, nullptr, dw::AdamScalars{}, last_step, hist, step};
-    (void)counts;   // (cleared by the placement scan; p_current false: k_lazy_boundary replays
-                    // the straddling rows whole)
+    (void)counts;   // (cleared by the placement scan)
     oa.pend = pending;    // the stepped rows are left pending (p at step - 1 for the centre pass)
     rc = dw::bound_step_rel(step, &oa.dyn, &oa.step_delta, "dw_sgns_owner_out_rows");
     if (rc != DW_OK) return rc;
@@ -3397,7 +3416,7 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     float *cs = reinterpret_cast<float *>(ws.v0);
 #define DW_OUT_ROWS(F, X)                                                                       \
     hipLaunchKernelGGL((k_out_rows<F, X>), g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa,    \
-                       g_out_local, cs, fx)
+                       g_out_local, cs, fx, pl.off)
     switch ((dim / 64) * 2 + (fx.acc ? 1 : 0)) {
         case 2: DW_OUT_ROWS(1, false); break;
         case 3: DW_OUT_ROWS(1, true); break;
@@ -3413,20 +3432,7 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     }
 #undef DW_OUT_ROWS
     DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/rows");
-    const int32_t brl = WAVES_PER_BLOCK * gch;   // k_out_rows' block ranges: the straddle unit
-    if (fx.acc) {   // the straddling rows' exact sums into g_out, before their step
-        hipLaunchKernelGGL(k_fixed_boundary, g, bl, 0, st, ws.k1, bound, brl, ws.bounds, fx,
-                           g_out_local, dim);
-        DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/fixed_boundary");
-    }
-    switch (dim / 64) {   // the straddling rows (g in g_out)
-        case 1: launch_boundary<1>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
-        case 2: launch_boundary<2>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
-        case 4: launch_boundary<4>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
-        default: launch_boundary<8>(st, ws.k1, bound, brl, g_out_local, dim, oa, ws.bounds); break;
-    }
-    DW_LAUNCH_CHECK("dw_sgns_owner_out_rows/boundary");
-    return DW_OK;
+    return DW_OK;   // (every row stepped whole by the range it starts in)
 }
 
 int dw_sgns_pairs(const int64_t *inputs, const int64_t *targets, int64_t batch, int32_t n_ctx,
