@@ -1483,17 +1483,14 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // the table (oa.pend[row] = 1), where the centre pass reads it; the parameter half of step s is
 // applied (dw::settle_pending) when the row is next replayed or flushed — the same operations
 // as adam_elem's, so the same bits, without a per-slot copy of p^{s-1} (138 MB at C3/64).
-// A block takes a range of 4 gch <= 256 placed records: its waves read them (one per lane: slots,
-// centre nodes and context flags looked up in one round trip) into LDS with the rows' starts,
+// A block takes a range of 4 gch <= 256 placed records: its waves read them (one packed 8-B
+// record per lane: centre node, slot and context flag, k_place_slots) into LDS with the rows' starts,
 // then take the range's rows one at a time from a block counter (an LDS atomic) — a row's time is
 // set by its deferred steps, ~4 on average but geometric, so four waves sharing ~150 rows finish
 // together where each wave's own fixed chunk left the slowest waves running alone — and ranges
 // small enough that there are about twice as many blocks as resident slots, which the hardware
 // hands out as blocks finish. Per row: four records' centre rows in flight (one per 16-lane group
-// for the logits). A row that straddles the range (its first or last row continues in the
-// neighbouring range) is replayed by each range that holds records of it (the same bits), adds
-// its part of the gradient to g_out with float atomics and is stepped by k_lazy_boundary (full
-// replay, p_current false).
+// for the logits). No row is split between ranges (whole rows, below).
 // (Four rows per wave, one per 16-lane group, measured 350-370 us against the three kernels'
 // ~280 us at C3's 64-walk batch: each group waited for the longest replay of the four, and the
 // 138-VGPR kernel ran three waves per SIMD.)
@@ -1504,8 +1501,7 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // SIMD (OUT_ROWS_WAVES).
 // EXACT (the deterministic mode, g_out registered): each term coef * w_in enters the row's sum
 // as a fixed-point integer (dw::to_fixed, the records gather's rule), so the sum is the same
-// whatever order the claim's atomics ranked the records in; a straddling row adds its integer
-// part into fo.acc, which k_fixed_boundary converts once every range has.
+// whatever order the claim's atomics ranked the records in.
 // Whole rows (round 6): a range steps the rows that START in it, whole — the records of its last
 // row that continue past the range end (up to off[row + 1], the placement's segment end) are
 // read from the placed arrays 64 at a time into the wave's registers — and skips the records of a
@@ -1519,8 +1515,7 @@ template <int F4, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
                const int64_t *__restrict__ range, int32_t gch, OutAdam oa,
-               float *__restrict__ g_out, float *__restrict__ coef_slot, dw::Fixed fo,
-               const uint32_t *__restrict__ off) {
+               float *__restrict__ coef_slot, dw::Fixed fo, const uint32_t *__restrict__ off) {
     constexpr int D = 64 * F4;
     constexpr int BR = WAVES_PER_BLOCK * WAVE;   // records per block range, at most
     bool fx_range = false;
@@ -3416,7 +3411,7 @@ int dw_sgns_owner_out_rows(const int32_t *walks, int64_t n_walks, int32_t walk_l
     float *cs = reinterpret_cast<float *>(ws.v0);
 #define DW_OUT_ROWS(F, X)                                                                       \
     hipLaunchKernelGGL((k_out_rows<F, X>), g, bl, 0, st, a, ws.k1, ws.v1, ws.bounds, gch, oa,    \
-                       g_out_local, cs, fx, pl.off)
+                       cs, fx, pl.off)
     switch ((dim / 64) * 2 + (fx.acc ? 1 : 0)) {
         case 2: DW_OUT_ROWS(1, false); break;
         case 3: DW_OUT_ROWS(1, true); break;
