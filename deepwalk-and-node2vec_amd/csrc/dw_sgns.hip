@@ -1497,8 +1497,9 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // Each row's first-round centre rows (independent of the replay) are issued together with the
 // row, and the next row's p / m / v / last / pend are issued before this row's replay (after its
 // centre rows, so waiting for those never waits for the prefetch: loads return in order), so one
-// round trip is left exposed per row; the registers this takes hold the kernel at six waves per
-// SIMD (OUT_ROWS_WAVES).
+// round trip is left exposed per row. Seven waves per SIMD (OUT_ROWS_WAVES, 72 VGPRs, a few
+// spills outside the row loop): 0.2635-0.2641 ms per step against 0.2676-0.268 at six and
+// 0.279-0.280 at eight (profiles/r06_pipe_order_ab.txt).
 // EXACT (the deterministic mode, g_out registered): each term coef * w_in enters the row's sum
 // as a fixed-point integer (dw::to_fixed, the records gather's rule), so the sum is the same
 // whatever order the claim's atomics ranked the records in.
@@ -1510,7 +1511,7 @@ void launch_boundary(hipStream_t st, const uint32_t *keys, int64_t n_rec, int32_
 // alone: the hubs have the low ids, so their ranges start first). (Stepping a straddling row by
 // the range that finishes it last — a device fence and a part counter per row — measured 0.41
 // against 0.295 ms: an agent-scope release on MI355X writes back the XCD's L2.)
-constexpr int OUT_ROWS_WAVES = 6;
+constexpr int OUT_ROWS_WAVES = 7;
 template <int F4, bool EXACT = false>
 __global__ void __launch_bounds__(WAVES_PER_BLOCK *WAVE, F4 <= 2 ? OUT_ROWS_WAVES : 2)
     k_out_rows(SgnsArgs a, const uint32_t *__restrict__ keys, const uint64_t *__restrict__ vals,
