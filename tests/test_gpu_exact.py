@@ -145,7 +145,9 @@ def test_exact_lazy_rows_major_repeatable_and_equal_dense(form, hip_device):
     from shallow_encoders.word2vec.sharding import (OwnerLazyTables, ShardedTables,
                                                     owner_lazy_step, owner_lazy_steps,
                                                     replicated_step)
-    V, d, R, K, L, n, steps = 4000, 128, 3, 5, 40, 64, 6
+    # (V: a step's 65K slots leave about half the out rows untouched, so out rows fall behind
+    # and k_out_rows replays their deferred steps; at V = 4,000 every row was touched every step)
+    V, d, R, K, L, n, steps = 100_000, 128, 3, 5, 40, 64, 6
     g = torch.Generator().manual_seed(3)
     walks = torch.randint(1, V, (steps, n, L), generator=g, dtype=torch.int32)
     walks[:, :, ::5] = 9                     # a hub out row straddling the out-rows chunks

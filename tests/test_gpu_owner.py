@@ -743,10 +743,42 @@ def test_rows_major_equals_gather_path(hip_device, d, wd, hub):
     (l0, i0, o0, a0), (l1, i1, o1, a1) = runs
     assert torch.equal(l0, l1)
     np.testing.assert_allclose(a0, a1, rtol=1e-6)
+    # hub rows hold hundreds of records summed in the claim's (run-dependent) order; each
+    # near-zero gradient entry then moves by up to a normalised Adam step: 1,026 of 1,024,000
+    # entries (0.1002%) measured once at d = 256 — the exact comparison is the deterministic
+    # test below
+    frac = 2e-3 if hub else 1e-3
     for got, exp in ((i0, i1), (o0, o1)):
-        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=1e-3,
+        assert_params_close(got, exp, lr, rtol=1e-5, atol=1e-6, max_frac=frac,
                             max_abs=2.05 * lr * steps)
         assert_no_row_drift(got, exp)
+
+
+@pytest.mark.parametrize('d', [128, 256])
+def test_rows_major_equals_gather_path_deterministic(hip_device, d):
+    """test_rows_major_equals_gather_path's hub case in the deterministic mode (integer sums:
+    no record order left): the rows-major step and the catch-up -> pass 1 -> lazy gather path
+    give the same tables and Adam state bit for bit."""
+    V, R, K, L, n, steps, lr = 4000, 2, 4, 14, 32, 8, 0.02
+    g = torch.Generator().manual_seed(23)
+    walks = torch.randint(1, V, (steps, n, L), generator=g, dtype=torch.int32)
+    mask = torch.rand((steps, n, L), generator=g) < 0.33
+    walks[mask] = torch.randint(1, 4, (int(mask.sum()),), generator=g, dtype=torch.int32)
+    per = L - 2 * R
+    runs = []
+    for rows_major in (True, False):
+        def cfg(t, rows_major=rows_major):
+            t.rows_major = rows_major
+            t.enable_exact(1.0 / (n * per * 2 * R))
+        t, _ = _lazy_vs_dense(hip_device, walks, V, d, R, K, lr, lazy_out=True, configure=cfg)
+        assert t._rows_step == rows_major
+        t.flush()
+        runs.append([x[:V].cpu().clone() for x in (t.params_in[0], t.m_in, t.v_in, t.w_out,
+                                                   t.m_out, t.v_out, t.last_out)])
+    names = ('w_in', 'm_in', 'v_in', 'w_out', 'm_out', 'v_out', 'last_out')
+    for name, x, y in zip(names, *runs):
+        diff = int((x != y).sum())
+        assert diff == 0, f'{name}: {diff} entries differ between the two forms'
 
 
 def test_owner_tables_refuse_unbuilt_width(hip_device):
