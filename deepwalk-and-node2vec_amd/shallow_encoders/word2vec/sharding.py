@@ -1500,12 +1500,17 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     # the out rows: 0.295-0.301; two streams both at the start: 0.299; one stream after the out
     # rows: 0.300-0.306; the centre pass captured before the forks: 0.324;
     # profiles/r06_pipe_order_ab.txt).
+    # The main stream joins step k + 1's preparation before step k's centre pass, not at step
+    # k + 1's start: each cross-stream edge costs the main chain ~6 us (a barrier where it waits,
+    # a signal where the side forks), and at the step boundary the two had met (10-20 us gaps);
+    # 0.2635-0.265 against 0.2672-0.2679 ms (profiles/r06_pipe_order_ab.txt). The preparation
+    # ends ~20 us before the out rows do, so the centre pass does not wait for it.
+    main.wait_event(ready)
     for k in range(n_steps):
         slot = k & 1
         if bind is not None:
             bind(k)
         t.begin_step()
-        main.wait_event(ready)
         w = batches[k]
         fork = torch.cuda.Event()   # step k + 1's preparation depends on what precedes this
         fork.record(main)           # point, but is captured after the out rows (launched first:
@@ -1514,6 +1519,7 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
             ready = ahead(k + 1, fork)
             if bind is not None:
                 bind(k)
+            main.wait_event(ready)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,
                          noise_offset=offs[k], grad_scale=grad_scale, status=status,
