@@ -1429,11 +1429,12 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
     front: GraphedOwnerStep's unrolled steps), pipelined on one rank with the rows-major out
     step (OwnerLazyTables.pipeline_ok; otherwise the plain sequence). Step k + 1's
     preparation — its out records' claim and placement (dw_sgns_owner_out_catch_up, flags 4),
-    its centres' touch claim and the catch-up of the centres step k does not touch — runs on two
-    side streams while step k's out rows, centre pass and in-table update run, from the moment
-    step k - 1 has finished (the buffers alternate by step parity: workspace slot, row counts,
-    touched list). Only the out rows' step, the centre pass and the in rows' update stay on the
-    step's critical path; the preparation forks after step k's out rows. The results equal the sequential steps': each kernel reads and writes
+    its centres' touch claim and the catch-up of the centres step k does not touch — runs on one
+    side stream beside step k's out rows, from the moment step k - 1 has finished (the buffers
+    alternate by step parity: workspace slot, row counts, touched list), and the main stream
+    joins it before step k's centre pass. Only the out rows' step, the centre pass and the in
+    rows' update stay on the step's critical path. The results equal the sequential steps':
+    each kernel reads and writes
     what it would there (the catch-up of step k + 1 skips the centres of step k, which step k
     updates itself). ``bind(k)``: called before enqueueing anything of step k (graph capture:
     binds step k's dw_step_scalars block). Returns the record count of the steps."""
