@@ -363,6 +363,7 @@ def c5_line(args, dev, n_walks: int, n_steps: int) -> dict:
     walks = torch.empty((n_walks, L), dtype=torch.int32, device=dev)
     steps = n_walks * (L - 1)
     # ---- the exact walker over the position index -------------------------------------------
+    torch.cuda.reset_peak_memory_stats(dev)
     a = time.perf_counter()
     dt = csr.device_tensors(dev, need_sorted=True, need_adj_pos=True, need_hub_bits=True,
                             need_edge_cn=True, need_n2v_index=True)
@@ -431,12 +432,14 @@ def c5_line(args, dev, n_walks: int, n_steps: int) -> dict:
                          c['steps'], kern_s, 1.0 + c['position_lines'] / cs, info['bytes'],
                          POS_LINES)}}
     del walks, st, ex, px
+    out['hbm_peak_bytes_walks'] = torch.cuda.max_memory_allocated(dev)
     # the index and the exact walker's other structures make room for the tables
     for k in ('n2v_rec', 'n2v_pos', 'edge_cn', 'adj_hpos', 'hub_bits', 'hub_idx', 'col_sorted'):
         dt.pop(k, None)
     del dt
     gc.collect()
     torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
     # ---- the SGNS step (test_gpu_c5_step's composition) ---------------------------------------
     walker = Node2Vec(csr, L, p=p, q=q, rng='philox', seed=1234, device=dev)
     tables = OwnerLazyTables(V, d, dev, lr=args.lr, init_seed=None, emulate_world=1)
@@ -476,6 +479,7 @@ def c5_line(args, dev, n_walks: int, n_steps: int) -> dict:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - a
     _native.check_status(status, 'bench c5')
+    hbm_step = torch.cuda.max_memory_allocated(dev)   # the step's footprint (before the check)
     ev_ms = e[0].elapsed_time(e[1]) / n_steps
     mean_loss = float(loss_terms(loss_acc, pairs * n_steps, K)['loss'])
     # one more step, checked from its pre-state (the sampled rows; the tables are 17 GB each)
@@ -521,6 +525,7 @@ def c5_line(args, dev, n_walks: int, n_steps: int) -> dict:
                      'bytes_per_step': alg, 'sgns_bytes': pairs * bpp,
                      'out_table_adam_bytes': out_adam, 'touched_in_rows': n_in,
                      'touched_in_rows_adam_bytes': in_adam},
+        'hbm_peak_bytes_step': hbm_step,
         'step_check': step_check})
     del tables, walker, csr
     gc.collect()
@@ -1134,6 +1139,9 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     _native.check_status(status, 'bench')
+    # the rank's device footprint so far (tables, Adam state, CSR and walker structures,
+    # workspaces: every device buffer is a torch allocation)
+    hbm_peak = torch.cuda.max_memory_allocated(dev)
     kern_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items() if v}
     if graphed is not None:   # one replay = `unroll` steps
         kern_ms = {k: v / graphed.unroll for k, v in kern_ms.items()}
@@ -1550,6 +1558,7 @@ def run(args, world: int, rank: int, local_rank: int, backend: str, dist_on: boo
             'phases': phase_info,
         },
         'cpu_baseline': None,
+        'hbm_peak_bytes': hbm_peak,
     }
     prof = os.path.join(REPO, 'profiles', 'sgns_pmc.json')
     if os.path.exists(prof):
