@@ -134,7 +134,8 @@ def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
     those rows (include/dw_hip.h; dw_common.h, dw::frozen_el): [2] F = max |nstep| when every
     box row has the same eps and (1 - beta1)(1 + 2^-20) <= sqrt(beta2) (m then shrinks at least
     as fast as RN(sqrt(v)) over g = 0 steps), else +inf (no replay tail is frozen); [3] that
-    eps."""
+    eps; [4], [5] the rows' 1 - beta1 and beta2 when every box row has the same (the betas never
+    changed: a frozen tail then steps m and v with them, no per-step history loads), else NaN."""
     ok = hist_rows_in_box(hist[1:last + 1])
     bad = np.flatnonzero(~ok)
     b = int(bad[-1]) + 2 if bad.size else 1
@@ -142,6 +143,7 @@ def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
     h0.view(np.uint32)[0] = HIST_BOX_TAG
     h0.view(np.int32)[1] = b
     h0[2] = np.inf
+    h0[4] = h0[5] = np.nan
     rows = np.ascontiguousarray(hist[b:last + 1], dtype=np.float32).reshape(-1, 8)
     if rows.shape[0]:
         w1, b2 = rows[:, 0].astype(np.float64), rows[:, 1].astype(np.float64)
@@ -149,6 +151,9 @@ def hist_header(hist: np.ndarray, last: int) -> np.ndarray:
         if (eps == eps[0]).all() and ((1.0 - w1) * (1.0 + 2.0 ** -20) <= np.sqrt(b2)).all():
             h0[2] = np.abs(rows[:, 4]).max()
             h0[3] = eps[0]
+        bits = rows[:, :2].view(np.uint32)
+        if (bits == bits[0]).all():
+            h0[4], h0[5] = rows[0, 0], rows[0, 1]
     return h0
 
 

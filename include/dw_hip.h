@@ -751,8 +751,10 @@ int dw_adam_dense_to(const float *param_src, float *param_dst, float *grad, floa
  *         fewer operations); [2] = F, [3] = eps of those rows: with every box row's eps equal to
  *         it, (1 - beta1)(1 + 2^-20) <= sqrt(beta2) and |nstep| <= F, a replay whose parameter
  *         can provably no longer move (|m| F / max(RN(sqrt(v)), eps) below |p| 2^-26) steps m
- *         and v alone for the rest of the run (the same bits; F = +inf: never); any other row
- *         0 = no step in the box;
+ *         and v alone for the rest of the run (the same bits; F = +inf: never); [4] = 1-beta1,
+ *         [5] = beta2 when every box row has those same values (the frozen steps then take them
+ *         from here, not from each row; NaN = the betas vary); any other row 0 = no step in the
+ *         box;
  *   grad_rows NULL: replay every listed row up to `step` (g = 0);
  *   grad_rows float32[n_rows_max, dim]: replay up to step - 1, then apply `step` with row i's
  *         gradient grad_rows[i];

@@ -302,17 +302,21 @@ def test_owner_tables_two_ranks_equal_single_process(hip_device):
 
 
 # ---- the touched-row in-table exchange: lazy exact Adam (dw_adam_rows, OwnerLazyTables) -------
-@pytest.mark.parametrize('d,sched', [(128, False), (64, True), (96, False)])
-def test_rows_adam_long_lag_bit_exact(hip_device, d, sched):
-    """Replays of up to 600 missed g = 0 steps through the box history (sharding.hist_row /
+@pytest.mark.parametrize('d,sched,S', [(128, False, 600), (64, True, 600), (96, False, 600),
+                                       (128, False, 2500)])
+def test_rows_adam_long_lag_bit_exact(hip_device, d, sched, S):
+    """Replays of up to S missed g = 0 steps through the box history (sharding.hist_row /
     hist_header, as OwnerLazyTables writes it): the tail where the parameter provably no longer
     moves runs m and v alone (dw::frozen_el) — the same bits as one dense dw_adam_dense per
     step, and as the same replay with the freeze disabled (header F = +inf). Rows include
-    p = -0 with m = -0 (never frozen), m = 0 and p = 0; sched: the lr changes along the run."""
+    p = -0 with m = -0 (never frozen), m = 0 and p = 0; sched: the lr changes along the run.
+    With the betas constant the frozen steps take them from the header (no per-step loads) and,
+    once m is +0 in every lane (S = 2500: m underflows after ~900 steps), step v alone; the
+    header's betas withheld (NaN) gives the per-step form — the same bits again."""
     import time
     from shallow_encoders.word2vec.sharding import hip_adam, hip_rows_adam, hist_header, hist_row
     g = torch.Generator().manual_seed(d)
-    V, S = 256, 600
+    V = 256
     betas, eps = (0.9, 0.999), 1e-8
     lrs = [0.01 if (not sched or s < 300) else 0.005 for s in range(S + 1)]
     hist = np.zeros((S + 1, 8), dtype=np.float32)
@@ -336,11 +340,14 @@ def test_rows_adam_long_lag_bit_exact(hip_device, d, sched):
                  lrs[s - 1], betas, eps, 0.0, False)
         for t, u in zip(ref, (pp, mm, vv)):
             t[rows] = u
+    assert np.isfinite(hist[0, 4]) and np.isfinite(hist[0, 5])   # constant betas certified
     out = {}
-    for freeze in (False, True):
+    for freeze in (False, True, 'per_step'):
         h = hist.copy()
         if not freeze:
             h[0, 2] = np.inf
+        if freeze == 'per_step':
+            h[0, 4] = h[0, 5] = np.nan
         hd = torch.from_numpy(h).cuda()
         p, m, v = (t.cuda().clone() for t in (p0, m0, v0))
         last = last0.cuda().clone()
@@ -352,7 +359,8 @@ def test_rows_adam_long_lag_bit_exact(hip_device, d, sched):
         assert int(last.min()) == S
     print(f'd={d}: replay {out[False][0] * 1e3:.2f} ms, with the frozen tail '
           f'{out[True][0] * 1e3:.2f} ms')
-    for freeze in (True, False):
+    print(f'   frozen steps with per-step betas {out["per_step"][0] * 1e3:.2f} ms')
+    for freeze in (True, False, 'per_step'):
         for name, a, b in zip('pmv', out[freeze][1:], ref):
             assert torch.equal(a, b), f'freeze={freeze} {name}: {int((a != b).sum())} differ'
 

@@ -541,6 +541,12 @@ def test_hist_box_header():
     h = hist(20)
     h0 = hist_header(h, 20)
     assert h0.view(np.uint32)[0] == HIST_BOX_TAG == 0x58424457 and h0.view(np.int32)[1] == 1
+    # [4], [5]: the box rows' constant 1 - beta1 and beta2 (the frozen replay tails use them)
+    assert h0[4] == h[1, 0] and h0[5] == h[1, 1]
+    hv = hist(20)
+    hv[12:] = np.stack([hist_row(s, 0.01, (0.8, 0.999), 1e-8, 0.0) for s in range(12, 21)])
+    hv0 = hist_header(hv, 20)
+    assert np.isnan(hv0[4]) and np.isnan(hv0[5])
     assert hist_header(hist(20, wd_at=(3, 7)), 20).view(np.int32)[1] == 8
     assert hist_header(hist(20, wd_at=(20,)), 20).view(np.int32)[1] == 21
     assert hist_header(hist(20, eps=1e-9), 20).view(np.int32)[1] == 21     # eps < 2^-27
