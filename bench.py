@@ -247,9 +247,11 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
 
     for s in range(warm):
         eager_step(s)
+    long_steps = max(int(getattr(args, 'batch64_long', 0) or 0), 0) // unroll * unroll
+    total = max(n_steps, long_steps)
     graphed = GraphedOwnerStep(tables, walker, epoch_starts, B, R, K, seed=seed,
                                grad_scale=grad_scale, loss_acc=loss_acc, status=status,
-                               first_walk_id=warm * B, n_steps=n_steps + unroll, unroll=unroll)
+                               first_walk_id=warm * B, n_steps=total + unroll, unroll=unroll)
     graphed.replay()                      # one untimed replay (first-launch costs)
     torch.cuda.synchronize(dev)
     loss_acc.zero_()
@@ -265,8 +267,30 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
     kern_ms = e0.elapsed_time(e1) / n_steps
     mean_loss = float(loss_terms(loss_acc, pairs * n_steps, K)['loss'])
 
+    # the steady state: the same replays on to `long_steps`, the last 4,000 timed (the step
+    # check below then runs from that state)
+    steady = None
+    if long_steps > n_steps:
+        rest = long_steps - n_steps
+        win = min(rest, 4000 // unroll * unroll)
+        for _ in range((rest - win) // unroll):
+            graphed.replay()
+        torch.cuda.synchronize(dev)
+        a2 = time.perf_counter()
+        for _ in range(win // unroll):
+            graphed.replay()
+        torch.cuda.synchronize(dev)
+        el2 = time.perf_counter() - a2
+        _native.check_status(status, 'bench batch64 steady state')
+        steady = {'steps_before': warm + unroll + n_steps + rest - win, 'steps': win,
+                  'ms_per_step': el2 / win * 1e3, 'value': pairs * win / el2,
+                  'unit': 'positive-pairs/s'}
+        n_done = n_steps + rest
+    else:
+        n_done = n_steps
+
     # one more step, eager, checked from its (flushed) pre-state
-    s = warm + unroll + n_steps
+    s = warm + unroll + n_done
     g0 = s * B
     pre = tables.full_state()
     walks = eager_step(s)
@@ -311,6 +335,7 @@ def batch64_line(csr, args, dev, epoch_starts, copy_gbs: float, n_steps: int) ->
             'ms_per_step_events': kern_ms, 'bytes_per_step': alg,
             'sgns_bytes': pairs * bpp, 'touched_rows_adam_bytes': adam_bytes,
             'touched_in_rows': n_in, 'touched_out_rows': n_out},
+        'steady_state': steady,
         'step_check': step_check,
         'deterministic': bool(args.deterministic),
         'cpu_baseline': None,
@@ -645,6 +670,10 @@ def main():
                          'SGNS (measured neutral on MI355X: the SGNS slows by what the walker '
                          'saves, 6.89 vs 6.89 ms/step at C3; on by default on the one-GPU lazy '
                          'path of small batches)')
+    ap.add_argument('--batch64-long', type=int, default=20000,
+                    help='batch64: keep replaying to this many steps and time the last 4,000 '
+                         '(the in rows\' lags, and so their catch-up, grow with the run: the '
+                         'steady state a reference epoch of ~163K steps runs in); 0 = skip')
     ap.add_argument('--batch64-steps', type=int, default=400,
                     help='the one-GPU C3 line: then also time this many steps at the reference '
                          'configs\' 64-walk batch (lazy exact Adam, graph-replayed) and report '

@@ -42,9 +42,11 @@ def test_bench_lazy_owner_64_walks_small_graph():
 def test_bench_headline_with_batch64_small_graph():
     d = _bench('--scale', '14', '--edges', '100000', '--batch-walks', '512', '--steps', '8',
                '--warmup', '2', '--no-cpu-baseline', '--no-walk-bench', '--exact-steps', '0',
-               '--batch64-steps', '32')
+               '--batch64-steps', '32', '--batch64-long', '160')
     b = d['batch64']
     assert b['value'] > 0 and b['step_check']['ok'], b['step_check']
+    # the steady-state leg: replays on to 160 steps, the last ones timed, then the check
+    assert b['steady_state']['steps'] == 128 and b['steady_state']['ms_per_step'] > 0
     assert b['roofline']['touched_out_rows'] > 0 and b['roofline']['touched_in_rows'] > 0
 
 
