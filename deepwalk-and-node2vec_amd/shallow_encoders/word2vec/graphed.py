@@ -182,6 +182,12 @@ class GraphedStep:
                 'step': int(b['step'])}
 
 
+# GraphedOwnerStep replays its side-first capture from this Adam step on (the in rows' lags, and
+# so their catch-up, grow with the run; C3 / 64 walks: side-after 0.259 / 0.484 ms per step at
+# steps 24-424 / 16,024-20,024, side-first 0.275 / 0.430)
+SIDE_FIRST_FROM = 2000
+
+
 class GraphedOwnerStep:
     """``owner_lazy_step`` on one GPU (OwnerLazyTables: the lazy exact Adam of the in table, and
     of the out table with ``lazy_out``) replayed as a HIP graph, with the walker in front of it:
@@ -255,23 +261,32 @@ class GraphedOwnerStep:
         if tables.pipeline_ok(R, K):   # owner_lazy_steps' second buffers, outside the capture
             tables._pipe_alloc(self.B, L, R, K)
         steps0, lr0 = tables.step_count, len(tables._lr_hist)
+        # Two captures of the same steps: the next step's preparation enqueued after this step's
+        # out rows (early in a run) or before them (once the in rows' lags have grown, from
+        # SIDE_FIRST_FROM steps on: the in-row catch-up is then the critical path and is
+        # dispatched first; owner_lazy_steps side_first). (Captured and replayed on a
+        # high-priority stream: 0.369 against 0.273 ms per step at C3 / 64 walks;
+        # profiles/r06_pipe_order_ab.txt.)
         self.graph = torch.cuda.CUDAGraph()
-        # (captured and replayed on a high-priority stream: 0.369 against 0.273 ms per step at
-        # C3 / 64 walks; profiles/r06_pipe_order_ab.txt)
-        try:
-            with torch.cuda.graph(self.graph, capture_error_mode='relaxed'):
-                self._body()
-        finally:
-            _native.call('dw_step_scalars_bind', None)
-            tables.step_count = steps0          # the capture ran no step
-            del tables._lr_hist[lr0:]
-            walker._next_walk_id = next_wid
+        self.graph_late = None
+        for late in ((False, True) if tables.pipeline_ok(R, K) else (False,)):
+            g = torch.cuda.CUDAGraph() if late else self.graph
+            try:
+                with torch.cuda.graph(g, capture_error_mode='relaxed'):
+                    self._body(side_first=late)
+            finally:
+                _native.call('dw_step_scalars_bind', None)
+                tables.step_count = steps0          # the capture ran no step
+                del tables._lr_hist[lr0:]
+                walker._next_walk_id = next_wid
+            if late:
+                self.graph_late = g
         torch.cuda.synchronize(dev)
 
     def _step_blk(self, k: int) -> int:
         return self.step_blocks.data_ptr() + k * _STEP_DTYPE.itemsize
 
-    def _body(self) -> None:
+    def _body(self, side_first: bool = False) -> None:
         t, dev, B = self.t, self.t.device, self.B
         with torch.cuda.device(dev):
             _native.call('dw_step_scalars_expand', _native.ptr(self.block), self._step_blk(0),
@@ -291,7 +306,7 @@ class GraphedOwnerStep:
         owner_lazy_steps(t, [self.walks[k * B:(k + 1) * B] for k in range(self.unroll)], self.R,
                          self.K, seed=self.seed, noise_offsets=[0] * self.unroll,
                          grad_scale=self.grad_scale, loss_acc=self.loss_acc, status=self.status,
-                         bind=bind)
+                         bind=bind, side_first=side_first)
 
     def replay(self) -> None:
         """``unroll`` training steps (enqueued on the current stream); the tables' host
@@ -307,7 +322,8 @@ class GraphedOwnerStep:
             raise RuntimeError(f'GraphedOwnerStep: the Adam-scalar history covers steps up to '
                                f'{self._last - self.unroll}; build a new GraphedOwnerStep '
                                f'(n_steps) to go on')
-        self.graph.replay()
+        late = self.graph_late is not None and t.step_count >= SIDE_FIRST_FROM
+        (self.graph_late if late else self.graph).replay()
         t.step_count += self.unroll
         t._lr_hist.extend([t.lr] * self.unroll)
 

@@ -1429,7 +1429,8 @@ class OwnerLazyTables(OwnerTables):
 
 def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
                      neg_samples: int, *, seed: int, noise_offsets, grad_scale: float,
-                     loss_acc: torch.Tensor, status: torch.Tensor, bind=None) -> int:
+                     loss_acc: torch.Tensor, status: torch.Tensor, bind=None,
+                     side_first: bool = False) -> int:
     """Consecutive owner_lazy_step calls over ``batches`` (int32 [n, L] walks each, known up
     front: GraphedOwnerStep's unrolled steps), pipelined on one rank with the rows-major out
     step (OwnerLazyTables.pipeline_ok; otherwise the plain sequence). Step k + 1's
@@ -1520,11 +1521,20 @@ def owner_lazy_steps(tables: OwnerLazyTables, batches, context_radius: int,
         w = batches[k]
         fork = torch.cuda.Event()   # step k + 1's preparation depends on what precedes this
         fork.record(main)           # point, but is captured after the out rows (launched first:
-        t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
-        if k + 1 < n_steps:         # 0.2731-0.2737 against 0.2749-0.2750 ms)
+        # side_first: step k + 1's preparation enqueued before step k's out rows, so that its
+        # in-row catch-up is dispatched first — slower early in a run (0.275 against 0.259 ms
+        # at C3 / 64 walks, steps 24-424) and faster once the in rows' lags have grown (0.430
+        # against 0.484 ms over steps 16,024-20,024; profiles/r06_pipe_order_ab.txt)
+        if side_first and k + 1 < n_steps:
             ready = ahead(k + 1, fork)
             if bind is not None:
                 bind(k)
+        t.out_rows_step(w, R, K, seed, offs[k], grad_scale, loss_acc, status, slot=slot)
+        if k + 1 < n_steps:         # 0.2731-0.2737 against 0.2749-0.2750 ms)
+            if not side_first:
+                ready = ahead(k + 1, fork)
+                if bind is not None:
+                    bind(k)
             main.wait_event(ready)
         sgns_owner_pass1(t.w_in_raw, t.w_out, t.grads_in, K, walks=w, context_radius=R,
                          owner=t.rank, n_owners=t.world, vocab_size=t.V, seed=seed,

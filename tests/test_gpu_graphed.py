@@ -89,14 +89,20 @@ def test_graphed_step_equals_eager(hip_device, scatter, overlap_in, unroll):
         assert_no_row_drift(got, exp)
 
 
-@pytest.mark.parametrize('lazy_out,unroll', [(True, 1), (True, 4), (False, 3), (True, 12)])
-def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll):
+@pytest.mark.parametrize('lazy_out,unroll,late', [(True, 1, False), (True, 4, False),
+                                                  (False, 3, False), (True, 12, False),
+                                                  (True, 4, True)])
+def test_graphed_owner_lazy_step_equals_eager(hip_device, lazy_out, unroll, late, monkeypatch):
     """The one-GPU lazy owner step (bench.py's path for the reference's 64-walk batch on a large
     graph) replayed as a HIP graph (GraphedOwnerStep: the lazy kernels' step numbers bound
     relative to the step blocks) equals the eager steps: the same walks, losses to float64-atomic
-    order, and both tables, flushed, to fp32 atomic-order noise."""
+    order, and both tables, flushed, to fp32 atomic-order noise. late: the side-first capture
+    (the next step's preparation enqueued before the out rows) replayed from the first step."""
+    from shallow_encoders.word2vec import graphed as graphed_mod
     from shallow_encoders.word2vec.graphed import GraphedOwnerStep
     from shallow_encoders.word2vec.sharding import OwnerLazyTables, owner_lazy_step
+    if late:
+        monkeypatch.setattr(graphed_mod, 'SIDE_FIRST_FROM', 0)
     dev = hip_device
     csr, walker, epoch = _setup(dev)
     V = csr.vocab_size
